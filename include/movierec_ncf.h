@@ -1,0 +1,177 @@
+/*
+ * movierec_ncf.h — C ABI of the MI355X-native NCF/NeuMF training hot path.
+ *
+ * This is the drop-in boundary below the Python mirror of the reference's
+ * `movierec.model.MovierecModel` (see INTEGRATION.md for the ctypes binding).
+ * The reference has no FFI of its own: its hot path is the Keras graph built
+ * in movierec/model.py:135-215 and executed by Keras' training loop
+ * (model.py:305-333).  Each entry point below names the reference behaviour it
+ * replaces.
+ *
+ * Conventions
+ *  - Every pointer argument that names device data is a caller-owned device
+ *    pointer (allocated e.g. by PyTorch's caching allocator).  The library
+ *    never allocates or frees device memory; scratch lives in a caller-provided
+ *    workspace (ncf_workspace_size / ncf_workspace_init).
+ *  - `stream` is a hipStream_t passed as void*; all work is enqueued on it, no
+ *    call synchronises, so every call is hipGraph-capturable.
+ *  - Return value: 0 = ok, NCF_EINVAL (-1) = invalid argument (the Python layer
+ *    raises ValueError, like the reference's parameter checks model.py:77-112),
+ *    NCF_EHIP (-2) = HIP error (RuntimeError).  The message is available from
+ *    ncf_last_error() (thread-local).  No C++ exception crosses the ABI.
+ *  - Reentrant: no global mutable state besides the thread-local error text.
+ *
+ * Device data layout (DESIGN.md §Data layout)
+ *  - One combined embedding table `emb`: rows [0, num_users) are users, rows
+ *    [num_users, num_users+num_items) are items; each row holds
+ *    [gmf part (gmf_dim, padded to gmf_stride) | mlp part (du or di, padded)],
+ *    `row_width` floats, 16-byte aligned rows.
+ *  - `mlp`: flat fp32 vector of the dense parameters, Keras layouts:
+ *    for l = 1..n-1: hidden_l kernel (layers[l-1] x layers[l], row-major) then
+ *    hidden_l bias (layers[l]); then output kernel (out_features) and output
+ *    bias (1).  out_features = gmf_dim + layers[n-1], ordered [gmf, mlp].
+ */
+#ifndef MOVIEREC_NCF_H
+#define MOVIEREC_NCF_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NCF_ABI_VERSION 1
+#define NCF_MAX_LAYERS 8
+#define NCF_EINVAL (-1)
+#define NCF_EHIP (-2)
+
+#define NCF_OPT_ADAM 0
+#define NCF_OPT_SGD 1
+
+/* stats accumulator layout (double[NCF_NUM_STATS], device) */
+#define NCF_STAT_LOSS_SUM 0   /* sum over steps of batch loss (BCE mean + L2) */
+#define NCF_STAT_HR_SUM 1     /* sum over steps of batch HR@k */
+#define NCF_STAT_DCG_SUM 2    /* sum over steps of batch DCG@k */
+#define NCF_STAT_STEPS 3      /* number of batches accumulated */
+#define NCF_STAT_LAST_LOSS 4
+#define NCF_STAT_LAST_HR 5
+#define NCF_STAT_LAST_DCG 6
+#define NCF_NUM_STATS 8
+
+/* summary of one forward/backward (float[NCF_NUM_SUMMARY], device);
+ * summed over ranks in data-parallel training */
+#define NCF_SUM_BCE 0      /* sum over samples of per-sample BCE */
+#define NCF_SUM_HIT 1      /* sum over groups of hit@k */
+#define NCF_SUM_DCG 2      /* sum over groups of dcg@k */
+#define NCF_SUM_GROUPS 3   /* number of groups */
+#define NCF_NUM_SUMMARY 4
+
+typedef struct ncf_shape {
+    /* inputs (MovierecModel params: num_users, num_items, layers_sizes; gmf_dim = NeuMF extension) */
+    int32_t num_users;
+    int32_t num_items;
+    int32_t num_layers;                 /* len(layers_sizes) >= 1 */
+    int32_t gmf_dim;                    /* 0 = the reference's MLP-only model */
+    int32_t layers[NCF_MAX_LAYERS];
+    /* derived by ncf_shape_init */
+    int32_t du, di;                     /* model.py:159-160 */
+    int32_t gmf_stride;                 /* gmf_dim rounded up to 4 */
+    int32_t row_width;                  /* floats per emb row */
+    int64_t num_rows;                   /* num_users + num_items */
+    int32_t out_features;               /* gmf_dim + layers[n-1] */
+    int32_t mlp_params;                 /* length of the flat dense vector */
+    int32_t layer_off[NCF_MAX_LAYERS];  /* [l] = offset of hidden_l kernel (l>=1); [0] = output kernel */
+    int32_t fast_path;                  /* 1 if the fused MFMA kernel supports this shape */
+    int32_t reserved[7];
+} ncf_shape_t;
+
+typedef struct ncf_model {
+    float* emb;   /* num_rows x row_width */
+    float* mlp;   /* mlp_params */
+} ncf_model_t;
+
+typedef struct ncf_optim {
+    float* emb_m;
+    float* emb_v;
+    float* mlp_m;
+    float* mlp_v;
+    int32_t* step;   /* device: Keras `iterations` (optimizer steps taken so far) */
+} ncf_optim_t;
+
+typedef struct ncf_hyper {
+    int32_t optimizer;                  /* NCF_OPT_ADAM / NCF_OPT_SGD (model.py:199-204) */
+    float lr, beta_1, beta_2, epsilon;  /* epsilon: Keras K.epsilon() = 1e-7 */
+    float l2[NCF_MAX_LAYERS];           /* layers_l2reg (model.py:163,168,178) */
+    int32_t group;                      /* samples per user group (num_negs_per_pos + 1) */
+    int32_t k;                          /* top-k of the hr/dcg metrics */
+    float inv_batch;                    /* 1 / (global batch) for the BCE mean */
+    int32_t force_generic;              /* 1: use the generic per-sample kernel even if fast_path */
+    int32_t reserved[6];
+} ncf_hyper_t;
+
+int ncf_abi_version(void);
+const char* ncf_last_error(void);
+
+/* Validate the model dimensions and fill the derived fields.
+ * Replaces the shape checks of MovierecModel.__init__ (model.py:73-80). */
+int ncf_shape_init(ncf_shape_t* shape, int32_t num_users, int32_t num_items, const int32_t* layers,
+                   int32_t num_layers, int32_t gmf_dim);
+
+/* Bytes of scratch needed for batches of up to max_batch samples. */
+int ncf_workspace_size(const ncf_shape_t* shape, int64_t max_batch, size_t* bytes);
+/* Zero the workspace's persistent region (call once after allocating it). */
+int ncf_workspace_init(const ncf_shape_t* shape, int64_t max_batch, void* ws, size_t ws_bytes, void* stream);
+
+/* Forward only: probs[n] = sigmoid output for (users[i], items[i]).
+ * Replaces Model.predict_on_batch output[0] (model.py:184-194). */
+int ncf_predict(const ncf_shape_t* shape, const ncf_model_t* model, const int32_t* users,
+                const int32_t* items, int64_t n, float* probs, void* ws, size_t ws_bytes, void* stream);
+
+/* RankLayer (model.py:344-352): per group of `group` consecutive probs, the
+ * stable descending order (ties: lower index first). rank_idx[n_groups*group]. */
+int ncf_rank(const float* probs, int64_t n_groups, int32_t group, int32_t* rank_idx, void* stream);
+
+/* Per-group hit@k and dcg@k (model.py:361-455): label = argmax of the group's
+ * labels, position = its place in the RankLayer order. hit/dcg[n_groups]. */
+int ncf_group_metrics(const float* probs, const float* labels, int64_t n_groups, int32_t group, int32_t k,
+                      float* hit, float* dcg, void* stream);
+
+/* One full training step on one device (Keras train_on_batch, model.py:329-333):
+ * forward, BCE, backward, deterministic embedding scatter-add and dense
+ * Adam/SGD on every parameter, metrics.  Adds the batch loss/hr/dcg to
+ * stats[] (double[NCF_NUM_STATS]) and increments optim->step.
+ * probs_out (optional, may be NULL) receives the batch predictions. */
+int ncf_train_step(const ncf_shape_t* shape, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* hyper,
+                   const int32_t* users, const int32_t* items, const float* labels, int64_t n,
+                   double* stats, float* probs_out, void* ws, size_t ws_bytes, void* stream);
+
+/* Validation batch (the evaluation pass Keras runs on validation_data inside
+ * fit_generator, model.py:329-333): forward, BCE, hr/dcg over groups of
+ * hyper->group; adds batch loss (BCE mean + L2 of the current weights), hr and
+ * dcg to stats[] without touching the weights or optim->step. */
+int ncf_evaluate(const ncf_shape_t* shape, const ncf_model_t* model, const ncf_hyper_t* hyper,
+                 const int32_t* users, const int32_t* items, const float* labels, int64_t n,
+                 double* stats, float* probs_out, void* ws, size_t ws_bytes, void* stream);
+
+/* Data-parallel split of ncf_train_step.
+ * ncf_forward_backward computes this rank's gradients with the BCE mean taken
+ * over hyper->inv_batch (= 1/global batch): dense embedding gradient
+ * emb_grad[num_rows x row_width] (every row written, zeros where untouched),
+ * mlp_grad[mlp_params], and summary[NCF_NUM_SUMMARY].  The caller sums these
+ * three over ranks (RCCL all-reduce) and then calls ncf_apply_update, which
+ * adds the L2 terms, applies the optimizer to every parameter, folds the
+ * summary into stats[] and increments optim->step. */
+int ncf_forward_backward(const ncf_shape_t* shape, const ncf_model_t* model, const ncf_hyper_t* hyper,
+                         const int32_t* users, const int32_t* items, const float* labels, int64_t n,
+                         float* emb_grad, float* mlp_grad, float* summary, float* probs_out,
+                         void* ws, size_t ws_bytes, void* stream);
+int ncf_apply_update(const ncf_shape_t* shape, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* hyper,
+                     const float* emb_grad, const float* mlp_grad, const float* summary, double* stats,
+                     void* ws, size_t ws_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MOVIEREC_NCF_H */

@@ -1,0 +1,355 @@
+// C ABI entry points (include/movierec_ncf.h).  Host orchestration only:
+// argument validation, workspace carving and the launch sequence of each call.
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "movierec_ncf.h"
+#include "ncf_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+int hip_check(hipError_t e, const char* what) {
+    if (e == hipSuccess) return 0;
+    return fail(NCF_EHIP, "%s: %s", what, hipGetErrorString(e));
+}
+
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+int check_shape(const ncf_shape_t* s) {
+    if (!s) return fail(NCF_EINVAL, "shape is NULL");
+    if (s->row_width <= 0 || s->mlp_params <= 0) return fail(NCF_EINVAL, "shape not initialised (ncf_shape_init)");
+    return 0;
+}
+
+int check_ws(const ncf_shape_t& s, int64_t n, void* ws, size_t ws_bytes, ncf::WsLayout* L) {
+    if (!ws) return fail(NCF_EINVAL, "workspace is NULL");
+    if (n <= 0) return fail(NCF_EINVAL, "batch size must be > 0, got %lld", (long long)n);
+    if (n > ncf::kMaxBatch) return fail(NCF_EINVAL, "batch size %lld exceeds %lld", (long long)n,
+                                        (long long)ncf::kMaxBatch);
+    // the layout depends on max_batch only through per-batch regions; recover it from ws_bytes
+    // by requiring the caller to size ws for at least n samples
+    ncf::WsLayout need = ncf::make_layout(s, n);
+    if (ws_bytes < need.total)
+        return fail(NCF_EINVAL, "workspace too small: %zu bytes for batch %lld (need %zu)", ws_bytes,
+                    (long long)n, need.total);
+    *L = need;
+    return 0;
+}
+
+int check_hyper(const ncf_hyper_t* h) {
+    if (!h) return fail(NCF_EINVAL, "hyper is NULL");
+    if (h->optimizer != NCF_OPT_ADAM && h->optimizer != NCF_OPT_SGD)
+        return fail(NCF_EINVAL, "Optimizer %d is not implemented.", h->optimizer);
+    if (h->group <= 0) return fail(NCF_EINVAL, "group must be > 0");
+    return 0;
+}
+
+bool use_fused(const ncf_shape_t& s, const ncf_hyper_t* h) {
+    return s.fast_path && !(h && h->force_generic) && ncf::fused_supported(s);
+}
+
+}  // namespace
+
+namespace ncf {
+
+WsLayout make_layout(const ncf_shape_t& s, int64_t B) {
+    WsLayout L{};
+    const int64_t R = s.num_rows;
+    const size_t a = 256;
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        size_t o = off;
+        off = align_up(off + bytes, a);
+        return o;
+    };
+    L.max_batch = B;
+    L.cnt = take((size_t)(R + 1) * 4);
+    L.heavy_n = take(4);
+    L.err = take(4);
+    L.persistent_end = off;
+    L.nscan = (int)((R + 1 + kScanBlock - 1) / kScanBlock);
+    L.nmetric = (int)((B + kBlock - 1) / kBlock);
+    int A = 0;
+    for (int l = 0; l < s.num_layers; ++l) A += s.layers[l];
+    A += s.gmf_dim;
+    int D = 1;
+    for (int l = 1; l < s.num_layers; ++l) D += s.layers[l];
+    L.act_w = A;
+    L.dz_w = D;
+    L.probs = take((size_t)B * 4);
+    L.gs = take((size_t)2 * B * s.row_width * 4);
+    L.list = take((size_t)2 * B * 4);
+    L.offs = take((size_t)(R + 1) * 4);
+    L.tot = take((size_t)L.nscan * 4);
+    L.heavy = take((size_t)2 * B * 4);
+    L.part_bce = take((size_t)kMaxSlabs * 4 + (size_t)L.nmetric * 4);
+    L.part_hit = take((size_t)L.nmetric * 4);
+    L.part_dcg = take((size_t)L.nmetric * 4);
+    L.part_reg = take((size_t)(kUpdateGrid + (s.mlp_params + kBlock - 1) / kBlock) * 4);
+    L.summary = take(NCF_NUM_SUMMARY * 4);
+    L.slabs = take((size_t)kMaxSlabs * s.mlp_params * 4);
+    L.mlp_grad = take((size_t)s.mlp_params * 4);
+    L.act = take((size_t)B * A * 4);
+    L.dz = take((size_t)B * D * 4);
+    L.total = off;
+    return L;
+}
+
+}  // namespace ncf
+
+extern "C" {
+
+int ncf_abi_version(void) { return NCF_ABI_VERSION; }
+
+const char* ncf_last_error(void) { return g_err.c_str(); }
+
+int ncf_shape_init(ncf_shape_t* s, int32_t num_users, int32_t num_items, const int32_t* layers, int32_t num_layers,
+                   int32_t gmf_dim) {
+    if (!s || !layers) return fail(NCF_EINVAL, "NULL argument");
+    if (num_layers < 1 || num_layers > NCF_MAX_LAYERS)
+        return fail(NCF_EINVAL, "num_layers must be in [1, %d], got %d", NCF_MAX_LAYERS, num_layers);
+    if (num_users <= 0 || num_items <= 0) return fail(NCF_EINVAL, "num_users and num_items must be > 0");
+    if (gmf_dim < 0) return fail(NCF_EINVAL, "gmf_dim must be >= 0");
+    for (int l = 0; l < num_layers; ++l)
+        if (layers[l] <= 0) return fail(NCF_EINVAL, "layers_sizes[%d] must be > 0", l);
+    if (layers[0] < 2) return fail(NCF_EINVAL, "layers_sizes[0] must be >= 2 (user and item halves)");
+    memset(s, 0, sizeof(*s));
+    s->num_users = num_users;
+    s->num_items = num_items;
+    s->num_layers = num_layers;
+    s->gmf_dim = gmf_dim;
+    for (int l = 0; l < num_layers; ++l) s->layers[l] = layers[l];
+    s->du = layers[0] / 2;
+    s->di = layers[0] - s->du;
+    s->gmf_stride = (gmf_dim + 3) / 4 * 4;
+    const int mlpw = ((s->du > s->di ? s->du : s->di) + 3) / 4 * 4;
+    s->row_width = s->gmf_stride + mlpw;
+    s->num_rows = (int64_t)num_users + num_items;
+    s->out_features = gmf_dim + layers[num_layers - 1];
+    int off = 0;
+    for (int l = 1; l < num_layers; ++l) {
+        s->layer_off[l] = off;
+        off += layers[l - 1] * layers[l] + layers[l];
+    }
+    s->layer_off[0] = off;
+    off += s->out_features + 1;
+    s->mlp_params = off;
+    if (s->num_rows * (int64_t)(s->row_width / 4) >= (int64_t)1 << 31)
+        return fail(NCF_EINVAL, "embedding table too large for one device (%lld rows)", (long long)s->num_rows);
+    s->fast_path = ncf::fused_supported(*s) ? 1 : 0;
+    return 0;
+}
+
+int ncf_workspace_size(const ncf_shape_t* s, int64_t max_batch, size_t* bytes) {
+    if (int r = check_shape(s)) return r;
+    if (!bytes) return fail(NCF_EINVAL, "bytes is NULL");
+    if (max_batch <= 0 || max_batch > ncf::kMaxBatch)
+        return fail(NCF_EINVAL, "max_batch must be in [1, %lld]", (long long)ncf::kMaxBatch);
+    *bytes = ncf::make_layout(*s, max_batch).total;
+    return 0;
+}
+
+int ncf_workspace_init(const ncf_shape_t* s, int64_t max_batch, void* ws, size_t ws_bytes, void* stream) {
+    if (int r = check_shape(s)) return r;
+    ncf::WsLayout L = ncf::make_layout(*s, max_batch);
+    if (!ws || ws_bytes < L.total) return fail(NCF_EINVAL, "workspace too small");
+    static bool configured = false;
+    if (!configured) {
+        // the heavy-segment sort needs up to 2*kMaxBatch/8 bytes of dynamic LDS
+        configured = true;
+    }
+    return hip_check(hipMemsetAsync(ws, 0, L.persistent_end, (hipStream_t)stream), "hipMemsetAsync");
+}
+
+int ncf_predict(const ncf_shape_t* s, const ncf_model_t* model, const int32_t* users, const int32_t* items,
+                int64_t n, float* probs, void* ws, size_t ws_bytes, void* stream) {
+    if (int r = check_shape(s)) return r;
+    ncf::WsLayout L;
+    if (int r = check_ws(*s, n, ws, ws_bytes, &L)) return r;
+    if (!model || !model->emb || !model->mlp || !users || !items || !probs)
+        return fail(NCF_EINVAL, "NULL device pointer");
+    int nbce = 0;
+    return hip_check(ncf::launch_predict_generic(*s, L, ws, model->emb, model->mlp, users, items, nullptr, n, probs,
+                                                 &nbce, (hipStream_t)stream),
+                     "ncf_predict");
+}
+
+int ncf_rank(const float* probs, int64_t n_groups, int32_t group, int32_t* rank_idx, void* stream) {
+    if (!probs || !rank_idx) return fail(NCF_EINVAL, "NULL device pointer");
+    if (group <= 0 || n_groups < 0) return fail(NCF_EINVAL, "invalid group/n_groups");
+    return hip_check(ncf::launch_rank(probs, n_groups, group, rank_idx, (hipStream_t)stream), "ncf_rank");
+}
+
+int ncf_group_metrics(const float* probs, const float* labels, int64_t n_groups, int32_t group, int32_t k,
+                      float* hit, float* dcg, void* stream) {
+    if (!probs || !labels) return fail(NCF_EINVAL, "NULL device pointer");
+    if (group <= 0 || n_groups < 0) return fail(NCF_EINVAL, "invalid group/n_groups");
+    int np = 0;
+    return hip_check(ncf::launch_group_metrics(probs, labels, n_groups, group, k, hit, dcg, nullptr, nullptr, &np,
+                                               (hipStream_t)stream),
+                     "ncf_group_metrics");
+}
+
+// forward + backward + index + metrics summary: shared by train_step and forward_backward
+static int run_fb(const ncf_shape_t& s, const ncf::WsLayout& L, const ncf_model_t* model, const ncf_hyper_t* h,
+                  const int32_t* users, const int32_t* items, const float* labels, int64_t n, void* ws,
+                  float* summary, float* probs_out, int* nslab, hipStream_t st) {
+    hipError_t e = ncf::launch_index_build(s, L, ws, users, items, n, st);
+    if (e != hipSuccess) return hip_check(e, "index build");
+    int nbce = 0;
+    if (use_fused(s, h))
+        e = ncf::launch_fb_fused(s, L, ws, model->emb, model->mlp, users, items, labels, n, h->inv_batch, nslab,
+                                 &nbce, st);
+    else
+        e = ncf::launch_fb_generic(s, L, ws, model->emb, model->mlp, users, items, labels, n, h->inv_batch, nslab,
+                                   &nbce, st);
+    if (e != hipSuccess) return hip_check(e, "forward/backward");
+    float* probs = ncf::at<float>(ws, L.probs);
+    const int64_t ng = n / h->group;
+    int nmet = 0;
+    e = ncf::launch_group_metrics(probs, labels, ng, h->group, h->k, nullptr, nullptr, ncf::at<float>(ws, L.part_hit),
+                                  ncf::at<float>(ws, L.part_dcg), &nmet, st);
+    if (e != hipSuccess) return hip_check(e, "metrics");
+    e = ncf::launch_summary(L, ws, nbce, nmet, (float)ng, summary, st);
+    if (e != hipSuccess) return hip_check(e, "summary");
+    if (probs_out) {
+        e = hipMemcpyAsync(probs_out, probs, (size_t)n * 4, hipMemcpyDeviceToDevice, st);
+        if (e != hipSuccess) return hip_check(e, "probs copy");
+    }
+    return 0;
+}
+
+static int check_train_args(const ncf_shape_t* s, const ncf_model_t* model, const ncf_hyper_t* h,
+                            const int32_t* users, const int32_t* items, const float* labels, int64_t n) {
+    if (int r = check_shape(s)) return r;
+    if (int r = check_hyper(h)) return r;
+    if (!model || !model->emb || !model->mlp || !users || !items || !labels)
+        return fail(NCF_EINVAL, "NULL device pointer");
+    if (n % h->group)
+        return fail(NCF_EINVAL, "Batch size must be divisible by (num_negs_per_pos + 1). Found: batch_size=%lld, "
+                    "group=%d", (long long)n, h->group);
+    return 0;
+}
+
+int ncf_train_step(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* h,
+                   const int32_t* users, const int32_t* items, const float* labels, int64_t n, double* stats,
+                   float* probs_out, void* ws, size_t ws_bytes, void* stream) {
+    if (int r = check_train_args(s, model, h, users, items, labels, n)) return r;
+    if (!optim || !optim->step || (h->optimizer == NCF_OPT_ADAM &&
+                                   (!optim->emb_m || !optim->emb_v || !optim->mlp_m || !optim->mlp_v)))
+        return fail(NCF_EINVAL, "NULL optimizer state");
+    ncf::WsLayout L;
+    if (int r = check_ws(*s, n, ws, ws_bytes, &L)) return r;
+    hipStream_t st = (hipStream_t)stream;
+    float* summary = ncf::at<float>(ws, L.summary);
+    int nslab = 0;
+    if (int r = run_fb(*s, L, model, h, users, items, labels, n, ws, summary, probs_out, &nslab, st)) return r;
+    hipError_t e = ncf::launch_emb_update(*s, L, ws, model->emb, optim->emb_m, optim->emb_v, optim->step, *h,
+                                          nullptr, st);
+    if (e != hipSuccess) return hip_check(e, "embedding update");
+    int nreg_mlp = 0;
+    e = ncf::launch_mlp_update(*s, L, ws, model->mlp, optim->mlp_m, optim->mlp_v, optim->step, *h, nslab, nullptr,
+                               nullptr, true, &nreg_mlp, st);
+    if (e != hipSuccess) return hip_check(e, "dense update");
+    const int nreg_emb = h->l2[0] != 0.0f ? ncf::kUpdateGrid : 0;
+    e = ncf::launch_stats(L, ws, summary, nreg_emb, nreg_mlp, h->inv_batch, stats, optim->step, true, st);
+    return hip_check(e, "stats");
+}
+
+int ncf_forward_backward(const ncf_shape_t* s, const ncf_model_t* model, const ncf_hyper_t* h, const int32_t* users,
+                         const int32_t* items, const float* labels, int64_t n, float* emb_grad, float* mlp_grad,
+                         float* summary, float* probs_out, void* ws, size_t ws_bytes, void* stream) {
+    if (int r = check_train_args(s, model, h, users, items, labels, n)) return r;
+    if (!emb_grad || !mlp_grad || !summary) return fail(NCF_EINVAL, "NULL gradient output");
+    ncf::WsLayout L;
+    if (int r = check_ws(*s, n, ws, ws_bytes, &L)) return r;
+    hipStream_t st = (hipStream_t)stream;
+    int nslab = 0;
+    if (int r = run_fb(*s, L, model, h, users, items, labels, n, ws, summary, probs_out, &nslab, st)) return r;
+    hipError_t e = ncf::launch_emb_grad_dense(*s, L, ws, emb_grad, st);
+    if (e != hipSuccess) return hip_check(e, "dense embedding gradient");
+    int nreg = 0;
+    e = ncf::launch_mlp_update(*s, L, ws, nullptr, nullptr, nullptr, nullptr, *h, nslab, nullptr, mlp_grad, false,
+                               &nreg, st);
+    return hip_check(e, "dense-layer gradient");
+}
+
+int ncf_evaluate(const ncf_shape_t* s, const ncf_model_t* model, const ncf_hyper_t* h, const int32_t* users,
+                 const int32_t* items, const float* labels, int64_t n, double* stats, float* probs_out, void* ws,
+                 size_t ws_bytes, void* stream) {
+    if (int r = check_train_args(s, model, h, users, items, labels, n)) return r;
+    ncf::WsLayout L;
+    if (int r = check_ws(*s, n, ws, ws_bytes, &L)) return r;
+    hipStream_t st = (hipStream_t)stream;
+    float* probs = ncf::at<float>(ws, L.probs);
+    int nbce = 0;
+    hipError_t e = ncf::launch_predict_generic(*s, L, ws, model->emb, model->mlp, users, items, labels, n, probs,
+                                               &nbce, st);
+    if (e != hipSuccess) return hip_check(e, "forward");
+    const int64_t ng = n / h->group;
+    int nmet = 0;
+    e = ncf::launch_group_metrics(probs, labels, ng, h->group, h->k, nullptr, nullptr, ncf::at<float>(ws, L.part_hit),
+                                  ncf::at<float>(ws, L.part_dcg), &nmet, st);
+    if (e != hipSuccess) return hip_check(e, "metrics");
+    float* summary = ncf::at<float>(ws, L.summary);
+    e = ncf::launch_summary(L, ws, nbce, nmet, (float)ng, summary, st);
+    if (e != hipSuccess) return hip_check(e, "summary");
+    int nreg_emb = 0, nreg_mlp = 0;
+    if (h->l2[0] != 0.0f) {
+        e = ncf::launch_emb_reg(*s, L, ws, model->emb, h->l2[0], st);
+        if (e != hipSuccess) return hip_check(e, "embedding l2");
+        nreg_emb = ncf::kUpdateGrid;
+    }
+    e = ncf::launch_mlp_update(*s, L, ws, model->mlp, nullptr, nullptr, nullptr, *h, 0, model->mlp, nullptr, false,
+                               &nreg_mlp, st, true);
+    if (e != hipSuccess) return hip_check(e, "dense l2");
+    if (probs_out) {
+        e = hipMemcpyAsync(probs_out, probs, (size_t)n * 4, hipMemcpyDeviceToDevice, st);
+        if (e != hipSuccess) return hip_check(e, "probs copy");
+    }
+    e = ncf::launch_stats(L, ws, summary, nreg_emb, nreg_mlp, h->inv_batch, stats, nullptr, false, st);
+    return hip_check(e, "stats");
+}
+
+int ncf_apply_update(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* h,
+                     const float* emb_grad, const float* mlp_grad, const float* summary, double* stats, void* ws,
+                     size_t ws_bytes, void* stream) {
+    if (int r = check_shape(s)) return r;
+    if (int r = check_hyper(h)) return r;
+    if (!model || !model->emb || !model->mlp || !emb_grad || !mlp_grad || !summary)
+        return fail(NCF_EINVAL, "NULL device pointer");
+    if (!optim || !optim->step || (h->optimizer == NCF_OPT_ADAM &&
+                                   (!optim->emb_m || !optim->emb_v || !optim->mlp_m || !optim->mlp_v)))
+        return fail(NCF_EINVAL, "NULL optimizer state");
+    ncf::WsLayout L;
+    if (int r = check_ws(*s, 1, ws, ws_bytes, &L)) return r;
+    hipStream_t st = (hipStream_t)stream;
+    hipError_t e = ncf::launch_emb_update(*s, L, ws, model->emb, optim->emb_m, optim->emb_v, optim->step, *h,
+                                          emb_grad, st);
+    if (e != hipSuccess) return hip_check(e, "embedding update");
+    int nreg_mlp = 0;
+    e = ncf::launch_mlp_update(*s, L, ws, model->mlp, optim->mlp_m, optim->mlp_v, optim->step, *h, 0, mlp_grad,
+                               nullptr, true, &nreg_mlp, st);
+    if (e != hipSuccess) return hip_check(e, "dense update");
+    const int nreg_emb = h->l2[0] != 0.0f ? ncf::kUpdateGrid : 0;
+    e = ncf::launch_stats(L, ws, summary, nreg_emb, nreg_mlp, h->inv_batch, stats, optim->step, true, st);
+    return hip_check(e, "stats");
+}
+
+}  // extern "C"

@@ -1,0 +1,383 @@
+// Optimizer sweeps, metrics and loss summaries.
+//
+// Reference semantics (movierec/model.py:199-215 → Keras v1 optimizers):
+//   Adam:  t += 1; lr_t = lr*sqrt(1-b2^t)/(1-b1^t)
+//          m = b1*m + (1-b1)*g;  v = b2*v + (1-b2)*g^2;  p -= lr_t*m/(sqrt(v)+eps)
+//   SGD:   p -= lr*g
+// applied DENSELY to every element of every variable (the embedding's
+// IndexedSlices gradient is densified: rows absent from the batch still decay
+// m, v and move p).  L2 (model.py:163,168,178) adds 2*lambda*p to the gradient
+// of the whole variable and lambda*sum(p^2) to the loss.
+//
+// k_emb_update is the fused "scatter-add + Adam" of the embedding table: one
+// HBM-bound sweep over the table (p, m, v: 24 B/param) that, per row, sums the
+// row's per-sample gradient contributions in ascending sample order through
+// the index built by ncf_index.hip (deterministic, no atomics).
+
+#include <cmath>
+
+#include "ncf_common.h"
+#include "ncf_internal.h"
+
+namespace ncf {
+
+__device__ inline float adam_lr_t(float lr, float b1, float b2, int t) {
+    const float ft = (float)t;
+    return lr * (sqrtf(1.0f - powf(b2, ft)) / (1.0f - powf(b1, ft)));
+}
+
+template <int OPT, int SRC, bool L2>
+__global__ __launch_bounds__(kBlock) void k_emb_update(float4* __restrict__ emb, float4* __restrict__ m4,
+                                                       float4* __restrict__ v4, uint32_t n4, uint32_t w4,
+                                                       const int32_t* __restrict__ offs,
+                                                       const int32_t* __restrict__ list,
+                                                       const float4* __restrict__ gs,
+                                                       const float4* __restrict__ dgrad,
+                                                       const int32_t* __restrict__ step, float lr, float b1,
+                                                       float b2, float eps, float lam, float* __restrict__ part_reg) {
+    __shared__ float red[4];
+    const int t = *step + 1;
+    const float lr_t = (OPT == NCF_OPT_ADAM) ? adam_lr_t(lr, b1, b2, t) : lr;
+    const float c1 = 1.0f - b1, c2 = 1.0f - b2;
+    float reg = 0.0f;
+    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n4; e += gridDim.x * blockDim.x) {
+        float4 p = emb[e];
+        float4 g;
+        if (SRC == kGradSparse) {
+            const uint32_t r = e / w4;
+            const uint32_t q = e - r * w4;
+            const int o = offs[r];
+            const int c = offs[r + 1] - o;
+            g = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int j = 0; j < c; ++j) g = f4add(g, gs[(size_t)list[o + j] * w4 + q]);
+        } else {
+            g = dgrad[e];
+        }
+        if (L2) {
+            reg += lam * (p.x * p.x + p.y * p.y + p.z * p.z + p.w * p.w);
+            const float l2 = 2.0f * lam;
+            g.x += l2 * p.x; g.y += l2 * p.y; g.z += l2 * p.z; g.w += l2 * p.w;
+        }
+        if (OPT == NCF_OPT_ADAM) {
+            float4 mm = m4[e], vv = v4[e];
+            mm.x = b1 * mm.x + c1 * g.x; mm.y = b1 * mm.y + c1 * g.y;
+            mm.z = b1 * mm.z + c1 * g.z; mm.w = b1 * mm.w + c1 * g.w;
+            vv.x = b2 * vv.x + c2 * (g.x * g.x); vv.y = b2 * vv.y + c2 * (g.y * g.y);
+            vv.z = b2 * vv.z + c2 * (g.z * g.z); vv.w = b2 * vv.w + c2 * (g.w * g.w);
+            p.x -= lr_t * mm.x / (sqrtf(vv.x) + eps); p.y -= lr_t * mm.y / (sqrtf(vv.y) + eps);
+            p.z -= lr_t * mm.z / (sqrtf(vv.z) + eps); p.w -= lr_t * mm.w / (sqrtf(vv.w) + eps);
+            m4[e] = mm;
+            v4[e] = vv;
+        } else {
+            p.x -= lr * g.x; p.y -= lr * g.y; p.z -= lr * g.z; p.w -= lr * g.w;
+        }
+        emb[e] = p;
+    }
+    if (L2) {
+        reg = block_sum_256(reg, red);
+        if (threadIdx.x == 0) part_reg[blockIdx.x] = reg;
+    }
+}
+
+// lambda * sum(p^2) over the table (evaluation loss; no update)
+__global__ __launch_bounds__(kBlock) void k_emb_reg(const float4* __restrict__ emb, uint32_t n4, float lam,
+                                                    float* __restrict__ part_reg) {
+    __shared__ float red[4];
+    float reg = 0.0f;
+    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n4; e += gridDim.x * blockDim.x) {
+        const float4 p = emb[e];
+        reg += lam * (p.x * p.x + p.y * p.y + p.z * p.z + p.w * p.w);
+    }
+    reg = block_sum_256(reg, red);
+    if (threadIdx.x == 0) part_reg[blockIdx.x] = reg;
+}
+
+// Dense embedding gradient (data-parallel path): every row written.
+__global__ __launch_bounds__(kBlock) void k_emb_grad_dense(float4* __restrict__ out, uint32_t n4, uint32_t w4,
+                                                           const int32_t* __restrict__ offs,
+                                                           const int32_t* __restrict__ list,
+                                                           const float4* __restrict__ gs) {
+    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n4; e += gridDim.x * blockDim.x) {
+        const uint32_t r = e / w4;
+        const uint32_t q = e - r * w4;
+        const int o = offs[r];
+        const int c = offs[r + 1] - o;
+        float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int j = 0; j < c; ++j) g = f4add(g, gs[(size_t)list[o + j] * w4 + q]);
+        out[e] = g;
+    }
+}
+
+struct L2Table {
+    int n;
+    int start[NCF_MAX_LAYERS];
+    int end[NCF_MAX_LAYERS];
+    float lam[NCF_MAX_LAYERS];
+};
+
+template <int OPT>
+__global__ __launch_bounds__(kBlock) void k_mlp_update(float* __restrict__ p, float* __restrict__ m,
+                                                       float* __restrict__ v, int P, const float* __restrict__ slabs,
+                                                       int nslab, const float* __restrict__ grad_in,
+                                                       float* __restrict__ grad_out, int do_update, int want_reg,
+                                                       const int32_t* __restrict__ step, float lr, float b1, float b2,
+                                                       float eps, L2Table l2t, float* __restrict__ part_reg) {
+    __shared__ float red[4];
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    float reg = 0.0f;
+    if (i < P) {
+        float g = 0.0f;
+        if (nslab > 0) {
+            // fixed slab order → deterministic
+            int s = 0;
+            float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+            for (; s + 4 <= nslab; s += 4) {
+                a0 += slabs[(size_t)(s + 0) * P + i];
+                a1 += slabs[(size_t)(s + 1) * P + i];
+                a2 += slabs[(size_t)(s + 2) * P + i];
+                a3 += slabs[(size_t)(s + 3) * P + i];
+            }
+            for (; s < nslab; ++s) a0 += slabs[(size_t)s * P + i];
+            g = (a0 + a1) + (a2 + a3);
+        } else {
+            g = grad_in[i];
+        }
+        if (grad_out) grad_out[i] = g;
+        if (do_update || want_reg) {
+            float w = p[i];
+            float lam = 0.0f;
+            for (int l = 0; l < l2t.n; ++l)
+                if (i >= l2t.start[l] && i < l2t.end[l]) lam = l2t.lam[l];
+            if (lam != 0.0f) {
+                reg = lam * w * w;
+                g += 2.0f * lam * w;
+            }
+        }
+        if (do_update) {
+            float w = p[i];
+            if (OPT == NCF_OPT_ADAM) {
+                const int t = *step + 1;
+                const float lr_t = adam_lr_t(lr, b1, b2, t);
+                float mm = b1 * m[i] + (1.0f - b1) * g;
+                float vv = b2 * v[i] + (1.0f - b2) * (g * g);
+                w -= lr_t * mm / (sqrtf(vv) + eps);
+                m[i] = mm;
+                v[i] = vv;
+            } else {
+                w -= lr * g;
+            }
+            p[i] = w;
+        }
+    }
+    reg = block_sum_256(reg, red);
+    if (threadIdx.x == 0 && part_reg) part_reg[blockIdx.x] = reg;
+}
+
+// Per-group hit@k / dcg@k: the label's position in the stable descending
+// order equals #(p_j > p_lab) + #(j < lab with p_j == p_lab)  (top_k ties →
+// lower index first; test/test_model.py:121-149).
+__global__ __launch_bounds__(kBlock) void k_group_metrics(const float* __restrict__ probs,
+                                                          const float* __restrict__ labels, int64_t ng, int group,
+                                                          int k, float* __restrict__ hit, float* __restrict__ dcg,
+                                                          float* __restrict__ part_hit, float* __restrict__ part_dcg) {
+    __shared__ float red[4];
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    float h = 0.f, d = 0.f;
+    if (g < ng) {
+        const float* pr = probs + g * group;
+        const float* lb = labels + g * group;
+        int lab = 0;
+        float best = lb[0];
+        for (int j = 1; j < group; ++j)
+            if (lb[j] > best) { best = lb[j]; lab = j; }
+        const float pl = pr[lab];
+        int pos = 0;
+        for (int j = 0; j < group; ++j) {
+            const float pj = pr[j];
+            pos += (pj > pl) || (pj == pl && j < lab);
+        }
+        h = pos < k ? 1.0f : 0.0f;
+        d = h * (logf(2.0f) / logf((float)pos + 2.0f));
+        if (hit) hit[g] = h;
+        if (dcg) dcg[g] = d;
+    }
+    h = block_sum_256(h, red);
+    d = block_sum_256(d, red);
+    if (threadIdx.x == 0) {
+        if (part_hit) part_hit[blockIdx.x] = h;
+        if (part_dcg) part_dcg[blockIdx.x] = d;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_rank(const float* __restrict__ probs, int64_t ng, int group,
+                                                 int32_t* __restrict__ out) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= ng) return;
+    const float* pr = probs + g * group;
+    int32_t* o = out + g * group;
+    for (int e = 0; e < group; ++e) {
+        const float pe = pr[e];
+        int pos = 0;
+        for (int j = 0; j < group; ++j) {
+            const float pj = pr[j];
+            pos += (pj > pe) || (pj == pe && j < e);
+        }
+        o[pos] = e;
+    }
+}
+
+__device__ inline float block_sum_array(const float* __restrict__ a, int n, float* red) {
+    float x = 0.f;
+    for (int j = threadIdx.x; j < n; j += kBlock) x += a[j];
+    return block_sum_256(x, red);
+}
+
+__global__ __launch_bounds__(kBlock) void k_summary(const float* __restrict__ part_bce, int nbce,
+                                                    const float* __restrict__ part_hit,
+                                                    const float* __restrict__ part_dcg, int nmet, float n_groups,
+                                                    float* __restrict__ summary) {
+    __shared__ float red[4];
+    const float b = block_sum_array(part_bce, nbce, red);
+    const float h = block_sum_array(part_hit, nmet, red);
+    const float d = block_sum_array(part_dcg, nmet, red);
+    if (threadIdx.x == 0) {
+        summary[NCF_SUM_BCE] = b;
+        summary[NCF_SUM_HIT] = h;
+        summary[NCF_SUM_DCG] = d;
+        summary[NCF_SUM_GROUPS] = n_groups;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_stats(const float* __restrict__ summary,
+                                                  const float* __restrict__ reg_emb, int nreg_emb,
+                                                  const float* __restrict__ reg_mlp, int nreg_mlp, float inv_batch,
+                                                  double* __restrict__ stats, int32_t* step, int bump) {
+    __shared__ float red[4];
+    const float re = block_sum_array(reg_emb, nreg_emb, red);
+    const float rm = block_sum_array(reg_mlp, nreg_mlp, red);
+    if (threadIdx.x == 0) {
+        const float loss = summary[NCF_SUM_BCE] * inv_batch + (re + rm);
+        const float ng = summary[NCF_SUM_GROUPS];
+        const float hr = ng > 0.f ? summary[NCF_SUM_HIT] / ng : 0.f;
+        const float dc = ng > 0.f ? summary[NCF_SUM_DCG] / ng : 0.f;
+        if (stats) {
+            stats[NCF_STAT_LOSS_SUM] += (double)loss;
+            stats[NCF_STAT_HR_SUM] += (double)hr;
+            stats[NCF_STAT_DCG_SUM] += (double)dc;
+            stats[NCF_STAT_STEPS] += 1.0;
+            stats[NCF_STAT_LAST_LOSS] = loss;
+            stats[NCF_STAT_LAST_HR] = hr;
+            stats[NCF_STAT_LAST_DCG] = dc;
+        }
+        if (bump) *step += 1;
+    }
+}
+
+// ---------------------------------------------------------------------------
+
+static L2Table make_l2_table(const ncf_shape_t& s, const ncf_hyper_t& h) {
+    L2Table t{};
+    t.n = 0;
+    for (int l = 1; l < s.num_layers; ++l) {
+        if (h.l2[l] == 0.0f) continue;
+        t.start[t.n] = s.layer_off[l];
+        t.end[t.n] = s.layer_off[l] + s.layers[l - 1] * s.layers[l];
+        t.lam[t.n] = h.l2[l];
+        ++t.n;
+    }
+    return t;
+}
+
+hipError_t launch_emb_update(const ncf_shape_t& s, const WsLayout& L, void* ws, float* emb, float* m, float* v,
+                             const int32_t* step, const ncf_hyper_t& h, const float* dense_grad, hipStream_t st) {
+    const uint32_t w4 = (uint32_t)(s.row_width / 4);
+    const uint32_t n4 = (uint32_t)(s.num_rows * w4);
+    const int32_t* offs = at<int32_t>(ws, L.offs);
+    const int32_t* list = at<int32_t>(ws, L.list);
+    const float4* gs = at<const float4>(ws, L.gs);
+    float* part = at<float>(ws, L.part_reg);
+    const bool l2 = h.l2[0] != 0.0f;
+    const int src = dense_grad ? kGradDense : kGradSparse;
+    dim3 grid(kUpdateGrid), blk(kBlock);
+#define NCF_EMB_LAUNCH(OPT, SRC, L2)                                                                          \
+    k_emb_update<OPT, SRC, L2><<<grid, blk, 0, st>>>((float4*)emb, (float4*)m, (float4*)v, n4, w4, offs, list, gs, \
+                                                     (const float4*)dense_grad, step, h.lr, h.beta_1, h.beta_2,    \
+                                                     h.epsilon, h.l2[0], part)
+    if (h.optimizer == NCF_OPT_ADAM) {
+        if (src == kGradSparse) { if (l2) NCF_EMB_LAUNCH(NCF_OPT_ADAM, kGradSparse, true); else NCF_EMB_LAUNCH(NCF_OPT_ADAM, kGradSparse, false); }
+        else { if (l2) NCF_EMB_LAUNCH(NCF_OPT_ADAM, kGradDense, true); else NCF_EMB_LAUNCH(NCF_OPT_ADAM, kGradDense, false); }
+    } else {
+        if (src == kGradSparse) { if (l2) NCF_EMB_LAUNCH(NCF_OPT_SGD, kGradSparse, true); else NCF_EMB_LAUNCH(NCF_OPT_SGD, kGradSparse, false); }
+        else { if (l2) NCF_EMB_LAUNCH(NCF_OPT_SGD, kGradDense, true); else NCF_EMB_LAUNCH(NCF_OPT_SGD, kGradDense, false); }
+    }
+#undef NCF_EMB_LAUNCH
+    return hipGetLastError();
+}
+
+hipError_t launch_emb_grad_dense(const ncf_shape_t& s, const WsLayout& L, void* ws, float* out, hipStream_t st) {
+    const uint32_t w4 = (uint32_t)(s.row_width / 4);
+    const uint32_t n4 = (uint32_t)(s.num_rows * w4);
+    k_emb_grad_dense<<<kUpdateGrid, kBlock, 0, st>>>((float4*)out, n4, w4, at<int32_t>(ws, L.offs),
+                                                     at<int32_t>(ws, L.list), at<const float4>(ws, L.gs));
+    return hipGetLastError();
+}
+
+hipError_t launch_emb_reg(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, float lam,
+                          hipStream_t st) {
+    const uint32_t n4 = (uint32_t)(s.num_rows * (s.row_width / 4));
+    k_emb_reg<<<kUpdateGrid, kBlock, 0, st>>>((const float4*)emb, n4, lam, at<float>(ws, L.part_reg));
+    return hipGetLastError();
+}
+
+hipError_t launch_mlp_update(const ncf_shape_t& s, const WsLayout& L, void* ws, float* mlp, float* m, float* v,
+                             const int32_t* step, const ncf_hyper_t& h, int nslab, const float* grad_in,
+                             float* grad_out, bool do_update, int* nreg, hipStream_t st, bool want_reg) {
+    const int P = s.mlp_params;
+    const int grid = (P + kBlock - 1) / kBlock;
+    float* part = at<float>(ws, L.part_reg) + kUpdateGrid;
+    const L2Table t = make_l2_table(s, h);
+    if (h.optimizer == NCF_OPT_ADAM)
+        k_mlp_update<NCF_OPT_ADAM><<<grid, kBlock, 0, st>>>(mlp, m, v, P, at<float>(ws, L.slabs), nslab, grad_in,
+                                                            grad_out, do_update ? 1 : 0, want_reg ? 1 : 0, step,
+                                                            h.lr, h.beta_1, h.beta_2, h.epsilon, t, part);
+    else
+        k_mlp_update<NCF_OPT_SGD><<<grid, kBlock, 0, st>>>(mlp, m, v, P, at<float>(ws, L.slabs), nslab, grad_in,
+                                                           grad_out, do_update ? 1 : 0, want_reg ? 1 : 0, step,
+                                                           h.lr, h.beta_1, h.beta_2, h.epsilon, t, part);
+    *nreg = ((do_update || want_reg) && t.n > 0) ? grid : 0;
+    return hipGetLastError();
+}
+
+hipError_t launch_group_metrics(const float* probs, const float* labels, int64_t n_groups, int group, int k,
+                                float* hit, float* dcg, float* part_hit, float* part_dcg, int* nparts,
+                                hipStream_t st) {
+    const int grid = (int)((n_groups + kBlock - 1) / kBlock);
+    *nparts = grid;
+    if (grid == 0) return hipSuccess;
+    k_group_metrics<<<grid, kBlock, 0, st>>>(probs, labels, n_groups, group, k, hit, dcg, part_hit, part_dcg);
+    return hipGetLastError();
+}
+
+hipError_t launch_rank(const float* probs, int64_t n_groups, int group, int32_t* rank_idx, hipStream_t st) {
+    const int grid = (int)((n_groups + kBlock - 1) / kBlock);
+    if (grid == 0) return hipSuccess;
+    k_rank<<<grid, kBlock, 0, st>>>(probs, n_groups, group, rank_idx);
+    return hipGetLastError();
+}
+
+hipError_t launch_summary(const WsLayout& L, void* ws, int nbce, int nmet, float n_groups, float* summary,
+                          hipStream_t st) {
+    k_summary<<<1, kBlock, 0, st>>>(at<float>(ws, L.part_bce), nbce, at<float>(ws, L.part_hit),
+                                    at<float>(ws, L.part_dcg), nmet, n_groups, summary);
+    return hipGetLastError();
+}
+
+hipError_t launch_stats(const WsLayout& L, void* ws, const float* summary, int nreg_emb, int nreg_mlp,
+                        float inv_batch, double* stats, int32_t* step, bool bump_step, hipStream_t st) {
+    const float* reg = at<float>(ws, L.part_reg);
+    k_stats<<<1, kBlock, 0, st>>>(summary, reg, nreg_emb, reg + kUpdateGrid, nreg_mlp, inv_batch, stats, step,
+                                  bump_step ? 1 : 0);
+    return hipGetLastError();
+}
+
+}  // namespace ncf

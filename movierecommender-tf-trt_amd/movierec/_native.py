@@ -1,0 +1,113 @@
+"""ctypes binding of the C ABI in ``include/movierec_ncf.h``.
+
+The shared library is ``movierec/_lib/libmovierec_ncf.so`` (built in-tree by
+``csrc/build.py`` / ``__graft_entry__.build()``).  There is no fallback: if
+the library is missing or cannot be loaded, :func:`lib` raises — the HIP path
+is the product.
+
+``torch`` is imported first on purpose: the library's NEEDED
+``libamdhip64.so.7`` then resolves to the HIP runtime PyTorch already loaded,
+so torch streams and device pointers are valid inside the library.
+"""
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the library load, see module doc)
+
+NCF_MAX_LAYERS = 8
+NCF_EINVAL = -1
+NCF_EHIP = -2
+NCF_OPT_ADAM = 0
+NCF_OPT_SGD = 1
+NCF_NUM_STATS = 8
+NCF_NUM_SUMMARY = 4
+STAT_LOSS_SUM, STAT_HR_SUM, STAT_DCG_SUM, STAT_STEPS, STAT_LAST_LOSS, STAT_LAST_HR, STAT_LAST_DCG = range(7)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libmovierec_ncf.so")
+
+_i32 = ctypes.c_int32
+_i64 = ctypes.c_int64
+_f32 = ctypes.c_float
+_vp = ctypes.c_void_p
+
+
+class NcfShape(ctypes.Structure):
+    _fields_ = [("num_users", _i32), ("num_items", _i32), ("num_layers", _i32), ("gmf_dim", _i32),
+                ("layers", _i32 * NCF_MAX_LAYERS),
+                ("du", _i32), ("di", _i32), ("gmf_stride", _i32), ("row_width", _i32),
+                ("num_rows", _i64), ("out_features", _i32), ("mlp_params", _i32),
+                ("layer_off", _i32 * NCF_MAX_LAYERS), ("fast_path", _i32), ("reserved", _i32 * 7)]
+
+
+class NcfModel(ctypes.Structure):
+    _fields_ = [("emb", _vp), ("mlp", _vp)]
+
+
+class NcfOptim(ctypes.Structure):
+    _fields_ = [("emb_m", _vp), ("emb_v", _vp), ("mlp_m", _vp), ("mlp_v", _vp), ("step", _vp)]
+
+
+class NcfHyper(ctypes.Structure):
+    _fields_ = [("optimizer", _i32), ("lr", _f32), ("beta_1", _f32), ("beta_2", _f32), ("epsilon", _f32),
+                ("l2", _f32 * NCF_MAX_LAYERS), ("group", _i32), ("k", _i32), ("inv_batch", _f32),
+                ("force_generic", _i32), ("reserved", _i32 * 6)]
+
+
+_P = ctypes.POINTER
+_SIGNATURES = {
+    "ncf_abi_version": (ctypes.c_int, []),
+    "ncf_last_error": (ctypes.c_char_p, []),
+    "ncf_shape_init": (ctypes.c_int, [_P(NcfShape), _i32, _i32, _P(_i32), _i32, _i32]),
+    "ncf_workspace_size": (ctypes.c_int, [_P(NcfShape), _i64, _P(ctypes.c_size_t)]),
+    "ncf_workspace_init": (ctypes.c_int, [_P(NcfShape), _i64, _vp, ctypes.c_size_t, _vp]),
+    "ncf_predict": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _vp, _vp, _i64, _vp, _vp, ctypes.c_size_t, _vp]),
+    "ncf_rank": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp]),
+    "ncf_group_metrics": (ctypes.c_int, [_vp, _vp, _i64, _i32, _i32, _vp, _vp, _vp]),
+    "ncf_train_step": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _vp, _vp, _vp, _i64,
+                                      _vp, _vp, _vp, ctypes.c_size_t, _vp]),
+    "ncf_evaluate": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfHyper), _vp, _vp, _vp, _i64, _vp, _vp, _vp,
+                                    ctypes.c_size_t, _vp]),
+    "ncf_forward_backward": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfHyper), _vp, _vp, _vp, _i64, _vp, _vp,
+                                            _vp, _vp, _vp, ctypes.c_size_t, _vp]),
+    "ncf_apply_update": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _vp, _vp, _vp, _vp,
+                                        _vp, ctypes.c_size_t, _vp]),
+}
+EXPORTED = sorted(_SIGNATURES)
+
+_lib = None
+
+
+def lib():
+    """Load (once) and return the library; raises if it is not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError("libmovierec_ncf.so not found at %s — run __graft_entry__.build() "
+                               "(there is no CPU fallback)" % LIB_PATH)
+        handle = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = handle
+    return _lib
+
+
+def check(rc):
+    if rc == 0:
+        return
+    msg = lib().ncf_last_error().decode("utf-8", "replace")
+    if rc == NCF_EINVAL:
+        if msg.startswith("Optimizer") and "not implemented" in msg:
+            raise NotImplementedError(msg)
+        raise ValueError(msg)
+    raise RuntimeError("HIP error in movierec native library: %s" % msg)
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def stream_handle(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)

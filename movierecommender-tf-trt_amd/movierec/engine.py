@@ -1,0 +1,272 @@
+"""Device-resident NCF/NeuMF state and the calls into the HIP library.
+
+``NCFEngine`` owns the model and optimizer tensors on one GPU (fp32, layouts
+described in ``include/movierec_ncf.h``) and exposes the hot path:
+``train_step`` (Keras ``train_on_batch``), ``evaluate`` (validation batch),
+``predict`` (``predict_on_batch`` output[0]), ``rank`` (``RankLayer``),
+``group_metrics`` (``hit_rate`` / ``discounted_cumulative_gain``), and the
+data-parallel split ``forward_backward`` + ``apply_update``.
+
+PyTorch provides device memory, the stream and torch.distributed; every
+arithmetic step of the path runs in the library's HIP kernels.
+"""
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _native as N
+
+KERAS_EPSILON = 1e-7
+
+
+def keras_weight_names(layers, gmf_dim):
+    names = ["user_embedding", "item_embedding"]
+    if gmf_dim > 0:
+        names += ["user_gmf_embedding", "item_gmf_embedding"]
+    for l in range(1, len(layers)):
+        names += ["hidden_%d/kernel" % l, "hidden_%d/bias" % l]
+    return names + ["output/kernel", "output/bias"]
+
+
+class NCFEngine(object):
+    """Model + optimizer state of one replica on one device."""
+
+    def __init__(self, num_users, num_items, layers_sizes, gmf_dim=0, max_batch=65536, device=None,
+                 optimizer="adam", lr=0.001, beta_1=0.9, beta_2=0.999, layers_l2reg=None,
+                 force_generic=False):
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise RuntimeError("NCFEngine needs a HIP device (got %s); there is no CPU path" % self.device)
+        L = N.lib()
+        self.layers = [int(x) for x in layers_sizes]
+        self.gmf_dim = int(gmf_dim)
+        self.shape = N.NcfShape()
+        arr = (ctypes.c_int32 * len(self.layers))(*self.layers)
+        N.check(L.ncf_shape_init(ctypes.byref(self.shape), int(num_users), int(num_items), arr, len(self.layers),
+                                 self.gmf_dim))
+        s = self.shape
+        self.num_users, self.num_items = int(num_users), int(num_items)
+        self.row_width = s.row_width
+        self.num_rows = s.num_rows
+        self.mlp_params = s.mlp_params
+        dev = self.device
+        with torch.cuda.device(dev):
+            self.emb = torch.zeros(s.num_rows, s.row_width, dtype=torch.float32, device=dev)
+            self.mlp = torch.zeros(s.mlp_params, dtype=torch.float32, device=dev)
+            self.emb_m = torch.zeros_like(self.emb)
+            self.emb_v = torch.zeros_like(self.emb)
+            self.mlp_m = torch.zeros_like(self.mlp)
+            self.mlp_v = torch.zeros_like(self.mlp)
+            self.step = torch.zeros(1, dtype=torch.int32, device=dev)
+            self.stats = torch.zeros(N.NCF_NUM_STATS, dtype=torch.float64, device=dev)
+            self.val_stats = torch.zeros(N.NCF_NUM_STATS, dtype=torch.float64, device=dev)
+            self.max_batch = 0
+            self.ws = None
+            self._ensure_ws(int(max_batch))
+        self.model_s = N.NcfModel(self.emb.data_ptr(), self.mlp.data_ptr())
+        self.optim_s = N.NcfOptim(self.emb_m.data_ptr(), self.emb_v.data_ptr(), self.mlp_m.data_ptr(),
+                                  self.mlp_v.data_ptr(), self.step.data_ptr())
+        self.hyper = N.NcfHyper()
+        self.set_hyper(optimizer, lr, beta_1, beta_2, layers_l2reg or [0.0] * len(self.layers))
+        self.hyper.force_generic = 1 if force_generic else 0
+
+    # ------------------------------------------------------------------ setup
+    @property
+    def fast_path(self):
+        return bool(self.shape.fast_path) and not self.hyper.force_generic
+
+    def set_hyper(self, optimizer, lr, beta_1=0.9, beta_2=0.999, layers_l2reg=None, group=None, k=None):
+        h = self.hyper
+        opt = {"adam": N.NCF_OPT_ADAM, "sgd": N.NCF_OPT_SGD}.get(optimizer)
+        if opt is None:
+            raise NotImplementedError("Optimizer {} is not implemented.".format(optimizer))
+        h.optimizer = opt
+        h.lr, h.beta_1, h.beta_2, h.epsilon = float(lr), float(beta_1), float(beta_2), KERAS_EPSILON
+        if layers_l2reg is not None:
+            for i in range(N.NCF_MAX_LAYERS):
+                h.l2[i] = float(layers_l2reg[i]) if i < len(layers_l2reg) else 0.0
+        if group is not None:
+            h.group = int(group)
+        if k is not None:
+            h.k = int(k)
+
+    def _ensure_ws(self, n):
+        if n <= self.max_batch:
+            return
+        L = N.lib()
+        nbytes = ctypes.c_size_t()
+        N.check(L.ncf_workspace_size(ctypes.byref(self.shape), int(n), ctypes.byref(nbytes)))
+        self.ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=self.device)
+        self.ws_bytes = int(nbytes.value)
+        N.check(L.ncf_workspace_init(ctypes.byref(self.shape), int(n), N.ptr(self.ws), self.ws_bytes,
+                                     N.stream_handle(self.device)))
+        self.max_batch = int(n)
+
+    # --------------------------------------------------- weights marshalling
+    def set_keras_weights(self, w):
+        """Load a dict of Keras-layout arrays (names as ``keras_weight_names``)."""
+        s = self.shape
+        U, G, G4 = self.num_users, self.gmf_dim, s.gmf_stride
+        emb = np.zeros((s.num_rows, s.row_width), dtype=np.float32)
+        emb[:U, G4:G4 + s.du] = np.asarray(w["user_embedding"], dtype=np.float32)
+        emb[U:, G4:G4 + s.di] = np.asarray(w["item_embedding"], dtype=np.float32)
+        if G > 0:
+            emb[:U, :G] = np.asarray(w["user_gmf_embedding"], dtype=np.float32)
+            emb[U:, :G] = np.asarray(w["item_gmf_embedding"], dtype=np.float32)
+        parts = []
+        for l in range(1, len(self.layers)):
+            parts += [np.asarray(w["hidden_%d/kernel" % l], np.float32).ravel(),
+                      np.asarray(w["hidden_%d/bias" % l], np.float32).ravel()]
+        parts += [np.asarray(w["output/kernel"], np.float32).ravel(), np.asarray(w["output/bias"], np.float32).ravel()]
+        flat = np.concatenate(parts)
+        assert flat.size == self.mlp_params
+        self.emb.copy_(torch.from_numpy(emb))
+        self.mlp.copy_(torch.from_numpy(flat))
+
+    def keras_weights(self, emb=None, mlp=None):
+        """Current weights (or the given device tensors in this layout) as a Keras-layout dict."""
+        s = self.shape
+        U, G, G4 = self.num_users, self.gmf_dim, s.gmf_stride
+        e = (self.emb if emb is None else emb).detach().cpu().numpy()
+        f = (self.mlp if mlp is None else mlp).detach().cpu().numpy()
+        w = {"user_embedding": e[:U, G4:G4 + s.du].copy(), "item_embedding": e[U:, G4:G4 + s.di].copy()}
+        if G > 0:
+            w["user_gmf_embedding"] = e[:U, :G].copy()
+            w["item_gmf_embedding"] = e[U:, :G].copy()
+        off = 0
+        for l in range(1, len(self.layers)):
+            a, b = self.layers[l - 1], self.layers[l]
+            w["hidden_%d/kernel" % l] = f[off:off + a * b].reshape(a, b).copy()
+            off += a * b
+            w["hidden_%d/bias" % l] = f[off:off + b].copy()
+            off += b
+        F = s.out_features
+        w["output/kernel"] = f[off:off + F].reshape(F, 1).copy()
+        w["output/bias"] = f[off + F:off + F + 1].copy()
+        return w
+
+    def optimizer_state(self):
+        """Adam moments as Keras-layout dicts (m, v) and the iteration count."""
+        return (self.keras_weights(self.emb_m, self.mlp_m), self.keras_weights(self.emb_v, self.mlp_v),
+                int(self.step.item()))
+
+    def set_optimizer_state(self, m, v, step):
+        saved = (self.emb.clone(), self.mlp.clone())
+        self.set_keras_weights(m)
+        self.emb_m.copy_(self.emb)
+        self.mlp_m.copy_(self.mlp)
+        self.set_keras_weights(v)
+        self.emb_v.copy_(self.emb)
+        self.mlp_v.copy_(self.mlp)
+        self.emb.copy_(saved[0])
+        self.mlp.copy_(saved[1])
+        self.step.fill_(int(step))
+
+    # ------------------------------------------------------------- hot path
+    def _ids(self, x):
+        if not torch.is_tensor(x):
+            x = torch.from_numpy(np.ascontiguousarray(np.asarray(x).reshape(-1), dtype=np.int32))
+        if x.dtype != torch.int32:
+            x = x.to(torch.int32)
+        return x.reshape(-1).to(self.device, non_blocking=True).contiguous()
+
+    def _labels(self, y):
+        if not torch.is_tensor(y):
+            y = torch.from_numpy(np.ascontiguousarray(np.asarray(y).reshape(-1), dtype=np.float32))
+        return y.reshape(-1).to(device=self.device, dtype=torch.float32, non_blocking=True).contiguous()
+
+    def check_ids(self, users, items):
+        """Host-side range check (TF's gather raises on out-of-range ids)."""
+        u = np.asarray(users)
+        i = np.asarray(items)
+        if u.size and (u.min() < 0 or u.max() >= self.num_users):
+            raise ValueError("user id out of range [0, %d)" % self.num_users)
+        if i.size and (i.min() < 0 or i.max() >= self.num_items):
+            raise ValueError("item id out of range [0, %d)" % self.num_items)
+
+    def train_step(self, users, items, labels, group, k, inv_batch=None, probs_out=None):
+        u, i, y = self._ids(users), self._ids(items), self._labels(labels)
+        n = u.numel()
+        self._ensure_ws(n)
+        h = self.hyper
+        h.group, h.k = int(group), int(k)
+        h.inv_batch = 1.0 / n if inv_batch is None else float(inv_batch)
+        N.check(N.lib().ncf_train_step(ctypes.byref(self.shape), ctypes.byref(self.model_s),
+                                       ctypes.byref(self.optim_s), ctypes.byref(h), N.ptr(u), N.ptr(i), N.ptr(y), n,
+                                       N.ptr(self.stats), N.ptr(probs_out), N.ptr(self.ws), self.ws_bytes,
+                                       N.stream_handle(self.device)))
+
+    def evaluate(self, users, items, labels, group, k, stats=None, probs_out=None):
+        u, i, y = self._ids(users), self._ids(items), self._labels(labels)
+        n = u.numel()
+        self._ensure_ws(n)
+        h = self.hyper
+        h.group, h.k = int(group), int(k)
+        h.inv_batch = 1.0 / n
+        st = self.val_stats if stats is None else stats
+        N.check(N.lib().ncf_evaluate(ctypes.byref(self.shape), ctypes.byref(self.model_s), ctypes.byref(h),
+                                     N.ptr(u), N.ptr(i), N.ptr(y), n, N.ptr(st), N.ptr(probs_out), N.ptr(self.ws),
+                                     self.ws_bytes, N.stream_handle(self.device)))
+
+    def predict(self, users, items):
+        u, i = self._ids(users), self._ids(items)
+        n = u.numel()
+        self._ensure_ws(n)
+        out = torch.empty(n, dtype=torch.float32, device=self.device)
+        N.check(N.lib().ncf_predict(ctypes.byref(self.shape), ctypes.byref(self.model_s), N.ptr(u), N.ptr(i), n,
+                                    N.ptr(out), N.ptr(self.ws), self.ws_bytes, N.stream_handle(self.device)))
+        return out
+
+    def rank(self, probs, group):
+        probs = probs.reshape(-1).contiguous()
+        ng = probs.numel() // group
+        out = torch.empty(ng, group, dtype=torch.int32, device=self.device)
+        N.check(N.lib().ncf_rank(N.ptr(probs), ng, int(group), N.ptr(out), N.stream_handle(self.device)))
+        return out
+
+    def group_metrics(self, probs, labels, group, k):
+        probs = probs.reshape(-1).contiguous()
+        y = self._labels(labels)
+        ng = probs.numel() // group
+        hit = torch.empty(ng, dtype=torch.float32, device=self.device)
+        dcg = torch.empty(ng, dtype=torch.float32, device=self.device)
+        N.check(N.lib().ncf_group_metrics(N.ptr(probs), N.ptr(y), ng, int(group), int(k), N.ptr(hit), N.ptr(dcg),
+                                          N.stream_handle(self.device)))
+        return hit, dcg
+
+    # ------------------------------------------------- data-parallel split
+    def alloc_grads(self):
+        return (torch.empty_like(self.emb), torch.empty_like(self.mlp),
+                torch.empty(N.NCF_NUM_SUMMARY, dtype=torch.float32, device=self.device))
+
+    def forward_backward(self, users, items, labels, group, k, inv_batch, grads, probs_out=None):
+        u, i, y = self._ids(users), self._ids(items), self._labels(labels)
+        n = u.numel()
+        self._ensure_ws(n)
+        h = self.hyper
+        h.group, h.k, h.inv_batch = int(group), int(k), float(inv_batch)
+        eg, mg, sm = grads
+        N.check(N.lib().ncf_forward_backward(ctypes.byref(self.shape), ctypes.byref(self.model_s), ctypes.byref(h),
+                                             N.ptr(u), N.ptr(i), N.ptr(y), n, N.ptr(eg), N.ptr(mg), N.ptr(sm),
+                                             N.ptr(probs_out), N.ptr(self.ws), self.ws_bytes,
+                                             N.stream_handle(self.device)))
+
+    def apply_update(self, grads, inv_batch):
+        eg, mg, sm = grads
+        self.hyper.inv_batch = float(inv_batch)
+        N.check(N.lib().ncf_apply_update(ctypes.byref(self.shape), ctypes.byref(self.model_s),
+                                         ctypes.byref(self.optim_s), ctypes.byref(self.hyper), N.ptr(eg), N.ptr(mg),
+                                         N.ptr(sm), N.ptr(self.stats), N.ptr(self.ws), self.ws_bytes,
+                                         N.stream_handle(self.device)))
+
+    # ------------------------------------------------------------- stats
+    @staticmethod
+    def read_stats(t):
+        s = t.detach().cpu().numpy()
+        steps = max(s[N.STAT_STEPS], 1.0)
+        return dict(loss=s[N.STAT_LOSS_SUM] / steps, hr=s[N.STAT_HR_SUM] / steps, dcg=s[N.STAT_DCG_SUM] / steps,
+                    steps=int(s[N.STAT_STEPS]))

@@ -1,0 +1,65 @@
+"""CPU-side checks of the C ABI: the library loads, exports every function
+declared in include/movierec_ncf.h, validates shapes and sizes workspaces
+(host-only entry points; no kernel launches)."""
+
+import ctypes
+import os
+import re
+
+import pytest
+
+from movierec import _native as N
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared():
+    text = open(os.path.join(ROOT, "include", "movierec_ncf.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(ncf_\w+)\s*\(", text, re.M)))
+
+
+def test_header_and_binding_agree():
+    assert _declared() == N.EXPORTED
+
+
+def test_library_exports_every_symbol():
+    L = N.lib()
+    for name in _declared():
+        assert hasattr(L, name), name
+    assert L.ncf_abi_version() == 1
+
+
+def _shape(nu, ni, layers, g):
+    s = N.NcfShape()
+    arr = (ctypes.c_int32 * len(layers))(*layers)
+    N.check(N.lib().ncf_shape_init(ctypes.byref(s), nu, ni, arr, len(layers), g))
+    return s
+
+
+def test_shape_init_derivations():
+    s = _shape(138493, 27278, [128, 64, 32, 16], 64)
+    assert (s.du, s.di, s.gmf_stride, s.row_width) == (64, 64, 64, 128)
+    assert s.num_rows == 138493 + 27278
+    assert s.out_features == 80
+    assert s.mlp_params == 128 * 64 + 64 + 64 * 32 + 32 + 32 * 16 + 16 + 80 + 1
+    s = _shape(5, 10, [7, 4], 3)   # odd split: du=3, di=4 (model.py:159-160)
+    assert (s.du, s.di, s.gmf_stride, s.row_width) == (3, 4, 4, 8)
+
+
+def test_shape_init_rejects_bad_dims():
+    s = N.NcfShape()
+    arr = (ctypes.c_int32 * 2)(0, 4)
+    with pytest.raises(ValueError):
+        N.check(N.lib().ncf_shape_init(ctypes.byref(s), 5, 10, arr, 2, 0))
+    with pytest.raises(ValueError):
+        N.check(N.lib().ncf_shape_init(ctypes.byref(s), 5, 10, arr, 0, 0))
+
+
+def test_workspace_size_scales_with_batch():
+    s = _shape(6040, 3952, [64, 32, 16, 8], 8)
+    a, b = ctypes.c_size_t(), ctypes.c_size_t()
+    N.check(N.lib().ncf_workspace_size(ctypes.byref(s), 1024, ctypes.byref(a)))
+    N.check(N.lib().ncf_workspace_size(ctypes.byref(s), 4096, ctypes.byref(b)))
+    assert b.value > a.value > 0
+    with pytest.raises(ValueError):
+        N.check(N.lib().ncf_workspace_size(ctypes.byref(s), 0, ctypes.byref(a)))

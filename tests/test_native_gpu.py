@@ -1,0 +1,216 @@
+"""HIP path vs the CPU oracle, through the C ABI (ctypes → libmovierec_ncf.so).
+
+Tolerances (fp32 device arithmetic vs float64 oracle; stated per north_star
+"within a stated fp32 tolerance"):
+  * probabilities: |dp| <= 2e-6
+  * loss: relative 1e-5
+  * gradients: |dg| <= 1e-5 * max|g| (+1e-9)
+  * weights after k optimizer steps: |dw| <= k * 2e-6 (Adam moves each element
+    by at most ~lr per step; fp32 rounding of m/sqrt(v) bounds the drift)
+  * hr/dcg, ranking: exact.
+"""
+
+import numpy as np
+import pytest
+
+from conftest import gpu_available
+from oracle import ncf_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+if gpu_available():
+    import torch
+    from movierec.engine import NCFEngine
+
+
+SHAPES = [
+    # (num_users, num_items, layers, gmf_dim)
+    (5, 10, [6, 4], 0),                 # reference test model (test/test_model.py:8-26)
+    (37, 53, [8, 6, 4], 4),
+    (120, 90, [64, 32, 16, 8], 8),      # config B shape (ml-1m NeuMF) at small row counts
+    (200, 150, [128, 64, 32, 16], 64),  # config C shape (ml-20m NeuMF)
+    (31, 17, [7, 5], 3),                # odd widths: du != di, gmf not a multiple of 4
+]
+
+
+def _weights(shape, seed, scale=4.0):
+    w = O.init_weights(shape, seed=seed)
+    rng = np.random.RandomState(seed + 100)
+    for k in w:
+        if k.endswith("embedding"):
+            w[k] = rng.uniform(-0.5, 0.5, size=w[k].shape)
+        else:
+            w[k] = w[k] * scale
+            if k.endswith("bias"):
+                w[k] = rng.uniform(-0.1, 0.1, size=w[k].shape)
+    # round to fp32 so both sides start from identical values
+    return {k: v.astype(np.float32).astype(np.float64) for k, v in w.items()}
+
+
+def _batch(shape, B, group, seed, dup_items=None):
+    rng = np.random.RandomState(seed)
+    users = rng.randint(0, shape.num_users, B // group).repeat(group)
+    hi = shape.num_items if dup_items is None else dup_items
+    items = rng.randint(0, hi, B)
+    y = np.tile([0] * (group - 1) + [1], B // group)
+    return users.astype(np.int32), items.astype(np.int32), y.astype(np.float32)
+
+
+def _engine(shape, w, **kw):
+    eng = NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=4096, **kw)
+    eng.set_keras_weights(w)
+    return eng
+
+
+def _close(a, b, atol, name=""):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    err = np.max(np.abs(a - b)) if a.size else 0.0
+    assert err <= atol, "%s: max err %g > %g" % (name, err, atol)
+
+
+@pytest.mark.parametrize("dims", SHAPES, ids=[str(s[2]) + "g" + str(s[3]) for s in SHAPES])
+def test_predict_matches_oracle(dims):
+    shape = O.NCFShape(*dims)
+    w = _weights(shape, 1)
+    users, items, _ = _batch(shape, 200, 4, 2)
+    eng = _engine(shape, w)
+    p = eng.predict(users, items).cpu().numpy()
+    ref, _ = O.forward(shape, w, users, items)
+    _close(p, ref, 2e-6, "probs")
+
+
+@pytest.mark.parametrize("dims", SHAPES, ids=[str(s[2]) + "g" + str(s[3]) for s in SHAPES])
+@pytest.mark.parametrize("force_generic", [False, True])
+def test_forward_backward_grads_match_oracle(dims, force_generic):
+    shape = O.NCFShape(*dims)
+    w = _weights(shape, 3)
+    users, items, y = _batch(shape, 256, 4, 4, dup_items=min(shape.num_items, 7))  # heavy duplicate rows
+    eng = _engine(shape, w, force_generic=force_generic)
+    grads = eng.alloc_grads()
+    eng.forward_backward(users, items, y, group=4, k=2, inv_batch=1.0 / 256, grads=grads)
+    l2 = [0.0] * len(shape.layers)
+    loss, g, _ = O.loss_and_grads(shape, w, users, items, y, l2)
+    got = eng.keras_weights(grads[0], grads[1])
+    for name in O.weight_names(shape):
+        scale = np.max(np.abs(g[name])) + 1e-12
+        _close(got[name], g[name], 1e-5 * scale + 1e-9, name)
+    summ = grads[2].cpu().numpy()
+    bce = O.bce_per_sample(O.forward(shape, w, users, items)[0], y).sum()
+    assert summ[0] == pytest.approx(bce, rel=1e-5)
+    hr, dcg = O.group_metrics(O.forward(shape, w, users, items)[0], y, 4, 2)
+    assert summ[1] / summ[3] == pytest.approx(hr, abs=1e-6)
+    assert summ[2] / summ[3] == pytest.approx(dcg, abs=1e-6)
+
+
+@pytest.mark.parametrize("dims", SHAPES, ids=[str(s[2]) + "g" + str(s[3]) for s in SHAPES])
+@pytest.mark.parametrize("opt,l2", [("adam", 0.0), ("adam", 0.01), ("sgd", 0.01)])
+def test_train_steps_match_oracle(dims, opt, l2):
+    shape = O.NCFShape(*dims)
+    w = _weights(shape, 5)
+    l2s = [l2] * len(shape.layers)
+    lr = 0.001 if opt == "adam" else 0.05
+    eng = _engine(shape, w, optimizer=opt, lr=lr, layers_l2reg=l2s)
+    ref = {k: v.copy() for k, v in w.items()}
+    st = O.new_opt_state(ref)
+    hyper = dict(optimizer=opt, lr=lr, beta_1=0.9, beta_2=0.999, layers_l2reg=l2s)
+    steps = 3
+    losses = []
+    for s in range(steps):
+        users, items, y = _batch(shape, 120, 6, 10 + s, dup_items=min(shape.num_items, 9) if s == 1 else None)
+        eng.train_step(users, items, y, group=6, k=3)
+        loss, _ = O.train_step(shape, ref, st, users, items, y, hyper)
+        losses.append(loss)
+    got = eng.keras_weights()
+    for name in O.weight_names(shape):
+        _close(got[name], ref[name], steps * 2e-6 + 2e-6 * np.max(np.abs(ref[name])), name)
+    stats = NCFEngine.read_stats(eng.stats)
+    assert stats["steps"] == steps
+    assert stats["loss"] == pytest.approx(np.mean(losses), rel=2e-5)
+    assert int(eng.step.item()) == (steps if True else 0)
+
+
+def test_apply_update_equals_train_step():
+    shape = O.NCFShape(200, 150, [128, 64, 32, 16], 64)
+    w = _weights(shape, 7)
+    a = _engine(shape, w)
+    b = _engine(shape, w)
+    users, items, y = _batch(shape, 512, 4, 8)
+    a.train_step(users, items, y, group=4, k=2)
+    grads = b.alloc_grads()
+    b.forward_backward(users, items, y, group=4, k=2, inv_batch=1.0 / 512, grads=grads)
+    b.apply_update(grads, inv_batch=1.0 / 512)
+    assert torch.equal(a.emb, b.emb) and torch.equal(a.mlp, b.mlp)
+    assert torch.equal(a.emb_m, b.emb_m) and torch.equal(a.emb_v, b.emb_v)
+
+
+def test_rank_and_metrics_kats():
+    """test/test_model.py:94-190 known answers, on the device."""
+    shape = O.NCFShape(5, 10, [6, 4], 0)
+    eng = _engine(shape, _weights(shape, 0))
+    dev = eng.device
+    p = torch.tensor([0.9, 0.8, 0.7, 0.7, 0.8, 0.9], device=dev)
+    np.testing.assert_equal(eng.rank(p, 3).cpu().numpy(), [[0, 1, 2], [2, 1, 0]])
+    p = torch.tensor([0.9, 0.8, 0.7, 0.6, 0.5, 0.9, 0.9, 0.9], device=dev)
+    np.testing.assert_equal(eng.rank(p, 4).cpu().numpy(), [[0, 1, 2, 3], [1, 2, 3, 0]])
+    y = np.array([0, 0, 0, 1, 0, 0, 0, 1], np.float32)
+    p = torch.tensor([0.1, 0.2, 0.9, 0.5, 0.9, 0.8, 0.7, 0.6], device=dev)
+    for k, exp_hr in {0: 0.0, 1: 0.0, 2: 0.5, 3: 0.5, 4: 1.0}.items():
+        hit, dcg = eng.group_metrics(p, y, 4, k)
+        assert hit.mean().item() == pytest.approx(exp_hr)
+        ref = O.discounted_cumulative_gain(y.reshape(2, 4), k, O.rank_layer(p.cpu().numpy(), 4))
+        assert dcg.mean().item() == pytest.approx(ref, rel=1e-6)
+    p = torch.tensor([0.9, 0.55, 0.55, 0.55], device=dev)   # ties: positive ranked last
+    for k in (0, 1, 2, 3):
+        hit, dcg = eng.group_metrics(p, y[:4], 4, k)
+        assert hit.item() == 0.0 and dcg.item() == 0.0
+    hit, _ = eng.group_metrics(p, y[:4], 4, 4)
+    assert hit.item() == 1.0
+
+
+def test_rank_random_matches_oracle():
+    shape = O.NCFShape(5, 10, [6, 4], 0)
+    eng = _engine(shape, _weights(shape, 0))
+    rng = np.random.RandomState(0)
+    p = np.round(rng.rand(100 * 37), 2).astype(np.float32)  # many ties
+    got = eng.rank(torch.from_numpy(p).to(eng.device), 100).cpu().numpy()
+    np.testing.assert_array_equal(got, O.rank_layer(p, 100))
+
+
+def test_evaluate_matches_oracle():
+    shape = O.NCFShape(120, 90, [64, 32, 16, 8], 8)
+    w = _weights(shape, 9)
+    l2s = [0.01, 0.02, 0.0, 0.01]
+    eng = _engine(shape, w, layers_l2reg=l2s)
+    users, items, y = _batch(shape, 400, 100, 3)
+    eng.evaluate(users, items, y, group=100, k=10)
+    p, _ = O.forward(shape, w, users, items)
+    loss = O.bce_per_sample(p, y).mean() + O.reg_loss(shape, w, l2s)
+    hr, dcg = O.group_metrics(p, y, 100, 10)
+    st = NCFEngine.read_stats(eng.val_stats)
+    assert st["loss"] == pytest.approx(loss, rel=1e-5)
+    assert st["hr"] == pytest.approx(hr, abs=1e-7)
+    assert st["dcg"] == pytest.approx(dcg, abs=1e-6)
+
+
+def test_deterministic_bitwise():
+    shape = O.NCFShape(1000, 300, [128, 64, 32, 16], 64)
+    w = _weights(shape, 11)
+    runs = []
+    for _ in range(2):
+        eng = _engine(shape, w)
+        for s in range(3):
+            users, items, y = _batch(shape, 4096, 4, 20 + s, dup_items=50)
+            eng.train_step(users, items, y, group=4, k=2)
+        runs.append((eng.emb.clone(), eng.mlp.clone()))
+    assert torch.equal(runs[0][0], runs[1][0]) and torch.equal(runs[0][1], runs[1][1])
+
+
+def test_invalid_params_raise():
+    with pytest.raises(ValueError):
+        NCFEngine(10, 10, [], 0)
+    shape = O.NCFShape(10, 10, [6, 4], 0)
+    eng = _engine(shape, _weights(shape, 0))
+    u, i, y = _batch(shape, 12, 4, 0)
+    with pytest.raises(ValueError):
+        eng.train_step(u, i, y, group=5, k=2)  # batch not divisible by group
