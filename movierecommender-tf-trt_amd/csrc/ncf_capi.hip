@@ -5,6 +5,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "movierec_ncf.h"
 #include "ncf_internal.h"
@@ -58,6 +59,23 @@ int check_hyper(const ncf_hyper_t* h) {
         return fail(NCF_EINVAL, "Optimizer %d is not implemented.", h->optimizer);
     if (h->group <= 0) return fail(NCF_EINVAL, "group must be > 0");
     return 0;
+}
+
+struct Profiler {
+    int kernel = -1;
+    std::vector<hipEvent_t> start, stop;
+    size_t used = 0;
+};
+thread_local Profiler g_prof;
+
+void prof_begin(int k, hipStream_t st) {
+    if (g_prof.kernel != k || g_prof.used >= g_prof.start.size()) return;
+    hipEventRecord(g_prof.start[g_prof.used], st);
+}
+void prof_end(int k, hipStream_t st) {
+    if (g_prof.kernel != k || g_prof.used >= g_prof.start.size()) return;
+    hipEventRecord(g_prof.stop[g_prof.used], st);
+    ++g_prof.used;
 }
 
 bool use_fused(const ncf_shape_t& s, const ncf_hyper_t* h) {
@@ -210,23 +228,29 @@ int ncf_group_metrics(const float* probs, const float* labels, int64_t n_groups,
 static int run_fb(const ncf_shape_t& s, const ncf::WsLayout& L, const ncf_model_t* model, const ncf_hyper_t* h,
                   const int32_t* users, const int32_t* items, const float* labels, int64_t n, void* ws,
                   float* summary, float* probs_out, int* nslab, hipStream_t st) {
+    prof_begin(NCF_K_INDEX, st);
     hipError_t e = ncf::launch_index_build(s, L, ws, users, items, n, st);
+    prof_end(NCF_K_INDEX, st);
     if (e != hipSuccess) return hip_check(e, "index build");
     int nbce = 0;
+    prof_begin(NCF_K_FWD_BWD, st);
     if (use_fused(s, h))
         e = ncf::launch_fb_fused(s, L, ws, model->emb, model->mlp, users, items, labels, n, h->inv_batch, nslab,
                                  &nbce, st);
     else
         e = ncf::launch_fb_generic(s, L, ws, model->emb, model->mlp, users, items, labels, n, h->inv_batch, nslab,
                                    &nbce, st);
+    prof_end(NCF_K_FWD_BWD, st);
     if (e != hipSuccess) return hip_check(e, "forward/backward");
     float* probs = ncf::at<float>(ws, L.probs);
     const int64_t ng = n / h->group;
     int nmet = 0;
+    prof_begin(NCF_K_METRICS, st);
     e = ncf::launch_group_metrics(probs, labels, ng, h->group, h->k, nullptr, nullptr, ncf::at<float>(ws, L.part_hit),
                                   ncf::at<float>(ws, L.part_dcg), &nmet, st);
     if (e != hipSuccess) return hip_check(e, "metrics");
     e = ncf::launch_summary(L, ws, nbce, nmet, (float)ng, summary, st);
+    prof_end(NCF_K_METRICS, st);
     if (e != hipSuccess) return hip_check(e, "summary");
     if (probs_out) {
         e = hipMemcpyAsync(probs_out, probs, (size_t)n * 4, hipMemcpyDeviceToDevice, st);
@@ -260,12 +284,16 @@ int ncf_train_step(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* optim,
     float* summary = ncf::at<float>(ws, L.summary);
     int nslab = 0;
     if (int r = run_fb(*s, L, model, h, users, items, labels, n, ws, summary, probs_out, &nslab, st)) return r;
+    prof_begin(NCF_K_EMB_UPDATE, st);
     hipError_t e = ncf::launch_emb_update(*s, L, ws, model->emb, optim->emb_m, optim->emb_v, optim->step, *h,
                                           nullptr, st);
+    prof_end(NCF_K_EMB_UPDATE, st);
     if (e != hipSuccess) return hip_check(e, "embedding update");
     int nreg_mlp = 0;
+    prof_begin(NCF_K_MLP_UPDATE, st);
     e = ncf::launch_mlp_update(*s, L, ws, model->mlp, optim->mlp_m, optim->mlp_v, optim->step, *h, nslab, nullptr,
                                nullptr, true, &nreg_mlp, st);
+    prof_end(NCF_K_MLP_UPDATE, st);
     if (e != hipSuccess) return hip_check(e, "dense update");
     const int nreg_emb = h->l2[0] != 0.0f ? ncf::kUpdateGrid : 0;
     e = ncf::launch_stats(L, ws, summary, nreg_emb, nreg_mlp, h->inv_batch, stats, optim->step, true, st);
@@ -340,16 +368,54 @@ int ncf_apply_update(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* opti
     ncf::WsLayout L;
     if (int r = check_ws(*s, 1, ws, ws_bytes, &L)) return r;
     hipStream_t st = (hipStream_t)stream;
+    prof_begin(NCF_K_EMB_UPDATE, st);
     hipError_t e = ncf::launch_emb_update(*s, L, ws, model->emb, optim->emb_m, optim->emb_v, optim->step, *h,
                                           emb_grad, st);
+    prof_end(NCF_K_EMB_UPDATE, st);
     if (e != hipSuccess) return hip_check(e, "embedding update");
     int nreg_mlp = 0;
+    prof_begin(NCF_K_MLP_UPDATE, st);
     e = ncf::launch_mlp_update(*s, L, ws, model->mlp, optim->mlp_m, optim->mlp_v, optim->step, *h, 0, mlp_grad,
                                nullptr, true, &nreg_mlp, st);
+    prof_end(NCF_K_MLP_UPDATE, st);
     if (e != hipSuccess) return hip_check(e, "dense update");
     const int nreg_emb = h->l2[0] != 0.0f ? ncf::kUpdateGrid : 0;
     e = ncf::launch_stats(L, ws, summary, nreg_emb, nreg_mlp, h->inv_batch, stats, optim->step, true, st);
     return hip_check(e, "stats");
+}
+
+int ncf_profile_enable(int32_t kernel_id, int32_t capacity) {
+    g_prof.kernel = kernel_id;
+    g_prof.used = 0;
+    if (kernel_id < 0) return 0;
+    if (capacity < 1) return fail(NCF_EINVAL, "capacity must be >= 1");
+    while ((int)g_prof.start.size() < capacity) {
+        hipEvent_t a, b;
+        if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess)
+            return fail(NCF_EHIP, "hipEventCreate failed");
+        g_prof.start.push_back(a);
+        g_prof.stop.push_back(b);
+    }
+    return 0;
+}
+
+int ncf_profile_read(double* total_ms, int64_t* launches) {
+    if (!total_ms || !launches) return fail(NCF_EINVAL, "NULL argument");
+    double tot = 0.0;
+    if (g_prof.used > 0) {
+        hipError_t e = hipEventSynchronize(g_prof.stop[g_prof.used - 1]);
+        if (e != hipSuccess) return hip_check(e, "hipEventSynchronize");
+    }
+    for (size_t i = 0; i < g_prof.used; ++i) {
+        float ms = 0.f;
+        hipError_t e = hipEventElapsedTime(&ms, g_prof.start[i], g_prof.stop[i]);
+        if (e != hipSuccess) return hip_check(e, "hipEventElapsedTime");
+        tot += ms;
+    }
+    *total_ms = tot;
+    *launches = (int64_t)g_prof.used;
+    g_prof.used = 0;
+    return 0;
 }
 
 }  // extern "C"

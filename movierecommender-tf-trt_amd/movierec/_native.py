@@ -72,8 +72,11 @@ _SIGNATURES = {
                                             _vp, _vp, _vp, ctypes.c_size_t, _vp]),
     "ncf_apply_update": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _vp, _vp, _vp, _vp,
                                         _vp, ctypes.c_size_t, _vp]),
+    "ncf_profile_enable": (ctypes.c_int, [_i32, _i32]),
+    "ncf_profile_read": (ctypes.c_int, [_P(ctypes.c_double), _P(_i64)]),
 }
 EXPORTED = sorted(_SIGNATURES)
+K_INDEX, K_FWD_BWD, K_EMB_UPDATE, K_MLP_UPDATE, K_METRICS = 1, 2, 3, 4, 5
 
 _lib = None
 

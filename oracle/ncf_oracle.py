@@ -139,11 +139,19 @@ def forward(shape, w, users, items):
     return p.astype(dt), cache
 
 
+def clip_bounds(eps=KERAS_EPSILON):
+    """The clip range as TF builds it in the model's float32 dtype:
+    ``eps_ = cast(K.epsilon(), float32)``, ``1 - eps_`` evaluated in float32."""
+    lo = np.float32(eps)
+    return float(lo), float(np.float32(1.0) - lo)
+
+
 def bce_per_sample(p, y, eps=KERAS_EPSILON):
     """Keras binary_crossentropy (TF 1.x backend): clip → logit → sigmoid xent."""
     p = np.asarray(p, dtype=np.float64)
     y = np.asarray(y, dtype=np.float64)
-    pc = np.clip(p, eps, 1.0 - eps)
+    lo, hi = clip_bounds(eps)
+    pc = np.clip(p, lo, hi)
     logit = np.log(pc / (1.0 - pc))
     return np.maximum(logit, 0) - logit * y + np.log1p(np.exp(-np.abs(logit)))
 
@@ -167,10 +175,7 @@ def loss_and_grads(shape, w, users, items, labels, layers_l2reg, batch_norm=None
     y = np.asarray(labels, dtype=np.float64).reshape(-1)
     B = p.shape[0]
     nb = float(B if batch_norm is None else batch_norm)
-    eps = KERAS_EPSILON
-    # fp32 clip bounds as TF computes them in the model's float dtype
-    lo = np.float32(eps)
-    hi = np.float32(1.0) - np.float32(eps)
+    lo, hi = clip_bounds()
     mask = (c["p"] >= lo) & (c["p"] <= hi)
     bce = bce_per_sample(c["p"], y)
     loss = float(np.sum(bce) / nb) + reg_loss(shape, w, layers_l2reg)

@@ -43,6 +43,14 @@ def _weights(shape, seed, scale=4.0):
             w[k] = w[k] * scale
             if k.endswith("bias"):
                 w[k] = rng.uniform(-0.1, 0.1, size=w[k].shape)
+    # keep logits well inside the BCE clip range (|z| <~ 6): near the clip
+    # boundary fp32 vs fp64 rounding may legitimately flip the clip mask
+    users = rng.randint(0, shape.num_users, 512)
+    items = rng.randint(0, shape.num_items, 512)
+    _, c = O.forward(shape, w, users, items)
+    f = 6.0 / max(np.max(np.abs(c["z"])), 1e-6)
+    w["output/kernel"] = w["output/kernel"] * f
+    w["output/bias"] = w["output/bias"] * f
     # round to fp32 so both sides start from identical values
     return {k: v.astype(np.float32).astype(np.float64) for k, v in w.items()}
 
@@ -128,6 +136,21 @@ def test_train_steps_match_oracle(dims, opt, l2):
     assert stats["steps"] == steps
     assert stats["loss"] == pytest.approx(np.mean(losses), rel=2e-5)
     assert int(eng.step.item()) == (steps if True else 0)
+
+
+def test_clipped_samples_have_zero_gradient():
+    """Keras BCE clips p to [eps, 1-eps]; TF's clip_by_value gradient is zero
+    outside the range, so saturated samples contribute no gradient."""
+    shape = O.NCFShape(40, 30, [8, 4], 4)
+    w = _weights(shape, 2)
+    w["output/bias"] = np.array([40.0])   # sigmoid saturates to 1 for every sample
+    eng = _engine(shape, w)
+    users, items, y = _batch(shape, 64, 4, 1)
+    grads = eng.alloc_grads()
+    eng.forward_backward(users, items, y, group=4, k=2, inv_batch=1.0 / 64, grads=grads)
+    assert float(grads[0].abs().max()) == 0.0 and float(grads[1].abs().max()) == 0.0
+    p, _ = O.forward(shape, w, users, items)
+    assert grads[2][0].item() == pytest.approx(O.bce_per_sample(p, y).sum(), rel=1e-5)
 
 
 def test_apply_update_equals_train_step():
