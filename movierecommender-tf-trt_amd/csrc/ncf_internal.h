@@ -41,6 +41,7 @@ struct WsLayout {
     size_t summary;   // float[NCF_NUM_SUMMARY]
     size_t slabs;     // float[kMaxSlabs * P]
     size_t mlp_grad;  // float[P] (reduced dense-layer gradient, single-device path)
+    size_t wt;        // float[P] transposed hidden kernels (fused path)
     size_t act;       // float[B * A] generic kernel activations
     size_t dz;        // float[B * D] generic kernel pre-activation gradients
     size_t total;
