@@ -123,7 +123,7 @@ WsLayout make_layout(const ncf_shape_t& s, int64_t B) {
     L.summary = take(NCF_NUM_SUMMARY * 4);
     L.slabs = take((size_t)kMaxSlabs * s.mlp_params * 4);
     L.mlp_grad = take((size_t)s.mlp_params * 4);
-    L.wt = take((size_t)s.mlp_params * 4);
+    L.slab_part = take((size_t)kSlabSplit * s.mlp_params * 4);
     L.act = take((size_t)B * A * 4);
     L.dz = take((size_t)B * D * 4);
     L.total = off;

@@ -57,19 +57,30 @@ struct FShape {
     // flat dense-parameter offsets (include/movierec_ncf.h layout)
     static constexpr int OW1 = 0, OB1 = L0 * L1, OW2 = OB1 + L1, OB2 = OW2 + L1 * L2, OW3 = OB2 + L2,
                          OB3 = OW3 + L2 * L3, OWO = OB3 + L3, OBO = OWO + G + L3, P = OBO + 1;
-    // transposed kernels [out][in]
-    static constexpr int T1 = 0, T2 = L0 * L1, T3 = T2 + L1 * L2, TP = T3 + L2 * L3;
-    // LDS staging rows per 32-sample block
+    // LDS copy of the dense parameters: kernels row-major [in][out] with rows padded to out+1
+    // floats, so the forward A operand (W[k][out], consecutive out) and the backward A operand
+    // (W[in][k], consecutive in: stride out+1, odd) are both bank-conflict-free ds_read_b32
+    static constexpr int LW1 = L1 + 1, LW2 = L2 + 1, LW3 = L3 + 1;
+    static constexpr int SW1 = 0, SW2 = SW1 + L0 * LW1, SW3 = SW2 + L1 * LW2, SB1 = SW3 + L2 * LW3,
+                         SB2 = SB1 + L1, SB3 = SB2 + L2, SWO = SB3 + L3, SBO = SWO + G + L3,
+                         WLDS = (SBO + 1 + 3) / 4 * 4;
+    // LDS staging rows per 32-sample block (G3 only has L3 real rows)
     static constexpr int RH1 = 0, RH2 = RH1 + 32 * NT1, RG1 = RH2 + 32 * NT2, RG2 = RG1 + 32 * NT1,
-                         RG3 = RG2 + 32 * NT2, RB = RG3 + 32 * NT3;
+                         RG3 = RG2 + 32 * NT2, RB = RG3 + L3;
     static constexpr int LS = 33;
+    // MFMA steps of a chain whose K runs over the (NT-tile, 16-register) rows of an
+    // activation with L real features: full tiles take 16 steps, a partial last tile
+    // only the steps whose rows (8 per 4 steps) reach below L
+    static constexpr int nsteps(int L) { return 16 * (cdiv(L, 32) - 1) + (4 * cdiv(L - 32 * (cdiv(L, 32) - 1), 8) < 16 ? 4 * cdiv(L - 32 * (cdiv(L, 32) - 1), 8) : 16); }
+    static constexpr int NS1 = nsteps(L1), NS2 = nsteps(L2), NS3 = nsteps(L3);
     static constexpr int NDW1 = NT0 * NT1, NDW2 = NT1 * NT2, NDW3 = NT2 * NT3, NDW = NDW1 + NDW2 + NDW3;
     static constexpr int MAXT = cdiv(NDW, 4);
     static constexpr int GH = G / 2;                     // GMF features per lane half
     static constexpr int GCH = GH >= 16 ? 16 : GH;       // reduction chunk (bounds register pressure)
     static constexpr int NGC = GH >= 16 ? GH / 16 : (GH > 0 ? 1 : 0);
     static constexpr int XCH = G + L3 + 2;               // per-wave exchange floats
-    static constexpr size_t LDS_BYTES = (size_t)(4 * RB * LS) * 4 + 256 * 4 + (size_t)4 * XCH * 4;
+    static constexpr size_t LDS_BYTES = (size_t)(4 * RB * LS + WLDS) * 4 + 256 * 4 + (size_t)4 * XCH * 4;
+    static_assert(LDS_BYTES <= 163840, "LDS budget");
 };
 
 // Sum x[0..V) over the 32 lanes of each wave half (V a power of two <= 32).
@@ -95,25 +106,57 @@ __device__ __forceinline__ float half_transpose_reduce(float* x, int lane) {
     return r;
 }
 
-// W_l^T for the backward chains (A operand rows must be contiguous in `in`).
-__global__ __launch_bounds__(kBlock) void k_transpose_kernels(const float* __restrict__ mlp, float* __restrict__ wt,
-                                                              int l0, int l1, int l2, int l3) {
-    const int dims[4] = {l0, l1, l2, l3};
-    int src = 0, dst = 0;
-    for (int l = 1; l <= 3; ++l) {
-        const int lin = dims[l - 1], lout = dims[l];
-        for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < lin * lout; e += gridDim.x * blockDim.x) {
-            const int i = e / lout, o = e - i * lout;
-            wt[dst + o * lin + i] = mlp[src + e];
+// acc += sum_t A(t) x B(t) over NS MFMA steps.  A(t) (an LDS/global read) is
+// double-buffered CH steps ahead; B(t) is a register (activation tile element).
+template <int NS, int CH, class FA, class FB>
+__device__ __forceinline__ f32x16 mchain(f32x16 acc, FA fa, FB fb) {
+    static_assert(NS % CH == 0, "chain length must be a multiple of the chunk");
+    float ab[2][CH];
+#pragma unroll
+    for (int e = 0; e < CH; ++e) ab[0][e] = fa(e);
+#pragma unroll
+    for (int c = 0; c < NS / CH; ++c) {
+        if (c + 1 < NS / CH) {
+#pragma unroll
+            for (int e = 0; e < CH; ++e) ab[(c + 1) & 1][e] = fa((c + 1) * CH + e);
         }
-        src += lin * lout + lout;
-        dst += lin * lout;
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int e = 0; e < CH; ++e) acc = mfma32(ab[c & 1][e], fb(c * CH + e), acc);
+        __builtin_amdgcn_sched_barrier(0);
     }
+    return acc;
+}
+
+// Same with both operands read from memory and double-buffered.
+template <int NS, int CH, class FA, class FB>
+__device__ __forceinline__ f32x16 mchain2(f32x16 acc, FA fa, FB fb) {
+    static_assert(NS % CH == 0, "chain length must be a multiple of the chunk");
+    float ab[2][CH], bb[2][CH];
+#pragma unroll
+    for (int e = 0; e < CH; ++e) {
+        ab[0][e] = fa(e);
+        bb[0][e] = fb(e);
+    }
+#pragma unroll
+    for (int c = 0; c < NS / CH; ++c) {
+        if (c + 1 < NS / CH) {
+#pragma unroll
+            for (int e = 0; e < CH; ++e) {
+                ab[(c + 1) & 1][e] = fa((c + 1) * CH + e);
+                bb[(c + 1) & 1][e] = fb((c + 1) * CH + e);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int e = 0; e < CH; ++e) acc = mfma32(ab[c & 1][e], bb[c & 1][e], acc);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    return acc;
 }
 
 template <class S>
-__global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict__ emb, const float* __restrict__ mlp_in,
-                                                        const float* __restrict__ wt_in,
+__global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict__ emb, const float* __restrict__ mlp,
                                                         const int32_t* __restrict__ users,
                                                         const int32_t* __restrict__ items,
                                                         const float* __restrict__ labels, int64_t n, int U, int I,
@@ -122,8 +165,9 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
                                                         float* __restrict__ part_bce) {
     constexpr int L0 = S::L0, L1 = S::L1, L2 = S::L2, L3 = S::L3, G = S::G, D0 = S::D0, W = S::W, LS = S::LS;
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    float* stg = lds;                                     // [4][RB][LS]
-    int* srow = reinterpret_cast<int*>(lds + 4 * S::RB * LS);  // [2][128] table rows (-1 = masked)
+    float* wl = lds;                                      // dense parameters (WLDS floats)
+    float* stg = lds + S::WLDS;                           // [4][RB][LS]
+    int* srow = reinterpret_cast<int*>(stg + 4 * S::RB * LS);  // [2][128] table rows (-1 = masked)
     float* xch = reinterpret_cast<float*>(srow + 256);    // [4][XCH]
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, j = lane & 31, h = lane >> 5;
@@ -139,24 +183,30 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
 #pragma unroll
     for (int c = 0; c < (S::NGC > 0 ? S::NGC : 1); ++c) acc_gmf[c] = 0.f;
 
+    // dense parameters → LDS (once per persistent workgroup)
+    for (int e = tid; e < L0 * L1; e += kBlock) wl[S::SW1 + (e / L1) * S::LW1 + e % L1] = mlp[S::OW1 + e];
+    for (int e = tid; e < L1 * L2; e += kBlock) wl[S::SW2 + (e / L2) * S::LW2 + e % L2] = mlp[S::OW2 + e];
+    for (int e = tid; e < L2 * L3; e += kBlock) wl[S::SW3 + (e / L3) * S::LW3 + e % L3] = mlp[S::OW3 + e];
+    for (int e = tid; e < L1; e += kBlock) wl[S::SB1 + e] = mlp[S::OB1 + e];
+    for (int e = tid; e < L2; e += kBlock) wl[S::SB2 + e] = mlp[S::OB2 + e];
+    for (int e = tid; e < L3; e += kBlock) wl[S::SB3 + e] = mlp[S::OB3 + e];
+    for (int e = tid; e < G + L3 + 1; e += kBlock) wl[S::SWO + e] = mlp[S::OWO + e];
+    __syncthreads();
+
     const int64_t niter = (n + 127) / 128;
     for (int64_t it = blockIdx.x; it < niter; it += gridDim.x) {
-        // Opaque per-iteration copies of the weight pointers: without them LICM hoists every
-        // (loop-invariant) weight load out of the tile loop and the kernel spills.
-        const float* mlp = mlp_in;
-        const float* wt = wt_in;
-        asm volatile("" : "+s"(mlp), "+s"(wt));
-
         const int64_t si = it * 128 + 32 * w + j;
-        bool ok = false;
-        int urow = 0, irow = 0;
+        const bool inb = si < n;
+        int u = 0, v = 0;
         float y = 0.f;
-        if (si < n) {
-            const int u = users[si], v = items[si];
-            ok = (unsigned)u < (unsigned)U && (unsigned)v < (unsigned)I;
-            if (ok) { urow = u; irow = U + v; }
+        if (inb) {
+            u = users[si];
+            v = items[si];
             y = labels[si];
         }
+        // Masked samples read row 0 (a valid address) and get dz = 0: they contribute nothing.
+        const bool ok = inb && (unsigned)u < (unsigned)U && (unsigned)v < (unsigned)I;
+        const int urow = ok ? u : 0, irow = ok ? U + v : 0;
         if (h == 0) {
             srow[32 * w + j] = ok ? urow : -1;
             srow[128 + 32 * w + j] = ok ? irow : -1;
@@ -165,48 +215,67 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
         const float* ei = emb + (size_t)irow * W;
         float* sb = stg + w * S::RB * LS;  // this wave's staging block
 
-        // ---- GMF forward partial over this half's features
+        // ---- bulk gather: this half's MLP vector and both GMF slices, all loads in flight at once
+        float4 xv[D0 / 4];
+        {
+            const float4* src = reinterpret_cast<const float4*>((h ? ei : eu) + G);
+#pragma unroll
+            for (int q = 0; q < D0 / 4; ++q) xv[q] = src[q];
+        }
         float zp = 0.f;
+        const float4* us = reinterpret_cast<const float4*>(eu + h * S::GH);
+        const float4* is = reinterpret_cast<const float4*>(ei + h * S::GH);
         if constexpr (G > 0) {
-            const float4* ug = reinterpret_cast<const float4*>(eu + h * S::GH);
-            const float4* ig = reinterpret_cast<const float4*>(ei + h * S::GH);
-            const float* wo = mlp + S::OWO + h * S::GH;
-#pragma unroll 2
+            float4 ua[S::GH / 4], ia[S::GH / 4];
+#pragma unroll
             for (int q = 0; q < S::GH / 4; ++q) {
-                if (ok) {
-                    const float4 a = ug[q], b = ig[q];
-                    zp += wo[4 * q] * (a.x * b.x) + wo[4 * q + 1] * (a.y * b.y) + wo[4 * q + 2] * (a.z * b.z) +
-                          wo[4 * q + 3] * (a.w * b.w);
-                }
+                ua[q] = us[q];
+                ia[q] = is[q];
             }
+            const float* wo = wl + S::SWO + h * S::GH;
+#pragma unroll
+            for (int q = 0; q < S::GH / 4; ++q)
+                zp += wo[4 * q] * (ua[q].x * ia[q].x) + wo[4 * q + 1] * (ua[q].y * ia[q].y) +
+                      wo[4 * q + 2] * (ua[q].z * ia[q].z) + wo[4 * q + 3] * (ua[q].w * ia[q].w);
         }
 
-        // ---- forward chain.  Layer 1: the lane half h supplies its sample's user (h=0) or
-        // item (h=1) MLP vector as the B operand, K order h*D0 + s; the row is streamed in
-        // float4 chunks straight from the gathered embedding row.  Each activation tile is
-        // staged to LDS for the weight-gradient phase as soon as it exists, and only its
-        // ReLU mask (one bit per register) is kept for the backward chain.
+        // ---- forward chain.  Layer 1: B operand = this half's MLP vector (K order h*D0 + s),
+        // A operand = W1[k][out] from LDS, double-buffered 4 steps ahead.  Each activation tile
+        // is staged to LDS for the weight-gradient phase as soon as it exists; only its ReLU
+        // mask (one bit per register) is kept for the backward chain.
         uint32_t m1[S::NT1], m2[S::NT2];
         f32x16 h1[S::NT1];
         {
             f32x16 acc[S::NT1];
 #pragma unroll
             for (int to = 0; to < S::NT1; ++to) acc[to] = f32x16{};
-            const float4* xsrc = reinterpret_cast<const float4*>((h ? ei : eu) + G);
-#pragma unroll 2
-            for (int q = 0; q < D0 / 4; ++q) {
-                const float4 xv = ok ? xsrc[q] : make_float4(0.f, 0.f, 0.f, 0.f);
-                const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+            float ab[2][4][S::NT1];
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int k = h * D0 + 4 * q + e;
+            for (int e = 0; e < 4; ++e)
 #pragma unroll
-                    for (int to = 0; to < S::NT1; ++to) {
-                        const int oc = 32 * to + j;
-                        const float a = (oc < L1) ? mlp[S::OW1 + k * L1 + oc] : 0.f;
-                        acc[to] = mfma32(a, xs[e], acc[to]);
-                    }
+                for (int to = 0; to < S::NT1; ++to) {
+                    const int oc = 32 * to + j;
+                    ab[0][e][to] = oc < L1 ? wl[S::SW1 + (h * D0 + e) * S::LW1 + oc] : 0.f;
                 }
+#pragma unroll
+            for (int c = 0; c < D0 / 4; ++c) {
+                if (c + 1 < D0 / 4) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+#pragma unroll
+                        for (int to = 0; to < S::NT1; ++to) {
+                            const int oc = 32 * to + j;
+                            ab[(c + 1) & 1][e][to] =
+                                oc < L1 ? wl[S::SW1 + (h * D0 + 4 * (c + 1) + e) * S::LW1 + oc] : 0.f;
+                        }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                const float xs[4] = {xv[c].x, xv[c].y, xv[c].z, xv[c].w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+#pragma unroll
+                    for (int to = 0; to < S::NT1; ++to) acc[to] = mfma32(ab[c & 1][e][to], xs[e], acc[to]);
+                __builtin_amdgcn_sched_barrier(0);
             }
 #pragma unroll
             for (int to = 0; to < S::NT1; ++to) {
@@ -214,53 +283,58 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const int f = 32 * to + drow(r, h);
-                    const float v = (f < L1) ? fmaxf(acc[to][r] + mlp[S::OB1 + f], 0.f) : 0.f;
-                    h1[to][r] = v;
-                    m1[to] |= (v > 0.f ? 1u : 0u) << r;
-                    sb[(S::RH1 + f) * LS + j] = v;
+                    const float val = (f < L1) ? fmaxf(acc[to][r] + wl[S::SB1 + f], 0.f) : 0.f;
+                    h1[to][r] = val;
+                    m1[to] |= (val > 0.f ? 1u : 0u) << r;
+                    sb[(S::RH1 + f) * LS + j] = val;
                 }
+            }
+        }
+        // GMF slices again for the backward (L2-resident by now; in flight during layers 2-3)
+        float4 ua[S::GH / 4 > 0 ? S::GH / 4 : 1], ia[S::GH / 4 > 0 ? S::GH / 4 : 1];
+        if constexpr (G > 0) {
+#pragma unroll
+            for (int q = 0; q < S::GH / 4; ++q) {
+                ua[q] = us[q];
+                ia[q] = is[q];
             }
         }
         f32x16 h2[S::NT2];
 #pragma unroll
         for (int to = 0; to < S::NT2; ++to) {
-            f32x16 acc = {};
             const int oc = 32 * to + j;
-#pragma unroll
-            for (int ti = 0; ti < S::NT1; ++ti)
-#pragma unroll
-                for (int s = 0; s < 16; ++s) {
-                    const int k = 32 * ti + drow(s, h);
-                    const float a = (oc < L2 && k < L1) ? mlp[S::OW2 + k * L2 + oc] : 0.f;
-                    acc = mfma32(a, h1[ti][s], acc);
-                }
+            const f32x16 acc = mchain<S::NS1, 4>(
+                f32x16{},
+                [&](int t) {
+                    const int k = 32 * (t / 16) + drow(t % 16, h);
+                    return (oc < L2 && k < L1) ? wl[S::SW2 + k * S::LW2 + oc] : 0.f;
+                },
+                [&](int t) { return h1[t / 16][t % 16]; });
             m2[to] = 0u;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int f = 32 * to + drow(r, h);
-                const float v = (f < L2) ? fmaxf(acc[r] + mlp[S::OB2 + f], 0.f) : 0.f;
-                h2[to][r] = v;
-                m2[to] |= (v > 0.f ? 1u : 0u) << r;
-                sb[(S::RH2 + f) * LS + j] = v;
+                const float val = (f < L2) ? fmaxf(acc[r] + wl[S::SB2 + f], 0.f) : 0.f;
+                h2[to][r] = val;
+                m2[to] |= (val > 0.f ? 1u : 0u) << r;
+                sb[(S::RH2 + f) * LS + j] = val;
             }
         }
         f32x16 h3[S::NT3];
 #pragma unroll
         for (int to = 0; to < S::NT3; ++to) {
-            f32x16 acc = {};
             const int oc = 32 * to + j;
-#pragma unroll
-            for (int ti = 0; ti < S::NT2; ++ti)
-#pragma unroll
-                for (int s = 0; s < 16; ++s) {
-                    const int k = 32 * ti + drow(s, h);
-                    const float a = (oc < L3 && k < L2) ? mlp[S::OW3 + k * L3 + oc] : 0.f;
-                    acc = mfma32(a, h2[ti][s], acc);
-                }
+            const f32x16 acc = mchain<S::NS2, 4>(
+                f32x16{},
+                [&](int t) {
+                    const int k = 32 * (t / 16) + drow(t % 16, h);
+                    return (oc < L3 && k < L2) ? wl[S::SW3 + k * S::LW3 + oc] : 0.f;
+                },
+                [&](int t) { return h2[t / 16][t % 16]; });
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int f = 32 * to + drow(r, h);
-                h3[to][r] = (f < L3) ? fmaxf(acc[r] + mlp[S::OB3 + f], 0.f) : 0.f;
+                h3[to][r] = (f < L3) ? fmaxf(acc[r] + wl[S::SB3 + f], 0.f) : 0.f;
             }
         }
         // ---- output, BCE, dz (both halves compute the same sample's values)
@@ -269,9 +343,9 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int f = 32 * t + drow(r, h);
-                if (f < L3) zp += mlp[S::OWO + G + f] * h3[t][r];
+                if (f < L3) zp += wl[S::SWO + G + f] * h3[t][r];
             }
-        const float z = (zp + __shfl_xor(zp, 32, 64)) + mlp[S::OBO];
+        const float z = (zp + __shfl_xor(zp, 32, 64)) + wl[S::SBO];
         const float p = 1.0f / (1.0f + expf(-z));
         float dz = 0.f, bce = 0.f;
         if (ok) {
@@ -281,7 +355,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
             dz = (p >= eps && p <= hi_clip) ? (p - y) * inv_batch : 0.0f;
         }
         if (h == 0) {
-            if (si < n) probs[si] = ok ? p : __int_as_float(0x7fc00000);
+            if (inb) probs[si] = ok ? p : __int_as_float(0x7fc00000);
             acc_bce += bce;
             acc_dbo += dz;
         }
@@ -290,21 +364,14 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
 
         // ---- GMF backward: embedding grads + output-kernel grads (transpose-reduced)
         if constexpr (G > 0) {
-            const float* ug = eu + h * S::GH;
-            const float* ig = ei + h * S::GH;
-            const float* wo = mlp + S::OWO + h * S::GH;
+            const float* wo = wl + S::SWO + h * S::GH;
 #pragma unroll
             for (int c = 0; c < S::NGC; ++c) {
-                __builtin_amdgcn_sched_barrier(0);
                 float contrib[S::GCH];
 #pragma unroll
                 for (int q = 0; q < S::GCH / 4; ++q) {
                     const int f = c * S::GCH + 4 * q;
-                    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
-                    if (ok) {
-                        a = *reinterpret_cast<const float4*>(ug + f);
-                        b = *reinterpret_cast<const float4*>(ig + f);
-                    }
+                    const float4 a = ua[f / 4], b = ia[f / 4];
                     contrib[4 * q] = dz * (a.x * b.x);
                     contrib[4 * q + 1] = dz * (a.y * b.y);
                     contrib[4 * q + 2] = dz * (a.z * b.z);
@@ -330,28 +397,25 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
             for (int r = 0; r < 16; ++r) {
                 const int f = 32 * t + drow(r, h);
                 contrib[r] = dz * h3[t][r];
-                const float g = (f < L3 && h3[t][r] > 0.f) ? dz * mlp[S::OWO + G + f] : 0.f;
+                const float g = (f < L3 && h3[t][r] > 0.f) ? dz * wl[S::SWO + G + f] : 0.f;
                 g3[t][r] = g;
-                sb[(S::RG3 + f) * LS + j] = g;
+                if (f < L3) sb[(S::RG3 + f) * LS + j] = g;
             }
             const float red = half_transpose_reduce<16>(contrib, lane);
             if (t == 0) acc_h3 += red;  // NT3 == 1 for the supported shapes
         }
-        // ---- backward data chain
+        // ---- backward data chain (A = W_l[in][out] read along `in`: row stride out+1)
         f32x16 g2[S::NT2];
 #pragma unroll
         for (int to = 0; to < S::NT2; ++to) {
-            f32x16 acc = {};
             const int oc = 32 * to + j;
-#pragma unroll
-            for (int ti = 0; ti < S::NT3; ++ti)
-#pragma unroll
-                for (int s = 0; s < 16; ++s) {
-                    if (32 * ti + 8 * (s >> 2) >= L3) continue;  // whole step beyond L3 (both halves)
-                    const int k = 32 * ti + drow(s, h);
-                    const float a = (oc < L2 && k < L3) ? wt[S::T3 + k * L2 + oc] : 0.f;
-                    acc = mfma32(a, g3[ti][s], acc);
-                }
+            const f32x16 acc = mchain<S::NS3, 4>(
+                f32x16{},
+                [&](int t) {
+                    const int k = 32 * (t / 16) + drow(t % 16, h);
+                    return (oc < L2 && k < L3) ? wl[S::SW3 + oc * S::LW3 + k] : 0.f;
+                },
+                [&](int t) { return g3[t / 16][t % 16]; });
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const float g = ((m2[to] >> r) & 1u) ? acc[r] : 0.f;
@@ -362,17 +426,14 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
         f32x16 g1[S::NT1];
 #pragma unroll
         for (int to = 0; to < S::NT1; ++to) {
-            f32x16 acc = {};
             const int oc = 32 * to + j;
-#pragma unroll
-            for (int ti = 0; ti < S::NT2; ++ti)
-#pragma unroll
-                for (int s = 0; s < 16; ++s) {
-                    if (32 * ti + 8 * (s >> 2) >= L2) continue;
-                    const int k = 32 * ti + drow(s, h);
-                    const float a = (oc < L1 && k < L2) ? wt[S::T2 + k * L1 + oc] : 0.f;
-                    acc = mfma32(a, g2[ti][s], acc);
-                }
+            const f32x16 acc = mchain<S::NS2, 4>(
+                f32x16{},
+                [&](int t) {
+                    const int k = 32 * (t / 16) + drow(t % 16, h);
+                    return (oc < L1 && k < L2) ? wl[S::SW2 + oc * S::LW2 + k] : 0.f;
+                },
+                [&](int t) { return g2[t / 16][t % 16]; });
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const float g = ((m1[to] >> r) & 1u) ? acc[r] : 0.f;
@@ -382,17 +443,14 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
         }
 #pragma unroll
         for (int to = 0; to < S::NT0; ++to) {
-            f32x16 acc = {};
             const int oc = 32 * to + j;
-#pragma unroll
-            for (int ti = 0; ti < S::NT1; ++ti)
-#pragma unroll
-                for (int s = 0; s < 16; ++s) {
-                    if (32 * ti + 8 * (s >> 2) >= L1) continue;
-                    const int k = 32 * ti + drow(s, h);
-                    const float a = (oc < L0 && k < L1) ? wt[S::T1 + k * L0 + oc] : 0.f;
-                    acc = mfma32(a, g1[ti][s], acc);
-                }
+            const f32x16 acc = mchain<S::NS1, 4>(
+                f32x16{},
+                [&](int t) {
+                    const int k = 32 * (t / 16) + drow(t % 16, h);
+                    return (oc < L0 && k < L1) ? wl[S::SW1 + oc * S::LW1 + k] : 0.f;
+                },
+                [&](int t) { return g1[t / 16][t % 16]; });
             if (ok) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
@@ -407,7 +465,8 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
         }
         __syncthreads();
 
-        // ---- weight gradients: wave w owns tiles w, w+4, w+8, ... (K = 128 samples)
+        // ---- weight gradients: wave w owns tiles w, w+4, w+8, ... (K = 128 samples,
+        // 64 MFMA steps per tile; both operands double-buffered one chunk ahead)
 #pragma unroll
         for (int m = 0; m < S::MAXT; ++m) {
             const int t = w + 4 * m;
@@ -418,31 +477,29 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
             else { layer = 3; ti = (t - S::NDW1 - S::NDW2) / S::NT3; to = (t - S::NDW1 - S::NDW2) % S::NT3; }
             const int fi = 32 * ti + j;  // A row (input feature) supplied by this lane
             const int fo = 32 * to + j;  // B column (output feature) supplied by this lane
-            const int arow = layer == 2 ? S::RH1 + fi : S::RH2 + fi;
+            const int lout = layer == 1 ? L1 : layer == 2 ? L2 : L3;
             const int brow = (layer == 1 ? S::RG1 : layer == 2 ? S::RG2 : S::RG3) + fo;
-            const int lin = layer == 1 ? L0 : layer == 2 ? L1 : L2;
-            f32x16 acc = dwacc[m];
-            for (int b = 0; b < 4; ++b) {
-                const float* bb = stg + b * S::RB * LS;
-                if (layer == 1) {
-                    const int side = fi < D0 ? 0 : 128;
-                    const int col = G + (fi < D0 ? fi : fi - D0);
-#pragma unroll 4
-                    for (int s = 0; s < 16; ++s) {
-                        const int c = 2 * s + h;
-                        const int row = srow[side + 32 * b + c];
-                        const float a = (row >= 0 && fi < lin) ? emb[(size_t)row * W + col] : 0.f;
-                        acc = mfma32(a, bb[brow * LS + c], acc);
-                    }
-                } else {
-#pragma unroll 4
-                    for (int s = 0; s < 16; ++s) {
-                        const int c = 2 * s + h;
-                        acc = mfma32(bb[arow * LS + c], bb[brow * LS + c], acc);
-                    }
-                }
+            const bool bok = fo < lout;
+            // B(t): G_l[fo][sample] of block t/16, column 2(t%16)+h
+            auto fb = [&](int tt) {
+                return bok ? stg[(tt >> 4) * S::RB * LS + brow * LS + 2 * (tt & 15) + h] : 0.f;
+            };
+            if (layer == 1) {
+                const int side = fi < D0 ? 0 : 128;
+                const int col = G + (fi < D0 ? fi : fi - D0);
+                const bool aok = fi < L0;
+                dwacc[m] = mchain2<64, 8>(dwacc[m],
+                                           [&](int tt) {
+                                               const int row = srow[side + 32 * (tt >> 4) + 2 * (tt & 15) + h];
+                                               return (aok && row >= 0) ? emb[(size_t)row * W + col] : 0.f;
+                                           },
+                                           fb);
+            } else {
+                const int arow = (layer == 2 ? S::RH1 : S::RH2) + fi;
+                dwacc[m] = mchain2<64, 8>(
+                    dwacc[m], [&](int tt) { return stg[(tt >> 4) * S::RB * LS + arow * LS + 2 * (tt & 15) + h]; },
+                    fb);
             }
-            dwacc[m] = acc;
         }
         // ---- bias gradients: one G row per thread, summed over the 128 samples
         if (tid < L1 + L2 + L3) {
@@ -459,7 +516,6 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
     }
 
     // ---- epilogue: this workgroup's dense-gradient slab and BCE partial
-    const float* mlp = mlp_in;
     float* slab = slabs + (size_t)blockIdx.x * S::P;
 #pragma unroll
     for (int m = 0; m < S::MAXT; ++m) {
@@ -546,12 +602,10 @@ static hipError_t launch_one(const ncf_shape_t& s, const WsLayout& L, void* ws, 
         if (e != hipSuccess) return e;
         configured = true;
     }
-    float* wt = at<float>(ws, L.wt);
-    k_transpose_kernels<<<16, kBlock, 0, st>>>(mlp, wt, S::L0, S::L1, S::L2, S::L3);
     const int64_t niter = (n + 127) / 128;
     int grid = (int)(niter < 256 ? niter : 256);
     if (grid > kMaxSlabs) grid = kMaxSlabs;
-    k_fb_fused<S><<<grid, kBlock, S::LDS_BYTES, st>>>(emb, mlp, wt, users, items, labels, n, s.num_users,
+    k_fb_fused<S><<<grid, kBlock, S::LDS_BYTES, st>>>(emb, mlp, users, items, labels, n, s.num_users,
                                                       s.num_items, inv_batch, at<float>(ws, L.probs),
                                                       at<float>(ws, L.gs), at<float>(ws, L.slabs),
                                                       at<float>(ws, L.part_bce));

@@ -13,6 +13,7 @@ constexpr int kBlock = 256;            // threads per workgroup for the streamin
 constexpr int kScanBlock = 2048;       // keys per block of the offset scan (8 per thread)
 constexpr int kSmallSeg = 16;          // segments up to this length are sorted in registers
 constexpr int kMaxSlabs = 1024;        // partial dense-gradient slabs (one per producing block)
+constexpr int kSlabSplit = 16;         // first-level slab reduction fan-in groups
 constexpr int kUpdateGrid = 2048;      // grid of the embedding-table sweep (fixed: deterministic partials)
 constexpr int64_t kMaxBatch = 524288;  // heavy-segment bitmap must fit the LDS (2*B bits)
 
@@ -41,7 +42,7 @@ struct WsLayout {
     size_t summary;   // float[NCF_NUM_SUMMARY]
     size_t slabs;     // float[kMaxSlabs * P]
     size_t mlp_grad;  // float[P] (reduced dense-layer gradient, single-device path)
-    size_t wt;        // float[P] transposed hidden kernels (fused path)
+    size_t slab_part; // float[kSlabSplit * P] first-level slab sums
     size_t act;       // float[B * A] generic kernel activations
     size_t dz;        // float[B * D] generic kernel pre-activation gradients
     size_t total;

@@ -108,6 +108,25 @@ __global__ __launch_bounds__(kBlock) void k_emb_grad_dense(float4* __restrict__ 
     }
 }
 
+// First level of the slab reduction: group c sums slabs [c*per, (c+1)*per) in order.
+__global__ __launch_bounds__(kBlock) void k_slab_partial(const float* __restrict__ slabs, int P, int nslab, int per,
+                                                         float* __restrict__ part) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P) return;
+    const int s0 = blockIdx.y * per;
+    const int s1 = min(nslab, s0 + per);
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int s = s0;
+    for (; s + 4 <= s1; s += 4) {
+        a0 += slabs[(size_t)(s + 0) * P + p];
+        a1 += slabs[(size_t)(s + 1) * P + p];
+        a2 += slabs[(size_t)(s + 2) * P + p];
+        a3 += slabs[(size_t)(s + 3) * P + p];
+    }
+    for (; s < s1; ++s) a0 += slabs[(size_t)s * P + p];
+    part[(size_t)blockIdx.y * P + p] = (a0 + a1) + (a2 + a3);
+}
+
 struct L2Table {
     int n;
     int start[NCF_MAX_LAYERS];
@@ -336,12 +355,21 @@ hipError_t launch_mlp_update(const ncf_shape_t& s, const WsLayout& L, void* ws, 
     const int grid = (P + kBlock - 1) / kBlock;
     float* part = at<float>(ws, L.part_reg) + kUpdateGrid;
     const L2Table t = make_l2_table(s, h);
+    const float* slabs = at<float>(ws, L.slabs);
+    if (nslab > 2 * kSlabSplit) {
+        const int per = (nslab + kSlabSplit - 1) / kSlabSplit;
+        const int nch = (nslab + per - 1) / per;
+        float* sp = at<float>(ws, L.slab_part);
+        k_slab_partial<<<dim3(grid, nch), kBlock, 0, st>>>(slabs, P, nslab, per, sp);
+        slabs = sp;
+        nslab = nch;
+    }
     if (h.optimizer == NCF_OPT_ADAM)
-        k_mlp_update<NCF_OPT_ADAM><<<grid, kBlock, 0, st>>>(mlp, m, v, P, at<float>(ws, L.slabs), nslab, grad_in,
+        k_mlp_update<NCF_OPT_ADAM><<<grid, kBlock, 0, st>>>(mlp, m, v, P, slabs, nslab, grad_in,
                                                             grad_out, do_update ? 1 : 0, want_reg ? 1 : 0, step,
                                                             h.lr, h.beta_1, h.beta_2, h.epsilon, t, part);
     else
-        k_mlp_update<NCF_OPT_SGD><<<grid, kBlock, 0, st>>>(mlp, m, v, P, at<float>(ws, L.slabs), nslab, grad_in,
+        k_mlp_update<NCF_OPT_SGD><<<grid, kBlock, 0, st>>>(mlp, m, v, P, slabs, nslab, grad_in,
                                                            grad_out, do_update ? 1 : 0, want_reg ? 1 : 0, step,
                                                            h.lr, h.beta_1, h.beta_2, h.epsilon, t, part);
     *nreg = ((do_update || want_reg) && t.n > 0) ? grid : 0;
