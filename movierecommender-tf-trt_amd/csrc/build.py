@@ -28,16 +28,18 @@ def _deps_mtime():
     return max(os.path.getmtime(f) for f in files)
 
 
-def build(force=False, verbose=False):
-    os.makedirs(OUT_DIR, exist_ok=True)
-    if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= _deps_mtime():
-        return LIB
-    obj_dir = os.path.join(OUT_DIR, "obj")
+def build(force=False, verbose=False, defines=(), out=None):
+    """Compile and link; ``defines``/``out`` build an experiment variant elsewhere."""
+    lib_path = out or LIB
+    os.makedirs(os.path.dirname(lib_path), exist_ok=True)
+    if not force and os.path.exists(lib_path) and os.path.getmtime(lib_path) >= _deps_mtime():
+        return lib_path
+    obj_dir = os.path.join(os.path.dirname(lib_path), "obj" + ("_" + os.path.basename(lib_path) if out else ""))
     os.makedirs(obj_dir, exist_ok=True)
 
     def compile_one(src):
         obj = os.path.join(obj_dir, src.replace(".hip", ".o"))
-        cmd = [HIPCC] + CFLAGS + ["-c", os.path.join(HERE, src), "-o", obj]
+        cmd = [HIPCC] + CFLAGS + ["-D" + d for d in defines] + ["-c", os.path.join(HERE, src), "-o", obj]
         if verbose:
             print(" ".join(cmd))
         r = subprocess.run(cmd, capture_output=True, text=True)
@@ -47,14 +49,20 @@ def build(force=False, verbose=False):
 
     with cf.ThreadPoolExecutor(max_workers=min(8, len(SOURCES))) as ex:
         objs = list(ex.map(compile_one, SOURCES))
-    tmp = LIB + ".tmp"
+    tmp = lib_path + ".tmp"
     cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-o", tmp] + objs
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError("link failed:\n%s\n%s" % (r.stdout, r.stderr))
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, lib_path)
+    return lib_path
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-D", dest="defines", action="append", default=[])
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    print(build(force=a.force, verbose=True, defines=a.defines, out=a.out))

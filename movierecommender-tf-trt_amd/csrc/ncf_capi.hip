@@ -3,7 +3,10 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -78,6 +81,56 @@ void prof_end(int k, hipStream_t st) {
     ++g_prof.used;
 }
 
+// Side stream (one per device, created on first use): the dense-layer tail (loss summary,
+// slab reduction, dense Adam) runs on it concurrently with the embedding sweep.  The fork/join
+// events make the pair capturable into one hipGraph.  NCF_SIDE_STREAM=0 disables it.
+struct SideStream {
+    hipStream_t s = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+};
+
+SideStream* side_stream() {
+    static const bool enabled = [] {
+        const char* e = getenv("NCF_SIDE_STREAM");
+        return !(e && atoi(e) == 0);
+    }();
+    if (!enabled) return nullptr;
+    static std::mutex mu;
+    static std::map<int, SideStream> streams;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lock(mu);
+    SideStream& ss = streams[dev];
+    if (!ss.s) {
+        if (hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&ss.join, hipEventDisableTiming) != hipSuccess) {
+            ss.s = nullptr;
+            return nullptr;
+        }
+    }
+    return &ss;
+}
+
+// fork: the side stream waits for everything enqueued on `st` so far; returns the stream to use
+hipStream_t fork_side(hipStream_t st, SideStream** out) {
+    SideStream* ss = side_stream();
+    *out = ss;
+    if (!ss) return st;
+    if (hipEventRecord(ss->fork, st) != hipSuccess || hipStreamWaitEvent(ss->s, ss->fork, 0) != hipSuccess) {
+        *out = nullptr;
+        return st;
+    }
+    return ss->s;
+}
+
+hipError_t join_side(hipStream_t st, SideStream* ss) {
+    if (!ss) return hipSuccess;
+    hipError_t e = hipEventRecord(ss->join, ss->s);
+    if (e != hipSuccess) return e;
+    return hipStreamWaitEvent(st, ss->join, 0);
+}
+
 bool use_fused(const ncf_shape_t& s, const ncf_hyper_t* h) {
     return s.fast_path && !(h && h->force_generic) && ncf::fused_supported(s);
 }
@@ -113,6 +166,7 @@ WsLayout make_layout(const ncf_shape_t& s, int64_t B) {
     L.probs = take((size_t)B * 4);
     L.gs = take((size_t)2 * B * s.row_width * 4);
     L.list = take((size_t)2 * B * 4);
+    L.offs_local = take((size_t)(R + 1) * 4);
     L.offs = take((size_t)(R + 1) * 4);
     L.tot = take((size_t)L.nscan * 4);
     L.heavy = take((size_t)2 * B * 4);
@@ -225,34 +279,38 @@ int ncf_group_metrics(const float* probs, const float* labels, int64_t n_groups,
                      "ncf_group_metrics");
 }
 
-// forward + backward + index + metrics summary: shared by train_step and forward_backward
+struct FbOut {
+    int nslab = 0, nbce = 0, nmet = 0;
+    float n_groups = 0.f;
+};
+
+// index build + forward/backward (+ group metrics): shared by train_step and forward_backward
 static int run_fb(const ncf_shape_t& s, const ncf::WsLayout& L, const ncf_model_t* model, const ncf_hyper_t* h,
                   const int32_t* users, const int32_t* items, const float* labels, int64_t n, void* ws,
-                  float* summary, float* probs_out, int* nslab, hipStream_t st) {
+                  float* probs_out, FbOut* out, hipStream_t st) {
     prof_begin(NCF_K_INDEX, st);
     hipError_t e = ncf::launch_index_build(s, L, ws, users, items, n, st);
     prof_end(NCF_K_INDEX, st);
     if (e != hipSuccess) return hip_check(e, "index build");
-    int nbce = 0;
     prof_begin(NCF_K_FWD_BWD, st);
     if (use_fused(s, h))
-        e = ncf::launch_fb_fused(s, L, ws, model->emb, model->mlp, users, items, labels, n, h->inv_batch, nslab,
-                                 &nbce, st);
+        e = ncf::launch_fb_fused(s, L, ws, model->emb, model->mlp, users, items, labels, n, h->inv_batch, h->group,
+                                 h->k, &out->nslab, &out->nbce, &out->nmet, st);
     else
-        e = ncf::launch_fb_generic(s, L, ws, model->emb, model->mlp, users, items, labels, n, h->inv_batch, nslab,
-                                   &nbce, st);
+        e = ncf::launch_fb_generic(s, L, ws, model->emb, model->mlp, users, items, labels, n, h->inv_batch,
+                                   &out->nslab, &out->nbce, st);
     prof_end(NCF_K_FWD_BWD, st);
     if (e != hipSuccess) return hip_check(e, "forward/backward");
     float* probs = ncf::at<float>(ws, L.probs);
     const int64_t ng = n / h->group;
-    int nmet = 0;
-    prof_begin(NCF_K_METRICS, st);
-    e = ncf::launch_group_metrics(probs, labels, ng, h->group, h->k, nullptr, nullptr, ncf::at<float>(ws, L.part_hit),
-                                  ncf::at<float>(ws, L.part_dcg), &nmet, st);
-    if (e != hipSuccess) return hip_check(e, "metrics");
-    e = ncf::launch_summary(L, ws, nbce, nmet, (float)ng, summary, st);
-    prof_end(NCF_K_METRICS, st);
-    if (e != hipSuccess) return hip_check(e, "summary");
+    out->n_groups = (float)ng;
+    if (out->nmet == 0) {
+        prof_begin(NCF_K_METRICS, st);
+        e = ncf::launch_group_metrics(probs, labels, ng, h->group, h->k, nullptr, nullptr,
+                                      ncf::at<float>(ws, L.part_hit), ncf::at<float>(ws, L.part_dcg), &out->nmet, st);
+        prof_end(NCF_K_METRICS, st);
+        if (e != hipSuccess) return hip_check(e, "metrics");
+    }
     if (probs_out) {
         e = hipMemcpyAsync(probs_out, probs, (size_t)n * 4, hipMemcpyDeviceToDevice, st);
         if (e != hipSuccess) return hip_check(e, "probs copy");
@@ -283,19 +341,25 @@ int ncf_train_step(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* optim,
     if (int r = check_ws(*s, n, ws, ws_bytes, &L)) return r;
     hipStream_t st = (hipStream_t)stream;
     float* summary = ncf::at<float>(ws, L.summary);
-    int nslab = 0;
-    if (int r = run_fb(*s, L, model, h, users, items, labels, n, ws, summary, probs_out, &nslab, st)) return r;
+    FbOut fb;
+    if (int r = run_fb(*s, L, model, h, users, items, labels, n, ws, probs_out, &fb, st)) return r;
+    // dense-layer tail on the side stream, embedding sweep on the main stream
+    SideStream* ss = nullptr;
+    hipStream_t st2 = fork_side(st, &ss);
+    hipError_t e = ncf::launch_summary(L, ws, fb.nbce, fb.nmet, fb.n_groups, summary, st2);
+    if (e != hipSuccess) return hip_check(e, "summary");
+    int nreg_mlp = 0;
+    prof_begin(NCF_K_MLP_UPDATE, st2);
+    e = ncf::launch_mlp_update(*s, L, ws, model->mlp, optim->mlp_m, optim->mlp_v, optim->step, *h, fb.nslab, nullptr,
+                               nullptr, true, &nreg_mlp, st2);
+    prof_end(NCF_K_MLP_UPDATE, st2);
+    if (e != hipSuccess) return hip_check(e, "dense update");
     prof_begin(NCF_K_EMB_UPDATE, st);
-    hipError_t e = ncf::launch_emb_update(*s, L, ws, model->emb, optim->emb_m, optim->emb_v, optim->step, *h,
-                                          nullptr, st);
+    e = ncf::launch_emb_update(*s, L, ws, model->emb, optim->emb_m, optim->emb_v, optim->step, *h, nullptr, st);
     prof_end(NCF_K_EMB_UPDATE, st);
     if (e != hipSuccess) return hip_check(e, "embedding update");
-    int nreg_mlp = 0;
-    prof_begin(NCF_K_MLP_UPDATE, st);
-    e = ncf::launch_mlp_update(*s, L, ws, model->mlp, optim->mlp_m, optim->mlp_v, optim->step, *h, nslab, nullptr,
-                               nullptr, true, &nreg_mlp, st);
-    prof_end(NCF_K_MLP_UPDATE, st);
-    if (e != hipSuccess) return hip_check(e, "dense update");
+    e = join_side(st, ss);
+    if (e != hipSuccess) return hip_check(e, "side-stream join");
     const int nreg_emb = h->l2[0] != 0.0f ? ncf::kUpdateGrid : 0;
     e = ncf::launch_stats(L, ws, summary, nreg_emb, nreg_mlp, h->inv_batch, stats, optim->step, true, st);
     return hip_check(e, "stats");
@@ -309,14 +373,19 @@ int ncf_forward_backward(const ncf_shape_t* s, const ncf_model_t* model, const n
     ncf::WsLayout L;
     if (int r = check_ws(*s, n, ws, ws_bytes, &L)) return r;
     hipStream_t st = (hipStream_t)stream;
-    int nslab = 0;
-    if (int r = run_fb(*s, L, model, h, users, items, labels, n, ws, summary, probs_out, &nslab, st)) return r;
-    hipError_t e = ncf::launch_emb_grad_dense(*s, L, ws, emb_grad, st);
-    if (e != hipSuccess) return hip_check(e, "dense embedding gradient");
+    FbOut fb;
+    if (int r = run_fb(*s, L, model, h, users, items, labels, n, ws, probs_out, &fb, st)) return r;
+    SideStream* ss = nullptr;
+    hipStream_t st2 = fork_side(st, &ss);
+    hipError_t e = ncf::launch_summary(L, ws, fb.nbce, fb.nmet, fb.n_groups, summary, st2);
+    if (e != hipSuccess) return hip_check(e, "summary");
     int nreg = 0;
-    e = ncf::launch_mlp_update(*s, L, ws, nullptr, nullptr, nullptr, nullptr, *h, nslab, nullptr, mlp_grad, false,
-                               &nreg, st);
-    return hip_check(e, "dense-layer gradient");
+    e = ncf::launch_mlp_update(*s, L, ws, nullptr, nullptr, nullptr, nullptr, *h, fb.nslab, nullptr, mlp_grad, false,
+                               &nreg, st2);
+    if (e != hipSuccess) return hip_check(e, "dense-layer gradient");
+    e = ncf::launch_emb_grad_dense(*s, L, ws, emb_grad, st);
+    if (e != hipSuccess) return hip_check(e, "dense embedding gradient");
+    return hip_check(join_side(st, ss), "side-stream join");
 }
 
 int ncf_evaluate(const ncf_shape_t* s, const ncf_model_t* model, const ncf_hyper_t* h, const int32_t* users,
@@ -369,17 +438,20 @@ int ncf_apply_update(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* opti
     ncf::WsLayout L;
     if (int r = check_ws(*s, 1, ws, ws_bytes, &L)) return r;
     hipStream_t st = (hipStream_t)stream;
+    SideStream* ss = nullptr;
+    hipStream_t st2 = fork_side(st, &ss);
+    int nreg_mlp = 0;
+    prof_begin(NCF_K_MLP_UPDATE, st2);
+    hipError_t e = ncf::launch_mlp_update(*s, L, ws, model->mlp, optim->mlp_m, optim->mlp_v, optim->step, *h, 0,
+                                          mlp_grad, nullptr, true, &nreg_mlp, st2);
+    prof_end(NCF_K_MLP_UPDATE, st2);
+    if (e != hipSuccess) return hip_check(e, "dense update");
     prof_begin(NCF_K_EMB_UPDATE, st);
-    hipError_t e = ncf::launch_emb_update(*s, L, ws, model->emb, optim->emb_m, optim->emb_v, optim->step, *h,
-                                          emb_grad, st);
+    e = ncf::launch_emb_update(*s, L, ws, model->emb, optim->emb_m, optim->emb_v, optim->step, *h, emb_grad, st);
     prof_end(NCF_K_EMB_UPDATE, st);
     if (e != hipSuccess) return hip_check(e, "embedding update");
-    int nreg_mlp = 0;
-    prof_begin(NCF_K_MLP_UPDATE, st);
-    e = ncf::launch_mlp_update(*s, L, ws, model->mlp, optim->mlp_m, optim->mlp_v, optim->step, *h, 0, mlp_grad,
-                               nullptr, true, &nreg_mlp, st);
-    prof_end(NCF_K_MLP_UPDATE, st);
-    if (e != hipSuccess) return hip_check(e, "dense update");
+    e = join_side(st, ss);
+    if (e != hipSuccess) return hip_check(e, "side-stream join");
     const int nreg_emb = h->l2[0] != 0.0f ? ncf::kUpdateGrid : 0;
     e = ncf::launch_stats(L, ws, summary, nreg_emb, nreg_mlp, h->inv_batch, stats, optim->step, true, st);
     return hip_check(e, "stats");

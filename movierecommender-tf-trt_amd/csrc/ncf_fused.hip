@@ -78,7 +78,7 @@ struct FShape {
     static constexpr int GH = G / 2;                     // GMF features per lane half
     static constexpr int GCH = GH >= 16 ? 16 : GH;       // reduction chunk (bounds register pressure)
     static constexpr int NGC = GH >= 16 ? GH / 16 : (GH > 0 ? 1 : 0);
-    static constexpr int XCH = G + L3 + 2;               // per-wave exchange floats
+    static constexpr int XCH = G + L3 + 4;               // per-wave exchange floats
     static constexpr size_t LDS_BYTES = (size_t)(4 * RB * LS + WLDS) * 4 + 256 * 4 + (size_t)4 * XCH * 4;
     static_assert(LDS_BYTES <= 163840, "LDS budget");
 };
@@ -106,6 +106,18 @@ __device__ __forceinline__ float half_transpose_reduce(float* x, int lane) {
     return r;
 }
 
+#ifndef NCF_DW1_CH
+#define NCF_DW1_CH 8
+#endif
+#ifndef NCF_SCHED_BARRIER
+#define NCF_SCHED_BARRIER 1
+#endif
+#if NCF_SCHED_BARRIER
+#define NCF_SB() __builtin_amdgcn_sched_barrier(0)
+#else
+#define NCF_SB() ((void)0)
+#endif
+
 // acc += sum_t A(t) x B(t) over NS MFMA steps.  A(t) (an LDS/global read) is
 // double-buffered CH steps ahead; B(t) is a register (activation tile element).
 template <int NS, int CH, class FA, class FB>
@@ -120,10 +132,10 @@ __device__ __forceinline__ f32x16 mchain(f32x16 acc, FA fa, FB fb) {
 #pragma unroll
             for (int e = 0; e < CH; ++e) ab[(c + 1) & 1][e] = fa((c + 1) * CH + e);
         }
-        __builtin_amdgcn_sched_barrier(0);
+        NCF_SB();
 #pragma unroll
         for (int e = 0; e < CH; ++e) acc = mfma32(ab[c & 1][e], fb(c * CH + e), acc);
-        __builtin_amdgcn_sched_barrier(0);
+        NCF_SB();
     }
     return acc;
 }
@@ -147,10 +159,10 @@ __device__ __forceinline__ f32x16 mchain2(f32x16 acc, FA fa, FB fb) {
                 bb[(c + 1) & 1][e] = fb((c + 1) * CH + e);
             }
         }
-        __builtin_amdgcn_sched_barrier(0);
+        NCF_SB();
 #pragma unroll
         for (int e = 0; e < CH; ++e) acc = mfma32(ab[c & 1][e], bb[c & 1][e], acc);
-        __builtin_amdgcn_sched_barrier(0);
+        NCF_SB();
     }
     return acc;
 }
@@ -162,7 +174,8 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
                                                         const float* __restrict__ labels, int64_t n, int U, int I,
                                                         float inv_batch, float* __restrict__ probs,
                                                         float* __restrict__ gs, float* __restrict__ slabs,
-                                                        float* __restrict__ part_bce) {
+                                                        float* __restrict__ part_bce, int group, int topk,
+                                                        float* __restrict__ part_hit, float* __restrict__ part_dcg) {
     constexpr int L0 = S::L0, L1 = S::L1, L2 = S::L2, L3 = S::L3, G = S::G, D0 = S::D0, W = S::W, LS = S::LS;
     extern __shared__ __attribute__((aligned(16))) float lds[];
     float* wl = lds;                                      // dense parameters (WLDS floats)
@@ -178,7 +191,8 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
     for (int m = 0; m < S::MAXT; ++m)
 #pragma unroll
         for (int r = 0; r < 16; ++r) dwacc[m][r] = 0.f;
-    float acc_bias = 0.f, acc_h3 = 0.f, acc_dbo = 0.f, acc_bce = 0.f;
+    float acc_bias = 0.f, acc_h3 = 0.f, acc_dbo = 0.f, acc_bce = 0.f, acc_hit = 0.f, acc_dcg = 0.f;
+    const bool metrics = part_hit != nullptr;  // groups never straddle a 32-sample block (group | 32)
     float acc_gmf[S::NGC > 0 ? S::NGC : 1];
 #pragma unroll
     for (int c = 0; c < (S::NGC > 0 ? S::NGC : 1); ++c) acc_gmf[c] = 0.f;
@@ -269,13 +283,13 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
                                 oc < L1 ? wl[S::SW1 + (h * D0 + 4 * (c + 1) + e) * S::LW1 + oc] : 0.f;
                         }
                 }
-                __builtin_amdgcn_sched_barrier(0);
+                NCF_SB();
                 const float xs[4] = {xv[c].x, xv[c].y, xv[c].z, xv[c].w};
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
 #pragma unroll
                     for (int to = 0; to < S::NT1; ++to) acc[to] = mfma32(ab[c & 1][e][to], xs[e], acc[to]);
-                __builtin_amdgcn_sched_barrier(0);
+                NCF_SB();
             }
 #pragma unroll
             for (int to = 0; to < S::NT1; ++to) {
@@ -358,6 +372,29 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
             if (inb) probs[si] = ok ? p : __int_as_float(0x7fc00000);
             acc_bce += bce;
             acc_dbo += dz;
+        }
+        // ---- hr@k / dcg@k of the user groups in this block (RankLayer + _get_hits_per_user,
+        // model.py:344-455): label = first max of y; position = #(p > p_lab) + #(earlier ties)
+        if (metrics) {
+            const int e = j % group;
+            const int base = 32 * h + j - e;
+            int lab = 0;
+            float best = __shfl(y, base, 64);
+            for (int q = 1; q < group; ++q) {
+                const float yq = __shfl(y, base + q, 64);
+                if (yq > best) { best = yq; lab = q; }
+            }
+            const float pl = __shfl(p, base + lab, 64);
+            int pos = 0;
+            for (int q = 0; q < group; ++q) {
+                const float pq = __shfl(p, base + q, 64);
+                pos += (pq > pl) || (pq == pl && q < lab);
+            }
+            if (h == 0 && e == 0 && inb) {
+                const float hit = pos < topk ? 1.f : 0.f;
+                acc_hit += hit;
+                acc_dcg += hit * (logf(2.0f) / logf((float)pos + 2.0f));
+            }
         }
         float* gu = gs + (size_t)(2 * si) * W;  // user contribution row
         float* gi = gu + W;                     // item contribution row
@@ -488,7 +525,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
                 const int side = fi < D0 ? 0 : 128;
                 const int col = G + (fi < D0 ? fi : fi - D0);
                 const bool aok = fi < L0;
-                dwacc[m] = mchain2<64, 8>(dwacc[m],
+                dwacc[m] = mchain2<64, NCF_DW1_CH>(dwacc[m],
                                            [&](int tt) {
                                                const int row = srow[side + 32 * (tt >> 4) + 2 * (tt & 15) + h];
                                                return (aok && row >= 0) ? emb[(size_t)row * W + col] : 0.f;
@@ -553,24 +590,30 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
         const int f = drow(j >> 1, h);
         if (f < L3) xw[G + f] = acc_h3;
     }
-    float dbo = acc_dbo, bce = acc_bce;
+    float dbo = acc_dbo, bce = acc_bce, hit = acc_hit, dcg = acc_dcg;
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) {
         dbo += __shfl_xor(dbo, m, 64);
         bce += __shfl_xor(bce, m, 64);
+        hit += __shfl_xor(hit, m, 64);
+        dcg += __shfl_xor(dcg, m, 64);
     }
     if (lane == 0) {
         xw[G + L3] = dbo;
         xw[G + L3 + 1] = bce;
+        xw[G + L3 + 2] = hit;
+        xw[G + L3 + 3] = dcg;
     }
     __syncthreads();
     if (tid < G + L3 + 1) {
         const float v = (xch[tid] + xch[S::XCH + tid]) + (xch[2 * S::XCH + tid] + xch[3 * S::XCH + tid]);
         slab[S::OWO + tid] = v;  // G + L3 kernel entries, then the bias at OBO = OWO + G + L3
     }
-    if (tid == 0) {
-        const int o = G + L3 + 1;
-        part_bce[blockIdx.x] = (xch[o] + xch[S::XCH + o]) + (xch[2 * S::XCH + o] + xch[3 * S::XCH + o]);
+    if (tid < 3) {
+        const int o = G + L3 + 1 + tid;
+        const float v = (xch[o] + xch[S::XCH + o]) + (xch[2 * S::XCH + o] + xch[3 * S::XCH + o]);
+        if (tid == 0) part_bce[blockIdx.x] = v;
+        else if (metrics) (tid == 1 ? part_hit : part_dcg)[blockIdx.x] = v;
     }
 }
 
@@ -594,7 +637,8 @@ bool fused_supported(const ncf_shape_t& s) {
 template <class S>
 static hipError_t launch_one(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, const float* mlp,
                              const int32_t* users, const int32_t* items, const float* labels, int64_t n,
-                             float inv_batch, int* nslab, int* nbce, hipStream_t st) {
+                             float inv_batch, int group, int topk, int* nslab, int* nbce, int* nmet,
+                             hipStream_t st) {
     static bool configured = false;
     if (!configured) {
         hipError_t e = hipFuncSetAttribute((const void*)k_fb_fused<S>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -605,20 +649,27 @@ static hipError_t launch_one(const ncf_shape_t& s, const WsLayout& L, void* ws, 
     const int64_t niter = (n + 127) / 128;
     int grid = (int)(niter < 256 ? niter : 256);
     if (grid > kMaxSlabs) grid = kMaxSlabs;
+    const bool in_kernel = group > 0 && group <= 32 && 32 % group == 0;
     k_fb_fused<S><<<grid, kBlock, S::LDS_BYTES, st>>>(emb, mlp, users, items, labels, n, s.num_users,
                                                       s.num_items, inv_batch, at<float>(ws, L.probs),
                                                       at<float>(ws, L.gs), at<float>(ws, L.slabs),
-                                                      at<float>(ws, L.part_bce));
+                                                      at<float>(ws, L.part_bce), group, topk,
+                                                      in_kernel ? at<float>(ws, L.part_hit) : nullptr,
+                                                      in_kernel ? at<float>(ws, L.part_dcg) : nullptr);
     *nslab = grid;
     *nbce = grid;
+    *nmet = in_kernel ? grid : 0;
     return hipGetLastError();
 }
 
 hipError_t launch_fb_fused(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, const float* mlp,
                            const int32_t* users, const int32_t* items, const float* labels, int64_t n,
-                           float inv_batch, int* nslab, int* nbce, hipStream_t st) {
-#define NCF_TRY(SH) \
-    if (matches<SH>(s)) return launch_one<SH>(s, L, ws, emb, mlp, users, items, labels, n, inv_batch, nslab, nbce, st)
+                           float inv_batch, int group, int topk, int* nslab, int* nbce, int* nmet,
+                           hipStream_t st) {
+#define NCF_TRY(SH)                                                                                             \
+    if (matches<SH>(s))                                                                                         \
+    return launch_one<SH>(s, L, ws, emb, mlp, users, items, labels, n, inv_batch, group, topk, nslab, nbce, nmet, \
+                          st)
     NCF_TRY(ShapeC);
     NCF_TRY(ShapeB);
     NCF_TRY(ShapeR);

@@ -10,12 +10,11 @@
 //
 //   k_count       cnt[row]++                     (int atomics; order-free)
 //   k_scan_local  per-2048-row exclusive scan + block totals
-//   k_scan_final  add the prefix of the block totals      -> offs[row]
-//   k_fill        list[offs[row] + --cnt[row]] = c        (cnt back to 0)
-//   k_sort_small  sort each row's list (<=16) in registers; longer rows
-//                 are queued for
-//   k_sort_heavy  one workgroup per long row: LDS bitmap over c, popcount
-//                 scan, write back in ascending order.
+//   k_fill        offs[row] = local + prefix(block totals);
+//                 list[offs[row] + --cnt[row]] = c        (cnt back to 0)
+//   k_sort        sort each row's list: <=16 entries in registers (one
+//                 thread), longer rows by the whole workgroup through an
+//                 LDS bitmap over c (popcount scan, ascending write-back).
 //
 // All HBM traffic here is O(B + R) int32 (R = table rows); see DESIGN.md.
 
@@ -76,75 +75,85 @@ __global__ __launch_bounds__(kBlock) void k_scan_local(const int32_t* __restrict
     if (threadIdx.x == 0) tot[blockIdx.x] = total;
 }
 
-__global__ __launch_bounds__(kBlock) void k_scan_final(int32_t* __restrict__ offs, int64_t r1,
-                                                       const int32_t* __restrict__ tot) {
-    __shared__ int sw[4];
-    if (blockIdx.x == 0) return;
-    int part = 0;
-    for (int j = threadIdx.x; j < (int)blockIdx.x; j += blockDim.x) part += tot[j];
-    int pre;
-    block_exscan_256(part, sw, &pre);
-    const int64_t base = (int64_t)blockIdx.x * kScanBlock + threadIdx.x * 8;
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-        if (base + j < r1) offs[base + j] += pre;
+// Exclusive prefix of the scan-block totals into LDS pre[0..nscan) (every thread participates).
+__device__ inline void block_prefix_of_totals(const int32_t* __restrict__ tot, int nscan, int* pre, int* sw) {
+    int carry = 0;
+    for (int base = 0; base < nscan; base += kBlock) {
+        const int x = base + (int)threadIdx.x < nscan ? tot[base + threadIdx.x] : 0;
+        int total;
+        const int ex = block_exscan_256(x, sw, &total);
+        if (base + (int)threadIdx.x < nscan) pre[base + threadIdx.x] = carry + ex;
+        carry += total;
+    }
+    __syncthreads();
 }
 
+// Finalise the row offsets (offs_g = local scan + prefix of block totals) and scatter every
+// contribution into its row's list slot; the per-row counter runs back down to zero.
 __global__ __launch_bounds__(kBlock) void k_fill(const int32_t* __restrict__ users, const int32_t* __restrict__ items,
                                                  int64_t n, int32_t U, int32_t I, int32_t* __restrict__ cnt,
-                                                 const int32_t* __restrict__ offs, int32_t* __restrict__ list) {
+                                                 const int32_t* __restrict__ local, const int32_t* __restrict__ tot,
+                                                 int nscan, int64_t r1, int32_t* __restrict__ offs_g,
+                                                 int32_t* __restrict__ list) {
+    extern __shared__ __attribute__((aligned(16))) int pre[];
+    __shared__ int sw[4];
+    block_prefix_of_totals(tot, nscan, pre, sw);
+    const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t gstride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t r = gt; r < r1; r += gstride) offs_g[r] = local[r] + pre[r / kScanBlock];
     const int64_t m = 2 * n;
-    for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < m; c += (int64_t)gridDim.x * blockDim.x) {
+    for (int64_t c = gt; c < m; c += gstride) {
         bool ok;
         const int key = contrib_key(c, users, items, U, I, &ok);
         if (!ok) continue;
         const int slot = atomicSub(&cnt[key], 1) - 1;
-        list[offs[key] + slot] = (int)c;
+        list[local[key] + pre[key / kScanBlock] + slot] = (int)c;
     }
 }
 
-__global__ __launch_bounds__(kBlock) void k_sort_small(const int32_t* __restrict__ offs, int64_t R,
-                                                       int32_t* __restrict__ list, int32_t* __restrict__ heavy,
-                                                       int32_t* heavy_n) {
-    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < R; r += (int64_t)gridDim.x * blockDim.x) {
-        const int o = offs[r];
-        const int c = offs[r + 1] - o;
-        if (c < 2) continue;
-        if (c > kSmallSeg) {
-            heavy[atomicAdd(heavy_n, 1)] = (int)r;
-            continue;
-        }
-        int v[kSmallSeg];
-#pragma unroll
-        for (int j = 0; j < kSmallSeg; ++j) v[j] = (j < c) ? list[o + j] : INT_MAX;
-        // odd-even transposition network (static indexing keeps v[] in VGPRs)
-#pragma unroll
-        for (int round = 0; round < kSmallSeg; ++round) {
-#pragma unroll
-            for (int j = round & 1; j + 1 < kSmallSeg; j += 2) {
-                const int a = min(v[j], v[j + 1]);
-                const int b = max(v[j], v[j + 1]);
-                v[j] = a;
-                v[j + 1] = b;
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < kSmallSeg; ++j)
-            if (j < c) list[o + j] = v[j];
-    }
-}
-
-__global__ __launch_bounds__(kBlock) void k_sort_heavy(const int32_t* __restrict__ offs, int32_t* __restrict__ list,
-                                                       const int32_t* __restrict__ heavy,
-                                                       const int32_t* __restrict__ heavy_n, int nwords) {
+// Sort each row's contribution list ascending.  Rows of <= kSmallSeg entries: one thread,
+// odd-even network in registers.  Longer rows: queued in LDS and sorted by the whole
+// workgroup with a bitmap over the contribution ids (set bits, popcount scan, write back).
+__global__ __launch_bounds__(kBlock) void k_sort(const int32_t* __restrict__ offs, int64_t R,
+                                                 int32_t* __restrict__ list, int nwords) {
     extern __shared__ __attribute__((aligned(16))) unsigned bm[];
+    __shared__ int hrows[kBlock];
+    __shared__ int nh;
     __shared__ int sw[4];
-    const int nh = *heavy_n;
-    const int per = (nwords + kBlock - 1) / kBlock;
-    for (int h = blockIdx.x; h < nh; h += gridDim.x) {
-        const int r = heavy[h];
+    if (threadIdx.x == 0) nh = 0;
+    __syncthreads();
+    const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (r < R) {
         const int o = offs[r];
         const int c = offs[r + 1] - o;
+        if (c > kSmallSeg) {
+            hrows[atomicAdd(&nh, 1)] = (int)r;
+        } else if (c >= 2) {
+            int v[kSmallSeg];
+#pragma unroll
+            for (int j = 0; j < kSmallSeg; ++j) v[j] = (j < c) ? list[o + j] : INT_MAX;
+#pragma unroll
+            for (int round = 0; round < kSmallSeg; ++round) {
+#pragma unroll
+                for (int j = round & 1; j + 1 < kSmallSeg; j += 2) {
+                    const int a = min(v[j], v[j + 1]);
+                    const int b = max(v[j], v[j + 1]);
+                    v[j] = a;
+                    v[j + 1] = b;
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < kSmallSeg; ++j)
+                if (j < c) list[o + j] = v[j];
+        }
+    }
+    __syncthreads();
+    const int count = nh;
+    const int per = (nwords + kBlock - 1) / kBlock;
+    for (int hh = 0; hh < count; ++hh) {
+        const int row = hrows[hh];
+        const int o = offs[row];
+        const int c = offs[row + 1] - o;
         for (int w = threadIdx.x; w < nwords; w += kBlock) bm[w] = 0u;
         __syncthreads();
         for (int j = threadIdx.x; j < c; j += kBlock) {
@@ -184,26 +193,26 @@ hipError_t launch_index_build(const ncf_shape_t& s, const WsLayout& L, void* ws,
     int32_t* cnt = at<int32_t>(ws, L.cnt);
     int32_t* heavy_n = at<int32_t>(ws, L.heavy_n);
     int32_t* err = at<int32_t>(ws, L.err);
+    int32_t* local = at<int32_t>(ws, L.offs_local);
     int32_t* offs = at<int32_t>(ws, L.offs);
     int32_t* tot = at<int32_t>(ws, L.tot);
     int32_t* list = at<int32_t>(ws, L.list);
-    int32_t* heavy = at<int32_t>(ws, L.heavy);
-    const int gc = grid_for(2 * n, 2048);
+    const int gc = grid_for(2 * n, 1024);
     k_count<<<gc, kBlock, 0, st>>>(users, items, n, s.num_users, s.num_items, cnt, heavy_n, err);
     const int nscan = (int)((r1 + kScanBlock - 1) / kScanBlock);
-    k_scan_local<<<nscan, kBlock, 0, st>>>(cnt, r1, offs, tot);
-    k_scan_final<<<nscan, kBlock, 0, st>>>(offs, r1, tot);
-    k_fill<<<gc, kBlock, 0, st>>>(users, items, n, s.num_users, s.num_items, cnt, offs, list);
-    k_sort_small<<<grid_for(R, 4096), kBlock, 0, st>>>(offs, R, list, heavy, heavy_n);
+    k_scan_local<<<nscan, kBlock, 0, st>>>(cnt, r1, local, tot);
+    const int gf = grid_for(2 * n > r1 ? 2 * n : r1, 1024);
+    k_fill<<<gf, kBlock, (size_t)nscan * 4, st>>>(users, items, n, s.num_users, s.num_items, cnt, local, tot, nscan,
+                                                  r1, offs, list);
     const int nwords = (int)((2 * n + 31) / 32);
     static bool lds_cfg = false;
     if (!lds_cfg && (size_t)nwords * 4 > 65536) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_sort_heavy, hipFuncAttributeMaxDynamicSharedMemorySize,
+        hipError_t e = hipFuncSetAttribute((const void*)k_sort, hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)((kMaxBatch * 2 / 32) * 4));
         if (e != hipSuccess) return e;
         lds_cfg = true;
     }
-    k_sort_heavy<<<256, kBlock, (size_t)nwords * 4, st>>>(offs, list, heavy, heavy_n, nwords);
+    k_sort<<<(unsigned)((R + kBlock - 1) / kBlock), kBlock, (size_t)nwords * 4, st>>>(offs, R, list, nwords);
     return hipGetLastError();
 }
 

@@ -15,7 +15,7 @@ constexpr int kSmallSeg = 16;          // segments up to this length are sorted 
 constexpr int kMaxSlabs = 1024;        // partial dense-gradient slabs (one per producing block)
 constexpr int kSlabSplit = 16;         // first-level slab reduction fan-in groups
 constexpr int kUpdateGrid = 2048;      // grid of the embedding-table sweep (fixed: deterministic partials)
-constexpr int64_t kMaxBatch = 524288;  // heavy-segment bitmap must fit the LDS (2*B bits)
+constexpr int64_t kMaxBatch = 262144;  // heavy-segment bitmap must fit the LDS (2*B bits = 64 KB)
 
 // Scalars every kernel of a step reads (device copy of hyper + derived).
 struct StepScalars {
@@ -32,6 +32,7 @@ struct WsLayout {
     size_t probs;     // float[B]
     size_t gs;        // float[2B * W] per-contribution gradient rows
     size_t list;      // int32[2B]   contributions grouped by table row (sorted inside a row)
+    size_t offs_local;// int32[R+1]  per-2048-row local exclusive scan
     size_t offs;      // int32[R+1]  row -> first list slot
     size_t tot;       // int32[nscan]
     size_t heavy;     // int32[2B]
@@ -78,9 +79,11 @@ hipError_t launch_predict_generic(const ncf_shape_t& s, const WsLayout& L, void*
                                   const float* labels, int64_t n, float* probs, int* nbce, hipStream_t st);
 
 // fused MFMA forward+backward (shapes with s.fast_path); same outputs as the generic kernel
+// also computes the hr/dcg group metrics in-kernel when group divides 32 (*nmet = partial count, else 0)
 hipError_t launch_fb_fused(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb,
                            const float* mlp, const int32_t* users, const int32_t* items, const float* labels,
-                           int64_t n, float inv_batch, int* nslab, int* nbce, hipStream_t st);
+                           int64_t n, float inv_batch, int group, int topk, int* nslab, int* nbce, int* nmet,
+                           hipStream_t st);
 bool fused_supported(const ncf_shape_t& s);
 
 // metrics / summaries

@@ -24,7 +24,8 @@ NCF_NUM_STATS = 8
 NCF_NUM_SUMMARY = 4
 STAT_LOSS_SUM, STAT_HR_SUM, STAT_DCG_SUM, STAT_STEPS, STAT_LAST_LOSS, STAT_LAST_HR, STAT_LAST_DCG = range(7)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libmovierec_ncf.so")
+LIB_PATH = os.environ.get("NCF_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib",
+                                                      "libmovierec_ncf.so")
 
 _i32 = ctypes.c_int32
 _i64 = ctypes.c_int64
