@@ -59,18 +59,16 @@ def parse():
     return ap.parse_args()
 
 
-def emb_update_bytes(cfg_shape, batch, dense_grad):
+def emb_update_bytes(cfg_shape, batch, dense_rows=None):
     """Algorithmic HBM bytes of one embedding scatter-add + Adam sweep launch:
-    read+write p, m, v of every table element (24 B/param), plus the gradient:
-    sparse (1 GPU): the 2B per-sample rows (W floats) + list (4 B/contrib) +
-    row offsets (4 B/row); dense (N GPUs): the all-reduced dense gradient."""
+    read+write p, m, v of every swept table element (24 B/param), plus the
+    gradient: sparse (1 GPU): the 2B per-sample rows (W floats) + list (4 B per
+    contribution) + row offsets (4 B/row); dense (N GPUs, ``dense_rows`` = this
+    rank's shard): the reduce-scattered dense gradient shard (4 B/param)."""
     R, W = cfg_shape.num_rows, cfg_shape.row_width
-    b = 24 * R * W
-    if dense_grad:
-        b += 4 * R * W
-    else:
-        b += 2 * batch * W * 4 + 2 * batch * 4 + (R + 1) * 4
-    return b
+    if dense_rows is not None:
+        return 28 * dense_rows * W
+    return 24 * R * W + 2 * batch * W * 4 + 2 * batch * 4 + (R + 1) * 4
 
 
 def cpu_baseline(cfg, budget_s):
@@ -132,17 +130,17 @@ def main():
         pool.append((u.contiguous(), it.contiguous(), y.contiguous()))
     k = 10 if g > 10 else g - 1
     inv = 1.0 / (B * world)
-    grads = eng.alloc_grads() if world > 1 else None
+    dp = None
+    if world > 1:
+        from movierec.distributed import ReplicatedDataParallel
+        dp = ReplicatedDataParallel(eng)
 
     def step(i):
         u, it, y = pool[i % len(pool)]
-        if world == 1:
+        if dp is None:
             eng.train_step(u, it, y, group=g, k=k, inv_batch=inv)
         else:
-            eng.forward_backward(u, it, y, group=g, k=k, inv_batch=inv, grads=grads)
-            for t in grads:
-                dist.all_reduce(t)
-            eng.apply_update(grads, inv_batch=inv)
+            dp.train_step(u, it, y, group=g, k=k)
 
     for i in range(args.warmup):
         step(i)
@@ -169,7 +167,7 @@ def main():
         elapsed = float(t.item())
     value = args.steps * B * world / elapsed
     kern_ms = ms.value / max(nl.value, 1)
-    nbytes = emb_update_bytes(eng.shape, B, dense_grad=world > 1)
+    nbytes = emb_update_bytes(eng.shape, B, dense_rows=dp.row_count if dp is not None else None)
     achieved = nbytes / (kern_ms * 1e-3) / 1e9
 
     # HR@10 on a synthetic validation set (1 positive + 99 sampled items per user)
@@ -199,7 +197,9 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
             "data": "synthetic (uniform ids, seeded; random-init weights)",
             "config": {"workload": cfg["workload"], "global_batch": B * world, "per_gpu_batch": B,
-                       "negatives_per_positive": cfg["negs"], "parallelism": "dp%d" % world,
+                       "negatives_per_positive": cfg["negs"],
+                       "parallelism": "dp%d" % world + ("" if world == 1 else " (replicated tables: reduce-scatter "
+                                                          "grads, sharded Adam, all-gather rows; all-reduce dense)"),
                        "kernel_path": "generic" if not eng.fast_path else "fused-mfma"},
             "roofline": {"bound": "hbm", "kernel": "embedding scatter-add + Adam sweep (k_emb_update)",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

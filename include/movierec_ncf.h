@@ -65,7 +65,8 @@ extern "C" {
 #define NCF_SUM_HIT 1      /* sum over groups of hit@k */
 #define NCF_SUM_DCG 2      /* sum over groups of dcg@k */
 #define NCF_SUM_GROUPS 3   /* number of groups */
-#define NCF_NUM_SUMMARY 4
+#define NCF_SUM_REG 4      /* L2 loss of the current weights covered by this rank (forward_backward) */
+#define NCF_NUM_SUMMARY 8
 
 typedef struct ncf_shape {
     /* inputs (MovierecModel params: num_users, num_items, layers_sizes; gmf_dim = NeuMF extension) */
@@ -158,17 +159,25 @@ int ncf_evaluate(const ncf_shape_t* shape, const ncf_model_t* model, const ncf_h
  * ncf_forward_backward computes this rank's gradients with the BCE mean taken
  * over hyper->inv_batch (= 1/global batch): dense embedding gradient
  * emb_grad[num_rows x row_width] (every row written, zeros where untouched),
- * mlp_grad[mlp_params], and summary[NCF_NUM_SUMMARY].  The caller sums these
- * three over ranks (RCCL all-reduce) and then calls ncf_apply_update, which
- * adds the L2 terms, applies the optimizer to every parameter, folds the
- * summary into stats[] and increments optim->step. */
+ * mlp_grad[mlp_params], and summary[NCF_NUM_SUMMARY].  summary[NCF_SUM_REG]
+ * holds the L2 loss of embedding rows [reg_row_begin, reg_row_begin +
+ * reg_row_count) plus, if include_dense_reg, of the dense kernels — so that the
+ * sum over ranks of disjoint row ranges is the full L2 term.  The caller sums
+ * the gradients and the summary over ranks (RCCL reduce-scatter / all-reduce).
+ * ncf_apply_update then applies the optimizer to embedding rows [row_begin,
+ * row_begin + row_count) — emb_grad, optim->emb_m and optim->emb_v are
+ * indexed from row_begin (a rank's shard; the whole table on one device) — and
+ * to every dense parameter, folds the summary into stats[] and increments
+ * optim->step.  Replicated data parallelism = reduce-scatter the dense
+ * embedding gradient, update the own shard, all-gather the table. */
 int ncf_forward_backward(const ncf_shape_t* shape, const ncf_model_t* model, const ncf_hyper_t* hyper,
                          const int32_t* users, const int32_t* items, const float* labels, int64_t n,
                          float* emb_grad, float* mlp_grad, float* summary, float* probs_out,
+                         int64_t reg_row_begin, int64_t reg_row_count, int32_t include_dense_reg,
                          void* ws, size_t ws_bytes, void* stream);
 int ncf_apply_update(const ncf_shape_t* shape, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* hyper,
-                     const float* emb_grad, const float* mlp_grad, const float* summary, double* stats,
-                     void* ws, size_t ws_bytes, void* stream);
+                     int64_t row_begin, int64_t row_count, const float* emb_grad, const float* mlp_grad,
+                     const float* summary, double* stats, void* ws, size_t ws_bytes, void* stream);
 
 /* Profiling hook (bench.py): while enabled, every launch group `kernel_id`
  * issued by this thread is bracketed by HIP events on its own stream (up to

@@ -346,7 +346,7 @@ int ncf_train_step(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* optim,
     // dense-layer tail on the side stream, embedding sweep on the main stream
     SideStream* ss = nullptr;
     hipStream_t st2 = fork_side(st, &ss);
-    hipError_t e = ncf::launch_summary(L, ws, fb.nbce, fb.nmet, fb.n_groups, summary, st2);
+    hipError_t e = ncf::launch_summary(L, ws, fb.nbce, fb.nmet, fb.n_groups, 0, 0, summary, st2);
     if (e != hipSuccess) return hip_check(e, "summary");
     int nreg_mlp = 0;
     prof_begin(NCF_K_MLP_UPDATE, st2);
@@ -355,7 +355,8 @@ int ncf_train_step(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* optim,
     prof_end(NCF_K_MLP_UPDATE, st2);
     if (e != hipSuccess) return hip_check(e, "dense update");
     prof_begin(NCF_K_EMB_UPDATE, st);
-    e = ncf::launch_emb_update(*s, L, ws, model->emb, optim->emb_m, optim->emb_v, optim->step, *h, nullptr, st);
+    e = ncf::launch_emb_update(*s, L, ws, model->emb, optim->emb_m, optim->emb_v, optim->step, *h, nullptr,
+                               s->num_rows, st);
     prof_end(NCF_K_EMB_UPDATE, st);
     if (e != hipSuccess) return hip_check(e, "embedding update");
     e = join_side(st, ss);
@@ -367,9 +368,13 @@ int ncf_train_step(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* optim,
 
 int ncf_forward_backward(const ncf_shape_t* s, const ncf_model_t* model, const ncf_hyper_t* h, const int32_t* users,
                          const int32_t* items, const float* labels, int64_t n, float* emb_grad, float* mlp_grad,
-                         float* summary, float* probs_out, void* ws, size_t ws_bytes, void* stream) {
+                         float* summary, float* probs_out, int64_t reg_row_begin, int64_t reg_row_count,
+                         int32_t include_dense_reg, void* ws, size_t ws_bytes, void* stream) {
     if (int r = check_train_args(s, model, h, users, items, labels, n)) return r;
     if (!emb_grad || !mlp_grad || !summary) return fail(NCF_EINVAL, "NULL gradient output");
+    if (reg_row_begin < 0 || reg_row_count < 0 || reg_row_begin > s->num_rows)
+        return fail(NCF_EINVAL, "invalid regulariser row range");
+    if (reg_row_begin + reg_row_count > s->num_rows) reg_row_count = s->num_rows - reg_row_begin;
     ncf::WsLayout L;
     if (int r = check_ws(*s, n, ws, ws_bytes, &L)) return r;
     hipStream_t st = (hipStream_t)stream;
@@ -377,12 +382,17 @@ int ncf_forward_backward(const ncf_shape_t* s, const ncf_model_t* model, const n
     if (int r = run_fb(*s, L, model, h, users, items, labels, n, ws, probs_out, &fb, st)) return r;
     SideStream* ss = nullptr;
     hipStream_t st2 = fork_side(st, &ss);
-    hipError_t e = ncf::launch_summary(L, ws, fb.nbce, fb.nmet, fb.n_groups, summary, st2);
-    if (e != hipSuccess) return hip_check(e, "summary");
-    int nreg = 0;
-    e = ncf::launch_mlp_update(*s, L, ws, nullptr, nullptr, nullptr, nullptr, *h, fb.nslab, nullptr, mlp_grad, false,
-                               &nreg, st2);
+    int nreg_mlp = 0, nreg_emb = 0;
+    hipError_t e = ncf::launch_mlp_update(*s, L, ws, model->mlp, nullptr, nullptr, nullptr, *h, fb.nslab, nullptr,
+                                          mlp_grad, false, &nreg_mlp, st2, include_dense_reg != 0);
     if (e != hipSuccess) return hip_check(e, "dense-layer gradient");
+    if (h->l2[0] != 0.0f && reg_row_count > 0) {
+        e = ncf::launch_emb_reg(*s, L, ws, model->emb + reg_row_begin * s->row_width, reg_row_count, h->l2[0], st2);
+        if (e != hipSuccess) return hip_check(e, "embedding l2");
+        nreg_emb = ncf::kUpdateGrid;
+    }
+    e = ncf::launch_summary(L, ws, fb.nbce, fb.nmet, fb.n_groups, nreg_emb, nreg_mlp, summary, st2);
+    if (e != hipSuccess) return hip_check(e, "summary");
     e = ncf::launch_emb_grad_dense(*s, L, ws, emb_grad, st);
     if (e != hipSuccess) return hip_check(e, "dense embedding gradient");
     return hip_check(join_side(st, ss), "side-stream join");
@@ -406,35 +416,37 @@ int ncf_evaluate(const ncf_shape_t* s, const ncf_model_t* model, const ncf_hyper
                                   ncf::at<float>(ws, L.part_dcg), &nmet, st);
     if (e != hipSuccess) return hip_check(e, "metrics");
     float* summary = ncf::at<float>(ws, L.summary);
-    e = ncf::launch_summary(L, ws, nbce, nmet, (float)ng, summary, st);
-    if (e != hipSuccess) return hip_check(e, "summary");
     int nreg_emb = 0, nreg_mlp = 0;
     if (h->l2[0] != 0.0f) {
-        e = ncf::launch_emb_reg(*s, L, ws, model->emb, h->l2[0], st);
+        e = ncf::launch_emb_reg(*s, L, ws, model->emb, s->num_rows, h->l2[0], st);
         if (e != hipSuccess) return hip_check(e, "embedding l2");
         nreg_emb = ncf::kUpdateGrid;
     }
     e = ncf::launch_mlp_update(*s, L, ws, model->mlp, nullptr, nullptr, nullptr, *h, 0, model->mlp, nullptr, false,
                                &nreg_mlp, st, true);
     if (e != hipSuccess) return hip_check(e, "dense l2");
+    e = ncf::launch_summary(L, ws, nbce, nmet, (float)ng, nreg_emb, nreg_mlp, summary, st);
+    if (e != hipSuccess) return hip_check(e, "summary");
     if (probs_out) {
         e = hipMemcpyAsync(probs_out, probs, (size_t)n * 4, hipMemcpyDeviceToDevice, st);
         if (e != hipSuccess) return hip_check(e, "probs copy");
     }
-    e = ncf::launch_stats(L, ws, summary, nreg_emb, nreg_mlp, h->inv_batch, stats, nullptr, false, st);
+    e = ncf::launch_stats(L, ws, summary, 0, 0, h->inv_batch, stats, nullptr, false, st);
     return hip_check(e, "stats");
 }
 
 int ncf_apply_update(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* h,
-                     const float* emb_grad, const float* mlp_grad, const float* summary, double* stats, void* ws,
-                     size_t ws_bytes, void* stream) {
+                     int64_t row_begin, int64_t row_count, const float* emb_grad, const float* mlp_grad,
+                     const float* summary, double* stats, void* ws, size_t ws_bytes, void* stream) {
     if (int r = check_shape(s)) return r;
     if (int r = check_hyper(h)) return r;
-    if (!model || !model->emb || !model->mlp || !emb_grad || !mlp_grad || !summary)
+    if (!model || !model->emb || !model->mlp || !mlp_grad || !summary || (row_count > 0 && !emb_grad))
         return fail(NCF_EINVAL, "NULL device pointer");
     if (!optim || !optim->step || (h->optimizer == NCF_OPT_ADAM &&
                                    (!optim->emb_m || !optim->emb_v || !optim->mlp_m || !optim->mlp_v)))
         return fail(NCF_EINVAL, "NULL optimizer state");
+    if (row_begin < 0 || row_count < 0 || row_begin > s->num_rows) return fail(NCF_EINVAL, "invalid row range");
+    if (row_begin + row_count > s->num_rows) row_count = s->num_rows - row_begin;
     ncf::WsLayout L;
     if (int r = check_ws(*s, 1, ws, ws_bytes, &L)) return r;
     hipStream_t st = (hipStream_t)stream;
@@ -446,14 +458,17 @@ int ncf_apply_update(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* opti
                                           mlp_grad, nullptr, true, &nreg_mlp, st2);
     prof_end(NCF_K_MLP_UPDATE, st2);
     if (e != hipSuccess) return hip_check(e, "dense update");
-    prof_begin(NCF_K_EMB_UPDATE, st);
-    e = ncf::launch_emb_update(*s, L, ws, model->emb, optim->emb_m, optim->emb_v, optim->step, *h, emb_grad, st);
-    prof_end(NCF_K_EMB_UPDATE, st);
-    if (e != hipSuccess) return hip_check(e, "embedding update");
+    if (row_count > 0) {
+        prof_begin(NCF_K_EMB_UPDATE, st);
+        e = ncf::launch_emb_update(*s, L, ws, model->emb + row_begin * s->row_width, optim->emb_m, optim->emb_v,
+                                   optim->step, *h, emb_grad, row_count, st);
+        prof_end(NCF_K_EMB_UPDATE, st);
+        if (e != hipSuccess) return hip_check(e, "embedding update");
+    }
     e = join_side(st, ss);
     if (e != hipSuccess) return hip_check(e, "side-stream join");
-    const int nreg_emb = h->l2[0] != 0.0f ? ncf::kUpdateGrid : 0;
-    e = ncf::launch_stats(L, ws, summary, nreg_emb, nreg_mlp, h->inv_batch, stats, optim->step, true, st);
+    // the L2 loss of the pre-update weights arrives in summary[NCF_SUM_REG]
+    e = ncf::launch_stats(L, ws, summary, 0, 0, h->inv_batch, stats, optim->step, true, st);
     return hip_check(e, "stats");
 }
 

@@ -91,21 +91,21 @@ hipError_t launch_group_metrics(const float* probs, const float* labels, int64_t
                                 float* hit, float* dcg, float* part_hit, float* part_dcg, int* nparts,
                                 hipStream_t st);
 hipError_t launch_rank(const float* probs, int64_t n_groups, int group, int32_t* rank_idx, hipStream_t st);
-hipError_t launch_summary(const WsLayout& L, void* ws, int nbce, int nmet, float n_groups, float* summary,
-                          hipStream_t st);
+hipError_t launch_summary(const WsLayout& L, void* ws, int nbce, int nmet, float n_groups, int nreg_emb,
+                          int nreg_mlp, float* summary, hipStream_t st);
 
 // updates
 enum GradSource { kGradSparse = 0, kGradDense = 1 };
 hipError_t launch_emb_update(const ncf_shape_t& s, const WsLayout& L, void* ws, float* emb, float* m, float* v,
-                             const int32_t* step, const ncf_hyper_t& h, const float* dense_grad,
+                             const int32_t* step, const ncf_hyper_t& h, const float* dense_grad, int64_t rows,
                              hipStream_t st);
 hipError_t launch_emb_grad_dense(const ncf_shape_t& s, const WsLayout& L, void* ws, float* out, hipStream_t st);
 // mlp: reduce slabs (if nslab > 0) or read grad_in; optionally write grad_out; optionally update
 hipError_t launch_mlp_update(const ncf_shape_t& s, const WsLayout& L, void* ws, float* mlp, float* m, float* v,
                              const int32_t* step, const ncf_hyper_t& h, int nslab, const float* grad_in,
                              float* grad_out, bool do_update, int* nreg, hipStream_t st, bool want_reg = false);
-hipError_t launch_emb_reg(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, float lam,
-                          hipStream_t st);
+hipError_t launch_emb_reg(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, int64_t rows,
+                          float lam, hipStream_t st);
 hipError_t launch_stats(const WsLayout& L, void* ws, const float* summary, int nreg_emb, int nreg_mlp,
                         float inv_batch, double* stats, int32_t* step, bool bump_step, hipStream_t st);
 

@@ -254,16 +254,19 @@ __device__ inline float block_sum_array(const float* __restrict__ a, int n, floa
 __global__ __launch_bounds__(kBlock) void k_summary(const float* __restrict__ part_bce, int nbce,
                                                     const float* __restrict__ part_hit,
                                                     const float* __restrict__ part_dcg, int nmet, float n_groups,
+                                                    const float* __restrict__ reg_emb, int nreg_emb,
+                                                    const float* __restrict__ reg_mlp, int nreg_mlp,
                                                     float* __restrict__ summary) {
     __shared__ float red[4];
     const float b = block_sum_array(part_bce, nbce, red);
     const float h = block_sum_array(part_hit, nmet, red);
     const float d = block_sum_array(part_dcg, nmet, red);
-    if (threadIdx.x == 0) {
-        summary[NCF_SUM_BCE] = b;
-        summary[NCF_SUM_HIT] = h;
-        summary[NCF_SUM_DCG] = d;
-        summary[NCF_SUM_GROUPS] = n_groups;
+    const float re = block_sum_array(reg_emb, nreg_emb, red);
+    const float rm = block_sum_array(reg_mlp, nreg_mlp, red);
+    if (threadIdx.x < NCF_NUM_SUMMARY) {
+        const int t = threadIdx.x;
+        summary[t] = t == NCF_SUM_BCE ? b : t == NCF_SUM_HIT ? h : t == NCF_SUM_DCG ? d
+                   : t == NCF_SUM_GROUPS ? n_groups : t == NCF_SUM_REG ? re + rm : 0.f;
     }
 }
 
@@ -275,7 +278,7 @@ __global__ __launch_bounds__(kBlock) void k_stats(const float* __restrict__ summ
     const float re = block_sum_array(reg_emb, nreg_emb, red);
     const float rm = block_sum_array(reg_mlp, nreg_mlp, red);
     if (threadIdx.x == 0) {
-        const float loss = summary[NCF_SUM_BCE] * inv_batch + (re + rm);
+        const float loss = summary[NCF_SUM_BCE] * inv_batch + summary[NCF_SUM_REG] + (re + rm);
         const float ng = summary[NCF_SUM_GROUPS];
         const float hr = ng > 0.f ? summary[NCF_SUM_HIT] / ng : 0.f;
         const float dc = ng > 0.f ? summary[NCF_SUM_DCG] / ng : 0.f;
@@ -308,9 +311,10 @@ static L2Table make_l2_table(const ncf_shape_t& s, const ncf_hyper_t& h) {
 }
 
 hipError_t launch_emb_update(const ncf_shape_t& s, const WsLayout& L, void* ws, float* emb, float* m, float* v,
-                             const int32_t* step, const ncf_hyper_t& h, const float* dense_grad, hipStream_t st) {
+                             const int32_t* step, const ncf_hyper_t& h, const float* dense_grad, int64_t rows,
+                             hipStream_t st) {
     const uint32_t w4 = (uint32_t)(s.row_width / 4);
-    const uint32_t n4 = (uint32_t)(s.num_rows * w4);
+    const uint32_t n4 = (uint32_t)(rows * w4);
     const int32_t* offs = at<int32_t>(ws, L.offs);
     const int32_t* list = at<int32_t>(ws, L.list);
     const float4* gs = at<const float4>(ws, L.gs);
@@ -341,9 +345,9 @@ hipError_t launch_emb_grad_dense(const ncf_shape_t& s, const WsLayout& L, void* 
     return hipGetLastError();
 }
 
-hipError_t launch_emb_reg(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, float lam,
-                          hipStream_t st) {
-    const uint32_t n4 = (uint32_t)(s.num_rows * (s.row_width / 4));
+hipError_t launch_emb_reg(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, int64_t rows,
+                          float lam, hipStream_t st) {
+    const uint32_t n4 = (uint32_t)(rows * (s.row_width / 4));
     k_emb_reg<<<kUpdateGrid, kBlock, 0, st>>>((const float4*)emb, n4, lam, at<float>(ws, L.part_reg));
     return hipGetLastError();
 }
@@ -393,10 +397,12 @@ hipError_t launch_rank(const float* probs, int64_t n_groups, int group, int32_t*
     return hipGetLastError();
 }
 
-hipError_t launch_summary(const WsLayout& L, void* ws, int nbce, int nmet, float n_groups, float* summary,
-                          hipStream_t st) {
+hipError_t launch_summary(const WsLayout& L, void* ws, int nbce, int nmet, float n_groups, int nreg_emb,
+                          int nreg_mlp, float* summary, hipStream_t st) {
+    const float* reg = at<float>(ws, L.part_reg);
     k_summary<<<1, kBlock, 0, st>>>(at<float>(ws, L.part_bce), nbce, at<float>(ws, L.part_hit),
-                                    at<float>(ws, L.part_dcg), nmet, n_groups, summary);
+                                    at<float>(ws, L.part_dcg), nmet, n_groups, reg, nreg_emb, reg + kUpdateGrid,
+                                    nreg_mlp, summary);
     return hipGetLastError();
 }
 

@@ -21,7 +21,8 @@ NCF_EHIP = -2
 NCF_OPT_ADAM = 0
 NCF_OPT_SGD = 1
 NCF_NUM_STATS = 8
-NCF_NUM_SUMMARY = 4
+NCF_NUM_SUMMARY = 8
+SUM_BCE, SUM_HIT, SUM_DCG, SUM_GROUPS, SUM_REG = range(5)
 STAT_LOSS_SUM, STAT_HR_SUM, STAT_DCG_SUM, STAT_STEPS, STAT_LAST_LOSS, STAT_LAST_HR, STAT_LAST_DCG = range(7)
 
 LIB_PATH = os.environ.get("NCF_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib",
@@ -70,9 +71,9 @@ _SIGNATURES = {
     "ncf_evaluate": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfHyper), _vp, _vp, _vp, _i64, _vp, _vp, _vp,
                                     ctypes.c_size_t, _vp]),
     "ncf_forward_backward": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfHyper), _vp, _vp, _vp, _i64, _vp, _vp,
-                                            _vp, _vp, _vp, ctypes.c_size_t, _vp]),
-    "ncf_apply_update": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _vp, _vp, _vp, _vp,
-                                        _vp, ctypes.c_size_t, _vp]),
+                                            _vp, _vp, _i64, _i64, _i32, _vp, ctypes.c_size_t, _vp]),
+    "ncf_apply_update": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _i64, _i64, _vp, _vp,
+                                        _vp, _vp, _vp, ctypes.c_size_t, _vp]),
     "ncf_profile_enable": (ctypes.c_int, [_i32, _i32]),
     "ncf_profile_read": (ctypes.c_int, [_P(ctypes.c_double), _P(_i64)]),
 }

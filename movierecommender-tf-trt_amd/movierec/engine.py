@@ -17,6 +17,7 @@ import numpy as np
 import torch
 
 from . import _native as N
+from .layout import Layout
 
 KERAS_EPSILON = 1e-7
 
@@ -49,6 +50,8 @@ class NCFEngine(object):
         N.check(L.ncf_shape_init(ctypes.byref(self.shape), int(num_users), int(num_items), arr, len(self.layers),
                                  self.gmf_dim))
         s = self.shape
+        self.layout = Layout(num_users, num_items, self.layers, self.gmf_dim)
+        assert (self.layout.row_width, self.layout.mlp_params) == (s.row_width, s.mlp_params)
         self.num_users, self.num_items = int(num_users), int(num_items)
         self.row_width = s.row_width
         self.num_rows = s.num_rows
@@ -109,45 +112,15 @@ class NCFEngine(object):
     # --------------------------------------------------- weights marshalling
     def set_keras_weights(self, w):
         """Load a dict of Keras-layout arrays (names as ``keras_weight_names``)."""
-        s = self.shape
-        U, G, G4 = self.num_users, self.gmf_dim, s.gmf_stride
-        emb = np.zeros((s.num_rows, s.row_width), dtype=np.float32)
-        emb[:U, G4:G4 + s.du] = np.asarray(w["user_embedding"], dtype=np.float32)
-        emb[U:, G4:G4 + s.di] = np.asarray(w["item_embedding"], dtype=np.float32)
-        if G > 0:
-            emb[:U, :G] = np.asarray(w["user_gmf_embedding"], dtype=np.float32)
-            emb[U:, :G] = np.asarray(w["item_gmf_embedding"], dtype=np.float32)
-        parts = []
-        for l in range(1, len(self.layers)):
-            parts += [np.asarray(w["hidden_%d/kernel" % l], np.float32).ravel(),
-                      np.asarray(w["hidden_%d/bias" % l], np.float32).ravel()]
-        parts += [np.asarray(w["output/kernel"], np.float32).ravel(), np.asarray(w["output/bias"], np.float32).ravel()]
-        flat = np.concatenate(parts)
-        assert flat.size == self.mlp_params
-        self.emb.copy_(torch.from_numpy(emb))
+        emb, flat = self.layout.to_device(w)
+        self.emb[:self.num_rows].copy_(torch.from_numpy(emb))
         self.mlp.copy_(torch.from_numpy(flat))
 
     def keras_weights(self, emb=None, mlp=None):
         """Current weights (or the given device tensors in this layout) as a Keras-layout dict."""
-        s = self.shape
-        U, G, G4 = self.num_users, self.gmf_dim, s.gmf_stride
-        e = (self.emb if emb is None else emb).detach().cpu().numpy()
+        e = (self.emb if emb is None else emb)[:self.num_rows].detach().cpu().numpy()
         f = (self.mlp if mlp is None else mlp).detach().cpu().numpy()
-        w = {"user_embedding": e[:U, G4:G4 + s.du].copy(), "item_embedding": e[U:, G4:G4 + s.di].copy()}
-        if G > 0:
-            w["user_gmf_embedding"] = e[:U, :G].copy()
-            w["item_gmf_embedding"] = e[U:, :G].copy()
-        off = 0
-        for l in range(1, len(self.layers)):
-            a, b = self.layers[l - 1], self.layers[l]
-            w["hidden_%d/kernel" % l] = f[off:off + a * b].reshape(a, b).copy()
-            off += a * b
-            w["hidden_%d/bias" % l] = f[off:off + b].copy()
-            off += b
-        F = s.out_features
-        w["output/kernel"] = f[off:off + F].reshape(F, 1).copy()
-        w["output/bias"] = f[off + F:off + F + 1].copy()
-        return w
+        return self.layout.from_device(e, f)
 
     def optimizer_state(self):
         """Adam moments as Keras-layout dicts (m, v) and the iteration count."""
@@ -239,29 +212,55 @@ class NCFEngine(object):
         return hit, dcg
 
     # ------------------------------------------------- data-parallel split
-    def alloc_grads(self):
-        return (torch.empty_like(self.emb), torch.empty_like(self.mlp),
-                torch.empty(N.NCF_NUM_SUMMARY, dtype=torch.float32, device=self.device))
+    def alloc_grads(self, rows=None):
+        """(dense embedding grad [rows x row_width], dense-layer grad, summary); ``rows`` >=
+        num_rows pads the embedding gradient (zero rows) for an equal-shard reduce-scatter."""
+        rows = self.num_rows if rows is None else int(rows)
+        eg = torch.zeros(rows, self.row_width, dtype=torch.float32, device=self.device)
+        return (eg, torch.empty_like(self.mlp),
+                torch.zeros(N.NCF_NUM_SUMMARY, dtype=torch.float32, device=self.device))
 
-    def forward_backward(self, users, items, labels, group, k, inv_batch, grads, probs_out=None):
+    def forward_backward(self, users, items, labels, group, k, inv_batch, grads, probs_out=None,
+                         reg_rows=None, include_dense_reg=True):
+        """This replica's gradients (BCE mean over ``inv_batch``); ``reg_rows`` = (begin, count)
+        of the embedding rows whose L2 loss this replica reports (default: all)."""
         u, i, y = self._ids(users), self._ids(items), self._labels(labels)
         n = u.numel()
         self._ensure_ws(n)
         h = self.hyper
         h.group, h.k, h.inv_batch = int(group), int(k), float(inv_batch)
         eg, mg, sm = grads
+        r0, rc = (0, self.num_rows) if reg_rows is None else reg_rows
         N.check(N.lib().ncf_forward_backward(ctypes.byref(self.shape), ctypes.byref(self.model_s), ctypes.byref(h),
                                              N.ptr(u), N.ptr(i), N.ptr(y), n, N.ptr(eg), N.ptr(mg), N.ptr(sm),
-                                             N.ptr(probs_out), N.ptr(self.ws), self.ws_bytes,
-                                             N.stream_handle(self.device)))
+                                             N.ptr(probs_out), int(r0), int(rc), 1 if include_dense_reg else 0,
+                                             N.ptr(self.ws), self.ws_bytes, N.stream_handle(self.device)))
 
-    def apply_update(self, grads, inv_batch):
+    def apply_update(self, grads, inv_batch, rows=None, emb_grad=None):
+        """Optimizer step: embedding rows ``rows`` = (begin, count) (default: all) from
+        ``emb_grad`` (default grads[0]; indexed from ``begin``), every dense parameter."""
         eg, mg, sm = grads
+        eg = eg if emb_grad is None else emb_grad
+        r0, rc = (0, self.num_rows) if rows is None else rows
         self.hyper.inv_batch = float(inv_batch)
         N.check(N.lib().ncf_apply_update(ctypes.byref(self.shape), ctypes.byref(self.model_s),
-                                         ctypes.byref(self.optim_s), ctypes.byref(self.hyper), N.ptr(eg), N.ptr(mg),
-                                         N.ptr(sm), N.ptr(self.stats), N.ptr(self.ws), self.ws_bytes,
-                                         N.stream_handle(self.device)))
+                                         ctypes.byref(self.optim_s), ctypes.byref(self.hyper), int(r0), int(rc),
+                                         N.ptr(eg), N.ptr(mg), N.ptr(sm), N.ptr(self.stats), N.ptr(self.ws),
+                                         self.ws_bytes, N.stream_handle(self.device)))
+
+    def shard_optimizer_state(self, row_begin, row_count, capacity_rows):
+        """Replicated data parallelism: keep Adam moments only for this rank's embedding shard
+        and pad the table to ``capacity_rows`` (= world * shard rows) for the all-gather."""
+        rows = int(capacity_rows)
+        if rows > self.emb.shape[0]:
+            emb = torch.zeros(rows, self.row_width, dtype=torch.float32, device=self.device)
+            emb[:self.num_rows].copy_(self.emb[:self.num_rows])
+            self.emb = emb
+        self.emb_m = self.emb_m[row_begin:row_begin + row_count].clone()
+        self.emb_v = self.emb_v[row_begin:row_begin + row_count].clone()
+        self.model_s = N.NcfModel(self.emb.data_ptr(), self.mlp.data_ptr())
+        self.optim_s = N.NcfOptim(self.emb_m.data_ptr(), self.emb_v.data_ptr(), self.mlp_m.data_ptr(),
+                                  self.mlp_v.data_ptr(), self.step.data_ptr())
 
     # ------------------------------------------------------------- stats
     @staticmethod

@@ -1,0 +1,169 @@
+"""Data-parallel orchestration (movierec.distributed) with world_size 2.
+
+CPU part (gloo, no GPU): ranks drive the oracle-backed OracleEngine through
+ReplicatedDataParallel; after several steps every replica must equal a
+single-process run on the concatenated global batch (float64, so only the
+cross-rank summation order differs).
+
+GPU part (-m gpu): two processes share the one GPU of the box with the gloo
+backend and drive the real HIP library (NCFEngine); compared against a
+single-process NCFEngine run on the global batch at the fp32 tolerance.
+"""
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import gpu_available
+from oracle import ncf_oracle as O
+
+SHAPE = (23, 17, [8, 6, 4], 4)
+L2 = [0.01, 0.02, 0.0]
+STEPS = 3
+B = 48          # global batch
+GROUP = 4
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _weights():
+    shape = O.NCFShape(*SHAPE)
+    w = O.init_weights(shape, seed=4)
+    return shape, {k: (v * 3).astype(np.float32).astype(np.float64) for k, v in w.items()}
+
+
+def _batches():
+    shape = O.NCFShape(*SHAPE)
+    rng = np.random.RandomState(7)
+    out = []
+    for _ in range(STEPS):
+        users = rng.randint(0, shape.num_users, B // GROUP).repeat(GROUP).astype(np.int32)
+        items = rng.randint(0, shape.num_items, B).astype(np.int32)
+        y = np.tile([0] * (GROUP - 1) + [1], B // GROUP).astype(np.float32)
+        out.append((users, items, y))
+    return out
+
+
+def _cpu_worker(rank, world, port, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [here, os.path.dirname(here), os.path.join(os.path.dirname(here), "movierecommender-tf-trt_amd")]
+    from oracle_engine import OracleEngine
+    from movierec.distributed import ReplicatedDataParallel
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    shape, w = _weights()
+    eng = OracleEngine(shape, w, layers_l2reg=L2)
+    dp = ReplicatedDataParallel(eng)
+    summaries = []
+    per = B // world
+    for users, items, y in _batches():
+        sl = slice(rank * per, (rank + 1) * per)
+        dp.train_step(users[sl], items[sl], y[sl], group=GROUP, k=2)
+        summaries.append(dp.grads[2].clone().numpy())
+    q.put((rank, eng.emb[:eng.num_rows].numpy().copy(), eng.mlp.numpy().copy(), summaries))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_replicated_dp_matches_single_process_cpu():
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from oracle_engine import OracleEngine
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_cpu_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, emb, mlp, summ = q.get(timeout=120)
+        res[r] = (emb, mlp, summ)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # single-process reference on the global batch
+    shape, w = _weights()
+    ref = OracleEngine(shape, w, layers_l2reg=L2)
+    grads = ref.alloc_grads()
+    ref_summ = []
+    for users, items, y in _batches():
+        ref.forward_backward(users, items, y, group=GROUP, k=2, inv_batch=1.0 / B, grads=grads)
+        ref_summ.append(grads[2].clone().numpy())
+        ref.apply_update(grads, 1.0 / B)
+    for r in range(world):
+        emb, mlp, summ = res[r]
+        np.testing.assert_allclose(emb, ref.emb[:ref.num_rows].numpy(), rtol=0, atol=1e-12)
+        np.testing.assert_allclose(mlp, ref.mlp.numpy(), rtol=0, atol=1e-12)
+        for a, b in zip(summ, ref_summ):
+            np.testing.assert_allclose(a[:5], b[:5], rtol=1e-6, atol=1e-9)
+
+
+# ---------------------------------------------------------------- GPU (HIP)
+
+def _gpu_worker(rank, world, port, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [here, os.path.dirname(here), os.path.join(os.path.dirname(here), "movierecommender-tf-trt_amd")]
+    from movierec.engine import NCFEngine
+    from movierec.distributed import ReplicatedDataParallel
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    shape, w = _weights()
+    eng = NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=B,
+                    layers_l2reg=L2)
+    eng.set_keras_weights(w)
+    dp = ReplicatedDataParallel(eng)
+    per = B // world
+    for users, items, y in _batches():
+        sl = slice(rank * per, (rank + 1) * per)
+        dp.train_step(users[sl], items[sl], y[sl], group=GROUP, k=2)
+    torch.cuda.synchronize()
+    q.put((rank, eng.keras_weights(), NCFEngine.read_stats(eng.stats)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_replicated_dp_matches_single_process_gpu():
+    from movierec.engine import NCFEngine
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, wts, st = q.get(timeout=300)
+        res[r] = (wts, st)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    shape, w = _weights()
+    ref = NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=B, layers_l2reg=L2)
+    ref.set_keras_weights(w)
+    for users, items, y in _batches():
+        ref.train_step(users, items, y, group=GROUP, k=2)
+    rw = ref.keras_weights()
+    rst = NCFEngine.read_stats(ref.stats)
+    for r in range(world):
+        wts, st = res[r]
+        for name in rw:
+            np.testing.assert_allclose(wts[name], rw[name], rtol=0, atol=1e-5, err_msg=name)
+        assert st["loss"] == pytest.approx(rst["loss"], rel=1e-5)
+        assert st["hr"] == pytest.approx(rst["hr"], abs=1e-6)
+    assert gpu_available()
