@@ -34,7 +34,8 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 METRIC = "train samples/sec (user-item pairs) NeuMF ml-20m at 1/2/4/8 MI355X; HR@10"
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+FP32_MFMA_PEAK_TFS = 157.3   # dense fp32 MFMA peak (v_mfma_f32_32x32x2_f32), MI355X_MICROARCH.md
 
 CONFIGS = {
     "C": dict(workload="ml-20m NeuMF (config C): 138493 users x 27278 items, gmf 64 + MLP [128,64,32,16], "
@@ -71,6 +72,25 @@ def emb_update_bytes(cfg_shape, batch, dense_rows=None):
     return 24 * R * W + 2 * batch * W * 4 + 2 * batch * 4 + (R + 1) * 4
 
 
+def fwd_bwd_flops(cfg):
+    """Algorithmic flops per sample of the fused forward+backward: 2 x MACs of the forward
+    (MLP layers, GMF product+dot, output), the backward data chain (dX, G_l) and the
+    weight gradients (dW_l, output kernel)."""
+    L, G = cfg["layers"], cfg["gmf_dim"]
+    mlp = sum(a * b for a, b in zip(L[:-1], L[1:]))
+    out = G + L[-1]
+    fwd = mlp + out + G
+    bwd_data = mlp + G * 2 + out
+    dw = mlp + out
+    return 2 * (fwd + bwd_data + dw)
+
+
+def fwd_bwd_bytes(shape, batch):
+    """Algorithmic HBM bytes of the fused kernel: ids+label (12 B), both gathered rows
+    (2W floats), both per-sample gradient rows written (2W floats), the probability."""
+    return batch * (12 + 2 * shape.row_width * 4 * 2 + 4)
+
+
 def cpu_baseline(cfg, budget_s):
     """numpy restatement (oracle/) of one training step, fp32, bounded sample."""
     from oracle import ncf_oracle as O
@@ -98,6 +118,15 @@ def cpu_baseline(cfg, budget_s):
     return dict(value=round(steps * B / t_total, 1), unit="samples/s", cores=int(threads), kind="port",
                 sample="%d full training steps of batch %d (dense Adam over every table row), numpy fp32, "
                        "%.1f s" % (steps, B, t_total))
+
+
+def pmc_traffic(name):
+    """HBM bytes per launch measured by tools/gpu_profile.sh (separate --pmc passes)."""
+    path = os.path.join(ROOT, "profiles", name)
+    try:
+        return json.load(open(path)).get("bytes_per_launch")
+    except (OSError, ValueError):
+        return None
 
 
 def main():
@@ -147,8 +176,7 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    L = N.lib()
-    N.check(L.ncf_profile_enable(N.K_EMB_UPDATE, args.steps))
+    N.profile_enable([N.K_EMB_UPDATE, N.K_FWD_BWD, N.K_INDEX], args.steps)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -157,16 +185,19 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    import ctypes
-    ms, nl = ctypes.c_double(), ctypes.c_int64()
-    N.check(L.ncf_profile_read(ctypes.byref(ms), ctypes.byref(nl)))
-    N.check(L.ncf_profile_enable(-1, 0))
+    ms_emb, nl = N.profile_read(N.K_EMB_UPDATE)
+    ms_fb, nfb = N.profile_read(N.K_FWD_BWD)
+    ms_idx, nidx = N.profile_read(N.K_INDEX)
+    N.profile_enable([], 0)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     value = args.steps * B * world / elapsed
-    kern_ms = ms.value / max(nl.value, 1)
+    kern_ms = ms_emb / max(nl, 1)
+    fb_ms = ms_fb / max(nfb, 1)
+    fb_flops = fwd_bwd_flops(cfg) * B
+    fb_bytes = fwd_bwd_bytes(eng.shape, B)
     nbytes = emb_update_bytes(eng.shape, B, dense_rows=dp.row_count if dp is not None else None)
     achieved = nbytes / (kern_ms * 1e-3) / 1e9
 
@@ -179,13 +210,8 @@ def main():
     eng.evaluate(ev_u, ev_i, ev_y, group=100, k=10, stats=st)
     hr = NCFEngine.read_stats(st)
 
-    traffic = None
-    tpath = os.path.join(ROOT, "profiles", "traffic_emb_update.json")
-    if os.path.exists(tpath) and world == 1:
-        try:
-            traffic = json.load(open(tpath)).get("bytes_per_launch")
-        except Exception:
-            traffic = None
+    traffic = pmc_traffic("traffic_emb_update.json") if world == 1 else None
+    fb_traffic = pmc_traffic("traffic_fb_fused.json") if world == 1 and eng.fast_path else None
 
     if rank == 0:
         cpu = None
@@ -204,7 +230,18 @@ def main():
             "roofline": {"bound": "hbm", "kernel": "embedding scatter-add + Adam sweep (k_emb_update)",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "algorithmic_bytes_per_launch": nbytes, "avg_launch_ms": round(kern_ms, 5)},
+                         "algorithmic_bytes_per_launch": nbytes, "avg_launch_ms": round(kern_ms, 5),
+                         "traffic_source": "rocprofv3 --pmc FETCH_SIZE(x2 gfx950) + WRITE_SIZE, "
+                                           "profiles/traffic_emb_update.json (per launch)"},
+            "roofline_fwd_bwd": {"bound": "mfma", "kernel": "fused NeuMF forward+backward (k_fb_fused, fp32 MFMA)"
+                                 if eng.fast_path else "generic forward+backward", "achieved": round(
+                                     fb_flops / (fb_ms * 1e-3) / 1e12, 2), "peak": FP32_MFMA_PEAK_TFS,
+                                 "unit": "TFLOP/s", "frac": round(fb_flops / (fb_ms * 1e-3) / 1e12 /
+                                                                  FP32_MFMA_PEAK_TFS, 4),
+                                 "algorithmic_flops_per_launch": fb_flops, "avg_launch_ms": round(fb_ms, 5),
+                                 "hbm_GBs": round(fb_bytes / (fb_ms * 1e-3) / 1e9, 1),
+                                 "algorithmic_bytes_per_launch": fb_bytes, "traffic": fb_traffic},
+            "index_build_ms": round(ms_idx / max(nidx, 1), 5),
             "cpu_baseline": cpu,
             "hr_at_10": {"value": round(hr["hr"], 4), "ndcg_at_10": round(hr["dcg"], 4),
                          "data": "synthetic eval groups (random ids; ~0.1 expected for an untrained model)"},

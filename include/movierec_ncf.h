@@ -179,18 +179,19 @@ int ncf_apply_update(const ncf_shape_t* shape, ncf_model_t* model, ncf_optim_t* 
                      int64_t row_begin, int64_t row_count, const float* emb_grad, const float* mlp_grad,
                      const float* summary, double* stats, void* ws, size_t ws_bytes, void* stream);
 
-/* Profiling hook (bench.py): while enabled, every launch group `kernel_id`
- * issued by this thread is bracketed by HIP events on its own stream (up to
- * `capacity` launches); ncf_profile_read synchronises on the last event and
- * returns the summed device time (ms) and the number of launches, then resets.
- * kernel_id < 0 disables. */
+/* Profiling hook (bench.py): while enabled, every launch of a group whose bit
+ * is set in `kernel_mask` (bit NCF_K_*) issued by this thread is bracketed by
+ * HIP events on its own stream (up to `capacity` launches per group);
+ * ncf_profile_read synchronises on the group's last event and returns the
+ * summed device time (ms) and the number of launches, then resets that group.
+ * kernel_mask <= 0 disables. */
 #define NCF_K_INDEX 1       /* count + scan + fill + segment sorts */
 #define NCF_K_FWD_BWD 2     /* gather + GMF + MLP fwd + BCE + MLP bwd (+ dense-weight partials) */
 #define NCF_K_EMB_UPDATE 3  /* embedding scatter-add + optimizer sweep */
 #define NCF_K_MLP_UPDATE 4  /* dense-weight gradient reduction + optimizer */
 #define NCF_K_METRICS 5     /* hr/dcg + loss summary */
-int ncf_profile_enable(int32_t kernel_id, int32_t capacity);
-int ncf_profile_read(double* total_ms, int64_t* launches);
+int ncf_profile_enable(int32_t kernel_mask, int32_t capacity);
+int ncf_profile_read(int32_t kernel_id, double* total_ms, int64_t* launches);
 
 #ifdef __cplusplus
 }

@@ -64,21 +64,26 @@ int check_hyper(const ncf_hyper_t* h) {
     return 0;
 }
 
-struct Profiler {
-    int kernel = -1;
+struct ProfSlot {
     std::vector<hipEvent_t> start, stop;
     size_t used = 0;
+};
+struct Profiler {
+    uint32_t mask = 0;  // bit k set: time launch group k
+    ProfSlot slot[8];
 };
 thread_local Profiler g_prof;
 
 void prof_begin(int k, hipStream_t st) {
-    if (g_prof.kernel != k || g_prof.used >= g_prof.start.size()) return;
-    hipEventRecord(g_prof.start[g_prof.used], st);
+    ProfSlot& p = g_prof.slot[k & 7];
+    if (!(g_prof.mask >> k & 1u) || p.used >= p.start.size()) return;
+    hipEventRecord(p.start[p.used], st);
 }
 void prof_end(int k, hipStream_t st) {
-    if (g_prof.kernel != k || g_prof.used >= g_prof.start.size()) return;
-    hipEventRecord(g_prof.stop[g_prof.used], st);
-    ++g_prof.used;
+    ProfSlot& p = g_prof.slot[k & 7];
+    if (!(g_prof.mask >> k & 1u) || p.used >= p.start.size()) return;
+    hipEventRecord(p.stop[p.used], st);
+    ++p.used;
 }
 
 // Side stream (one per device, created on first use): the dense-layer tail (loss summary,
@@ -472,37 +477,41 @@ int ncf_apply_update(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* opti
     return hip_check(e, "stats");
 }
 
-int ncf_profile_enable(int32_t kernel_id, int32_t capacity) {
-    g_prof.kernel = kernel_id;
-    g_prof.used = 0;
-    if (kernel_id < 0) return 0;
-    if (capacity < 1) return fail(NCF_EINVAL, "capacity must be >= 1");
-    while ((int)g_prof.start.size() < capacity) {
-        hipEvent_t a, b;
-        if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess)
-            return fail(NCF_EHIP, "hipEventCreate failed");
-        g_prof.start.push_back(a);
-        g_prof.stop.push_back(b);
+int ncf_profile_enable(int32_t kernel_mask, int32_t capacity) {
+    g_prof.mask = kernel_mask < 0 ? 0u : (uint32_t)kernel_mask;
+    for (int k = 0; k < 8; ++k) {
+        ProfSlot& p = g_prof.slot[k];
+        p.used = 0;
+        if (!(g_prof.mask >> k & 1u)) continue;
+        if (capacity < 1) return fail(NCF_EINVAL, "capacity must be >= 1");
+        while ((int)p.start.size() < capacity) {
+            hipEvent_t a, b;
+            if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess)
+                return fail(NCF_EHIP, "hipEventCreate failed");
+            p.start.push_back(a);
+            p.stop.push_back(b);
+        }
     }
     return 0;
 }
 
-int ncf_profile_read(double* total_ms, int64_t* launches) {
-    if (!total_ms || !launches) return fail(NCF_EINVAL, "NULL argument");
+int ncf_profile_read(int32_t kernel_id, double* total_ms, int64_t* launches) {
+    if (!total_ms || !launches || kernel_id < 0 || kernel_id > 7) return fail(NCF_EINVAL, "invalid argument");
+    ProfSlot& p = g_prof.slot[kernel_id];
     double tot = 0.0;
-    if (g_prof.used > 0) {
-        hipError_t e = hipEventSynchronize(g_prof.stop[g_prof.used - 1]);
+    if (p.used > 0) {
+        hipError_t e = hipEventSynchronize(p.stop[p.used - 1]);
         if (e != hipSuccess) return hip_check(e, "hipEventSynchronize");
     }
-    for (size_t i = 0; i < g_prof.used; ++i) {
+    for (size_t i = 0; i < p.used; ++i) {
         float ms = 0.f;
-        hipError_t e = hipEventElapsedTime(&ms, g_prof.start[i], g_prof.stop[i]);
+        hipError_t e = hipEventElapsedTime(&ms, p.start[i], p.stop[i]);
         if (e != hipSuccess) return hip_check(e, "hipEventElapsedTime");
         tot += ms;
     }
     *total_ms = tot;
-    *launches = (int64_t)g_prof.used;
-    g_prof.used = 0;
+    *launches = (int64_t)p.used;
+    p.used = 0;
     return 0;
 }
 

@@ -75,10 +75,25 @@ _SIGNATURES = {
     "ncf_apply_update": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _i64, _i64, _vp, _vp,
                                         _vp, _vp, _vp, ctypes.c_size_t, _vp]),
     "ncf_profile_enable": (ctypes.c_int, [_i32, _i32]),
-    "ncf_profile_read": (ctypes.c_int, [_P(ctypes.c_double), _P(_i64)]),
+    "ncf_profile_read": (ctypes.c_int, [_i32, _P(ctypes.c_double), _P(_i64)]),
 }
 EXPORTED = sorted(_SIGNATURES)
 K_INDEX, K_FWD_BWD, K_EMB_UPDATE, K_MLP_UPDATE, K_METRICS = 1, 2, 3, 4, 5
+
+
+def profile_enable(kernels, capacity):
+    """Time the given launch groups (K_* ids) with HIP events on their streams."""
+    mask = 0
+    for k in kernels:
+        mask |= 1 << k
+    check(lib().ncf_profile_enable(mask, int(capacity)))
+
+
+def profile_read(kernel):
+    """(summed device ms, launches) of one launch group since profile_enable."""
+    ms, n = ctypes.c_double(), ctypes.c_int64()
+    check(lib().ncf_profile_read(int(kernel), ctypes.byref(ms), ctypes.byref(n)))
+    return ms.value, n.value
 
 _lib = None
 
