@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define NCF_ABI_VERSION 1
+#define NCF_ABI_VERSION 2
 #define NCF_MAX_LAYERS 8
 #define NCF_EINVAL (-1)
 #define NCF_EHIP (-2)
@@ -178,6 +178,57 @@ int ncf_forward_backward(const ncf_shape_t* shape, const ncf_model_t* model, con
 int ncf_apply_update(const ncf_shape_t* shape, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* hyper,
                      int64_t row_begin, int64_t row_count, const float* emb_grad, const float* mlp_grad,
                      const float* summary, double* stats, void* ws, size_t ws_bytes, void* stream);
+
+/* Row-sharded data parallelism (no reference counterpart — the
+ * reference trains on one CPU).  Rank r of `world` (1..16) owns the table rows g
+ * (users 0..U-1, items U..U+I-1) with g % world == r, stored at local row
+ * g / world of its (shard_rows x row_width) shard, shard_rows = ceil(R/world),
+ * with the Adam moments of those rows.  Dense parameters are replicated.  A step:
+ *   ncf_shard_plan            unique rows of the local batch, grouped by owner
+ *                             (uniq_rows[] = local row ids at the owner,
+ *                             send_counts[world]); compact ids kept in ws
+ *   all_to_all (host, RCCL)   row ids to their owners
+ *   ncf_gather_rows           owner: rows requested by every rank
+ *   all_to_all                row values back, in uniq_rows order
+ *   ncf_shard_forward_backward  fused forward/backward on the unique rows:
+ *                             per-unique-row gradient uniq_grad, dense-layer
+ *                             gradient, summary
+ *   all_to_all                unique-row gradients to their owners;
+ *                             all_reduce of the dense gradient and summary
+ *   ncf_shard_apply_update    owner: sums the received gradients per row in
+ *                             ascending source order, Adam/SGD over its whole
+ *                             shard (dense semantics, F5) and the dense layers
+ * The result equals ncf_train_step on the concatenated global batch up to fp32
+ * summation order; with world == 1 it is bitwise identical.
+ * The workspace comes from ncf_shard_workspace_size / _init (not
+ * ncf_workspace_size) and must be used with the same world. */
+int ncf_shard_rows(const ncf_shape_t* shape, int32_t world, int64_t* rows);
+int ncf_shard_workspace_size(const ncf_shape_t* shape, int64_t max_batch, int32_t world, size_t* bytes);
+int ncf_shard_workspace_init(const ncf_shape_t* shape, int64_t max_batch, int32_t world, void* ws, size_t ws_bytes,
+                             void* stream);
+/* uniq_rows: int32[2n] capacity, send_counts: int32[world] (device). */
+int ncf_shard_plan(const ncf_shape_t* shape, int32_t world, const int32_t* users, const int32_t* items, int64_t n,
+                   int32_t* uniq_rows, int32_t* send_counts, void* ws, size_t ws_bytes, void* stream);
+/* out[j] = table[rows[j]] for j < m (rows outside [0, table_rows) give zero rows). */
+int ncf_gather_rows(const ncf_shape_t* shape, const float* table, int64_t table_rows, const int32_t* rows, int64_t m,
+                    float* out, void* stream);
+/* model->emb = the plan's unique rows (in uniq_rows order), model->mlp the dense
+ * parameters; uniq_grad: float[2n x row_width] capacity.  reg_table/reg_rows:
+ * this rank's shard, whose L2 loss goes into summary[NCF_SUM_REG]. */
+int ncf_shard_forward_backward(const ncf_shape_t* shape, const ncf_model_t* model, const ncf_hyper_t* hyper,
+                               int32_t world, const float* labels, int64_t n, float* uniq_grad, float* mlp_grad,
+                               float* summary, float* probs_out, const float* reg_table, int64_t reg_rows,
+                               int32_t include_dense_reg, void* ws, size_t ws_bytes, void* stream);
+/* model->emb / optim->emb_m / emb_v = this rank's shard; recv_rows[m] /
+ * recv_grad[m x row_width] = the rows requested by (and gradients from) every
+ * rank, concatenated in source-rank order; mlp_grad and summary summed over ranks. */
+int ncf_shard_apply_update(const ncf_shape_t* shape, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* hyper,
+                           int32_t world, const int32_t* recv_rows, const float* recv_grad, int64_t m,
+                           const float* mlp_grad, const float* summary, double* stats, void* ws, size_t ws_bytes,
+                           void* stream);
+/* Predictions for the batch of the last ncf_shard_plan (model->emb = its unique rows). */
+int ncf_shard_predict(const ncf_shape_t* shape, const ncf_model_t* model, int32_t world, int64_t n, float* probs,
+                      void* ws, size_t ws_bytes, void* stream);
 
 /* Profiling hook (bench.py): while enabled, every launch of a group whose bit
  * is set in `kernel_mask` (bit NCF_K_*) issued by this thread is bracketed by

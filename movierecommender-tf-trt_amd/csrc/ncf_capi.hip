@@ -41,18 +41,24 @@ int check_shape(const ncf_shape_t* s) {
     return 0;
 }
 
-int check_ws(const ncf_shape_t& s, int64_t n, void* ws, size_t ws_bytes, ncf::WsLayout* L) {
+int check_ws(const ncf_shape_t& s, int64_t n, void* ws, size_t ws_bytes, ncf::WsLayout* L, int world = 0) {
     if (!ws) return fail(NCF_EINVAL, "workspace is NULL");
     if (n <= 0) return fail(NCF_EINVAL, "batch size must be > 0, got %lld", (long long)n);
     if (n > ncf::kMaxBatch) return fail(NCF_EINVAL, "batch size %lld exceeds %lld", (long long)n,
                                         (long long)ncf::kMaxBatch);
     // the layout depends on max_batch only through per-batch regions; recover it from ws_bytes
     // by requiring the caller to size ws for at least n samples
-    ncf::WsLayout need = ncf::make_layout(s, n);
+    ncf::WsLayout need = ncf::make_layout(s, n, world);
     if (ws_bytes < need.total)
         return fail(NCF_EINVAL, "workspace too small: %zu bytes for batch %lld (need %zu)", ws_bytes,
                     (long long)n, need.total);
     *L = need;
+    return 0;
+}
+
+int check_world(int world) {
+    if (world < 1 || world > ncf::kSmallSeg)
+        return fail(NCF_EINVAL, "world must be in [1, %d] for the row-sharded path, got %d", ncf::kSmallSeg, world);
     return 0;
 }
 
@@ -144,7 +150,7 @@ bool use_fused(const ncf_shape_t& s, const ncf_hyper_t* h) {
 
 namespace ncf {
 
-WsLayout make_layout(const ncf_shape_t& s, int64_t B) {
+WsLayout make_layout(const ncf_shape_t& s, int64_t B, int world) {
     WsLayout L{};
     const int64_t R = s.num_rows;
     const size_t a = 256;
@@ -155,11 +161,20 @@ WsLayout make_layout(const ncf_shape_t& s, int64_t B) {
         return o;
     };
     L.max_batch = B;
-    L.cnt = take((size_t)(R + 1) * 4);
+    L.world = world;
+    L.shard_rows = shard_rows_of(R, world);
+    L.keys = world > 0 ? (int64_t)world * L.shard_rows : R;
+    const int64_t K = L.keys;
+    L.list_cap = 2 * B;
+    if (world > 0) {
+        const int64_t per = 2 * B < L.shard_rows ? 2 * B : L.shard_rows;
+        if ((int64_t)world * per > L.list_cap) L.list_cap = (int64_t)world * per;
+    }
+    L.cnt = take((size_t)(K + 1) * 4);
     L.heavy_n = take(4);
     L.err = take(4);
     L.persistent_end = off;
-    L.nscan = (int)((R + 1 + kScanBlock - 1) / kScanBlock);
+    L.nscan = (int)((K + 1 + kScanBlock - 1) / kScanBlock);
     L.nmetric = (int)((B + kBlock - 1) / kBlock);
     int A = 0;
     for (int l = 0; l < s.num_layers; ++l) A += s.layers[l];
@@ -170,11 +185,10 @@ WsLayout make_layout(const ncf_shape_t& s, int64_t B) {
     L.dz_w = D;
     L.probs = take((size_t)B * 4);
     L.gs = take((size_t)2 * B * s.row_width * 4);
-    L.list = take((size_t)2 * B * 4);
-    L.offs_local = take((size_t)(R + 1) * 4);
-    L.offs = take((size_t)(R + 1) * 4);
+    L.list = take((size_t)L.list_cap * 4);
+    L.offs_local = take((size_t)(K + 1) * 4);
+    L.offs = take((size_t)(K + 1) * 4);
     L.tot = take((size_t)L.nscan * 4);
-    L.heavy = take((size_t)2 * B * 4);
     L.part_bce = take((size_t)kMaxSlabs * 4 + (size_t)L.nmetric * 4);
     L.part_hit = take((size_t)L.nmetric * 4);
     L.part_dcg = take((size_t)L.nmetric * 4);
@@ -183,6 +197,14 @@ WsLayout make_layout(const ncf_shape_t& s, int64_t B) {
     L.slabs = take((size_t)kMaxSlabs * s.mlp_params * 4);
     L.mlp_grad = take((size_t)s.mlp_params * 4);
     L.slab_part = take((size_t)kSlabSplit * s.mlp_params * 4);
+    if (world > 0) {
+        L.uloc = take((size_t)(K + 1) * 4);
+        L.utot = take((size_t)L.nscan * 4);
+        L.cid_u = take((size_t)B * 4);
+        L.cid_i = take((size_t)B * 4);
+        L.uoffs = take((size_t)(2 * B + 1) * 4);
+        L.nuniq = take(4);
+    }
     L.act = take((size_t)B * A * 4);
     L.dz = take((size_t)B * D * 4);
     L.total = off;
@@ -264,7 +286,7 @@ int ncf_predict(const ncf_shape_t* s, const ncf_model_t* model, const int32_t* u
         return fail(NCF_EINVAL, "NULL device pointer");
     int nbce = 0;
     return hip_check(ncf::launch_predict_generic(*s, L, ws, model->emb, model->mlp, users, items, nullptr, n, probs,
-                                                 &nbce, (hipStream_t)stream),
+                                                 ncf::table_ids(*s), &nbce, (hipStream_t)stream),
                      "ncf_predict");
 }
 
@@ -290,19 +312,28 @@ struct FbOut {
 };
 
 // index build + forward/backward (+ group metrics): shared by train_step and forward_backward
+// sharded: ids are the compact ids of the last ncf_shard_plan (model->emb = its unique rows)
 static int run_fb(const ncf_shape_t& s, const ncf::WsLayout& L, const ncf_model_t* model, const ncf_hyper_t* h,
                   const int32_t* users, const int32_t* items, const float* labels, int64_t n, void* ws,
-                  float* probs_out, FbOut* out, hipStream_t st) {
-    prof_begin(NCF_K_INDEX, st);
-    hipError_t e = ncf::launch_index_build(s, L, ws, users, items, n, st);
-    prof_end(NCF_K_INDEX, st);
-    if (e != hipSuccess) return hip_check(e, "index build");
+                  float* probs_out, FbOut* out, hipStream_t st, bool sharded = false) {
+    hipError_t e = hipSuccess;
+    ncf::IdSpace ids = ncf::table_ids(s);
+    if (sharded) {
+        users = ncf::at<int32_t>(ws, L.cid_u);
+        items = ncf::at<int32_t>(ws, L.cid_i);
+        ids = ncf::compact_ids(n);
+    } else {
+        prof_begin(NCF_K_INDEX, st);
+        e = ncf::launch_index_build(s, L, ws, users, items, n, st);
+        prof_end(NCF_K_INDEX, st);
+        if (e != hipSuccess) return hip_check(e, "index build");
+    }
     prof_begin(NCF_K_FWD_BWD, st);
     if (use_fused(s, h))
-        e = ncf::launch_fb_fused(s, L, ws, model->emb, model->mlp, users, items, labels, n, h->inv_batch, h->group,
-                                 h->k, &out->nslab, &out->nbce, &out->nmet, st);
+        e = ncf::launch_fb_fused(s, L, ws, model->emb, model->mlp, users, items, labels, n, h->inv_batch, ids,
+                                 h->group, h->k, &out->nslab, &out->nbce, &out->nmet, st);
     else
-        e = ncf::launch_fb_generic(s, L, ws, model->emb, model->mlp, users, items, labels, n, h->inv_batch,
+        e = ncf::launch_fb_generic(s, L, ws, model->emb, model->mlp, users, items, labels, n, h->inv_batch, ids,
                                    &out->nslab, &out->nbce, st);
     prof_end(NCF_K_FWD_BWD, st);
     if (e != hipSuccess) return hip_check(e, "forward/backward");
@@ -413,7 +444,7 @@ int ncf_evaluate(const ncf_shape_t* s, const ncf_model_t* model, const ncf_hyper
     float* probs = ncf::at<float>(ws, L.probs);
     int nbce = 0;
     hipError_t e = ncf::launch_predict_generic(*s, L, ws, model->emb, model->mlp, users, items, labels, n, probs,
-                                               &nbce, st);
+                                               ncf::table_ids(*s), &nbce, st);
     if (e != hipSuccess) return hip_check(e, "forward");
     const int64_t ng = n / h->group;
     int nmet = 0;
@@ -475,6 +506,153 @@ int ncf_apply_update(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* opti
     // the L2 loss of the pre-update weights arrives in summary[NCF_SUM_REG]
     e = ncf::launch_stats(L, ws, summary, 0, 0, h->inv_batch, stats, optim->step, true, st);
     return hip_check(e, "stats");
+}
+
+// ------------------------------------------------------------ row-sharded data parallelism
+
+int ncf_shard_rows(const ncf_shape_t* s, int32_t world, int64_t* rows) {
+    if (int r = check_shape(s)) return r;
+    if (int r = check_world(world)) return r;
+    if (!rows) return fail(NCF_EINVAL, "rows is NULL");
+    *rows = ncf::shard_rows_of(s->num_rows, world);
+    return 0;
+}
+
+int ncf_shard_workspace_size(const ncf_shape_t* s, int64_t max_batch, int32_t world, size_t* bytes) {
+    if (int r = check_shape(s)) return r;
+    if (int r = check_world(world)) return r;
+    if (!bytes) return fail(NCF_EINVAL, "bytes is NULL");
+    if (max_batch <= 0 || max_batch > ncf::kMaxBatch)
+        return fail(NCF_EINVAL, "max_batch must be in [1, %lld]", (long long)ncf::kMaxBatch);
+    *bytes = ncf::make_layout(*s, max_batch, world).total;
+    return 0;
+}
+
+int ncf_shard_workspace_init(const ncf_shape_t* s, int64_t max_batch, int32_t world, void* ws, size_t ws_bytes,
+                             void* stream) {
+    if (int r = check_shape(s)) return r;
+    if (int r = check_world(world)) return r;
+    ncf::WsLayout L = ncf::make_layout(*s, max_batch, world);
+    if (!ws || ws_bytes < L.total) return fail(NCF_EINVAL, "workspace too small");
+    return hip_check(hipMemsetAsync(ws, 0, L.persistent_end, (hipStream_t)stream), "hipMemsetAsync");
+}
+
+int ncf_shard_plan(const ncf_shape_t* s, int32_t world, const int32_t* users, const int32_t* items, int64_t n,
+                   int32_t* uniq_rows, int32_t* send_counts, void* ws, size_t ws_bytes, void* stream) {
+    if (int r = check_shape(s)) return r;
+    if (int r = check_world(world)) return r;
+    if (!users || !items || !uniq_rows || !send_counts) return fail(NCF_EINVAL, "NULL device pointer");
+    ncf::WsLayout L;
+    if (int r = check_ws(*s, n, ws, ws_bytes, &L, world)) return r;
+    hipStream_t st = (hipStream_t)stream;
+    prof_begin(NCF_K_INDEX, st);
+    hipError_t e = ncf::launch_shard_plan(*s, L, ws, users, items, n, uniq_rows, send_counts, st);
+    prof_end(NCF_K_INDEX, st);
+    return hip_check(e, "shard plan");
+}
+
+int ncf_gather_rows(const ncf_shape_t* s, const float* table, int64_t table_rows, const int32_t* rows, int64_t m,
+                    float* out, void* stream) {
+    if (int r = check_shape(s)) return r;
+    if (m < 0 || table_rows < 0) return fail(NCF_EINVAL, "negative row count");
+    if (m > 0 && (!table || !rows || !out)) return fail(NCF_EINVAL, "NULL device pointer");
+    return hip_check(ncf::launch_gather_rows(*s, table, table_rows, rows, m, out, (hipStream_t)stream),
+                     "gather rows");
+}
+
+int ncf_shard_forward_backward(const ncf_shape_t* s, const ncf_model_t* model, const ncf_hyper_t* h, int32_t world,
+                               const float* labels, int64_t n, float* uniq_grad, float* mlp_grad, float* summary,
+                               float* probs_out, const float* reg_table, int64_t reg_rows,
+                               int32_t include_dense_reg, void* ws, size_t ws_bytes, void* stream) {
+    if (int r = check_shape(s)) return r;
+    if (int r = check_hyper(h)) return r;
+    if (int r = check_world(world)) return r;
+    if (!model || !model->emb || !model->mlp || !labels) return fail(NCF_EINVAL, "NULL device pointer");
+    if (!uniq_grad || !mlp_grad || !summary) return fail(NCF_EINVAL, "NULL gradient output");
+    if (n % h->group)
+        return fail(NCF_EINVAL, "Batch size must be divisible by (num_negs_per_pos + 1). Found: batch_size=%lld, "
+                    "group=%d", (long long)n, h->group);
+    if (reg_rows < 0 || (h->l2[0] != 0.0f && reg_rows > 0 && !reg_table))
+        return fail(NCF_EINVAL, "invalid regulariser rows");
+    ncf::WsLayout L;
+    if (int r = check_ws(*s, n, ws, ws_bytes, &L, world)) return r;
+    hipStream_t st = (hipStream_t)stream;
+    FbOut fb;
+    if (int r = run_fb(*s, L, model, h, nullptr, nullptr, labels, n, ws, probs_out, &fb, st, true)) return r;
+    SideStream* ss = nullptr;
+    hipStream_t st2 = fork_side(st, &ss);
+    int nreg_mlp = 0, nreg_emb = 0;
+    hipError_t e = ncf::launch_mlp_update(*s, L, ws, model->mlp, nullptr, nullptr, nullptr, *h, fb.nslab, nullptr,
+                                          mlp_grad, false, &nreg_mlp, st2, include_dense_reg != 0);
+    if (e != hipSuccess) return hip_check(e, "dense-layer gradient");
+    if (h->l2[0] != 0.0f && reg_rows > 0) {
+        e = ncf::launch_emb_reg(*s, L, ws, reg_table, reg_rows, h->l2[0], st2);
+        if (e != hipSuccess) return hip_check(e, "embedding l2");
+        nreg_emb = ncf::kUpdateGrid;
+    }
+    e = ncf::launch_summary(L, ws, fb.nbce, fb.nmet, fb.n_groups, nreg_emb, nreg_mlp, summary, st2);
+    if (e != hipSuccess) return hip_check(e, "summary");
+    e = ncf::launch_uniq_grad(*s, L, ws, n, uniq_grad, st);
+    if (e != hipSuccess) return hip_check(e, "compact embedding gradient");
+    return hip_check(join_side(st, ss), "side-stream join");
+}
+
+int ncf_shard_apply_update(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* h,
+                           int32_t world, const int32_t* recv_rows, const float* recv_grad, int64_t m,
+                           const float* mlp_grad, const float* summary, double* stats, void* ws, size_t ws_bytes,
+                           void* stream) {
+    if (int r = check_shape(s)) return r;
+    if (int r = check_hyper(h)) return r;
+    if (int r = check_world(world)) return r;
+    if (!model || !model->emb || !model->mlp || !mlp_grad || !summary || (m > 0 && (!recv_rows || !recv_grad)))
+        return fail(NCF_EINVAL, "NULL device pointer");
+    if (!optim || !optim->step || (h->optimizer == NCF_OPT_ADAM &&
+                                   (!optim->emb_m || !optim->emb_v || !optim->mlp_m || !optim->mlp_v)))
+        return fail(NCF_EINVAL, "NULL optimizer state");
+    const int64_t S = ncf::shard_rows_of(s->num_rows, world);
+    if (m < 0 || m > (int64_t)world * S)
+        return fail(NCF_EINVAL, "received row count %lld outside [0, world * shard_rows]", (long long)m);
+    // smallest batch whose layout holds m received rows (the workspace was sized for a larger one)
+    int64_t nb = (m + 2 * world - 1) / (2 * world);
+    if (nb < 1) nb = 1;
+    ncf::WsLayout L;
+    if (int r = check_ws(*s, nb, ws, ws_bytes, &L, world)) return r;
+    hipStream_t st = (hipStream_t)stream;
+    prof_begin(NCF_K_INDEX, st);
+    hipError_t e = ncf::launch_owner_index(L, ws, recv_rows, m, st);
+    prof_end(NCF_K_INDEX, st);
+    if (e != hipSuccess) return hip_check(e, "owner index");
+    SideStream* ss = nullptr;
+    hipStream_t st2 = fork_side(st, &ss);
+    int nreg_mlp = 0;
+    prof_begin(NCF_K_MLP_UPDATE, st2);
+    e = ncf::launch_mlp_update(*s, L, ws, model->mlp, optim->mlp_m, optim->mlp_v, optim->step, *h, 0, mlp_grad,
+                               nullptr, true, &nreg_mlp, st2);
+    prof_end(NCF_K_MLP_UPDATE, st2);
+    if (e != hipSuccess) return hip_check(e, "dense update");
+    prof_begin(NCF_K_EMB_UPDATE, st);
+    e = ncf::launch_emb_update(*s, L, ws, model->emb, optim->emb_m, optim->emb_v, optim->step, *h, nullptr, S, st,
+                               recv_grad);
+    prof_end(NCF_K_EMB_UPDATE, st);
+    if (e != hipSuccess) return hip_check(e, "embedding update");
+    e = join_side(st, ss);
+    if (e != hipSuccess) return hip_check(e, "side-stream join");
+    e = ncf::launch_stats(L, ws, summary, 0, 0, h->inv_batch, stats, optim->step, true, st);
+    return hip_check(e, "stats");
+}
+
+int ncf_shard_predict(const ncf_shape_t* s, const ncf_model_t* model, int32_t world, int64_t n, float* probs,
+                      void* ws, size_t ws_bytes, void* stream) {
+    if (int r = check_shape(s)) return r;
+    if (int r = check_world(world)) return r;
+    if (!model || !model->emb || !model->mlp || !probs) return fail(NCF_EINVAL, "NULL device pointer");
+    ncf::WsLayout L;
+    if (int r = check_ws(*s, n, ws, ws_bytes, &L, world)) return r;
+    int nbce = 0;
+    return hip_check(ncf::launch_predict_generic(*s, L, ws, model->emb, model->mlp, ncf::at<int32_t>(ws, L.cid_u),
+                                                 ncf::at<int32_t>(ws, L.cid_i), nullptr, n, probs,
+                                                 ncf::compact_ids(n), &nbce, (hipStream_t)stream),
+                     "shard predict");
 }
 
 int ncf_profile_enable(int32_t kernel_mask, int32_t capacity) {

@@ -171,7 +171,7 @@ template <class S>
 __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict__ emb, const float* __restrict__ mlp,
                                                         const int32_t* __restrict__ users,
                                                         const int32_t* __restrict__ items,
-                                                        const float* __restrict__ labels, int64_t n, int U, int I,
+                                                        const float* __restrict__ labels, int64_t n, IdSpace ids,
                                                         float inv_batch, float* __restrict__ probs,
                                                         float* __restrict__ gs, float* __restrict__ slabs,
                                                         float* __restrict__ part_bce, int group, int topk,
@@ -219,8 +219,8 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
             y = labels[si];
         }
         // Masked samples read row 0 (a valid address) and get dz = 0: they contribute nothing.
-        const bool ok = inb && (unsigned)u < (unsigned)U && (unsigned)v < (unsigned)I;
-        const int urow = ok ? u : 0, irow = ok ? U + v : 0;
+        const bool ok = inb && (unsigned)u < (unsigned)ids.ubound && (unsigned)v < (unsigned)ids.ibound;
+        const int urow = ok ? u : 0, irow = ok ? ids.ibase + v : 0;
         if (h == 0) {
             srow[32 * w + j] = ok ? urow : -1;
             srow[128 + 32 * w + j] = ok ? irow : -1;
@@ -637,7 +637,7 @@ bool fused_supported(const ncf_shape_t& s) {
 template <class S>
 static hipError_t launch_one(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, const float* mlp,
                              const int32_t* users, const int32_t* items, const float* labels, int64_t n,
-                             float inv_batch, int group, int topk, int* nslab, int* nbce, int* nmet,
+                             float inv_batch, IdSpace ids, int group, int topk, int* nslab, int* nbce, int* nmet,
                              hipStream_t st) {
     static bool configured = false;
     if (!configured) {
@@ -650,8 +650,7 @@ static hipError_t launch_one(const ncf_shape_t& s, const WsLayout& L, void* ws, 
     int grid = (int)(niter < 256 ? niter : 256);
     if (grid > kMaxSlabs) grid = kMaxSlabs;
     const bool in_kernel = group > 0 && group <= 32 && 32 % group == 0;
-    k_fb_fused<S><<<grid, kBlock, S::LDS_BYTES, st>>>(emb, mlp, users, items, labels, n, s.num_users,
-                                                      s.num_items, inv_batch, at<float>(ws, L.probs),
+    k_fb_fused<S><<<grid, kBlock, S::LDS_BYTES, st>>>(emb, mlp, users, items, labels, n, ids, inv_batch, at<float>(ws, L.probs),
                                                       at<float>(ws, L.gs), at<float>(ws, L.slabs),
                                                       at<float>(ws, L.part_bce), group, topk,
                                                       in_kernel ? at<float>(ws, L.part_hit) : nullptr,
@@ -664,12 +663,12 @@ static hipError_t launch_one(const ncf_shape_t& s, const WsLayout& L, void* ws, 
 
 hipError_t launch_fb_fused(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, const float* mlp,
                            const int32_t* users, const int32_t* items, const float* labels, int64_t n,
-                           float inv_batch, int group, int topk, int* nslab, int* nbce, int* nmet,
+                           float inv_batch, IdSpace ids, int group, int topk, int* nslab, int* nbce, int* nmet,
                            hipStream_t st) {
 #define NCF_TRY(SH)                                                                                             \
     if (matches<SH>(s))                                                                                         \
-    return launch_one<SH>(s, L, ws, emb, mlp, users, items, labels, n, inv_batch, group, topk, nslab, nbce, nmet, \
-                          st)
+    return launch_one<SH>(s, L, ws, emb, mlp, users, items, labels, n, inv_batch, ids, group, topk, nslab, nbce, \
+                          nmet, st)
     NCF_TRY(ShapeC);
     NCF_TRY(ShapeB);
     NCF_TRY(ShapeR);

@@ -26,7 +26,7 @@ namespace ncf {
 struct GenShape {
     int n;             // num_layers
     int L[NCF_MAX_LAYERS];
-    int U, I, G, G4, W, du, di, P, F;
+    int U, I, IB, G, G4, W, du, di, P, F;  // U / I: id bounds, IB: row of item 0
     int off[NCF_MAX_LAYERS];      // [l>=1] hidden kernel offset, [0] output kernel offset
     int act_off[NCF_MAX_LAYERS];  // h_l offset inside an activation row
     int gmf_off;                  // gmf product offset inside an activation row
@@ -35,12 +35,13 @@ struct GenShape {
     int D;                        // dz row width (last entry = output dz)
 };
 
-static GenShape make_gen_shape(const ncf_shape_t& s) {
+static GenShape make_gen_shape(const ncf_shape_t& s, IdSpace ids) {
     GenShape g{};
     g.n = s.num_layers;
     for (int l = 0; l < s.num_layers; ++l) g.L[l] = s.layers[l];
-    g.U = s.num_users;
-    g.I = s.num_items;
+    g.U = ids.ubound;
+    g.I = ids.ibound;
+    g.IB = ids.ibase;
     g.G = s.gmf_dim;
     g.G4 = s.gmf_stride;
     g.W = s.row_width;
@@ -86,7 +87,7 @@ __global__ __launch_bounds__(kBlock) void k_fb_generic(GenShape S, const float* 
         const bool ok = (unsigned)u < (unsigned)S.U && (unsigned)v < (unsigned)S.I;
         float* a = act + (size_t)i * S.A;
         const float* eu = emb + (size_t)u * S.W;
-        const float* ei = emb + ((size_t)S.U + (size_t)v) * S.W;
+        const float* ei = emb + ((size_t)S.IB + (size_t)v) * S.W;
         const float* wo = Wt + S.off[0];
         float p;
         if (ok) {
@@ -219,9 +220,9 @@ __global__ __launch_bounds__(kBlock) void k_dw_generic(GenShape S, const float* 
 
 hipError_t launch_fb_generic(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb,
                              const float* mlp, const int32_t* users, const int32_t* items,
-                             const float* labels, int64_t n, float inv_batch, int* nslab, int* nbce,
+                             const float* labels, int64_t n, float inv_batch, IdSpace ids, int* nslab, int* nbce,
                              hipStream_t st) {
-    const GenShape S = make_gen_shape(s);
+    const GenShape S = make_gen_shape(s, ids);
     const int use_lds = s.mlp_params <= kLdsWeightsMax ? 1 : 0;
     const int grid = (int)((n + kBlock - 1) / kBlock);
     k_fb_generic<true><<<grid, kBlock, use_lds ? (size_t)s.mlp_params * 4 : 0, st>>>(
@@ -243,8 +244,9 @@ hipError_t launch_fb_generic(const ncf_shape_t& s, const WsLayout& L, void* ws, 
 
 hipError_t launch_predict_generic(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb,
                                   const float* mlp, const int32_t* users, const int32_t* items,
-                                  const float* labels, int64_t n, float* probs, int* nbce, hipStream_t st) {
-    const GenShape S = make_gen_shape(s);
+                                  const float* labels, int64_t n, float* probs, IdSpace ids, int* nbce,
+                                  hipStream_t st) {
+    const GenShape S = make_gen_shape(s, ids);
     const int use_lds = s.mlp_params <= kLdsWeightsMax ? 1 : 0;
     const int grid = (int)((n + kBlock - 1) / kBlock);
     k_fb_generic<false><<<grid, kBlock, use_lds ? (size_t)s.mlp_params * 4 : 0, st>>>(

@@ -25,28 +25,55 @@
 
 namespace ncf {
 
-__device__ inline int contrib_key(int64_t c, const int32_t* __restrict__ users, const int32_t* __restrict__ items,
-                                  int32_t U, int32_t I, bool* ok) {
-    const int64_t i = c >> 1;
-    if (c & 1) {
-        const int v = items[i];
-        *ok = (unsigned)v < (unsigned)I;
-        return U + v;
+// Where contribution c's key comes from.
+enum KeyMode {
+    kKeyPair = 0,      // c = 2i + side: user row users[i] / item row U + items[i]
+    kKeyPairPerm = 1,  // same rows, keyed owner-major for a row-sharded plan
+    kKeyList = 2,      // c indexes keys[] directly (owner index over received row ids)
+};
+
+struct KeySrc {
+    const int32_t* users;
+    const int32_t* items;
+    const int32_t* keys;
+    int32_t U, I;
+    int32_t world;
+    int32_t S;  // shard rows (kKeyPairPerm) / key count (kKeyList)
+};
+
+template <int MODE>
+__device__ inline int contrib_key(int64_t c, const KeySrc& k, bool* ok) {
+    if constexpr (MODE == kKeyList) {
+        const int v = k.keys[c];
+        *ok = (unsigned)v < (unsigned)k.S;
+        return v;
+    } else {
+        const int64_t i = c >> 1;
+        int g;
+        if (c & 1) {
+            const int v = k.items[i];
+            *ok = (unsigned)v < (unsigned)k.I;
+            g = k.U + v;
+        } else {
+            const int u = k.users[i];
+            *ok = (unsigned)u < (unsigned)k.U;
+            g = u;
+        }
+        if constexpr (MODE == kKeyPairPerm) {
+            const int q = g / k.world;
+            g = (g - q * k.world) * k.S + q;
+        }
+        return g;
     }
-    const int u = users[i];
-    *ok = (unsigned)u < (unsigned)U;
-    return u;
 }
 
-__global__ __launch_bounds__(kBlock) void k_count(const int32_t* __restrict__ users,
-                                                  const int32_t* __restrict__ items, int64_t n, int32_t U,
-                                                  int32_t I, int32_t* __restrict__ cnt, int32_t* heavy_n,
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_count(KeySrc ks, int64_t m, int32_t* __restrict__ cnt, int32_t* heavy_n,
                                                   int32_t* err) {
     if (blockIdx.x == 0 && threadIdx.x == 0) *heavy_n = 0;
-    const int64_t m = 2 * n;
     for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < m; c += (int64_t)gridDim.x * blockDim.x) {
         bool ok;
-        const int key = contrib_key(c, users, items, U, I, &ok);
+        const int key = contrib_key<MODE>(c, ks, &ok);
         if (ok)
             atomicAdd(&cnt[key], 1);
         else
@@ -54,16 +81,20 @@ __global__ __launch_bounds__(kBlock) void k_count(const int32_t* __restrict__ us
     }
 }
 
+// Per-2048-key exclusive scan of cnt (and, for a plan, of the occupied-key flags cnt > 0).
+template <bool UNIQ>
 __global__ __launch_bounds__(kBlock) void k_scan_local(const int32_t* __restrict__ cnt, int64_t r1,
-                                                       int32_t* __restrict__ offs, int32_t* __restrict__ tot) {
+                                                       int32_t* __restrict__ offs, int32_t* __restrict__ tot,
+                                                       int32_t* __restrict__ uloc, int32_t* __restrict__ utot) {
     __shared__ int sw[4];
     const int64_t base = (int64_t)blockIdx.x * kScanBlock + threadIdx.x * 8;
     int v[8];
-    int sum = 0;
+    int sum = 0, nz = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         v[j] = (base + j < r1) ? cnt[base + j] : 0;
         sum += v[j];
+        nz += v[j] > 0;
     }
     int total;
     int run = block_exscan_256(sum, sw, &total);
@@ -73,6 +104,16 @@ __global__ __launch_bounds__(kBlock) void k_scan_local(const int32_t* __restrict
         run += v[j];
     }
     if (threadIdx.x == 0) tot[blockIdx.x] = total;
+    if constexpr (UNIQ) {
+        int utotal;
+        int urun = block_exscan_256(nz, sw, &utotal);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if (base + j < r1) uloc[base + j] = urun;
+            urun += v[j] > 0;
+        }
+        if (threadIdx.x == 0) utot[blockIdx.x] = utotal;
+    }
 }
 
 // Exclusive prefix of the scan-block totals into LDS pre[0..nscan) (every thread participates).
@@ -88,31 +129,75 @@ __device__ inline void block_prefix_of_totals(const int32_t* __restrict__ tot, i
     __syncthreads();
 }
 
-// Finalise the row offsets (offs_g = local scan + prefix of block totals) and scatter every
-// contribution into its row's list slot; the per-row counter runs back down to zero.
-__global__ __launch_bounds__(kBlock) void k_fill(const int32_t* __restrict__ users, const int32_t* __restrict__ items,
-                                                 int64_t n, int32_t U, int32_t I, int32_t* __restrict__ cnt,
+// Plan outputs of k_fill (UNIQ only).
+struct PlanOut {
+    const int32_t* uloc;
+    const int32_t* utot;
+    int32_t* uniq_rows;    // [nuniq] local row id at the owner, grouped by owner
+    int32_t* send_counts;  // [world]
+    int32_t* cid_u;        // [n]
+    int32_t* cid_i;        // [n]
+    int32_t* uoffs;        // [nuniq + 1]
+    int32_t* nuniq;
+};
+
+// Finalise the key offsets (offs_g = local scan + prefix of block totals) and scatter every
+// contribution into its key's list slot; the per-key counter runs back down to zero.  A plan
+// (UNIQ) also numbers the occupied keys (compact ids) and writes the per-owner counts.
+template <int MODE, bool UNIQ>
+__global__ __launch_bounds__(kBlock) void k_fill(KeySrc ks, int64_t m, int32_t* __restrict__ cnt,
                                                  const int32_t* __restrict__ local, const int32_t* __restrict__ tot,
                                                  int nscan, int64_t r1, int32_t* __restrict__ offs_g,
-                                                 int32_t* __restrict__ list) {
-    extern __shared__ __attribute__((aligned(16))) int pre[];
+                                                 int32_t* __restrict__ list, PlanOut po) {
+    extern __shared__ __attribute__((aligned(16))) int pre[];  // [nscan] (+ [nscan] unique prefix)
     __shared__ int sw[4];
+    int* upre = pre + nscan;
     block_prefix_of_totals(tot, nscan, pre, sw);
+    if constexpr (UNIQ) block_prefix_of_totals(po.utot, nscan, upre, sw);
     const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t gstride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t r = gt; r < r1; r += gstride) offs_g[r] = local[r] + pre[r / kScanBlock];
-    const int64_t m = 2 * n;
+    const int64_t K = r1 - 1;
+    for (int64_t r = gt; r < r1; r += gstride) {
+        const int o = local[r] + pre[r / kScanBlock];
+        offs_g[r] = o;
+        if constexpr (UNIQ) {
+            if (r < K) {
+                const int o1 = local[r + 1] + pre[(r + 1) / kScanBlock];
+                if (o1 > o) {
+                    const int u = po.uloc[r] + upre[r / kScanBlock];
+                    po.uniq_rows[u] = (int)(r % ks.S);
+                    po.uoffs[u] = o;
+                }
+            }
+        }
+    }
+    if constexpr (UNIQ) {
+        if (blockIdx.x == 0) {
+            auto uprefix = [&](int64_t x) { return po.uloc[x] + upre[x / kScanBlock]; };
+            for (int d = threadIdx.x; d < ks.world; d += kBlock)
+                po.send_counts[d] = uprefix((int64_t)(d + 1) * ks.S) - uprefix((int64_t)d * ks.S);
+            if (threadIdx.x == 0) {
+                const int nu = uprefix(K);
+                *po.nuniq = nu;
+                po.uoffs[nu] = (int)m;
+            }
+        }
+    }
     for (int64_t c = gt; c < m; c += gstride) {
         bool ok;
-        const int key = contrib_key(c, users, items, U, I, &ok);
+        const int key = contrib_key<MODE>(c, ks, &ok);
+        if constexpr (UNIQ) {
+            const int u = ok ? po.uloc[key] + upre[key / kScanBlock] : -1;
+            ((c & 1) ? po.cid_i : po.cid_u)[c >> 1] = u;
+        }
         if (!ok) continue;
         const int slot = atomicSub(&cnt[key], 1) - 1;
         list[local[key] + pre[key / kScanBlock] + slot] = (int)c;
     }
 }
 
-// Sort each row's contribution list ascending.  Rows of <= kSmallSeg entries: one thread,
-// odd-even network in registers.  Longer rows: queued in LDS and sorted by the whole
+// Sort each key's contribution list ascending.  Keys of <= kSmallSeg entries: one thread,
+// odd-even network in registers.  Longer keys: queued in LDS and sorted by the whole
 // workgroup with a bitmap over the contribution ids (set bits, popcount scan, write back).
 __global__ __launch_bounds__(kBlock) void k_sort(const int32_t* __restrict__ offs, int64_t R,
                                                  int32_t* __restrict__ list, int nwords) {
@@ -186,25 +271,7 @@ static int grid_for(int64_t work, int cap) {
     return (int)g;
 }
 
-hipError_t launch_index_build(const ncf_shape_t& s, const WsLayout& L, void* ws, const int32_t* users,
-                              const int32_t* items, int64_t n, hipStream_t st) {
-    const int64_t R = s.num_rows;
-    const int64_t r1 = R + 1;
-    int32_t* cnt = at<int32_t>(ws, L.cnt);
-    int32_t* heavy_n = at<int32_t>(ws, L.heavy_n);
-    int32_t* err = at<int32_t>(ws, L.err);
-    int32_t* local = at<int32_t>(ws, L.offs_local);
-    int32_t* offs = at<int32_t>(ws, L.offs);
-    int32_t* tot = at<int32_t>(ws, L.tot);
-    int32_t* list = at<int32_t>(ws, L.list);
-    const int gc = grid_for(2 * n, 1024);
-    k_count<<<gc, kBlock, 0, st>>>(users, items, n, s.num_users, s.num_items, cnt, heavy_n, err);
-    const int nscan = (int)((r1 + kScanBlock - 1) / kScanBlock);
-    k_scan_local<<<nscan, kBlock, 0, st>>>(cnt, r1, local, tot);
-    const int gf = grid_for(2 * n > r1 ? 2 * n : r1, 1024);
-    k_fill<<<gf, kBlock, (size_t)nscan * 4, st>>>(users, items, n, s.num_users, s.num_items, cnt, local, tot, nscan,
-                                                  r1, offs, list);
-    const int nwords = (int)((2 * n + 31) / 32);
+static hipError_t set_sort_lds(int nwords) {
     static bool lds_cfg = false;
     if (!lds_cfg && (size_t)nwords * 4 > 65536) {
         hipError_t e = hipFuncSetAttribute((const void*)k_sort, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -212,8 +279,54 @@ hipError_t launch_index_build(const ncf_shape_t& s, const WsLayout& L, void* ws,
         if (e != hipSuccess) return e;
         lds_cfg = true;
     }
-    k_sort<<<(unsigned)((R + kBlock - 1) / kBlock), kBlock, (size_t)nwords * 4, st>>>(offs, R, list, nwords);
+    return hipSuccess;
+}
+
+// count -> scan -> fill -> sort over K keys for m contributions.
+template <int MODE, bool UNIQ>
+static hipError_t build(const WsLayout& L, void* ws, const KeySrc& ks, int64_t m, int64_t K, PlanOut po,
+                        int nwords, hipStream_t st) {
+    const int64_t r1 = K + 1;
+    int32_t* cnt = at<int32_t>(ws, L.cnt);
+    int32_t* local = at<int32_t>(ws, L.offs_local);
+    int32_t* offs = at<int32_t>(ws, L.offs);
+    int32_t* tot = at<int32_t>(ws, L.tot);
+    int32_t* list = at<int32_t>(ws, L.list);
+    const int nscan = (int)((r1 + kScanBlock - 1) / kScanBlock);
+    if (m > 0)
+        k_count<MODE><<<grid_for(m, 1024), kBlock, 0, st>>>(ks, m, cnt, at<int32_t>(ws, L.heavy_n),
+                                                            at<int32_t>(ws, L.err));
+    k_scan_local<UNIQ><<<nscan, kBlock, 0, st>>>(cnt, r1, local, tot, UNIQ ? at<int32_t>(ws, L.uloc) : nullptr,
+                                                 UNIQ ? at<int32_t>(ws, L.utot) : nullptr);
+    const size_t pre_bytes = (size_t)nscan * 4 * (UNIQ ? 2 : 1);
+    k_fill<MODE, UNIQ><<<grid_for(m > r1 ? m : r1, 1024), kBlock, pre_bytes, st>>>(ks, m, cnt, local, tot, nscan, r1,
+                                                                                   offs, list, po);
+    if (hipError_t e = set_sort_lds(nwords)) return e;
+    k_sort<<<(unsigned)((K + kBlock - 1) / kBlock), kBlock, (size_t)nwords * 4, st>>>(offs, K, list, nwords);
     return hipGetLastError();
+}
+
+hipError_t launch_index_build(const ncf_shape_t& s, const WsLayout& L, void* ws, const int32_t* users,
+                              const int32_t* items, int64_t n, hipStream_t st) {
+    KeySrc ks{users, items, nullptr, s.num_users, s.num_items, 1, 0};
+    return build<kKeyPair, false>(L, ws, ks, 2 * n, s.num_rows, PlanOut{}, (int)((2 * n + 31) / 32), st);
+}
+
+hipError_t launch_shard_plan(const ncf_shape_t& s, const WsLayout& L, void* ws, const int32_t* users,
+                             const int32_t* items, int64_t n, int32_t* uniq_rows, int32_t* send_counts,
+                             hipStream_t st) {
+    KeySrc ks{users, items, nullptr, s.num_users, s.num_items, L.world, (int32_t)L.shard_rows};
+    PlanOut po{at<int32_t>(ws, L.uloc), at<int32_t>(ws, L.utot), uniq_rows, send_counts, at<int32_t>(ws, L.cid_u),
+               at<int32_t>(ws, L.cid_i), at<int32_t>(ws, L.uoffs), at<int32_t>(ws, L.nuniq)};
+    return build<kKeyPairPerm, true>(L, ws, ks, 2 * n, L.keys, po, (int)((2 * n + 31) / 32), st);
+}
+
+hipError_t launch_owner_index(const WsLayout& L, void* ws, const int32_t* keys, int64_t m, hipStream_t st) {
+    KeySrc ks{nullptr, nullptr, keys, 0, 0, L.world, (int32_t)L.shard_rows};
+    // every source sends a row at most once: a key has <= world entries, so keys longer than
+    // kSmallSeg (bitmap sort over m ids) exist only for world > kSmallSeg
+    const int nwords = L.world > kSmallSeg ? (int)((m + 31) / 32) : 0;
+    return build<kKeyList, false>(L, ws, ks, m, L.shard_rows, PlanOut{}, nwords, st);
 }
 
 }  // namespace ncf

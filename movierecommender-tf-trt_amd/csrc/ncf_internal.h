@@ -31,11 +31,10 @@ struct WsLayout {
     size_t persistent_end;
     size_t probs;     // float[B]
     size_t gs;        // float[2B * W] per-contribution gradient rows
-    size_t list;      // int32[2B]   contributions grouped by table row (sorted inside a row)
+    size_t list;      // int32[list_cap] contributions grouped by key (sorted inside a key)
     size_t offs_local;// int32[R+1]  per-2048-row local exclusive scan
     size_t offs;      // int32[R+1]  row -> first list slot
     size_t tot;       // int32[nscan]
-    size_t heavy;     // int32[2B]
     size_t part_bce;  // float[kMaxSlabs]
     size_t part_hit;  // float[nmetric]
     size_t part_dcg;  // float[nmetric]
@@ -44,6 +43,13 @@ struct WsLayout {
     size_t slabs;     // float[kMaxSlabs * P]
     size_t mlp_grad;  // float[P] (reduced dense-layer gradient, single-device path)
     size_t slab_part; // float[kSlabSplit * P] first-level slab sums
+    // row-sharded plan (world > 0 only; else empty): unique table rows of the batch
+    size_t uloc;      // int32[K+1]  per-2048-key local exclusive scan of (cnt > 0)
+    size_t utot;      // int32[nscan]
+    size_t cid_u;     // int32[B]    compact (unique-row) id of each sample's user row
+    size_t cid_i;     // int32[B]    compact id of each sample's item row
+    size_t uoffs;     // int32[2B+1] compact row -> first list slot
+    size_t nuniq;     // int32       number of unique rows
     size_t act;       // float[B * A] generic kernel activations
     size_t dz;        // float[B * D] generic kernel pre-activation gradients
     size_t total;
@@ -52,9 +58,27 @@ struct WsLayout {
     int nmetric;      // max blocks of the metrics kernel
     int act_w;        // A
     int dz_w;         // D
+    int world;        // 0: single table; > 0: row-sharded plan layout for this many ranks
+    int64_t shard_rows;  // S = ceil(R / world) (R when world == 0)
+    int64_t keys;     // key space of the index: world * S (R when world == 0)
+    int64_t list_cap; // contribution capacity of list (2B, or world * min(2B, S) for the owner index)
 };
 
-WsLayout make_layout(const ncf_shape_t& s, int64_t max_batch);
+// world == 0: single-table layout; world >= 1: row-sharded layout (ncf_shard_*)
+WsLayout make_layout(const ncf_shape_t& s, int64_t max_batch, int world = 0);
+
+// Table row numbering of the row-sharded layout: global row g (users 0..U-1,
+// items U..U+I-1) is owned by rank g % world at local row g / world.  The plan's index keys
+// rows by owner first: key = (g % world) * S + g / world.
+inline int64_t shard_rows_of(int64_t R, int world) { return world > 0 ? (R + world - 1) / world : R; }
+
+// Which ids a forward/backward kernel reads: table rows (user u -> row u, item v -> row
+// ibase + v, bounds ubound/ibound), or the compact unique-row ids of a row-sharded plan.
+struct IdSpace {
+    int ubound, ibound, ibase;
+};
+inline IdSpace table_ids(const ncf_shape_t& s) { return IdSpace{s.num_users, s.num_items, s.num_users}; }
+inline IdSpace compact_ids(int64_t n) { return IdSpace{(int)(2 * n), (int)(2 * n), 0}; }
 
 template <typename T>
 __host__ __device__ inline T* at(void* base, size_t off) {
@@ -66,24 +90,37 @@ __host__ __device__ inline T* at(void* base, size_t off) {
 // index build: contribution c = 2*i + side (0 user row, 1 item row) grouped by table row
 hipError_t launch_index_build(const ncf_shape_t& s, const WsLayout& L, void* ws, const int32_t* users,
                               const int32_t* items, int64_t n, hipStream_t st);
+// row-sharded plan: index over owner-major keys + unique-row compaction (uniq_rows = local row
+// ids grouped by owner, send_counts[world], cid_u/cid_i/uoffs/nuniq in the workspace)
+hipError_t launch_shard_plan(const ncf_shape_t& s, const WsLayout& L, void* ws, const int32_t* users,
+                             const int32_t* items, int64_t n, int32_t* uniq_rows, int32_t* send_counts,
+                             hipStream_t st);
+// owner index: m received local row ids keys[j] grouped by row (ascending j), S = L.shard_rows keys
+hipError_t launch_owner_index(const WsLayout& L, void* ws, const int32_t* keys, int64_t m, hipStream_t st);
+// compact gradient: out[u] = sum over the plan's contributions of unique row u (ascending c)
+hipError_t launch_uniq_grad(const ncf_shape_t& s, const WsLayout& L, void* ws, int64_t n, float* out,
+                            hipStream_t st);
+hipError_t launch_gather_rows(const ncf_shape_t& s, const float* table, int64_t table_rows, const int32_t* rows,
+                              int64_t m, float* out, hipStream_t st);
 
 // forward+backward, generic per-sample kernel: writes probs, gs rows, bce partials, dense slabs.
 // returns number of slabs written in *nslab, bce partial count in *nbce
 hipError_t launch_fb_generic(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb,
                              const float* mlp, const int32_t* users, const int32_t* items,
-                             const float* labels, int64_t n, float inv_batch, int* nslab, int* nbce,
+                             const float* labels, int64_t n, float inv_batch, IdSpace ids, int* nslab, int* nbce,
                              hipStream_t st);
 // forward only; with labels also writes per-block BCE partials (*nbce of them)
 hipError_t launch_predict_generic(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb,
                                   const float* mlp, const int32_t* users, const int32_t* items,
-                                  const float* labels, int64_t n, float* probs, int* nbce, hipStream_t st);
+                                  const float* labels, int64_t n, float* probs, IdSpace ids, int* nbce,
+                                  hipStream_t st);
 
 // fused MFMA forward+backward (shapes with s.fast_path); same outputs as the generic kernel
 // also computes the hr/dcg group metrics in-kernel when group divides 32 (*nmet = partial count, else 0)
 hipError_t launch_fb_fused(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb,
                            const float* mlp, const int32_t* users, const int32_t* items, const float* labels,
-                           int64_t n, float inv_batch, int group, int topk, int* nslab, int* nbce, int* nmet,
-                           hipStream_t st);
+                           int64_t n, float inv_batch, IdSpace ids, int group, int topk, int* nslab, int* nbce,
+                           int* nmet, hipStream_t st);
 bool fused_supported(const ncf_shape_t& s);
 
 // metrics / summaries
@@ -96,9 +133,11 @@ hipError_t launch_summary(const WsLayout& L, void* ws, int nbce, int nmet, float
 
 // updates
 enum GradSource { kGradSparse = 0, kGradDense = 1 };
+// sparse mode (dense_grad == nullptr): per-row sums of gs rows (nullptr: the workspace's
+// per-contribution rows) through the workspace index
 hipError_t launch_emb_update(const ncf_shape_t& s, const WsLayout& L, void* ws, float* emb, float* m, float* v,
                              const int32_t* step, const ncf_hyper_t& h, const float* dense_grad, int64_t rows,
-                             hipStream_t st);
+                             hipStream_t st, const float* gs = nullptr);
 hipError_t launch_emb_grad_dense(const ncf_shape_t& s, const WsLayout& L, void* ws, float* out, hipStream_t st);
 // mlp: reduce slabs (if nslab > 0) or read grad_in; optionally write grad_out; optionally update
 hipError_t launch_mlp_update(const ncf_shape_t& s, const WsLayout& L, void* ws, float* mlp, float* m, float* v,

@@ -108,6 +108,36 @@ __global__ __launch_bounds__(kBlock) void k_emb_grad_dense(float4* __restrict__ 
     }
 }
 
+// Compact gradient of a row-sharded plan: out[u] = sum of unique row u's contributions
+// (ascending c through the plan's sorted list); nuniq is read on the device.
+__global__ __launch_bounds__(kBlock) void k_uniq_grad(float4* __restrict__ out, const int32_t* __restrict__ nuniq,
+                                                      uint32_t w4, const int32_t* __restrict__ uoffs,
+                                                      const int32_t* __restrict__ list,
+                                                      const float4* __restrict__ gs) {
+    const uint32_t n4 = (uint32_t)*nuniq * w4;
+    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n4; e += gridDim.x * blockDim.x) {
+        const uint32_t u = e / w4;
+        const uint32_t q = e - u * w4;
+        const int o = uoffs[u];
+        const int c = uoffs[u + 1] - o;
+        float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int j = 0; j < c; ++j) g = f4add(g, gs[(size_t)list[o + j] * w4 + q]);
+        out[e] = g;
+    }
+}
+
+// out[j] = table[rows[j]] (rows outside [0, nrows) give zero rows)
+__global__ __launch_bounds__(kBlock) void k_gather_rows(float4* __restrict__ out, const float4* __restrict__ table,
+                                                        int64_t nrows, const int32_t* __restrict__ rows, uint32_t n4,
+                                                        uint32_t w4) {
+    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n4; e += gridDim.x * blockDim.x) {
+        const uint32_t j = e / w4;
+        const uint32_t q = e - j * w4;
+        const int r = rows[j];
+        out[e] = (r >= 0 && r < nrows) ? table[(size_t)r * w4 + q] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+}
+
 // First level of the slab reduction: group c sums slabs [c*per, (c+1)*per) in order.
 __global__ __launch_bounds__(kBlock) void k_slab_partial(const float* __restrict__ slabs, int P, int nslab, int per,
                                                          float* __restrict__ part) {
@@ -312,12 +342,12 @@ static L2Table make_l2_table(const ncf_shape_t& s, const ncf_hyper_t& h) {
 
 hipError_t launch_emb_update(const ncf_shape_t& s, const WsLayout& L, void* ws, float* emb, float* m, float* v,
                              const int32_t* step, const ncf_hyper_t& h, const float* dense_grad, int64_t rows,
-                             hipStream_t st) {
+                             hipStream_t st, const float* gs_rows) {
     const uint32_t w4 = (uint32_t)(s.row_width / 4);
     const uint32_t n4 = (uint32_t)(rows * w4);
     const int32_t* offs = at<int32_t>(ws, L.offs);
     const int32_t* list = at<int32_t>(ws, L.list);
-    const float4* gs = at<const float4>(ws, L.gs);
+    const float4* gs = gs_rows ? (const float4*)gs_rows : at<const float4>(ws, L.gs);
     float* part = at<float>(ws, L.part_reg);
     const bool l2 = h.l2[0] != 0.0f;
     const int src = dense_grad ? kGradDense : kGradSparse;
@@ -342,6 +372,27 @@ hipError_t launch_emb_grad_dense(const ncf_shape_t& s, const WsLayout& L, void* 
     const uint32_t n4 = (uint32_t)(s.num_rows * w4);
     k_emb_grad_dense<<<kUpdateGrid, kBlock, 0, st>>>((float4*)out, n4, w4, at<int32_t>(ws, L.offs),
                                                      at<int32_t>(ws, L.list), at<const float4>(ws, L.gs));
+    return hipGetLastError();
+}
+
+hipError_t launch_uniq_grad(const ncf_shape_t& s, const WsLayout& L, void* ws, int64_t n, float* out,
+                            hipStream_t st) {
+    const uint32_t w4 = (uint32_t)(s.row_width / 4);
+    int64_t g = (2 * n * w4 + kBlock - 1) / kBlock;
+    if (g > kUpdateGrid) g = kUpdateGrid;
+    k_uniq_grad<<<(unsigned)g, kBlock, 0, st>>>((float4*)out, at<int32_t>(ws, L.nuniq), w4, at<int32_t>(ws, L.uoffs),
+                                                at<int32_t>(ws, L.list), at<const float4>(ws, L.gs));
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_rows(const ncf_shape_t& s, const float* table, int64_t table_rows, const int32_t* rows,
+                              int64_t m, float* out, hipStream_t st) {
+    if (m <= 0) return hipSuccess;
+    const uint32_t w4 = (uint32_t)(s.row_width / 4);
+    int64_t g = (m * w4 + kBlock - 1) / kBlock;
+    if (g > kUpdateGrid) g = kUpdateGrid;
+    k_gather_rows<<<(unsigned)g, kBlock, 0, st>>>((float4*)out, (const float4*)table, table_rows, rows,
+                                                  (uint32_t)(m * w4), w4);
     return hipGetLastError();
 }
 

@@ -74,6 +74,16 @@ _SIGNATURES = {
                                             _vp, _vp, _i64, _i64, _i32, _vp, ctypes.c_size_t, _vp]),
     "ncf_apply_update": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _i64, _i64, _vp, _vp,
                                         _vp, _vp, _vp, ctypes.c_size_t, _vp]),
+    "ncf_shard_rows": (ctypes.c_int, [_P(NcfShape), _i32, _P(_i64)]),
+    "ncf_shard_workspace_size": (ctypes.c_int, [_P(NcfShape), _i64, _i32, _P(ctypes.c_size_t)]),
+    "ncf_shard_workspace_init": (ctypes.c_int, [_P(NcfShape), _i64, _i32, _vp, ctypes.c_size_t, _vp]),
+    "ncf_shard_plan": (ctypes.c_int, [_P(NcfShape), _i32, _vp, _vp, _i64, _vp, _vp, _vp, ctypes.c_size_t, _vp]),
+    "ncf_gather_rows": (ctypes.c_int, [_P(NcfShape), _vp, _i64, _vp, _i64, _vp, _vp]),
+    "ncf_shard_forward_backward": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfHyper), _i32, _vp, _i64, _vp,
+                                                  _vp, _vp, _vp, _vp, _i64, _i32, _vp, ctypes.c_size_t, _vp]),
+    "ncf_shard_apply_update": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _i32, _vp,
+                                              _vp, _i64, _vp, _vp, _vp, _vp, ctypes.c_size_t, _vp]),
+    "ncf_shard_predict": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _i32, _i64, _vp, _vp, ctypes.c_size_t, _vp]),
     "ncf_profile_enable": (ctypes.c_int, [_i32, _i32]),
     "ncf_profile_read": (ctypes.c_int, [_i32, _P(ctypes.c_double), _P(_i64)]),
 }

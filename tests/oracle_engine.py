@@ -89,3 +89,113 @@ class OracleEngine(object):
         p = self.emb[r0:r0 + rc]
         self._adam(p, eg[:rc] + 2.0 * self.l2[0] * p, self.emb_m[:rc], self.emb_v[:rc])
         self._adam(self.mlp, grads[1] + 2.0 * self.mlp_lam * self.mlp, self.mlp_m, self.mlp_v)
+
+
+class OracleShardedEngine(object):
+    """CPU look-alike of movierec.sharded.ShardedNCFEngine (float64, oracle arithmetic): the
+    same plan / gather_rows / forward_backward / apply_update surface and buffers, so that
+    RowShardedDataParallel's exchanges can be tested with gloo on CPU."""
+
+    def __init__(self, shape, w, world, rank, lr=0.001, beta_1=0.9, beta_2=0.999, layers_l2reg=None):
+        self.shape = shape
+        self.world, self.rank = int(world), int(rank)
+        self.layout = Layout(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim)
+        self.num_rows = self.layout.num_rows
+        self.row_width = self.layout.row_width
+        self.shard_rows = -(-self.num_rows // self.world)
+        emb, flat = self.layout.to_device(w, dtype=np.float64)
+        g = self.owned_rows()
+        shard = np.zeros((self.shard_rows, self.row_width))
+        shard[g >= 0] = emb[g[g >= 0]]
+        self.emb = torch.from_numpy(shard)
+        self.mlp = torch.from_numpy(flat)
+        self.emb_m = torch.zeros_like(self.emb)
+        self.emb_v = torch.zeros_like(self.emb)
+        self.mlp_m = torch.zeros_like(self.mlp)
+        self.mlp_v = torch.zeros_like(self.mlp)
+        P = self.layout.mlp_params
+        self.dense_buf = torch.zeros(P + 8, dtype=torch.float64)
+        self.mlp_grad = self.dense_buf[:P]
+        self.summary = self.dense_buf[P:]
+        self.send_counts = torch.zeros(self.world, dtype=torch.int32)
+        self.t = 0
+        self.lr, self.b1, self.b2 = lr, beta_1, beta_2
+        self.l2 = list(layers_l2reg or [0.0] * len(shape.layers))
+        lam = np.zeros(P)
+        off = 0
+        for l in range(1, len(shape.layers)):
+            a, b = shape.layers[l - 1], shape.layers[l]
+            lam[off:off + a * b] = self.l2[l]
+            off += a * b + b
+        self.mlp_lam = torch.from_numpy(lam)
+
+    def owned_rows(self):
+        g = np.arange(self.shard_rows, dtype=np.int64) * self.world + self.rank
+        g[g >= self.num_rows] = -1
+        return g
+
+    def plan(self, users, items):
+        u = np.asarray(users, dtype=np.int64)
+        v = np.asarray(items, dtype=np.int64)
+        rows = np.stack([u, self.shape.num_users + v], 1).reshape(-1)   # c = 2i + side
+        keys = (rows % self.world) * self.shard_rows + rows // self.world
+        ukeys = np.unique(keys)
+        self._users, self._items = u, v
+        self._ukeys = ukeys
+        self.send_counts = torch.from_numpy(np.bincount(ukeys // self.shard_rows, minlength=self.world)
+                                            .astype(np.int32))
+        n2 = rows.size
+        cap = self.world * min(n2, self.shard_rows)
+        self.uniq = torch.from_numpy((ukeys % self.shard_rows).astype(np.int32))
+        self.uniq_vals = torch.zeros(ukeys.size, self.row_width, dtype=torch.float64)
+        self.uniq_grad = torch.zeros(ukeys.size, self.row_width, dtype=torch.float64)
+        self.recv_rows = torch.zeros(cap, dtype=torch.int32)
+        self.recv_vals = torch.zeros(cap, self.row_width, dtype=torch.float64)
+        self.recv_grad = torch.zeros(cap, self.row_width, dtype=torch.float64)
+        return self.uniq, self.send_counts
+
+    def gather_rows(self, rows, m):
+        self.recv_vals[:m] = self.emb[rows[:m].long()]
+        return self.recv_vals[:m]
+
+    def _global_of_uniq(self):
+        owner = self._ukeys // self.shard_rows
+        local = self._ukeys % self.shard_rows
+        return local * self.world + owner
+
+    def forward_backward(self, labels, group, k, inv_batch, include_dense_reg=True, probs_out=None):
+        g = self._global_of_uniq()
+        full = np.zeros((self.num_rows, self.row_width))
+        full[g] = self.uniq_vals.numpy()
+        w = self.layout.from_device(full, self.mlp.numpy())
+        zero_l2 = [0.0] * len(self.shape.layers)
+        _, grads, p = O.loss_and_grads(self.shape, w, self._users, self._items, labels, zero_l2,
+                                       batch_norm=1.0 / inv_batch)
+        eg, mg = self.layout.to_device(grads, dtype=np.float64)
+        self.uniq_grad[:] = torch.from_numpy(eg[g])
+        self.mlp_grad[:] = torch.from_numpy(mg)
+        y = np.asarray(labels, dtype=np.float64)
+        ng = len(y) // group
+        hr, dcg = O.group_metrics(p, y, group, k)
+        reg = self.l2[0] * float((self.emb ** 2).sum())
+        if include_dense_reg:
+            reg += float((self.mlp_lam * self.mlp ** 2).sum())
+        sm = self.summary
+        sm.zero_()
+        sm[0] = float(O.bce_per_sample(p, y).sum())
+        sm[1], sm[2], sm[3], sm[4] = hr * ng, dcg * ng, ng, reg
+
+    def _adam(self, p, g, m, v):
+        m.mul_(self.b1).add_((1 - self.b1) * g)
+        v.mul_(self.b2).add_((1 - self.b2) * g * g)
+        lr_t = O.adam_lr_t(self.lr, self.b1, self.b2, self.t)
+        p.sub_(lr_t * m / (v.sqrt() + O.KERAS_EPSILON))
+
+    def apply_update(self, recv_rows, recv_grad, m, inv_batch):
+        self.t += 1
+        G = torch.zeros_like(self.emb)
+        rows = recv_rows[:m].long()
+        for j in range(int(m)):                    # ascending source order
+            G[rows[j]] += recv_grad[j]
+        self._adam(self.emb, G + 2.0 * self.l2[0] * self.emb, self.emb_m, self.emb_v)
+        self._adam(self.mlp, self.mlp_grad + 2.0 * self.mlp_lam * self.mlp, self.mlp_m, self.mlp_v)

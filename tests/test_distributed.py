@@ -1,13 +1,15 @@
-"""Data-parallel orchestration (movierec.distributed) with world_size 2.
+"""Data-parallel orchestration (movierec.distributed) with world_size 2 and 3.
 
-CPU part (gloo, no GPU): ranks drive the oracle-backed OracleEngine through
-ReplicatedDataParallel; after several steps every replica must equal a
-single-process run on the concatenated global batch (float64, so only the
-cross-rank summation order differs).
+CPU part (gloo, no GPU): ranks drive the oracle-backed OracleEngine /
+OracleShardedEngine through ReplicatedDataParallel / RowShardedDataParallel;
+after several steps every rank's weights must equal a single-process run on the
+concatenated global batch (float64, so only the cross-rank summation order
+differs).
 
-GPU part (-m gpu): two processes share the one GPU of the box with the gloo
-backend and drive the real HIP library (NCFEngine); compared against a
-single-process NCFEngine run on the global batch at the fp32 tolerance.
+GPU part (-m gpu): processes share the one GPU of the box with the gloo backend
+and drive the real HIP library (NCFEngine / ShardedNCFEngine); compared against
+a single-process NCFEngine run on the global batch at the fp32 tolerance.  The
+row-sharded path with world 1 must be bitwise identical to ncf_train_step.
 """
 
 import os
@@ -111,6 +113,70 @@ def test_replicated_dp_matches_single_process_cpu():
             np.testing.assert_allclose(a[:5], b[:5], rtol=1e-6, atol=1e-9)
 
 
+def _cpu_sharded_worker(rank, world, port, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [here, os.path.dirname(here), os.path.join(os.path.dirname(here), "movierecommender-tf-trt_amd")]
+    from oracle_engine import OracleShardedEngine
+    from movierec.distributed import RowShardedDataParallel
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    shape, w = _weights()
+    eng = OracleShardedEngine(shape, w, world, rank, layers_l2reg=L2)
+    dp = RowShardedDataParallel(eng)
+    summaries, probs = [], []
+    per = B // world
+    for users, items, y in _batches():
+        sl = slice(rank * per, (rank + 1) * per)
+        dp.train_step(users[sl], items[sl], y[sl], group=GROUP, k=2, global_batch=B)
+        summaries.append(eng.summary.clone().numpy())
+    full = dp.full_table().numpy().copy()
+    q.put((rank, full, eng.mlp.numpy().copy(), summaries))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _run_cpu(worker, world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, emb, mlp, summ = q.get(timeout=120)
+        res[r] = (emb, mlp, summ)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_row_sharded_dp_matches_single_process_cpu(world):
+    """Row-sharded exchanges (plan, all_to_all of ids/rows/grads, owner update) reproduce the
+    single-process step; world 3 leaves padding rows in the last shard (40 rows)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from oracle_engine import OracleEngine
+    assert B % (world * GROUP) == 0
+    res = _run_cpu(_cpu_sharded_worker, world)
+    shape, w = _weights()
+    ref = OracleEngine(shape, w, layers_l2reg=L2)
+    grads = ref.alloc_grads()
+    ref_summ = []
+    for users, items, y in _batches():
+        ref.forward_backward(users, items, y, group=GROUP, k=2, inv_batch=1.0 / B, grads=grads)
+        ref_summ.append(grads[2].clone().numpy())
+        ref.apply_update(grads, 1.0 / B)
+    for r in range(world):
+        emb, mlp, summ = res[r]
+        np.testing.assert_allclose(emb, ref.emb[:ref.num_rows].numpy(), rtol=0, atol=1e-12)
+        np.testing.assert_allclose(mlp, ref.mlp.numpy(), rtol=0, atol=1e-12)
+        for a, b in zip(summ, ref_summ):
+            np.testing.assert_allclose(a[:5], b[:5], rtol=1e-6, atol=1e-9)
+
+
 # ---------------------------------------------------------------- GPU (HIP)
 
 def _gpu_worker(rank, world, port, q):
@@ -166,4 +232,76 @@ def test_replicated_dp_matches_single_process_gpu():
             np.testing.assert_allclose(wts[name], rw[name], rtol=0, atol=1e-5, err_msg=name)
         assert st["loss"] == pytest.approx(rst["loss"], rel=1e-5)
         assert st["hr"] == pytest.approx(rst["hr"], abs=1e-6)
+    assert gpu_available()
+
+
+def _gpu_sharded_worker(rank, world, port, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [here, os.path.dirname(here), os.path.join(os.path.dirname(here), "movierecommender-tf-trt_amd")]
+    from movierec.sharded import ShardedNCFEngine
+    from movierec.distributed import RowShardedDataParallel
+    from movierec.engine import NCFEngine
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    shape, w = _weights()
+    eng = ShardedNCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, world=world, rank=rank,
+                           max_batch=B, layers_l2reg=L2)
+    eng.set_keras_weights(w)
+    dp = RowShardedDataParallel(eng)
+    per = B // world
+    probs = []
+    for users, items, y in _batches():
+        sl = slice(rank * per, (rank + 1) * per)
+        dp.train_step(users[sl], items[sl], y[sl], group=GROUP, k=2, global_batch=B)
+        probs.append(dp.predict(users[sl], items[sl]).cpu().numpy())
+    torch.cuda.synchronize()
+    q.put((rank, dp.keras_weights(), NCFEngine.read_stats(eng.stats), probs))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _gpu_reference():
+    from movierec.engine import NCFEngine
+    shape, w = _weights()
+    ref = NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=B, layers_l2reg=L2)
+    ref.set_keras_weights(w)
+    probs = []
+    for users, items, y in _batches():
+        ref.train_step(users, items, y, group=GROUP, k=2)
+        probs.append(ref.predict(users, items).cpu().numpy())
+    return ref.keras_weights(), NCFEngine.read_stats(ref.stats), probs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [1, 2])
+def test_row_sharded_dp_matches_single_process_gpu(world):
+    """HIP row-sharded path (gloo between processes sharing the GPU) vs ncf_train_step on the
+    global batch: bitwise at world 1, fp32 tolerance at world 2."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_sharded_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, wts, st, pr = q.get(timeout=300)
+        res[r] = (wts, st, pr)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    rw, rst, rprobs = _gpu_reference()
+    per = B // world
+    for r in range(world):
+        wts, st, pr = res[r]
+        for name in rw:
+            if world == 1:
+                np.testing.assert_array_equal(wts[name], rw[name], err_msg=name)
+            else:
+                np.testing.assert_allclose(wts[name], rw[name], rtol=0, atol=1e-5, err_msg=name)
+        assert st["loss"] == pytest.approx(rst["loss"], rel=1e-5)
+        assert st["hr"] == pytest.approx(rst["hr"], abs=1e-6)
+        for a, b in zip(pr, rprobs):
+            np.testing.assert_allclose(a, b[r * per:(r + 1) * per], rtol=0, atol=2e-6)
     assert gpu_available()
