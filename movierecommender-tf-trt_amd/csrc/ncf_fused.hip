@@ -75,10 +75,27 @@ struct FShape {
     static constexpr int NS1 = nsteps(L1), NS2 = nsteps(L2), NS3 = nsteps(L3);
     static constexpr int NDW1 = NT0 * NT1, NDW2 = NT1 * NT2, NDW3 = NT2 * NT3, NDW = NDW1 + NDW2 + NDW3;
     static constexpr int MAXT = cdiv(NDW, 4);
+    // weight-gradient tile t (0..NDW-1, dW1 tiles t = ti*NT1 + to first) of slot m of wave w:
+    // when the dW1 tiles split evenly into per-wave input-feature groups (NT0 % 4 == 0), wave w
+    // takes the NT1 output tiles of groups ti = w, w+4, ... back to back (the second chain
+    // re-reads the gathered rows the first one just pulled into L2), then dW2/dW3 tiles go to
+    // waves 3, 2, 1, 0, ...; otherwise round-robin t = w + 4m.  -1: no tile.
+    static constexpr int NSLOT1 = (NT0 % 4 == 0) ? (NT0 / 4) * NT1 : 0;
+    __device__ static constexpr int dw_tile(int w, int m) {
+        if (NSLOT1 == 0) return w + 4 * m < NDW ? w + 4 * m : -1;
+        if (m < NSLOT1) return (w + 4 * (m / NT1)) * NT1 + m % NT1;
+        const int u = 4 * (m - NSLOT1) + (3 - w);
+        return u < NDW - NDW1 ? NDW1 + u : -1;
+    }
     static constexpr int GH = G / 2;                     // GMF features per lane half
     static constexpr int GCH = GH >= 16 ? 16 : GH;       // reduction chunk (bounds register pressure)
     static constexpr int NGC = GH >= 16 ? GH / 16 : (GH > 0 ? 1 : 0);
     static constexpr int XCH = G + L3 + 4;               // per-wave exchange floats
+    // end-of-tile transpose images in a wave's staging block: [32 samples][2G] and [32][L0],
+    // rows padded by 4 floats (16-byte aligned, conflict-free ds_write_b128)
+    static constexpr int P1 = 2 * G + 4, P2 = L0 + 4;
+    static_assert(32 * P1 + 3 <= RB * LS && 32 * P2 + 3 <= RB * LS, "transpose image must fit the staging block");
+    static_assert(G % 4 == 0 && D0 % 4 == 0, "float4 row pieces");
     static constexpr size_t LDS_BYTES = (size_t)(4 * RB * LS + WLDS) * 4 + 256 * 4 + (size_t)4 * XCH * 4;
     static_assert(LDS_BYTES <= 163840, "LDS budget");
 };
@@ -95,8 +112,12 @@ __device__ __forceinline__ float half_transpose_reduce(float* x, int lane) {
         const bool hi = (lane & m) != 0;
 #pragma unroll
         for (int v = 0; v < c / 2; ++v) {
-            const float send = hi ? x[v] : x[v + c / 2];
-            const float keep = hi ? x[v + c / 2] : x[v];
+            // opaque copies: selecting between two array elements would otherwise be folded into
+            // one lane-dependent index into x[] (a c-way v_cndmask chain per element)
+            float a = x[v], b = x[v + c / 2];
+            asm volatile("" : "+v"(a), "+v"(b));
+            const float send = hi ? a : b;
+            const float keep = hi ? b : a;
             x[v] = keep + __shfl_xor(send, m, 64);
         }
     }
@@ -106,6 +127,9 @@ __device__ __forceinline__ float half_transpose_reduce(float* x, int lane) {
     return r;
 }
 
+#ifndef NCF_DW1_SHARED
+#define NCF_DW1_SHARED 1
+#endif
 #ifndef NCF_DW1_CH
 #define NCF_DW1_CH 8
 #endif
@@ -167,6 +191,19 @@ __device__ __forceinline__ f32x16 mchain2(f32x16 acc, FA fa, FB fb) {
     return acc;
 }
 
+// Phase timestamps of waves 0 and 3 (lane 0) for the first two tiles of every workgroup:
+// a profiling build (-DNCF_FUSED_TIMING) only; read with ncf_debug_fused_timing.
+#ifdef NCF_FUSED_TIMING
+__device__ unsigned long long g_fused_t[256 * 2 * 2 * 16];
+#define NCF_T(ph)                                                                                    \
+    do {                                                                                             \
+        if (lane == 0 && (w == 0 || w == 3) && blockIdx.x < 256 && itl < 2)                          \
+            g_fused_t[((blockIdx.x * 2 + itl) * 2 + (w == 3)) * 16 + (ph)] = __builtin_readcyclecounter(); \
+    } while (0)
+#else
+#define NCF_T(ph) ((void)0)
+#endif
+
 template <class S>
 __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict__ emb, const float* __restrict__ mlp,
                                                         const int32_t* __restrict__ users,
@@ -208,16 +245,58 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
     __syncthreads();
 
     const int64_t niter = (n + 127) / 128;
+    // ---- a tile's ids and rows are requested at the end of the previous tile (the first one
+    // here), so the HBM gather latency overlaps the previous tile's gradient-row stores
+    constexpr int GQ = S::GH / 4 > 0 ? S::GH / 4 : 1;
+    float4 nxv[D0 / 4], nua[GQ], nia[GQ];
+    int nu = 0, nv = 0;
+    float ny = 0.f;
+    auto issue_ids = [&](int64_t it2) {
+        const int64_t s2 = it2 * 128 + 32 * w + j;
+        nu = 0;
+        nv = 0;
+        ny = 0.f;
+        if (s2 < n) {
+            nu = users[s2];
+            nv = items[s2];
+            ny = labels[s2];
+        }
+    };
+    auto issue_rows = [&](int64_t it2) {
+        const int64_t s2 = it2 * 128 + 32 * w + j;
+        const bool ok2 = s2 < n && (unsigned)nu < (unsigned)ids.ubound && (unsigned)nv < (unsigned)ids.ibound;
+        const float* eu2 = emb + (size_t)(ok2 ? nu : 0) * W;
+        const float* ei2 = emb + (size_t)(ok2 ? ids.ibase + nv : 0) * W;
+        const float4* src = reinterpret_cast<const float4*>((h ? ei2 : eu2) + G);
+#pragma unroll
+        for (int q = 0; q < D0 / 4; ++q) nxv[q] = src[q];
+        if constexpr (G > 0) {
+            const float4* us2 = reinterpret_cast<const float4*>(eu2 + h * S::GH);
+            const float4* is2 = reinterpret_cast<const float4*>(ei2 + h * S::GH);
+#pragma unroll
+            for (int q = 0; q < GQ; ++q) {
+                nua[q] = us2[q];
+                nia[q] = is2[q];
+            }
+        }
+    };
+    if ((int64_t)blockIdx.x < niter) {
+        issue_ids(blockIdx.x);
+        issue_rows(blockIdx.x);
+    }
+    int itl = -1;
     for (int64_t it = blockIdx.x; it < niter; it += gridDim.x) {
+        // lane coordinates re-derived opaquely every tile: keeps the compiler from hoisting the
+        // hundreds of lane-dependent LDS addresses out of the loop (and spilling them)
+        int lane_t = lane;
+        asm volatile("" : "+v"(lane_t));
+        const int j = lane_t & 31, h = lane_t >> 5;
+        ++itl;
+        NCF_T(0);
         const int64_t si = it * 128 + 32 * w + j;
         const bool inb = si < n;
-        int u = 0, v = 0;
-        float y = 0.f;
-        if (inb) {
-            u = users[si];
-            v = items[si];
-            y = labels[si];
-        }
+        const int u = nu, v = nv;
+        const float y = ny;
         // Masked samples read row 0 (a valid address) and get dz = 0: they contribute nothing.
         const bool ok = inb && (unsigned)u < (unsigned)ids.ubound && (unsigned)v < (unsigned)ids.ibound;
         const int urow = ok ? u : 0, irow = ok ? ids.ibase + v : 0;
@@ -228,31 +307,21 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
         const float* eu = emb + (size_t)urow * W;
         const float* ei = emb + (size_t)irow * W;
         float* sb = stg + w * S::RB * LS;  // this wave's staging block
-
-        // ---- bulk gather: this half's MLP vector and both GMF slices, all loads in flight at once
         float4 xv[D0 / 4];
-        {
-            const float4* src = reinterpret_cast<const float4*>((h ? ei : eu) + G);
 #pragma unroll
-            for (int q = 0; q < D0 / 4; ++q) xv[q] = src[q];
-        }
+        for (int q = 0; q < D0 / 4; ++q) xv[q] = nxv[q];
         float zp = 0.f;
         const float4* us = reinterpret_cast<const float4*>(eu + h * S::GH);
         const float4* is = reinterpret_cast<const float4*>(ei + h * S::GH);
         if constexpr (G > 0) {
-            float4 ua[S::GH / 4], ia[S::GH / 4];
-#pragma unroll
-            for (int q = 0; q < S::GH / 4; ++q) {
-                ua[q] = us[q];
-                ia[q] = is[q];
-            }
             const float* wo = wl + S::SWO + h * S::GH;
 #pragma unroll
             for (int q = 0; q < S::GH / 4; ++q)
-                zp += wo[4 * q] * (ua[q].x * ia[q].x) + wo[4 * q + 1] * (ua[q].y * ia[q].y) +
-                      wo[4 * q + 2] * (ua[q].z * ia[q].z) + wo[4 * q + 3] * (ua[q].w * ia[q].w);
+                zp += wo[4 * q] * (nua[q].x * nia[q].x) + wo[4 * q + 1] * (nua[q].y * nia[q].y) +
+                      wo[4 * q + 2] * (nua[q].z * nia[q].z) + wo[4 * q + 3] * (nua[q].w * nia[q].w);
         }
 
+        NCF_T(1);
         // ---- forward chain.  Layer 1: B operand = this half's MLP vector (K order h*D0 + s),
         // A operand = W1[k][out] from LDS, double-buffered 4 steps ahead.  Each activation tile
         // is staged to LDS for the weight-gradient phase as soon as it exists; only its ReLU
@@ -304,6 +373,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
                 }
             }
         }
+        NCF_T(2);
         // GMF slices again for the backward (L2-resident by now; in flight during layers 2-3)
         float4 ua[S::GH / 4 > 0 ? S::GH / 4 : 1], ia[S::GH / 4 > 0 ? S::GH / 4 : 1];
         if constexpr (G > 0) {
@@ -351,6 +421,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
                 h3[to][r] = (f < L3) ? fmaxf(acc[r] + wl[S::SB3 + f], 0.f) : 0.f;
             }
         }
+        NCF_T(3);
         // ---- output, BCE, dz (both halves compute the same sample's values)
 #pragma unroll
         for (int t = 0; t < S::NT3; ++t)
@@ -396,12 +467,11 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
                 acc_dcg += hit * (logf(2.0f) / logf((float)pos + 2.0f));
             }
         }
-        float* gu = gs + (size_t)(2 * si) * W;  // user contribution row
-        float* gi = gu + W;                     // item contribution row
+        NCF_T(4);
 
-        // ---- GMF backward: embedding grads + output-kernel grads (transpose-reduced)
+        // ---- GMF backward: output-kernel grads (transpose-reduced); the embedding-row grads are
+        // formed at the end of the tile
         if constexpr (G > 0) {
-            const float* wo = wl + S::SWO + h * S::GH;
 #pragma unroll
             for (int c = 0; c < S::NGC; ++c) {
                 float contrib[S::GCH];
@@ -413,18 +483,11 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
                     contrib[4 * q + 1] = dz * (a.y * b.y);
                     contrib[4 * q + 2] = dz * (a.z * b.z);
                     contrib[4 * q + 3] = dz * (a.w * b.w);
-                    if (ok) {
-                        const float4 gu4 = make_float4(dz * wo[f] * b.x, dz * wo[f + 1] * b.y, dz * wo[f + 2] * b.z,
-                                                       dz * wo[f + 3] * b.w);
-                        const float4 gi4 = make_float4(dz * wo[f] * a.x, dz * wo[f + 1] * a.y, dz * wo[f + 2] * a.z,
-                                                       dz * wo[f + 3] * a.w);
-                        *reinterpret_cast<float4*>(gu + h * S::GH + f) = gu4;
-                        *reinterpret_cast<float4*>(gi + h * S::GH + f) = gi4;
-                    }
                 }
                 acc_gmf[c] += half_transpose_reduce<S::GCH>(contrib, lane);
             }
         }
+        NCF_T(5);
         // ---- output-kernel grads of the MLP features, and G3
         f32x16 g3[S::NT3];
 #pragma unroll
@@ -460,6 +523,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
                 sb[(S::RG2 + 32 * to + drow(r, h)) * LS + j] = g;
             }
         }
+        NCF_T(6);
         f32x16 g1[S::NT1];
 #pragma unroll
         for (int to = 0; to < S::NT1; ++to) {
@@ -478,36 +542,68 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
                 sb[(S::RG1 + 32 * to + drow(r, h)) * LS + j] = g;
             }
         }
+        NCF_T(7);
+        NCF_T(8);
+        __syncthreads();
+        NCF_T(9);
+
+        // ---- weight gradients: wave w owns tiles dw_tile(w, m) (K = 128 samples, 64 MFMA
+        // steps per tile; both operands double-buffered one chunk ahead)
+#if NCF_DW1_SHARED
+        // the NT1 output tiles of an input-feature group in one chain: each gathered-row value
+        // (the A operand, re-read from L2/HBM) is fetched once for all of them
+        if constexpr (S::NSLOT1 > 0) {
 #pragma unroll
-        for (int to = 0; to < S::NT0; ++to) {
-            const int oc = 32 * to + j;
-            const f32x16 acc = mchain<S::NS1, 4>(
-                f32x16{},
-                [&](int t) {
-                    const int k = 32 * (t / 16) + drow(t % 16, h);
-                    return (oc < L0 && k < L1) ? wl[S::SW1 + oc * S::LW1 + k] : 0.f;
-                },
-                [&](int t) { return g1[t / 16][t % 16]; });
-            if (ok) {
+            for (int g = 0; g < S::NSLOT1 / S::NT1; ++g) {
+                const int ti = w + 4 * g;
+                const int fi = 32 * ti + j;
+                const int side = fi < D0 ? 0 : 128;
+                const int col = G + (fi < D0 ? fi : fi - D0);
+                const bool aok = fi < L0;
+                auto lda = [&](int tt) {
+                    const int row = srow[side + 32 * (tt >> 4) + 2 * (tt & 15) + h];
+                    return (aok && row >= 0) ? emb[(size_t)row * W + col] : 0.f;
+                };
+                auto ldb = [&](int tt, int o) {
+                    const int fo = 32 * o + j;
+                    return fo < L1 ? stg[(tt >> 4) * S::RB * LS + (S::RG1 + fo) * LS + 2 * (tt & 15) + h] : 0.f;
+                };
+                constexpr int CH = NCF_DW1_CH;
+                float ab[2][CH], bb[2][CH][S::NT1];
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int f = 32 * to + 8 * q + 4 * h;  // rows drow(4q..4q+3, h) are f..f+3
-                    if (f < L0) {
-                        float* dst = (f < D0) ? gu + G + f : gi + G + (f - D0);
-                        *reinterpret_cast<float4*>(dst) =
-                            make_float4(acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]);
+                for (int e = 0; e < CH; ++e) {
+                    ab[0][e] = lda(e);
+#pragma unroll
+                    for (int o = 0; o < S::NT1; ++o) bb[0][e][o] = ldb(e, o);
+                }
+#pragma unroll
+                for (int c = 0; c < 64 / CH; ++c) {
+                    if (c + 1 < 64 / CH) {
+#pragma unroll
+                        for (int e = 0; e < CH; ++e) {
+                            ab[(c + 1) & 1][e] = lda(CH * (c + 1) + e);
+#pragma unroll
+                            for (int o = 0; o < S::NT1; ++o) bb[(c + 1) & 1][e][o] = ldb(CH * (c + 1) + e, o);
+                        }
                     }
+                    NCF_SB();
+#pragma unroll
+                    for (int e = 0; e < CH; ++e)
+#pragma unroll
+                        for (int o = 0; o < S::NT1; ++o)
+                            dwacc[g * S::NT1 + o] = mfma32(ab[c & 1][e], bb[c & 1][e][o], dwacc[g * S::NT1 + o]);
+                    NCF_SB();
                 }
             }
         }
-        __syncthreads();
-
-        // ---- weight gradients: wave w owns tiles w, w+4, w+8, ... (K = 128 samples,
-        // 64 MFMA steps per tile; both operands double-buffered one chunk ahead)
+#endif
 #pragma unroll
         for (int m = 0; m < S::MAXT; ++m) {
-            const int t = w + 4 * m;
-            if (t >= S::NDW) break;
+            const int t = S::dw_tile(w, m);
+            if (t < 0) continue;
+#if NCF_DW1_SHARED
+            if (m < S::NSLOT1) continue;
+#endif
             int layer, ti, to;
             if (t < S::NDW1) { layer = 1; ti = t / S::NT1; to = t % S::NT1; }
             else if (t < S::NDW1 + S::NDW2) { layer = 2; ti = (t - S::NDW1) / S::NT2; to = (t - S::NDW1) % S::NT2; }
@@ -538,6 +634,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
                     fb);
             }
         }
+        NCF_T(10);
         // ---- bias gradients: one G row per thread, summed over the 128 samples
         if (tid < L1 + L2 + L3) {
             const int rr = tid < L1 ? S::RG1 + tid : tid < L1 + L2 ? S::RG2 + (tid - L1) : S::RG3 + (tid - L1 - L2);
@@ -549,15 +646,102 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
             }
             acc_bias += sacc;
         }
+        NCF_T(11);
         __syncthreads();
+        NCF_T(12);
+
+        // ---- end of tile.  Every wave is done with the staging, so this wave's block becomes a
+        // transpose buffer: the per-sample gradient rows are assembled [sample][features] in LDS
+        // and written as 256-byte pieces (lane-per-sample stores scatter 16-byte pieces, and on
+        // gfx9 a later load waits for every store issued before it).  This tile's GMF slices are
+        // read once more (L2) before the next tile's gather is issued: vmcnt is in order, and
+        // waiting for them must not wait for the HBM gather.
+        {
+            // the next tile's ids first: every load issued after this phase's stores would wait
+            // for them to drain
+            const bool has_next = it + gridDim.x < niter;
+            if (has_next) issue_ids(it + gridDim.x);
+            float4 ua3[GQ], ia3[GQ];
+            if constexpr (G > 0) {
+#pragma unroll
+                for (int q = 0; q < GQ; ++q) {
+                    ua3[q] = us[q];
+                    ia3[q] = is[q];
+                }
+            }
+            f32x16 g1r[S::NT1];
+#pragma unroll
+            for (int to = 0; to < S::NT1; ++to)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) g1r[to][r] = sb[(S::RG1 + 32 * to + drow(r, h)) * LS + j];
+            float* img = stg + ((w * S::RB * LS + 3) & ~3);
+            const int64_t si0 = it * 128 + 32 * w;
+            float* gbase = gs + (size_t)(2 * si0) * W;
+            if constexpr (G > 0) {
+                // GMF parts: image row = [user G | item G]
+                const float* wo = wl + S::SWO + h * S::GH;
+#pragma unroll
+                for (int q = 0; q < S::GH / 4; ++q) {
+                    const int f = 4 * q;
+                    const float4 a = ua3[q], b = ia3[q];
+                    *reinterpret_cast<float4*>(img + j * S::P1 + h * S::GH + f) =
+                        make_float4(dz * wo[f] * b.x, dz * wo[f + 1] * b.y, dz * wo[f + 2] * b.z, dz * wo[f + 3] * b.w);
+                    *reinterpret_cast<float4*>(img + j * S::P1 + G + h * S::GH + f) =
+                        make_float4(dz * wo[f] * a.x, dz * wo[f + 1] * a.y, dz * wo[f + 2] * a.z, dz * wo[f + 3] * a.w);
+                }
+                if (has_next) issue_rows(it + gridDim.x);
+#pragma unroll
+                for (int k = 0; k < G / 4; ++k) {
+                    const int e = 64 * k + lane;
+                    const int smp = e / (G / 2), rr = e % (G / 2), side = rr / (G / 4), c = rr % (G / 4);
+                    const float4 val = *reinterpret_cast<const float4*>(img + smp * S::P1 + side * G + 4 * c);
+                    if (srow[32 * w + smp] >= 0)
+                        *reinterpret_cast<float4*>(gbase + (size_t)(2 * smp + side) * W + 4 * c) = val;
+                }
+            }
+            NCF_T(13);
+            if constexpr (G == 0) {
+                if (has_next) issue_rows(it + gridDim.x);
+            }
+            // MLP parts: dX = W1 G1 (A = W1 read along `in`), image row = [user D0 | item D0]
+#pragma unroll
+            for (int to = 0; to < S::NT0; ++to) {
+                const int oc = 32 * to + j;
+                const f32x16 acc = mchain<S::NS1, 4>(
+                    f32x16{},
+                    [&](int t) {
+                        const int k = 32 * (t / 16) + drow(t % 16, h);
+                        return (oc < L0 && k < L1) ? wl[S::SW1 + oc * S::LW1 + k] : 0.f;
+                    },
+                    [&](int t) { return g1r[t / 16][t % 16]; });
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int f = 32 * to + 8 * q + 4 * h;  // rows drow(4q..4q+3, h) are f..f+3
+                    if (f < L0)
+                        *reinterpret_cast<float4*>(img + j * S::P2 + f) =
+                            make_float4(acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]);
+                }
+            }
+            NCF_T(14);
+#pragma unroll
+            for (int k = 0; k < L0 / 8; ++k) {
+                const int e = 64 * k + lane;
+                const int smp = e / (L0 / 4), f = 4 * (e % (L0 / 4));
+                const int side = f / D0;
+                const float4 val = *reinterpret_cast<const float4*>(img + smp * S::P2 + f);
+                if (srow[32 * w + smp] >= 0)
+                    *reinterpret_cast<float4*>(gbase + (size_t)(2 * smp + side) * W + G + (f - side * D0)) = val;
+            }
+            NCF_T(15);
+        }
     }
 
     // ---- epilogue: this workgroup's dense-gradient slab and BCE partial
     float* slab = slabs + (size_t)blockIdx.x * S::P;
 #pragma unroll
     for (int m = 0; m < S::MAXT; ++m) {
-        const int t = w + 4 * m;
-        if (t >= S::NDW) break;
+        const int t = S::dw_tile(w, m);
+        if (t < 0) continue;
         int off, lin, lout, ti, to;
         if (t < S::NDW1) { off = S::OW1; lin = L0; lout = L1; ti = t / S::NT1; to = t % S::NT1; }
         else if (t < S::NDW1 + S::NDW2) {
@@ -678,3 +862,10 @@ hipError_t launch_fb_fused(const ncf_shape_t& s, const WsLayout& L, void* ws, co
 }
 
 }  // namespace ncf
+
+#ifdef NCF_FUSED_TIMING
+extern "C" int ncf_debug_fused_timing(unsigned long long* out, size_t count) {
+    size_t n = count < sizeof(ncf::g_fused_t) / 8 ? count : sizeof(ncf::g_fused_t) / 8;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(ncf::g_fused_t), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -2;
+}
+#endif
