@@ -91,11 +91,6 @@ struct FShape {
     static constexpr int GCH = GH >= 16 ? 16 : GH;       // reduction chunk (bounds register pressure)
     static constexpr int NGC = GH >= 16 ? GH / 16 : (GH > 0 ? 1 : 0);
     static constexpr int XCH = G + L3 + 4;               // per-wave exchange floats
-    // end-of-tile transpose images in a wave's staging block: [32 samples][2G] and [32][L0],
-    // rows padded by 4 floats (16-byte aligned, conflict-free ds_write_b128)
-    static constexpr int P1 = 2 * G + 4, P2 = L0 + 4;
-    static_assert(32 * P1 + 3 <= RB * LS && 32 * P2 + 3 <= RB * LS, "transpose image must fit the staging block");
-    static_assert(G % 4 == 0 && D0 % 4 == 0, "float4 row pieces");
     static constexpr size_t LDS_BYTES = (size_t)(4 * RB * LS + WLDS) * 4 + 256 * 4 + (size_t)4 * XCH * 4;
     static_assert(LDS_BYTES <= 163840, "LDS budget");
 };
@@ -245,45 +240,6 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
     __syncthreads();
 
     const int64_t niter = (n + 127) / 128;
-    // ---- a tile's ids and rows are requested at the end of the previous tile (the first one
-    // here), so the HBM gather latency overlaps the previous tile's gradient-row stores
-    constexpr int GQ = S::GH / 4 > 0 ? S::GH / 4 : 1;
-    float4 nxv[D0 / 4], nua[GQ], nia[GQ];
-    int nu = 0, nv = 0;
-    float ny = 0.f;
-    auto issue_ids = [&](int64_t it2) {
-        const int64_t s2 = it2 * 128 + 32 * w + j;
-        nu = 0;
-        nv = 0;
-        ny = 0.f;
-        if (s2 < n) {
-            nu = users[s2];
-            nv = items[s2];
-            ny = labels[s2];
-        }
-    };
-    auto issue_rows = [&](int64_t it2) {
-        const int64_t s2 = it2 * 128 + 32 * w + j;
-        const bool ok2 = s2 < n && (unsigned)nu < (unsigned)ids.ubound && (unsigned)nv < (unsigned)ids.ibound;
-        const float* eu2 = emb + (size_t)(ok2 ? nu : 0) * W;
-        const float* ei2 = emb + (size_t)(ok2 ? ids.ibase + nv : 0) * W;
-        const float4* src = reinterpret_cast<const float4*>((h ? ei2 : eu2) + G);
-#pragma unroll
-        for (int q = 0; q < D0 / 4; ++q) nxv[q] = src[q];
-        if constexpr (G > 0) {
-            const float4* us2 = reinterpret_cast<const float4*>(eu2 + h * S::GH);
-            const float4* is2 = reinterpret_cast<const float4*>(ei2 + h * S::GH);
-#pragma unroll
-            for (int q = 0; q < GQ; ++q) {
-                nua[q] = us2[q];
-                nia[q] = is2[q];
-            }
-        }
-    };
-    if ((int64_t)blockIdx.x < niter) {
-        issue_ids(blockIdx.x);
-        issue_rows(blockIdx.x);
-    }
     int itl = -1;
     for (int64_t it = blockIdx.x; it < niter; it += gridDim.x) {
         // lane coordinates re-derived opaquely every tile: keeps the compiler from hoisting the
@@ -295,8 +251,13 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
         NCF_T(0);
         const int64_t si = it * 128 + 32 * w + j;
         const bool inb = si < n;
-        const int u = nu, v = nv;
-        const float y = ny;
+        int u = 0, v = 0;
+        float y = 0.f;
+        if (inb) {
+            u = users[si];
+            v = items[si];
+            y = labels[si];
+        }
         // Masked samples read row 0 (a valid address) and get dz = 0: they contribute nothing.
         const bool ok = inb && (unsigned)u < (unsigned)ids.ubound && (unsigned)v < (unsigned)ids.ibound;
         const int urow = ok ? u : 0, irow = ok ? ids.ibase + v : 0;
@@ -307,18 +268,29 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
         const float* eu = emb + (size_t)urow * W;
         const float* ei = emb + (size_t)irow * W;
         float* sb = stg + w * S::RB * LS;  // this wave's staging block
+
+        // ---- bulk gather: this half's MLP vector and both GMF slices, all loads in flight at once
         float4 xv[D0 / 4];
+        {
+            const float4* src = reinterpret_cast<const float4*>((h ? ei : eu) + G);
 #pragma unroll
-        for (int q = 0; q < D0 / 4; ++q) xv[q] = nxv[q];
+            for (int q = 0; q < D0 / 4; ++q) xv[q] = src[q];
+        }
         float zp = 0.f;
         const float4* us = reinterpret_cast<const float4*>(eu + h * S::GH);
         const float4* is = reinterpret_cast<const float4*>(ei + h * S::GH);
         if constexpr (G > 0) {
+            float4 ua[S::GH / 4], ia[S::GH / 4];
+#pragma unroll
+            for (int q = 0; q < S::GH / 4; ++q) {
+                ua[q] = us[q];
+                ia[q] = is[q];
+            }
             const float* wo = wl + S::SWO + h * S::GH;
 #pragma unroll
             for (int q = 0; q < S::GH / 4; ++q)
-                zp += wo[4 * q] * (nua[q].x * nia[q].x) + wo[4 * q + 1] * (nua[q].y * nia[q].y) +
-                      wo[4 * q + 2] * (nua[q].z * nia[q].z) + wo[4 * q + 3] * (nua[q].w * nia[q].w);
+                zp += wo[4 * q] * (ua[q].x * ia[q].x) + wo[4 * q + 1] * (ua[q].y * ia[q].y) +
+                      wo[4 * q + 2] * (ua[q].z * ia[q].z) + wo[4 * q + 3] * (ua[q].w * ia[q].w);
         }
 
         NCF_T(1);
@@ -468,10 +440,12 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
             }
         }
         NCF_T(4);
+        float* gu = gs + (size_t)(2 * si) * W;  // user contribution row
+        float* gi = gu + W;                     // item contribution row
 
-        // ---- GMF backward: output-kernel grads (transpose-reduced); the embedding-row grads are
-        // formed at the end of the tile
+        // ---- GMF backward: embedding grads + output-kernel grads (transpose-reduced)
         if constexpr (G > 0) {
+            const float* wo = wl + S::SWO + h * S::GH;
 #pragma unroll
             for (int c = 0; c < S::NGC; ++c) {
                 float contrib[S::GCH];
@@ -483,6 +457,14 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
                     contrib[4 * q + 1] = dz * (a.y * b.y);
                     contrib[4 * q + 2] = dz * (a.z * b.z);
                     contrib[4 * q + 3] = dz * (a.w * b.w);
+                    if (ok) {
+                        const float4 gu4 = make_float4(dz * wo[f] * b.x, dz * wo[f + 1] * b.y, dz * wo[f + 2] * b.z,
+                                                       dz * wo[f + 3] * b.w);
+                        const float4 gi4 = make_float4(dz * wo[f] * a.x, dz * wo[f + 1] * a.y, dz * wo[f + 2] * a.z,
+                                                       dz * wo[f + 3] * a.w);
+                        *reinterpret_cast<float4*>(gu + h * S::GH + f) = gu4;
+                        *reinterpret_cast<float4*>(gi + h * S::GH + f) = gi4;
+                    }
                 }
                 acc_gmf[c] += half_transpose_reduce<S::GCH>(contrib, lane);
             }
@@ -543,6 +525,28 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
             }
         }
         NCF_T(7);
+#pragma unroll
+        for (int to = 0; to < S::NT0; ++to) {
+            const int oc = 32 * to + j;
+            const f32x16 acc = mchain<S::NS1, 4>(
+                f32x16{},
+                [&](int t) {
+                    const int k = 32 * (t / 16) + drow(t % 16, h);
+                    return (oc < L0 && k < L1) ? wl[S::SW1 + oc * S::LW1 + k] : 0.f;
+                },
+                [&](int t) { return g1[t / 16][t % 16]; });
+            if (ok) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int f = 32 * to + 8 * q + 4 * h;  // rows drow(4q..4q+3, h) are f..f+3
+                    if (f < L0) {
+                        float* dst = (f < D0) ? gu + G + f : gi + G + (f - D0);
+                        *reinterpret_cast<float4*>(dst) =
+                            make_float4(acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]);
+                    }
+                }
+            }
+        }
         NCF_T(8);
         __syncthreads();
         NCF_T(9);
@@ -560,9 +564,14 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
                 const int side = fi < D0 ? 0 : 128;
                 const int col = G + (fi < D0 ? fi : fi - D0);
                 const bool aok = fi < L0;
+                // Unconditional loads, unmasked: a masked sample (row -1) reads row 0, but its G1
+                // column (the B operand) is exactly zero; lanes past L0 feed only dW1 rows that are
+                // never written.  (A load under a branch, or a select on its value right after the
+                // load, makes the compiler wait for all outstanding loads before the next chunk.)
+                const int colc = aok ? col : 0;
                 auto lda = [&](int tt) {
                     const int row = srow[side + 32 * (tt >> 4) + 2 * (tt & 15) + h];
-                    return (aok && row >= 0) ? emb[(size_t)row * W + col] : 0.f;
+                    return emb[(size_t)(row < 0 ? 0 : row) * W + colc];
                 };
                 auto ldb = [&](int tt, int o) {
                     const int fo = 32 * o + j;
@@ -621,10 +630,11 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
                 const int side = fi < D0 ? 0 : 128;
                 const int col = G + (fi < D0 ? fi : fi - D0);
                 const bool aok = fi < L0;
+                const int colc = aok ? col : 0;  // see the shared chain above: no masks needed
                 dwacc[m] = mchain2<64, NCF_DW1_CH>(dwacc[m],
                                            [&](int tt) {
                                                const int row = srow[side + 32 * (tt >> 4) + 2 * (tt & 15) + h];
-                                               return (aok && row >= 0) ? emb[(size_t)row * W + col] : 0.f;
+                                               return emb[(size_t)(row < 0 ? 0 : row) * W + colc];
                                            },
                                            fb);
             } else {
@@ -649,91 +659,6 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
         NCF_T(11);
         __syncthreads();
         NCF_T(12);
-
-        // ---- end of tile.  Every wave is done with the staging, so this wave's block becomes a
-        // transpose buffer: the per-sample gradient rows are assembled [sample][features] in LDS
-        // and written as 256-byte pieces (lane-per-sample stores scatter 16-byte pieces, and on
-        // gfx9 a later load waits for every store issued before it).  This tile's GMF slices are
-        // read once more (L2) before the next tile's gather is issued: vmcnt is in order, and
-        // waiting for them must not wait for the HBM gather.
-        {
-            // the next tile's ids first: every load issued after this phase's stores would wait
-            // for them to drain
-            const bool has_next = it + gridDim.x < niter;
-            if (has_next) issue_ids(it + gridDim.x);
-            float4 ua3[GQ], ia3[GQ];
-            if constexpr (G > 0) {
-#pragma unroll
-                for (int q = 0; q < GQ; ++q) {
-                    ua3[q] = us[q];
-                    ia3[q] = is[q];
-                }
-            }
-            f32x16 g1r[S::NT1];
-#pragma unroll
-            for (int to = 0; to < S::NT1; ++to)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) g1r[to][r] = sb[(S::RG1 + 32 * to + drow(r, h)) * LS + j];
-            float* img = stg + ((w * S::RB * LS + 3) & ~3);
-            const int64_t si0 = it * 128 + 32 * w;
-            float* gbase = gs + (size_t)(2 * si0) * W;
-            if constexpr (G > 0) {
-                // GMF parts: image row = [user G | item G]
-                const float* wo = wl + S::SWO + h * S::GH;
-#pragma unroll
-                for (int q = 0; q < S::GH / 4; ++q) {
-                    const int f = 4 * q;
-                    const float4 a = ua3[q], b = ia3[q];
-                    *reinterpret_cast<float4*>(img + j * S::P1 + h * S::GH + f) =
-                        make_float4(dz * wo[f] * b.x, dz * wo[f + 1] * b.y, dz * wo[f + 2] * b.z, dz * wo[f + 3] * b.w);
-                    *reinterpret_cast<float4*>(img + j * S::P1 + G + h * S::GH + f) =
-                        make_float4(dz * wo[f] * a.x, dz * wo[f + 1] * a.y, dz * wo[f + 2] * a.z, dz * wo[f + 3] * a.w);
-                }
-                if (has_next) issue_rows(it + gridDim.x);
-#pragma unroll
-                for (int k = 0; k < G / 4; ++k) {
-                    const int e = 64 * k + lane;
-                    const int smp = e / (G / 2), rr = e % (G / 2), side = rr / (G / 4), c = rr % (G / 4);
-                    const float4 val = *reinterpret_cast<const float4*>(img + smp * S::P1 + side * G + 4 * c);
-                    if (srow[32 * w + smp] >= 0)
-                        *reinterpret_cast<float4*>(gbase + (size_t)(2 * smp + side) * W + 4 * c) = val;
-                }
-            }
-            NCF_T(13);
-            if constexpr (G == 0) {
-                if (has_next) issue_rows(it + gridDim.x);
-            }
-            // MLP parts: dX = W1 G1 (A = W1 read along `in`), image row = [user D0 | item D0]
-#pragma unroll
-            for (int to = 0; to < S::NT0; ++to) {
-                const int oc = 32 * to + j;
-                const f32x16 acc = mchain<S::NS1, 4>(
-                    f32x16{},
-                    [&](int t) {
-                        const int k = 32 * (t / 16) + drow(t % 16, h);
-                        return (oc < L0 && k < L1) ? wl[S::SW1 + oc * S::LW1 + k] : 0.f;
-                    },
-                    [&](int t) { return g1r[t / 16][t % 16]; });
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int f = 32 * to + 8 * q + 4 * h;  // rows drow(4q..4q+3, h) are f..f+3
-                    if (f < L0)
-                        *reinterpret_cast<float4*>(img + j * S::P2 + f) =
-                            make_float4(acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]);
-                }
-            }
-            NCF_T(14);
-#pragma unroll
-            for (int k = 0; k < L0 / 8; ++k) {
-                const int e = 64 * k + lane;
-                const int smp = e / (L0 / 4), f = 4 * (e % (L0 / 4));
-                const int side = f / D0;
-                const float4 val = *reinterpret_cast<const float4*>(img + smp * S::P2 + f);
-                if (srow[32 * w + smp] >= 0)
-                    *reinterpret_cast<float4*>(gbase + (size_t)(2 * smp + side) * W + G + (f - side * D0)) = val;
-            }
-            NCF_T(15);
-        }
     }
 
     // ---- epilogue: this workgroup's dense-gradient slab and BCE partial
