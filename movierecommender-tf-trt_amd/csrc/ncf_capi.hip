@@ -80,21 +80,27 @@ struct Profiler {
 };
 thread_local Profiler g_prof;
 
-void prof_begin(int k, hipStream_t st) {
+// A profiled launch group's events ride on its kernels' dispatch packets (ncf::launch).
+void prof_begin(int k, hipStream_t) {
     ProfSlot& p = g_prof.slot[k & 7];
     if (!(g_prof.mask >> k & 1u) || p.used >= p.start.size()) return;
-    hipEventRecord(p.start[p.used], st);
+    ncf::LaunchEvents& ev = ncf::launch_events();
+    ev.start = p.start[p.used];
+    ev.stop = p.stop[p.used];
+    ev.launches = 0;
 }
-void prof_end(int k, hipStream_t st) {
+void prof_end(int k, hipStream_t) {
     ProfSlot& p = g_prof.slot[k & 7];
     if (!(g_prof.mask >> k & 1u) || p.used >= p.start.size()) return;
-    hipEventRecord(p.stop[p.used], st);
-    ++p.used;
+    ncf::LaunchEvents& ev = ncf::launch_events();
+    if (ev.launches > 0) ++p.used;
+    ev = ncf::LaunchEvents{};
 }
 
-// Side stream (one per device, created on first use): the dense-layer tail (loss summary,
-// slab reduction, dense Adam) runs on it concurrently with the embedding sweep.  The fork/join
-// events make the pair capturable into one hipGraph.  NCF_SIDE_STREAM=0 disables it.
+// Side stream (one per device, created on first use, opt-in with NCF_SIDE_STREAM=1): the
+// index build and the dense-layer tail run on it beside the forward/backward and the
+// embedding sweep.  Measured on MI355X the cross-stream fork/join packets cost more than the
+// overlap gains (225 vs 232 us per config-C step), so one stream is the default.
 struct SideStream {
     hipStream_t s = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
@@ -103,7 +109,7 @@ struct SideStream {
 SideStream* side_stream() {
     static const bool enabled = [] {
         const char* e = getenv("NCF_SIDE_STREAM");
-        return !(e && atoi(e) == 0);
+        return e && atoi(e) != 0;
     }();
     if (!enabled) return nullptr;
     static std::mutex mu;
@@ -211,6 +217,11 @@ WsLayout make_layout(const ncf_shape_t& s, int64_t B, int world) {
     return L;
 }
 
+LaunchEvents& launch_events() {
+    thread_local LaunchEvents ev;
+    return ev;
+}
+
 }  // namespace ncf
 
 extern "C" {
@@ -309,7 +320,16 @@ int ncf_group_metrics(const float* probs, const float* labels, int64_t n_groups,
 struct FbOut {
     int nslab = 0, nbce = 0, nmet = 0;
     float n_groups = 0.f;
+    SideStream* index_side = nullptr;  // index built on this side stream: join before using it
 };
+
+// make `st` wait for an index built on the side stream
+static int index_join(hipStream_t st, FbOut& fb) {
+    if (!fb.index_side) return 0;
+    hipError_t e = join_side(st, fb.index_side);
+    fb.index_side = nullptr;
+    return hip_check(e, "index join");
+}
 
 // index build + forward/backward (+ group metrics): shared by train_step and forward_backward
 // sharded: ids are the compact ids of the last ncf_shard_plan (model->emb = its unique rows)
@@ -323,10 +343,16 @@ static int run_fb(const ncf_shape_t& s, const ncf::WsLayout& L, const ncf_model_
         items = ncf::at<int32_t>(ws, L.cid_i);
         ids = ncf::compact_ids(n);
     } else {
-        prof_begin(NCF_K_INDEX, st);
-        e = ncf::launch_index_build(s, L, ws, users, items, n, st);
-        prof_end(NCF_K_INDEX, st);
+        // the index depends only on the ids: it is built on the side stream while the
+        // forward/backward runs (the fused kernel leaves registers and a little LDS free on every
+        // CU); the caller's next launch on `st` that needs it comes after index_join
+        SideStream* ss = nullptr;
+        hipStream_t sti = fork_side(st, &ss);
+        prof_begin(NCF_K_INDEX, sti);
+        e = ncf::launch_index_build(s, L, ws, users, items, n, sti);
+        prof_end(NCF_K_INDEX, sti);
         if (e != hipSuccess) return hip_check(e, "index build");
+        out->index_side = ss;
     }
     prof_begin(NCF_K_FWD_BWD, st);
     if (use_fused(s, h))
@@ -379,6 +405,8 @@ int ncf_train_step(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* optim,
     float* summary = ncf::at<float>(ws, L.summary);
     FbOut fb;
     if (int r = run_fb(*s, L, model, h, users, items, labels, n, ws, probs_out, &fb, st)) return r;
+    // the index (side stream) must be complete before the side stream takes the dense tail
+    if (int r = index_join(st, fb)) return r;
     // dense-layer tail on the side stream, embedding sweep on the main stream
     SideStream* ss = nullptr;
     hipStream_t st2 = fork_side(st, &ss);
@@ -416,6 +444,8 @@ int ncf_forward_backward(const ncf_shape_t* s, const ncf_model_t* model, const n
     hipStream_t st = (hipStream_t)stream;
     FbOut fb;
     if (int r = run_fb(*s, L, model, h, users, items, labels, n, ws, probs_out, &fb, st)) return r;
+    // the index (side stream) must be complete before the side stream takes the dense tail
+    if (int r = index_join(st, fb)) return r;
     SideStream* ss = nullptr;
     hipStream_t st2 = fork_side(st, &ss);
     int nreg_mlp = 0, nreg_emb = 0;

@@ -759,7 +759,7 @@ static hipError_t launch_one(const ncf_shape_t& s, const WsLayout& L, void* ws, 
     int grid = (int)(niter < 256 ? niter : 256);
     if (grid > kMaxSlabs) grid = kMaxSlabs;
     const bool in_kernel = group > 0 && group <= 32 && 32 % group == 0;
-    k_fb_fused<S><<<grid, kBlock, S::LDS_BYTES, st>>>(emb, mlp, users, items, labels, n, ids, inv_batch, at<float>(ws, L.probs),
+    launch(k_fb_fused<S>, grid, kBlock, S::LDS_BYTES, st, emb, mlp, users, items, labels, n, ids, inv_batch, at<float>(ws, L.probs),
                                                       at<float>(ws, L.gs), at<float>(ws, L.slabs),
                                                       at<float>(ws, L.part_bce), group, topk,
                                                       in_kernel ? at<float>(ws, L.part_hit) : nullptr,

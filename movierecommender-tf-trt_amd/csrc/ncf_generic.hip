@@ -225,7 +225,7 @@ hipError_t launch_fb_generic(const ncf_shape_t& s, const WsLayout& L, void* ws, 
     const GenShape S = make_gen_shape(s, ids);
     const int use_lds = s.mlp_params <= kLdsWeightsMax ? 1 : 0;
     const int grid = (int)((n + kBlock - 1) / kBlock);
-    k_fb_generic<true><<<grid, kBlock, use_lds ? (size_t)s.mlp_params * 4 : 0, st>>>(
+    launch(k_fb_generic<true>, grid, kBlock, use_lds ? (size_t)s.mlp_params * 4 : 0, st, 
         S, emb, mlp, users, items, labels, n, inv_batch, at<float>(ws, L.probs), at<float>(ws, L.act),
         at<float>(ws, L.dz), at<float>(ws, L.gs), at<float>(ws, L.part_bce), use_lds);
     *nbce = grid;
@@ -236,7 +236,7 @@ hipError_t launch_fb_generic(const ncf_shape_t& s, const WsLayout& L, void* ws, 
         ns = (n + chunk - 1) / chunk;
     }
     dim3 g2((s.mlp_params + kBlock - 1) / kBlock, (unsigned)ns);
-    k_dw_generic<<<g2, kBlock, 0, st>>>(S, at<float>(ws, L.act), at<float>(ws, L.dz), n, chunk,
+    launch(k_dw_generic, g2, kBlock, 0, st, S, at<float>(ws, L.act), at<float>(ws, L.dz), n, chunk,
                                         at<float>(ws, L.slabs));
     *nslab = (int)ns;
     return hipGetLastError();
@@ -249,7 +249,7 @@ hipError_t launch_predict_generic(const ncf_shape_t& s, const WsLayout& L, void*
     const GenShape S = make_gen_shape(s, ids);
     const int use_lds = s.mlp_params <= kLdsWeightsMax ? 1 : 0;
     const int grid = (int)((n + kBlock - 1) / kBlock);
-    k_fb_generic<false><<<grid, kBlock, use_lds ? (size_t)s.mlp_params * 4 : 0, st>>>(
+    launch(k_fb_generic<false>, grid, kBlock, use_lds ? (size_t)s.mlp_params * 4 : 0, st, 
         S, emb, mlp, users, items, labels, n, 0.0f, probs, at<float>(ws, L.act), nullptr, nullptr,
         labels ? at<float>(ws, L.part_bce) : nullptr, use_lds);
     *nbce = labels ? grid : 0;

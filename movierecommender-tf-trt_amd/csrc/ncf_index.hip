@@ -294,15 +294,15 @@ static hipError_t build(const WsLayout& L, void* ws, const KeySrc& ks, int64_t m
     int32_t* list = at<int32_t>(ws, L.list);
     const int nscan = (int)((r1 + kScanBlock - 1) / kScanBlock);
     if (m > 0)
-        k_count<MODE><<<grid_for(m, 1024), kBlock, 0, st>>>(ks, m, cnt, at<int32_t>(ws, L.heavy_n),
+        launch(k_count<MODE>, grid_for(m, 1024), kBlock, 0, st, ks, m, cnt, at<int32_t>(ws, L.heavy_n),
                                                             at<int32_t>(ws, L.err));
-    k_scan_local<UNIQ><<<nscan, kBlock, 0, st>>>(cnt, r1, local, tot, UNIQ ? at<int32_t>(ws, L.uloc) : nullptr,
+    launch(k_scan_local<UNIQ>, nscan, kBlock, 0, st, cnt, r1, local, tot, UNIQ ? at<int32_t>(ws, L.uloc) : nullptr,
                                                  UNIQ ? at<int32_t>(ws, L.utot) : nullptr);
     const size_t pre_bytes = (size_t)nscan * 4 * (UNIQ ? 2 : 1);
-    k_fill<MODE, UNIQ><<<grid_for(m > r1 ? m : r1, 1024), kBlock, pre_bytes, st>>>(ks, m, cnt, local, tot, nscan, r1,
+    launch(k_fill<MODE, UNIQ>, grid_for(m > r1 ? m : r1, 1024), kBlock, pre_bytes, st, ks, m, cnt, local, tot, nscan, r1,
                                                                                    offs, list, po);
     if (hipError_t e = set_sort_lds(nwords)) return e;
-    k_sort<<<(unsigned)((K + kBlock - 1) / kBlock), kBlock, (size_t)nwords * 4, st>>>(offs, K, list, nwords);
+    launch(k_sort, (unsigned)((K + kBlock - 1) / kBlock), kBlock, (size_t)nwords * 4, st, offs, K, list, nwords);
     return hipGetLastError();
 }
 

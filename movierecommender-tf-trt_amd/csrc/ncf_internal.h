@@ -2,6 +2,7 @@
 // Not part of the ABI (see include/movierec_ncf.h).
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -66,6 +67,30 @@ struct WsLayout {
 
 // world == 0: single-table layout; world >= 1: row-sharded layout (ncf_shard_*)
 WsLayout make_layout(const ncf_shape_t& s, int64_t max_batch, int world = 0);
+
+// Timing events attached to kernel dispatches by the profiler (ncf_profile_enable): while set,
+// every dispatch through launch() carries them in its AQL packet (hipExtLaunchKernel), so a
+// launch group is timed from its first kernel's start to its last kernel's end without the
+// marker packets a hipEventRecord would add to the stream.
+struct LaunchEvents {
+    hipEvent_t start = nullptr, stop = nullptr;
+    int launches = 0;
+};
+LaunchEvents& launch_events();  // thread-local
+
+template <typename... KArgs, typename... Args>
+inline void launch(void (*k)(KArgs...), dim3 grid, dim3 block, size_t shmem, hipStream_t st, Args... args) {
+    static_assert(sizeof...(KArgs) == sizeof...(Args), "kernel argument count");
+    LaunchEvents& ev = launch_events();
+    if (ev.stop) {
+        hipEvent_t s0 = ev.start;
+        ev.start = nullptr;  // the group's first dispatch carries the start stamp
+        ++ev.launches;
+        hipExtLaunchKernelGGL(k, grid, block, (std::uint32_t)shmem, st, s0, ev.stop, 0u, static_cast<KArgs>(args)...);
+    } else {
+        hipLaunchKernelGGL(k, grid, block, shmem, st, static_cast<KArgs>(args)...);
+    }
+}
 
 // Table row numbering of the row-sharded layout: global row g (users 0..U-1,
 // items U..U+I-1) is owned by rank g % world at local row g / world.  The plan's index keys

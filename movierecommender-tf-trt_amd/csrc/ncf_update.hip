@@ -353,7 +353,7 @@ hipError_t launch_emb_update(const ncf_shape_t& s, const WsLayout& L, void* ws, 
     const int src = dense_grad ? kGradDense : kGradSparse;
     dim3 grid(kUpdateGrid), blk(kBlock);
 #define NCF_EMB_LAUNCH(OPT, SRC, L2)                                                                          \
-    k_emb_update<OPT, SRC, L2><<<grid, blk, 0, st>>>((float4*)emb, (float4*)m, (float4*)v, n4, w4, offs, list, gs, \
+    launch(k_emb_update<OPT, SRC, L2>, grid, blk, 0, st, (float4*)emb, (float4*)m, (float4*)v, n4, w4, offs, list, gs, \
                                                      (const float4*)dense_grad, step, h.lr, h.beta_1, h.beta_2,    \
                                                      h.epsilon, h.l2[0], part)
     if (h.optimizer == NCF_OPT_ADAM) {
@@ -370,7 +370,7 @@ hipError_t launch_emb_update(const ncf_shape_t& s, const WsLayout& L, void* ws, 
 hipError_t launch_emb_grad_dense(const ncf_shape_t& s, const WsLayout& L, void* ws, float* out, hipStream_t st) {
     const uint32_t w4 = (uint32_t)(s.row_width / 4);
     const uint32_t n4 = (uint32_t)(s.num_rows * w4);
-    k_emb_grad_dense<<<kUpdateGrid, kBlock, 0, st>>>((float4*)out, n4, w4, at<int32_t>(ws, L.offs),
+    launch(k_emb_grad_dense, kUpdateGrid, kBlock, 0, st, (float4*)out, n4, w4, at<int32_t>(ws, L.offs),
                                                      at<int32_t>(ws, L.list), at<const float4>(ws, L.gs));
     return hipGetLastError();
 }
@@ -380,7 +380,7 @@ hipError_t launch_uniq_grad(const ncf_shape_t& s, const WsLayout& L, void* ws, i
     const uint32_t w4 = (uint32_t)(s.row_width / 4);
     int64_t g = (2 * n * w4 + kBlock - 1) / kBlock;
     if (g > kUpdateGrid) g = kUpdateGrid;
-    k_uniq_grad<<<(unsigned)g, kBlock, 0, st>>>((float4*)out, at<int32_t>(ws, L.nuniq), w4, at<int32_t>(ws, L.uoffs),
+    launch(k_uniq_grad, (unsigned)g, kBlock, 0, st, (float4*)out, at<int32_t>(ws, L.nuniq), w4, at<int32_t>(ws, L.uoffs),
                                                 at<int32_t>(ws, L.list), at<const float4>(ws, L.gs));
     return hipGetLastError();
 }
@@ -391,7 +391,7 @@ hipError_t launch_gather_rows(const ncf_shape_t& s, const float* table, int64_t 
     const uint32_t w4 = (uint32_t)(s.row_width / 4);
     int64_t g = (m * w4 + kBlock - 1) / kBlock;
     if (g > kUpdateGrid) g = kUpdateGrid;
-    k_gather_rows<<<(unsigned)g, kBlock, 0, st>>>((float4*)out, (const float4*)table, table_rows, rows,
+    launch(k_gather_rows, (unsigned)g, kBlock, 0, st, (float4*)out, (const float4*)table, table_rows, rows,
                                                   (uint32_t)(m * w4), w4);
     return hipGetLastError();
 }
@@ -399,7 +399,7 @@ hipError_t launch_gather_rows(const ncf_shape_t& s, const float* table, int64_t 
 hipError_t launch_emb_reg(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, int64_t rows,
                           float lam, hipStream_t st) {
     const uint32_t n4 = (uint32_t)(rows * (s.row_width / 4));
-    k_emb_reg<<<kUpdateGrid, kBlock, 0, st>>>((const float4*)emb, n4, lam, at<float>(ws, L.part_reg));
+    launch(k_emb_reg, kUpdateGrid, kBlock, 0, st, (const float4*)emb, n4, lam, at<float>(ws, L.part_reg));
     return hipGetLastError();
 }
 
@@ -415,16 +415,16 @@ hipError_t launch_mlp_update(const ncf_shape_t& s, const WsLayout& L, void* ws, 
         const int per = (nslab + kSlabSplit - 1) / kSlabSplit;
         const int nch = (nslab + per - 1) / per;
         float* sp = at<float>(ws, L.slab_part);
-        k_slab_partial<<<dim3(grid, nch), kBlock, 0, st>>>(slabs, P, nslab, per, sp);
+        launch(k_slab_partial, dim3(grid, nch), kBlock, 0, st, slabs, P, nslab, per, sp);
         slabs = sp;
         nslab = nch;
     }
     if (h.optimizer == NCF_OPT_ADAM)
-        k_mlp_update<NCF_OPT_ADAM><<<grid, kBlock, 0, st>>>(mlp, m, v, P, slabs, nslab, grad_in,
+        launch(k_mlp_update<NCF_OPT_ADAM>, grid, kBlock, 0, st, mlp, m, v, P, slabs, nslab, grad_in,
                                                             grad_out, do_update ? 1 : 0, want_reg ? 1 : 0, step,
                                                             h.lr, h.beta_1, h.beta_2, h.epsilon, t, part);
     else
-        k_mlp_update<NCF_OPT_SGD><<<grid, kBlock, 0, st>>>(mlp, m, v, P, slabs, nslab, grad_in,
+        launch(k_mlp_update<NCF_OPT_SGD>, grid, kBlock, 0, st, mlp, m, v, P, slabs, nslab, grad_in,
                                                            grad_out, do_update ? 1 : 0, want_reg ? 1 : 0, step,
                                                            h.lr, h.beta_1, h.beta_2, h.epsilon, t, part);
     *nreg = ((do_update || want_reg) && t.n > 0) ? grid : 0;
@@ -437,21 +437,21 @@ hipError_t launch_group_metrics(const float* probs, const float* labels, int64_t
     const int grid = (int)((n_groups + kBlock - 1) / kBlock);
     *nparts = grid;
     if (grid == 0) return hipSuccess;
-    k_group_metrics<<<grid, kBlock, 0, st>>>(probs, labels, n_groups, group, k, hit, dcg, part_hit, part_dcg);
+    launch(k_group_metrics, grid, kBlock, 0, st, probs, labels, n_groups, group, k, hit, dcg, part_hit, part_dcg);
     return hipGetLastError();
 }
 
 hipError_t launch_rank(const float* probs, int64_t n_groups, int group, int32_t* rank_idx, hipStream_t st) {
     const int grid = (int)((n_groups + kBlock - 1) / kBlock);
     if (grid == 0) return hipSuccess;
-    k_rank<<<grid, kBlock, 0, st>>>(probs, n_groups, group, rank_idx);
+    launch(k_rank, grid, kBlock, 0, st, probs, n_groups, group, rank_idx);
     return hipGetLastError();
 }
 
 hipError_t launch_summary(const WsLayout& L, void* ws, int nbce, int nmet, float n_groups, int nreg_emb,
                           int nreg_mlp, float* summary, hipStream_t st) {
     const float* reg = at<float>(ws, L.part_reg);
-    k_summary<<<1, kBlock, 0, st>>>(at<float>(ws, L.part_bce), nbce, at<float>(ws, L.part_hit),
+    launch(k_summary, 1, kBlock, 0, st, at<float>(ws, L.part_bce), nbce, at<float>(ws, L.part_hit),
                                     at<float>(ws, L.part_dcg), nmet, n_groups, reg, nreg_emb, reg + kUpdateGrid,
                                     nreg_mlp, summary);
     return hipGetLastError();
@@ -460,7 +460,7 @@ hipError_t launch_summary(const WsLayout& L, void* ws, int nbce, int nmet, float
 hipError_t launch_stats(const WsLayout& L, void* ws, const float* summary, int nreg_emb, int nreg_mlp,
                         float inv_batch, double* stats, int32_t* step, bool bump_step, hipStream_t st) {
     const float* reg = at<float>(ws, L.part_reg);
-    k_stats<<<1, kBlock, 0, st>>>(summary, reg, nreg_emb, reg + kUpdateGrid, nreg_mlp, inv_batch, stats, step,
+    launch(k_stats, 1, kBlock, 0, st, summary, reg, nreg_emb, reg + kUpdateGrid, nreg_mlp, inv_batch, stats, step,
                                   bump_step ? 1 : 0);
     return hipGetLastError();
 }
