@@ -230,6 +230,27 @@ int ncf_shard_apply_update(const ncf_shape_t* shape, ncf_model_t* model, ncf_opt
 int ncf_shard_predict(const ncf_shape_t* shape, const ncf_model_t* model, int32_t world, int64_t n, float* probs,
                       void* ws, size_t ws_bytes, void* stream);
 
+/* All-item scoring + top-k (BASELINE config E).  Replaces the serving workload of
+ * trt_client.py:43-57 (score items for a user with the exported model's
+ * output/Sigmoid, keep the K = 10 best by np.argsort) for a whole list of users
+ * against the whole catalogue.  For q < n_users: top_items[q*k .. q*k+k) = the k
+ * items with the highest score for user users[q], best first, ties broken by the
+ * lower item id; top_scores = their sigmoid output.  Entries past the catalogue
+ * (k > num_items) and users outside [0, num_users) give item -1, score 0.
+ *   NCF_SCORE_FP16: fp16 operands, fp32 accumulation on MFMA (v_mfma_f32_32x32x16_f16),
+ *                   ranked by the logit; shapes where ncf_score_supported() is 1 only.
+ *   NCF_SCORE_FP32: the fp32 forward of ncf_predict, ranked by probability; any shape
+ *                   (slow: one generic forward per pair).
+ * 1 <= k <= NCF_SCORE_MAX_K; n_users <= the max_users the workspace was sized for. */
+#define NCF_SCORE_FP16 0
+#define NCF_SCORE_FP32 1
+#define NCF_SCORE_MAX_K 32
+int ncf_score_supported(const ncf_shape_t* shape, int32_t precision);
+int ncf_score_workspace_size(const ncf_shape_t* shape, int64_t max_users, size_t* bytes);
+int ncf_score_topk(const ncf_shape_t* shape, const ncf_model_t* model, const int32_t* users, int64_t n_users,
+                   int32_t k, int32_t precision, int32_t* top_items, float* top_scores, void* ws, size_t ws_bytes,
+                   void* stream);
+
 /* Profiling hook (bench.py): while enabled, every launch of a group whose bit
  * is set in `kernel_mask` (bit NCF_K_*) issued by this thread is bracketed by
  * HIP events on its own stream (up to `capacity` launches per group);
@@ -241,6 +262,7 @@ int ncf_shard_predict(const ncf_shape_t* shape, const ncf_model_t* model, int32_
 #define NCF_K_EMB_UPDATE 3  /* embedding scatter-add + optimizer sweep */
 #define NCF_K_MLP_UPDATE 4  /* dense-weight gradient reduction + optimizer */
 #define NCF_K_METRICS 5     /* hr/dcg + loss summary */
+#define NCF_K_SCORE 6       /* all-item scoring + top-k (MFMA kernel only, not its preparation) */
 int ncf_profile_enable(int32_t kernel_mask, int32_t capacity);
 int ncf_profile_read(int32_t kernel_id, double* total_ms, int64_t* launches);
 

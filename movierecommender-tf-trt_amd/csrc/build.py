@@ -15,7 +15,7 @@ ROOT = os.path.dirname(PKG)
 INCLUDE = os.path.join(ROOT, "include")
 OUT_DIR = os.path.join(PKG, "movierec", "_lib")
 LIB = os.path.join(OUT_DIR, "libmovierec_ncf.so")
-SOURCES = ["ncf_index.hip", "ncf_update.hip", "ncf_generic.hip", "ncf_fused.hip", "ncf_capi.hip"]
+SOURCES = ["ncf_index.hip", "ncf_update.hip", "ncf_generic.hip", "ncf_fused.hip", "ncf_score.hip", "ncf_capi.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 CFLAGS = ["--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17", "-I" + INCLUDE, "-I" + HERE,

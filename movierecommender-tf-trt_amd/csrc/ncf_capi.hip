@@ -685,6 +685,74 @@ int ncf_shard_predict(const ncf_shape_t* s, const ncf_model_t* model, int32_t wo
                      "shard predict");
 }
 
+// ------------------------------------------------------------ all-item scoring + top-k
+
+int ncf_score_supported(const ncf_shape_t* s, int32_t precision) {
+    if (check_shape(s)) return 0;
+    if (precision == NCF_SCORE_FP32) return 1;
+    if (precision == NCF_SCORE_FP16) return ncf::score_fast_supported(*s) ? 1 : 0;
+    return 0;
+}
+
+int ncf_score_workspace_size(const ncf_shape_t* s, int64_t max_users, size_t* bytes) {
+    if (int r = check_shape(s)) return r;
+    if (!bytes) return fail(NCF_EINVAL, "bytes is NULL");
+    if (max_users <= 0 || max_users > ((int64_t)1 << 26))
+        return fail(NCF_EINVAL, "max_users must be in [1, 2^26], got %lld", (long long)max_users);
+    *bytes = ncf::make_score_layout(*s, max_users).total;
+    return 0;
+}
+
+int ncf_score_topk(const ncf_shape_t* s, const ncf_model_t* model, const int32_t* users, int64_t n, int32_t k,
+                   int32_t precision, int32_t* top_items, float* top_scores, void* ws, size_t ws_bytes,
+                   void* stream) {
+    if (int r = check_shape(s)) return r;
+    if (!model || !model->emb || !model->mlp || !users || !top_items || !top_scores || !ws)
+        return fail(NCF_EINVAL, "NULL device pointer");
+    if (k < 1 || k > NCF_SCORE_MAX_K) return fail(NCF_EINVAL, "k must be in [1, %d], got %d", NCF_SCORE_MAX_K, k);
+    if (n <= 0) return 0;
+    if (precision != NCF_SCORE_FP16 && precision != NCF_SCORE_FP32)
+        return fail(NCF_EINVAL, "unknown scoring precision %d", precision);
+    if (precision == NCF_SCORE_FP16 && !ncf::score_fast_supported(*s))
+        return fail(NCF_EINVAL, "the fp16 MFMA scorer needs a 4-layer model with layers[1] <= 64, layers[2] <= 32, "
+                    "layers[3] <= 32, gmf_dim <= 64 (use NCF_SCORE_FP32)");
+    // nothing persists between calls: the layout for n users fits any workspace sized for >= n
+    const ncf::ScoreLayout L = ncf::make_score_layout(*s, n);
+    if (ws_bytes < L.total)
+        return fail(NCF_EINVAL, "score workspace too small: %zu bytes for %lld users (need %zu)", ws_bytes,
+                    (long long)n, L.total);
+    hipStream_t st = (hipStream_t)stream;
+    hipError_t e;
+    if (precision == NCF_SCORE_FP16) {
+        e = ncf::launch_score_prep(*s, L, ws, model->emb, model->mlp, users, n, st);
+        if (e != hipSuccess) return hip_check(e, "score preparation");
+        prof_begin(NCF_K_SCORE, st);
+        e = ncf::launch_score_main(*s, L, ws, n, k, top_items, top_scores, st);
+        prof_end(NCF_K_SCORE, st);
+        return hip_check(e, "score top-k");
+    }
+    const int I = s->num_items;
+    if (I > ncf::kMaxBatch)
+        return fail(NCF_EINVAL, "the fp32 scorer handles catalogues of up to %lld items", (long long)ncf::kMaxBatch);
+    void* pws = ncf::at<char>(ws, L.pred_ws);
+    ncf::WsLayout PL = ncf::make_layout(*s, L.chunk * I > ncf::kMaxBatch ? ncf::kMaxBatch : L.chunk * I);
+    for (int64_t q0 = 0; q0 < n; q0 += L.chunk) {
+        const int64_t nq = n - q0 < L.chunk ? n - q0 : L.chunk;
+        int32_t* pu = ncf::at<int32_t>(ws, L.pu);
+        int32_t* pi = ncf::at<int32_t>(ws, L.pi);
+        float* probs = ncf::at<float>(ws, L.probs);
+        e = ncf::launch_score_pairs(users + q0, nq, I, pu, pi, st);
+        if (e != hipSuccess) return hip_check(e, "score pairs");
+        int nbce = 0;
+        e = ncf::launch_predict_generic(*s, PL, pws, model->emb, model->mlp, pu, pi, nullptr, nq * I, probs,
+                                        ncf::table_ids(*s), &nbce, st);
+        if (e != hipSuccess) return hip_check(e, "score forward");
+        e = ncf::launch_topk_rows(probs, nq, I, k, top_items + q0 * k, top_scores + q0 * k, st);
+        if (e != hipSuccess) return hip_check(e, "score top-k");
+    }
+    return 0;
+}
+
 int ncf_profile_enable(int32_t kernel_mask, int32_t capacity) {
     g_prof.mask = kernel_mask < 0 ? 0u : (uint32_t)kernel_mask;
     for (int k = 0; k < 8; ++k) {

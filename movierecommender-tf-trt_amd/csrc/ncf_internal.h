@@ -173,4 +173,31 @@ hipError_t launch_emb_reg(const ncf_shape_t& s, const WsLayout& L, void* ws, con
 hipError_t launch_stats(const WsLayout& L, void* ws, const float* summary, int nreg_emb, int nreg_mlp,
                         float inv_batch, double* stats, int32_t* step, bool bump_step, hipStream_t st);
 
+// all-item scoring + top-k (ncf_score.hip) ---------------------------------------------------
+struct ScoreDims {
+    int U, I, W, gmf_stride, du, di, G, L0, L1, L2, L3;
+    int off_w2, off_w3, off_out;  // flat offsets of hidden_2 / hidden_3 / output kernels
+    int ks2, ks3, nr3, ksg;       // MFMA k-steps of layer 2 / layer 3 / GMF, layer-3 output registers
+    bool fast;                    // dimensions within the MFMA scorer's limits
+};
+struct ScoreLayout {
+    // MFMA path (empty when the shape is not supported)
+    size_t ic, ig, nega, init2, ug, a2, a3, init3, wh, bo, uok;
+    // exact path: pair lists + probabilities of `chunk` users x all items, generic-forward ws
+    size_t pu, pi, probs, pred_ws, pred_ws_bytes;
+    int64_t chunk;
+    int64_t max_users;
+    size_t total;
+};
+ScoreDims score_dims(const ncf_shape_t& s);
+ScoreLayout make_score_layout(const ncf_shape_t& s, int64_t max_users);
+bool score_fast_supported(const ncf_shape_t& s);
+hipError_t launch_score_prep(const ncf_shape_t& s, const ScoreLayout& L, void* ws, const float* emb,
+                             const float* mlp, const int32_t* users, int64_t n, hipStream_t st);
+hipError_t launch_score_main(const ncf_shape_t& s, const ScoreLayout& L, void* ws, int64_t n, int k,
+                             int32_t* top_items, float* top_scores, hipStream_t st);
+hipError_t launch_score_pairs(const int32_t* users, int64_t nq, int I, int32_t* pu, int32_t* pi, hipStream_t st);
+hipError_t launch_topk_rows(const float* probs, int64_t rows, int I, int k, int32_t* top_items, float* top_scores,
+                            hipStream_t st);
+
 }  // namespace ncf

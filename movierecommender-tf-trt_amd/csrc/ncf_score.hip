@@ -1,0 +1,526 @@
+// All-item scoring + top-k (BASELINE.json config E).
+//
+// Reference workload: movierec/trt_client.py:43-57 sends one user with
+// NUM_ITEMS_PREDICT random items to the served model (output/Sigmoid of
+// model.py:184-194) and keeps the K = 10 best by np.argsort.  Here every user
+// of a list is scored against the WHOLE catalogue and the k best items are
+// kept, best first, ties broken by the lower item id.
+//
+// Fast path (NCF_SCORE_FP16, 4-layer models with layers[1] <= 64,
+// layers[2] <= 32, layers[3] <= 32, gmf_dim <= 64): fp16 operands, fp32
+// accumulation on v_mfma_f32_32x32x16_f16.  The first layer splits over the
+// concatenated input (model.py:171-181):
+//     h1 = relu(a_u + c_i),  a_u = b1 + W1[:du]^T e_u,  c_i = W1[du:]^T e_i
+// and relu(a + c) = a + max(c, -a), so
+//     W2^T h1 = W2^T a_u + W2^T max(c_i, -a_u).
+// W2^T a_u + b2 is a per-user vector (prepared once, fp32) that initialises
+// the layer-2 accumulator; the per-pair operand is a single v_pk_max_f16 of
+// the item term and the negated user term.  Layer 2 and 3 are feature-major
+// MFMA chains (item on the lane, features in registers; a D tile feeds the
+// next MFMA's B operand register-for-register), the GMF term
+// (w_g ⊙ e_u^g) · e_i^g is one 32-user x 32-item MFMA tile per item tile.
+// One wave owns 32 users and sweeps all items in 32-item tiles (the item
+// tiles stream from L2 for every wave of an XCD); a running per-user
+// threshold (the k-th best so far) filters candidates with one compare and
+// a ballot, and the rare insertions into the per-user list (LDS) run after
+// the tile.  Ranking is by the logit z (sigmoid is monotonic); the reported
+// score is sigmoid(z).
+//
+// Exact path (NCF_SCORE_FP32, any shape): the generic fp32 forward
+// (ncf_predict) over (user, item) pairs for a chunk of users, then a per-user
+// top-k by probability — the reference's own ranking quantity.
+
+#include <cmath>
+
+#include "ncf_common.h"
+#include "ncf_internal.h"
+
+namespace ncf {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef float sf32x16 __attribute__((ext_vector_type(16)));
+typedef uint32_t su32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kScoreTopMax = 32;  // largest k of the MFMA path
+
+__device__ __forceinline__ int drow_s(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+__device__ __forceinline__ sf32x16 mfma16(f16x8 a, f16x8 b, sf32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+// elementwise max of packed halves (v_pk_max_f16, no IEEE canonicalisation of the inputs)
+__device__ __forceinline__ f16x8 pkmax(f16x8 a, f16x8 b) {
+    su32x4 x = __builtin_bit_cast(su32x4, a), y = __builtin_bit_cast(su32x4, b), r;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) asm("v_pk_max_f16 %0, %1, %2" : "=v"(r[i]) : "v"(x[i]), "v"(y[i]));
+    return __builtin_bit_cast(f16x8, r);
+}
+
+__device__ __forceinline__ f16x8 relu_f16(f16x8 a) {
+    su32x4 x = __builtin_bit_cast(su32x4, a), r;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) asm("v_pk_max_f16 %0, %1, 0" : "=v"(r[i]) : "v"(x[i]));
+    return __builtin_bit_cast(f16x8, r);
+}
+
+// ----------------------------------------------------------------------------- preparation
+
+// Weight fragments.  a2[s][lane][e] = W2[k][i] (lane (i, h), k = 16s + 8h + e);
+// a3[s][lane][e] = W3[x][i] with x = 16s + 8(e>>2) + 4h + (e&3), the row of the layer-2 D
+// tile that register 8s+e of lane half h holds; init3/wh[h][r] = b3 / w_out at row drow(r, h).
+__global__ __launch_bounds__(kBlock) void k_score_weights(const float* __restrict__ mlp, ScoreDims d,
+                                                          _Float16* __restrict__ a2, _Float16* __restrict__ a3,
+                                                          float* __restrict__ init3, float* __restrict__ wh,
+                                                          float* __restrict__ bo) {
+    const float* W2 = mlp + d.off_w2;
+    const float* W3 = mlp + d.off_w3;
+    const float* b3 = W3 + d.L2 * d.L3;
+    const float* wout = mlp + d.off_out;
+    for (int x = threadIdx.x; x < d.ks2 * 512; x += kBlock) {
+        const int s = x >> 9, lane = (x >> 3) & 63, e = x & 7;
+        const int i = lane & 31, k = 16 * s + 8 * (lane >> 5) + e;
+        a2[x] = (_Float16)((k < d.L1 && i < d.L2) ? W2[k * d.L2 + i] : 0.0f);
+    }
+    for (int x = threadIdx.x; x < d.ks3 * 512; x += kBlock) {
+        const int s = x >> 9, lane = (x >> 3) & 63, e = x & 7;
+        const int i = lane & 31, row = 16 * s + 8 * (e >> 2) + 4 * (lane >> 5) + (e & 3);
+        a3[x] = (_Float16)((row < d.L2 && i < d.L3) ? W3[row * d.L3 + i] : 0.0f);
+    }
+    if (threadIdx.x < 32) {
+        const int h = threadIdx.x >> 4, r = threadIdx.x & 15, row = drow_s(r, h);
+        init3[threadIdx.x] = row < d.L3 ? b3[row] : 0.0f;
+        wh[threadIdx.x] = row < d.L3 ? wout[d.G + row] : 0.0f;
+    }
+    if (threadIdx.x == 0) bo[0] = wout[d.G + d.L3];
+}
+
+// Item tiles, fragment-major: ic[((t*ks2 + s)*64 + lane)*8 + e] = c_i[16s + 8h + e] for item
+// i = 32t + (lane & 31), h = lane >> 5 (zero past num_items / L1); ig likewise for e_i^g.
+__global__ __launch_bounds__(kBlock) void k_score_items(const float* __restrict__ emb, const float* __restrict__ mlp,
+                                                        ScoreDims d, _Float16* __restrict__ ic,
+                                                        _Float16* __restrict__ ig) {
+    __shared__ float xe[32][65];  // the tile's item MLP vectors (di <= 64)
+    const int t = blockIdx.x;
+    const float* W1 = mlp;  // hidden_1 kernel [L0][L1] at offset 0
+    for (int x = threadIdx.x; x < 32 * 64; x += kBlock) {
+        const int j = x >> 6, k = x & 63, item = 32 * t + j;
+        xe[j][k] = (item < d.I && k < d.di) ? emb[(int64_t)(d.U + item) * d.W + d.gmf_stride + k] : 0.0f;
+    }
+    __syncthreads();
+    const int L1P = 16 * d.ks2;
+    for (int x = threadIdx.x; x < 32 * L1P; x += kBlock) {
+        const int j = x / L1P, f = x - j * L1P;
+        float c = 0.0f;
+        if (f < d.L1)
+            for (int k = 0; k < d.di; ++k) c = fmaf(W1[(d.du + k) * d.L1 + f], xe[j][k], c);
+        const int s = f >> 4, h = (f >> 3) & 1, e = f & 7;
+        ic[(((int64_t)t * d.ks2 + s) * 64 + h * 32 + j) * 8 + e] = (_Float16)c;
+    }
+    const int GP = 16 * d.ksg;
+    for (int x = threadIdx.x; x < 32 * GP; x += kBlock) {
+        const int j = x / GP, f = x - j * GP, item = 32 * t + j;
+        const float g = (item < d.I && f < d.G) ? emb[(int64_t)(d.U + item) * d.W + f] : 0.0f;
+        const int s = f >> 4, h = (f >> 3) & 1, e = f & 7;
+        ig[(((int64_t)t * d.ksg + s) * 64 + h * 32 + j) * 8 + e] = (_Float16)g;
+    }
+}
+
+// Per-user terms (one 64-thread block per user slot q; slots past n are zero):
+// nega[q][f] = -(b1 + W1[:du]^T e_u)[f]; init2[q][h][r] = (b2 + W2^T a_u)[drow(r, h)];
+// ug = GMF A fragments (w_g ⊙ e_u^g) of the 32-user block.
+__global__ __launch_bounds__(64) void k_score_users(const float* __restrict__ emb, const float* __restrict__ mlp,
+                                                    ScoreDims d, const int32_t* __restrict__ users, int64_t n,
+                                                    _Float16* __restrict__ nega, float* __restrict__ init2,
+                                                    _Float16* __restrict__ ug, int32_t* __restrict__ uok) {
+    __shared__ float a[64];
+    __shared__ float xu[64];
+    const int64_t q = blockIdx.x;
+    const int uid = q < n ? users[q] : -1;
+    const bool valid = uid >= 0 && uid < d.U;  // out-of-range ids: no recommendations (items -1)
+    const int u = valid ? uid : 0;
+    if (threadIdx.x == 0) uok[q] = valid ? 1 : 0;
+    const float* W1 = mlp;
+    const float* b1 = mlp + d.L0 * d.L1;
+    const float* W2 = mlp + d.off_w2;
+    const float* b2 = W2 + d.L1 * d.L2;
+    const float* wout = mlp + d.off_out;
+    const int f = threadIdx.x;
+    xu[f] = (valid && f < d.du) ? emb[(int64_t)u * d.W + d.gmf_stride + f] : 0.0f;
+    __syncthreads();
+    float av = 0.0f;
+    if (valid && f < d.L1) {
+        av = b1[f];
+        for (int k = 0; k < d.du; ++k) av = fmaf(W1[k * d.L1 + f], xu[k], av);
+    }
+    a[f] = av;
+    if (f < 16 * d.ks2) nega[q * 16 * d.ks2 + f] = (_Float16)(-av);
+    __syncthreads();
+    if (f < 32) {
+        const int h = f >> 4, r = f & 15, row = drow_s(r, h);
+        float v = 0.0f;
+        if (valid && row < d.L2) {
+            v = b2[row];
+            for (int k = 0; k < d.L1; ++k) v = fmaf(W2[k * d.L2 + row], a[k], v);
+        }
+        init2[q * 32 + f] = v;
+    }
+    if (f < 16 * d.ksg) {
+        const float g = (valid && f < d.G) ? wout[f] * emb[(int64_t)u * d.W + f] : 0.0f;
+        const int64_t ub = q >> 5;
+        const int i = (int)(q & 31), s = f >> 4, h = (f >> 3) & 1, e = f & 7;
+        ug[((ub * d.ksg + s) * 64 + h * 32 + i) * 8 + e] = (_Float16)g;
+    }
+}
+
+// ----------------------------------------------------------------------------- MFMA scorer
+
+struct ScoreArgs {
+    const f16x8* ic;
+    const f16x8* ig;
+    const _Float16* nega;
+    const float4* init2;
+    const f16x8* ug;
+    const f16x8* a2;
+    const f16x8* a3;
+    const float* init3;
+    const float* wh;
+    const float* bo;
+    const int32_t* uok;
+    int64_t n;
+    int nub, ntiles, num_items, k;
+    int32_t* top_items;
+    float* top_scores;
+};
+
+template <int KS2, int KS3, int NR3, int KSG>
+__global__ __launch_bounds__(kBlock) void k_score_topk(ScoreArgs a) {
+    constexpr int L1P = 16 * KS2;
+    __shared__ __attribute__((aligned(16))) _Float16 s_nega[4][32][L1P];
+    __shared__ float4 s_init2[4][32][8];
+    __shared__ float2 s_top[4][32][kScoreTopMax];
+    __shared__ float s_z[4][32][32];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, j = lane & 31;
+    const int ub = blockIdx.x * 4 + w;
+    const bool active = ub < a.nub;
+    const int64_t q0 = (int64_t)(active ? ub : 0) * 32;
+    const int K = a.k;
+    // stage this wave's users
+    {
+        const float4* src = reinterpret_cast<const float4*>(a.nega + q0 * L1P);
+        float4* dst = reinterpret_cast<float4*>(&s_nega[w][0][0]);
+        for (int x = lane; x < 32 * L1P / 8; x += 64) dst[x] = src[x];
+        for (int x = lane; x < 32 * 8; x += 64) s_init2[w][x >> 3][x & 7] = a.init2[q0 * 8 + x];
+        for (int x = lane; x < 32 * kScoreTopMax; x += 64)
+            s_top[w][x / kScoreTopMax][x % kScoreTopMax] = make_float2(-INFINITY, __int_as_float(-1));
+    }
+    __syncthreads();
+    if (!active) return;
+
+    f16x8 A2[KS2], A3[KS3], AG[KSG > 0 ? KSG : 1];
+#pragma unroll
+    for (int s = 0; s < KS2; ++s) A2[s] = a.a2[s * 64 + lane];
+#pragma unroll
+    for (int s = 0; s < KS3; ++s) A3[s] = a.a3[s * 64 + lane];
+#pragma unroll
+    for (int s = 0; s < KSG; ++s) AG[s] = a.ug[((int64_t)ub * KSG + s) * 64 + lane];
+    sf32x16 init3;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) init3[r] = a.init3[h * 16 + r];
+    float wh[NR3];
+#pragma unroll
+    for (int r = 0; r < NR3; ++r) wh[r] = a.wh[h * 16 + r];
+    const float bo = a.bo[0];
+    // lane q (< 32) holds user q0+q's admission threshold (k-th best so far)
+    float thr = (lane < 32 && a.uok[q0 + (lane & 31)]) ? -INFINITY : INFINITY;
+
+    f16x8 BC[KS2], BG[KSG > 0 ? KSG : 1];
+#pragma unroll
+    for (int s = 0; s < KS2; ++s) BC[s] = a.ic[s * 64 + lane];
+#pragma unroll
+    for (int s = 0; s < KSG; ++s) BG[s] = a.ig[s * 64 + lane];
+
+    for (int t = 0; t < a.ntiles; ++t) {
+        // next tile's operands (consumed next iteration)
+        const int tn = t + 1 < a.ntiles ? t + 1 : t;
+        f16x8 NC[KS2], NG[KSG > 0 ? KSG : 1];
+#pragma unroll
+        for (int s = 0; s < KS2; ++s) NC[s] = a.ic[((int64_t)tn * KS2 + s) * 64 + lane];
+#pragma unroll
+        for (int s = 0; s < KSG; ++s) NG[s] = a.ig[((int64_t)tn * KSG + s) * 64 + lane];
+
+        sf32x16 accg;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) accg[r] = bo;
+#pragma unroll
+        for (int s = 0; s < KSG; ++s) accg = mfma16(AG[s], BG[s], accg);
+
+        const bool item_ok = h == 0 && 32 * t + j < a.num_items;
+        uint32_t flagged = 0;
+#pragma unroll
+        for (int q = 0; q < 32; ++q) {
+            sf32x16 acc2;
+            {
+                const float4* ip = &s_init2[w][q][h * 4];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const float4 v = ip[c];
+                    acc2[4 * c + 0] = v.x; acc2[4 * c + 1] = v.y; acc2[4 * c + 2] = v.z; acc2[4 * c + 3] = v.w;
+                }
+            }
+#pragma unroll
+            for (int s = 0; s < KS2; ++s) {
+                const f16x8 na = *reinterpret_cast<const f16x8*>(&s_nega[w][q][16 * s + 8 * h]);
+                acc2 = mfma16(A2[s], pkmax(BC[s], na), acc2);
+            }
+            sf32x16 acc3 = init3;
+#pragma unroll
+            for (int s = 0; s < KS3; ++s) {
+                f16x8 x;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) x[e] = (_Float16)acc2[8 * s + e];
+                acc3 = mfma16(A3[s], relu_f16(x), acc3);
+            }
+            float z = 0.0f;
+#pragma unroll
+            for (int r = 0; r < NR3; ++r) z = fmaf(fmaxf(acc3[r], 0.0f), wh[r], z);
+            const int hq = (q >> 2) & 1, rq = (q & 3) + 4 * (q >> 3);
+            z += (h == hq) ? accg[rq] : 0.0f;
+            // v_permlane32_swap(vdst = z, src = z): the new src holds the upper half's z in lanes
+            // 0-31, so lanes 0-31 (the only ones read below) get the full sum
+            const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(z), __float_as_uint(z), false, false);
+            z += __uint_as_float(sw[1]);
+            const float tq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(thr), q));
+            if (__ballot(item_ok && z > tq)) {
+                if (h == 0) s_z[w][q][j] = z;
+                flagged |= 1u << q;
+            }
+        }
+        // insertions (rare once the lists fill): ascending item order, ties keep the earlier item
+        while (flagged) {
+            const int q = __builtin_ctz(flagged);
+            flagged &= flagged - 1;
+            float tq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(thr), q));
+            const float zl = s_z[w][q][j];
+            uint64_t m = __ballot(item_ok && zl > tq);
+            float2 ent = lane < K ? s_top[w][q][lane] : make_float2(-INFINITY, __int_as_float(-1));
+            while (m) {
+                const int c = __builtin_ctzll(m);
+                m &= m - 1;
+                const float zc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(zl), c));
+                if (!(zc > tq)) continue;
+                const int p = __popcll(__ballot(lane < K && ent.x >= zc));
+                const float px = __shfl_up(ent.x, 1, 64), py = __shfl_up(ent.y, 1, 64);
+                if (lane == p) ent = make_float2(zc, __int_as_float(32 * t + c));
+                else if (lane > p) ent = make_float2(px, py);
+                tq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ent.x), K - 1));
+            }
+            if (lane < K) s_top[w][q][lane] = ent;
+            if (lane == q) thr = tq;
+        }
+#pragma unroll
+        for (int s = 0; s < KS2; ++s) BC[s] = NC[s];
+#pragma unroll
+        for (int s = 0; s < KSG; ++s) BG[s] = NG[s];
+    }
+    for (int q = 0; q < 32; ++q) {
+        if (q0 + q >= a.n) break;
+        if (lane < K) {
+            const float2 e = s_top[w][q][lane];
+            const int item = __float_as_int(e.y);
+            a.top_items[(q0 + q) * K + lane] = item;
+            a.top_scores[(q0 + q) * K + lane] = item >= 0 ? 1.0f / (1.0f + expf(-e.x)) : 0.0f;
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------- exact path
+
+// pair lists of users [q0, q0 + nq) x all items
+__global__ __launch_bounds__(kBlock) void k_score_pairs(const int32_t* __restrict__ users, int64_t nq, int I,
+                                                        int32_t* __restrict__ pu, int32_t* __restrict__ pi) {
+    const int64_t x = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (x >= nq * I) return;
+    const int64_t q = x / I;
+    pu[x] = users[q];
+    pi[x] = (int32_t)(x - q * I);
+}
+
+// per row of I probabilities: the k best (descending, ties: lower item), k rounds of a
+// block-wide arg-max over the items that come after the previous pick in that order
+__global__ __launch_bounds__(kBlock) void k_topk_rows(const float* __restrict__ probs, int I, int K,
+                                                      int32_t* __restrict__ top_items,
+                                                      float* __restrict__ top_scores) {
+    __shared__ float sv[kBlock / 64];
+    __shared__ int si[kBlock / 64];
+    const float* p = probs + (int64_t)blockIdx.x * I;
+    float pv = INFINITY;
+    int pidx = -1;
+    for (int r = 0; r < K; ++r) {
+        float bv = -INFINITY;
+        int bi = INT32_MAX;
+        for (int i = threadIdx.x; i < I; i += kBlock) {
+            const float v = p[i];
+            const bool after = v < pv || (v == pv && i > pidx);
+            if (after && (v > bv || (v == bv && i < bi))) { bv = v; bi = i; }
+        }
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            const float ov = __shfl_xor(bv, d, 64);
+            const int oi = __shfl_xor(bi, d, 64);
+            if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+        }
+        __syncthreads();
+        if ((threadIdx.x & 63) == 0) { sv[threadIdx.x >> 6] = bv; si[threadIdx.x >> 6] = bi; }
+        __syncthreads();
+        bv = sv[0];
+        bi = si[0];
+        for (int x = 1; x < kBlock / 64; ++x)
+            if (sv[x] > bv || (sv[x] == bv && si[x] < bi)) { bv = sv[x]; bi = si[x]; }
+        if (threadIdx.x == 0) {
+            const bool ok = bi != INT32_MAX;
+            top_items[(int64_t)blockIdx.x * K + r] = ok ? bi : -1;
+            top_scores[(int64_t)blockIdx.x * K + r] = ok ? bv : 0.0f;
+        }
+        pv = bv;
+        pidx = bi;
+    }
+}
+
+// ----------------------------------------------------------------------------- host side
+
+static inline int cdiv_i(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+ScoreDims score_dims(const ncf_shape_t& s) {
+    ScoreDims d{};
+    d.U = s.num_users;
+    d.I = s.num_items;
+    d.W = s.row_width;
+    d.gmf_stride = s.gmf_stride;
+    d.du = s.du;
+    d.di = s.di;
+    d.G = s.gmf_dim;
+    d.L0 = s.layers[0];
+    d.L1 = s.num_layers > 1 ? s.layers[1] : 0;
+    d.L2 = s.num_layers > 2 ? s.layers[2] : 0;
+    d.L3 = s.num_layers > 3 ? s.layers[3] : 0;
+    d.off_w2 = s.num_layers > 2 ? s.layer_off[2] : 0;
+    d.off_w3 = s.num_layers > 3 ? s.layer_off[3] : 0;
+    d.off_out = s.layer_off[0];
+    d.ks2 = cdiv_i(d.L1, 16);
+    d.ks3 = cdiv_i(d.L2, 16);
+    d.nr3 = 4 * cdiv_i(d.L3, 8);
+    d.ksg = cdiv_i(d.G, 16);
+    d.fast = s.num_layers == 4 && d.L1 <= 64 && d.L2 <= 32 && d.L3 <= 32 && d.G <= 64 && d.du <= 64 &&
+             d.di <= 64;
+    return d;
+}
+
+ScoreLayout make_score_layout(const ncf_shape_t& s, int64_t max_users) {
+    ScoreLayout L{};
+    const ScoreDims d = score_dims(s);
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        size_t o = off;
+        off = (off + bytes + 255) / 256 * 256;
+        return o;
+    };
+    L.max_users = max_users;
+    const int64_t nub = (max_users + 31) / 32;
+    const int64_t nt = (s.num_items + 31) / 32;
+    if (d.fast) {
+        L.ic = take((size_t)nt * d.ks2 * 64 * 16);
+        L.ig = take((size_t)nt * (d.ksg > 0 ? d.ksg : 1) * 64 * 16);
+        L.nega = take((size_t)nub * 32 * d.ks2 * 16 * 2);
+        L.init2 = take((size_t)nub * 32 * 32 * 4);
+        L.ug = take((size_t)nub * (d.ksg > 0 ? d.ksg : 1) * 64 * 16);
+        L.a2 = take((size_t)d.ks2 * 64 * 16);
+        L.a3 = take((size_t)d.ks3 * 64 * 16);
+        L.init3 = take(32 * 4);
+        L.wh = take(32 * 4);
+        L.bo = take(4);
+        L.uok = take((size_t)nub * 32 * 4);
+    }
+    // exact path: chunks of users x all items through the generic forward
+    int64_t chunk = kMaxBatch / s.num_items;
+    if (chunk < 1) chunk = 1;
+    if (chunk > max_users) chunk = max_users;
+    L.chunk = chunk;
+    const int64_t np = chunk * s.num_items;
+    L.pu = take((size_t)np * 4);
+    L.pi = take((size_t)np * 4);
+    L.probs = take((size_t)np * 4);
+    L.pred_ws = off;
+    L.pred_ws_bytes = make_layout(s, np > kMaxBatch ? kMaxBatch : np).total;
+    L.total = off + L.pred_ws_bytes;
+    return L;
+}
+
+hipError_t launch_score_prep(const ncf_shape_t& s, const ScoreLayout& L, void* ws, const float* emb,
+                             const float* mlp, const int32_t* users, int64_t n, hipStream_t st) {
+    const ScoreDims d = score_dims(s);
+    const int nt = cdiv_i(s.num_items, 32);
+    const int nub = cdiv_i(n, 32);
+    launch(k_score_weights, 1, kBlock, 0, st, mlp, d, at<_Float16>(ws, L.a2), at<_Float16>(ws, L.a3),
+           at<float>(ws, L.init3), at<float>(ws, L.wh), at<float>(ws, L.bo));
+    launch(k_score_items, nt, kBlock, 0, st, emb, mlp, d, at<_Float16>(ws, L.ic), at<_Float16>(ws, L.ig));
+    launch(k_score_users, nub * 32, 64, 0, st, emb, mlp, d, users, n, at<_Float16>(ws, L.nega),
+           at<float>(ws, L.init2), at<_Float16>(ws, L.ug), at<int32_t>(ws, L.uok));
+    return hipGetLastError();
+}
+
+hipError_t launch_score_main(const ncf_shape_t& s, const ScoreLayout& L, void* ws, int64_t n, int k,
+                             int32_t* top_items, float* top_scores, hipStream_t st) {
+    const ScoreDims d = score_dims(s);
+    const int nub = cdiv_i(n, 32);
+    ScoreArgs a;
+    a.ic = at<const f16x8>(ws, L.ic);
+    a.ig = at<const f16x8>(ws, L.ig);
+    a.nega = at<const _Float16>(ws, L.nega);
+    a.init2 = at<const float4>(ws, L.init2);
+    a.ug = at<const f16x8>(ws, L.ug);
+    a.a2 = at<const f16x8>(ws, L.a2);
+    a.a3 = at<const f16x8>(ws, L.a3);
+    a.init3 = at<const float>(ws, L.init3);
+    a.wh = at<const float>(ws, L.wh);
+    a.bo = at<const float>(ws, L.bo);
+    a.uok = at<const int32_t>(ws, L.uok);
+    a.n = n;
+    a.nub = nub;
+    a.ntiles = cdiv_i(s.num_items, 32);
+    a.num_items = s.num_items;
+    a.k = k;
+    a.top_items = top_items;
+    a.top_scores = top_scores;
+    const int grid = cdiv_i(nub, 4);
+#define NCF_SCORE_LAUNCH(A, B, C, D) launch(k_score_topk<A, B, C, D>, grid, kBlock, 0, st, a)
+    if (d.ks2 == 4 && d.ks3 == 2 && d.nr3 == 8 && d.ksg == 4) NCF_SCORE_LAUNCH(4, 2, 8, 4);       // ml-20m NeuMF (configs C/E)
+    else if (d.ks2 == 4 && d.ks3 == 2 && d.nr3 == 8 && d.ksg == 0) NCF_SCORE_LAUNCH(4, 2, 8, 0);  // its MLP-only form
+    else if (d.ks2 == 2 && d.ks3 == 1 && d.nr3 == 4 && d.ksg == 1) NCF_SCORE_LAUNCH(2, 1, 4, 1);  // ml-1m NeuMF (config B)
+    else if (d.ks2 == 2 && d.ks3 == 1 && d.nr3 == 4 && d.ksg == 0) NCF_SCORE_LAUNCH(2, 1, 4, 0);  // trainer default [64,32,16,8]
+    else return hipErrorInvalidValue;
+#undef NCF_SCORE_LAUNCH
+    return hipGetLastError();
+}
+
+bool score_fast_supported(const ncf_shape_t& s) {
+    const ScoreDims d = score_dims(s);
+    if (!d.fast) return false;
+    return (d.ks2 == 4 && d.ks3 == 2 && d.nr3 == 8 && (d.ksg == 4 || d.ksg == 0)) ||
+           (d.ks2 == 2 && d.ks3 == 1 && d.nr3 == 4 && (d.ksg == 1 || d.ksg == 0));
+}
+
+hipError_t launch_score_pairs(const int32_t* users, int64_t nq, int I, int32_t* pu, int32_t* pi, hipStream_t st) {
+    const int64_t np = nq * I;
+    launch(k_score_pairs, cdiv_i(np, kBlock), kBlock, 0, st, users, nq, I, pu, pi);
+    return hipGetLastError();
+}
+
+hipError_t launch_topk_rows(const float* probs, int64_t rows, int I, int k, int32_t* top_items, float* top_scores,
+                            hipStream_t st) {
+    if (rows <= 0) return hipSuccess;
+    launch(k_topk_rows, (unsigned)rows, kBlock, 0, st, probs, I, k, top_items, top_scores);
+    return hipGetLastError();
+}
+
+}  // namespace ncf

@@ -84,11 +84,16 @@ _SIGNATURES = {
     "ncf_shard_apply_update": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _i32, _vp,
                                               _vp, _i64, _vp, _vp, _vp, _vp, ctypes.c_size_t, _vp]),
     "ncf_shard_predict": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _i32, _i64, _vp, _vp, ctypes.c_size_t, _vp]),
+    "ncf_score_supported": (ctypes.c_int, [_P(NcfShape), _i32]),
+    "ncf_score_workspace_size": (ctypes.c_int, [_P(NcfShape), _i64, _P(ctypes.c_size_t)]),
+    "ncf_score_topk": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _vp, _i64, _i32, _i32, _vp, _vp, _vp,
+                                      ctypes.c_size_t, _vp]),
     "ncf_profile_enable": (ctypes.c_int, [_i32, _i32]),
     "ncf_profile_read": (ctypes.c_int, [_i32, _P(ctypes.c_double), _P(_i64)]),
 }
 EXPORTED = sorted(_SIGNATURES)
-K_INDEX, K_FWD_BWD, K_EMB_UPDATE, K_MLP_UPDATE, K_METRICS = 1, 2, 3, 4, 5
+K_INDEX, K_FWD_BWD, K_EMB_UPDATE, K_MLP_UPDATE, K_METRICS, K_SCORE = 1, 2, 3, 4, 5, 6
+NCF_SCORE_FP16, NCF_SCORE_FP32, NCF_SCORE_MAX_K = 0, 1, 32
 
 
 def profile_enable(kernels, capacity):

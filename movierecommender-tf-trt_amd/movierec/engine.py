@@ -211,6 +211,33 @@ class NCFEngine(object):
                                           N.stream_handle(self.device)))
         return hit, dcg
 
+    # ---------------------------------------------- all-item scoring + top-k
+    def score_topk(self, users, k=10, precision="fp16"):
+        """For each user id: the k items with the highest score over the whole catalogue, best
+        first (ties: lower item id), and their sigmoid outputs — BASELINE config E, the
+        workload of trt_client.py:43-57 batched over users.  precision "fp16": MFMA scorer
+        (fp16 operands, fp32 accumulation); "fp32": the generic fp32 forward, any shape."""
+        prec = {"fp16": N.NCF_SCORE_FP16, "fp32": N.NCF_SCORE_FP32}.get(precision)
+        if prec is None:
+            raise ValueError("precision must be 'fp16' or 'fp32', got %r" % (precision,))
+        L = N.lib()
+        if not L.ncf_score_supported(ctypes.byref(self.shape), prec):
+            raise ValueError("model shape not supported by the %s scorer" % precision)
+        u = self._ids(users)
+        n = u.numel()
+        items = torch.empty(n, int(k), dtype=torch.int32, device=self.device)
+        scores = torch.empty(n, int(k), dtype=torch.float32, device=self.device)
+        if n == 0:
+            return items, scores
+        nbytes = ctypes.c_size_t()
+        N.check(L.ncf_score_workspace_size(ctypes.byref(self.shape), n, ctypes.byref(nbytes)))
+        if getattr(self, "_score_ws", None) is None or self._score_ws.numel() < nbytes.value:
+            self._score_ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=self.device)
+        N.check(L.ncf_score_topk(ctypes.byref(self.shape), ctypes.byref(self.model_s), N.ptr(u), n, int(k), prec,
+                                 N.ptr(items), N.ptr(scores), N.ptr(self._score_ws), self._score_ws.numel(),
+                                 N.stream_handle(self.device)))
+        return items, scores
+
     # ------------------------------------------------- data-parallel split
     def alloc_grads(self, rows=None):
         """(dense embedding grad [rows x row_width], dense-layer grad, summary); ``rows`` >=

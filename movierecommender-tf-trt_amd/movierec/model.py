@@ -357,6 +357,18 @@ class MovierecModel(object):
             eng.evaluate(xu, xi, y, group=group, k=k, stats=stats)
         return eng.read_stats(stats)
 
+    def recommend(self, user_ids, k=10, precision="fp16"):
+        """Top-k recommendations over the whole catalogue (new; BASELINE config E): the
+        serving workload of trt_client.py:43-57 — score items for a user with the model's
+        sigmoid output and keep the K = 10 best (``np.argsort(output)[-K:][::-1]``) — for
+        every user of ``user_ids`` and every item.  Returns numpy ``(items (n, k) int32,
+        scores (n, k) float32)``, best first, ties broken by the lower item id."""
+        user_ids = np.asarray(user_ids).reshape(-1)
+        if user_ids.size and (user_ids.min() < 0 or user_ids.max() >= self._num_users):
+            raise ValueError("user id out of range [0, %d)" % self._num_users)
+        items, scores = self.model.engine.score_topk(user_ids, k=k, precision=precision)
+        return items.cpu().numpy(), scores.cpu().numpy()
+
 
 def _prefetch(gen, order, depth):
     """Produce ``gen[i]`` for i in order on one background thread (Keras'

@@ -302,6 +302,32 @@ def group_metrics(pred, labels, group, k):
 
 
 # ---------------------------------------------------------------------------
+# all-item scoring + top-k (BASELINE config E)
+# ---------------------------------------------------------------------------
+
+def score_all_items(shape, w, users):
+    """Logits z (n_users, num_items) of every (user, item) pair: the forward of
+    ``model.py:154-188`` without the sigmoid, the workload ``trt_client.py:43-57``
+    sends to the served model for one user and NUM_ITEMS_PREDICT random items."""
+    users = np.asarray(users).reshape(-1).astype(np.int64)
+    items = np.arange(shape.num_items)
+    out = np.empty((users.size, shape.num_items))
+    for q, u in enumerate(users):
+        _, c = forward(shape, w, np.full(shape.num_items, u), items)
+        out[q] = c["z"]
+    return out
+
+
+def top_k_items(scores, k):
+    """Per row: the k best columns, best first, ties broken by the lower column index
+    (``trt_client.py:55-57`` takes ``np.argsort(output)[-K:][::-1]``, whose tie order numpy
+    leaves unspecified; the build fixes it to the stable order).  Returns (items, scores)."""
+    scores = np.asarray(scores)
+    idx = np.argsort(-scores, axis=1, kind="stable")[:, :k]
+    return idx.astype(np.int32), np.take_along_axis(scores, idx, axis=1)
+
+
+# ---------------------------------------------------------------------------
 # conversion helpers to / from the device layout used by the HIP library
 # ---------------------------------------------------------------------------
 

@@ -63,3 +63,18 @@ def test_workspace_size_scales_with_batch():
     assert b.value > a.value > 0
     with pytest.raises(ValueError):
         N.check(N.lib().ncf_workspace_size(ctypes.byref(s), 0, ctypes.byref(a)))
+
+
+def test_score_support_and_workspace():
+    L = N.lib()
+    c = _shape(138493, 27278, [128, 64, 32, 16], 64)
+    assert L.ncf_score_supported(ctypes.byref(c), N.NCF_SCORE_FP16) == 1
+    assert L.ncf_score_supported(ctypes.byref(c), N.NCF_SCORE_FP32) == 1
+    d = _shape(1000, 500, [256, 128, 64, 32], 128)   # config D widths: fp32 scorer only
+    assert L.ncf_score_supported(ctypes.byref(d), N.NCF_SCORE_FP16) == 0
+    a, b = ctypes.c_size_t(), ctypes.c_size_t()
+    N.check(L.ncf_score_workspace_size(ctypes.byref(c), 32, ctypes.byref(a)))
+    N.check(L.ncf_score_workspace_size(ctypes.byref(c), 138493, ctypes.byref(b)))
+    assert b.value > a.value > 0
+    with pytest.raises(ValueError):
+        N.check(L.ncf_score_workspace_size(ctypes.byref(c), 0, ctypes.byref(a)))

@@ -87,3 +87,18 @@ def test_adam_matches_closed_form_first_step():
     exp = np.array([1.0, -2.0]) - lr_t * (0.1 * np.array([0.5, -0.25])) / (
         np.sqrt(0.001 * np.array([0.25, 0.0625])) + 1e-7)
     np.testing.assert_allclose(w["a"], exp, rtol=1e-12)
+
+
+def test_top_k_items_order_and_ties():
+    s = np.array([[0.1, 0.9, 0.5, 0.9, 0.2], [3.0, 3.0, 3.0, 1.0, 4.0]])
+    items, vals = O.top_k_items(s, 3)
+    np.testing.assert_array_equal(items, [[1, 3, 2], [4, 0, 1]])
+    np.testing.assert_allclose(vals, [[0.9, 0.9, 0.5], [4.0, 3.0, 3.0]])
+
+
+def test_score_all_items_matches_forward():
+    shape = O.NCFShape(6, 9, [8, 6, 4], 4)
+    w = O.init_weights(shape, seed=2)
+    z = O.score_all_items(shape, w, [0, 5])
+    _, c = O.forward(shape, w, [5] * 9, np.arange(9))
+    np.testing.assert_allclose(z[1], c["z"])
