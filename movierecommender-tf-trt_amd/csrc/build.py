@@ -16,6 +16,9 @@ INCLUDE = os.path.join(ROOT, "include")
 OUT_DIR = os.path.join(PKG, "movierec", "_lib")
 LIB = os.path.join(OUT_DIR, "libmovierec_ncf.so")
 SOURCES = ["ncf_index.hip", "ncf_update.hip", "ncf_generic.hip", "ncf_fused.hip", "ncf_score.hip", "ncf_capi.hip"]
+# per-source extra flags: the scorer keeps its MFMA accumulators in VGPRs (no v_accvgpr_read
+# before every epilogue op; its 226 registers fit the unified file at 2 waves/SIMD)
+EXTRA = {"ncf_score.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 CFLAGS = ["--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17", "-I" + INCLUDE, "-I" + HERE,
@@ -39,7 +42,8 @@ def build(force=False, verbose=False, defines=(), out=None):
 
     def compile_one(src):
         obj = os.path.join(obj_dir, src.replace(".hip", ".o"))
-        cmd = [HIPCC] + CFLAGS + ["-D" + d for d in defines] + ["-c", os.path.join(HERE, src), "-o", obj]
+        cmd = ([HIPCC] + CFLAGS + EXTRA.get(src, []) + ["-D" + d for d in defines] +
+               ["-c", os.path.join(HERE, src), "-o", obj])
         if verbose:
             print(" ".join(cmd))
         r = subprocess.run(cmd, capture_output=True, text=True)

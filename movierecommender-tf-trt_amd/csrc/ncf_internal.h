@@ -182,7 +182,7 @@ struct ScoreDims {
 };
 struct ScoreLayout {
     // MFMA path (empty when the shape is not supported)
-    size_t ic, ig, nega, init2, ug, a2, a3, init3, wh, bo, uok;
+    size_t ic, ig, nega, init2, ug, a2, a3, init3, wh, bo, uok, part, gthr;
     // exact path: pair lists + probabilities of `chunk` users x all items, generic-forward ws
     size_t pu, pi, probs, pred_ws, pred_ws_bytes;
     int64_t chunk;

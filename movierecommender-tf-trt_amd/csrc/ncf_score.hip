@@ -132,14 +132,18 @@ __global__ __launch_bounds__(kBlock) void k_score_items(const float* __restrict_
 __global__ __launch_bounds__(64) void k_score_users(const float* __restrict__ emb, const float* __restrict__ mlp,
                                                     ScoreDims d, const int32_t* __restrict__ users, int64_t n,
                                                     _Float16* __restrict__ nega, float* __restrict__ init2,
-                                                    _Float16* __restrict__ ug, int32_t* __restrict__ uok) {
+                                                    _Float16* __restrict__ ug, int32_t* __restrict__ uok,
+                                                    int32_t* __restrict__ gthr) {
     __shared__ float a[64];
     __shared__ float xu[64];
     const int64_t q = blockIdx.x;
     const int uid = q < n ? users[q] : -1;
     const bool valid = uid >= 0 && uid < d.U;  // out-of-range ids: no recommendations (items -1)
     const int u = valid ? uid : 0;
-    if (threadIdx.x == 0) uok[q] = valid ? 1 : 0;
+    if (threadIdx.x == 0) {
+        uok[q] = valid ? 1 : 0;
+        gthr[q] = (int32_t)0x807fffff;  // key of -inf
+    }
     const float* W1 = mlp;
     const float* b1 = mlp + d.L0 * d.L1;
     const float* W2 = mlp + d.off_w2;
@@ -189,21 +193,50 @@ struct ScoreArgs {
     const int32_t* uok;
     int64_t n;
     int nub, ntiles, num_items, k;
+    int splits, tiles_per;  // the catalogue is cut into `splits` ranges of tiles_per 32-item tiles
     int32_t* top_items;
     float* top_scores;
+    float2* part;           // splits > 1: per-range lists [split][nub*32][k] of (logit, item)
+    int32_t* gthr;          // per user: best k-th logit published by any of its ranges (ordered key)
 };
 
+// float <-> int key with the same order (atomicMax on floats of either sign)
+__device__ __forceinline__ int fkey(float f) {
+    const int i = __float_as_int(f);
+    return i >= 0 ? i : i ^ 0x7fffffff;
+}
+__device__ __forceinline__ float unkey(int k) { return __int_as_float(k >= 0 ? k : k ^ 0x7fffffff); }
+// admission bound from another range's k-th best g: admit z >= g (ties resolve in the merge)
+__device__ __forceinline__ float below(float g) { return g - fmaxf(fabsf(g) * 1e-6f, 1e-30f); }
+
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+
+// relu of two packed halves (v_pk_max_f16 with 0).  Its input must come from a VALU op (here
+// v_cvt_pk_f16_f32), never straight from an MFMA: the compiler's MFMA->VALU hazard padding does
+// not see through inline-asm operands.
+__device__ __forceinline__ h2v relu_h2(h2v a) {
+    uint32_t r;
+    asm("v_pk_max_f16 %0, %1, 0" : "=v"(r) : "v"(__builtin_bit_cast(uint32_t, a)));
+    return __builtin_bit_cast(h2v, r);
+}
+
 template <int KS2, int KS3, int NR3, int KSG>
-__global__ __launch_bounds__(kBlock) void k_score_topk(ScoreArgs a) {
+__global__ __launch_bounds__(kBlock, 2) void k_score_topk(ScoreArgs a) {
     constexpr int L1P = 16 * KS2;
     __shared__ __attribute__((aligned(16))) _Float16 s_nega[4][32][L1P];
     __shared__ float4 s_init2[4][32][8];
     __shared__ float2 s_top[4][32][kScoreTopMax];
     __shared__ float s_z[4][32][32];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, j = lane & 31;
-    const int ub = blockIdx.x * 4 + w;
-    const bool active = ub < a.nub;
-    const int64_t q0 = (int64_t)(active ? ub : 0) * 32;
+    // wave g: users block g % nub, item range g / nub (waves in flight together share a range:
+    // its tiles stay in L2)
+    const int g = blockIdx.x * 4 + w;
+    const bool active = g < a.nub * a.splits;
+    const int ub = active ? g % a.nub : 0;
+    const int sp = active ? g / a.nub : 0;
+    const int t0 = sp * a.tiles_per;
+    const int t1 = min(a.ntiles, t0 + a.tiles_per);
+    const int64_t q0 = (int64_t)ub * 32;
     const int K = a.k;
     // stage this wave's users
     {
@@ -217,62 +250,81 @@ __global__ __launch_bounds__(kBlock) void k_score_topk(ScoreArgs a) {
     __syncthreads();
     if (!active) return;
 
-    f16x8 A2[KS2], A3[KS3], AG[KSG > 0 ? KSG : 1];
+    f16x8 A2[KS2], A3[KS3];
 #pragma unroll
     for (int s = 0; s < KS2; ++s) A2[s] = a.a2[s * 64 + lane];
 #pragma unroll
     for (int s = 0; s < KS3; ++s) A3[s] = a.a3[s * 64 + lane];
-#pragma unroll
-    for (int s = 0; s < KSG; ++s) AG[s] = a.ug[((int64_t)ub * KSG + s) * 64 + lane];
+    const f16x8* ag = a.ug + (int64_t)ub * KSG * 64 + lane;  // GMF A fragments, re-read per tile (L1)
     sf32x16 init3;
 #pragma unroll
     for (int r = 0; r < 16; ++r) init3[r] = a.init3[h * 16 + r];
-    float wh[NR3];
+    h2v wh[NR3 / 2];
 #pragma unroll
-    for (int r = 0; r < NR3; ++r) wh[r] = a.wh[h * 16 + r];
+    for (int r = 0; r < NR3 / 2; ++r) wh[r] = h2v{(_Float16)a.wh[h * 16 + 2 * r], (_Float16)a.wh[h * 16 + 2 * r + 1]};
     const float bo = a.bo[0];
-    // lane q (< 32) holds user q0+q's admission threshold (k-th best so far)
+    // lane q (< 32): user q0+q's own k-th best so far (thr) and admission bound (adm >= thr is
+    // raised further by the k-th best any other range of the user has published: an item
+    // below it cannot make the user's final top k)
     float thr = (lane < 32 && a.uok[q0 + (lane & 31)]) ? -INFINITY : INFINITY;
+    int32_t* gth = a.gthr + q0 + (lane & 31);
+    float adm = thr;
+    int pub = fkey(-INFINITY);  // last key this wave published for its lane's user
 
     f16x8 BC[KS2], BG[KSG > 0 ? KSG : 1];
 #pragma unroll
-    for (int s = 0; s < KS2; ++s) BC[s] = a.ic[s * 64 + lane];
+    for (int s = 0; s < KS2; ++s) BC[s] = a.ic[((int64_t)t0 * KS2 + s) * 64 + lane];
 #pragma unroll
-    for (int s = 0; s < KSG; ++s) BG[s] = a.ig[s * 64 + lane];
+    for (int s = 0; s < KSG; ++s) BG[s] = a.ig[((int64_t)t0 * KSG + s) * 64 + lane];
 
-    for (int t = 0; t < a.ntiles; ++t) {
-        // next tile's operands (consumed next iteration)
-        const int tn = t + 1 < a.ntiles ? t + 1 : t;
-        f16x8 NC[KS2], NG[KSG > 0 ? KSG : 1];
+    for (int t = t0; t < t1; ++t) {
+        if (a.splits > 1 && lane < 32) {
+            const int gk = __hip_atomic_load(gth, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (gk > pub) adm = fmaxf(adm, below(unkey(gk)));
+        }
+        // GMF + output bias of the 32 users x 32 items, parked in LDS ([user][item]) for the
+        // user loop; a user's slot is then reused for its flagged logits
+        {
+            sf32x16 accg;
 #pragma unroll
-        for (int s = 0; s < KS2; ++s) NC[s] = a.ic[((int64_t)tn * KS2 + s) * 64 + lane];
+            for (int r = 0; r < 16; ++r) accg[r] = bo;
 #pragma unroll
-        for (int s = 0; s < KSG; ++s) NG[s] = a.ig[((int64_t)tn * KSG + s) * 64 + lane];
-
-        sf32x16 accg;
+            for (int s = 0; s < KSG; ++s) accg = mfma16(ag[s * 64], BG[s], accg);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) accg[r] = bo;
-#pragma unroll
-        for (int s = 0; s < KSG; ++s) accg = mfma16(AG[s], BG[s], accg);
+            for (int r = 0; r < 16; ++r) s_z[w][drow_s(r, h)][j] = accg[r];
+        }
 
         const bool item_ok = h == 0 && 32 * t + j < a.num_items;
         uint32_t flagged = 0;
+        // per-user operands from LDS, fetched one user ahead of their use
+        float4 ui[4];
+        f16x8 un[KS2];
+        float ug = s_z[w][0][j];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) ui[c] = s_init2[w][0][h * 4 + c];
+#pragma unroll
+        for (int s = 0; s < KS2; ++s) un[s] = *reinterpret_cast<const f16x8*>(&s_nega[w][0][16 * s + 8 * h]);
 #pragma unroll
         for (int q = 0; q < 32; ++q) {
+            float4 vi[4];
+            f16x8 vn[KS2];
+            float vg = 0.0f;
+            if (q + 1 < 32) {
+                vg = s_z[w][q + 1][j];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) vi[c] = s_init2[w][q + 1][h * 4 + c];
+#pragma unroll
+                for (int s = 0; s < KS2; ++s)
+                    vn[s] = *reinterpret_cast<const f16x8*>(&s_nega[w][q + 1][16 * s + 8 * h]);
+            }
             sf32x16 acc2;
-            {
-                const float4* ip = &s_init2[w][q][h * 4];
 #pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const float4 v = ip[c];
-                    acc2[4 * c + 0] = v.x; acc2[4 * c + 1] = v.y; acc2[4 * c + 2] = v.z; acc2[4 * c + 3] = v.w;
-                }
+            for (int c = 0; c < 4; ++c) {
+                acc2[4 * c + 0] = ui[c].x; acc2[4 * c + 1] = ui[c].y;
+                acc2[4 * c + 2] = ui[c].z; acc2[4 * c + 3] = ui[c].w;
             }
 #pragma unroll
-            for (int s = 0; s < KS2; ++s) {
-                const f16x8 na = *reinterpret_cast<const f16x8*>(&s_nega[w][q][16 * s + 8 * h]);
-                acc2 = mfma16(A2[s], pkmax(BC[s], na), acc2);
-            }
+            for (int s = 0; s < KS2; ++s) acc2 = mfma16(A2[s], pkmax(BC[s], un[s]), acc2);
             sf32x16 acc3 = init3;
 #pragma unroll
             for (int s = 0; s < KS3; ++s) {
@@ -281,26 +333,44 @@ __global__ __launch_bounds__(kBlock) void k_score_topk(ScoreArgs a) {
                 for (int e = 0; e < 8; ++e) x[e] = (_Float16)acc2[8 * s + e];
                 acc3 = mfma16(A3[s], relu_f16(x), acc3);
             }
+            // output layer: relu(h3) . w_out in packed halves (cvt_pk, pk_max, dot2: 1.5 ops/feature)
             float z = 0.0f;
 #pragma unroll
-            for (int r = 0; r < NR3; ++r) z = fmaf(fmaxf(acc3[r], 0.0f), wh[r], z);
-            const int hq = (q >> 2) & 1, rq = (q & 3) + 4 * (q >> 3);
-            z += (h == hq) ? accg[rq] : 0.0f;
+            for (int r = 0; r < NR3 / 2; ++r) {
+                const h2v hv = relu_h2(h2v{(_Float16)acc3[2 * r], (_Float16)acc3[2 * r + 1]});
+                z = __builtin_amdgcn_fdot2(hv, wh[r], z, false);
+            }
+            z += h == 0 ? ug : 0.0f;
             // v_permlane32_swap(vdst = z, src = z): the new src holds the upper half's z in lanes
             // 0-31, so lanes 0-31 (the only ones read below) get the full sum
             const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(z), __float_as_uint(z), false, false);
             z += __uint_as_float(sw[1]);
-            const float tq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(thr), q));
+            const float tq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(adm), q));
             if (__ballot(item_ok && z > tq)) {
                 if (h == 0) s_z[w][q][j] = z;
                 flagged |= 1u << q;
             }
+            if (q + 1 < 32) {
+                ug = vg;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) ui[c] = vi[c];
+#pragma unroll
+                for (int s = 0; s < KS2; ++s) un[s] = vn[s];
+            }
+        }
+        // the next tile's item operands: loads in flight over the insertions below
+        if (t + 1 < t1) {
+#pragma unroll
+            for (int s = 0; s < KS2; ++s) BC[s] = a.ic[((int64_t)(t + 1) * KS2 + s) * 64 + lane];
+#pragma unroll
+            for (int s = 0; s < KSG; ++s) BG[s] = a.ig[((int64_t)(t + 1) * KSG + s) * 64 + lane];
         }
         // insertions (rare once the lists fill): ascending item order, ties keep the earlier item
         while (flagged) {
             const int q = __builtin_ctz(flagged);
             flagged &= flagged - 1;
-            float tq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(thr), q));
+            float tq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(adm), q));
+            float tk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(thr), q));
             const float zl = s_z[w][q][j];
             uint64_t m = __ballot(item_ok && zl > tq);
             float2 ent = lane < K ? s_top[w][q][lane] : make_float2(-INFINITY, __int_as_float(-1));
@@ -313,24 +383,63 @@ __global__ __launch_bounds__(kBlock) void k_score_topk(ScoreArgs a) {
                 const float px = __shfl_up(ent.x, 1, 64), py = __shfl_up(ent.y, 1, 64);
                 if (lane == p) ent = make_float2(zc, __int_as_float(32 * t + c));
                 else if (lane > p) ent = make_float2(px, py);
-                tq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ent.x), K - 1));
+                tk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ent.x), K - 1));
+                tq = fmaxf(tq, tk);
             }
             if (lane < K) s_top[w][q][lane] = ent;
-            if (lane == q) thr = tq;
+            if (lane == q) {
+                thr = tk;
+                adm = tq;
+                // publish a full list's k-th best for the user's other ranges
+                if (a.splits > 1 && tk > -INFINITY && fkey(tk) > pub) {
+                    pub = fkey(tk);
+                    atomicMax(gth, pub);
+                }
+            }
         }
-#pragma unroll
-        for (int s = 0; s < KS2; ++s) BC[s] = NC[s];
-#pragma unroll
-        for (int s = 0; s < KSG; ++s) BG[s] = NG[s];
     }
     for (int q = 0; q < 32; ++q) {
         if (q0 + q >= a.n) break;
         if (lane < K) {
             const float2 e = s_top[w][q][lane];
-            const int item = __float_as_int(e.y);
-            a.top_items[(q0 + q) * K + lane] = item;
-            a.top_scores[(q0 + q) * K + lane] = item >= 0 ? 1.0f / (1.0f + expf(-e.x)) : 0.0f;
+            if (a.splits > 1) {
+                a.part[((int64_t)sp * a.nub * 32 + q0 + q) * K + lane] = e;
+            } else {
+                const int item = __float_as_int(e.y);
+                a.top_items[(q0 + q) * K + lane] = item;
+                a.top_scores[(q0 + q) * K + lane] = item >= 0 ? 1.0f / (1.0f + expf(-e.x)) : 0.0f;
+            }
         }
+    }
+}
+
+// Merge the per-range lists of each user (one thread per user): k rounds of a max over the
+// splits*k entries that come after the previous pick in (logit desc, item asc) order.
+__global__ __launch_bounds__(kBlock) void k_score_merge(const float2* __restrict__ part, int64_t n, int64_t stride,
+                                                        int splits, int K, int32_t* __restrict__ top_items,
+                                                        float* __restrict__ top_scores) {
+    const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (q >= n) return;
+    float pv = INFINITY;
+    int pi = -1;
+    for (int r = 0; r < K; ++r) {
+        float bv = -INFINITY;
+        int bi = INT32_MAX;
+        for (int sp = 0; sp < splits; ++sp) {
+            const float2* l = part + ((int64_t)sp * stride + q) * K;
+            for (int e = 0; e < K; ++e) {
+                const float2 x = l[e];
+                const int it = __float_as_int(x.y);
+                if (it < 0) break;  // lists are sorted; -1 entries only at the tail
+                const bool after = x.x < pv || (x.x == pv && it > pi);
+                if (after && (x.x > bv || (x.x == bv && it < bi))) { bv = x.x; bi = it; }
+            }
+        }
+        const bool ok = bi != INT32_MAX;
+        top_items[q * K + r] = ok ? bi : -1;
+        top_scores[q * K + r] = ok ? 1.0f / (1.0f + expf(-bv)) : 0.0f;
+        pv = bv;
+        pi = bi;
     }
 }
 
@@ -391,6 +500,13 @@ __global__ __launch_bounds__(kBlock) void k_topk_rows(const float* __restrict__ 
 
 static inline int cdiv_i(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 
+// Item ranges per user block: enough waves (users/32 x splits) to fill the 2048 wave slots of the
+// chip many times over, so the last round of waves is short; ranges of >= 64 tiles.
+static inline int score_splits(int ntiles) {
+    int s = cdiv_i(ntiles, 64);
+    return s < 1 ? 1 : (s > 8 ? 8 : s);
+}
+
 ScoreDims score_dims(const ncf_shape_t& s) {
     ScoreDims d{};
     d.U = s.num_users;
@@ -440,6 +556,8 @@ ScoreLayout make_score_layout(const ncf_shape_t& s, int64_t max_users) {
         L.wh = take(32 * 4);
         L.bo = take(4);
         L.uok = take((size_t)nub * 32 * 4);
+        L.part = take((size_t)score_splits((int)nt) * nub * 32 * kScoreTopMax * 8);
+        L.gthr = take((size_t)nub * 32 * 4);
     }
     // exact path: chunks of users x all items through the generic forward
     int64_t chunk = kMaxBatch / s.num_items;
@@ -465,7 +583,7 @@ hipError_t launch_score_prep(const ncf_shape_t& s, const ScoreLayout& L, void* w
            at<float>(ws, L.init3), at<float>(ws, L.wh), at<float>(ws, L.bo));
     launch(k_score_items, nt, kBlock, 0, st, emb, mlp, d, at<_Float16>(ws, L.ic), at<_Float16>(ws, L.ig));
     launch(k_score_users, nub * 32, 64, 0, st, emb, mlp, d, users, n, at<_Float16>(ws, L.nega),
-           at<float>(ws, L.init2), at<_Float16>(ws, L.ug), at<int32_t>(ws, L.uok));
+           at<float>(ws, L.init2), at<_Float16>(ws, L.ug), at<int32_t>(ws, L.uok), at<int32_t>(ws, L.gthr));
     return hipGetLastError();
 }
 
@@ -492,7 +610,11 @@ hipError_t launch_score_main(const ncf_shape_t& s, const ScoreLayout& L, void* w
     a.k = k;
     a.top_items = top_items;
     a.top_scores = top_scores;
-    const int grid = cdiv_i(nub, 4);
+    a.splits = score_splits(a.ntiles);
+    a.tiles_per = cdiv_i(a.ntiles, a.splits);
+    a.part = at<float2>(ws, L.part);
+    a.gthr = at<int32_t>(ws, L.gthr);
+    const int grid = cdiv_i((int64_t)nub * a.splits, 4);
 #define NCF_SCORE_LAUNCH(A, B, C, D) launch(k_score_topk<A, B, C, D>, grid, kBlock, 0, st, a)
     if (d.ks2 == 4 && d.ks3 == 2 && d.nr3 == 8 && d.ksg == 4) NCF_SCORE_LAUNCH(4, 2, 8, 4);       // ml-20m NeuMF (configs C/E)
     else if (d.ks2 == 4 && d.ks3 == 2 && d.nr3 == 8 && d.ksg == 0) NCF_SCORE_LAUNCH(4, 2, 8, 0);  // its MLP-only form
@@ -500,6 +622,9 @@ hipError_t launch_score_main(const ncf_shape_t& s, const ScoreLayout& L, void* w
     else if (d.ks2 == 2 && d.ks3 == 1 && d.nr3 == 4 && d.ksg == 0) NCF_SCORE_LAUNCH(2, 1, 4, 0);  // trainer default [64,32,16,8]
     else return hipErrorInvalidValue;
 #undef NCF_SCORE_LAUNCH
+    if (a.splits > 1)
+        launch(k_score_merge, cdiv_i(n, kBlock), kBlock, 0, st, (const float2*)a.part, n, (int64_t)nub * 32,
+               a.splits, k, top_items, top_scores);
     return hipGetLastError();
 }
 

@@ -90,6 +90,7 @@ SHAPES = [
     (150, 640, [128, 64, 32, 16], 0),    # its MLP-only form
     (100, 333, [64, 32, 16, 8], 8),      # ml-1m NeuMF (config B)
     (90, 257, [64, 32, 16, 8], 0),       # the trainer default model (trainer.py:8-27)
+    (70, 5000, [128, 64, 32, 16], 64),   # 157 item tiles: 3 item ranges per user block + merge
 ]
 
 
