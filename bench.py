@@ -48,7 +48,11 @@ CONFIGS = {
               num_users=138493, num_items=27278, layers=[128, 64, 32, 16], gmf_dim=64, negs=3, batch=65536),
     "B": dict(workload="ml-1m NeuMF (config B shape): 6040 users x 3952 items, gmf 8 + MLP [64,32,16,8], 4 neg/pos",
               num_users=6040, num_items=3952, layers=[64, 32, 16, 8], gmf_dim=8, negs=4, batch=4095),
+    "E": dict(workload="ml-20m all-item scoring + top-10 (config E): every one of 138493 users x all 27278 items, "
+                       "NeuMF gmf 64 + MLP [128,64,32,16] (config C's model), fp16 MFMA / fp32 accumulate",
+              num_users=138493, num_items=27278, layers=[128, 64, 32, 16], gmf_dim=64, negs=3, batch=65536),
 }
+FP16_MFMA_PEAK_TFS = 2500.0  # dense fp16/bf16 MFMA peak (MI355X_MICROARCH.md), no sparsity
 
 
 def parse():
@@ -132,6 +136,88 @@ def cpu_baseline(cfg, budget_s):
                        "%.1f s" % (steps, B, t_total))
 
 
+def score_flops(cfg):
+    """Algorithmic flops per (user, item) pair of the scorer after the first-layer split
+    (ncf_score.hip): layers 2.., output layer and the GMF dot; and of the naive forward."""
+    L, G = cfg["layers"], cfg["gmf_dim"]
+    rewritten = 2 * (sum(a * b for a, b in zip(L[1:-1], L[2:])) + L[-1] + G)
+    naive = 2 * (sum(a * b for a, b in zip(L[:-1], L[1:])) + L[-1] + 2 * G)
+    return rewritten, naive
+
+
+def cpu_score_baseline(cfg, budget_s):
+    """numpy restatement (oracle/) of all-item scoring + top-10 for a bounded sample of users."""
+    from oracle import ncf_oracle as O
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    except Exception:
+        threads = 1
+    shape = O.NCFShape(cfg["num_users"], cfg["num_items"], cfg["layers"], cfg["gmf_dim"])
+    w = O.init_weights(shape, seed=0, dtype=np.float32)
+    t_total, n = 0.0, 0
+    while t_total < budget_s and n < 200:
+        t0 = time.perf_counter()
+        O.top_k_items(O.score_all_items(shape, w, [n]), 10)
+        t_total += time.perf_counter() - t0
+        n += 1
+    return dict(value=round(n * cfg["num_items"] / t_total, 1), unit="pairs/s", cores=int(threads), kind="port",
+                sample="%d users x all %d items scored + top-10, numpy, %.1f s" % (n, cfg["num_items"], t_total))
+
+
+def score_main(args, cfg, world, rank):
+    """Config E: every user x every item, top-10 per user; users split across ranks (no collective)."""
+    from movierec.engine import NCFEngine
+    from movierec.model import initial_weights
+    from movierec import _native as N
+    U, I = cfg["num_users"], cfg["num_items"]
+    eng = NCFEngine(U, I, cfg["layers"], cfg["gmf_dim"], max_batch=1024)
+    eng.set_keras_weights(initial_weights(U, I, cfg["layers"], cfg["gmf_dim"], seed=0))
+    lo, hi = rank * U // world, (rank + 1) * U // world
+    users = torch.arange(lo, hi, dtype=torch.int32, device="cuda")
+    for _ in range(args.warmup):
+        eng.score_topk(users, k=10)
+    torch.cuda.synchronize()
+    if dist.is_initialized():
+        dist.barrier()
+    N.profile_enable([N.K_SCORE], args.steps + 1)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.score_topk(users, k=10)
+    torch.cuda.synchronize()
+    if dist.is_initialized():
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ms, nl = N.profile_read(N.K_SCORE)
+    N.profile_enable([], 0)
+    if dist.is_initialized():
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    pairs = U * I
+    value = args.steps * pairs / elapsed
+    kern_ms = ms / max(nl, 1)
+    fl, fl_naive = score_flops(cfg)
+    my_pairs = (hi - lo) * I
+    achieved = fl * my_pairs / (kern_ms * 1e-3) / 1e12
+    if rank == 0:
+        cpu = None if (world > 1 or args.no_cpu_baseline) else cpu_score_baseline(cfg, args.cpu_seconds)
+        print(json.dumps({
+            "metric": "all-item scoring + top-10 (user, item) pairs/s, ml-20m NeuMF (config E)", "value": round(value, 1),
+            "unit": "pairs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "fp16 (fp32 accumulate)", "data": "synthetic (random-init weights)",
+            "config": {"workload": cfg["workload"], "users": U, "items": I, "k": 10,
+                       "parallelism": "users split across %d ranks" % world},
+            "roofline": {"bound": "mfma", "kernel": "k_score_topk (+ k_score_merge)", "achieved": round(achieved, 1),
+                         "peak": FP16_MFMA_PEAK_TFS, "unit": "TFLOP/s", "frac": round(achieved / FP16_MFMA_PEAK_TFS, 4),
+                         "traffic": None, "algorithmic_flops_per_pair": fl, "naive_flops_per_pair": fl_naive,
+                         "avg_launch_ms": round(kern_ms, 4)},
+            "cpu_baseline": cpu}), flush=True)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
 def pmc_traffic(name):
     """HBM bytes per launch measured by tools/gpu_profile.sh (separate --pmc passes)."""
     path = os.path.join(ROOT, "profiles", name)
@@ -159,11 +245,13 @@ def main():
         sk.close()
         dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=0, world_size=1,
                                 device_id=torch.device("cuda", local))
+    cfg = dict(CONFIGS[args.config])
+    if args.config == "E":
+        return score_main(args, cfg, world, rank)
     from movierec.engine import NCFEngine
     from movierec.model import initial_weights
     from movierec import _native as N
 
-    cfg = dict(CONFIGS[args.config])
     if args.batch:
         cfg["batch"] = args.batch
     B, g = cfg["batch"], cfg["negs"] + 1
