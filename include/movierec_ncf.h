@@ -251,6 +251,32 @@ int ncf_score_topk(const ncf_shape_t* shape, const ncf_model_t* model, const int
                    int32_t k, int32_t precision, int32_t* top_items, float* top_scores, void* ws, size_t ws_bytes,
                    void* stream);
 
+/* On-device negative sampling + batch assembly.  Replaces
+ * MovieLensDataGenerator.__getitem__ (data_pipeline.py:115-150): for the n_pos positives
+ * order[first .. first+n_pos) (indexes into pos_users/pos_items, the epoch's shuffled order,
+ * data_pipeline.py:136,152-154), group g of the batch is users [u]*(negs+1), items
+ * [neg_1 .. neg_negs, pos], labels [0]*negs + [1] (data_pipeline.py:141-148).  Negatives are
+ * uniform over the items in [0, num_items) absent from the user's excluded list
+ * (excl_items[excl_ptr[u] .. excl_ptr[u+1]), ascending and unique: the user's positives in
+ * data + extra, data_pipeline.py:103-108), distinct within a group unless the user has fewer
+ * candidates than negs (data_pipeline.py:111-112).  Random stream: counter-based
+ * Philox4x32-10 keyed by (seed, stream), counted by the positive's slot in the order — NOT
+ * numpy's stream (the host generator keeps the reference-exact mode).
+ * err (device int32, OR-ed): 1 user id out of range, 2 user without candidates (item -1;
+ * the reference raises), 4 attempt bound hit (a deterministic pick was used). */
+typedef struct ncf_sampler_data {
+    const int32_t* pos_users;   /* [num_pos] */
+    const int32_t* pos_items;   /* [num_pos] */
+    int64_t num_pos;
+    const int32_t* excl_ptr;    /* [num_users + 1] */
+    const int32_t* excl_items;  /* [excl_ptr[num_users]] */
+    int32_t num_users;
+    int32_t num_items;
+} ncf_sampler_data_t;
+int ncf_sample_batch(const ncf_sampler_data_t* data, const int32_t* order, int64_t first, int32_t n_pos,
+                     int32_t negs, uint64_t seed, uint64_t stream, int32_t* x_user, int32_t* x_item, float* labels,
+                     int32_t* err, void* hip_stream);
+
 /* Profiling hook (bench.py): while enabled, every launch of a group whose bit
  * is set in `kernel_mask` (bit NCF_K_*) issued by this thread is bracketed by
  * HIP events on its own stream (up to `capacity` launches per group);
@@ -263,6 +289,7 @@ int ncf_score_topk(const ncf_shape_t* shape, const ncf_model_t* model, const int
 #define NCF_K_MLP_UPDATE 4  /* dense-weight gradient reduction + optimizer */
 #define NCF_K_METRICS 5     /* hr/dcg + loss summary */
 #define NCF_K_SCORE 6       /* all-item scoring + top-k (MFMA kernel only, not its preparation) */
+#define NCF_K_SAMPLE 7      /* on-device negative sampling + batch assembly */
 int ncf_profile_enable(int32_t kernel_mask, int32_t capacity);
 int ncf_profile_read(int32_t kernel_id, double* total_ms, int64_t* launches);
 

@@ -685,6 +685,28 @@ int ncf_shard_predict(const ncf_shape_t* s, const ncf_model_t* model, int32_t wo
                      "shard predict");
 }
 
+// ------------------------------------------------------------ negative sampling
+
+int ncf_sample_batch(const ncf_sampler_data_t* d, const int32_t* order, int64_t first, int32_t n_pos, int32_t negs,
+                     uint64_t seed, uint64_t stream_id, int32_t* x_user, int32_t* x_item, float* labels, int32_t* err,
+                     void* stream) {
+    if (!d || !d->pos_users || !d->pos_items || !d->excl_ptr || !d->excl_items || !order || !x_user || !x_item ||
+        !labels || !err)
+        return fail(NCF_EINVAL, "NULL pointer");
+    if (negs <= 0) return fail(NCF_EINVAL, "negatives_per_positive must be > 0, found %d", negs);
+    if (d->num_users <= 0 || d->num_items <= 0) return fail(NCF_EINVAL, "num_users and num_items must be > 0");
+    if (n_pos < 0 || first < 0 || first + n_pos > d->num_pos)
+        return fail(NCF_EINVAL, "positives [%lld, %lld) outside the epoch order of %lld", (long long)first,
+                    (long long)(first + n_pos), (long long)d->num_pos);
+    hipStream_t st = (hipStream_t)stream;
+    prof_begin(NCF_K_SAMPLE, st);
+    hipError_t e = ncf::launch_sample_batch(d->pos_users, d->pos_items, d->excl_ptr, d->excl_items, d->num_users,
+                                            d->num_items, order, first, n_pos, negs, seed, stream_id, x_user, x_item,
+                                            labels, err, st);
+    prof_end(NCF_K_SAMPLE, st);
+    return hip_check(e, "sample batch");
+}
+
 // ------------------------------------------------------------ all-item scoring + top-k
 
 int ncf_score_supported(const ncf_shape_t* s, int32_t precision) {

@@ -173,6 +173,12 @@ hipError_t launch_emb_reg(const ncf_shape_t& s, const WsLayout& L, void* ws, con
 hipError_t launch_stats(const WsLayout& L, void* ws, const float* summary, int nreg_emb, int nreg_mlp,
                         float inv_batch, double* stats, int32_t* step, bool bump_step, hipStream_t st);
 
+// on-device negative sampling (ncf_sample.hip)
+hipError_t launch_sample_batch(const int32_t* pos_users, const int32_t* pos_items, const int32_t* excl_ptr,
+                               const int32_t* excl_items, int num_users, int num_items, const int32_t* order,
+                               int64_t first, int n_pos, int negs, uint64_t seed, uint64_t stream,
+                               int32_t* x_user, int32_t* x_item, float* labels, int32_t* err, hipStream_t st);
+
 // all-item scoring + top-k (ncf_score.hip) ---------------------------------------------------
 struct ScoreDims {
     int U, I, W, gmf_stride, du, di, G, L0, L1, L2, L3;

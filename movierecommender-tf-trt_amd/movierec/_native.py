@@ -56,6 +56,11 @@ class NcfHyper(ctypes.Structure):
                 ("force_generic", _i32), ("reserved", _i32 * 6)]
 
 
+class NcfSamplerData(ctypes.Structure):
+    _fields_ = [("pos_users", _vp), ("pos_items", _vp), ("num_pos", _i64), ("excl_ptr", _vp), ("excl_items", _vp),
+                ("num_users", _i32), ("num_items", _i32)]
+
+
 _P = ctypes.POINTER
 _SIGNATURES = {
     "ncf_abi_version": (ctypes.c_int, []),
@@ -84,6 +89,8 @@ _SIGNATURES = {
     "ncf_shard_apply_update": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _i32, _vp,
                                               _vp, _i64, _vp, _vp, _vp, _vp, ctypes.c_size_t, _vp]),
     "ncf_shard_predict": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _i32, _i64, _vp, _vp, ctypes.c_size_t, _vp]),
+    "ncf_sample_batch": (ctypes.c_int, [_P(NcfSamplerData), _vp, _i64, _i32, _i32, ctypes.c_uint64, ctypes.c_uint64,
+                                        _vp, _vp, _vp, _vp, _vp]),
     "ncf_score_supported": (ctypes.c_int, [_P(NcfShape), _i32]),
     "ncf_score_workspace_size": (ctypes.c_int, [_P(NcfShape), _i64, _P(ctypes.c_size_t)]),
     "ncf_score_topk": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _vp, _i64, _i32, _i32, _vp, _vp, _vp,
@@ -92,7 +99,7 @@ _SIGNATURES = {
     "ncf_profile_read": (ctypes.c_int, [_i32, _P(ctypes.c_double), _P(_i64)]),
 }
 EXPORTED = sorted(_SIGNATURES)
-K_INDEX, K_FWD_BWD, K_EMB_UPDATE, K_MLP_UPDATE, K_METRICS, K_SCORE = 1, 2, 3, 4, 5, 6
+K_INDEX, K_FWD_BWD, K_EMB_UPDATE, K_MLP_UPDATE, K_METRICS, K_SCORE, K_SAMPLE = 1, 2, 3, 4, 5, 6, 7
 NCF_SCORE_FP16, NCF_SCORE_FP32, NCF_SCORE_MAX_K = 0, 1, 32
 
 

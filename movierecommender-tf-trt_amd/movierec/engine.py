@@ -153,7 +153,10 @@ class NCFEngine(object):
         return y.reshape(-1).to(device=self.device, dtype=torch.float32, non_blocking=True).contiguous()
 
     def check_ids(self, users, items):
-        """Host-side range check (TF's gather raises on out-of-range ids)."""
+        """Host-side range check (TF's gather raises on out-of-range ids).  Batches already on
+        the device (DeviceMovieLensDataGenerator) were range-checked by the sampler."""
+        if torch.is_tensor(users) and users.is_cuda:
+            return
         u = np.asarray(users)
         i = np.asarray(items)
         if u.size and (u.min() < 0 or u.max() >= self.num_users):

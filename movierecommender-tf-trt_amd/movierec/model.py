@@ -309,6 +309,8 @@ class MovierecModel(object):
             for (xu, xi), y in _prefetch(train_data_generator, order, prefetch):
                 eng.check_ids(xu, xi)
                 eng.train_step(xu, xi, y, group=group_t, k=self._k)
+            if hasattr(train_data_generator, "check_errors"):
+                train_data_generator.check_errors()
             train_data_generator.on_epoch_end()
             tr = eng.read_stats(eng.stats)
             self.model.learning_phase = 0

@@ -328,6 +328,70 @@ def top_k_items(scores, k):
 
 
 # ---------------------------------------------------------------------------
+# on-device negative sampler (ncf_sample.hip), restated
+# ---------------------------------------------------------------------------
+
+_M32 = 0xFFFFFFFF
+
+
+def philox_u32(a, b, c, d, k0, k1):
+    """First word of Philox4x32-10 (Salmon et al., SC'11) of counter (a, b, c, d) and key
+    (k0, k1) — the generator ncf_sample.hip draws from."""
+    for _ in range(10):
+        p0 = 0xD2511F53 * a
+        p1 = 0xCD9E8D57 * c
+        a, b, c, d = ((p1 >> 32) ^ b ^ k0) & _M32, p1 & _M32, ((p0 >> 32) ^ d ^ k1) & _M32, p0 & _M32
+        k0 = (k0 + 0x9E3779B9) & _M32
+        k1 = (k1 + 0xBB67AE85) & _M32
+    return a
+
+
+def kth_candidate(excluded, c):
+    """The c-th item (0-based) absent from the ascending array ``excluded``."""
+    excluded = np.asarray(excluded, dtype=np.int64)
+    return int(c + np.count_nonzero(excluded - np.arange(len(excluded)) <= c))
+
+
+def sample_batch(pos_users, pos_items, excluded, num_items, order, first, n_pos, negs, seed, stream):
+    """Batch assembly of ``MovieLensDataGenerator.__getitem__`` (``data_pipeline.py:115-150``:
+    groups ``[neg_1 .. neg_n, pos]``, users repeated, labels ``[0]*n + [1]``; negatives uniform
+    over the user's items absent from data + extra (``:103-108``), without replacement unless
+    fewer than n candidates (``:111-112``)) with the device sampler's random stream: candidate
+    index = Lemire(Philox(k, attempt, slot_lo, slot_hi ^ stream_hi; seed_lo ^ stream_lo,
+    seed_hi)).  ``excluded[u]`` = ascending unique excluded items of user u."""
+    k0, k1 = seed & _M32, (seed >> 32) & _M32
+    s0, s1 = stream & _M32, (stream >> 32) & _M32
+    xu, xi, y = [], [], []
+    for g in range(n_pos):
+        slot = first + g
+        pidx = int(order[slot])
+        u, ip = int(pos_users[pidx]), int(pos_items[pidx])
+        ex = np.asarray(excluded.get(u, []), dtype=np.int64)
+        C = num_items - len(ex)
+        replace = C < negs
+        thresh = ((1 << 32) - C) % C
+        sl, sh = slot & _M32, ((slot >> 32) ^ s1) & _M32
+        group = []
+        for k in range(negs):
+            a = 0
+            while True:
+                r = philox_u32(k, a, sl, sh, k0 ^ s0, k1)
+                a += 1
+                m = r * C
+                if (m & _M32) < thresh:
+                    continue
+                cand = kth_candidate(ex, m >> 32)
+                if not replace and cand in group:
+                    continue
+                group.append(cand)
+                break
+        xu += [u] * (negs + 1)
+        xi += group + [ip]
+        y += [0.0] * negs + [1.0]
+    return np.array(xu, np.int32), np.array(xi, np.int32), np.array(y, np.float32)
+
+
+# ---------------------------------------------------------------------------
 # conversion helpers to / from the device layout used by the HIP library
 # ---------------------------------------------------------------------------
 

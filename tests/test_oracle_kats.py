@@ -102,3 +102,22 @@ def test_score_all_items_matches_forward():
     z = O.score_all_items(shape, w, [0, 5])
     _, c = O.forward(shape, w, [5] * 9, np.arange(9))
     np.testing.assert_allclose(z[1], c["z"])
+
+
+def test_philox_known_answers():
+    """Philox4x32-10 known-answer vectors (Random123 kat_vectors, first output word)."""
+    assert O.philox_u32(0, 0, 0, 0, 0, 0) == 0x6627e8d5
+    m = 0xFFFFFFFF
+    assert O.philox_u32(m, m, m, m, m, m) == 0x408f276d
+    assert O.philox_u32(0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344, 0xa4093822, 0x299f31d0) == 0xd16cfe09
+
+
+def test_sampler_restatement_invariants():
+    excluded = {0: np.array([1, 2, 3]), 1: np.arange(0, 18)}   # user 1: 2 candidates < 4 negatives
+    order = np.array([1, 0, 2])
+    xu, xi, y = O.sample_batch(np.array([0, 0, 1]), np.array([1, 2, 5]), excluded, 20, order, 0, 3, 4, 9, 5)
+    xi = xi.reshape(3, 5)
+    assert list(xi[:, -1]) == [2, 1, 5]
+    assert len(set(xi[0, :4])) == 4 and not set(xi[0, :4]) & {1, 2, 3}
+    assert set(xi[2, :4]) <= {18, 19}
+    np.testing.assert_array_equal(y, np.tile([0, 0, 0, 0, 1], 3))
