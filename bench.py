@@ -66,6 +66,9 @@ def parse():
     ap.add_argument("--generic", action="store_true", help="force the generic (non-MFMA) kernel")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
+    ap.add_argument("--e2e", action="store_true",
+                    help="end-to-end: each step also samples its batch on the device (ncf_sample_batch) from an "
+                         "ml-20m-shaped synthetic ratings set (20M positives)")
     ap.add_argument("--dp", default="auto", choices=["auto", "sharded", "replicated"],
                     help="multi-GPU table layout (auto: single engine at N=1, sharded at N>1)")
     return ap.parse_args()
@@ -218,6 +221,27 @@ def score_main(args, cfg, world, rank):
         dist.destroy_process_group()
 
 
+def synthetic_device_generator(cfg, batch, group, seed):
+    """ml-20m-shaped synthetic ratings (20M positives over the config's users x items, uniform)
+    behind the on-device sampler: a step = sample one batch + train on it."""
+    import pandas as pd
+    from movierec.sampler import DeviceMovieLensDataGenerator
+    from movierec.util import movielens_utils as ml
+    rng = np.random.RandomState(seed)
+    n = 20000263  # ml-20m ratings
+    df = pd.DataFrame({"userId": rng.randint(0, cfg["num_users"], n).astype(np.int32),
+                       "itemId": rng.randint(0, cfg["num_items"], n).astype(np.int32)})
+    name = "ml-20m"
+    saved = (ml.NUM_USERS[name], ml.NUM_ITEMS[name])
+    ml.NUM_USERS[name], ml.NUM_ITEMS[name] = cfg["num_users"], cfg["num_items"]
+    try:
+        gen = DeviceMovieLensDataGenerator(name, df, batch, group - 1, seed=seed)
+    finally:
+        ml.NUM_USERS[name], ml.NUM_ITEMS[name] = saved
+    gen[0]
+    return gen
+
+
 def pmc_traffic(name):
     """HBM bytes per launch measured by tools/gpu_profile.sh (separate --pmc passes)."""
     path = os.path.join(ROOT, "profiles", name)
@@ -274,6 +298,9 @@ def main():
             dp = ReplicatedDataParallel(eng)
     del w0
     gen = torch.Generator(device="cuda").manual_seed(1234 + rank)
+    sampler = None
+    if args.e2e:
+        sampler = synthetic_device_generator(cfg, B, g, seed=1234 + rank)
     pool = []
     for _ in range(args.pool):
         u = torch.randint(0, cfg["num_users"], (B // g,), generator=gen, device="cuda", dtype=torch.int32)
@@ -285,7 +312,10 @@ def main():
     inv = 1.0 / (B * world)
 
     def step(i):
-        u, it, y = pool[i % len(pool)]
+        if sampler is not None:
+            (u, it), y = sampler[i % len(sampler)]
+        else:
+            u, it, y = pool[i % len(pool)]
         if dp is None:
             eng.train_step(u, it, y, group=g, k=k, inv_batch=inv)
         else:
@@ -302,7 +332,7 @@ def main():
     barrier()
     # timed region.  The profiled launch groups carry HIP events in their dispatch packets
     # (hipExtLaunchKernel): per-kernel durations with no marker packets added to the stream.
-    N.profile_enable([N.K_EMB_UPDATE, N.K_FWD_BWD, N.K_INDEX], 2 * args.steps)
+    N.profile_enable([N.K_EMB_UPDATE, N.K_FWD_BWD, N.K_INDEX, N.K_SAMPLE], 2 * args.steps)
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i)
@@ -311,6 +341,7 @@ def main():
     ms_emb, nl = N.profile_read(N.K_EMB_UPDATE)
     ms_fb, nfb = N.profile_read(N.K_FWD_BWD)
     ms_idx, nidx = N.profile_read(N.K_INDEX)
+    ms_smp, nsmp = N.profile_read(N.K_SAMPLE)
     N.profile_enable([], 0)
     if dist.is_initialized():
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
@@ -362,7 +393,9 @@ def main():
             "metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
-            "data": "synthetic (uniform ids, seeded; random-init weights)",
+            "data": ("synthetic ml-20m-shaped ratings (%d positives), negatives sampled on the device each step"
+                     % len(sampler.data) if sampler is not None else
+                     "synthetic (uniform ids, seeded; random-init weights)"),
             "config": {"workload": cfg["workload"], "global_batch": B * world, "per_gpu_batch": B,
                        "negatives_per_positive": cfg["negs"], "parallelism": par,
                        "kernel_path": "generic" if not eng.fast_path else "fused-mfma"},
@@ -381,6 +414,7 @@ def main():
                                  "hbm_GBs": round(fb_bytes / (fb_ms * 1e-3) / 1e9, 1),
                                  "algorithmic_bytes_per_launch": fb_bytes, "traffic": fb_traffic},
             "index_build_ms": round(ms_idx / max(nidx, 1), 5),
+            "sampler_ms": round(ms_smp / nsmp, 5) if nsmp else None,
             "cpu_baseline": cpu,
             "hr_at_10": {"value": round(hr["hr"], 4), "ndcg_at_10": round(hr["dcg"], 4),
                          "data": "synthetic eval groups (random ids; ~0.1 expected for an untrained model)"},
