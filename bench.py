@@ -69,12 +69,14 @@ def parse():
     ap.add_argument("--e2e", action="store_true",
                     help="end-to-end: each step also samples its batch on the device (ncf_sample_batch) from an "
                          "ml-20m-shaped synthetic ratings set (20M positives)")
+    ap.add_argument("--dense-sweep", action="store_true",
+                    help="sweep every embedding row every step instead of the deferred exact decay (same result)")
     ap.add_argument("--dp", default="auto", choices=["auto", "sharded", "replicated"],
                     help="multi-GPU table layout (auto: single engine at N=1, sharded at N>1)")
     return ap.parse_args()
 
 
-def emb_update_bytes(cfg_shape, batch, dense_rows=None, sparse_rows=None):
+def emb_update_bytes(cfg_shape, batch, dense_rows=None, sparse_rows=None, touched_rows=None):
     """Algorithmic HBM bytes of one embedding scatter-add + Adam sweep launch:
     read+write p, m, v of every swept table element (24 B/param), plus the
     gradient.  Single table: the 2B per-sample gradient rows (W floats) + list
@@ -83,6 +85,9 @@ def emb_update_bytes(cfg_shape, batch, dense_rows=None, sparse_rows=None):
     (4 B/param).  Row-sharded DP (``sparse_rows`` = (shard rows, received
     gradient rows m)): the m received rows + list + offsets of the shard."""
     R, W = cfg_shape.num_rows, cfg_shape.row_width
+    if touched_rows is not None:
+        # deferred exact decay: only the batch's touched rows are read and written
+        return 24 * touched_rows * W + 2 * batch * W * 4 + 2 * batch * 4 + (R + 1) * 4
     if dense_rows is not None:
         return 28 * dense_rows * W
     if sparse_rows is not None:
@@ -242,13 +247,17 @@ def synthetic_device_generator(cfg, batch, group, seed):
     return gen
 
 
-def pmc_traffic(name):
-    """HBM bytes per launch measured by tools/gpu_profile.sh (separate --pmc passes)."""
+def pmc_traffic(name, kernel=None):
+    """HBM bytes per launch measured by tools/gpu_profile.sh (separate --pmc passes), if the
+    committed measurement is of ``kernel``."""
     path = os.path.join(ROOT, "profiles", name)
     try:
-        return json.load(open(path)).get("bytes_per_launch")
+        d = json.load(open(path))
     except (OSError, ValueError):
         return None
+    if kernel is not None and d.get("kernel") != kernel:
+        return None
+    return d.get("bytes_per_launch")
 
 
 def main():
@@ -291,7 +300,7 @@ def main():
         dp = RowShardedDataParallel(eng)
     else:
         eng = NCFEngine(cfg["num_users"], cfg["num_items"], cfg["layers"], cfg["gmf_dim"], max_batch=B,
-                        force_generic=args.generic)
+                        force_generic=args.generic, lazy_adam=(mode == "single" and not args.dense_sweep))
         eng.set_keras_weights(w0)
         if mode == "replicated":
             from movierec.distributed import ReplicatedDataParallel
@@ -332,16 +341,21 @@ def main():
     barrier()
     # timed region.  The profiled launch groups carry HIP events in their dispatch packets
     # (hipExtLaunchKernel): per-kernel durations with no marker packets added to the stream.
-    N.profile_enable([N.K_EMB_UPDATE, N.K_FWD_BWD, N.K_INDEX, N.K_SAMPLE], 2 * args.steps)
+    N.profile_enable([N.K_EMB_UPDATE, N.K_FWD_BWD, N.K_INDEX, N.K_SAMPLE, N.K_CATCHUP], 2 * args.steps)
+    eng.flush() if hasattr(eng, "flush") else None
+    barrier()
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i)
+    if hasattr(eng, "flush"):
+        eng.flush()   # deferred decay settled inside the timed region: the table ends in the dense state
     barrier()
     elapsed = time.perf_counter() - t0
     ms_emb, nl = N.profile_read(N.K_EMB_UPDATE)
     ms_fb, nfb = N.profile_read(N.K_FWD_BWD)
     ms_idx, nidx = N.profile_read(N.K_INDEX)
     ms_smp, nsmp = N.profile_read(N.K_SAMPLE)
+    ms_cu, ncu = N.profile_read(N.K_CATCHUP)
     N.profile_enable([], 0)
     if dist.is_initialized():
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
@@ -355,6 +369,9 @@ def main():
     train_exchange = dp.last_exchange if mode == "sharded" else None
     if mode == "sharded":
         nbytes = emb_update_bytes(eng.shape, B, sparse_rows=(eng.shard_rows, train_exchange[1]))
+    elif getattr(eng, "lazy", False):
+        touched = float(np.mean([torch.unique(u).numel() + torch.unique(it).numel() for u, it, _ in pool]))
+        nbytes = emb_update_bytes(eng.shape, B, touched_rows=touched)
     else:
         nbytes = emb_update_bytes(eng.shape, B, dense_rows=dp.row_count if dp is not None else None)
     achieved = nbytes / (kern_ms * 1e-3) / 1e9
@@ -377,7 +394,8 @@ def main():
         dist.all_reduce(hd)
     hr = {"hr": float(hd[0]) / (ev_users * world), "dcg": float(hd[1]) / (ev_users * world)}
 
-    traffic = pmc_traffic("traffic_emb_update.json") if mode == "single" else None
+    traffic = pmc_traffic("traffic_emb_update.json", "k_emb_adam_touched" if getattr(eng, "lazy", False)
+                          else "k_emb_update") if mode == "single" else None
     fb_traffic = pmc_traffic("traffic_fb_fused.json") if mode == "single" and eng.fast_path else None
     par = {"single": "dp1 (one table)",
            "sharded": "dp%d row-sharded tables (rank r owns rows g %% %d == r + their Adam state; all_to_all of "
@@ -399,7 +417,10 @@ def main():
             "config": {"workload": cfg["workload"], "global_batch": B * world, "per_gpu_batch": B,
                        "negatives_per_positive": cfg["negs"], "parallelism": par,
                        "kernel_path": "generic" if not eng.fast_path else "fused-mfma"},
-            "roofline": {"bound": "hbm", "kernel": "embedding scatter-add + Adam sweep (k_emb_update)",
+            "roofline": {"bound": "hbm", "kernel": ("embedding scatter-add + Adam on the batch's touched rows "
+                                                    "(k_emb_adam_touched; deferred exact decay)"
+                                                    if getattr(eng, "lazy", False) else
+                                                    "embedding scatter-add + Adam sweep (k_emb_update)"),
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "algorithmic_bytes_per_launch": nbytes, "avg_launch_ms": round(kern_ms, 5),
@@ -415,6 +436,10 @@ def main():
                                  "algorithmic_bytes_per_launch": fb_bytes, "traffic": fb_traffic},
             "index_build_ms": round(ms_idx / max(nidx, 1), 5),
             "sampler_ms": round(ms_smp / nsmp, 5) if nsmp else None,
+            "catchup_ms": round(ms_cu / ncu, 5) if ncu else None,
+            "adam": ("deferred exact decay (untouched rows replay their zero-gradient steps when next touched; "
+                     "flushed inside the timed region; bitwise the dense Keras sweep)"
+                     if getattr(eng, "lazy", False) else "dense sweep of every row every step (Keras, F5)"),
             "cpu_baseline": cpu,
             "hr_at_10": {"value": round(hr["hr"], 4), "ndcg_at_10": round(hr["dcg"], 4),
                          "data": "synthetic eval groups (random ids; ~0.1 expected for an untrained model)"},

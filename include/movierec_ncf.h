@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define NCF_ABI_VERSION 2
+#define NCF_ABI_VERSION 3
 #define NCF_MAX_LAYERS 8
 #define NCF_EINVAL (-1)
 #define NCF_EHIP (-2)
@@ -98,6 +98,13 @@ typedef struct ncf_optim {
     float* mlp_m;
     float* mlp_v;
     int32_t* step;   /* device: Keras `iterations` (optimizer steps taken so far) */
+    /* Deferred exact decay (optional, NULL = sweep every row every step).  int32[num_rows]: the
+     * optimizer steps row r has received.  ncf_train_step then updates only the batch's rows:
+     * their missed zero-gradient steps are replayed (same arithmetic, so the result is bitwise
+     * the dense sweep's) before the forward pass, then the step is applied to them.  Needs
+     * layers_l2reg[0] == 0.  Every other entry point reads the table as stored: call
+     * ncf_lazy_flush first. */
+    int32_t* row_step;
 } ncf_optim_t;
 
 typedef struct ncf_hyper {
@@ -154,6 +161,11 @@ int ncf_train_step(const ncf_shape_t* shape, ncf_model_t* model, ncf_optim_t* op
 int ncf_evaluate(const ncf_shape_t* shape, const ncf_model_t* model, const ncf_hyper_t* hyper,
                  const int32_t* users, const int32_t* items, const float* labels, int64_t n,
                  double* stats, float* probs_out, void* ws, size_t ws_bytes, void* stream);
+
+/* Deferred exact decay: bring every row up to optim->step (replay its missed zero-gradient
+ * Adam steps) and set row_step[r] = step.  After it the table equals the dense-sweep state. */
+int ncf_lazy_flush(const ncf_shape_t* shape, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* hyper,
+                   void* ws, size_t ws_bytes, void* stream);
 
 /* Data-parallel split of ncf_train_step.
  * ncf_forward_backward computes this rank's gradients with the BCE mean taken
@@ -290,6 +302,8 @@ int ncf_sample_batch(const ncf_sampler_data_t* data, const int32_t* order, int64
 #define NCF_K_METRICS 5     /* hr/dcg + loss summary */
 #define NCF_K_SCORE 6       /* all-item scoring + top-k (MFMA kernel only, not its preparation) */
 #define NCF_K_SAMPLE 7      /* on-device negative sampling + batch assembly */
+#define NCF_K_CATCHUP 8     /* deferred decay: replay of the batch's stale rows before the forward pass
+                             * (NCF_K_EMB_UPDATE then times the touched-row update only) */
 int ncf_profile_enable(int32_t kernel_mask, int32_t capacity);
 int ncf_profile_read(int32_t kernel_id, double* total_ms, int64_t* launches);
 

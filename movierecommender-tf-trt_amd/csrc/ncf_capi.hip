@@ -76,13 +76,13 @@ struct ProfSlot {
 };
 struct Profiler {
     uint32_t mask = 0;  // bit k set: time launch group k
-    ProfSlot slot[8];
+    ProfSlot slot[16];
 };
 thread_local Profiler g_prof;
 
 // A profiled launch group's events ride on its kernels' dispatch packets (ncf::launch).
 void prof_begin(int k, hipStream_t) {
-    ProfSlot& p = g_prof.slot[k & 7];
+    ProfSlot& p = g_prof.slot[k & 15];
     if (!(g_prof.mask >> k & 1u) || p.used >= p.start.size()) return;
     ncf::LaunchEvents& ev = ncf::launch_events();
     ev.start = p.start[p.used];
@@ -90,7 +90,7 @@ void prof_begin(int k, hipStream_t) {
     ev.launches = 0;
 }
 void prof_end(int k, hipStream_t) {
-    ProfSlot& p = g_prof.slot[k & 7];
+    ProfSlot& p = g_prof.slot[k & 15];
     if (!(g_prof.mask >> k & 1u) || p.used >= p.start.size()) return;
     ncf::LaunchEvents& ev = ncf::launch_events();
     if (ev.launches > 0) ++p.used;
@@ -203,13 +203,15 @@ WsLayout make_layout(const ncf_shape_t& s, int64_t B, int world) {
     L.slabs = take((size_t)kMaxSlabs * s.mlp_params * 4);
     L.mlp_grad = take((size_t)s.mlp_params * 4);
     L.slab_part = take((size_t)kSlabSplit * s.mlp_params * 4);
+    L.uloc = take((size_t)(K + 1) * 4);
+    L.utot = take((size_t)L.nscan * 4);
+    L.nuniq = take(4);
     if (world > 0) {
-        L.uloc = take((size_t)(K + 1) * 4);
-        L.utot = take((size_t)L.nscan * 4);
         L.cid_u = take((size_t)B * 4);
         L.cid_i = take((size_t)B * 4);
         L.uoffs = take((size_t)(2 * B + 1) * 4);
-        L.nuniq = take(4);
+    } else {
+        L.touched = take((size_t)(R < 2 * B ? R : 2 * B) * 4);
     }
     L.act = take((size_t)B * A * 4);
     L.dz = take((size_t)B * D * 4);
@@ -323,6 +325,25 @@ struct FbOut {
     SideStream* index_side = nullptr;  // index built on this side stream: join before using it
 };
 
+// deferred exact decay: bring the batch's rows up to date before the forward pass reads them
+struct CatchupCtx {
+    const ncf_shape_t* s;
+    const ncf::WsLayout* L;
+    ncf_model_t* model;
+    ncf_optim_t* optim;
+    const ncf_hyper_t* h;
+    void* ws;
+    hipStream_t st;
+};
+static int catchup_touched(void* p) {
+    const CatchupCtx& c = *static_cast<CatchupCtx*>(p);
+    prof_begin(NCF_K_CATCHUP, c.st);
+    hipError_t e = ncf::launch_emb_catchup(*c.s, *c.L, c.ws, c.model->emb, c.optim->emb_m, c.optim->emb_v,
+                                           c.optim->row_step, c.optim->step, *c.h, false, c.st);
+    prof_end(NCF_K_CATCHUP, c.st);
+    return hip_check(e, "touched-row catch-up");
+}
+
 // make `st` wait for an index built on the side stream
 static int index_join(hipStream_t st, FbOut& fb) {
     if (!fb.index_side) return 0;
@@ -333,9 +354,11 @@ static int index_join(hipStream_t st, FbOut& fb) {
 
 // index build + forward/backward (+ group metrics): shared by train_step and forward_backward
 // sharded: ids are the compact ids of the last ncf_shard_plan (model->emb = its unique rows)
+// after_index(ctx) (optional) runs once the index is enqueued, before the forward/backward
 static int run_fb(const ncf_shape_t& s, const ncf::WsLayout& L, const ncf_model_t* model, const ncf_hyper_t* h,
                   const int32_t* users, const int32_t* items, const float* labels, int64_t n, void* ws,
-                  float* probs_out, FbOut* out, hipStream_t st, bool sharded = false) {
+                  float* probs_out, FbOut* out, hipStream_t st, bool sharded = false,
+                  int (*after_index)(void*) = nullptr, void* ctx = nullptr) {
     hipError_t e = hipSuccess;
     ncf::IdSpace ids = ncf::table_ids(s);
     if (sharded) {
@@ -349,10 +372,14 @@ static int run_fb(const ncf_shape_t& s, const ncf::WsLayout& L, const ncf_model_
         SideStream* ss = nullptr;
         hipStream_t sti = fork_side(st, &ss);
         prof_begin(NCF_K_INDEX, sti);
-        e = ncf::launch_index_build(s, L, ws, users, items, n, sti);
+        e = ncf::launch_index_build(s, L, ws, users, items, n, sti, after_index != nullptr);
         prof_end(NCF_K_INDEX, sti);
         if (e != hipSuccess) return hip_check(e, "index build");
         out->index_side = ss;
+        if (after_index) {
+            if (int r = index_join(st, *out)) return r;
+            if (int r = after_index(ctx)) return r;
+        }
     }
     prof_begin(NCF_K_FWD_BWD, st);
     if (use_fused(s, h))
@@ -404,7 +431,15 @@ int ncf_train_step(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* optim,
     hipStream_t st = (hipStream_t)stream;
     float* summary = ncf::at<float>(ws, L.summary);
     FbOut fb;
-    if (int r = run_fb(*s, L, model, h, users, items, labels, n, ws, probs_out, &fb, st)) return r;
+    // Deferred exact decay (optim->row_step set, L2 off): untouched rows are not swept; the
+    // batch's rows catch up on their missed zero-gradient steps right after the index build
+    const bool lazy = optim->row_step != nullptr;
+    if (lazy && h->l2[0] != 0.0f)
+        return fail(NCF_EINVAL, "deferred decay (row_step) needs the embedding L2 off: the loss sums the whole table");
+    CatchupCtx cc{s, &L, model, optim, h, ws, st};
+    if (int r = run_fb(*s, L, model, h, users, items, labels, n, ws, probs_out, &fb, st, false,
+                       lazy ? catchup_touched : nullptr, &cc))
+        return r;
     // the index (side stream) must be complete before the side stream takes the dense tail
     if (int r = index_join(st, fb)) return r;
     // dense-layer tail on the side stream, embedding sweep on the main stream
@@ -419,8 +454,12 @@ int ncf_train_step(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* optim,
     prof_end(NCF_K_MLP_UPDATE, st2);
     if (e != hipSuccess) return hip_check(e, "dense update");
     prof_begin(NCF_K_EMB_UPDATE, st);
-    e = ncf::launch_emb_update(*s, L, ws, model->emb, optim->emb_m, optim->emb_v, optim->step, *h, nullptr,
-                               s->num_rows, st);
+    if (lazy)
+        e = ncf::launch_emb_update_touched(*s, L, ws, model->emb, optim->emb_m, optim->emb_v, optim->row_step,
+                                           optim->step, *h, st);
+    else
+        e = ncf::launch_emb_update(*s, L, ws, model->emb, optim->emb_m, optim->emb_v, optim->step, *h, nullptr,
+                                   s->num_rows, st);
     prof_end(NCF_K_EMB_UPDATE, st);
     if (e != hipSuccess) return hip_check(e, "embedding update");
     e = join_side(st, ss);
@@ -685,6 +724,24 @@ int ncf_shard_predict(const ncf_shape_t* s, const ncf_model_t* model, int32_t wo
                      "shard predict");
 }
 
+// ------------------------------------------------------------ deferred exact decay
+
+int ncf_lazy_flush(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* h, void* ws,
+                   size_t ws_bytes, void* stream) {
+    if (int r = check_shape(s)) return r;
+    if (int r = check_hyper(h)) return r;
+    if (!model || !model->emb || !optim || !optim->step || !optim->row_step)
+        return fail(NCF_EINVAL, "NULL device pointer");
+    if (h->optimizer == NCF_OPT_ADAM && (!optim->emb_m || !optim->emb_v)) return fail(NCF_EINVAL, "NULL Adam state");
+    ncf::WsLayout L;
+    if (int r = check_ws(*s, 1, ws, ws_bytes, &L)) return r;
+    hipStream_t st = (hipStream_t)stream;
+    hipError_t e = ncf::launch_emb_catchup(*s, L, ws, model->emb, optim->emb_m, optim->emb_v, optim->row_step,
+                                           optim->step, *h, true, st);
+    if (e != hipSuccess) return hip_check(e, "flush");
+    return hip_check(ncf::launch_row_step_fill(optim->row_step, s->num_rows, optim->step, st), "row-step fill");
+}
+
 // ------------------------------------------------------------ negative sampling
 
 int ncf_sample_batch(const ncf_sampler_data_t* d, const int32_t* order, int64_t first, int32_t n_pos, int32_t negs,
@@ -777,7 +834,7 @@ int ncf_score_topk(const ncf_shape_t* s, const ncf_model_t* model, const int32_t
 
 int ncf_profile_enable(int32_t kernel_mask, int32_t capacity) {
     g_prof.mask = kernel_mask < 0 ? 0u : (uint32_t)kernel_mask;
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < 16; ++k) {
         ProfSlot& p = g_prof.slot[k];
         p.used = 0;
         if (!(g_prof.mask >> k & 1u)) continue;
@@ -794,7 +851,7 @@ int ncf_profile_enable(int32_t kernel_mask, int32_t capacity) {
 }
 
 int ncf_profile_read(int32_t kernel_id, double* total_ms, int64_t* launches) {
-    if (!total_ms || !launches || kernel_id < 0 || kernel_id > 7) return fail(NCF_EINVAL, "invalid argument");
+    if (!total_ms || !launches || kernel_id < 0 || kernel_id > 15) return fail(NCF_EINVAL, "invalid argument");
     ProfSlot& p = g_prof.slot[kernel_id];
     double tot = 0.0;
     if (p.used > 0) {

@@ -144,7 +144,9 @@ struct PlanOut {
 // Finalise the key offsets (offs_g = local scan + prefix of block totals) and scatter every
 // contribution into its key's list slot; the per-key counter runs back down to zero.  A plan
 // (UNIQ) also numbers the occupied keys (compact ids) and writes the per-owner counts.
-template <int MODE, bool UNIQ>
+// LIST (single table): also the compact list of the occupied keys (touched rows, ascending) and
+// its length, for the deferred-decay kernels.
+template <int MODE, bool UNIQ, bool LIST>
 __global__ __launch_bounds__(kBlock) void k_fill(KeySrc ks, int64_t m, int32_t* __restrict__ cnt,
                                                  const int32_t* __restrict__ local, const int32_t* __restrict__ tot,
                                                  int nscan, int64_t r1, int32_t* __restrict__ offs_g,
@@ -153,23 +155,30 @@ __global__ __launch_bounds__(kBlock) void k_fill(KeySrc ks, int64_t m, int32_t* 
     __shared__ int sw[4];
     int* upre = pre + nscan;
     block_prefix_of_totals(tot, nscan, pre, sw);
-    if constexpr (UNIQ) block_prefix_of_totals(po.utot, nscan, upre, sw);
+    if constexpr (UNIQ || LIST) block_prefix_of_totals(po.utot, nscan, upre, sw);
     const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t gstride = (int64_t)gridDim.x * blockDim.x;
     const int64_t K = r1 - 1;
     for (int64_t r = gt; r < r1; r += gstride) {
         const int o = local[r] + pre[r / kScanBlock];
         offs_g[r] = o;
-        if constexpr (UNIQ) {
+        if constexpr (UNIQ || LIST) {
             if (r < K) {
                 const int o1 = local[r + 1] + pre[(r + 1) / kScanBlock];
                 if (o1 > o) {
                     const int u = po.uloc[r] + upre[r / kScanBlock];
-                    po.uniq_rows[u] = (int)(r % ks.S);
-                    po.uoffs[u] = o;
+                    if constexpr (UNIQ) {
+                        po.uniq_rows[u] = (int)(r % ks.S);
+                        po.uoffs[u] = o;
+                    } else {
+                        po.uniq_rows[u] = (int)r;
+                    }
                 }
             }
         }
+    }
+    if constexpr (LIST) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) *po.nuniq = po.uloc[K] + upre[K / kScanBlock];
     }
     if constexpr (UNIQ) {
         if (blockIdx.x == 0) {
@@ -283,7 +292,7 @@ static hipError_t set_sort_lds(int nwords) {
 }
 
 // count -> scan -> fill -> sort over K keys for m contributions.
-template <int MODE, bool UNIQ>
+template <int MODE, bool UNIQ, bool LIST = false>
 static hipError_t build(const WsLayout& L, void* ws, const KeySrc& ks, int64_t m, int64_t K, PlanOut po,
                         int nwords, hipStream_t st) {
     const int64_t r1 = K + 1;
@@ -296,19 +305,28 @@ static hipError_t build(const WsLayout& L, void* ws, const KeySrc& ks, int64_t m
     if (m > 0)
         launch(k_count<MODE>, grid_for(m, 1024), kBlock, 0, st, ks, m, cnt, at<int32_t>(ws, L.heavy_n),
                                                             at<int32_t>(ws, L.err));
-    launch(k_scan_local<UNIQ>, nscan, kBlock, 0, st, cnt, r1, local, tot, UNIQ ? at<int32_t>(ws, L.uloc) : nullptr,
-                                                 UNIQ ? at<int32_t>(ws, L.utot) : nullptr);
-    const size_t pre_bytes = (size_t)nscan * 4 * (UNIQ ? 2 : 1);
-    launch(k_fill<MODE, UNIQ>, grid_for(m > r1 ? m : r1, 1024), kBlock, pre_bytes, st, ks, m, cnt, local, tot, nscan, r1,
-                                                                                   offs, list, po);
+    constexpr bool U2 = UNIQ || LIST;
+    launch(k_scan_local<U2>, nscan, kBlock, 0, st, cnt, r1, local, tot, U2 ? at<int32_t>(ws, L.uloc) : nullptr,
+                                               U2 ? at<int32_t>(ws, L.utot) : nullptr);
+    const size_t pre_bytes = (size_t)nscan * 4 * (U2 ? 2 : 1);
+    launch(k_fill<MODE, UNIQ, LIST>, grid_for(m > r1 ? m : r1, 1024), kBlock, pre_bytes, st, ks, m, cnt, local, tot,
+                                                                                         nscan, r1, offs, list, po);
     if (hipError_t e = set_sort_lds(nwords)) return e;
     launch(k_sort, (unsigned)((K + kBlock - 1) / kBlock), kBlock, (size_t)nwords * 4, st, offs, K, list, nwords);
     return hipGetLastError();
 }
 
 hipError_t launch_index_build(const ncf_shape_t& s, const WsLayout& L, void* ws, const int32_t* users,
-                              const int32_t* items, int64_t n, hipStream_t st) {
+                              const int32_t* items, int64_t n, hipStream_t st, bool touched_list) {
     KeySrc ks{users, items, nullptr, s.num_users, s.num_items, 1, 0};
+    if (touched_list) {
+        PlanOut po{};
+        po.uloc = at<int32_t>(ws, L.uloc);
+        po.utot = at<int32_t>(ws, L.utot);
+        po.uniq_rows = at<int32_t>(ws, L.touched);
+        po.nuniq = at<int32_t>(ws, L.nuniq);
+        return build<kKeyPair, false, true>(L, ws, ks, 2 * n, s.num_rows, po, (int)((2 * n + 31) / 32), st);
+    }
     return build<kKeyPair, false>(L, ws, ks, 2 * n, s.num_rows, PlanOut{}, (int)((2 * n + 31) / 32), st);
 }
 

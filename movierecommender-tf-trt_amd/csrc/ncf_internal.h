@@ -50,7 +50,8 @@ struct WsLayout {
     size_t cid_u;     // int32[B]    compact (unique-row) id of each sample's user row
     size_t cid_i;     // int32[B]    compact id of each sample's item row
     size_t uoffs;     // int32[2B+1] compact row -> first list slot
-    size_t nuniq;     // int32       number of unique rows
+    size_t nuniq;     // int32       number of unique rows (single table: of touched rows)
+    size_t touched;   // int32[min(R, 2B)] single table, deferred decay: the touched rows, ascending
     size_t act;       // float[B * A] generic kernel activations
     size_t dz;        // float[B * D] generic kernel pre-activation gradients
     size_t total;
@@ -113,8 +114,9 @@ __host__ __device__ inline T* at(void* base, size_t off) {
 // Launchers (return hipError_t of the launch). ------------------------------
 
 // index build: contribution c = 2*i + side (0 user row, 1 item row) grouped by table row
+// touched_list: also the ascending list of the touched rows (ws touched, count in nuniq)
 hipError_t launch_index_build(const ncf_shape_t& s, const WsLayout& L, void* ws, const int32_t* users,
-                              const int32_t* items, int64_t n, hipStream_t st);
+                              const int32_t* items, int64_t n, hipStream_t st, bool touched_list = false);
 // row-sharded plan: index over owner-major keys + unique-row compaction (uniq_rows = local row
 // ids grouped by owner, send_counts[world], cid_u/cid_i/uoffs/nuniq in the workspace)
 hipError_t launch_shard_plan(const ncf_shape_t& s, const WsLayout& L, void* ws, const int32_t* users,
@@ -163,6 +165,16 @@ enum GradSource { kGradSparse = 0, kGradDense = 1 };
 hipError_t launch_emb_update(const ncf_shape_t& s, const WsLayout& L, void* ws, float* emb, float* m, float* v,
                              const int32_t* step, const ncf_hyper_t& h, const float* dense_grad, int64_t rows,
                              hipStream_t st, const float* gs = nullptr);
+// deferred exact decay (ncf_update.hip, L2 off): replay the missed zero-gradient Adam steps of
+// the touched rows (all_rows: every row, ncf_lazy_flush) up to *step; then the step's update of
+// the touched rows, which records row_step[r] = *step + 1.  Bitwise the dense sweep.
+hipError_t launch_emb_catchup(const ncf_shape_t& s, const WsLayout& L, void* ws, float* emb, float* m, float* v,
+                              const int32_t* row_step, const int32_t* step, const ncf_hyper_t& h, bool all_rows,
+                              hipStream_t st);
+hipError_t launch_row_step_fill(int32_t* row_step, int64_t R, const int32_t* step, hipStream_t st);
+hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, void* ws, float* emb, float* m,
+                                     float* v, int32_t* row_step, const int32_t* step, const ncf_hyper_t& h,
+                                     hipStream_t st);
 hipError_t launch_emb_grad_dense(const ncf_shape_t& s, const WsLayout& L, void* ws, float* out, hipStream_t st);
 // mlp: reduce slabs (if nslab > 0) or read grad_in; optionally write grad_out; optionally update
 hipError_t launch_mlp_update(const ncf_shape_t& s, const WsLayout& L, void* ws, float* mlp, float* m, float* v,

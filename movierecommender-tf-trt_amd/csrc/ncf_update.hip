@@ -26,6 +26,20 @@ __device__ inline float adam_lr_t(float lr, float b1, float b2, int t) {
     return lr * (sqrtf(1.0f - powf(b2, ft)) / (1.0f - powf(b1, ft)));
 }
 
+// One Adam step of one float4 element (Keras v1 update, see top of file).  Every sweep of the
+// table goes through this one function, so the dense sweep, the touched-row update and the
+// zero-gradient replay round identically.
+__device__ __forceinline__ void adam4(float4& p, float4& m, float4& v, const float4& g, float lr_t, float b1,
+                                      float b2, float eps) {
+    const float c1 = 1.0f - b1, c2 = 1.0f - b2;
+    m.x = b1 * m.x + c1 * g.x; m.y = b1 * m.y + c1 * g.y;
+    m.z = b1 * m.z + c1 * g.z; m.w = b1 * m.w + c1 * g.w;
+    v.x = b2 * v.x + c2 * (g.x * g.x); v.y = b2 * v.y + c2 * (g.y * g.y);
+    v.z = b2 * v.z + c2 * (g.z * g.z); v.w = b2 * v.w + c2 * (g.w * g.w);
+    p.x -= lr_t * m.x / (sqrtf(v.x) + eps); p.y -= lr_t * m.y / (sqrtf(v.y) + eps);
+    p.z -= lr_t * m.z / (sqrtf(v.z) + eps); p.w -= lr_t * m.w / (sqrtf(v.w) + eps);
+}
+
 template <int OPT, int SRC, bool L2>
 __global__ __launch_bounds__(kBlock) void k_emb_update(float4* __restrict__ emb, float4* __restrict__ m4,
                                                        float4* __restrict__ v4, uint32_t n4, uint32_t w4,
@@ -38,7 +52,6 @@ __global__ __launch_bounds__(kBlock) void k_emb_update(float4* __restrict__ emb,
     __shared__ float red[4];
     const int t = *step + 1;
     const float lr_t = (OPT == NCF_OPT_ADAM) ? adam_lr_t(lr, b1, b2, t) : lr;
-    const float c1 = 1.0f - b1, c2 = 1.0f - b2;
     float reg = 0.0f;
     for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n4; e += gridDim.x * blockDim.x) {
         float4 p = emb[e];
@@ -60,12 +73,7 @@ __global__ __launch_bounds__(kBlock) void k_emb_update(float4* __restrict__ emb,
         }
         if (OPT == NCF_OPT_ADAM) {
             float4 mm = m4[e], vv = v4[e];
-            mm.x = b1 * mm.x + c1 * g.x; mm.y = b1 * mm.y + c1 * g.y;
-            mm.z = b1 * mm.z + c1 * g.z; mm.w = b1 * mm.w + c1 * g.w;
-            vv.x = b2 * vv.x + c2 * (g.x * g.x); vv.y = b2 * vv.y + c2 * (g.y * g.y);
-            vv.z = b2 * vv.z + c2 * (g.z * g.z); vv.w = b2 * vv.w + c2 * (g.w * g.w);
-            p.x -= lr_t * mm.x / (sqrtf(vv.x) + eps); p.y -= lr_t * mm.y / (sqrtf(vv.y) + eps);
-            p.z -= lr_t * mm.z / (sqrtf(vv.z) + eps); p.w -= lr_t * mm.w / (sqrtf(vv.w) + eps);
+            adam4(p, mm, vv, g, lr_t, b1, b2, eps);
             m4[e] = mm;
             v4[e] = vv;
         } else {
@@ -76,6 +84,133 @@ __global__ __launch_bounds__(kBlock) void k_emb_update(float4* __restrict__ emb,
     if (L2) {
         reg = block_sum_256(reg, red);
         if (threadIdx.x == 0) part_reg[blockIdx.x] = reg;
+    }
+}
+
+// Deferred exact decay ("lazy" dense Adam, L2 off).  Keras' dense Adam (F5) moves EVERY row
+// every step; a row no sample touches gets g = 0, so its update is a pure function of
+// (p, m, v, t).  Instead of sweeping those rows, row_step[r] records how many steps row r has
+// received; a row is brought up to date (its missed zero-gradient steps replayed with the
+// same per-step arithmetic) only when a batch touches it (before the forward pass reads it)
+// or when the whole table is read (ncf_lazy_flush).  The result is bitwise that of the dense
+// sweep, and a step moves only the touched rows instead of the whole table.
+
+// Rows are processed a wave at a time: lane l takes element l % w4 of row (l / w4) of the
+// wave's group of 64 / w4 rows (w4 <= 64; wider rows loop over their elements).  Every row's
+// loads are independent, so latency hides across the many waves in flight instead of inside
+// a grid-stride chain of dependent index loads.
+struct RowLanes {
+    int rpw, sub, q, qstep;
+    bool on;
+    __device__ RowLanes(uint32_t w4) {
+        const int lane = threadIdx.x & 63;
+        rpw = w4 <= 64 ? 64 / (int)w4 : 1;
+        sub = w4 <= 64 ? lane / (int)w4 : 0;
+        q = w4 <= 64 ? lane % (int)w4 : lane;
+        qstep = w4 <= 64 ? (int)w4 : 64;
+        on = sub < rpw;
+    }
+};
+
+constexpr int kLrLut = 64;  // bias-corrected lr of the last kLrLut steps, per block in LDS
+
+// replay the zero-gradient steps (s, t] of the touched rows list[0..*nlist) (ALL: every row,
+// ncf_lazy_flush)
+template <bool ALL>
+__global__ __launch_bounds__(kBlock) void k_emb_catchup(float4* __restrict__ emb, float4* __restrict__ m4,
+                                                        float4* __restrict__ v4, uint32_t w4,
+                                                        const int32_t* __restrict__ list,
+                                                        const int32_t* __restrict__ nlist, int64_t R,
+                                                        const int32_t* __restrict__ row_step,
+                                                        const int32_t* __restrict__ step, float lr, float b1,
+                                                        float b2, float eps) {
+    __shared__ float lut[kLrLut];
+    const int t = *step;  // steps every row should have received
+    if (threadIdx.x < kLrLut) lut[threadIdx.x] = t - (int)threadIdx.x >= 1 ? adam_lr_t(lr, b1, b2, t - threadIdx.x) : 0.f;
+    __syncthreads();
+    const RowLanes rl(w4);
+    if (!rl.on) return;
+    const int64_t n = ALL ? R : (int64_t)*nlist;
+    const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+    const int64_t waves = ((int64_t)gridDim.x * kBlock) >> 6;
+    const float4 zero = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t i = wave * rl.rpw + rl.sub; i < n; i += waves * rl.rpw) {
+        const int64_t r = ALL ? i : list[i];
+        const int s = row_step[r];
+        if (s >= t) continue;
+        for (uint32_t q = rl.q; q < w4; q += rl.qstep) {
+            const size_t e = (size_t)r * w4 + q;
+            float4 p = emb[e], m = m4[e], v = v4[e];
+            for (int j = s + 1; j <= t; ++j)
+                adam4(p, m, v, zero, t - j < kLrLut ? lut[t - j] : adam_lr_t(lr, b1, b2, j), b1, b2, eps);
+            emb[e] = p;
+            m4[e] = m;
+            v4[e] = v;
+        }
+    }
+}
+
+// row_step[r] = *step for every row (after a flush: the replay kernel above only reads row_step)
+__global__ __launch_bounds__(kBlock) void k_row_step_fill(int32_t* __restrict__ row_step, int64_t R,
+                                                          const int32_t* __restrict__ step) {
+    const int t = *step;
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < R; r += (int64_t)gridDim.x * blockDim.x)
+        row_step[r] = t;
+}
+
+// Adam step t = *step + 1 on the touched rows, which were brought up to step t-1 before the
+// forward pass; records row_step[r] = t.
+__global__ __launch_bounds__(kBlock) void k_emb_adam_touched(float4* __restrict__ emb, float4* __restrict__ m4,
+                                                             float4* __restrict__ v4, uint32_t w4,
+                                                             const int32_t* __restrict__ list,
+                                                             const int32_t* __restrict__ nlist,
+                                                             const int32_t* __restrict__ offs,
+                                                             const int32_t* __restrict__ clist,
+                                                             const float4* __restrict__ gs,
+                                                             int32_t* __restrict__ row_step,
+                                                             const int32_t* __restrict__ step, float lr, float b1,
+                                                             float b2, float eps) {
+    const RowLanes rl(w4);
+    if (!rl.on) return;
+    const int t = *step + 1;
+    const float lr_t = adam_lr_t(lr, b1, b2, t);
+    const int64_t n = *nlist;
+    const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+    const int64_t waves = ((int64_t)gridDim.x * kBlock) >> 6;
+    for (int64_t i = wave * rl.rpw + rl.sub; i < n; i += waves * rl.rpw) {
+        const int r = list[i];
+        const int o = offs[r];
+        const int c = offs[r + 1] - o;
+        for (uint32_t q = rl.q; q < w4; q += rl.qstep) {
+            const size_t e = (size_t)r * w4 + q;
+            float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int j = 0; j < c; ++j) g = f4add(g, gs[(size_t)clist[o + j] * w4 + q]);
+            float4 p = emb[e], m = m4[e], v = v4[e];
+            adam4(p, m, v, g, lr_t, b1, b2, eps);
+            emb[e] = p;
+            m4[e] = m;
+            v4[e] = v;
+        }
+        if (rl.q == 0) row_step[r] = t;
+    }
+}
+
+// SGD on the hot rows only (cold rows: p - lr*0 = p, bitwise)
+__global__ __launch_bounds__(kBlock) void k_emb_sgd_hot(float4* __restrict__ emb, uint32_t n4, uint32_t w4,
+                                                        const int32_t* __restrict__ offs,
+                                                        const int32_t* __restrict__ list,
+                                                        const float4* __restrict__ gs, float lr) {
+    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n4; e += gridDim.x * blockDim.x) {
+        const uint32_t r = e / w4;
+        const int o = offs[r];
+        const int c = offs[r + 1] - o;
+        if (c == 0) continue;
+        const uint32_t q = e - r * w4;
+        float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int j = 0; j < c; ++j) g = f4add(g, gs[(size_t)list[o + j] * w4 + q]);
+        float4 p = emb[e];
+        p.x -= lr * g.x; p.y -= lr * g.y; p.z -= lr * g.z; p.w -= lr * g.w;
+        emb[e] = p;
     }
 }
 
@@ -364,6 +499,53 @@ hipError_t launch_emb_update(const ncf_shape_t& s, const WsLayout& L, void* ws, 
         else { if (l2) NCF_EMB_LAUNCH(NCF_OPT_SGD, kGradDense, true); else NCF_EMB_LAUNCH(NCF_OPT_SGD, kGradDense, false); }
     }
 #undef NCF_EMB_LAUNCH
+    return hipGetLastError();
+}
+
+static unsigned row_grid(int64_t rows, uint32_t w4) {
+    const int64_t rpw = w4 <= 64 ? 64 / w4 : 1;
+    int64_t g = (rows + rpw * 4 - 1) / (rpw * 4);  // 4 waves per block
+    return (unsigned)(g < 1 ? 1 : (g > 8192 ? 8192 : g));
+}
+
+hipError_t launch_emb_catchup(const ncf_shape_t& s, const WsLayout& L, void* ws, float* emb, float* m, float* v,
+                              const int32_t* row_step, const int32_t* step, const ncf_hyper_t& h, bool all_rows,
+                              hipStream_t st) {
+    if (h.optimizer != NCF_OPT_ADAM) return hipSuccess;  // SGD: an untouched row does not move
+    const uint32_t w4 = (uint32_t)(s.row_width / 4);
+    const int64_t R = s.num_rows;
+    const int64_t nmax = R < 2 * L.max_batch ? R : 2 * L.max_batch;
+    if (all_rows)
+        launch(k_emb_catchup<true>, row_grid(R, w4), kBlock, 0, st, (float4*)emb, (float4*)m, (float4*)v, w4,
+               (const int32_t*)nullptr, (const int32_t*)nullptr, R, row_step, step, h.lr, h.beta_1, h.beta_2,
+               h.epsilon);
+    else
+        launch(k_emb_catchup<false>, row_grid(nmax, w4), kBlock, 0, st, (float4*)emb, (float4*)m, (float4*)v, w4,
+               at<const int32_t>(ws, L.touched), at<const int32_t>(ws, L.nuniq), R, row_step, step, h.lr, h.beta_1,
+               h.beta_2, h.epsilon);
+    return hipGetLastError();
+}
+
+hipError_t launch_row_step_fill(int32_t* row_step, int64_t R, const int32_t* step, hipStream_t st) {
+    launch(k_row_step_fill, kUpdateGrid, kBlock, 0, st, row_step, R, step);
+    return hipGetLastError();
+}
+
+hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, void* ws, float* emb, float* m,
+                                     float* v, int32_t* row_step, const int32_t* step, const ncf_hyper_t& h,
+                                     hipStream_t st) {
+    const uint32_t w4 = (uint32_t)(s.row_width / 4);
+    const uint32_t n4 = (uint32_t)(s.num_rows * w4);
+    const int32_t* offs = at<int32_t>(ws, L.offs);
+    const int32_t* list = at<int32_t>(ws, L.list);
+    const float4* gs = at<const float4>(ws, L.gs);
+    const int64_t R = s.num_rows;
+    if (h.optimizer == NCF_OPT_ADAM)
+        launch(k_emb_adam_touched, row_grid(R < 2 * L.max_batch ? R : 2 * L.max_batch, w4), kBlock, 0, st,
+               (float4*)emb, (float4*)m, (float4*)v, w4, at<const int32_t>(ws, L.touched),
+               at<const int32_t>(ws, L.nuniq), offs, list, gs, row_step, step, h.lr, h.beta_1, h.beta_2, h.epsilon);
+    else
+        launch(k_emb_sgd_hot, kUpdateGrid, kBlock, 0, st, (float4*)emb, n4, w4, offs, list, gs, h.lr);
     return hipGetLastError();
 }
 

@@ -47,7 +47,7 @@ class NcfModel(ctypes.Structure):
 
 
 class NcfOptim(ctypes.Structure):
-    _fields_ = [("emb_m", _vp), ("emb_v", _vp), ("mlp_m", _vp), ("mlp_v", _vp), ("step", _vp)]
+    _fields_ = [("emb_m", _vp), ("emb_v", _vp), ("mlp_m", _vp), ("mlp_v", _vp), ("step", _vp), ("row_step", _vp)]
 
 
 class NcfHyper(ctypes.Structure):
@@ -77,6 +77,8 @@ _SIGNATURES = {
                                     ctypes.c_size_t, _vp]),
     "ncf_forward_backward": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfHyper), _vp, _vp, _vp, _i64, _vp, _vp,
                                             _vp, _vp, _i64, _i64, _i32, _vp, ctypes.c_size_t, _vp]),
+    "ncf_lazy_flush": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _vp, ctypes.c_size_t,
+                                      _vp]),
     "ncf_apply_update": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _i64, _i64, _vp, _vp,
                                         _vp, _vp, _vp, ctypes.c_size_t, _vp]),
     "ncf_shard_rows": (ctypes.c_int, [_P(NcfShape), _i32, _P(_i64)]),
@@ -99,7 +101,7 @@ _SIGNATURES = {
     "ncf_profile_read": (ctypes.c_int, [_i32, _P(ctypes.c_double), _P(_i64)]),
 }
 EXPORTED = sorted(_SIGNATURES)
-K_INDEX, K_FWD_BWD, K_EMB_UPDATE, K_MLP_UPDATE, K_METRICS, K_SCORE, K_SAMPLE = 1, 2, 3, 4, 5, 6, 7
+K_INDEX, K_FWD_BWD, K_EMB_UPDATE, K_MLP_UPDATE, K_METRICS, K_SCORE, K_SAMPLE, K_CATCHUP = 1, 2, 3, 4, 5, 6, 7, 8
 NCF_SCORE_FP16, NCF_SCORE_FP32, NCF_SCORE_MAX_K = 0, 1, 32
 
 

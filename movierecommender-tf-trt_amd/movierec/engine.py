@@ -36,7 +36,11 @@ class NCFEngine(object):
 
     def __init__(self, num_users, num_items, layers_sizes, gmf_dim=0, max_batch=65536, device=None,
                  optimizer="adam", lr=0.001, beta_1=0.9, beta_2=0.999, layers_l2reg=None,
-                 force_generic=False):
+                 force_generic=False, lazy_adam=False):
+        """``lazy_adam``: deferred exact decay (``ncf_optim_t.row_step``) — a training step updates
+        only the batch's rows, the others catch up on their missed zero-gradient steps when next
+        touched or read; bitwise the dense Keras sweep (F5).  Needs layers_l2reg[0] == 0; the
+        table is flushed before every read (predict, evaluate, scoring, weights export)."""
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device())
         self.device = torch.device(device)
@@ -65,15 +69,16 @@ class NCFEngine(object):
             self.mlp_m = torch.zeros_like(self.mlp)
             self.mlp_v = torch.zeros_like(self.mlp)
             self.step = torch.zeros(1, dtype=torch.int32, device=dev)
+            self.row_step = torch.zeros(s.num_rows, dtype=torch.int32, device=dev) if lazy_adam else None
+            self._dirty = False
             self.stats = torch.zeros(N.NCF_NUM_STATS, dtype=torch.float64, device=dev)
             self.val_stats = torch.zeros(N.NCF_NUM_STATS, dtype=torch.float64, device=dev)
             self.max_batch = 0
             self.ws = None
             self._ensure_ws(int(max_batch))
         self.model_s = N.NcfModel(self.emb.data_ptr(), self.mlp.data_ptr())
-        self.optim_s = N.NcfOptim(self.emb_m.data_ptr(), self.emb_v.data_ptr(), self.mlp_m.data_ptr(),
-                                  self.mlp_v.data_ptr(), self.step.data_ptr())
         self.hyper = N.NcfHyper()
+        self._bind_optim()
         self.set_hyper(optimizer, lr, beta_1, beta_2, layers_l2reg or [0.0] * len(self.layers))
         self.hyper.force_generic = 1 if force_generic else 0
 
@@ -82,7 +87,34 @@ class NCFEngine(object):
     def fast_path(self):
         return bool(self.shape.fast_path) and not self.hyper.force_generic
 
+    def _bind_optim(self):
+        self.optim_s = N.NcfOptim(self.emb_m.data_ptr(), self.emb_v.data_ptr(), self.mlp_m.data_ptr(),
+                                  self.mlp_v.data_ptr(), self.step.data_ptr(),
+                                  self.row_step.data_ptr() if self.row_step is not None else None)
+
+    @property
+    def lazy(self):
+        return self.row_step is not None
+
+    def flush(self):
+        """Deferred decay: bring every row up to the current step (a no-op in dense mode)."""
+        if self.row_step is not None and self._dirty:
+            N.check(N.lib().ncf_lazy_flush(ctypes.byref(self.shape), ctypes.byref(self.model_s),
+                                           ctypes.byref(self.optim_s), ctypes.byref(self.hyper), N.ptr(self.ws),
+                                           self.ws_bytes, N.stream_handle(self.device)))
+        self._dirty = False
+
+    def disable_lazy(self):
+        """Flush and return to the dense sweep (data-parallel paths update every row)."""
+        self.flush()
+        self.row_step = None
+        self._bind_optim()
+
     def set_hyper(self, optimizer, lr, beta_1=0.9, beta_2=0.999, layers_l2reg=None, group=None, k=None):
+        if getattr(self, "row_step", None) is not None:
+            self.flush()  # pending decay is owed under the previous hyper-parameters
+            if layers_l2reg is not None and float(layers_l2reg[0]) != 0.0:
+                self.disable_lazy()
         h = self.hyper
         opt = {"adam": N.NCF_OPT_ADAM, "sgd": N.NCF_OPT_SGD}.get(optimizer)
         if opt is None:
@@ -112,12 +144,14 @@ class NCFEngine(object):
     # --------------------------------------------------- weights marshalling
     def set_keras_weights(self, w):
         """Load a dict of Keras-layout arrays (names as ``keras_weight_names``)."""
+        self.flush()
         emb, flat = self.layout.to_device(w)
         self.emb[:self.num_rows].copy_(torch.from_numpy(emb))
         self.mlp.copy_(torch.from_numpy(flat))
 
     def keras_weights(self, emb=None, mlp=None):
         """Current weights (or the given device tensors in this layout) as a Keras-layout dict."""
+        self.flush()
         e = (self.emb if emb is None else emb)[:self.num_rows].detach().cpu().numpy()
         f = (self.mlp if mlp is None else mlp).detach().cpu().numpy()
         return self.layout.from_device(e, f)
@@ -128,6 +162,7 @@ class NCFEngine(object):
                 int(self.step.item()))
 
     def set_optimizer_state(self, m, v, step):
+        self.flush()
         saved = (self.emb.clone(), self.mlp.clone())
         self.set_keras_weights(m)
         self.emb_m.copy_(self.emb)
@@ -138,6 +173,8 @@ class NCFEngine(object):
         self.emb.copy_(saved[0])
         self.mlp.copy_(saved[1])
         self.step.fill_(int(step))
+        if self.row_step is not None:
+            self.row_step.fill_(int(step))
 
     # ------------------------------------------------------------- hot path
     def _ids(self, x):
@@ -175,6 +212,7 @@ class NCFEngine(object):
                                        ctypes.byref(self.optim_s), ctypes.byref(h), N.ptr(u), N.ptr(i), N.ptr(y), n,
                                        N.ptr(self.stats), N.ptr(probs_out), N.ptr(self.ws), self.ws_bytes,
                                        N.stream_handle(self.device)))
+        self._dirty = self.row_step is not None
 
     def evaluate(self, users, items, labels, group, k, stats=None, probs_out=None):
         u, i, y = self._ids(users), self._ids(items), self._labels(labels)
@@ -183,12 +221,14 @@ class NCFEngine(object):
         h = self.hyper
         h.group, h.k = int(group), int(k)
         h.inv_batch = 1.0 / n
+        self.flush()
         st = self.val_stats if stats is None else stats
         N.check(N.lib().ncf_evaluate(ctypes.byref(self.shape), ctypes.byref(self.model_s), ctypes.byref(h),
                                      N.ptr(u), N.ptr(i), N.ptr(y), n, N.ptr(st), N.ptr(probs_out), N.ptr(self.ws),
                                      self.ws_bytes, N.stream_handle(self.device)))
 
     def predict(self, users, items):
+        self.flush()
         u, i = self._ids(users), self._ids(items)
         n = u.numel()
         self._ensure_ws(n)
@@ -226,6 +266,7 @@ class NCFEngine(object):
         L = N.lib()
         if not L.ncf_score_supported(ctypes.byref(self.shape), prec):
             raise ValueError("model shape not supported by the %s scorer" % precision)
+        self.flush()
         u = self._ids(users)
         n = u.numel()
         items = torch.empty(n, int(k), dtype=torch.int32, device=self.device)
@@ -254,6 +295,8 @@ class NCFEngine(object):
                          reg_rows=None, include_dense_reg=True):
         """This replica's gradients (BCE mean over ``inv_batch``); ``reg_rows`` = (begin, count)
         of the embedding rows whose L2 loss this replica reports (default: all)."""
+        if self.row_step is not None:
+            self.disable_lazy()   # data-parallel updates sweep every row
         u, i, y = self._ids(users), self._ids(items), self._labels(labels)
         n = u.numel()
         self._ensure_ws(n)
@@ -269,6 +312,8 @@ class NCFEngine(object):
     def apply_update(self, grads, inv_batch, rows=None, emb_grad=None):
         """Optimizer step: embedding rows ``rows`` = (begin, count) (default: all) from
         ``emb_grad`` (default grads[0]; indexed from ``begin``), every dense parameter."""
+        if self.row_step is not None:
+            self.disable_lazy()
         eg, mg, sm = grads
         eg = eg if emb_grad is None else emb_grad
         r0, rc = (0, self.num_rows) if rows is None else rows
@@ -281,6 +326,8 @@ class NCFEngine(object):
     def shard_optimizer_state(self, row_begin, row_count, capacity_rows):
         """Replicated data parallelism: keep Adam moments only for this rank's embedding shard
         and pad the table to ``capacity_rows`` (= world * shard rows) for the all-gather."""
+        if self.row_step is not None:
+            self.disable_lazy()
         rows = int(capacity_rows)
         if rows > self.emb.shape[0]:
             emb = torch.zeros(rows, self.row_width, dtype=torch.float32, device=self.device)
@@ -289,8 +336,7 @@ class NCFEngine(object):
         self.emb_m = self.emb_m[row_begin:row_begin + row_count].clone()
         self.emb_v = self.emb_v[row_begin:row_begin + row_count].clone()
         self.model_s = N.NcfModel(self.emb.data_ptr(), self.mlp.data_ptr())
-        self.optim_s = N.NcfOptim(self.emb_m.data_ptr(), self.emb_v.data_ptr(), self.mlp_m.data_ptr(),
-                                  self.mlp_v.data_ptr(), self.step.data_ptr())
+        self._bind_optim()
 
     # ------------------------------------------------------------- stats
     @staticmethod

@@ -233,7 +233,8 @@ class MovierecModel(object):
         from .engine import NCFEngine
         eng = NCFEngine(self._num_users, self._num_items, self._layers_sizes, self._gmf_dim,
                         max_batch=self._max_batch, optimizer=self._optimizer, lr=self._lr, beta_1=self._beta_1,
-                        beta_2=self._beta_2, layers_l2reg=self._layers_l2reg)
+                        beta_2=self._beta_2, layers_l2reg=self._layers_l2reg,
+                        lazy_adam=bool(params_lazy(self._layers_l2reg)))
         eng.set_keras_weights(initial_weights(self._num_users, self._num_items, self._layers_sizes, self._gmf_dim,
                                               self._seed))
         return NCFNetwork(eng, self._layers_sizes, self._gmf_dim, self._num_negs_per_pos,
@@ -472,6 +473,11 @@ def discounted_cumulative_gain(y_true, _, k, pred_rank_idx):
     hits, pos = _get_hits_per_user(y_true, pred_rank_idx, k)
     dcg = np.float32(math.log(2.0)) / np.log(pos.astype(np.float32) + np.float32(2.0))
     return float(np.mean(dcg * hits, axis=-1))
+
+
+def params_lazy(layers_l2reg):
+    """Deferred exact decay is used whenever the embedding L2 is off (trainer default)."""
+    return float(layers_l2reg[0]) == 0.0
 
 
 def params_copy(params):

@@ -237,3 +237,35 @@ def test_invalid_params_raise():
     u, i, y = _batch(shape, 12, 4, 0)
     with pytest.raises(ValueError):
         eng.train_step(u, i, y, group=5, k=2)  # batch not divisible by group
+
+
+@pytest.mark.parametrize("opt", ["adam", "sgd"])
+@pytest.mark.parametrize("dims", [SHAPES[3], SHAPES[1]], ids=["configC", "small"])
+def test_lazy_decay_bitwise_equals_dense_sweep(dims, opt):
+    """Deferred exact decay (ncf_optim_t.row_step): rows untouched for several steps replay
+    their zero-gradient Adam steps when next touched or flushed — bitwise the dense sweep."""
+    shape = O.NCFShape(*dims)
+    w = _weights(shape, 12)
+    lr = 0.001 if opt == "adam" else 0.05
+    dense = _engine(shape, w, optimizer=opt, lr=lr)
+    lazy = _engine(shape, w, optimizer=opt, lr=lr, lazy_adam=True)
+    assert lazy.lazy and not dense.lazy
+    for s in range(7):
+        # small batches over a larger table: most rows stay untouched for several steps
+        users, items, y = _batch(shape, 24, 4, 40 + s, dup_items=min(shape.num_items, 11) if s % 3 == 0 else None)
+        dense.train_step(users, items, y, group=4, k=2)
+        lazy.train_step(users, items, y, group=4, k=2)
+        if s in (2, 6):
+            lazy.flush()
+            assert torch.equal(dense.emb, lazy.emb) and torch.equal(dense.mlp, lazy.mlp)
+            if opt == "adam":
+                assert torch.equal(dense.emb_m, lazy.emb_m) and torch.equal(dense.emb_v, lazy.emb_v)
+            assert int(lazy.row_step.min()) == int(lazy.step.item()) == s + 1
+    # reads flush implicitly
+    users, items, y = _batch(shape, 40, 4, 99)
+    dense.train_step(users, items, y, group=4, k=2)
+    lazy.train_step(users, items, y, group=4, k=2)
+    assert torch.equal(dense.predict(users, items), lazy.predict(users, items))
+    assert torch.equal(dense.emb, lazy.emb)
+    np.testing.assert_array_equal(dense.keras_weights()["item_embedding"], lazy.keras_weights()["item_embedding"])
+    assert NCFEngine.read_stats(dense.stats) == NCFEngine.read_stats(lazy.stats)
