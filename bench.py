@@ -71,8 +71,8 @@ def parse():
                          "ml-20m-shaped synthetic ratings set (20M positives)")
     ap.add_argument("--dense-sweep", action="store_true",
                     help="sweep every embedding row every step instead of the deferred exact decay (same result)")
-    ap.add_argument("--dp", default="auto", choices=["auto", "sharded", "replicated"],
-                    help="multi-GPU table layout (auto: single engine at N=1, sharded at N>1)")
+    ap.add_argument("--dp", default="auto", choices=["auto", "user", "sharded", "replicated"],
+                    help="multi-GPU layout (auto: single engine at N=1, user-partitioned at N>1)")
     return ap.parse_args()
 
 
@@ -226,19 +226,21 @@ def score_main(args, cfg, world, rank):
         dist.destroy_process_group()
 
 
-def synthetic_device_generator(cfg, batch, group, seed):
+def synthetic_device_generator(cfg, batch, group, seed, num_users=None, world=1):
     """ml-20m-shaped synthetic ratings (20M positives over the config's users x items, uniform)
-    behind the on-device sampler: a step = sample one batch + train on it."""
+    behind the on-device sampler: a step = sample one batch + train on it.  User-partitioned
+    data parallelism: this rank's 1/world of the ratings over its ``num_users`` (local ids)."""
     import pandas as pd
     from movierec.sampler import DeviceMovieLensDataGenerator
     from movierec.util import movielens_utils as ml
     rng = np.random.RandomState(seed)
-    n = 20000263  # ml-20m ratings
-    df = pd.DataFrame({"userId": rng.randint(0, cfg["num_users"], n).astype(np.int32),
+    n = 20000263 // world  # ml-20m ratings
+    nu = cfg["num_users"] if num_users is None else int(num_users)
+    df = pd.DataFrame({"userId": rng.randint(0, nu, n).astype(np.int32),
                        "itemId": rng.randint(0, cfg["num_items"], n).astype(np.int32)})
     name = "ml-20m"
     saved = (ml.NUM_USERS[name], ml.NUM_ITEMS[name])
-    ml.NUM_USERS[name], ml.NUM_ITEMS[name] = cfg["num_users"], cfg["num_items"]
+    ml.NUM_USERS[name], ml.NUM_ITEMS[name] = nu, cfg["num_items"]
     try:
         gen = DeviceMovieLensDataGenerator(name, df, batch, group - 1, seed=seed)
     finally:
@@ -266,7 +268,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
-    mode = args.dp if args.dp != "auto" else ("single" if world == 1 else "sharded")
+    mode = args.dp if args.dp != "auto" else ("single" if world == 1 else "user")
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     elif mode != "single":
@@ -298,6 +300,14 @@ def main():
                                rank=rank, max_batch=B, force_generic=args.generic)
         eng.set_keras_weights(w0)
         dp = RowShardedDataParallel(eng)
+    elif mode == "user":
+        from movierec.distributed import UserPartitionedDataParallel, partition_keras_weights
+        n_loc = (cfg["num_users"] - rank + world - 1) // world
+        eng = NCFEngine(n_loc, cfg["num_items"], cfg["layers"], cfg["gmf_dim"], max_batch=B,
+                        force_generic=args.generic)
+        eng.set_keras_weights(partition_keras_weights(w0, world, rank))
+        dp = UserPartitionedDataParallel(eng)
+        dp.broadcast_parameters()
     else:
         eng = NCFEngine(cfg["num_users"], cfg["num_items"], cfg["layers"], cfg["gmf_dim"], max_batch=B,
                         force_generic=args.generic, lazy_adam=(mode == "single" and not args.dense_sweep))
@@ -309,10 +319,16 @@ def main():
     gen = torch.Generator(device="cuda").manual_seed(1234 + rank)
     sampler = None
     if args.e2e:
-        sampler = synthetic_device_generator(cfg, B, g, seed=1234 + rank)
+        if mode in ("user", "single"):
+            sampler = synthetic_device_generator(cfg, B, g, seed=1234 + rank, world=world,
+                                                 num_users=eng.num_users if mode == "user" else None)
+        else:
+            raise SystemExit("--e2e supports the single-table and user-partitioned layouts")
     pool = []
     for _ in range(args.pool):
-        u = torch.randint(0, cfg["num_users"], (B // g,), generator=gen, device="cuda", dtype=torch.int32)
+        # user-partitioned data: this rank's users only, as local ids (u // world)
+        u = torch.randint(0, eng.num_users if mode == "user" else cfg["num_users"], (B // g,), generator=gen,
+                          device="cuda", dtype=torch.int32)
         u = u.repeat_interleave(g)
         it = torch.randint(0, cfg["num_items"], (B,), generator=gen, device="cuda", dtype=torch.int32)
         y = torch.tensor([0.0] * (g - 1) + [1.0], device="cuda").repeat(B // g)
@@ -373,12 +389,14 @@ def main():
         touched = float(np.mean([torch.unique(u).numel() + torch.unique(it).numel() for u, it, _ in pool]))
         nbytes = emb_update_bytes(eng.shape, B, touched_rows=touched)
     else:
-        nbytes = emb_update_bytes(eng.shape, B, dense_rows=dp.row_count if dp is not None else None)
+        nbytes = emb_update_bytes(eng.shape, B, dense_rows=(dp.row_count if mode == "replicated" else
+                                                            eng.num_rows if mode == "user" else None))
     achieved = nbytes / (kern_ms * 1e-3) / 1e9
 
     # HR@10 on a synthetic validation set (1 positive + 99 sampled items per user), per rank
     ev_users = 2000
-    ev_u = (torch.arange(ev_users, device="cuda", dtype=torch.int32) + rank * ev_users).repeat_interleave(100)
+    ev_base = 0 if mode == "user" else rank * ev_users   # user mode: this rank's own (local) users
+    ev_u = (torch.arange(ev_users, device="cuda", dtype=torch.int32) + ev_base).repeat_interleave(100)
     ev_i = torch.randint(0, cfg["num_items"], (ev_users * 100,), generator=gen, device="cuda", dtype=torch.int32)
     ev_y = torch.tensor([0.0] * 99 + [1.0], device="cuda").repeat(ev_users)
     if mode == "sharded":
@@ -398,6 +416,9 @@ def main():
                           else "k_emb_update") if mode == "single" else None
     fb_traffic = pmc_traffic("traffic_fb_fused.json") if mode == "single" and eng.fast_path else None
     par = {"single": "dp1 (one table)",
+           "user": "dp%d user-partitioned data (rank r trains users u %% %d == r and alone holds their rows + "
+                   "Adam state); item table replicated; ONE all-reduce per step of [item-row grad | dense-layer "
+                   "grad | summary]" % (world, world),
            "sharded": "dp%d row-sharded tables (rank r owns rows g %% %d == r + their Adam state; all_to_all of "
                       "unique row ids / rows / row grads, all-reduce of the dense-layer grad)" % (world, world),
            "replicated": "dp%d replicated tables (reduce-scatter of the dense embedding grad, sharded Adam, "
@@ -444,6 +465,9 @@ def main():
             "hr_at_10": {"value": round(hr["hr"], 4), "ndcg_at_10": round(hr["dcg"], 4),
                          "data": "synthetic eval groups (random ids; ~0.1 expected for an untrained model)"},
         }
+        if mode == "user":
+            line["exchange"] = {"allreduce_bytes_per_step": dp.shared.numel() * dp.shared.element_size(),
+                                "local_users": eng.num_users, "collectives_per_step": 1}
         if mode == "sharded":
             line["exchange"] = {"unique_rows_per_rank": train_exchange[0],
                                 "rows_served_per_rank": train_exchange[1],

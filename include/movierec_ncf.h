@@ -191,6 +191,35 @@ int ncf_apply_update(const ncf_shape_t* shape, ncf_model_t* model, ncf_optim_t* 
                      int64_t row_begin, int64_t row_count, const float* emb_grad, const float* mlp_grad,
                      const float* summary, double* stats, void* ws, size_t ws_bytes, void* stream);
 
+/* User-partitioned data parallelism (no reference counterpart — the
+ * reference trains on one CPU).  The training ratings are partitioned by user:
+ * rank r trains the users u % world == r, so rows [0, shared_row_begin) of its
+ * table (its own users, local row u / world) are read and written by this rank
+ * only, and rows [shared_row_begin, num_rows) (the items) are replicated.  A step:
+ *   ncf_forward_backward_part  = ncf_forward_backward, but the dense embedding
+ *                              gradient shared_grad is written for the replicated
+ *                              rows only (indexed from shared_row_begin); the
+ *                              per-sample gradient rows stay in ws
+ *   all_reduce                 [shared_grad | mlp_grad | summary] (RCCL, async)
+ *   ncf_update_rows            meanwhile: fused scatter-add + optimizer of the own
+ *                              rows [row_begin, row_begin + row_count) from the
+ *                              per-sample rows in ws (n = the batch size given to
+ *                              ncf_forward_backward_part, which fixes where they
+ *                              sit in ws; optim->emb_m/emb_v indexed
+ *                              by table row; step *optim->step + 1, not bumped)
+ *   ncf_apply_update           the replicated rows (row_begin = shared_row_begin,
+ *                              moments pointers offset to that row), the dense
+ *                              layers, stats, step++.
+ * The result equals ncf_train_step on the concatenated global batch up to fp32
+ * summation order of the cross-rank sum. */
+int ncf_forward_backward_part(const ncf_shape_t* shape, const ncf_model_t* model, const ncf_hyper_t* hyper,
+                              const int32_t* users, const int32_t* items, const float* labels, int64_t n,
+                              int64_t shared_row_begin, float* shared_grad, float* mlp_grad, float* summary,
+                              float* probs_out, int64_t reg_row_begin, int64_t reg_row_count,
+                              int32_t include_dense_reg, void* ws, size_t ws_bytes, void* stream);
+int ncf_update_rows(const ncf_shape_t* shape, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* hyper,
+                    int64_t n, int64_t row_begin, int64_t row_count, void* ws, size_t ws_bytes, void* stream);
+
 /* Row-sharded data parallelism (no reference counterpart — the
  * reference trains on one CPU).  Rank r of `world` (1..16) owns the table rows g
  * (users 0..U-1, items U..U+I-1) with g % world == r, stored at local row

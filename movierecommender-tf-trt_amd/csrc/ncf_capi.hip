@@ -469,10 +469,11 @@ int ncf_train_step(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* optim,
     return hip_check(e, "stats");
 }
 
-int ncf_forward_backward(const ncf_shape_t* s, const ncf_model_t* model, const ncf_hyper_t* h, const int32_t* users,
-                         const int32_t* items, const float* labels, int64_t n, float* emb_grad, float* mlp_grad,
-                         float* summary, float* probs_out, int64_t reg_row_begin, int64_t reg_row_count,
-                         int32_t include_dense_reg, void* ws, size_t ws_bytes, void* stream) {
+static int forward_backward_rows(const ncf_shape_t* s, const ncf_model_t* model, const ncf_hyper_t* h,
+                                 const int32_t* users, const int32_t* items, const float* labels, int64_t n,
+                                 int64_t grad_row_begin, float* emb_grad, float* mlp_grad, float* summary,
+                                 float* probs_out, int64_t reg_row_begin, int64_t reg_row_count,
+                                 int32_t include_dense_reg, void* ws, size_t ws_bytes, void* stream) {
     if (int r = check_train_args(s, model, h, users, items, labels, n)) return r;
     if (!emb_grad || !mlp_grad || !summary) return fail(NCF_EINVAL, "NULL gradient output");
     if (reg_row_begin < 0 || reg_row_count < 0 || reg_row_begin > s->num_rows)
@@ -498,9 +499,50 @@ int ncf_forward_backward(const ncf_shape_t* s, const ncf_model_t* model, const n
     }
     e = ncf::launch_summary(L, ws, fb.nbce, fb.nmet, fb.n_groups, nreg_emb, nreg_mlp, summary, st2);
     if (e != hipSuccess) return hip_check(e, "summary");
-    e = ncf::launch_emb_grad_dense(*s, L, ws, emb_grad, st);
+    e = ncf::launch_emb_grad_dense(*s, L, ws, emb_grad, st, grad_row_begin);
     if (e != hipSuccess) return hip_check(e, "dense embedding gradient");
     return hip_check(join_side(st, ss), "side-stream join");
+}
+
+int ncf_forward_backward(const ncf_shape_t* s, const ncf_model_t* model, const ncf_hyper_t* h, const int32_t* users,
+                         const int32_t* items, const float* labels, int64_t n, float* emb_grad, float* mlp_grad,
+                         float* summary, float* probs_out, int64_t reg_row_begin, int64_t reg_row_count,
+                         int32_t include_dense_reg, void* ws, size_t ws_bytes, void* stream) {
+    return forward_backward_rows(s, model, h, users, items, labels, n, 0, emb_grad, mlp_grad, summary, probs_out,
+                                 reg_row_begin, reg_row_count, include_dense_reg, ws, ws_bytes, stream);
+}
+
+int ncf_forward_backward_part(const ncf_shape_t* s, const ncf_model_t* model, const ncf_hyper_t* h,
+                              const int32_t* users, const int32_t* items, const float* labels, int64_t n,
+                              int64_t shared_row_begin, float* shared_grad, float* mlp_grad, float* summary,
+                              float* probs_out, int64_t reg_row_begin, int64_t reg_row_count,
+                              int32_t include_dense_reg, void* ws, size_t ws_bytes, void* stream) {
+    if (!s) return fail(NCF_EINVAL, "NULL shape");
+    if (shared_row_begin < 0 || shared_row_begin > s->num_rows) return fail(NCF_EINVAL, "invalid shared row range");
+    return forward_backward_rows(s, model, h, users, items, labels, n, shared_row_begin, shared_grad, mlp_grad, summary,
+                                 probs_out, reg_row_begin, reg_row_count, include_dense_reg, ws, ws_bytes, stream);
+}
+
+int ncf_update_rows(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* h,
+                    int64_t n, int64_t row_begin, int64_t row_count, void* ws, size_t ws_bytes, void* stream) {
+    if (int r = check_shape(s)) return r;
+    if (int r = check_hyper(h)) return r;
+    if (!model || !model->emb) return fail(NCF_EINVAL, "NULL device pointer");
+    if (!optim || !optim->step || (h->optimizer == NCF_OPT_ADAM && (!optim->emb_m || !optim->emb_v)))
+        return fail(NCF_EINVAL, "NULL optimizer state");
+    if (row_begin < 0 || row_count < 0 || row_begin + row_count > s->num_rows)
+        return fail(NCF_EINVAL, "invalid row range");
+    // the per-sample rows, list and offsets sit where the layout of the preceding batch n put them
+    ncf::WsLayout L;
+    if (int r = check_ws(*s, n, ws, ws_bytes, &L)) return r;
+    hipStream_t st = (hipStream_t)stream;
+    const int64_t off = row_begin * s->row_width;
+    prof_begin(NCF_K_EMB_UPDATE, st);
+    hipError_t e = ncf::launch_emb_update(*s, L, ws, model->emb + off, optim->emb_m ? optim->emb_m + off : nullptr,
+                                          optim->emb_v ? optim->emb_v + off : nullptr, optim->step, *h, nullptr,
+                                          row_count, st, nullptr, row_begin);
+    prof_end(NCF_K_EMB_UPDATE, st);
+    return hip_check(e, "local row update");
 }
 
 int ncf_evaluate(const ncf_shape_t* s, const ncf_model_t* model, const ncf_hyper_t* h, const int32_t* users,

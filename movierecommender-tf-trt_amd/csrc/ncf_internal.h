@@ -164,7 +164,7 @@ enum GradSource { kGradSparse = 0, kGradDense = 1 };
 // per-contribution rows) through the workspace index
 hipError_t launch_emb_update(const ncf_shape_t& s, const WsLayout& L, void* ws, float* emb, float* m, float* v,
                              const int32_t* step, const ncf_hyper_t& h, const float* dense_grad, int64_t rows,
-                             hipStream_t st, const float* gs = nullptr);
+                             hipStream_t st, const float* gs = nullptr, int64_t offs_row = 0);
 // deferred exact decay (ncf_update.hip, L2 off): replay the missed zero-gradient Adam steps of
 // the touched rows (all_rows: every row, ncf_lazy_flush) up to *step; then the step's update of
 // the touched rows, which records row_step[r] = *step + 1.  Bitwise the dense sweep.
@@ -175,7 +175,9 @@ hipError_t launch_row_step_fill(int32_t* row_step, int64_t R, const int32_t* ste
 hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, void* ws, float* emb, float* m,
                                      float* v, int32_t* row_step, const int32_t* step, const ncf_hyper_t& h,
                                      hipStream_t st);
-hipError_t launch_emb_grad_dense(const ncf_shape_t& s, const WsLayout& L, void* ws, float* out, hipStream_t st);
+// dense gradient of rows [row_begin, num_rows) into out (indexed from row_begin)
+hipError_t launch_emb_grad_dense(const ncf_shape_t& s, const WsLayout& L, void* ws, float* out, hipStream_t st,
+                                  int64_t row_begin = 0);
 // mlp: reduce slabs (if nslab > 0) or read grad_in; optionally write grad_out; optionally update
 hipError_t launch_mlp_update(const ncf_shape_t& s, const WsLayout& L, void* ws, float* mlp, float* m, float* v,
                              const int32_t* step, const ncf_hyper_t& h, int nslab, const float* grad_in,

@@ -477,10 +477,11 @@ static L2Table make_l2_table(const ncf_shape_t& s, const ncf_hyper_t& h) {
 
 hipError_t launch_emb_update(const ncf_shape_t& s, const WsLayout& L, void* ws, float* emb, float* m, float* v,
                              const int32_t* step, const ncf_hyper_t& h, const float* dense_grad, int64_t rows,
-                             hipStream_t st, const float* gs_rows) {
+                             hipStream_t st, const float* gs_rows, int64_t offs_row) {
     const uint32_t w4 = (uint32_t)(s.row_width / 4);
     const uint32_t n4 = (uint32_t)(rows * w4);
-    const int32_t* offs = at<int32_t>(ws, L.offs);
+    if (n4 == 0) return hipSuccess;
+    const int32_t* offs = at<int32_t>(ws, L.offs) + offs_row;
     const int32_t* list = at<int32_t>(ws, L.list);
     const float4* gs = gs_rows ? (const float4*)gs_rows : at<const float4>(ws, L.gs);
     float* part = at<float>(ws, L.part_reg);
@@ -549,10 +550,12 @@ hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, vo
     return hipGetLastError();
 }
 
-hipError_t launch_emb_grad_dense(const ncf_shape_t& s, const WsLayout& L, void* ws, float* out, hipStream_t st) {
+hipError_t launch_emb_grad_dense(const ncf_shape_t& s, const WsLayout& L, void* ws, float* out, hipStream_t st,
+                                  int64_t row_begin) {
     const uint32_t w4 = (uint32_t)(s.row_width / 4);
-    const uint32_t n4 = (uint32_t)(s.num_rows * w4);
-    launch(k_emb_grad_dense, kUpdateGrid, kBlock, 0, st, (float4*)out, n4, w4, at<int32_t>(ws, L.offs),
+    const uint32_t n4 = (uint32_t)((s.num_rows - row_begin) * w4);
+    if (n4 == 0) return hipSuccess;
+    launch(k_emb_grad_dense, kUpdateGrid, kBlock, 0, st, (float4*)out, n4, w4, at<int32_t>(ws, L.offs) + row_begin,
                                                      at<int32_t>(ws, L.list), at<const float4>(ws, L.gs));
     return hipGetLastError();
 }

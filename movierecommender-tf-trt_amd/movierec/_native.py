@@ -77,6 +77,11 @@ _SIGNATURES = {
                                     ctypes.c_size_t, _vp]),
     "ncf_forward_backward": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfHyper), _vp, _vp, _vp, _i64, _vp, _vp,
                                             _vp, _vp, _i64, _i64, _i32, _vp, ctypes.c_size_t, _vp]),
+    "ncf_forward_backward_part": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfHyper), _vp, _vp, _vp, _i64,
+                                                 _i64, _vp, _vp, _vp, _vp, _i64, _i64, _i32, _vp, ctypes.c_size_t,
+                                                 _vp]),
+    "ncf_update_rows": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _i64, _i64, _i64, _vp,
+                                       ctypes.c_size_t, _vp]),
     "ncf_lazy_flush": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _vp, ctypes.c_size_t,
                                       _vp]),
     "ncf_apply_update": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _i64, _i64, _vp, _vp,

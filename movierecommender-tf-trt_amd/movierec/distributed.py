@@ -8,6 +8,12 @@ all-reduced.  Two table layouts:
 ``ReplicatedDataParallel`` — every rank holds the whole table (the north star's
 layout at MovieLens scale).
 
+``UserPartitionedDataParallel`` — the training ratings are partitioned by user
+(rank r trains the users u % world == r and alone holds their rows and Adam
+state); the item table is replicated and its dense gradient is all-reduced in
+the same RCCL call as the dense-layer gradient.  One collective per step, no
+host synchronisation; the default multi-GPU layout for MovieLens-sized tables.
+
 ``RowShardedDataParallel`` — rank r owns the rows g % world == r and their Adam
 state (SURVEY §8e, config D and the recommended layout for config C's scaling
 run).  Per step only the batch's unique rows move: row ids and row values
@@ -33,6 +39,7 @@ The result equals a single-device step on the concatenated global batch (up
 to fp32 summation order of the cross-rank gradient sum).
 """
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -69,6 +76,23 @@ def _all_to_all(out, inp, out_splits, in_splits, group):
         out.copy_(o)
     else:
         dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
+
+
+def _broadcast(t, src, group):
+    if t.is_cuda and dist.get_backend(group) == "gloo":
+        h = t.cpu()
+        dist.broadcast(h, src, group=group)
+        t.copy_(h)
+    else:
+        dist.broadcast(t, src, group=group)
+
+
+def _all_reduce_async(t, group):
+    """Start an all-reduce; returns the work handle (None if it already completed)."""
+    if t.is_cuda and dist.get_backend(group) == "gloo":
+        _all_reduce(t, group)
+        return None
+    return dist.all_reduce(t, group=group, async_op=True)
 
 
 def _all_reduce(t, group):
@@ -196,3 +220,100 @@ class ReplicatedDataParallel(object):
         dist.all_reduce(sm, group=self.group)
         eng.apply_update(self.grads, inv, rows=(self.row_begin, self.row_count), emb_grad=self.grad_shard)
         _all_gather_inplace(eng.emb, self.shard_rows, self.group)
+
+
+def partition_keras_weights(w, world, rank):
+    """Keras-layout weights of rank ``rank``'s local model under user partitioning: the user
+    rows u % world == rank (local row u // world), every item row, the dense layers."""
+    out = dict(w)
+    for name in ("user_embedding", "user_gmf_embedding"):
+        if name in w:
+            out[name] = w[name][rank::world]
+    return out
+
+
+class UserPartitionedDataParallel(object):
+    """Data parallelism with the training data partitioned by user.
+
+    The reference samples each batch user by user (``data_pipeline.py:115-150``); here rank r
+    is given the ratings of the users u with u % world == r, so a user's embedding row is read
+    and written by one rank only.  Each rank's ``engine`` is an ordinary single-device engine
+    built for ``num_users = ceil((U - r) / world)`` local users (user u at local row u // world)
+    and every item; the item rows and the dense layers are replicated.
+
+    One step:
+
+      1. ``forward_backward_part`` on the local batch (user ids already local), BCE mean over
+         the GLOBAL batch: dense gradient of the item rows, dense-layer gradient and summary,
+         laid out back to back in one buffer; per-sample gradient rows stay in the workspace
+      2. ONE asynchronous ``all_reduce`` of [item-row gradient | dense-layer gradient | summary]
+         (RCCL, on its own stream) ...
+      3. ... while the compute stream applies the fused scatter-add + Adam to the own user rows
+         (``update_rows``), which needs nothing from the other ranks
+      4. wait; ``apply_update``: Adam over the item rows (identical on every rank), the dense
+         layers, stats, step counter
+
+    The own-user gradient never leaves the rank, so each step moves the item table's gradient
+    (ml-20m: 27,278 x 512 B = 14 MB) instead of the whole table's.  The result equals one
+    device stepping on the concatenated global batch, up to fp32 order of the cross-rank sum.
+    """
+
+    def __init__(self, engine, group=None):
+        self.eng = engine
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        U, R, W = int(engine.num_users), int(engine.num_rows), int(engine.row_width)
+        _, mg0, sm0 = engine.alloc_grads(rows=0)
+        P, S = mg0.numel(), sm0.numel()
+        dev = engine.emb.device
+        self.flat = torch.zeros((R - U) * W + P + S, dtype=engine.emb.dtype, device=dev)
+        self.grads = (self.flat[:(R - U) * W].view(R - U, W), self.flat[(R - U) * W:(R - U) * W + P],
+                      self.flat[(R - U) * W + P:])
+        self.shared = self.flat                  # item rows | dense-layer grad | summary
+        self.num_local_users = U
+        # the L2 loss of the replicated item rows is reported by rank 0 only
+        self.reg_rows = (0, R) if self.rank == 0 else (0, U)
+
+    def broadcast_parameters(self, src=0):
+        """Make the replicated part (item rows, dense layers) equal to rank ``src``'s."""
+        U = self.num_local_users
+        items = self.eng.emb[U:self.eng.num_rows]
+        buf = items.contiguous()
+        _broadcast(buf, src, self.group)
+        items.copy_(buf)
+        _broadcast(self.eng.mlp, src, self.group)
+
+    def train_step(self, users, items, labels, group, k, global_batch=None):
+        """``users``: LOCAL user ids (u // world of users owned by this rank)."""
+        n = len(users)
+        gb = n * self.world if global_batch is None else int(global_batch)
+        inv = 1.0 / gb
+        eng = self.eng
+        U, R = self.num_local_users, int(eng.num_rows)
+        eng.forward_backward_part(users, items, labels, group=group, k=k, inv_batch=inv, shared_row_begin=U,
+                                  grads=self.grads, reg_rows=self.reg_rows, include_dense_reg=self.rank == 0)
+        work = _all_reduce_async(self.shared, self.group)
+        eng.update_rows(0, U, inv)               # own users: overlaps the all-reduce
+        if work is not None:
+            work.wait()
+        eng.apply_update(self.grads, inv, rows=(U, R - U), moments_by_row=True)
+
+    def keras_weights(self):
+        """Full Keras-layout weights (collective: every rank must call it): user rows gathered
+        from their owners, items and dense layers from this rank."""
+        eng = self.eng
+        local = eng.keras_weights() if hasattr(eng, "keras_weights") else eng.weights()
+        out = dict(local)
+        for name in ("user_embedding", "user_gmf_embedding"):
+            if name not in local:
+                continue
+            mine = torch.from_numpy(np.ascontiguousarray(local[name]))
+            rows = [None] * self.world
+            dist.all_gather_object(rows, mine.numpy(), group=self.group)
+            total = sum(r.shape[0] for r in rows)
+            full = np.empty((total,) + mine.shape[1:], dtype=mine.numpy().dtype)
+            for r in range(self.world):
+                full[r::self.world] = rows[r]
+            out[name] = full
+        return out

@@ -309,17 +309,55 @@ class NCFEngine(object):
                                              N.ptr(probs_out), int(r0), int(rc), 1 if include_dense_reg else 0,
                                              N.ptr(self.ws), self.ws_bytes, N.stream_handle(self.device)))
 
-    def apply_update(self, grads, inv_batch, rows=None, emb_grad=None):
+    def forward_backward_part(self, users, items, labels, group, k, inv_batch, shared_row_begin, grads,
+                              probs_out=None, reg_rows=None, include_dense_reg=True):
+        """``forward_backward`` with the dense embedding gradient written for the replicated rows
+        [shared_row_begin, num_rows) only (``grads[0]`` indexed from that row); the own rows are
+        updated from the per-sample gradients by ``update_rows`` (user-partitioned DP)."""
+        if self.row_step is not None:
+            self.disable_lazy()
+        u, i, y = self._ids(users), self._ids(items), self._labels(labels)
+        n = u.numel()
+        self._ensure_ws(n)
+        h = self.hyper
+        h.group, h.k, h.inv_batch = int(group), int(k), float(inv_batch)
+        eg, mg, sm = grads
+        r0, rc = (0, self.num_rows) if reg_rows is None else reg_rows
+        N.check(N.lib().ncf_forward_backward_part(
+            ctypes.byref(self.shape), ctypes.byref(self.model_s), ctypes.byref(h), N.ptr(u), N.ptr(i), N.ptr(y), n,
+            int(shared_row_begin), N.ptr(eg), N.ptr(mg), N.ptr(sm), N.ptr(probs_out), int(r0), int(rc),
+            1 if include_dense_reg else 0, N.ptr(self.ws), self.ws_bytes, N.stream_handle(self.device)))
+        self._part_n = n
+
+    def update_rows(self, row_begin, row_count, inv_batch):
+        """Optimizer step of rows [row_begin, row_begin + row_count) from the per-sample gradient
+        rows of the last ``forward_backward_part`` (step counter not advanced)."""
+        n = getattr(self, "_part_n", None)
+        if n is None:
+            raise RuntimeError("update_rows needs a preceding forward_backward_part")
+        self.hyper.inv_batch = float(inv_batch)
+        N.check(N.lib().ncf_update_rows(ctypes.byref(self.shape), ctypes.byref(self.model_s),
+                                        ctypes.byref(self.optim_s), ctypes.byref(self.hyper), int(n), int(row_begin),
+                                        int(row_count), N.ptr(self.ws), self.ws_bytes,
+                                        N.stream_handle(self.device)))
+
+    def apply_update(self, grads, inv_batch, rows=None, emb_grad=None, moments_by_row=False):
         """Optimizer step: embedding rows ``rows`` = (begin, count) (default: all) from
-        ``emb_grad`` (default grads[0]; indexed from ``begin``), every dense parameter."""
+        ``emb_grad`` (default grads[0]; indexed from ``begin``), every dense parameter.
+        ``moments_by_row``: the Adam moments cover the whole table (indexed by row), not just
+        the range (user-partitioned DP)."""
         if self.row_step is not None:
             self.disable_lazy()
         eg, mg, sm = grads
         eg = eg if emb_grad is None else emb_grad
         r0, rc = (0, self.num_rows) if rows is None else rows
         self.hyper.inv_batch = float(inv_batch)
+        optim = self.optim_s
+        if moments_by_row and r0:
+            optim = N.NcfOptim(self.emb_m[r0:].data_ptr(), self.emb_v[r0:].data_ptr(), self.mlp_m.data_ptr(),
+                               self.mlp_v.data_ptr(), self.step.data_ptr(), None)
         N.check(N.lib().ncf_apply_update(ctypes.byref(self.shape), ctypes.byref(self.model_s),
-                                         ctypes.byref(self.optim_s), ctypes.byref(self.hyper), int(r0), int(rc),
+                                         ctypes.byref(optim), ctypes.byref(self.hyper), int(r0), int(rc),
                                          N.ptr(eg), N.ptr(mg), N.ptr(sm), N.ptr(self.stats), N.ptr(self.ws),
                                          self.ws_bytes, N.stream_handle(self.device)))
 

@@ -20,6 +20,7 @@ class OracleEngine(object):
         self.layout = Layout(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim)
         self.num_rows = self.layout.num_rows
         self.row_width = self.layout.row_width
+        self.num_users, self.num_items = shape.num_users, shape.num_items
         emb, flat = self.layout.to_device(w, dtype=np.float64)
         self.emb = torch.from_numpy(emb)
         self.mlp = torch.from_numpy(flat)
@@ -82,12 +83,30 @@ class OracleEngine(object):
         lr_t = O.adam_lr_t(self.lr, self.b1, self.b2, self.t)
         p.sub_(lr_t * m / (v.sqrt() + O.KERAS_EPSILON))
 
-    def apply_update(self, grads, inv_batch, rows=None, emb_grad=None):
+    def forward_backward_part(self, users, items, labels, group, k, inv_batch, shared_row_begin, grads,
+                              probs_out=None, reg_rows=None, include_dense_reg=True):
+        full = self.alloc_grads()
+        self.forward_backward(users, items, labels, group, k, inv_batch, full, reg_rows=reg_rows,
+                              include_dense_reg=include_dense_reg)
+        self._local_grad = full[0]
+        grads[0][:] = full[0][shared_row_begin:self.num_rows]
+        grads[1][:] = full[1]
+        grads[2][:] = full[2]
+
+    def update_rows(self, row_begin, row_count, inv_batch):
+        t, self.t = self.t, self.t + 1     # this step's t, not advanced
+        sl = slice(row_begin, row_begin + row_count)
+        p = self.emb[sl]
+        self._adam(p, self._local_grad[sl] + 2.0 * self.l2[0] * p, self.emb_m[sl], self.emb_v[sl])
+        self.t = t
+
+    def apply_update(self, grads, inv_batch, rows=None, emb_grad=None, moments_by_row=False):
         self.t += 1
         eg = grads[0] if emb_grad is None else emb_grad
         r0, rc = (0, self.num_rows) if rows is None else rows
         p = self.emb[r0:r0 + rc]
-        self._adam(p, eg[:rc] + 2.0 * self.l2[0] * p, self.emb_m[:rc], self.emb_v[:rc])
+        mo = r0 if moments_by_row else 0
+        self._adam(p, eg[:rc] + 2.0 * self.l2[0] * p, self.emb_m[mo:mo + rc], self.emb_v[mo:mo + rc])
         self._adam(self.mlp, grads[1] + 2.0 * self.mlp_lam * self.mlp, self.mlp_m, self.mlp_v)
 
 

@@ -177,6 +177,74 @@ def test_row_sharded_dp_matches_single_process_cpu(world):
             np.testing.assert_allclose(a[:5], b[:5], rtol=1e-6, atol=1e-9)
 
 
+def _user_part_batches(world):
+    """Per-step, per-rank batches with the users partitioned by rank (u % world == r); global
+    user ids, ranks' parts concatenated in rank order = the global batch."""
+    shape = O.NCFShape(*SHAPE)
+    rng = np.random.RandomState(11)
+    per = B // world
+    out = []
+    for _ in range(STEPS):
+        parts = []
+        for r in range(world):
+            n_loc = (shape.num_users - r + world - 1) // world
+            users = (rng.randint(0, n_loc, per // GROUP) * world + r).repeat(GROUP).astype(np.int32)
+            items = rng.randint(0, shape.num_items, per).astype(np.int32)
+            y = np.tile([0] * (GROUP - 1) + [1], per // GROUP).astype(np.float32)
+            parts.append((users, items, y))
+        out.append(parts)
+    return out
+
+
+def _cpu_user_part_worker(rank, world, port, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [here, os.path.dirname(here), os.path.join(os.path.dirname(here), "movierecommender-tf-trt_amd")]
+    from oracle_engine import OracleEngine
+    from movierec.distributed import UserPartitionedDataParallel, partition_keras_weights
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    shape, w = _weights()
+    n_loc = (shape.num_users - rank + world - 1) // world
+    local = O.NCFShape(n_loc, shape.num_items, shape.layers, shape.gmf_dim)
+    eng = OracleEngine(local, partition_keras_weights(w, world, rank), layers_l2reg=L2)
+    dp = UserPartitionedDataParallel(eng)
+    dp.broadcast_parameters()
+    summaries = []
+    for parts in _user_part_batches(world):
+        users, items, y = parts[rank]
+        dp.train_step(users // world, items, y, group=GROUP, k=2, global_batch=B)
+        summaries.append(dp.grads[2].clone().numpy())
+    q.put((rank, dp.keras_weights(), None, summaries))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_user_partitioned_dp_matches_single_process_cpu(world):
+    """User-partitioned data + replicated items (one all-reduce per step) reproduce the
+    single-process step on the concatenated global batch; world 3 gives unequal user shards."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from oracle_engine import OracleEngine
+    res = _run_cpu(_cpu_user_part_worker, world)
+    shape, w = _weights()
+    ref = OracleEngine(shape, w, layers_l2reg=L2)
+    grads = ref.alloc_grads()
+    ref_summ = []
+    for parts in _user_part_batches(world):
+        users, items, y = (np.concatenate(x) for x in zip(*parts))
+        ref.forward_backward(users, items, y, group=GROUP, k=2, inv_batch=1.0 / B, grads=grads)
+        ref_summ.append(grads[2].clone().numpy())
+        ref.apply_update(grads, 1.0 / B)
+    rw = ref.weights()
+    for r in range(world):
+        wts, _, summ = res[r]
+        for name in rw:
+            np.testing.assert_allclose(wts[name], rw[name], rtol=0, atol=1e-12, err_msg=name)
+        for a, b in zip(summ, ref_summ):
+            np.testing.assert_allclose(a[:5], b[:5], rtol=1e-6, atol=1e-9)
+
+
 # ---------------------------------------------------------------- GPU (HIP)
 
 def _gpu_worker(rank, world, port, q):
@@ -304,4 +372,63 @@ def test_row_sharded_dp_matches_single_process_gpu(world):
         assert st["hr"] == pytest.approx(rst["hr"], abs=1e-6)
         for a, b in zip(pr, rprobs):
             np.testing.assert_allclose(a, b[r * per:(r + 1) * per], rtol=0, atol=2e-6)
+    assert gpu_available()
+
+
+def _gpu_user_part_worker(rank, world, port, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [here, os.path.dirname(here), os.path.join(os.path.dirname(here), "movierecommender-tf-trt_amd")]
+    from movierec.engine import NCFEngine
+    from movierec.distributed import UserPartitionedDataParallel, partition_keras_weights
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    shape, w = _weights()
+    n_loc = (shape.num_users - rank + world - 1) // world
+    eng = NCFEngine(n_loc, shape.num_items, shape.layers, shape.gmf_dim, max_batch=B, layers_l2reg=L2)
+    eng.set_keras_weights(partition_keras_weights(w, world, rank))
+    dp = UserPartitionedDataParallel(eng)
+    dp.broadcast_parameters()
+    for parts in _user_part_batches(world):
+        users, items, y = parts[rank]
+        dp.train_step(users // world, items, y, group=GROUP, k=2, global_batch=B)
+    torch.cuda.synchronize()
+    q.put((rank, dp.keras_weights(), NCFEngine.read_stats(eng.stats)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [1, 2])
+def test_user_partitioned_dp_matches_single_process_gpu(world):
+    """HIP user-partitioned path (gloo between processes sharing the GPU) vs ncf_train_step on
+    the concatenated global batch, at the fp32 tolerance."""
+    from movierec.engine import NCFEngine
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_user_part_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, wts, st = q.get(timeout=300)
+        res[r] = (wts, st)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    shape, w = _weights()
+    ref = NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=B, layers_l2reg=L2)
+    ref.set_keras_weights(w)
+    for parts in _user_part_batches(world):
+        users, items, y = (np.concatenate(x) for x in zip(*parts))
+        ref.train_step(users, items, y, group=GROUP, k=2)
+    rw = ref.keras_weights()
+    rst = NCFEngine.read_stats(ref.stats)
+    for r in range(world):
+        wts, st = res[r]
+        for name in rw:
+            np.testing.assert_allclose(wts[name], rw[name], rtol=0, atol=1e-5, err_msg=name)
+        assert st["loss"] == pytest.approx(rst["loss"], rel=1e-5)
+        assert st["hr"] == pytest.approx(rst["hr"], abs=1e-6)
     assert gpu_available()
