@@ -48,6 +48,9 @@ CONFIGS = {
               num_users=138493, num_items=27278, layers=[128, 64, 32, 16], gmf_dim=64, negs=3, batch=65536),
     "B": dict(workload="ml-1m NeuMF (config B shape): 6040 users x 3952 items, gmf 8 + MLP [64,32,16,8], 4 neg/pos",
               num_users=6040, num_items=3952, layers=[64, 32, 16, 8], gmf_dim=8, negs=4, batch=4095),
+    "D": dict(workload="synthetic 10M users x 1M items (config D): gmf 128 + MLP [256,128,64,32], 3 neg/pos, "
+                       "Adam dense semantics via deferred exact decay, one GPU (layered rocBLAS GEMM path)",
+              num_users=10000000, num_items=1000000, layers=[256, 128, 64, 32], gmf_dim=128, negs=3, batch=65536),
     "E": dict(workload="ml-20m all-item scoring + top-10 (config E): every one of 138493 users x all 27278 items, "
                        "NeuMF gmf 64 + MLP [128,64,32,16] (config C's model), fp16 MFMA / fp32 accumulate",
               num_users=138493, num_items=27278, layers=[128, 64, 32, 16], gmf_dim=64, negs=3, batch=65536),
@@ -249,6 +252,25 @@ def synthetic_device_generator(cfg, batch, group, seed, num_users=None, world=1)
     return gen
 
 
+def device_glorot_init(eng, w_small, seed):
+    """Keras glorot_uniform embedding tables drawn on the device (config D's 11 GB table); dense
+    layers from ``w_small`` (initial_weights of the same layers)."""
+    from movierec.layout import Layout
+    lay = Layout(1, 1, eng.layers, eng.gmf_dim)
+    eng.mlp.copy_(torch.from_numpy(lay.to_device(w_small)[1]))
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    U, G, G4 = eng.num_users, eng.gmf_dim, eng.shape.gmf_stride
+    du, di = eng.shape.du, eng.shape.di
+    eng.emb.zero_()
+    for rows, n, d, col in ((slice(0, U), U, du, G4), (slice(U, eng.num_rows), eng.num_items, di, G4)):
+        for width, c0 in ((G, 0), (d, col)):
+            if width:
+                lim = (6.0 / (n + width)) ** 0.5
+                part = eng.emb[rows, c0:c0 + width]
+                part.copy_(torch.rand(part.shape, generator=g, device="cuda") * (2 * lim) - lim)
+    torch.cuda.synchronize()
+
+
 def pmc_traffic(name, kernel=None):
     """HBM bytes per launch measured by tools/gpu_profile.sh (separate --pmc passes), if the
     committed measurement is of ``kernel``."""
@@ -291,7 +313,11 @@ def main():
         cfg["batch"] = args.batch
     B, g = cfg["batch"], cfg["negs"] + 1
     assert B % g == 0, "batch must be divisible by negs+1"
-    w0 = initial_weights(cfg["num_users"], cfg["num_items"], cfg["layers"], cfg["gmf_dim"], seed=0)
+    big = args.config == "D"   # 11 GB table: initialised on the device, not through host numpy
+    if big and mode != "single":
+        raise SystemExit("config D is benchmarked on one GPU (its row-sharded DP path is covered by tests)")
+    w0 = initial_weights(1 if big else cfg["num_users"], 1 if big else cfg["num_items"], cfg["layers"],
+                         cfg["gmf_dim"], seed=0)
     dp = None
     if mode == "sharded":
         from movierec.sharded import ShardedNCFEngine
@@ -311,7 +337,10 @@ def main():
     else:
         eng = NCFEngine(cfg["num_users"], cfg["num_items"], cfg["layers"], cfg["gmf_dim"], max_batch=B,
                         force_generic=args.generic, lazy_adam=(mode == "single" and not args.dense_sweep))
-        eng.set_keras_weights(w0)
+        if big:
+            device_glorot_init(eng, w0, seed=0)
+        else:
+            eng.set_keras_weights(w0)
         if mode == "replicated":
             from movierec.distributed import ReplicatedDataParallel
             dp = ReplicatedDataParallel(eng)
@@ -426,7 +455,7 @@ def main():
 
     if rank == 0:
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and not big:
             cpu = cpu_baseline(cfg, args.cpu_seconds)
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world,
@@ -437,7 +466,7 @@ def main():
                      "synthetic (uniform ids, seeded; random-init weights)"),
             "config": {"workload": cfg["workload"], "global_batch": B * world, "per_gpu_batch": B,
                        "negatives_per_positive": cfg["negs"], "parallelism": par,
-                       "kernel_path": "generic" if not eng.fast_path else "fused-mfma"},
+                       "kernel_path": getattr(eng, "kernel_path", "fused-mfma" if eng.fast_path else "generic")},
             "roofline": {"bound": "hbm", "kernel": ("embedding scatter-add + Adam on the batch's touched rows "
                                                     "(k_emb_adam_touched; deferred exact decay)"
                                                     if getattr(eng, "lazy", False) else
@@ -447,8 +476,11 @@ def main():
                          "algorithmic_bytes_per_launch": nbytes, "avg_launch_ms": round(kern_ms, 5),
                          "traffic_source": "rocprofv3 --pmc FETCH_SIZE(x2 gfx950) + WRITE_SIZE, "
                                            "profiles/traffic_emb_update.json (per launch)"},
-            "roofline_fwd_bwd": {"bound": "mfma", "kernel": "fused NeuMF forward+backward (k_fb_fused, fp32 MFMA)"
-                                 if eng.fast_path else "generic forward+backward", "achieved": round(
+            "roofline_fwd_bwd": {"bound": "mfma", "kernel": {
+                                     "fused-mfma": "fused NeuMF forward+backward (k_fb_fused, fp32 MFMA)",
+                                     "layered-rocblas": "layer-by-layer forward+backward (rocBLAS fp32 GEMMs + glue "
+                                                        "kernels, ncf_layered.hip)"}.get(
+                                     getattr(eng, "kernel_path", ""), "generic forward+backward"), "achieved": round(
                                      fb_flops / (fb_ms * 1e-3) / 1e12, 2), "peak": FP32_MFMA_PEAK_TFS,
                                  "unit": "TFLOP/s", "frac": round(fb_flops / (fb_ms * 1e-3) / 1e12 /
                                                                   FP32_MFMA_PEAK_TFS, 4),

@@ -114,7 +114,10 @@ typedef struct ncf_hyper {
     int32_t group;                      /* samples per user group (num_negs_per_pos + 1) */
     int32_t k;                          /* top-k of the hr/dcg metrics */
     float inv_batch;                    /* 1 / (global batch) for the BCE mean */
-    int32_t force_generic;              /* 1: use the generic per-sample kernel even if fast_path */
+    int32_t force_generic;              /* 1: the generic per-sample kernel even if fast_path;
+                                           2: the layer-by-layer GEMM path (default for shapes the
+                                           fused kernel does not hold whose dense weights exceed
+                                           12288 floats, e.g. config D) */
     int32_t reserved[6];
 } ncf_hyper_t;
 

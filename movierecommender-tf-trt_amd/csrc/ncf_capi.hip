@@ -152,6 +152,16 @@ bool use_fused(const ncf_shape_t& s, const ncf_hyper_t* h) {
     return s.fast_path && !(h && h->force_generic) && ncf::fused_supported(s);
 }
 
+// Shapes the fused kernel does not hold: the layer-by-layer GEMM path when the dense weights
+// outgrow the generic kernel's LDS staging (config D), or when asked for (force_generic == 2);
+// the per-sample generic kernel for small models (the reference's test shapes) or force_generic == 1.
+bool use_layered(const ncf_shape_t& s, const ncf_hyper_t* h) {
+    if (!ncf::layered_supported(s)) return false;
+    if (h && h->force_generic == 2) return true;
+    if (h && h->force_generic == 1) return false;
+    return !use_fused(s, h) && s.mlp_params > 12288;
+}
+
 }  // namespace
 
 namespace ncf {
@@ -215,6 +225,7 @@ WsLayout make_layout(const ncf_shape_t& s, int64_t B, int world) {
     }
     L.act = take((size_t)B * A * 4);
     L.dz = take((size_t)B * D * 4);
+    L.ones = take((size_t)B * 4);
     L.total = off;
     return L;
 }
@@ -385,6 +396,9 @@ static int run_fb(const ncf_shape_t& s, const ncf::WsLayout& L, const ncf_model_
     if (use_fused(s, h))
         e = ncf::launch_fb_fused(s, L, ws, model->emb, model->mlp, users, items, labels, n, h->inv_batch, ids,
                                  h->group, h->k, &out->nslab, &out->nbce, &out->nmet, st);
+    else if (use_layered(s, h))
+        e = ncf::launch_fb_layered(s, L, ws, model->emb, model->mlp, users, items, labels, n, h->inv_batch, ids,
+                                   &out->nslab, &out->nbce, st);
     else
         e = ncf::launch_fb_generic(s, L, ws, model->emb, model->mlp, users, items, labels, n, h->inv_batch, ids,
                                    &out->nslab, &out->nbce, st);

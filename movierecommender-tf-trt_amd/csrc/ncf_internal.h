@@ -53,7 +53,8 @@ struct WsLayout {
     size_t nuniq;     // int32       number of unique rows (single table: of touched rows)
     size_t touched;   // int32[min(R, 2B)] single table, deferred decay: the touched rows, ascending
     size_t act;       // float[B * A] generic kernel activations
-    size_t dz;        // float[B * D] generic kernel pre-activation gradients
+    size_t dz;        // float[B * D] generic kernel pre-activation grad
+    size_t ones;      // float[B] layered path: all-ones vector (column sums as GEMV)ients
     size_t total;
     int64_t max_batch;
     int nscan;        // blocks of the offset scan
@@ -149,6 +150,12 @@ hipError_t launch_fb_fused(const ncf_shape_t& s, const WsLayout& L, void* ws, co
                            int64_t n, float inv_batch, IdSpace ids, int group, int topk, int* nslab, int* nbce,
                            int* nmet, hipStream_t st);
 bool fused_supported(const ncf_shape_t& s);
+// layer-by-layer path (ncf_layered.hip): rocBLAS fp32 GEMMs + HBM-bound glue kernels, same
+// outputs as launch_fb_generic (probs, gs, part_bce, one slab)
+bool layered_supported(const ncf_shape_t& s);
+hipError_t launch_fb_layered(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, const float* mlp,
+                             const int32_t* users, const int32_t* items, const float* labels, int64_t n,
+                             float inv_batch, IdSpace ids, int* nslab, int* nbce, hipStream_t st);
 
 // metrics / summaries
 hipError_t launch_group_metrics(const float* probs, const float* labels, int64_t n_groups, int group, int k,

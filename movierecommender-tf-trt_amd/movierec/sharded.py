@@ -27,7 +27,7 @@ class ShardedNCFEngine(object):
 
     def __init__(self, num_users, num_items, layers_sizes, gmf_dim=0, world=1, rank=0, max_batch=65536,
                  device=None, optimizer="adam", lr=0.001, beta_1=0.9, beta_2=0.999, layers_l2reg=None,
-                 force_generic=False):
+                 force_generic=False, force_layered=False):
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device())
         self.device = torch.device(device)
@@ -72,7 +72,7 @@ class ShardedNCFEngine(object):
                                   self.mlp_v.data_ptr(), self.step.data_ptr())
         self.hyper = N.NcfHyper()
         self.set_hyper(optimizer, lr, beta_1, beta_2, layers_l2reg or [0.0] * len(self.layers))
-        self.hyper.force_generic = 1 if force_generic else 0
+        self.hyper.force_generic = 1 if force_generic else (2 if force_layered else 0)
 
     # ------------------------------------------------------------------ setup
     @property

@@ -30,6 +30,7 @@ SHAPES = [
     (120, 90, [64, 32, 16, 8], 8),      # config B shape (ml-1m NeuMF) at small row counts
     (200, 150, [128, 64, 32, 16], 64),  # config C shape (ml-20m NeuMF)
     (31, 17, [7, 5], 3),                # odd widths: du != di, gmf not a multiple of 4
+    (40, 30, [256, 128, 64, 32], 128),  # config D shape: weights outgrow LDS -> layered GEMM path
 ]
 
 
@@ -89,12 +90,14 @@ def test_predict_matches_oracle(dims):
 
 
 @pytest.mark.parametrize("dims", SHAPES, ids=[str(s[2]) + "g" + str(s[3]) for s in SHAPES])
-@pytest.mark.parametrize("force_generic", [False, True])
-def test_forward_backward_grads_match_oracle(dims, force_generic):
+@pytest.mark.parametrize("path", ["auto", "generic", "layered"])
+def test_forward_backward_grads_match_oracle(dims, path):
+    """Every forward/backward kernel path (fused MFMA / layered rocBLAS GEMMs / per-sample
+    generic) against the oracle's gradients."""
     shape = O.NCFShape(*dims)
     w = _weights(shape, 3)
     users, items, y = _batch(shape, 256, 4, 4, dup_items=min(shape.num_items, 7))  # heavy duplicate rows
-    eng = _engine(shape, w, force_generic=force_generic)
+    eng = _engine(shape, w, force_generic=path == "generic", force_layered=path == "layered")
     grads = eng.alloc_grads()
     eng.forward_backward(users, items, y, group=4, k=2, inv_batch=1.0 / 256, grads=grads)
     l2 = [0.0] * len(shape.layers)
@@ -240,7 +243,7 @@ def test_invalid_params_raise():
 
 
 @pytest.mark.parametrize("opt", ["adam", "sgd"])
-@pytest.mark.parametrize("dims", [SHAPES[3], SHAPES[1]], ids=["configC", "small"])
+@pytest.mark.parametrize("dims", [SHAPES[3], SHAPES[1], SHAPES[5]], ids=["configC", "small", "configD"])
 def test_lazy_decay_bitwise_equals_dense_sweep(dims, opt):
     """Deferred exact decay (ncf_optim_t.row_step): rows untouched for several steps replay
     their zero-gradient Adam steps when next touched or flushed — bitwise the dense sweep."""
