@@ -31,6 +31,9 @@ __device__ inline float adam_lr_t(float lr, float b1, float b2, int t) {
 // zero-gradient replay round identically.
 __device__ __forceinline__ void adam4(float4& p, float4& m, float4& v, const float4& g, float lr_t, float b1,
                                       float b2, float eps) {
+    // no FMA contraction: which product an fma would absorb depends on how the surrounding
+    // kernel got scheduled, and every caller must round identically
+#pragma clang fp contract(off)
     const float c1 = 1.0f - b1, c2 = 1.0f - b2;
     m.x = b1 * m.x + c1 * g.x; m.y = b1 * m.y + c1 * g.y;
     m.z = b1 * m.z + c1 * g.z; m.w = b1 * m.w + c1 * g.w;
@@ -38,6 +41,13 @@ __device__ __forceinline__ void adam4(float4& p, float4& m, float4& v, const flo
     v.z = b2 * v.z + c2 * (g.z * g.z); v.w = b2 * v.w + c2 * (g.w * g.w);
     p.x -= lr_t * m.x / (sqrtf(v.x) + eps); p.y -= lr_t * m.y / (sqrtf(v.y) + eps);
     p.z -= lr_t * m.z / (sqrtf(v.z) + eps); p.w -= lr_t * m.w / (sqrtf(v.w) + eps);
+}
+
+// adam4's moment updates with g = 0: b1*m + c1*0 and b2*v + c2*0 round like b1*m + 0, b2*v + 0
+__device__ __forceinline__ void decay4(float4& m, float4& v, float b1, float b2) {
+#pragma clang fp contract(off)
+    m.x = b1 * m.x + 0.0f; m.y = b1 * m.y + 0.0f; m.z = b1 * m.z + 0.0f; m.w = b1 * m.w + 0.0f;
+    v.x = b2 * v.x + 0.0f; v.y = b2 * v.y + 0.0f; v.z = b2 * v.z + 0.0f; v.w = b2 * v.w + 0.0f;
 }
 
 template <int OPT, int SRC, bool L2>
@@ -86,6 +96,10 @@ __global__ __launch_bounds__(kBlock) void k_emb_update(float4* __restrict__ emb,
         if (threadIdx.x == 0) part_reg[blockIdx.x] = reg;
     }
 }
+
+#ifndef NCF_CATCHUP_P_ONLY
+#define NCF_CATCHUP_P_ONLY 1
+#endif
 
 // Deferred exact decay ("lazy" dense Adam, L2 off).  Keras' dense Adam (F5) moves EVERY row
 // every step; a row no sample touches gets g = 0, so its update is a pure function of
@@ -144,8 +158,12 @@ __global__ __launch_bounds__(kBlock) void k_emb_catchup(float4* __restrict__ emb
             for (int j = s + 1; j <= t; ++j)
                 adam4(p, m, v, zero, t - j < kLrLut ? lut[t - j] : adam_lr_t(lr, b1, b2, j), b1, b2, eps);
             emb[e] = p;
-            m4[e] = m;
-            v4[e] = v;
+            if (ALL || !NCF_CATCHUP_P_ONLY) {  // the flush leaves the dense state; with P_ONLY the
+                        // per-step replay writes only p (the forward pass reads p) and
+                        // k_emb_adam_touched re-derives m and v from row_step
+                m4[e] = m;
+                v4[e] = v;
+            }
         }
     }
 }
@@ -181,11 +199,17 @@ __global__ __launch_bounds__(kBlock) void k_emb_adam_touched(float4* __restrict_
         const int r = list[i];
         const int o = offs[r];
         const int c = offs[r + 1] - o;
+        const int k = NCF_CATCHUP_P_ONLY ? t - 1 - row_step[r] : 0;  // m/v decay steps still owed
         for (uint32_t q = rl.q; q < w4; q += rl.qstep) {
             const size_t e = (size_t)r * w4 + q;
+            // the row's state does not depend on the gradient chain: its loads go out first and
+            // overlap the list -> gradient-row loads
+            float4 p = emb[e], m = m4[e], v = v4[e];
+            // k_emb_catchup<false> brought p up to step t-1 and left m, v at row_step: the same
+            // per-step decay adam4 applies with g = 0 (b1*m + 0, b2*v + 0), bitwise
+            for (int j = 0; j < k; ++j) decay4(m, v, b1, b2);
             float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
             for (int j = 0; j < c; ++j) g = f4add(g, gs[(size_t)clist[o + j] * w4 + q]);
-            float4 p = emb[e], m = m4[e], v = v4[e];
             adam4(p, m, v, g, lr_t, b1, b2, eps);
             emb[e] = p;
             m4[e] = m;
