@@ -225,9 +225,15 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
         for (int r = 0; r < 16; ++r) dwacc[m][r] = 0.f;
     float acc_bias = 0.f, acc_h3 = 0.f, acc_dbo = 0.f, acc_bce = 0.f, acc_hit = 0.f, acc_dcg = 0.f;
     const bool metrics = part_hit != nullptr;  // groups never straddle a 32-sample block (group | 32)
-    float acc_gmf[S::NGC > 0 ? S::NGC : 1];
+    // output-kernel gradients, accumulated per lane (its own samples) across tiles and reduced
+    // across lanes once, in the epilogue: a per-tile transpose-reduction is a chain of 16
+    // dependent cross-lane shuffles
+    float acc_gmf_l[S::GH > 0 ? S::GH : 1];
 #pragma unroll
-    for (int c = 0; c < (S::NGC > 0 ? S::NGC : 1); ++c) acc_gmf[c] = 0.f;
+    for (int c = 0; c < (S::GH > 0 ? S::GH : 1); ++c) acc_gmf_l[c] = 0.f;
+    float acc_h3_l[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc_h3_l[r] = 0.f;
 
     // dense parameters → LDS (once per persistent workgroup)
     for (int e = tid; e < L0 * L1; e += kBlock) wl[S::SW1 + (e / L1) * S::LW1 + e % L1] = mlp[S::OW1 + e];
@@ -466,7 +472,8 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
                         *reinterpret_cast<float4*>(gi + h * S::GH + f) = gi4;
                     }
                 }
-                acc_gmf[c] += half_transpose_reduce<S::GCH>(contrib, lane);
+#pragma unroll
+                for (int q = 0; q < S::GCH; ++q) acc_gmf_l[c * S::GCH + q] += contrib[q];
             }
         }
         NCF_T(5);
@@ -483,8 +490,10 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
                 g3[t][r] = g;
                 if (f < L3) sb[(S::RG3 + f) * LS + j] = g;
             }
-            const float red = half_transpose_reduce<16>(contrib, lane);
-            if (t == 0) acc_h3 += red;  // NT3 == 1 for the supported shapes
+            if (t == 0) {  // NT3 == 1 for the supported shapes
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc_h3_l[r] += contrib[r];
+            }
         }
         // ---- backward data chain (A = W_l[in][out] read along `in`: row stride out+1)
         f32x16 g2[S::NT2];
@@ -686,7 +695,14 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
     else if (tid < L1 + L2) slab[S::OB2 + (tid - L1)] = acc_bias;
     else if (tid < L1 + L2 + L3) slab[S::OB3 + (tid - L1 - L2)] = acc_bias;
 
-    // output layer: combine the 4 waves in fixed order through LDS
+    // output layer: reduce the per-lane partials across each wave half, then combine the 4
+    // waves in fixed order through LDS
+    float acc_gmf[S::NGC > 0 ? S::NGC : 1];
+    if constexpr (G > 0) {
+#pragma unroll
+        for (int c = 0; c < S::NGC; ++c) acc_gmf[c] = half_transpose_reduce<S::GCH>(acc_gmf_l + c * S::GCH, lane);
+    }
+    acc_h3 = half_transpose_reduce<16>(acc_h3_l, lane);
     float* xw = xch + w * S::XCH;
     if constexpr (G > 0) {
 #pragma unroll
