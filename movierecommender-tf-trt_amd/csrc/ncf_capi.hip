@@ -459,12 +459,20 @@ int ncf_train_step(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* optim,
     // dense-layer tail on the side stream, embedding sweep on the main stream
     SideStream* ss = nullptr;
     hipStream_t st2 = fork_side(st, &ss);
-    hipError_t e = ncf::launch_summary(L, ws, fb.nbce, fb.nmet, fb.n_groups, 0, 0, summary, st2);
-    if (e != hipSuccess) return hip_check(e, "summary");
+    // one stream (the default): the batch summary rides in the slab reduction's launch.  (Folding
+    // the stats into the touched update's last block was measured 8x slower: a device-scope fence
+    // per block on a multi-XCD part writes back L2.)
+    const bool fold = ss == nullptr;
+    hipError_t e = hipSuccess;
+    if (!fold) {
+        e = ncf::launch_summary(L, ws, fb.nbce, fb.nmet, fb.n_groups, 0, 0, summary, st2);
+        if (e != hipSuccess) return hip_check(e, "summary");
+    }
     int nreg_mlp = 0;
     prof_begin(NCF_K_MLP_UPDATE, st2);
     e = ncf::launch_mlp_update(*s, L, ws, model->mlp, optim->mlp_m, optim->mlp_v, optim->step, *h, fb.nslab, nullptr,
-                               nullptr, true, &nreg_mlp, st2);
+                               nullptr, true, &nreg_mlp, st2, false, fold ? fb.nbce : -1, fb.nmet, fb.n_groups,
+                               fold ? summary : nullptr);
     prof_end(NCF_K_MLP_UPDATE, st2);
     if (e != hipSuccess) return hip_check(e, "dense update");
     prof_begin(NCF_K_EMB_UPDATE, st);

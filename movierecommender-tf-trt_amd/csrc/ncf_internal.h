@@ -180,15 +180,19 @@ hipError_t launch_emb_catchup(const ncf_shape_t& s, const WsLayout& L, void* ws,
                               hipStream_t st);
 hipError_t launch_row_step_fill(int32_t* row_step, int64_t R, const int32_t* step, hipStream_t st);
 hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, void* ws, float* emb, float* m,
-                                     float* v, int32_t* row_step, const int32_t* step, const ncf_hyper_t& h,
+                                     float* v, int32_t* row_step, int32_t* step, const ncf_hyper_t& h,
                                      hipStream_t st);
 // dense gradient of rows [row_begin, num_rows) into out (indexed from row_begin)
 hipError_t launch_emb_grad_dense(const ncf_shape_t& s, const WsLayout& L, void* ws, float* out, hipStream_t st,
                                   int64_t row_begin = 0);
 // mlp: reduce slabs (if nslab > 0) or read grad_in; optionally write grad_out; optionally update
+// summary_nbce >= 0: the first-level slab reduction also writes the batch summary (what
+// launch_summary(L, ws, summary_nbce, summary_nmet, n_groups, 0, 0, summary) does)
 hipError_t launch_mlp_update(const ncf_shape_t& s, const WsLayout& L, void* ws, float* mlp, float* m, float* v,
                              const int32_t* step, const ncf_hyper_t& h, int nslab, const float* grad_in,
-                             float* grad_out, bool do_update, int* nreg, hipStream_t st, bool want_reg = false);
+                             float* grad_out, bool do_update, int* nreg, hipStream_t st, bool want_reg = false,
+                             int summary_nbce = -1, int summary_nmet = 0, float n_groups = 0.f,
+                             float* summary = nullptr);
 hipError_t launch_emb_reg(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, int64_t rows,
                           float lam, hipStream_t st);
 hipError_t launch_stats(const WsLayout& L, void* ws, const float* summary, int nreg_emb, int nreg_mlp,

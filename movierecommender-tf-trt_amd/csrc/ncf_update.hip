@@ -43,6 +43,54 @@ __device__ __forceinline__ void adam4(float4& p, float4& m, float4& v, const flo
     p.z -= lr_t * m.z / (sqrtf(v.z) + eps); p.w -= lr_t * m.w / (sqrtf(v.w) + eps);
 }
 
+__device__ inline float block_sum_array(const float* __restrict__ a, int n, float* red) {
+    float x = 0.f;
+    for (int j = threadIdx.x; j < n; j += kBlock) x += a[j];
+    return block_sum_256(x, red);
+}
+
+// batch summary from the per-block partials (whole block)
+__device__ inline void summary_body(const float* __restrict__ part_bce, int nbce, const float* __restrict__ part_hit,
+                                    const float* __restrict__ part_dcg, int nmet, float n_groups,
+                                    const float* __restrict__ reg_emb, int nreg_emb,
+                                    const float* __restrict__ reg_mlp, int nreg_mlp, float* __restrict__ summary,
+                                    float* red) {
+    const float b = block_sum_array(part_bce, nbce, red);
+    const float h = block_sum_array(part_hit, nmet, red);
+    const float d = block_sum_array(part_dcg, nmet, red);
+    const float re = block_sum_array(reg_emb, nreg_emb, red);
+    const float rm = block_sum_array(reg_mlp, nreg_mlp, red);
+    if (threadIdx.x < NCF_NUM_SUMMARY) {
+        const int t = threadIdx.x;
+        summary[t] = t == NCF_SUM_BCE ? b : t == NCF_SUM_HIT ? h : t == NCF_SUM_DCG ? d
+                   : t == NCF_SUM_GROUPS ? n_groups : t == NCF_SUM_REG ? re + rm : 0.f;
+    }
+}
+
+// fold the summary into stats[] (loss, hr, dcg running sums) and bump the step (whole block)
+__device__ inline void stats_body(const float* __restrict__ summary, const float* __restrict__ reg_emb, int nreg_emb,
+                                  const float* __restrict__ reg_mlp, int nreg_mlp, float inv_batch,
+                                  double* __restrict__ stats, int32_t* step, int bump, float* red) {
+    const float re = block_sum_array(reg_emb, nreg_emb, red);
+    const float rm = block_sum_array(reg_mlp, nreg_mlp, red);
+    if (threadIdx.x == 0) {
+        const float loss = summary[NCF_SUM_BCE] * inv_batch + summary[NCF_SUM_REG] + (re + rm);
+        const float ng = summary[NCF_SUM_GROUPS];
+        const float hr = ng > 0.f ? summary[NCF_SUM_HIT] / ng : 0.f;
+        const float dc = ng > 0.f ? summary[NCF_SUM_DCG] / ng : 0.f;
+        if (stats) {
+            stats[NCF_STAT_LOSS_SUM] += (double)loss;
+            stats[NCF_STAT_HR_SUM] += (double)hr;
+            stats[NCF_STAT_DCG_SUM] += (double)dc;
+            stats[NCF_STAT_STEPS] += 1.0;
+            stats[NCF_STAT_LAST_LOSS] = loss;
+            stats[NCF_STAT_LAST_HR] = hr;
+            stats[NCF_STAT_LAST_DCG] = dc;
+        }
+        if (bump) *step += 1;
+    }
+}
+
 // adam4's moment updates with g = 0: b1*m + c1*0 and b2*v + c2*0 round like b1*m + 0, b2*v + 0
 __device__ __forceinline__ void decay4(float4& m, float4& v, float b1, float b2) {
 #pragma clang fp contract(off)
@@ -185,37 +233,37 @@ __global__ __launch_bounds__(kBlock) void k_emb_adam_touched(float4* __restrict_
                                                              const int32_t* __restrict__ offs,
                                                              const int32_t* __restrict__ clist,
                                                              const float4* __restrict__ gs,
-                                                             int32_t* __restrict__ row_step,
-                                                             const int32_t* __restrict__ step, float lr, float b1,
-                                                             float b2, float eps) {
+                                                             int32_t* __restrict__ row_step, const int32_t* step,
+                                                             float lr, float b1, float b2, float eps) {
     const RowLanes rl(w4);
-    if (!rl.on) return;
     const int t = *step + 1;
-    const float lr_t = adam_lr_t(lr, b1, b2, t);
-    const int64_t n = *nlist;
-    const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
-    const int64_t waves = ((int64_t)gridDim.x * kBlock) >> 6;
-    for (int64_t i = wave * rl.rpw + rl.sub; i < n; i += waves * rl.rpw) {
-        const int r = list[i];
-        const int o = offs[r];
-        const int c = offs[r + 1] - o;
-        const int k = NCF_CATCHUP_P_ONLY ? t - 1 - row_step[r] : 0;  // m/v decay steps still owed
-        for (uint32_t q = rl.q; q < w4; q += rl.qstep) {
-            const size_t e = (size_t)r * w4 + q;
-            // the row's state does not depend on the gradient chain: its loads go out first and
-            // overlap the list -> gradient-row loads
-            float4 p = emb[e], m = m4[e], v = v4[e];
-            // k_emb_catchup<false> brought p up to step t-1 and left m, v at row_step: the same
-            // per-step decay adam4 applies with g = 0 (b1*m + 0, b2*v + 0), bitwise
-            for (int j = 0; j < k; ++j) decay4(m, v, b1, b2);
-            float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
-            for (int j = 0; j < c; ++j) g = f4add(g, gs[(size_t)clist[o + j] * w4 + q]);
-            adam4(p, m, v, g, lr_t, b1, b2, eps);
-            emb[e] = p;
-            m4[e] = m;
-            v4[e] = v;
+    if (rl.on) {
+        const float lr_t = adam_lr_t(lr, b1, b2, t);
+        const int64_t n = *nlist;
+        const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+        const int64_t waves = ((int64_t)gridDim.x * kBlock) >> 6;
+        for (int64_t i = wave * rl.rpw + rl.sub; i < n; i += waves * rl.rpw) {
+            const int r = list[i];
+            const int o = offs[r];
+            const int c = offs[r + 1] - o;
+            const int k = NCF_CATCHUP_P_ONLY ? t - 1 - row_step[r] : 0;  // m/v decay steps still owed
+            for (uint32_t q = rl.q; q < w4; q += rl.qstep) {
+                const size_t e = (size_t)r * w4 + q;
+                // the row's state does not depend on the gradient chain: its loads go out first and
+                // overlap the list -> gradient-row loads
+                float4 p = emb[e], m = m4[e], v = v4[e];
+                // k_emb_catchup<false> brought p up to step t-1 and left m, v at row_step: the same
+                // per-step decay adam4 applies with g = 0 (b1*m + 0, b2*v + 0), bitwise
+                for (int j = 0; j < k; ++j) decay4(m, v, b1, b2);
+                float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+                for (int j = 0; j < c; ++j) g = f4add(g, gs[(size_t)clist[o + j] * w4 + q]);
+                adam4(p, m, v, g, lr_t, b1, b2, eps);
+                emb[e] = p;
+                m4[e] = m;
+                v4[e] = v;
+            }
+            if (rl.q == 0) row_step[r] = t;
         }
-        if (rl.q == 0) row_step[r] = t;
     }
 }
 
@@ -298,8 +346,25 @@ __global__ __launch_bounds__(kBlock) void k_gather_rows(float4* __restrict__ out
 }
 
 // First level of the slab reduction: group c sums slabs [c*per, (c+1)*per) in order.
+struct SummaryArgs {
+    float* summary;            // nullptr: no summary block
+    const float* part_bce;
+    const float* part_hit;
+    const float* part_dcg;
+    int nbce, nmet;
+    float n_groups;
+};
+
 __global__ __launch_bounds__(kBlock) void k_slab_partial(const float* __restrict__ slabs, int P, int nslab, int per,
-                                                         float* __restrict__ part) {
+                                                         float* __restrict__ part, SummaryArgs sa) {
+    if (sa.summary && blockIdx.x == gridDim.x - 1) {  // the extra column: the batch summary
+        if (blockIdx.y == 0) {
+            __shared__ float red[4];
+            summary_body(sa.part_bce, sa.nbce, sa.part_hit, sa.part_dcg, sa.nmet, sa.n_groups, nullptr, 0, nullptr, 0,
+                         sa.summary, red);
+        }
+        return;
+    }
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= P) return;
     const int s0 = blockIdx.y * per;
@@ -434,11 +499,6 @@ __global__ __launch_bounds__(kBlock) void k_rank(const float* __restrict__ probs
     }
 }
 
-__device__ inline float block_sum_array(const float* __restrict__ a, int n, float* red) {
-    float x = 0.f;
-    for (int j = threadIdx.x; j < n; j += kBlock) x += a[j];
-    return block_sum_256(x, red);
-}
 
 __global__ __launch_bounds__(kBlock) void k_summary(const float* __restrict__ part_bce, int nbce,
                                                     const float* __restrict__ part_hit,
@@ -447,16 +507,8 @@ __global__ __launch_bounds__(kBlock) void k_summary(const float* __restrict__ pa
                                                     const float* __restrict__ reg_mlp, int nreg_mlp,
                                                     float* __restrict__ summary) {
     __shared__ float red[4];
-    const float b = block_sum_array(part_bce, nbce, red);
-    const float h = block_sum_array(part_hit, nmet, red);
-    const float d = block_sum_array(part_dcg, nmet, red);
-    const float re = block_sum_array(reg_emb, nreg_emb, red);
-    const float rm = block_sum_array(reg_mlp, nreg_mlp, red);
-    if (threadIdx.x < NCF_NUM_SUMMARY) {
-        const int t = threadIdx.x;
-        summary[t] = t == NCF_SUM_BCE ? b : t == NCF_SUM_HIT ? h : t == NCF_SUM_DCG ? d
-                   : t == NCF_SUM_GROUPS ? n_groups : t == NCF_SUM_REG ? re + rm : 0.f;
-    }
+    summary_body(part_bce, nbce, part_hit, part_dcg, nmet, n_groups, reg_emb, nreg_emb, reg_mlp, nreg_mlp, summary,
+                 red);
 }
 
 __global__ __launch_bounds__(kBlock) void k_stats(const float* __restrict__ summary,
@@ -464,24 +516,7 @@ __global__ __launch_bounds__(kBlock) void k_stats(const float* __restrict__ summ
                                                   const float* __restrict__ reg_mlp, int nreg_mlp, float inv_batch,
                                                   double* __restrict__ stats, int32_t* step, int bump) {
     __shared__ float red[4];
-    const float re = block_sum_array(reg_emb, nreg_emb, red);
-    const float rm = block_sum_array(reg_mlp, nreg_mlp, red);
-    if (threadIdx.x == 0) {
-        const float loss = summary[NCF_SUM_BCE] * inv_batch + summary[NCF_SUM_REG] + (re + rm);
-        const float ng = summary[NCF_SUM_GROUPS];
-        const float hr = ng > 0.f ? summary[NCF_SUM_HIT] / ng : 0.f;
-        const float dc = ng > 0.f ? summary[NCF_SUM_DCG] / ng : 0.f;
-        if (stats) {
-            stats[NCF_STAT_LOSS_SUM] += (double)loss;
-            stats[NCF_STAT_HR_SUM] += (double)hr;
-            stats[NCF_STAT_DCG_SUM] += (double)dc;
-            stats[NCF_STAT_STEPS] += 1.0;
-            stats[NCF_STAT_LAST_LOSS] = loss;
-            stats[NCF_STAT_LAST_HR] = hr;
-            stats[NCF_STAT_LAST_DCG] = dc;
-        }
-        if (bump) *step += 1;
-    }
+    stats_body(summary, reg_emb, nreg_emb, reg_mlp, nreg_mlp, inv_batch, stats, step, bump, red);
 }
 
 // ---------------------------------------------------------------------------
@@ -557,7 +592,7 @@ hipError_t launch_row_step_fill(int32_t* row_step, int64_t R, const int32_t* ste
 }
 
 hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, void* ws, float* emb, float* m,
-                                     float* v, int32_t* row_step, const int32_t* step, const ncf_hyper_t& h,
+                                     float* v, int32_t* row_step, int32_t* step, const ncf_hyper_t& h,
                                      hipStream_t st) {
     const uint32_t w4 = (uint32_t)(s.row_width / 4);
     const uint32_t n4 = (uint32_t)(s.num_rows * w4);
@@ -568,7 +603,8 @@ hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, vo
     if (h.optimizer == NCF_OPT_ADAM)
         launch(k_emb_adam_touched, row_grid(R < 2 * L.max_batch ? R : 2 * L.max_batch, w4), kBlock, 0, st,
                (float4*)emb, (float4*)m, (float4*)v, w4, at<const int32_t>(ws, L.touched),
-               at<const int32_t>(ws, L.nuniq), offs, list, gs, row_step, step, h.lr, h.beta_1, h.beta_2, h.epsilon);
+               at<const int32_t>(ws, L.nuniq), offs, list, gs, row_step, (const int32_t*)step, h.lr, h.beta_1, h.beta_2,
+               h.epsilon);
     else
         launch(k_emb_sgd_hot, kUpdateGrid, kBlock, 0, st, (float4*)emb, n4, w4, offs, list, gs, h.lr);
     return hipGetLastError();
@@ -614,19 +650,30 @@ hipError_t launch_emb_reg(const ncf_shape_t& s, const WsLayout& L, void* ws, con
 
 hipError_t launch_mlp_update(const ncf_shape_t& s, const WsLayout& L, void* ws, float* mlp, float* m, float* v,
                              const int32_t* step, const ncf_hyper_t& h, int nslab, const float* grad_in,
-                             float* grad_out, bool do_update, int* nreg, hipStream_t st, bool want_reg) {
+                             float* grad_out, bool do_update, int* nreg, hipStream_t st, bool want_reg,
+                             int summary_nbce, int summary_nmet, float n_groups, float* summary) {
     const int P = s.mlp_params;
     const int grid = (P + kBlock - 1) / kBlock;
     float* part = at<float>(ws, L.part_reg) + kUpdateGrid;
     const L2Table t = make_l2_table(s, h);
     const float* slabs = at<float>(ws, L.slabs);
+    bool summary_done = summary == nullptr || summary_nbce < 0;
     if (nslab > 2 * kSlabSplit) {
         const int per = (nslab + kSlabSplit - 1) / kSlabSplit;
         const int nch = (nslab + per - 1) / per;
         float* sp = at<float>(ws, L.slab_part);
-        launch(k_slab_partial, dim3(grid, nch), kBlock, 0, st, slabs, P, nslab, per, sp);
+        SummaryArgs sa{nullptr, nullptr, nullptr, nullptr, 0, 0, 0.f};
+        if (!summary_done)
+            sa = SummaryArgs{summary, at<float>(ws, L.part_bce), at<float>(ws, L.part_hit), at<float>(ws, L.part_dcg),
+                             summary_nbce, summary_nmet, n_groups};
+        launch(k_slab_partial, dim3(grid + (summary_done ? 0 : 1), nch), kBlock, 0, st, slabs, P, nslab, per, sp, sa);
+        summary_done = true;
         slabs = sp;
         nslab = nch;
+    }
+    if (!summary_done) {
+        hipError_t e = launch_summary(L, ws, summary_nbce, summary_nmet, n_groups, 0, 0, summary, st);
+        if (e != hipSuccess) return e;
     }
     if (h.optimizer == NCF_OPT_ADAM)
         launch(k_mlp_update<NCF_OPT_ADAM>, grid, kBlock, 0, st, mlp, m, v, P, slabs, nslab, grad_in,
