@@ -106,12 +106,16 @@ struct SideStream {
     hipEvent_t fork = nullptr, join = nullptr;
 };
 
-SideStream* side_stream() {
-    static const bool enabled = [] {
+int side_stream_mode() {
+    static const int mode = [] {
         const char* e = getenv("NCF_SIDE_STREAM");
-        return e && atoi(e) != 0;
+        return e ? atoi(e) : 0;
     }();
-    if (!enabled) return nullptr;
+    return mode;
+}
+
+SideStream* side_stream() {
+    if (side_stream_mode() == 0) return nullptr;
     static std::mutex mu;
     static std::map<int, SideStream> streams;
     int dev = 0;
@@ -381,7 +385,8 @@ static int run_fb(const ncf_shape_t& s, const ncf::WsLayout& L, const ncf_model_
         // forward/backward runs (the fused kernel leaves registers and a little LDS free on every
         // CU); the caller's next launch on `st` that needs it comes after index_join
         SideStream* ss = nullptr;
-        hipStream_t sti = fork_side(st, &ss);
+        // NCF_SIDE_STREAM=2: only the dense-layer tail leaves the main stream
+        hipStream_t sti = side_stream_mode() == 2 ? st : fork_side(st, &ss);
         prof_begin(NCF_K_INDEX, sti);
         e = ncf::launch_index_build(s, L, ws, users, items, n, sti, after_index != nullptr);
         prof_end(NCF_K_INDEX, sti);
