@@ -562,10 +562,19 @@ hipError_t launch_emb_update(const ncf_shape_t& s, const WsLayout& L, void* ws, 
     return hipGetLastError();
 }
 
-static unsigned row_grid(int64_t rows, uint32_t w4) {
+// Block caps of the row kernels (measured on MI355X, config C): the replay kernel runs best
+// with few, long-lived waves (2048 blocks: 17.7 us vs 21 us at 8192), the touched update with
+// one pass over the rows (8192).
+#ifndef NCF_CATCHUP_GRID_MAX
+#define NCF_CATCHUP_GRID_MAX 2048
+#endif
+#ifndef NCF_TOUCHED_GRID_MAX
+#define NCF_TOUCHED_GRID_MAX 8192
+#endif
+static unsigned row_grid(int64_t rows, uint32_t w4, int64_t cap) {
     const int64_t rpw = w4 <= 64 ? 64 / w4 : 1;
     int64_t g = (rows + rpw * 4 - 1) / (rpw * 4);  // 4 waves per block
-    return (unsigned)(g < 1 ? 1 : (g > 8192 ? 8192 : g));
+    return (unsigned)(g < 1 ? 1 : (g > cap ? cap : g));
 }
 
 hipError_t launch_emb_catchup(const ncf_shape_t& s, const WsLayout& L, void* ws, float* emb, float* m, float* v,
@@ -576,11 +585,11 @@ hipError_t launch_emb_catchup(const ncf_shape_t& s, const WsLayout& L, void* ws,
     const int64_t R = s.num_rows;
     const int64_t nmax = R < 2 * L.max_batch ? R : 2 * L.max_batch;
     if (all_rows)
-        launch(k_emb_catchup<true>, row_grid(R, w4), kBlock, 0, st, (float4*)emb, (float4*)m, (float4*)v, w4,
+        launch(k_emb_catchup<true>, row_grid(R, w4, 8192), kBlock, 0, st, (float4*)emb, (float4*)m, (float4*)v, w4,
                (const int32_t*)nullptr, (const int32_t*)nullptr, R, row_step, step, h.lr, h.beta_1, h.beta_2,
                h.epsilon);
     else
-        launch(k_emb_catchup<false>, row_grid(nmax, w4), kBlock, 0, st, (float4*)emb, (float4*)m, (float4*)v, w4,
+        launch(k_emb_catchup<false>, row_grid(nmax, w4, NCF_CATCHUP_GRID_MAX), kBlock, 0, st, (float4*)emb, (float4*)m, (float4*)v, w4,
                at<const int32_t>(ws, L.touched), at<const int32_t>(ws, L.nuniq), R, row_step, step, h.lr, h.beta_1,
                h.beta_2, h.epsilon);
     return hipGetLastError();
@@ -601,7 +610,7 @@ hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, vo
     const float4* gs = at<const float4>(ws, L.gs);
     const int64_t R = s.num_rows;
     if (h.optimizer == NCF_OPT_ADAM)
-        launch(k_emb_adam_touched, row_grid(R < 2 * L.max_batch ? R : 2 * L.max_batch, w4), kBlock, 0, st,
+        launch(k_emb_adam_touched, row_grid(R < 2 * L.max_batch ? R : 2 * L.max_batch, w4, NCF_TOUCHED_GRID_MAX), kBlock, 0, st,
                (float4*)emb, (float4*)m, (float4*)v, w4, at<const int32_t>(ws, L.touched),
                at<const int32_t>(ws, L.nuniq), offs, list, gs, row_step, (const int32_t*)step, h.lr, h.beta_1, h.beta_2,
                h.epsilon);
