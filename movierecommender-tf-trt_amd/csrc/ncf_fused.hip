@@ -463,7 +463,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
                     contrib[4 * q + 1] = dz * (a.y * b.y);
                     contrib[4 * q + 2] = dz * (a.z * b.z);
                     contrib[4 * q + 3] = dz * (a.w * b.w);
-                    if (ok) {
+                    if (inb) {  // masked samples (dz = 0) write zero rows: the index may count their other, valid id
                         const float4 gu4 = make_float4(dz * wo[f] * b.x, dz * wo[f + 1] * b.y, dz * wo[f + 2] * b.z,
                                                        dz * wo[f + 3] * b.w);
                         const float4 gi4 = make_float4(dz * wo[f] * a.x, dz * wo[f + 1] * a.y, dz * wo[f + 2] * a.z,
@@ -544,7 +544,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
                     return (oc < L0 && k < L1) ? wl[S::SW1 + oc * S::LW1 + k] : 0.f;
                 },
                 [&](int t) { return g1[t / 16][t % 16]; });
-            if (ok) {
+            if (inb) {  // masked samples (dz = 0) write zero rows: the index may count their other, valid id
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const int f = 32 * to + 8 * q + 4 * h;  // rows drow(4q..4q+3, h) are f..f+3

@@ -272,3 +272,66 @@ def test_lazy_decay_bitwise_equals_dense_sweep(dims, opt):
     assert torch.equal(dense.emb, lazy.emb)
     np.testing.assert_array_equal(dense.keras_weights()["item_embedding"], lazy.keras_weights()["item_embedding"])
     assert NCFEngine.read_stats(dense.stats) == NCFEngine.read_stats(lazy.stats)
+
+
+@pytest.mark.parametrize("dims", [SHAPES[3], SHAPES[1], SHAPES[5]], ids=["configC", "small", "configD"])
+@pytest.mark.parametrize("path", ["auto", "generic", "layered"])
+def test_out_of_range_ids_are_masked(dims, path):
+    """Device semantics for ids outside the table (the Python layer rejects them first, like
+    TF's gather; a device batch can still carry them): such a sample predicts NaN and
+    contributes no gradient, loss or metric; the rest of the batch is untouched — the
+    gradients equal the oracle's on the valid samples with the same 1/B normalisation."""
+    shape = O.NCFShape(*dims)
+    w = _weights(shape, 21)
+    users, items, y = _batch(shape, 128, 4, 22)
+    bad = np.zeros(128, bool)
+    bad[[3, 50, 77]] = True
+    users[3], items[50], users[77], items[77] = shape.num_users, -1, -5, shape.num_items + 9
+    eng = _engine(shape, w, force_generic=path == "generic", force_layered=path == "layered")
+    grads = eng.alloc_grads()
+    probs = torch.empty(128, dtype=torch.float32, device="cuda")
+    eng.forward_backward(users, items, y, group=4, k=2, inv_batch=1.0 / 128, grads=grads, probs_out=probs)
+    p = probs.cpu().numpy()
+    assert np.isnan(p[bad]).all() and np.isfinite(p[~bad]).all()
+    ok = ~bad
+    _, g, _ = O.loss_and_grads(shape, w, users[ok], items[ok], y[ok], [0.0] * len(shape.layers), batch_norm=128)
+    got = eng.keras_weights(grads[0], grads[1])
+    for name in O.weight_names(shape):
+        scale = np.max(np.abs(g[name])) + 1e-12
+        _close(got[name], g[name], 1e-5 * scale + 1e-9, name)
+    pref, _ = O.forward(shape, w, users[ok], items[ok])
+    _close(p[ok], pref, 2e-6, "probs")
+    bce = O.bce_per_sample(pref, y[ok]).sum()
+    assert grads[2][0].item() == pytest.approx(bce, rel=1e-5)
+
+
+def test_model_rejects_out_of_range_ids():
+    """MovierecModel raises ValueError before the device sees an id outside the table."""
+    from movierec.model import MovierecModel
+    params = dict(num_users=20, num_items=30, layers_sizes=[8, 4], layers_l2reg=[0, 0], optimizer="adam",
+                  lr=0.001, beta_1=0.9, beta_2=0.999, batch_size=8, num_negs_per_pos=3, batch_size_eval=8,
+                  num_negs_per_pos_eval=3, k=2)
+    m = MovierecModel(params, output_dir="/tmp/movierec_models", verbose=0)
+    with pytest.raises(ValueError):
+        m.model.predict_on_batch([np.array([0, 20], np.int32), np.array([1, 2], np.int32)])
+    with pytest.raises(ValueError):
+        m.model.predict_on_batch([np.array([0, 1], np.int32), np.array([1, 30], np.int32)])
+
+
+@pytest.mark.parametrize("group", [5, 100])
+def test_single_group_batch(group):
+    """Smallest batch: one user group (group does not divide 32 -> metrics outside the fused
+    kernel; 100 = the evaluation group)."""
+    shape = O.NCFShape(*SHAPES[3])
+    w = _weights(shape, 30)
+    users, items, y = _batch(shape, group, group, 31)
+    eng = _engine(shape, w)
+    ref = {k: v.copy() for k, v in w.items()}
+    st = O.new_opt_state(ref)
+    eng.train_step(users, items, y, group=group, k=2)
+    loss, _ = O.train_step(shape, ref, st, users, items, y, dict(optimizer="adam", lr=0.001, beta_1=0.9,
+                                                                  beta_2=0.999, layers_l2reg=[0.0] * 4))
+    got = eng.keras_weights()
+    for name in O.weight_names(shape):
+        _close(got[name], ref[name], 2e-6 + 2e-6 * np.max(np.abs(ref[name])), name)
+    assert NCFEngine.read_stats(eng.stats)["loss"] == pytest.approx(loss, rel=2e-5)
