@@ -74,6 +74,8 @@ def parse():
                          "ml-20m-shaped synthetic ratings set (20M positives)")
     ap.add_argument("--dense-sweep", action="store_true",
                     help="sweep every embedding row every step instead of the deferred exact decay (same result)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: rehearse N ranks sharing one GPU (correctness only, not a measurement)")
     ap.add_argument("--dp", default="auto", choices=["auto", "user", "sharded", "replicated"],
                     help="multi-GPU layout (auto: single engine at N=1, user-partitioned at N>1)")
     return ap.parse_args()
@@ -317,10 +319,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    torch.cuda.set_device(local if args.dist_backend == "nccl" else 0)
     mode = args.dp if args.dp != "auto" else ("single" if world == 1 else "user")
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "gloo":   # rehearsal of the multi-rank logic on one GPU (tests)
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     elif mode != "single":
         # one-rank process group: exercises the data-parallel path on one GPU
         import socket
