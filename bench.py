@@ -405,6 +405,9 @@ def main():
             u, it, y = pool[i % len(pool)]
         if dp is None:
             eng.train_step(u, it, y, group=g, k=k, inv_batch=inv)
+        elif mode == "user" and sampler is None:
+            nu, ni, _ = pool[(i + 1) % len(pool)]
+            dp.train_step(u, it, y, group=g, k=k, next_batch=(nu, ni))
         else:
             dp.train_step(u, it, y, group=g, k=k)
 

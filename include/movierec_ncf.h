@@ -118,7 +118,9 @@ typedef struct ncf_hyper {
                                            2: the layer-by-layer GEMM path (default for shapes the
                                            fused kernel does not hold whose dense weights exceed
                                            12288 floats, e.g. config D) */
-    int32_t reserved[6];
+    int32_t index_ready;                /* 1: the contribution index of this call's batch was built
+                                           beforehand by ncf_build_index (same ids, same ws): skip it */
+    int32_t reserved[5];
 } ncf_hyper_t;
 
 int ncf_abi_version(void);
@@ -222,6 +224,13 @@ int ncf_forward_backward_part(const ncf_shape_t* shape, const ncf_model_t* model
                               int32_t include_dense_reg, void* ws, size_t ws_bytes, void* stream);
 int ncf_update_rows(const ncf_shape_t* shape, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* hyper,
                     int64_t n, int64_t row_begin, int64_t row_count, void* ws, size_t ws_bytes, void* stream);
+/* Build the contribution index of the NEXT batch (users/items, n samples) into ws ahead of time,
+ * e.g. while the current step's all-reduce is in flight: the call replaces the index of the
+ * previous batch, so it must follow that batch's ncf_update_rows on the stream.  The next
+ * ncf_forward_backward_part / ncf_forward_backward with hyper->index_ready = 1 then skips its own
+ * index build (the caller guarantees it passes the same ids). */
+int ncf_build_index(const ncf_shape_t* shape, const int32_t* users, const int32_t* items, int64_t n, void* ws,
+                    size_t ws_bytes, void* stream);
 
 /* Row-sharded data parallelism (no reference counterpart — the
  * reference trains on one CPU).  Rank r of `world` (1..16) owns the table rows g

@@ -380,6 +380,9 @@ static int run_fb(const ncf_shape_t& s, const ncf::WsLayout& L, const ncf_model_
         users = ncf::at<int32_t>(ws, L.cid_u);
         items = ncf::at<int32_t>(ws, L.cid_i);
         ids = ncf::compact_ids(n);
+    } else if (h->index_ready && !after_index) {
+        // ncf_build_index already built this batch's index on `st` (the deferred-decay step needs
+        // the touched-row list too and always builds its own)
     } else {
         // the index depends only on the ids: it is built on the side stream while the
         // forward/backward runs (the fused kernel leaves registers and a little LDS free on every
@@ -548,6 +551,19 @@ int ncf_forward_backward_part(const ncf_shape_t* s, const ncf_model_t* model, co
     if (shared_row_begin < 0 || shared_row_begin > s->num_rows) return fail(NCF_EINVAL, "invalid shared row range");
     return forward_backward_rows(s, model, h, users, items, labels, n, shared_row_begin, shared_grad, mlp_grad, summary,
                                  probs_out, reg_row_begin, reg_row_count, include_dense_reg, ws, ws_bytes, stream);
+}
+
+int ncf_build_index(const ncf_shape_t* s, const int32_t* users, const int32_t* items, int64_t n, void* ws,
+                    size_t ws_bytes, void* stream) {
+    if (int r = check_shape(s)) return r;
+    if (!users || !items) return fail(NCF_EINVAL, "NULL device pointer");
+    ncf::WsLayout L;
+    if (int r = check_ws(*s, n, ws, ws_bytes, &L)) return r;
+    hipStream_t st = (hipStream_t)stream;
+    prof_begin(NCF_K_INDEX, st);
+    hipError_t e = ncf::launch_index_build(*s, L, ws, users, items, n, st, false);
+    prof_end(NCF_K_INDEX, st);
+    return hip_check(e, "index build");
 }
 
 int ncf_update_rows(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* h,

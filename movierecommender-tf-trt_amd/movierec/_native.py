@@ -53,7 +53,7 @@ class NcfOptim(ctypes.Structure):
 class NcfHyper(ctypes.Structure):
     _fields_ = [("optimizer", _i32), ("lr", _f32), ("beta_1", _f32), ("beta_2", _f32), ("epsilon", _f32),
                 ("l2", _f32 * NCF_MAX_LAYERS), ("group", _i32), ("k", _i32), ("inv_batch", _f32),
-                ("force_generic", _i32), ("reserved", _i32 * 6)]
+                ("force_generic", _i32), ("index_ready", _i32), ("reserved", _i32 * 5)]
 
 
 class NcfSamplerData(ctypes.Structure):
@@ -82,6 +82,7 @@ _SIGNATURES = {
                                                  _vp]),
     "ncf_update_rows": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _i64, _i64, _i64, _vp,
                                        ctypes.c_size_t, _vp]),
+    "ncf_build_index": (ctypes.c_int, [_P(NcfShape), _vp, _vp, _i64, _vp, ctypes.c_size_t, _vp]),
     "ncf_lazy_flush": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _vp, ctypes.c_size_t,
                                       _vp]),
     "ncf_apply_update": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _i64, _i64, _vp, _vp,

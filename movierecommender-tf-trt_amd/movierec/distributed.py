@@ -284,8 +284,10 @@ class UserPartitionedDataParallel(object):
         items.copy_(buf)
         _broadcast(self.eng.mlp, src, self.group)
 
-    def train_step(self, users, items, labels, group, k, global_batch=None):
-        """``users``: LOCAL user ids (u // world of users owned by this rank)."""
+    def train_step(self, users, items, labels, group, k, global_batch=None, next_batch=None):
+        """``users``: LOCAL user ids (u // world of users owned by this rank).  ``next_batch`` =
+        (users, items) device tensors of the following step: its index is built under this step's
+        all-reduce (pass the same tensors to the next call)."""
         n = len(users)
         gb = n * self.world if global_batch is None else int(global_batch)
         inv = 1.0 / gb
@@ -295,6 +297,8 @@ class UserPartitionedDataParallel(object):
                                   grads=self.grads, reg_rows=self.reg_rows, include_dense_reg=self.rank == 0)
         work = _all_reduce_async(self.shared, self.group)
         eng.update_rows(0, U, inv)               # own users: overlaps the all-reduce
+        if next_batch is not None and hasattr(eng, "build_index"):
+            eng.build_index(*next_batch)         # so does the next step's index
         if work is not None:
             work.wait()
         eng.apply_update(self.grads, inv, rows=(U, R - U), moments_by_row=True)

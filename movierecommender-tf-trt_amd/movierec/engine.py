@@ -75,6 +75,7 @@ class NCFEngine(object):
             self.val_stats = torch.zeros(N.NCF_NUM_STATS, dtype=torch.float64, device=dev)
             self.max_batch = 0
             self.ws = None
+            self._prebuilt = None   # (users ptr, items ptr, n) of an index built ahead by build_index
             self._ensure_ws(int(max_batch))
         self.model_s = N.NcfModel(self.emb.data_ptr(), self.mlp.data_ptr())
         self.hyper = N.NcfHyper()
@@ -147,6 +148,7 @@ class NCFEngine(object):
         nbytes = ctypes.c_size_t()
         N.check(L.ncf_workspace_size(ctypes.byref(self.shape), int(n), ctypes.byref(nbytes)))
         self.ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=self.device)
+        self._prebuilt = None
         self.ws_bytes = int(nbytes.value)
         N.check(L.ncf_workspace_init(ctypes.byref(self.shape), int(n), N.ptr(self.ws), self.ws_bytes,
                                      N.stream_handle(self.device)))
@@ -332,13 +334,37 @@ class NCFEngine(object):
         self._ensure_ws(n)
         h = self.hyper
         h.group, h.k, h.inv_batch = int(group), int(k), float(inv_batch)
+        # an index prebuilt by build_index is used only for the very tensors it was built from
+        pb = self._prebuilt
+        ready = pb is not None and pb[0].data_ptr() == u.data_ptr() and pb[1].data_ptr() == i.data_ptr() and \
+            pb[2] == n
+        h.index_ready = 1 if ready else 0
         eg, mg, sm = grads
         r0, rc = (0, self.num_rows) if reg_rows is None else reg_rows
-        N.check(N.lib().ncf_forward_backward_part(
-            ctypes.byref(self.shape), ctypes.byref(self.model_s), ctypes.byref(h), N.ptr(u), N.ptr(i), N.ptr(y), n,
-            int(shared_row_begin), N.ptr(eg), N.ptr(mg), N.ptr(sm), N.ptr(probs_out), int(r0), int(rc),
-            1 if include_dense_reg else 0, N.ptr(self.ws), self.ws_bytes, N.stream_handle(self.device)))
+        try:
+            N.check(N.lib().ncf_forward_backward_part(
+                ctypes.byref(self.shape), ctypes.byref(self.model_s), ctypes.byref(h), N.ptr(u), N.ptr(i), N.ptr(y),
+                n, int(shared_row_begin), N.ptr(eg), N.ptr(mg), N.ptr(sm), N.ptr(probs_out), int(r0), int(rc),
+                1 if include_dense_reg else 0, N.ptr(self.ws), self.ws_bytes, N.stream_handle(self.device)))
+        finally:
+            h.index_ready = 0
+            self._prebuilt = None
         self._part_n = n
+
+    def build_index(self, users, items):
+        """Build the contribution index of the NEXT ``forward_backward_part`` batch now (e.g. under
+        the current step's all-reduce); call after this step's ``update_rows``.  That call must
+        pass the same id tensors (checked by identity) or the index is rebuilt."""
+        self._prebuilt = None
+        if not (torch.is_tensor(users) and torch.is_tensor(items) and users.is_cuda and items.is_cuda):
+            return   # host ids get converted per call: nothing stable to key the index on
+        u, i = self._ids(users), self._ids(items)
+        n = u.numel()
+        if n > self.max_batch or u.data_ptr() != users.data_ptr() or i.data_ptr() != items.data_ptr():
+            return
+        N.check(N.lib().ncf_build_index(ctypes.byref(self.shape), N.ptr(u), N.ptr(i), n, N.ptr(self.ws),
+                                        self.ws_bytes, N.stream_handle(self.device)))
+        self._prebuilt = (u, i, n)   # holds the tensors: their memory cannot be reused meanwhile
 
     def update_rows(self, row_begin, row_count, inv_batch):
         """Optimizer step of rows [row_begin, row_begin + row_count) from the per-sample gradient

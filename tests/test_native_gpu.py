@@ -335,3 +335,31 @@ def test_single_group_batch(group):
     for name in O.weight_names(shape):
         _close(got[name], ref[name], 2e-6 + 2e-6 * np.max(np.abs(ref[name])), name)
     assert NCFEngine.read_stats(eng.stats)["loss"] == pytest.approx(loss, rel=2e-5)
+
+
+def test_prebuilt_index_equals_inline_build():
+    """User-partitioned step with the next batch's index built ahead (ncf_build_index under the
+    all-reduce, hyper.index_ready) is bitwise the step that builds its own index."""
+    shape = O.NCFShape(*SHAPES[3])
+    w = _weights(shape, 40)
+    U = shape.num_users
+    batches = []
+    for s in range(4):
+        users, items, y = _batch(shape, 256, 4, 41 + s)
+        batches.append((torch.from_numpy(users).cuda(), torch.from_numpy(items).cuda(), torch.from_numpy(y).cuda()))
+    engines = [_engine(shape, w), _engine(shape, w)]
+    outs = []
+    for e, ahead in zip(engines, (False, True)):
+        grads = (torch.zeros(shape.num_items, e.row_width, device="cuda"), torch.zeros(e.mlp_params, device="cuda"),
+                 torch.zeros(8, device="cuda"))
+        for s, (u, it, y) in enumerate(batches):
+            e.forward_backward_part(u, it, y, group=4, k=2, inv_batch=1.0 / 256, shared_row_begin=U, grads=grads)
+            e.update_rows(0, U, 1.0 / 256)
+            if ahead and s + 1 < len(batches):
+                e.build_index(batches[s + 1][0], batches[s + 1][1])
+                assert e._prebuilt is not None
+            e.apply_update(grads, 1.0 / 256, rows=(U, shape.num_items), moments_by_row=True)
+        torch.cuda.synchronize()
+        outs.append((e.emb.clone(), e.mlp.clone(), e.emb_m.clone()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
