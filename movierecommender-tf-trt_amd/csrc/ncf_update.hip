@@ -241,28 +241,44 @@ __global__ __launch_bounds__(kBlock) void k_emb_adam_touched(float4* __restrict_
         const float lr_t = adam_lr_t(lr, b1, b2, t);
         const int64_t n = *nlist;
         const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
-        const int64_t waves = ((int64_t)gridDim.x * kBlock) >> 6;
-        for (int64_t i = wave * rl.rpw + rl.sub; i < n; i += waves * rl.rpw) {
-            const int r = list[i];
+        const int64_t stride = (((int64_t)gridDim.x * kBlock) >> 6) * rl.rpw;
+        int64_t i = wave * rl.rpw + rl.sub;
+        // software pipeline over this lane group's rows: the next row's id is loaded while the
+        // current row is processed, so the list -> offsets -> contribution chain of row i+1
+        // overlaps row i's state and gradient traffic
+        int r = i < n ? list[i] : 0;
+        for (; i < n; i += stride) {
+            const int rn = i + stride < n ? list[i + stride] : 0;
             const int o = offs[r];
             const int c = offs[r + 1] - o;
             const int k = NCF_CATCHUP_P_ONLY ? t - 1 - row_step[r] : 0;  // m/v decay steps still owed
             for (uint32_t q = rl.q; q < w4; q += rl.qstep) {
                 const size_t e = (size_t)r * w4 + q;
-                // the row's state does not depend on the gradient chain: its loads go out first and
-                // overlap the list -> gradient-row loads
+                // the row's state does not depend on the gradient chain: its loads go out first
                 float4 p = emb[e], m = m4[e], v = v4[e];
                 // k_emb_catchup<false> brought p up to step t-1 and left m, v at row_step: the same
                 // per-step decay adam4 applies with g = 0 (b1*m + 0, b2*v + 0), bitwise
                 for (int j = 0; j < k; ++j) decay4(m, v, b1, b2);
+                // contributions summed in ascending order; four gradient rows in flight at a time
                 float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
-                for (int j = 0; j < c; ++j) g = f4add(g, gs[(size_t)clist[o + j] * w4 + q]);
+                int j = 0;
+                for (; j + 4 <= c; j += 4) {
+                    const int c0 = clist[o + j], c1 = clist[o + j + 1], c2 = clist[o + j + 2], c3 = clist[o + j + 3];
+                    const float4 g0 = gs[(size_t)c0 * w4 + q], g1 = gs[(size_t)c1 * w4 + q];
+                    const float4 g2 = gs[(size_t)c2 * w4 + q], g3 = gs[(size_t)c3 * w4 + q];
+                    g = f4add(g, g0);
+                    g = f4add(g, g1);
+                    g = f4add(g, g2);
+                    g = f4add(g, g3);
+                }
+                for (; j < c; ++j) g = f4add(g, gs[(size_t)clist[o + j] * w4 + q]);
                 adam4(p, m, v, g, lr_t, b1, b2, eps);
                 emb[e] = p;
                 m4[e] = m;
                 v4[e] = v;
             }
             if (rl.q == 0) row_step[r] = t;
+            r = rn;
         }
     }
 }
