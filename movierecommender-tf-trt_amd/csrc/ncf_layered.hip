@@ -7,13 +7,13 @@
 // MFMA-backed on gfx950, atomics off so every sum runs in a fixed order), with the gather,
 // bias+ReLU, output/BCE, ReLU-mask and gradient-row scatter as small HBM-bound kernels:
 //
-//   k_lay_gather   X0 = [E_u_mlp | E_i_mlp], GMF = E_u_gmf * E_i_gmf       (model.py:161-172)
+//   k_lay_gather(4)  X0 = [E_u_mlp | E_i_mlp], GMF = E_u_gmf * E_i_gmf     (model.py:161-172)
 //   sgemm + k_bias_relu   X_l = relu(X_{l-1} W_l + b_l)                     (model.py:175-181)
-//   k_lay_out      p = sigmoid([GMF, X_{n-1}] w_out + b_out); Keras BCE, dz; G_{n-1}
-//                                                                          (model.py:184-188, 213-214)
+//   k_lay_out2 + k_lay_gl   p = sigmoid([GMF, X_{n-1}] w_out + b_out); Keras BCE, dz;
+//                  G_{n-1} = dz w_mlp * relu'(X_{n-1})                     (model.py:184-188, 213-214)
 //   sgemm          dW_l = X_{l-1}^T G_l;  sgemv: db_l, output-layer grads (one slab)
 //   sgemm + k_relu_mask   G_{l-1} = (G_l W_l^T) * relu'(X_{l-1});  dX0 = G_1 W_1^T
-//   k_lay_scatter  per-sample gradient rows gs[2i] (user) / gs[2i+1] (item)
+//   k_lay_scatter(4)  per-sample gradient rows gs[2i] (user) / gs[2i+1] (item)
 //
 // The outputs are exactly those of the generic kernel (probs, gs, part_bce, one dense-gradient
 // slab), so the index build, the optimizer sweeps and the data-parallel paths are shared.
@@ -85,6 +85,67 @@ __global__ __launch_bounds__(kBlock) void k_lay_gather(const float* __restrict__
     }
 }
 
+// float4 variant (du, di, G multiples of 4 and G == G4): one thread per float4 of the
+// [X0 | GMF] row, the row id loaded once per float4 instead of once per float
+__global__ __launch_bounds__(kBlock) void k_lay_gather4(const float4* __restrict__ emb,
+                                                        const int32_t* __restrict__ users,
+                                                        const int32_t* __restrict__ items, int64_t n, IdSpace ids,
+                                                        int W4, int G4q, int du4, int di4, float4* __restrict__ x0,
+                                                        float4* __restrict__ gmf) {
+    const int C = du4 + di4 + G4q;
+    const int64_t total = n * C;
+    const float4 zero = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = e / C;
+        const int c = (int)(e - i * C);
+        const int u = users[i], v = items[i];
+        const bool ok = (unsigned)u < (unsigned)ids.ubound && (unsigned)v < (unsigned)ids.ibound;
+        const float4* eu = emb + (size_t)(ok ? u : 0) * W4;
+        const float4* ei = emb + (size_t)(ok ? ids.ibase + v : 0) * W4;
+        if (c < du4) {
+            x0[i * (du4 + di4) + c] = ok ? eu[G4q + c] : zero;
+        } else if (c < du4 + di4) {
+            x0[i * (du4 + di4) + c] = ok ? ei[G4q + c - du4] : zero;
+        } else {
+            const int f = c - du4 - di4;
+            const float4 a = eu[f], b = ei[f];
+            gmf[i * G4q + f] = ok ? make_float4(a.x * b.x, a.y * b.y, a.z * b.z, a.w * b.w) : zero;
+        }
+    }
+}
+
+// float4 variant of k_lay_scatter (same alignment conditions)
+__global__ __launch_bounds__(kBlock) void k_lay_scatter4(const float4* __restrict__ emb, const float* __restrict__ mlp,
+                                                         int wo_off, const int32_t* __restrict__ users,
+                                                         const int32_t* __restrict__ items, int64_t n, IdSpace ids,
+                                                         int W4, int G4q, int du4, int di4,
+                                                         const float* __restrict__ dzo,
+                                                         const float4* __restrict__ dx0, float4* __restrict__ gs) {
+    const int64_t total = n * 2 * W4;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t rowc = e / W4;  // contribution 2i (user) / 2i+1 (item)
+        const int q = (int)(e - rowc * W4);
+        const int64_t i = rowc >> 1;
+        const int side = (int)(rowc & 1);
+        float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (q < G4q) {
+            const int u = users[i], v = items[i];
+            const bool ok = (unsigned)u < (unsigned)ids.ubound && (unsigned)v < (unsigned)ids.ibound;
+            if (ok) {
+                const float4 o = emb[(size_t)(side ? u : ids.ibase + v) * W4 + q];  // the other side's GMF
+                const float d = dzo[i];
+                const float* w = mlp + wo_off + 4 * q;
+                g = make_float4(d * w[0] * o.x, d * w[1] * o.y, d * w[2] * o.z, d * w[3] * o.w);
+            }
+        } else {
+            const int k = q - G4q;
+            if (side == 0 && k < du4) g = dx0[i * (du4 + di4) + k];
+            else if (side == 1 && k < di4) g = dx0[i * (du4 + di4) + du4 + k];
+        }
+        gs[e] = g;
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void k_bias_relu(float* __restrict__ x, int64_t total, int lout,
                                                       const float* __restrict__ bias) {
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x)
@@ -97,26 +158,39 @@ __global__ __launch_bounds__(kBlock) void k_relu_mask(float* __restrict__ g, con
         g[e] = x[e] > 0.f ? g[e] : 0.f;
 }
 
-// One thread per sample: output layer, sigmoid, Keras BCE (clip -> logit -> sigmoid xent) and
-// dz = (p - y) / B where the clip is inactive; G_{n-1} = dz w_out[mlp] * relu'(X_{n-1}).
-__global__ __launch_bounds__(kBlock) void k_lay_out(const float* __restrict__ gmf, const float* __restrict__ xl,
-                                                    const float* __restrict__ mlp, int wo_off, int G, int Ll,
-                                                    const int32_t* __restrict__ users,
-                                                    const int32_t* __restrict__ items, IdSpace ids,
-                                                    const float* __restrict__ labels, int64_t n, float inv_batch,
-                                                    float* __restrict__ probs, float* __restrict__ dzo,
-                                                    float* __restrict__ gl, float* __restrict__ ones,
-                                                    float* __restrict__ part_bce) {
+// Output layer: one thread per sample, z = [GMF, X_{n-1}] w_out + b_out (float4 reads when both
+// widths are multiples of 4), sigmoid, Keras BCE, dz; G_{n-1} elementwise in k_lay_gl.
+template <bool VEC>
+__global__ __launch_bounds__(kBlock) void k_lay_out2(const float* __restrict__ gmf, const float* __restrict__ xl,
+                                                     const float* __restrict__ wo, int G, int Ll,
+                                                     const int32_t* __restrict__ users,
+                                                     const int32_t* __restrict__ items, IdSpace ids,
+                                                     const float* __restrict__ labels, int64_t n, float inv_batch,
+                                                     float* __restrict__ probs, float* __restrict__ dzo,
+                                                     float* __restrict__ ones, float* __restrict__ part_bce) {
     __shared__ float red[4];
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     float bce = 0.f;
     if (i < n) {
         const int u = users[i], v = items[i];
         const bool ok = (unsigned)u < (unsigned)ids.ubound && (unsigned)v < (unsigned)ids.ibound;
-        const float* wo = mlp + wo_off;
         float z = 0.f;
-        for (int f = 0; f < G; ++f) z += gmf[i * G + f] * wo[f];
-        for (int o = 0; o < Ll; ++o) z += xl[i * Ll + o] * wo[G + o];
+        if (VEC) {
+            const float4* g4 = reinterpret_cast<const float4*>(gmf + i * G);
+            const float4* x4 = reinterpret_cast<const float4*>(xl + i * Ll);
+            for (int f = 0; f < G / 4; ++f) {
+                const float4 a = g4[f];
+                z += a.x * wo[4 * f] + a.y * wo[4 * f + 1] + a.z * wo[4 * f + 2] + a.w * wo[4 * f + 3];
+            }
+            for (int o = 0; o < Ll / 4; ++o) {
+                const float4 a = x4[o];
+                const float* w = wo + G + 4 * o;
+                z += a.x * w[0] + a.y * w[1] + a.z * w[2] + a.w * w[3];
+            }
+        } else {
+            for (int f = 0; f < G; ++f) z += gmf[i * G + f] * wo[f];
+            for (int o = 0; o < Ll; ++o) z += xl[i * Ll + o] * wo[G + o];
+        }
         z += wo[G + Ll];
         const float p = 1.0f / (1.0f + expf(-z));
         float d = 0.f;
@@ -131,10 +205,19 @@ __global__ __launch_bounds__(kBlock) void k_lay_out(const float* __restrict__ gm
         probs[i] = ok ? p : __int_as_float(0x7fc00000);
         dzo[i] = d;
         ones[i] = 1.0f;
-        for (int o = 0; o < Ll; ++o) gl[i * Ll + o] = xl[i * Ll + o] > 0.f ? d * wo[G + o] : 0.f;
     }
     bce = block_sum_256(bce, red);
     if (threadIdx.x == 0) part_bce[blockIdx.x] = bce;
+}
+
+__global__ __launch_bounds__(kBlock) void k_lay_gl(const float* __restrict__ xl, const float* __restrict__ dzo,
+                                                   const float* __restrict__ wmlp, int Ll, int64_t total,
+                                                   float* __restrict__ gl) {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = e / Ll;
+        const int o = (int)(e - i * Ll);
+        gl[e] = xl[e] > 0.f ? dzo[i] * wmlp[o] : 0.f;
+    }
 }
 
 // gs[2i] = [dz w_gmf * E_i_gmf | dX0[:du] | 0-pad], gs[2i+1] = [dz w_gmf * E_u_gmf | dX0[du:] | 0-pad]
@@ -209,8 +292,14 @@ hipError_t launch_fb_layered(const ncf_shape_t& s, const WsLayout& L, void* ws, 
     float* gs = at<float>(ws, L.gs);
     const float one = 1.0f, zero = 0.0f;
 
-    launch(k_lay_gather, grid_for(n * (du + di + G)), kBlock, 0, st, emb, users, items, n, ids, W, G, G4, du, di, X[0],
-           gmf);
+    // float4 paths when every part of the row is float4-aligned (config D); float otherwise
+    const bool vec4 = du % 4 == 0 && di % 4 == 0 && G == G4 && W % 4 == 0;
+    if (vec4)
+        launch(k_lay_gather4, grid_for(n * (du + di + G) / 4), kBlock, 0, st, (const float4*)emb, users, items, n, ids,
+               W / 4, G / 4, du / 4, di / 4, (float4*)X[0], (float4*)gmf);
+    else
+        launch(k_lay_gather, grid_for(n * (du + di + G)), kBlock, 0, st, emb, users, items, n, ids, W, G, G4, du, di,
+               X[0], gmf);
     for (int l = 1; l < nl; ++l) {
         const int lin = s.layers[l - 1], lout = s.layers[l];
         const float* Wl = mlp + s.layer_off[l];
@@ -221,8 +310,14 @@ hipError_t launch_fb_layered(const ncf_shape_t& s, const WsLayout& L, void* ws, 
         launch(k_bias_relu, grid_for(n * lout), kBlock, 0, st, X[l], n * lout, lout, Wl + (int64_t)lin * lout);
     }
     const unsigned gb = (unsigned)((n + kBlock - 1) / kBlock);
-    launch(k_lay_out, gb, kBlock, 0, st, (const float*)gmf, (const float*)X[nl - 1], mlp, wo_off, G, Ll, users, items,
-           ids, labels, n, inv_batch, probs, dzo, Gd[nl - 1], ones, at<float>(ws, L.part_bce));
+    if (G % 4 == 0 && Ll % 4 == 0)
+        launch(k_lay_out2<true>, gb, kBlock, 0, st, (const float*)gmf, (const float*)X[nl - 1], mlp + wo_off, G, Ll,
+               users, items, ids, labels, n, inv_batch, probs, dzo, ones, at<float>(ws, L.part_bce));
+    else
+        launch(k_lay_out2<false>, gb, kBlock, 0, st, (const float*)gmf, (const float*)X[nl - 1], mlp + wo_off, G, Ll,
+               users, items, ids, labels, n, inv_batch, probs, dzo, ones, at<float>(ws, L.part_bce));
+    launch(k_lay_gl, grid_for(n * Ll), kBlock, 0, st, (const float*)X[nl - 1], (const float*)dzo, mlp + wo_off + G, Ll,
+           n * Ll, Gd[nl - 1]);
     *nbce = (int)gb;
     // Gradients that reduce over the batch (dW_l, db_l, output layer) are computed per chunk of
     // `chunk` samples into slab s (split-K by hand: a GEMM with K = batch and a 128 x 256
@@ -283,8 +378,12 @@ hipError_t launch_fb_layered(const ncf_shape_t& s, const WsLayout& L, void* ws, 
         if (e != hipSuccess) return e;
         if (l >= 2) launch(k_relu_mask, grid_for(n * lin), kBlock, 0, st, Gd[l - 1], (const float*)X[l - 1], n * lin);
     }
-    launch(k_lay_scatter, grid_for(n * 2 * W), kBlock, 0, st, emb, mlp, wo_off, users, items, n, ids, W, G, G4, du, di,
-           (const float*)dzo, (const float*)X[0], gs);
+    if (vec4)
+        launch(k_lay_scatter4, grid_for(n * 2 * W / 4), kBlock, 0, st, (const float4*)emb, mlp, wo_off, users, items, n,
+               ids, W / 4, G / 4, du / 4, di / 4, (const float*)dzo, (const float4*)X[0], (float4*)gs);
+    else
+        launch(k_lay_scatter, grid_for(n * 2 * W), kBlock, 0, st, emb, mlp, wo_off, users, items, n, ids, W, G, G4, du,
+               di, (const float*)dzo, (const float*)X[0], gs);
     *nslab = nfull + (rem > 0 ? 1 : 0);
     return hipGetLastError();
 }
