@@ -165,7 +165,8 @@ def cpu_sampler_baseline(cfg, budget_s):
     ml.NUM_USERS[name], ml.NUM_ITEMS[name] = cfg["num_users"], cfg["num_items"]
     try:
         np.random.seed(0)
-        gen = MovieLensDataGenerator(name, df, 4096, cfg["negs"])
+        bs = 4096 // (cfg["negs"] + 1) * (cfg["negs"] + 1)
+        gen = MovieLensDataGenerator(name, df, bs, cfg["negs"])
         gen[0]   # builds the per-user CSR (one-off)
         t0, b = time.perf_counter(), 1
         while time.perf_counter() - t0 < budget_s and b < len(gen):
@@ -174,7 +175,7 @@ def cpu_sampler_baseline(cfg, budget_s):
         dt = time.perf_counter() - t0
     finally:
         ml.NUM_USERS[name], ml.NUM_ITEMS[name] = saved
-    return (b - 1) * 4096 / dt, "%d batches of 4096 from 2M synthetic ratings, %.1f s" % (b - 1, dt)
+    return (b - 1) * bs / dt, "%d batches of %d from 2M synthetic ratings, %.1f s" % (b - 1, bs, dt)
 
 
 def score_flops(cfg):
