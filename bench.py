@@ -74,6 +74,9 @@ def parse():
                          "ml-20m-shaped synthetic ratings set (20M positives)")
     ap.add_argument("--dense-sweep", action="store_true",
                     help="sweep every embedding row every step instead of the deferred exact decay (same result)")
+    ap.add_argument("--emulate-world", type=int, default=1,
+                    help="--dp user at N=1 only: size the local table as rank 0 of this many ranks would "
+                         "(per-rank compute of the N-GPU step without its all-reduce; a diagnostic, not a result)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse N ranks sharing one GPU (correctness only, not a measurement)")
     ap.add_argument("--dp", default="auto", choices=["auto", "user", "sharded", "replicated"],
@@ -362,10 +365,11 @@ def main():
         dp = RowShardedDataParallel(eng)
     elif mode == "user":
         from movierec.distributed import UserPartitionedDataParallel, partition_keras_weights
-        n_loc = (cfg["num_users"] - rank + world - 1) // world
+        ew = max(world, args.emulate_world)
+        n_loc = (cfg["num_users"] - rank + ew - 1) // ew
         eng = NCFEngine(n_loc, cfg["num_items"], cfg["layers"], cfg["gmf_dim"], max_batch=B,
                         force_generic=args.generic)
-        eng.set_keras_weights(partition_keras_weights(w0, world, rank))
+        eng.set_keras_weights(partition_keras_weights(w0, ew, rank))
         dp = UserPartitionedDataParallel(eng)
         dp.broadcast_parameters()
     else:

@@ -13,8 +13,9 @@
 //   k_fill        offs[row] = local + prefix(block totals);
 //                 list[offs[row] + --cnt[row]] = c        (cnt back to 0)
 //   k_sort        sort each row's list: <=16 entries in registers (one
-//                 thread), longer rows by the whole workgroup through an
-//                 LDS bitmap over c (popcount scan, ascending write-back).
+//                 thread), 17..64 by one wave (bitonic network across lanes),
+//                 longer rows by the whole workgroup through an LDS bitmap
+//                 over c (popcount scan, ascending write-back).
 //
 // All HBM traffic here is O(B + R) int32 (R = table rows); see DESIGN.md.
 
@@ -212,16 +213,19 @@ __global__ __launch_bounds__(kBlock) void k_sort(const int32_t* __restrict__ off
                                                  int32_t* __restrict__ list, int nwords) {
     extern __shared__ __attribute__((aligned(16))) unsigned bm[];
     __shared__ int hrows[kBlock];
-    __shared__ int nh;
+    __shared__ int mrows[kBlock];
+    __shared__ int nh, nm;
     __shared__ int sw[4];
-    if (threadIdx.x == 0) nh = 0;
+    if (threadIdx.x == 0) nh = nm = 0;
     __syncthreads();
     const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (r < R) {
         const int o = offs[r];
         const int c = offs[r + 1] - o;
-        if (c > kSmallSeg) {
+        if (c > 64) {
             hrows[atomicAdd(&nh, 1)] = (int)r;
+        } else if (c > kSmallSeg) {
+            mrows[atomicAdd(&nm, 1)] = (int)r;
         } else if (c >= 2) {
             int v[kSmallSeg];
 #pragma unroll
@@ -242,6 +246,28 @@ __global__ __launch_bounds__(kBlock) void k_sort(const int32_t* __restrict__ off
         }
     }
     __syncthreads();
+    // rows of 17..64 entries (frequent when a rank's users are few — user-partitioned DP): one
+    // wave each, a bitonic network across the 64 lanes (one entry per lane, INT_MAX padding)
+    {
+        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+        for (int hh = wv; hh < nm; hh += kBlock / 64) {
+            const int row = mrows[hh];
+            const int o = offs[row];
+            const int c = offs[row + 1] - o;
+            int x = lane < c ? list[o + lane] : INT_MAX;
+#pragma unroll
+            for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+                for (int j = k >> 1; j > 0; j >>= 1) {
+                    const int y = __shfl_xor(x, j, 64);
+                    const bool asc = (lane & k) == 0;
+                    const bool lower = (lane & j) == 0;
+                    x = (lower == asc) ? min(x, y) : max(x, y);
+                }
+            }
+            if (lane < c) list[o + lane] = x;
+        }
+    }
     const int count = nh;
     const int per = (nwords + kBlock - 1) / kBlock;
     for (int hh = 0; hh < count; ++hh) {

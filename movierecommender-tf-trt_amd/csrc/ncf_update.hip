@@ -120,7 +120,16 @@ __global__ __launch_bounds__(kBlock) void k_emb_update(float4* __restrict__ emb,
             const int o = offs[r];
             const int c = offs[r + 1] - o;
             g = make_float4(0.f, 0.f, 0.f, 0.f);
-            for (int j = 0; j < c; ++j) g = f4add(g, gs[(size_t)list[o + j] * w4 + q]);
+            int j = 0;
+            for (; j + 4 <= c; j += 4) {  // four rows in flight, summed in ascending order
+                const float4 g0 = gs[(size_t)list[o + j] * w4 + q], g1 = gs[(size_t)list[o + j + 1] * w4 + q];
+                const float4 g2 = gs[(size_t)list[o + j + 2] * w4 + q], g3 = gs[(size_t)list[o + j + 3] * w4 + q];
+                g = f4add(g, g0);
+                g = f4add(g, g1);
+                g = f4add(g, g2);
+                g = f4add(g, g3);
+            }
+            for (; j < c; ++j) g = f4add(g, gs[(size_t)list[o + j] * w4 + q]);
         } else {
             g = dgrad[e];
         }
@@ -326,7 +335,16 @@ __global__ __launch_bounds__(kBlock) void k_emb_grad_dense(float4* __restrict__ 
         const int o = offs[r];
         const int c = offs[r + 1] - o;
         float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int j = 0; j < c; ++j) g = f4add(g, gs[(size_t)list[o + j] * w4 + q]);
+        int j = 0;
+        for (; j + 4 <= c; j += 4) {  // four rows in flight, summed in ascending order
+            const float4 g0 = gs[(size_t)list[o + j] * w4 + q], g1 = gs[(size_t)list[o + j + 1] * w4 + q];
+            const float4 g2 = gs[(size_t)list[o + j + 2] * w4 + q], g3 = gs[(size_t)list[o + j + 3] * w4 + q];
+            g = f4add(g, g0);
+            g = f4add(g, g1);
+            g = f4add(g, g2);
+            g = f4add(g, g3);
+        }
+        for (; j < c; ++j) g = f4add(g, gs[(size_t)list[o + j] * w4 + q]);
         out[e] = g;
     }
 }
