@@ -235,8 +235,22 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc_h3_l[r] = 0.f;
 
-    // dense parameters → LDS (once per persistent workgroup)
-    for (int e = tid; e < L0 * L1; e += kBlock) wl[S::SW1 + (e / L1) * S::LW1 + e % L1] = mlp[S::OW1 + e];
+    // dense parameters → LDS (once per persistent workgroup).  W1 is most of them: all of this
+    // thread's loads are issued before the first LDS store, so the L2 latency is paid once
+    {
+        constexpr int NW1 = (L0 * L1 + kBlock - 1) / kBlock;
+        float w1r[NW1];
+#pragma unroll
+        for (int q = 0; q < NW1; ++q) {
+            const int e = tid + q * kBlock;
+            w1r[q] = e < L0 * L1 ? mlp[S::OW1 + e] : 0.f;
+        }
+#pragma unroll
+        for (int q = 0; q < NW1; ++q) {
+            const int e = tid + q * kBlock;
+            if (e < L0 * L1) wl[S::SW1 + (e / L1) * S::LW1 + e % L1] = w1r[q];
+        }
+    }
     for (int e = tid; e < L1 * L2; e += kBlock) wl[S::SW2 + (e / L2) * S::LW2 + e % L2] = mlp[S::OW2 + e];
     for (int e = tid; e < L2 * L3; e += kBlock) wl[S::SW3 + (e / L3) * S::LW3 + e % L3] = mlp[S::OW3 + e];
     for (int e = tid; e < L1; e += kBlock) wl[S::SB1 + e] = mlp[S::OB1 + e];
