@@ -50,3 +50,21 @@ __device__ inline float4 f4add(float4 a, float4 b) {
 }
 
 }  // namespace ncf
+
+#ifndef NCF_NT_STORES
+#define NCF_NT_STORES 0
+#endif
+namespace ncf {
+// Store of a streamed result nothing re-reads soon.  NCF_NT_STORES=1 makes it non-temporal:
+// measured on MI355X it slows the fused kernel's gradient-row stores 80 -> 130 us per launch
+// (config C) and the touched update 34 -> 37 us, so it is off.
+__device__ __forceinline__ void st_stream(float4* p, const float4& v) {
+#if NCF_NT_STORES
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<f4v*>(p));
+#else
+    *p = v;
+#endif
+}
+}  // namespace ncf

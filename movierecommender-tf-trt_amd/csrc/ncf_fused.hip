@@ -482,8 +482,8 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
                                                        dz * wo[f + 3] * b.w);
                         const float4 gi4 = make_float4(dz * wo[f] * a.x, dz * wo[f + 1] * a.y, dz * wo[f + 2] * a.z,
                                                        dz * wo[f + 3] * a.w);
-                        *reinterpret_cast<float4*>(gu + h * S::GH + f) = gu4;
-                        *reinterpret_cast<float4*>(gi + h * S::GH + f) = gi4;
+                        st_stream(reinterpret_cast<float4*>(gu + h * S::GH + f), gu4);
+                        st_stream(reinterpret_cast<float4*>(gi + h * S::GH + f), gi4);
                     }
                 }
 #pragma unroll
@@ -564,8 +564,8 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
                     const int f = 32 * to + 8 * q + 4 * h;  // rows drow(4q..4q+3, h) are f..f+3
                     if (f < L0) {
                         float* dst = (f < D0) ? gu + G + f : gi + G + (f - D0);
-                        *reinterpret_cast<float4*>(dst) =
-                            make_float4(acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]);
+                        st_stream(reinterpret_cast<float4*>(dst),
+                                  make_float4(acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]));
                     }
                 }
             }

@@ -214,7 +214,7 @@ __global__ __launch_bounds__(kBlock) void k_emb_catchup(float4* __restrict__ emb
             float4 p = emb[e], m = m4[e], v = v4[e];
             for (int j = s + 1; j <= t; ++j)
                 adam4(p, m, v, zero, t - j < kLrLut ? lut[t - j] : adam_lr_t(lr, b1, b2, j), b1, b2, eps);
-            emb[e] = p;
+            st_stream(&emb[e], p);
             if (ALL || !NCF_CATCHUP_P_ONLY) {  // the flush leaves the dense state; with P_ONLY the
                         // per-step replay writes only p (the forward pass reads p) and
                         // k_emb_adam_touched re-derives m and v from row_step
@@ -282,9 +282,9 @@ __global__ __launch_bounds__(kBlock) void k_emb_adam_touched(float4* __restrict_
                 }
                 for (; j < c; ++j) g = f4add(g, gs[(size_t)clist[o + j] * w4 + q]);
                 adam4(p, m, v, g, lr_t, b1, b2, eps);
-                emb[e] = p;
-                m4[e] = m;
-                v4[e] = v;
+                st_stream(&emb[e], p);
+                st_stream(&m4[e], m);
+                st_stream(&v4[e], v);
             }
             if (rl.q == 0) row_step[r] = t;
             r = rn;
