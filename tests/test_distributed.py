@@ -39,14 +39,22 @@ def _free_port():
     return port
 
 
-def _weights():
-    shape = O.NCFShape(*SHAPE)
+SHAPE_D = (40, 30, [256, 128, 64, 32], 128)   # config D's model (layered path), small tables
+
+
+def _weights(dims=SHAPE):
+    shape = O.NCFShape(*dims)
     w = O.init_weights(shape, seed=4)
-    return shape, {k: (v * 3).astype(np.float32).astype(np.float64) for k, v in w.items()}
+    scale = 3 if dims == SHAPE else 1
+    return shape, {k: (v * scale).astype(np.float32).astype(np.float64) for k, v in w.items()}
 
 
-def _batches():
-    shape = O.NCFShape(*SHAPE)
+def _l2(dims):
+    return L2 if dims == SHAPE else [0.0] * len(dims[2])
+
+
+def _batches(dims=SHAPE):
+    shape = O.NCFShape(*dims)
     rng = np.random.RandomState(7)
     out = []
     for _ in range(STEPS):
@@ -303,7 +311,7 @@ def test_replicated_dp_matches_single_process_gpu():
     assert gpu_available()
 
 
-def _gpu_sharded_worker(rank, world, port, q):
+def _gpu_sharded_worker(rank, world, port, q, dims=SHAPE):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path[:0] = [here, os.path.dirname(here), os.path.join(os.path.dirname(here), "movierecommender-tf-trt_amd")]
@@ -312,14 +320,14 @@ def _gpu_sharded_worker(rank, world, port, q):
     from movierec.engine import NCFEngine
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
-    shape, w = _weights()
+    shape, w = _weights(dims)
     eng = ShardedNCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, world=world, rank=rank,
-                           max_batch=B, layers_l2reg=L2)
+                           max_batch=B, layers_l2reg=_l2(dims))
     eng.set_keras_weights(w)
     dp = RowShardedDataParallel(eng)
     per = B // world
     probs = []
-    for users, items, y in _batches():
+    for users, items, y in _batches(dims):
         sl = slice(rank * per, (rank + 1) * per)
         dp.train_step(users[sl], items[sl], y[sl], group=GROUP, k=2, global_batch=B)
         probs.append(dp.predict(users[sl], items[sl]).cpu().numpy())
@@ -329,13 +337,14 @@ def _gpu_sharded_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def _gpu_reference():
+def _gpu_reference(dims=SHAPE):
     from movierec.engine import NCFEngine
-    shape, w = _weights()
-    ref = NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=B, layers_l2reg=L2)
+    shape, w = _weights(dims)
+    ref = NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=B,
+                    layers_l2reg=_l2(dims))
     ref.set_keras_weights(w)
     probs = []
-    for users, items, y in _batches():
+    for users, items, y in _batches(dims):
         ref.train_step(users, items, y, group=GROUP, k=2)
         probs.append(ref.predict(users, items).cpu().numpy())
     return ref.keras_weights(), NCFEngine.read_stats(ref.stats), probs
@@ -431,4 +440,34 @@ def test_user_partitioned_dp_matches_single_process_gpu(world):
             np.testing.assert_allclose(wts[name], rw[name], rtol=0, atol=1e-5, err_msg=name)
         assert st["loss"] == pytest.approx(rst["loss"], rel=1e-5)
         assert st["hr"] == pytest.approx(rst["hr"], abs=1e-6)
+    assert gpu_available()
+
+
+@pytest.mark.gpu
+def test_row_sharded_dp_config_d_model_gpu():
+    """Config D's model (MLP [256,128,64,32] + GMF 128: the layered GEMM path on compact row
+    ids) through the row-sharded exchanges at world 2 vs one process on the global batch."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_sharded_worker, args=(r, world, port, q, SHAPE_D)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, wts, st, pr = q.get(timeout=300)
+        res[r] = (wts, st, pr)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    rw, rst, rprobs = _gpu_reference(SHAPE_D)
+    per = B // world
+    for r in range(world):
+        wts, st, pr = res[r]
+        for name in rw:
+            np.testing.assert_allclose(wts[name], rw[name], rtol=0, atol=1e-5, err_msg=name)
+        assert st["loss"] == pytest.approx(rst["loss"], rel=1e-5)
+        for a, b in zip(pr, rprobs):
+            np.testing.assert_allclose(a, b[r * per:(r + 1) * per], rtol=0, atol=2e-6)
     assert gpu_available()
