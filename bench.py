@@ -247,7 +247,7 @@ def score_main(args, cfg, world, rank):
     achieved = fl * my_pairs / (kern_ms * 1e-3) / 1e12
     if rank == 0:
         cpu = None if (world > 1 or args.no_cpu_baseline) else cpu_score_baseline(cfg, args.cpu_seconds)
-        print(json.dumps({
+        emit(json.dumps({
             "metric": "all-item scoring + top-10 (user, item) pairs/s, ml-20m NeuMF (config E)", "value": round(value, 1),
             "unit": "pairs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "strong",
@@ -258,7 +258,7 @@ def score_main(args, cfg, world, rank):
                          "peak": FP16_MFMA_PEAK_TFS, "unit": "TFLOP/s", "frac": round(achieved / FP16_MFMA_PEAK_TFS, 4),
                          "traffic": None, "algorithmic_flops_per_pair": fl, "naive_flops_per_pair": fl_naive,
                          "avg_launch_ms": round(kern_ms, 4)},
-            "cpu_baseline": cpu}), flush=True)
+            "cpu_baseline": cpu}))
     if dist.is_initialized():
         dist.destroy_process_group()
 
@@ -318,7 +318,26 @@ def pmc_traffic(name, kernel=None):
     return d.get("bytes_per_launch")
 
 
+_RESULT_OUT = None
+
+
+def _keep_stdout_for_result():
+    """stdout carries exactly one line, the result: everything else written to file descriptor 1
+    (RCCL's version banner on every rank, gloo's connection chatter) goes to stderr."""
+    global _RESULT_OUT
+    if _RESULT_OUT is None:
+        sys.stdout.flush()
+        _RESULT_OUT = os.fdopen(os.dup(1), "w")
+        os.dup2(2, 1)
+
+
+def emit(text):
+    _RESULT_OUT.write(text + "\n")
+    _RESULT_OUT.flush()
+
+
 def main():
+    _keep_stdout_for_result()
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -553,7 +572,7 @@ def main():
             line["exchange"] = {"unique_rows_per_rank": train_exchange[0],
                                 "rows_served_per_rank": train_exchange[1],
                                 "shard_rows": eng.shard_rows}
-        print(json.dumps(line), flush=True)
+        emit(json.dumps(line))
     if dist.is_initialized():
         dist.destroy_process_group()
 
