@@ -354,7 +354,9 @@ class NCFEngine(object):
     def build_index(self, users, items):
         """Build the contribution index of the NEXT ``forward_backward_part`` batch now (e.g. under
         the current step's all-reduce); call after this step's ``update_rows``.  That call must
-        pass the same id tensors (checked by identity) or the index is rebuilt."""
+        pass the same id tensors (checked by identity, else the index is rebuilt), and their
+        contents must not change in between (a sampler that refills one buffer in place must not
+        use this)."""
         self._prebuilt = None
         if not (torch.is_tensor(users) and torch.is_tensor(items) and users.is_cuda and items.is_cuda):
             return   # host ids get converted per call: nothing stable to key the index on
