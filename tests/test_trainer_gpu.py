@@ -1,0 +1,65 @@
+"""End to end through the reference's entry point (trainer.py:30-80): a MovieLens ratings
+file on disk -> leave-two-out split -> host generators (reference RNG stream) ->
+MovierecModel.fit_generator (validation, EarlyStopping / best checkpoints) -> save ->
+MovierecModel.load_from_dir, on the HIP path.
+
+The data is an ml-100k-format file (u.data, tab separated, 1-based ids) written here with
+ml-100k's table sizes (943 users x 1682 items) and a learnable structure; no download.
+"""
+
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from conftest import gpu_available
+
+pytestmark = pytest.mark.gpu
+
+
+def _write_ml100k(data_dir, seed=0):
+    rng = np.random.RandomState(seed)
+    U, I = 943, 1682
+    fu, fi = rng.normal(size=(U, 4)), rng.normal(size=(I, 4))
+    rows = []
+    ts = 0
+    for u in range(U):
+        pref = np.argsort(-(fi @ fu[u] + 0.3 * rng.normal(size=I)))[:8]   # each user's 8 favourites
+        for it in pref:
+            ts += 1
+            rows.append("%d\t%d\t%d\t%d" % (u + 1, it + 1, rng.randint(1, 6), ts))
+    os.makedirs(os.path.join(data_dir, "ml-100k"), exist_ok=True)
+    with open(os.path.join(data_dir, "ml-100k", "u.data"), "w") as f:
+        f.write("\n".join(rows) + "\n")
+
+
+def test_trainer_end_to_end(tmp_path):
+    import random
+    from movierec import trainer
+    from movierec.model import MovierecModel
+    data_dir, out_dir = str(tmp_path / "data"), str(tmp_path / "models")
+    _write_ml100k(data_dir)
+    np.random.seed(0)
+    random.seed(0)
+    params = dict(trainer.DEFAULT_PARAMS)
+    params.update(layers_sizes=[16, 8], layers_l2reg=[0, 0], batch_size=240, num_negs_per_pos=3,
+                  batch_size_eval=200, num_negs_per_pos_eval=99, k=4, epochs=3, gmf_dim=8, seed=1)
+    model, history = trainer.train("e2e", "ml-100k", data_dir, out_dir, params, verbose=0)
+
+    h = history.history
+    for key in ("loss", "output_hr", "output_dcg", "val_loss", "val_output_hr", "val_output_dcg"):
+        assert len(h[key]) >= 1 and all(np.isfinite(h[key])), key
+    assert h["loss"][-1] < h["loss"][0]                       # training lowers the loss
+    assert os.path.exists(MovierecModel.get_model_weights_path(out_dir, "e2e"))
+    assert os.path.exists(MovierecModel.get_params_json_path(out_dir, "e2e"))
+    assert glob.glob(os.path.join(out_dir, "e2e-checkpoint-*"))  # best-only checkpoints
+
+    # the saved model reloads to the same predictions
+    users = np.arange(20, dtype=np.int32).repeat(5)
+    items = np.tile(np.arange(5, dtype=np.int32), 20)
+    p0, _ = model.model.predict_on_batch([users, items])
+    loaded = MovierecModel.load_from_dir(out_dir, "e2e", verbose=0)
+    p1, _ = loaded.model.predict_on_batch([users, items])
+    np.testing.assert_array_equal(p0, p1)
+    assert gpu_available()
