@@ -427,7 +427,10 @@ def main():
             (u, it), y = sampler[i % len(sampler)]
         else:
             u, it, y = pool[i % len(pool)]
-        if dp is None:
+        if dp is None and sampler is None:
+            nu, ni, _ = pool[(i + 1) % len(pool)]   # the next step's ids: counted inside this step
+            eng.train_step(u, it, y, group=g, k=k, inv_batch=inv, next_batch=(nu, ni))
+        elif dp is None:
             eng.train_step(u, it, y, group=g, k=k, inv_batch=inv)
         elif mode == "user" and sampler is None:
             nu, ni, _ = pool[(i + 1) % len(pool)]
@@ -477,6 +480,8 @@ def main():
     elif getattr(eng, "lazy", False):
         touched = float(np.mean([torch.unique(u).numel() + torch.unique(it).numel() for u, it, _ in pool]))
         nbytes = emb_update_bytes(eng.shape, B, touched_rows=touched)
+        if sampler is None:
+            nbytes += 2 * B * (4 + 8)   # the launch also counts the next batch: id reads + counter atomics
     else:
         nbytes = emb_update_bytes(eng.shape, B, dense_rows=(dp.row_count if mode == "replicated" else
                                                             eng.num_rows if mode == "user" else None))
@@ -535,7 +540,9 @@ def main():
                        "negatives_per_positive": cfg["negs"], "parallelism": par,
                        "kernel_path": getattr(eng, "kernel_path", "fused-mfma" if eng.fast_path else "generic")},
             "roofline": {"bound": "hbm", "kernel": ("embedding scatter-add + Adam on the batch's touched rows "
-                                                    "(k_emb_adam_touched; deferred exact decay)"
+                                                    "(k_emb_adam_touched; deferred exact decay"
+                                                    + ("; its launch also counts the next batch's index "
+                                                       "contributions)" if sampler is None else ")")
                                                     if getattr(eng, "lazy", False) else
                                                     "embedding scatter-add + Adam sweep (k_emb_update)"),
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

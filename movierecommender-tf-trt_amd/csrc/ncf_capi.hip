@@ -380,7 +380,7 @@ static int run_fb(const ncf_shape_t& s, const ncf::WsLayout& L, const ncf_model_
         users = ncf::at<int32_t>(ws, L.cid_u);
         items = ncf::at<int32_t>(ws, L.cid_i);
         ids = ncf::compact_ids(n);
-    } else if (h->index_ready && !after_index) {
+    } else if (h->index_ready == 1 && !after_index) {
         // ncf_build_index already built this batch's index on `st` (the deferred-decay step needs
         // the touched-row list too and always builds its own)
     } else {
@@ -391,7 +391,7 @@ static int run_fb(const ncf_shape_t& s, const ncf::WsLayout& L, const ncf_model_
         // NCF_SIDE_STREAM=2: only the dense-layer tail leaves the main stream
         hipStream_t sti = side_stream_mode() == 2 ? st : fork_side(st, &ss);
         prof_begin(NCF_K_INDEX, sti);
-        e = ncf::launch_index_build(s, L, ws, users, items, n, sti, after_index != nullptr);
+        e = ncf::launch_index_build(s, L, ws, users, items, n, sti, after_index != nullptr, h->index_ready == 2);
         prof_end(NCF_K_INDEX, sti);
         if (e != hipSuccess) return hip_check(e, "index build");
         out->index_side = ss;
@@ -441,9 +441,10 @@ static int check_train_args(const ncf_shape_t* s, const ncf_model_t* model, cons
     return 0;
 }
 
-int ncf_train_step(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* h,
-                   const int32_t* users, const int32_t* items, const float* labels, int64_t n, double* stats,
-                   float* probs_out, void* ws, size_t ws_bytes, void* stream) {
+static int train_step_impl(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* h,
+                           const int32_t* users, const int32_t* items, const float* labels, int64_t n,
+                           const int32_t* next_users, const int32_t* next_items, int64_t n_next, double* stats,
+                           float* probs_out, void* ws, size_t ws_bytes, void* stream) {
     if (int r = check_train_args(s, model, h, users, items, labels, n)) return r;
     if (!optim || !optim->step || (h->optimizer == NCF_OPT_ADAM &&
                                    (!optim->emb_m || !optim->emb_v || !optim->mlp_m || !optim->mlp_v)))
@@ -486,7 +487,7 @@ int ncf_train_step(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* optim,
     prof_begin(NCF_K_EMB_UPDATE, st);
     if (lazy)
         e = ncf::launch_emb_update_touched(*s, L, ws, model->emb, optim->emb_m, optim->emb_v, optim->row_step,
-                                           optim->step, *h, st);
+                                           optim->step, *h, st, next_users, next_items, n_next);
     else
         e = ncf::launch_emb_update(*s, L, ws, model->emb, optim->emb_m, optim->emb_v, optim->step, *h, nullptr,
                                    s->num_rows, st);
@@ -497,6 +498,26 @@ int ncf_train_step(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* optim,
     const int nreg_emb = h->l2[0] != 0.0f ? ncf::kUpdateGrid : 0;
     e = ncf::launch_stats(L, ws, summary, nreg_emb, nreg_mlp, h->inv_batch, stats, optim->step, true, st);
     return hip_check(e, "stats");
+}
+
+int ncf_train_step(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* h,
+                   const int32_t* users, const int32_t* items, const float* labels, int64_t n, double* stats,
+                   float* probs_out, void* ws, size_t ws_bytes, void* stream) {
+    return train_step_impl(s, model, optim, h, users, items, labels, n, nullptr, nullptr, 0, stats, probs_out, ws,
+                           ws_bytes, stream);
+}
+
+int ncf_train_step_ahead(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* h,
+                         const int32_t* users, const int32_t* items, const float* labels, int64_t n,
+                         const int32_t* next_users, const int32_t* next_items, int64_t n_next, double* stats,
+                         float* probs_out, void* ws, size_t ws_bytes, void* stream) {
+    if (!s || !optim || !h) return fail(NCF_EINVAL, "NULL argument");
+    if (!next_users || !next_items || n_next <= 0 || n_next > n)
+        return fail(NCF_EINVAL, "next batch: NULL ids or n_next outside [1, n]");
+    if (!optim->row_step || h->optimizer != NCF_OPT_ADAM)
+        return fail(NCF_EINVAL, "counting ahead needs deferred-decay Adam (optim->row_step)");
+    return train_step_impl(s, model, optim, h, users, items, labels, n, next_users, next_items, n_next, stats,
+                           probs_out, ws, ws_bytes, stream);
 }
 
 static int forward_backward_rows(const ncf_shape_t* s, const ncf_model_t* model, const ncf_hyper_t* h,

@@ -320,7 +320,7 @@ static hipError_t set_sort_lds(int nwords) {
 // count -> scan -> fill -> sort over K keys for m contributions.
 template <int MODE, bool UNIQ, bool LIST = false>
 static hipError_t build(const WsLayout& L, void* ws, const KeySrc& ks, int64_t m, int64_t K, PlanOut po,
-                        int nwords, hipStream_t st) {
+                        int nwords, hipStream_t st, bool counted = false) {
     const int64_t r1 = K + 1;
     int32_t* cnt = at<int32_t>(ws, L.cnt);
     int32_t* local = at<int32_t>(ws, L.offs_local);
@@ -328,7 +328,7 @@ static hipError_t build(const WsLayout& L, void* ws, const KeySrc& ks, int64_t m
     int32_t* tot = at<int32_t>(ws, L.tot);
     int32_t* list = at<int32_t>(ws, L.list);
     const int nscan = (int)((r1 + kScanBlock - 1) / kScanBlock);
-    if (m > 0)
+    if (m > 0 && !counted)  // counted: the previous step's touched update already counted these ids
         launch(k_count<MODE>, grid_for(m, 1024), kBlock, 0, st, ks, m, cnt, at<int32_t>(ws, L.heavy_n),
                                                             at<int32_t>(ws, L.err));
     constexpr bool U2 = UNIQ || LIST;
@@ -343,7 +343,7 @@ static hipError_t build(const WsLayout& L, void* ws, const KeySrc& ks, int64_t m
 }
 
 hipError_t launch_index_build(const ncf_shape_t& s, const WsLayout& L, void* ws, const int32_t* users,
-                              const int32_t* items, int64_t n, hipStream_t st, bool touched_list) {
+                              const int32_t* items, int64_t n, hipStream_t st, bool touched_list, bool counted) {
     KeySrc ks{users, items, nullptr, s.num_users, s.num_items, 1, 0};
     if (touched_list) {
         PlanOut po{};
@@ -351,9 +351,10 @@ hipError_t launch_index_build(const ncf_shape_t& s, const WsLayout& L, void* ws,
         po.utot = at<int32_t>(ws, L.utot);
         po.uniq_rows = at<int32_t>(ws, L.touched);
         po.nuniq = at<int32_t>(ws, L.nuniq);
-        return build<kKeyPair, false, true>(L, ws, ks, 2 * n, s.num_rows, po, (int)((2 * n + 31) / 32), st);
+        return build<kKeyPair, false, true>(L, ws, ks, 2 * n, s.num_rows, po, (int)((2 * n + 31) / 32), st,
+                                            counted);
     }
-    return build<kKeyPair, false>(L, ws, ks, 2 * n, s.num_rows, PlanOut{}, (int)((2 * n + 31) / 32), st);
+    return build<kKeyPair, false>(L, ws, ks, 2 * n, s.num_rows, PlanOut{}, (int)((2 * n + 31) / 32), st, counted);
 }
 
 hipError_t launch_shard_plan(const ncf_shape_t& s, const WsLayout& L, void* ws, const int32_t* users,

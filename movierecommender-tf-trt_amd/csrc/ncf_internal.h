@@ -117,7 +117,8 @@ __host__ __device__ inline T* at(void* base, size_t off) {
 // index build: contribution c = 2*i + side (0 user row, 1 item row) grouped by table row
 // touched_list: also the ascending list of the touched rows (ws touched, count in nuniq)
 hipError_t launch_index_build(const ncf_shape_t& s, const WsLayout& L, void* ws, const int32_t* users,
-                              const int32_t* items, int64_t n, hipStream_t st, bool touched_list = false);
+                              const int32_t* items, int64_t n, hipStream_t st, bool touched_list = false,
+                              bool counted = false);
 // row-sharded plan: index over owner-major keys + unique-row compaction (uniq_rows = local row
 // ids grouped by owner, send_counts[world], cid_u/cid_i/uoffs/nuniq in the workspace)
 hipError_t launch_shard_plan(const ncf_shape_t& s, const WsLayout& L, void* ws, const int32_t* users,
@@ -179,9 +180,12 @@ hipError_t launch_emb_catchup(const ncf_shape_t& s, const WsLayout& L, void* ws,
                               const int32_t* row_step, const int32_t* step, const ncf_hyper_t& h, bool all_rows,
                               hipStream_t st);
 hipError_t launch_row_step_fill(int32_t* row_step, int64_t R, const int32_t* step, hipStream_t st);
+// next_users/next_items (optional, n_next samples): extra blocks of the same launch count the NEXT
+// batch's contributions into the index counters (the next build skips its k_count)
 hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, void* ws, float* emb, float* m,
                                      float* v, int32_t* row_step, int32_t* step, const ncf_hyper_t& h,
-                                     hipStream_t st);
+                                     hipStream_t st, const int32_t* next_users = nullptr,
+                                     const int32_t* next_items = nullptr, int64_t n_next = 0);
 // dense gradient of rows [row_begin, num_rows) into out (indexed from row_begin)
 hipError_t launch_emb_grad_dense(const ncf_shape_t& s, const WsLayout& L, void* ws, float* out, hipStream_t st,
                                   int64_t row_begin = 0);

@@ -235,6 +235,15 @@ __global__ __launch_bounds__(kBlock) void k_row_step_fill(int32_t* __restrict__ 
 
 // Adam step t = *step + 1 on the touched rows, which were brought up to step t-1 before the
 // forward pass; records row_step[r] = t.
+struct CountAhead {
+    int nupd;                  // blocks [0, nupd) update rows; blocks >= nupd count
+    const int32_t* users;      // next batch (m = 2 * n_next contributions)
+    const int32_t* items;
+    int64_t m;
+    int32_t U, I;
+    int32_t* cnt;
+};
+
 __global__ __launch_bounds__(kBlock) void k_emb_adam_touched(float4* __restrict__ emb, float4* __restrict__ m4,
                                                              float4* __restrict__ v4, uint32_t w4,
                                                              const int32_t* __restrict__ list,
@@ -243,14 +252,28 @@ __global__ __launch_bounds__(kBlock) void k_emb_adam_touched(float4* __restrict_
                                                              const int32_t* __restrict__ clist,
                                                              const float4* __restrict__ gs,
                                                              int32_t* __restrict__ row_step, const int32_t* step,
-                                                             float lr, float b1, float b2, float eps) {
+                                                             float lr, float b1, float b2, float eps,
+                                                             CountAhead ca) {
+    if ((int)blockIdx.x >= ca.nupd) {
+        // extra blocks: count the NEXT batch's contributions (k_count's work) while this step's
+        // rows stream; the counters are free here (the fill of this step's index emptied them)
+        const int64_t first = (int64_t)(blockIdx.x - ca.nupd) * kBlock + threadIdx.x;
+        const int64_t cstride = (int64_t)(gridDim.x - ca.nupd) * kBlock;
+        for (int64_t c = first; c < ca.m; c += cstride) {
+            const int64_t i = c >> 1;
+            const int id = (c & 1) ? ca.items[i] : ca.users[i];
+            const int bound = (c & 1) ? ca.I : ca.U;
+            if ((unsigned)id < (unsigned)bound) atomicAdd(&ca.cnt[(c & 1) ? ca.U + id : id], 1);
+        }
+        return;
+    }
     const RowLanes rl(w4);
     const int t = *step + 1;
     if (rl.on) {
         const float lr_t = adam_lr_t(lr, b1, b2, t);
         const int64_t n = *nlist;
         const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
-        const int64_t stride = (((int64_t)gridDim.x * kBlock) >> 6) * rl.rpw;
+        const int64_t stride = (((int64_t)ca.nupd * kBlock) >> 6) * rl.rpw;
         int64_t i = wave * rl.rpw + rl.sub;
         // software pipeline over this lane group's rows: the next row's id is loaded while the
         // current row is processed, so the list -> offsets -> contribution chain of row i+1
@@ -636,19 +659,25 @@ hipError_t launch_row_step_fill(int32_t* row_step, int64_t R, const int32_t* ste
 
 hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, void* ws, float* emb, float* m,
                                      float* v, int32_t* row_step, int32_t* step, const ncf_hyper_t& h,
-                                     hipStream_t st) {
+                                     hipStream_t st, const int32_t* next_users, const int32_t* next_items,
+                                     int64_t n_next) {
     const uint32_t w4 = (uint32_t)(s.row_width / 4);
     const uint32_t n4 = (uint32_t)(s.num_rows * w4);
     const int32_t* offs = at<int32_t>(ws, L.offs);
     const int32_t* list = at<int32_t>(ws, L.list);
     const float4* gs = at<const float4>(ws, L.gs);
     const int64_t R = s.num_rows;
-    if (h.optimizer == NCF_OPT_ADAM)
-        launch(k_emb_adam_touched, row_grid(R < 2 * L.max_batch ? R : 2 * L.max_batch, w4, NCF_TOUCHED_GRID_MAX), kBlock, 0, st,
+    if (h.optimizer == NCF_OPT_ADAM) {
+        const unsigned nupd = row_grid(R < 2 * L.max_batch ? R : 2 * L.max_batch, w4, NCF_TOUCHED_GRID_MAX);
+        CountAhead ca{(int)nupd, next_users, next_items, next_users ? 2 * n_next : 0, s.num_users, s.num_items,
+                      at<int32_t>(ws, L.cnt)};
+        const unsigned ncount = ca.m > 0 ? (unsigned)((ca.m + kBlock - 1) / kBlock < 512 ? (ca.m + kBlock - 1) / kBlock
+                                                                                             : 512) : 0u;
+        launch(k_emb_adam_touched, nupd + ncount, kBlock, 0, st,
                (float4*)emb, (float4*)m, (float4*)v, w4, at<const int32_t>(ws, L.touched),
                at<const int32_t>(ws, L.nuniq), offs, list, gs, row_step, (const int32_t*)step, h.lr, h.beta_1, h.beta_2,
-               h.epsilon);
-    else
+               h.epsilon, ca);
+    } else
         launch(k_emb_sgd_hot, kUpdateGrid, kBlock, 0, st, (float4*)emb, n4, w4, offs, list, gs, h.lr);
     return hipGetLastError();
 }

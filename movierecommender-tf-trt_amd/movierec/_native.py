@@ -73,6 +73,8 @@ _SIGNATURES = {
     "ncf_group_metrics": (ctypes.c_int, [_vp, _vp, _i64, _i32, _i32, _vp, _vp, _vp]),
     "ncf_train_step": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _vp, _vp, _vp, _i64,
                                       _vp, _vp, _vp, ctypes.c_size_t, _vp]),
+    "ncf_train_step_ahead": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _vp, _vp, _vp,
+                                            _i64, _vp, _vp, _i64, _vp, _vp, _vp, ctypes.c_size_t, _vp]),
     "ncf_evaluate": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfHyper), _vp, _vp, _vp, _i64, _vp, _vp, _vp,
                                     ctypes.c_size_t, _vp]),
     "ncf_forward_backward": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfHyper), _vp, _vp, _vp, _i64, _vp, _vp,

@@ -75,7 +75,8 @@ class NCFEngine(object):
             self.val_stats = torch.zeros(N.NCF_NUM_STATS, dtype=torch.float64, device=dev)
             self.max_batch = 0
             self.ws = None
-            self._prebuilt = None   # (users ptr, items ptr, n) of an index built ahead by build_index
+            self._prebuilt = None   # (users, items, n) of an index built ahead by build_index
+            self._counted = None    # (users, items, n) whose index counts ncf_train_step_ahead took
             self._ensure_ws(int(max_batch))
         self.model_s = N.NcfModel(self.emb.data_ptr(), self.mlp.data_ptr())
         self.hyper = N.NcfHyper()
@@ -149,6 +150,7 @@ class NCFEngine(object):
         N.check(L.ncf_workspace_size(ctypes.byref(self.shape), int(n), ctypes.byref(nbytes)))
         self.ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=self.device)
         self._prebuilt = None
+        self._counted = None
         self.ws_bytes = int(nbytes.value)
         N.check(L.ncf_workspace_init(ctypes.byref(self.shape), int(n), N.ptr(self.ws), self.ws_bytes,
                                      N.stream_handle(self.device)))
@@ -214,18 +216,54 @@ class NCFEngine(object):
         if i.size and (i.min() < 0 or i.max() >= self.num_items):
             raise ValueError("item id out of range [0, %d)" % self.num_items)
 
-    def train_step(self, users, items, labels, group, k, inv_batch=None, probs_out=None):
+    def train_step(self, users, items, labels, group, k, inv_batch=None, probs_out=None, next_batch=None):
+        """Keras ``train_on_batch``.  ``next_batch`` = (users, items) device int32 tensors of the
+        following call (deferred-decay Adam): their index counts are taken inside this step's
+        touched-row update, and the next call skips its count kernel if it passes exactly these
+        tensors (identity-checked; their contents must not change in between)."""
         u, i, y = self._ids(users), self._ids(items), self._labels(labels)
         n = u.numel()
         self._ensure_ws(n)
         h = self.hyper
         h.group, h.k = int(group), int(k)
         h.inv_batch = 1.0 / n if inv_batch is None else float(inv_batch)
-        N.check(N.lib().ncf_train_step(ctypes.byref(self.shape), ctypes.byref(self.model_s),
-                                       ctypes.byref(self.optim_s), ctypes.byref(h), N.ptr(u), N.ptr(i), N.ptr(y), n,
-                                       N.ptr(self.stats), N.ptr(probs_out), N.ptr(self.ws), self.ws_bytes,
-                                       N.stream_handle(self.device)))
+        pc = self._counted
+        ready = pc is not None and pc[0].data_ptr() == u.data_ptr() and pc[1].data_ptr() == i.data_ptr() and \
+            pc[2] == n
+        if pc is not None and not ready:
+            self._discard_counted()
+        nu = ni = None
+        if next_batch is not None and self.row_step is not None and h.optimizer == N.NCF_OPT_ADAM:
+            nu, ni = next_batch
+            if not (torch.is_tensor(nu) and torch.is_tensor(ni) and nu.is_cuda and ni.is_cuda and
+                    nu.dtype == torch.int32 and ni.dtype == torch.int32 and nu.is_contiguous() and
+                    ni.is_contiguous() and nu.numel() == ni.numel() and 0 < nu.numel() <= n):
+                nu = ni = None
+        h.index_ready = 2 if ready else 0
+        self._counted = None
+        try:
+            if nu is not None:
+                N.check(N.lib().ncf_train_step_ahead(
+                    ctypes.byref(self.shape), ctypes.byref(self.model_s), ctypes.byref(self.optim_s), ctypes.byref(h),
+                    N.ptr(u), N.ptr(i), N.ptr(y), n, N.ptr(nu), N.ptr(ni), nu.numel(), N.ptr(self.stats),
+                    N.ptr(probs_out), N.ptr(self.ws), self.ws_bytes, N.stream_handle(self.device)))
+                self._counted = (nu, ni, nu.numel())   # holds the tensors: their memory stays theirs
+            else:
+                N.check(N.lib().ncf_train_step(ctypes.byref(self.shape), ctypes.byref(self.model_s),
+                                               ctypes.byref(self.optim_s), ctypes.byref(h), N.ptr(u), N.ptr(i),
+                                               N.ptr(y), n, N.ptr(self.stats), N.ptr(probs_out), N.ptr(self.ws),
+                                               self.ws_bytes, N.stream_handle(self.device)))
+        finally:
+            h.index_ready = 0
         self._dirty = self.row_step is not None
+
+    def _discard_counted(self):
+        """Clear the index counters holding a next batch's counts (ncf_train_step_ahead) before any
+        other index build uses them."""
+        if self._counted is not None:
+            N.check(N.lib().ncf_workspace_init(ctypes.byref(self.shape), self.max_batch, N.ptr(self.ws),
+                                               self.ws_bytes, N.stream_handle(self.device)))
+            self._counted = None
 
     def evaluate(self, users, items, labels, group, k, stats=None, probs_out=None):
         u, i, y = self._ids(users), self._ids(items), self._labels(labels)
@@ -308,6 +346,7 @@ class NCFEngine(object):
                          reg_rows=None, include_dense_reg=True):
         """This replica's gradients (BCE mean over ``inv_batch``); ``reg_rows`` = (begin, count)
         of the embedding rows whose L2 loss this replica reports (default: all)."""
+        self._discard_counted()
         if self.row_step is not None:
             self.disable_lazy()   # data-parallel updates sweep every row
         u, i, y = self._ids(users), self._ids(items), self._labels(labels)
@@ -327,6 +366,7 @@ class NCFEngine(object):
         """``forward_backward`` with the dense embedding gradient written for the replicated rows
         [shared_row_begin, num_rows) only (``grads[0]`` indexed from that row); the own rows are
         updated from the per-sample gradients by ``update_rows`` (user-partitioned DP)."""
+        self._discard_counted()
         if self.row_step is not None:
             self.disable_lazy()
         u, i, y = self._ids(users), self._ids(items), self._labels(labels)
@@ -357,6 +397,7 @@ class NCFEngine(object):
         pass the same id tensors (checked by identity, else the index is rebuilt), and their
         contents must not change in between (a sampler that refills one buffer in place must not
         use this)."""
+        self._discard_counted()
         self._prebuilt = None
         if not (torch.is_tensor(users) and torch.is_tensor(items) and users.is_cuda and items.is_cuda):
             return   # host ids get converted per call: nothing stable to key the index on

@@ -363,3 +363,32 @@ def test_prebuilt_index_equals_inline_build():
         outs.append((e.emb.clone(), e.mlp.clone(), e.emb_m.clone()))
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+def test_count_ahead_equals_plain_steps():
+    """ncf_train_step_ahead (the next batch's index counts taken inside this step's touched-row
+    update, hyper.index_ready = 2 on the next call) is bitwise the plain step sequence, including
+    a call whose batch differs from the counted one (counters discarded) and reads in between."""
+    shape = O.NCFShape(*SHAPES[3])
+    w = _weights(shape, 50)
+    bt = []
+    for s in range(6):
+        users, items, y = _batch(shape, 256, 4, 51 + s)
+        bt.append((torch.from_numpy(users).cuda(), torch.from_numpy(items).cuda(), torch.from_numpy(y).cuda()))
+    a = _engine(shape, w, lazy_adam=True)
+    b = _engine(shape, w, lazy_adam=True)
+    order = [0, 1, 2, 4, 5]           # the step after 2 was announced as 3 but 4 comes
+    announced = [1, 2, 3, 5, None]
+    for s, j in enumerate(order):
+        nxt = announced[s]
+        a.train_step(*bt[j], group=4, k=2, next_batch=None if nxt is None else (bt[nxt][0], bt[nxt][1]))
+        if s == 1:
+            a.predict(bt[0][0], bt[0][1])   # a read (flush) between counted steps
+        b.train_step(*bt[j], group=4, k=2)
+        if s == 1:
+            b.predict(bt[0][0], bt[0][1])
+    a.flush()
+    b.flush()
+    torch.cuda.synchronize()
+    for x, y in ((a.emb, b.emb), (a.emb_m, b.emb_m), (a.emb_v, b.emb_v), (a.mlp, b.mlp), (a.stats, b.stats)):
+        assert torch.equal(x, y)
