@@ -120,8 +120,8 @@ typedef struct ncf_hyper {
                                            12288 floats, e.g. config D) */
     int32_t index_ready;                /* 1: the contribution index of this call's batch was built
                                            beforehand by ncf_build_index (same ids, same ws): skip it;
-                                           2: its contributions were counted by the previous
-                                           ncf_train_step_ahead (same ids, same ws): skip the count */
+                                           2: its contributions were counted and scanned by the
+                                           previous ncf_train_step_ahead (same ids, same ws) */
     int32_t reserved[5];
 } ncf_hyper_t;
 
@@ -161,11 +161,12 @@ int ncf_train_step(const ncf_shape_t* shape, ncf_model_t* model, ncf_optim_t* op
                    const int32_t* users, const int32_t* items, const float* labels, int64_t n,
                    double* stats, float* probs_out, void* ws, size_t ws_bytes, void* stream);
 
-/* ncf_train_step that also counts the NEXT batch's contributions (next_users/next_items, n_next
- * samples) inside the step's touched-row update launch (extra workgroups), so the next call —
- * made with hyper->index_ready = 2 and exactly these ids — skips its count kernel.  Deferred-decay
- * Adam only (optim->row_step).  No other index-building call may come in between (the counters
- * hold the next batch's counts; ncf_workspace_init clears them). */
+/* ncf_train_step that also prepares the NEXT batch's index (next_users/next_items, n_next == n
+ * samples): its contributions are counted by extra workgroups of this step's touched-row update
+ * and its per-block key scan rides in this step's stats launch, so the next call — made with
+ * hyper->index_ready = 2 and exactly these ids — skips both kernels.  Deferred-decay Adam only
+ * (optim->row_step).  No other index-building call may come in between (the counters hold the
+ * next batch's counts; ncf_workspace_init clears them). */
 int ncf_train_step_ahead(const ncf_shape_t* shape, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* hyper,
                          const int32_t* users, const int32_t* items, const float* labels, int64_t n,
                          const int32_t* next_users, const int32_t* next_items, int64_t n_next, double* stats,

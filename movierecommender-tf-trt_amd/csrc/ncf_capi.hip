@@ -496,7 +496,9 @@ static int train_step_impl(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t
     e = join_side(st, ss);
     if (e != hipSuccess) return hip_check(e, "side-stream join");
     const int nreg_emb = h->l2[0] != 0.0f ? ncf::kUpdateGrid : 0;
-    e = ncf::launch_stats(L, ws, summary, nreg_emb, nreg_mlp, h->inv_batch, stats, optim->step, true, st);
+    // counting ahead: the stats launch also scans the next batch's counts
+    e = ncf::launch_stats(L, ws, summary, nreg_emb, nreg_mlp, h->inv_batch, stats, optim->step, true, st,
+                          lazy && next_users != nullptr, s->num_rows);
     return hip_check(e, "stats");
 }
 
@@ -512,8 +514,10 @@ int ncf_train_step_ahead(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* 
                          const int32_t* next_users, const int32_t* next_items, int64_t n_next, double* stats,
                          float* probs_out, void* ws, size_t ws_bytes, void* stream) {
     if (!s || !optim || !h) return fail(NCF_EINVAL, "NULL argument");
-    if (!next_users || !next_items || n_next <= 0 || n_next > n)
-        return fail(NCF_EINVAL, "next batch: NULL ids or n_next outside [1, n]");
+    // the scan ahead lands in workspace regions placed by the batch size: the next batch must
+    // have this batch's size
+    if (!next_users || !next_items || n_next != n)
+        return fail(NCF_EINVAL, "next batch: NULL ids or n_next != n");
     if (!optim->row_step || h->optimizer != NCF_OPT_ADAM)
         return fail(NCF_EINVAL, "counting ahead needs deferred-decay Adam (optim->row_step)");
     return train_step_impl(s, model, optim, h, users, items, labels, n, next_users, next_items, n_next, stats,

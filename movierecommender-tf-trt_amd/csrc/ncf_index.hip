@@ -82,39 +82,13 @@ __global__ __launch_bounds__(kBlock) void k_count(KeySrc ks, int64_t m, int32_t*
     }
 }
 
-// Per-2048-key exclusive scan of cnt (and, for a plan, of the occupied-key flags cnt > 0).
+// Per-2048-key exclusive scan of cnt (and, for a plan, of the occupied-key flags cnt > 0): the
+// body (scan_local_body, ncf_internal.h) is shared with the stats launch that scans ahead.
 template <bool UNIQ>
 __global__ __launch_bounds__(kBlock) void k_scan_local(const int32_t* __restrict__ cnt, int64_t r1,
                                                        int32_t* __restrict__ offs, int32_t* __restrict__ tot,
                                                        int32_t* __restrict__ uloc, int32_t* __restrict__ utot) {
-    __shared__ int sw[4];
-    const int64_t base = (int64_t)blockIdx.x * kScanBlock + threadIdx.x * 8;
-    int v[8];
-    int sum = 0, nz = 0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        v[j] = (base + j < r1) ? cnt[base + j] : 0;
-        sum += v[j];
-        nz += v[j] > 0;
-    }
-    int total;
-    int run = block_exscan_256(sum, sw, &total);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        if (base + j < r1) offs[base + j] = run;
-        run += v[j];
-    }
-    if (threadIdx.x == 0) tot[blockIdx.x] = total;
-    if constexpr (UNIQ) {
-        int utotal;
-        int urun = block_exscan_256(nz, sw, &utotal);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            if (base + j < r1) uloc[base + j] = urun;
-            urun += v[j] > 0;
-        }
-        if (threadIdx.x == 0) utot[blockIdx.x] = utotal;
-    }
+    scan_local_body<UNIQ>(cnt, r1, offs, tot, uloc, utot, (int)blockIdx.x);
 }
 
 // Exclusive prefix of the scan-block totals into LDS pre[0..nscan) (every thread participates).
@@ -321,6 +295,7 @@ static hipError_t set_sort_lds(int nwords) {
 template <int MODE, bool UNIQ, bool LIST = false>
 static hipError_t build(const WsLayout& L, void* ws, const KeySrc& ks, int64_t m, int64_t K, PlanOut po,
                         int nwords, hipStream_t st, bool counted = false) {
+    // counted: the previous step counted AND scanned these ids (touched update + stats launch)
     const int64_t r1 = K + 1;
     int32_t* cnt = at<int32_t>(ws, L.cnt);
     int32_t* local = at<int32_t>(ws, L.offs_local);
@@ -332,8 +307,9 @@ static hipError_t build(const WsLayout& L, void* ws, const KeySrc& ks, int64_t m
         launch(k_count<MODE>, grid_for(m, 1024), kBlock, 0, st, ks, m, cnt, at<int32_t>(ws, L.heavy_n),
                                                             at<int32_t>(ws, L.err));
     constexpr bool U2 = UNIQ || LIST;
-    launch(k_scan_local<U2>, nscan, kBlock, 0, st, cnt, r1, local, tot, U2 ? at<int32_t>(ws, L.uloc) : nullptr,
-                                               U2 ? at<int32_t>(ws, L.utot) : nullptr);
+    if (!counted)
+        launch(k_scan_local<U2>, nscan, kBlock, 0, st, cnt, r1, local, tot, U2 ? at<int32_t>(ws, L.uloc) : nullptr,
+                                                   U2 ? at<int32_t>(ws, L.utot) : nullptr);
     const size_t pre_bytes = (size_t)nscan * 4 * (U2 ? 2 : 1);
     launch(k_fill<MODE, UNIQ, LIST>, grid_for(m > r1 ? m : r1, 1024), kBlock, pre_bytes, st, ks, m, cnt, local, tot,
                                                                                          nscan, r1, offs, list, po);

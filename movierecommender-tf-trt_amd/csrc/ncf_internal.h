@@ -7,6 +7,7 @@
 #include <stdint.h>
 
 #include "movierec_ncf.h"
+#include "ncf_common.h"
 
 namespace ncf {
 
@@ -66,6 +67,42 @@ struct WsLayout {
     int64_t keys;     // key space of the index: world * S (R when world == 0)
     int64_t list_cap; // contribution capacity of list (2B, or world * min(2B, S) for the owner index)
 };
+
+// Per-kScanBlock-key exclusive scan of cnt into offs (+ block total), and for UNIQ of the flags
+// cnt > 0 into uloc / utot: the body of k_scan_local for scan block `blk` (whole workgroup).
+template <bool UNIQ>
+__device__ inline void scan_local_body(const int32_t* __restrict__ cnt, int64_t r1, int32_t* __restrict__ offs,
+                                       int32_t* __restrict__ tot, int32_t* __restrict__ uloc,
+                                       int32_t* __restrict__ utot, int blk) {
+    __shared__ int sw[4];
+    const int64_t base = (int64_t)blk * kScanBlock + threadIdx.x * 8;
+    int v[8];
+    int sum = 0, nz = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        v[j] = (base + j < r1) ? cnt[base + j] : 0;
+        sum += v[j];
+        nz += v[j] > 0;
+    }
+    int total;
+    int run = block_exscan_256(sum, sw, &total);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        if (base + j < r1) offs[base + j] = run;
+        run += v[j];
+    }
+    if (threadIdx.x == 0) tot[blk] = total;
+    if constexpr (UNIQ) {
+        int utotal;
+        int urun = block_exscan_256(nz, sw, &utotal);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if (base + j < r1) uloc[base + j] = urun;
+            urun += v[j] > 0;
+        }
+        if (threadIdx.x == 0) utot[blk] = utotal;
+    }
+}
 
 // world == 0: single-table layout; world >= 1: row-sharded layout (ncf_shard_*)
 WsLayout make_layout(const ncf_shape_t& s, int64_t max_batch, int world = 0);
@@ -199,8 +236,11 @@ hipError_t launch_mlp_update(const ncf_shape_t& s, const WsLayout& L, void* ws, 
                              float* summary = nullptr);
 hipError_t launch_emb_reg(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, int64_t rows,
                           float lam, hipStream_t st);
+// scan_ahead: the same launch also runs the next batch's per-block key scan (k_scan_local<true>
+// over the counts the touched update took ahead)
 hipError_t launch_stats(const WsLayout& L, void* ws, const float* summary, int nreg_emb, int nreg_mlp,
-                        float inv_batch, double* stats, int32_t* step, bool bump_step, hipStream_t st);
+                        float inv_batch, double* stats, int32_t* step, bool bump_step, hipStream_t st,
+                        bool scan_ahead = false, int64_t scan_keys = 0);
 
 // on-device negative sampling (ncf_sample.hip)
 hipError_t launch_sample_batch(const int32_t* pos_users, const int32_t* pos_items, const int32_t* excl_ptr,

@@ -576,6 +576,26 @@ __global__ __launch_bounds__(kBlock) void k_stats(const float* __restrict__ summ
     stats_body(summary, reg_emb, nreg_emb, reg_mlp, nreg_mlp, inv_batch, stats, step, bump, red);
 }
 
+// Block 0: k_stats; blocks 1..: the next batch's per-block key scan (k_scan_local<true>) over the
+// counts the touched update took ahead — one launch instead of two.
+struct ScanAhead {
+    const int32_t* cnt;
+    int64_t r1;
+    int32_t *offs, *tot, *uloc, *utot;
+};
+__global__ __launch_bounds__(kBlock) void k_stats_scan(const float* __restrict__ summary,
+                                                       const float* __restrict__ reg_emb, int nreg_emb,
+                                                       const float* __restrict__ reg_mlp, int nreg_mlp,
+                                                       float inv_batch, double* __restrict__ stats, int32_t* step,
+                                                       int bump, ScanAhead sc) {
+    if (blockIdx.x == 0) {
+        __shared__ float red[4];
+        stats_body(summary, reg_emb, nreg_emb, reg_mlp, nreg_mlp, inv_batch, stats, step, bump, red);
+    } else {
+        scan_local_body<true>(sc.cnt, sc.r1, sc.offs, sc.tot, sc.uloc, sc.utot, (int)blockIdx.x - 1);
+    }
+}
+
 // ---------------------------------------------------------------------------
 
 static L2Table make_l2_table(const ncf_shape_t& s, const ncf_hyper_t& h) {
@@ -786,8 +806,18 @@ hipError_t launch_summary(const WsLayout& L, void* ws, int nbce, int nmet, float
 }
 
 hipError_t launch_stats(const WsLayout& L, void* ws, const float* summary, int nreg_emb, int nreg_mlp,
-                        float inv_batch, double* stats, int32_t* step, bool bump_step, hipStream_t st) {
+                        float inv_batch, double* stats, int32_t* step, bool bump_step, hipStream_t st,
+                        bool scan_ahead, int64_t scan_keys) {
     const float* reg = at<float>(ws, L.part_reg);
+    if (scan_ahead) {
+        const int64_t r1 = scan_keys + 1;
+        const int nscan = (int)((r1 + kScanBlock - 1) / kScanBlock);
+        ScanAhead sc{at<const int32_t>(ws, L.cnt), r1, at<int32_t>(ws, L.offs_local), at<int32_t>(ws, L.tot),
+                     at<int32_t>(ws, L.uloc), at<int32_t>(ws, L.utot)};
+        launch(k_stats_scan, 1 + nscan, kBlock, 0, st, summary, reg, nreg_emb, reg + kUpdateGrid, nreg_mlp, inv_batch,
+               stats, step, bump_step ? 1 : 0, sc);
+        return hipGetLastError();
+    }
     launch(k_stats, 1, kBlock, 0, st, summary, reg, nreg_emb, reg + kUpdateGrid, nreg_mlp, inv_batch, stats, step,
                                   bump_step ? 1 : 0);
     return hipGetLastError();

@@ -237,7 +237,7 @@ class NCFEngine(object):
             nu, ni = next_batch
             if not (torch.is_tensor(nu) and torch.is_tensor(ni) and nu.is_cuda and ni.is_cuda and
                     nu.dtype == torch.int32 and ni.dtype == torch.int32 and nu.is_contiguous() and
-                    ni.is_contiguous() and nu.numel() == ni.numel() and 0 < nu.numel() <= n):
+                    ni.is_contiguous() and nu.numel() == ni.numel() == n):
                 nu = ni = None
         h.index_ready = 2 if ready else 0
         self._counted = None
