@@ -349,12 +349,13 @@ struct CatchupCtx {
     const ncf_hyper_t* h;
     void* ws;
     hipStream_t st;
+    int64_t n;  // batch size (the catch-up launch also sorts the index lists)
 };
 static int catchup_touched(void* p) {
     const CatchupCtx& c = *static_cast<CatchupCtx*>(p);
     prof_begin(NCF_K_CATCHUP, c.st);
     hipError_t e = ncf::launch_emb_catchup(*c.s, *c.L, c.ws, c.model->emb, c.optim->emb_m, c.optim->emb_v,
-                                           c.optim->row_step, c.optim->step, *c.h, false, c.st);
+                                           c.optim->row_step, c.optim->step, *c.h, false, c.st, true, c.n);
     prof_end(NCF_K_CATCHUP, c.st);
     return hip_check(e, "touched-row catch-up");
 }
@@ -391,7 +392,9 @@ static int run_fb(const ncf_shape_t& s, const ncf::WsLayout& L, const ncf_model_
         // NCF_SIDE_STREAM=2: only the dense-layer tail leaves the main stream
         hipStream_t sti = side_stream_mode() == 2 ? st : fork_side(st, &ss);
         prof_begin(NCF_K_INDEX, sti);
-        e = ncf::launch_index_build(s, L, ws, users, items, n, sti, after_index != nullptr, h->index_ready == 2);
+        // deferred decay: the catch-up launch (after_index) sorts the lists in extra workgroups
+        e = ncf::launch_index_build(s, L, ws, users, items, n, sti, after_index != nullptr, h->index_ready == 2,
+                                    after_index != nullptr);
         prof_end(NCF_K_INDEX, sti);
         if (e != hipSuccess) return hip_check(e, "index build");
         out->index_side = ss;
@@ -459,7 +462,7 @@ static int train_step_impl(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t
     const bool lazy = optim->row_step != nullptr;
     if (lazy && h->l2[0] != 0.0f)
         return fail(NCF_EINVAL, "deferred decay (row_step) needs the embedding L2 off: the loss sums the whole table");
-    CatchupCtx cc{s, &L, model, optim, h, ws, st};
+    CatchupCtx cc{s, &L, model, optim, h, ws, st, n};
     if (int r = run_fb(*s, L, model, h, users, items, labels, n, ws, probs_out, &fb, st, false,
                        lazy ? catchup_touched : nullptr, &cc))
         return r;

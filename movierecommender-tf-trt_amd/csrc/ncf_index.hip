@@ -185,92 +185,7 @@ __global__ __launch_bounds__(kBlock) void k_fill(KeySrc ks, int64_t m, int32_t* 
 // workgroup with a bitmap over the contribution ids (set bits, popcount scan, write back).
 __global__ __launch_bounds__(kBlock) void k_sort(const int32_t* __restrict__ offs, int64_t R,
                                                  int32_t* __restrict__ list, int nwords) {
-    extern __shared__ __attribute__((aligned(16))) unsigned bm[];
-    __shared__ int hrows[kBlock];
-    __shared__ int mrows[kBlock];
-    __shared__ int nh, nm;
-    __shared__ int sw[4];
-    if (threadIdx.x == 0) nh = nm = 0;
-    __syncthreads();
-    const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (r < R) {
-        const int o = offs[r];
-        const int c = offs[r + 1] - o;
-        if (c > 64) {
-            hrows[atomicAdd(&nh, 1)] = (int)r;
-        } else if (c > kSmallSeg) {
-            mrows[atomicAdd(&nm, 1)] = (int)r;
-        } else if (c >= 2) {
-            int v[kSmallSeg];
-#pragma unroll
-            for (int j = 0; j < kSmallSeg; ++j) v[j] = (j < c) ? list[o + j] : INT_MAX;
-#pragma unroll
-            for (int round = 0; round < kSmallSeg; ++round) {
-#pragma unroll
-                for (int j = round & 1; j + 1 < kSmallSeg; j += 2) {
-                    const int a = min(v[j], v[j + 1]);
-                    const int b = max(v[j], v[j + 1]);
-                    v[j] = a;
-                    v[j + 1] = b;
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < kSmallSeg; ++j)
-                if (j < c) list[o + j] = v[j];
-        }
-    }
-    __syncthreads();
-    // rows of 17..64 entries (frequent when a rank's users are few — user-partitioned DP): one
-    // wave each, a bitonic network across the 64 lanes (one entry per lane, INT_MAX padding)
-    {
-        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-        for (int hh = wv; hh < nm; hh += kBlock / 64) {
-            const int row = mrows[hh];
-            const int o = offs[row];
-            const int c = offs[row + 1] - o;
-            int x = lane < c ? list[o + lane] : INT_MAX;
-#pragma unroll
-            for (int k = 2; k <= 64; k <<= 1) {
-#pragma unroll
-                for (int j = k >> 1; j > 0; j >>= 1) {
-                    const int y = __shfl_xor(x, j, 64);
-                    const bool asc = (lane & k) == 0;
-                    const bool lower = (lane & j) == 0;
-                    x = (lower == asc) ? min(x, y) : max(x, y);
-                }
-            }
-            if (lane < c) list[o + lane] = x;
-        }
-    }
-    const int count = nh;
-    const int per = (nwords + kBlock - 1) / kBlock;
-    for (int hh = 0; hh < count; ++hh) {
-        const int row = hrows[hh];
-        const int o = offs[row];
-        const int c = offs[row + 1] - o;
-        for (int w = threadIdx.x; w < nwords; w += kBlock) bm[w] = 0u;
-        __syncthreads();
-        for (int j = threadIdx.x; j < c; j += kBlock) {
-            const unsigned v = (unsigned)list[o + j];
-            atomicOr(&bm[v >> 5], 1u << (v & 31));
-        }
-        __syncthreads();
-        const int w0 = threadIdx.x * per;
-        const int w1 = min(w0 + per, nwords);
-        int mine = 0;
-        for (int w = w0; w < w1; ++w) mine += __popc(bm[w]);
-        int total;
-        int pos = o + block_exscan_256(mine, sw, &total);
-        for (int w = w0; w < w1; ++w) {
-            unsigned b = bm[w];
-            while (b) {
-                const int bit = __ffs(b) - 1;
-                list[pos++] = w * 32 + bit;
-                b &= b - 1;
-            }
-        }
-        __syncthreads();
-    }
+    sort_rows_body(offs, R, list, nwords, (int)blockIdx.x);
 }
 
 static int grid_for(int64_t work, int cap) {
@@ -294,7 +209,8 @@ static hipError_t set_sort_lds(int nwords) {
 // count -> scan -> fill -> sort over K keys for m contributions.
 template <int MODE, bool UNIQ, bool LIST = false>
 static hipError_t build(const WsLayout& L, void* ws, const KeySrc& ks, int64_t m, int64_t K, PlanOut po,
-                        int nwords, hipStream_t st, bool counted = false) {
+                        int nwords, hipStream_t st, bool counted = false, bool skip_sort = false) {
+    // skip_sort: the caller's next launch (the touched-row catch-up) sorts the lists in extra blocks
     // counted: the previous step counted AND scanned these ids (touched update + stats launch)
     const int64_t r1 = K + 1;
     int32_t* cnt = at<int32_t>(ws, L.cnt);
@@ -313,13 +229,15 @@ static hipError_t build(const WsLayout& L, void* ws, const KeySrc& ks, int64_t m
     const size_t pre_bytes = (size_t)nscan * 4 * (U2 ? 2 : 1);
     launch(k_fill<MODE, UNIQ, LIST>, grid_for(m > r1 ? m : r1, 1024), kBlock, pre_bytes, st, ks, m, cnt, local, tot,
                                                                                          nscan, r1, offs, list, po);
+    if (skip_sort) return hipGetLastError();
     if (hipError_t e = set_sort_lds(nwords)) return e;
     launch(k_sort, (unsigned)((K + kBlock - 1) / kBlock), kBlock, (size_t)nwords * 4, st, offs, K, list, nwords);
     return hipGetLastError();
 }
 
 hipError_t launch_index_build(const ncf_shape_t& s, const WsLayout& L, void* ws, const int32_t* users,
-                              const int32_t* items, int64_t n, hipStream_t st, bool touched_list, bool counted) {
+                              const int32_t* items, int64_t n, hipStream_t st, bool touched_list, bool counted,
+                              bool skip_sort) {
     KeySrc ks{users, items, nullptr, s.num_users, s.num_items, 1, 0};
     if (touched_list) {
         PlanOut po{};
@@ -328,7 +246,7 @@ hipError_t launch_index_build(const ncf_shape_t& s, const WsLayout& L, void* ws,
         po.uniq_rows = at<int32_t>(ws, L.touched);
         po.nuniq = at<int32_t>(ws, L.nuniq);
         return build<kKeyPair, false, true>(L, ws, ks, 2 * n, s.num_rows, po, (int)((2 * n + 31) / 32), st,
-                                            counted);
+                                            counted, skip_sort);
     }
     return build<kKeyPair, false>(L, ws, ks, 2 * n, s.num_rows, PlanOut{}, (int)((2 * n + 31) / 32), st, counted);
 }

@@ -2,6 +2,8 @@
 // Not part of the ABI (see include/movierec_ncf.h).
 #pragma once
 
+#include <climits>
+
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -104,6 +106,97 @@ __device__ inline void scan_local_body(const int32_t* __restrict__ cnt, int64_t 
     }
 }
 
+template <int UNUSED = 0>
+__device__ inline void sort_rows_body(const int32_t* __restrict__ offs, int64_t R, int32_t* __restrict__ list,
+                                      int nwords, int blk) {
+    extern __shared__ __attribute__((aligned(16))) unsigned bm[];
+    __shared__ int hrows[kBlock];
+    __shared__ int mrows[kBlock];
+    __shared__ int nh, nm;
+    __shared__ int sw[4];
+    if (threadIdx.x == 0) nh = nm = 0;
+    __syncthreads();
+    const int64_t r = (int64_t)blk * kBlock + threadIdx.x;
+    if (r < R) {
+        const int o = offs[r];
+        const int c = offs[r + 1] - o;
+        if (c > 64) {
+            hrows[atomicAdd(&nh, 1)] = (int)r;
+        } else if (c > kSmallSeg) {
+            mrows[atomicAdd(&nm, 1)] = (int)r;
+        } else if (c >= 2) {
+            int v[kSmallSeg];
+#pragma unroll
+            for (int j = 0; j < kSmallSeg; ++j) v[j] = (j < c) ? list[o + j] : INT_MAX;
+#pragma unroll
+            for (int round = 0; round < kSmallSeg; ++round) {
+#pragma unroll
+                for (int j = round & 1; j + 1 < kSmallSeg; j += 2) {
+                    const int a = min(v[j], v[j + 1]);
+                    const int b = max(v[j], v[j + 1]);
+                    v[j] = a;
+                    v[j + 1] = b;
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < kSmallSeg; ++j)
+                if (j < c) list[o + j] = v[j];
+        }
+    }
+    __syncthreads();
+    // rows of 17..64 entries (frequent when a rank's users are few — user-partitioned DP): one
+    // wave each, a bitonic network across the 64 lanes (one entry per lane, INT_MAX padding)
+    {
+        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+        for (int hh = wv; hh < nm; hh += kBlock / 64) {
+            const int row = mrows[hh];
+            const int o = offs[row];
+            const int c = offs[row + 1] - o;
+            int x = lane < c ? list[o + lane] : INT_MAX;
+#pragma unroll
+            for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+                for (int j = k >> 1; j > 0; j >>= 1) {
+                    const int y = __shfl_xor(x, j, 64);
+                    const bool asc = (lane & k) == 0;
+                    const bool lower = (lane & j) == 0;
+                    x = (lower == asc) ? min(x, y) : max(x, y);
+                }
+            }
+            if (lane < c) list[o + lane] = x;
+        }
+    }
+    const int count = nh;
+    const int per = (nwords + kBlock - 1) / kBlock;
+    for (int hh = 0; hh < count; ++hh) {
+        const int row = hrows[hh];
+        const int o = offs[row];
+        const int c = offs[row + 1] - o;
+        for (int w = threadIdx.x; w < nwords; w += kBlock) bm[w] = 0u;
+        __syncthreads();
+        for (int j = threadIdx.x; j < c; j += kBlock) {
+            const unsigned v = (unsigned)list[o + j];
+            atomicOr(&bm[v >> 5], 1u << (v & 31));
+        }
+        __syncthreads();
+        const int w0 = threadIdx.x * per;
+        const int w1 = min(w0 + per, nwords);
+        int mine = 0;
+        for (int w = w0; w < w1; ++w) mine += __popc(bm[w]);
+        int total;
+        int pos = o + block_exscan_256(mine, sw, &total);
+        for (int w = w0; w < w1; ++w) {
+            unsigned b = bm[w];
+            while (b) {
+                const int bit = __ffs(b) - 1;
+                list[pos++] = w * 32 + bit;
+                b &= b - 1;
+            }
+        }
+        __syncthreads();
+    }
+}
+
 // world == 0: single-table layout; world >= 1: row-sharded layout (ncf_shard_*)
 WsLayout make_layout(const ncf_shape_t& s, int64_t max_batch, int world = 0);
 
@@ -155,7 +248,7 @@ __host__ __device__ inline T* at(void* base, size_t off) {
 // touched_list: also the ascending list of the touched rows (ws touched, count in nuniq)
 hipError_t launch_index_build(const ncf_shape_t& s, const WsLayout& L, void* ws, const int32_t* users,
                               const int32_t* items, int64_t n, hipStream_t st, bool touched_list = false,
-                              bool counted = false);
+                              bool counted = false, bool skip_sort = false);
 // row-sharded plan: index over owner-major keys + unique-row compaction (uniq_rows = local row
 // ids grouped by owner, send_counts[world], cid_u/cid_i/uoffs/nuniq in the workspace)
 hipError_t launch_shard_plan(const ncf_shape_t& s, const WsLayout& L, void* ws, const int32_t* users,
@@ -213,9 +306,11 @@ hipError_t launch_emb_update(const ncf_shape_t& s, const WsLayout& L, void* ws, 
 // deferred exact decay (ncf_update.hip, L2 off): replay the missed zero-gradient Adam steps of
 // the touched rows (all_rows: every row, ncf_lazy_flush) up to *step; then the step's update of
 // the touched rows, which records row_step[r] = *step + 1.  Bitwise the dense sweep.
+// sort_lists (touched rows only): extra blocks of the same launch run k_sort over the index the
+// build left unsorted (launch_index_build(..., skip_sort = true)), for batch size n
 hipError_t launch_emb_catchup(const ncf_shape_t& s, const WsLayout& L, void* ws, float* emb, float* m, float* v,
                               const int32_t* row_step, const int32_t* step, const ncf_hyper_t& h, bool all_rows,
-                              hipStream_t st);
+                              hipStream_t st, bool sort_lists = false, int64_t n = 0);
 hipError_t launch_row_step_fill(int32_t* row_step, int64_t R, const int32_t* step, hipStream_t st);
 // next_users/next_items (optional, n_next samples): extra blocks of the same launch count the NEXT
 // batch's contributions into the index counters (the next build skips its k_count)

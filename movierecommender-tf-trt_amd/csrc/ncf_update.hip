@@ -187,6 +187,14 @@ constexpr int kLrLut = 64;  // bias-corrected lr of the last kLrLut steps, per b
 
 // replay the zero-gradient steps (s, t] of the touched rows list[0..*nlist) (ALL: every row,
 // ncf_lazy_flush)
+struct SortAhead {
+    int ncatch;                // blocks [0, ncatch) replay rows; blocks >= ncatch sort lists
+    const int32_t* offs;
+    int64_t keys;
+    int32_t* list;
+    int nwords;
+};
+
 template <bool ALL>
 __global__ __launch_bounds__(kBlock) void k_emb_catchup(float4* __restrict__ emb, float4* __restrict__ m4,
                                                         float4* __restrict__ v4, uint32_t w4,
@@ -194,7 +202,13 @@ __global__ __launch_bounds__(kBlock) void k_emb_catchup(float4* __restrict__ emb
                                                         const int32_t* __restrict__ nlist, int64_t R,
                                                         const int32_t* __restrict__ row_step,
                                                         const int32_t* __restrict__ step, float lr, float b1,
-                                                        float b2, float eps) {
+                                                        float b2, float eps, SortAhead so) {
+    if (!ALL && (int)blockIdx.x >= so.ncatch) {
+        // the contribution lists of this step's index, sorted while the rows replay (k_sort's work;
+        // only the touched-row update after the forward pass reads them)
+        sort_rows_body(so.offs, so.keys, so.list, so.nwords, (int)blockIdx.x - so.ncatch);
+        return;
+    }
     __shared__ float lut[kLrLut];
     const int t = *step;  // steps every row should have received
     if (threadIdx.x < kLrLut) lut[threadIdx.x] = t - (int)threadIdx.x >= 1 ? adam_lr_t(lr, b1, b2, t - threadIdx.x) : 0.f;
@@ -203,7 +217,7 @@ __global__ __launch_bounds__(kBlock) void k_emb_catchup(float4* __restrict__ emb
     if (!rl.on) return;
     const int64_t n = ALL ? R : (int64_t)*nlist;
     const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
-    const int64_t waves = ((int64_t)gridDim.x * kBlock) >> 6;
+    const int64_t waves = ((int64_t)(ALL ? gridDim.x : so.ncatch) * kBlock) >> 6;
     const float4 zero = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int64_t i = wave * rl.rpw + rl.sub; i < n; i += waves * rl.rpw) {
         const int64_t r = ALL ? i : list[i];
@@ -656,19 +670,46 @@ static unsigned row_grid(int64_t rows, uint32_t w4, int64_t cap) {
 
 hipError_t launch_emb_catchup(const ncf_shape_t& s, const WsLayout& L, void* ws, float* emb, float* m, float* v,
                               const int32_t* row_step, const int32_t* step, const ncf_hyper_t& h, bool all_rows,
-                              hipStream_t st) {
-    if (h.optimizer != NCF_OPT_ADAM) return hipSuccess;  // SGD: an untouched row does not move
+                              hipStream_t st, bool sort_lists, int64_t n) {
     const uint32_t w4 = (uint32_t)(s.row_width / 4);
     const int64_t R = s.num_rows;
     const int64_t nmax = R < 2 * L.max_batch ? R : 2 * L.max_batch;
-    if (all_rows)
+    SortAhead so{0, nullptr, 0, nullptr, 0};
+    unsigned nsort = 0;
+    size_t lds = 0;
+    if (sort_lists && !all_rows) {
+        so = SortAhead{0, at<const int32_t>(ws, L.offs), R, at<int32_t>(ws, L.list), (int)((2 * n + 31) / 32)};
+        nsort = (unsigned)((R + kBlock - 1) / kBlock);
+        lds = (size_t)so.nwords * 4;
+        static bool lds_cfg = false;
+        if (!lds_cfg && lds > 65536) {
+            hipError_t e = hipFuncSetAttribute((const void*)k_emb_catchup<false>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               (int)((kMaxBatch * 2 / 32) * 4));
+            if (e != hipSuccess) return e;
+            lds_cfg = true;
+        }
+    }
+    if (h.optimizer != NCF_OPT_ADAM) {  // SGD: an untouched row does not move; only the sort remains
+        if (nsort) {
+            so.ncatch = 0;
+            launch(k_emb_catchup<false>, nsort, kBlock, lds, st, (float4*)emb, (float4*)m, (float4*)v, w4,
+                   at<const int32_t>(ws, L.touched), at<const int32_t>(ws, L.nuniq), R, row_step, step, h.lr,
+                   h.beta_1, h.beta_2, h.epsilon, so);
+        }
+        return hipGetLastError();
+    }
+    if (all_rows) {
         launch(k_emb_catchup<true>, row_grid(R, w4, 8192), kBlock, 0, st, (float4*)emb, (float4*)m, (float4*)v, w4,
                (const int32_t*)nullptr, (const int32_t*)nullptr, R, row_step, step, h.lr, h.beta_1, h.beta_2,
-               h.epsilon);
-    else
-        launch(k_emb_catchup<false>, row_grid(nmax, w4, NCF_CATCHUP_GRID_MAX), kBlock, 0, st, (float4*)emb, (float4*)m, (float4*)v, w4,
+               h.epsilon, so);
+    } else {
+        const unsigned ncatch = row_grid(nmax, w4, NCF_CATCHUP_GRID_MAX);
+        so.ncatch = (int)ncatch;
+        launch(k_emb_catchup<false>, ncatch + nsort, kBlock, lds, st, (float4*)emb, (float4*)m, (float4*)v, w4,
                at<const int32_t>(ws, L.touched), at<const int32_t>(ws, L.nuniq), R, row_step, step, h.lr, h.beta_1,
-               h.beta_2, h.epsilon);
+               h.beta_2, h.epsilon, so);
+    }
     return hipGetLastError();
 }
 
