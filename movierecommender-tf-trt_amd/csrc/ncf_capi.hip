@@ -481,16 +481,21 @@ static int train_step_impl(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t
         if (e != hipSuccess) return hip_check(e, "summary");
     }
     int nreg_mlp = 0;
+    // one stream + deferred decay: the dense layers' Adam step runs in extra workgroups of the
+    // touched-row update launch (one launch fewer)
+    ncf::MlpDeferred mlp_def{nullptr, nullptr, nullptr, nullptr, 0};
+    const bool defer_mlp = fold && lazy;
     prof_begin(NCF_K_MLP_UPDATE, st2);
     e = ncf::launch_mlp_update(*s, L, ws, model->mlp, optim->mlp_m, optim->mlp_v, optim->step, *h, fb.nslab, nullptr,
                                nullptr, true, &nreg_mlp, st2, false, fold ? fb.nbce : -1, fb.nmet, fb.n_groups,
-                               fold ? summary : nullptr);
+                               fold ? summary : nullptr, defer_mlp ? &mlp_def : nullptr);
     prof_end(NCF_K_MLP_UPDATE, st2);
     if (e != hipSuccess) return hip_check(e, "dense update");
     prof_begin(NCF_K_EMB_UPDATE, st);
     if (lazy)
         e = ncf::launch_emb_update_touched(*s, L, ws, model->emb, optim->emb_m, optim->emb_v, optim->row_step,
-                                           optim->step, *h, st, next_users, next_items, n_next);
+                                           optim->step, *h, st, next_users, next_items, n_next,
+                                           mlp_def.p ? &mlp_def : nullptr);
     else
         e = ncf::launch_emb_update(*s, L, ws, model->emb, optim->emb_m, optim->emb_v, optim->step, *h, nullptr,
                                    s->num_rows, st);

@@ -314,10 +314,18 @@ hipError_t launch_emb_catchup(const ncf_shape_t& s, const WsLayout& L, void* ws,
 hipError_t launch_row_step_fill(int32_t* row_step, int64_t R, const int32_t* step, hipStream_t st);
 // next_users/next_items (optional, n_next samples): extra blocks of the same launch count the NEXT
 // batch's contributions into the index counters (the next build skips its k_count)
+// The dense layers' Adam step handed from launch_mlp_update to launch_emb_update_touched
+// (same stream): it then runs in extra workgroups of the touched-row update launch.
+struct MlpDeferred {
+    float *p, *m, *v;          // p == nullptr: not deferred (launch_mlp_update launched it)
+    const float* slabs;        // reduced slab partials
+    int nslab;
+};
 hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, void* ws, float* emb, float* m,
                                      float* v, int32_t* row_step, int32_t* step, const ncf_hyper_t& h,
                                      hipStream_t st, const int32_t* next_users = nullptr,
-                                     const int32_t* next_items = nullptr, int64_t n_next = 0);
+                                     const int32_t* next_items = nullptr, int64_t n_next = 0,
+                                     const MlpDeferred* mlp = nullptr);
 // dense gradient of rows [row_begin, num_rows) into out (indexed from row_begin)
 hipError_t launch_emb_grad_dense(const ncf_shape_t& s, const WsLayout& L, void* ws, float* out, hipStream_t st,
                                   int64_t row_begin = 0);
@@ -328,7 +336,7 @@ hipError_t launch_mlp_update(const ncf_shape_t& s, const WsLayout& L, void* ws, 
                              const int32_t* step, const ncf_hyper_t& h, int nslab, const float* grad_in,
                              float* grad_out, bool do_update, int* nreg, hipStream_t st, bool want_reg = false,
                              int summary_nbce = -1, int summary_nmet = 0, float n_groups = 0.f,
-                             float* summary = nullptr);
+                             float* summary = nullptr, MlpDeferred* defer = nullptr);
 hipError_t launch_emb_reg(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, int64_t rows,
                           float lam, hipStream_t st);
 // scan_ahead: the same launch also runs the next batch's per-block key scan (k_scan_local<true>

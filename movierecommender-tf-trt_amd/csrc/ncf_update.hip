@@ -249,13 +249,91 @@ __global__ __launch_bounds__(kBlock) void k_row_step_fill(int32_t* __restrict__ 
 
 // Adam step t = *step + 1 on the touched rows, which were brought up to step t-1 before the
 // forward pass; records row_step[r] = t.
+struct L2Table {
+    int n;
+    int start[NCF_MAX_LAYERS];
+    int end[NCF_MAX_LAYERS];
+    float lam[NCF_MAX_LAYERS];
+};
+
+template <int OPT>
+__device__ inline void mlp_update_body(float* __restrict__ p, float* __restrict__ m, float* __restrict__ v, int P,
+                                       const float* __restrict__ slabs, int nslab, const float* __restrict__ grad_in,
+                                       float* __restrict__ grad_out, int do_update, int want_reg,
+                                       const int32_t* __restrict__ step, float lr, float b1, float b2, float eps,
+                                       const L2Table& l2t, float* __restrict__ part_reg, int blk) {
+    __shared__ float red[4];
+    const int i = blk * kBlock + threadIdx.x;
+    float reg = 0.0f;
+    if (i < P) {
+        float g = 0.0f;
+        if (nslab > 0) {
+            // fixed slab order → deterministic
+            int s = 0;
+            float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+            for (; s + 4 <= nslab; s += 4) {
+                a0 += slabs[(size_t)(s + 0) * P + i];
+                a1 += slabs[(size_t)(s + 1) * P + i];
+                a2 += slabs[(size_t)(s + 2) * P + i];
+                a3 += slabs[(size_t)(s + 3) * P + i];
+            }
+            for (; s < nslab; ++s) a0 += slabs[(size_t)s * P + i];
+            g = (a0 + a1) + (a2 + a3);
+        } else {
+            g = grad_in[i];
+        }
+        if (grad_out) grad_out[i] = g;
+        if (do_update || want_reg) {
+            float w = p[i];
+            float lam = 0.0f;
+            for (int l = 0; l < l2t.n; ++l)
+                if (i >= l2t.start[l] && i < l2t.end[l]) lam = l2t.lam[l];
+            if (lam != 0.0f) {
+                reg = lam * w * w;
+                g += 2.0f * lam * w;
+            }
+        }
+        if (do_update) {
+            float w = p[i];
+            if (OPT == NCF_OPT_ADAM) {
+                const int t = *step + 1;
+                const float lr_t = adam_lr_t(lr, b1, b2, t);
+                float mm = b1 * m[i] + (1.0f - b1) * g;
+                float vv = b2 * v[i] + (1.0f - b2) * (g * g);
+                w -= lr_t * mm / (sqrtf(vv) + eps);
+                m[i] = mm;
+                v[i] = vv;
+            } else {
+                w -= lr * g;
+            }
+            p[i] = w;
+        }
+    }
+    reg = block_sum_256(reg, red);
+    if (threadIdx.x == 0 && part_reg) part_reg[blk] = reg;
+}
+
 struct CountAhead {
-    int nupd;                  // blocks [0, nupd) update rows; blocks >= nupd count
+    int nupd;                  // blocks [0, nupd) update rows; [nupd, nupd + ncount) count
+    int ncount;
     const int32_t* users;      // next batch (m = 2 * n_next contributions)
     const int32_t* items;
     int64_t m;
     int32_t U, I;
     int32_t* cnt;
+};
+
+// the dense layers' Adam (k_mlp_update<ADAM>'s work) in blocks >= nupd + ncount of the same launch
+struct MlpTail {
+    int nblocks;               // 0: none
+    float *p, *m, *v;
+    int P;
+    const float* slabs;
+    int nslab;
+    const int32_t* step;
+    float lr, b1, b2, eps;
+    L2Table l2t;
+    float* part_reg;
 };
 
 __global__ __launch_bounds__(kBlock) void k_emb_adam_touched(float4* __restrict__ emb, float4* __restrict__ m4,
@@ -267,12 +345,18 @@ __global__ __launch_bounds__(kBlock) void k_emb_adam_touched(float4* __restrict_
                                                              const float4* __restrict__ gs,
                                                              int32_t* __restrict__ row_step, const int32_t* step,
                                                              float lr, float b1, float b2, float eps,
-                                                             CountAhead ca) {
+                                                             CountAhead ca, MlpTail mt) {
+    if ((int)blockIdx.x >= ca.nupd + ca.ncount) {
+        mlp_update_body<NCF_OPT_ADAM>(mt.p, mt.m, mt.v, mt.P, mt.slabs, mt.nslab, nullptr, nullptr, 1, 0, mt.step,
+                                      mt.lr, mt.b1, mt.b2, mt.eps, mt.l2t, mt.part_reg,
+                                      (int)blockIdx.x - ca.nupd - ca.ncount);
+        return;
+    }
     if ((int)blockIdx.x >= ca.nupd) {
         // extra blocks: count the NEXT batch's contributions (k_count's work) while this step's
         // rows stream; the counters are free here (the fill of this step's index emptied them)
         const int64_t first = (int64_t)(blockIdx.x - ca.nupd) * kBlock + threadIdx.x;
-        const int64_t cstride = (int64_t)(gridDim.x - ca.nupd) * kBlock;
+        const int64_t cstride = (int64_t)ca.ncount * kBlock;
         for (int64_t c = first; c < ca.m; c += cstride) {
             const int64_t i = c >> 1;
             const int id = (c & 1) ? ca.items[i] : ca.users[i];
@@ -452,12 +536,7 @@ __global__ __launch_bounds__(kBlock) void k_slab_partial(const float* __restrict
     part[(size_t)blockIdx.y * P + p] = (a0 + a1) + (a2 + a3);
 }
 
-struct L2Table {
-    int n;
-    int start[NCF_MAX_LAYERS];
-    int end[NCF_MAX_LAYERS];
-    float lam[NCF_MAX_LAYERS];
-};
+
 
 template <int OPT>
 __global__ __launch_bounds__(kBlock) void k_mlp_update(float* __restrict__ p, float* __restrict__ m,
@@ -466,55 +545,8 @@ __global__ __launch_bounds__(kBlock) void k_mlp_update(float* __restrict__ p, fl
                                                        float* __restrict__ grad_out, int do_update, int want_reg,
                                                        const int32_t* __restrict__ step, float lr, float b1, float b2,
                                                        float eps, L2Table l2t, float* __restrict__ part_reg) {
-    __shared__ float red[4];
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    float reg = 0.0f;
-    if (i < P) {
-        float g = 0.0f;
-        if (nslab > 0) {
-            // fixed slab order → deterministic
-            int s = 0;
-            float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-            for (; s + 4 <= nslab; s += 4) {
-                a0 += slabs[(size_t)(s + 0) * P + i];
-                a1 += slabs[(size_t)(s + 1) * P + i];
-                a2 += slabs[(size_t)(s + 2) * P + i];
-                a3 += slabs[(size_t)(s + 3) * P + i];
-            }
-            for (; s < nslab; ++s) a0 += slabs[(size_t)s * P + i];
-            g = (a0 + a1) + (a2 + a3);
-        } else {
-            g = grad_in[i];
-        }
-        if (grad_out) grad_out[i] = g;
-        if (do_update || want_reg) {
-            float w = p[i];
-            float lam = 0.0f;
-            for (int l = 0; l < l2t.n; ++l)
-                if (i >= l2t.start[l] && i < l2t.end[l]) lam = l2t.lam[l];
-            if (lam != 0.0f) {
-                reg = lam * w * w;
-                g += 2.0f * lam * w;
-            }
-        }
-        if (do_update) {
-            float w = p[i];
-            if (OPT == NCF_OPT_ADAM) {
-                const int t = *step + 1;
-                const float lr_t = adam_lr_t(lr, b1, b2, t);
-                float mm = b1 * m[i] + (1.0f - b1) * g;
-                float vv = b2 * v[i] + (1.0f - b2) * (g * g);
-                w -= lr_t * mm / (sqrtf(vv) + eps);
-                m[i] = mm;
-                v[i] = vv;
-            } else {
-                w -= lr * g;
-            }
-            p[i] = w;
-        }
-    }
-    reg = block_sum_256(reg, red);
-    if (threadIdx.x == 0 && part_reg) part_reg[blockIdx.x] = reg;
+    mlp_update_body<OPT>(p, m, v, P, slabs, nslab, grad_in, grad_out, do_update, want_reg, step, lr, b1, b2, eps, l2t,
+                         part_reg, (int)blockIdx.x);
 }
 
 // Per-group hit@k / dcg@k: the label's position in the stable descending
@@ -721,7 +753,7 @@ hipError_t launch_row_step_fill(int32_t* row_step, int64_t R, const int32_t* ste
 hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, void* ws, float* emb, float* m,
                                      float* v, int32_t* row_step, int32_t* step, const ncf_hyper_t& h,
                                      hipStream_t st, const int32_t* next_users, const int32_t* next_items,
-                                     int64_t n_next) {
+                                     int64_t n_next, const MlpDeferred* mlp) {
     const uint32_t w4 = (uint32_t)(s.row_width / 4);
     const uint32_t n4 = (uint32_t)(s.num_rows * w4);
     const int32_t* offs = at<int32_t>(ws, L.offs);
@@ -730,14 +762,21 @@ hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, vo
     const int64_t R = s.num_rows;
     if (h.optimizer == NCF_OPT_ADAM) {
         const unsigned nupd = row_grid(R < 2 * L.max_batch ? R : 2 * L.max_batch, w4, NCF_TOUCHED_GRID_MAX);
-        CountAhead ca{(int)nupd, next_users, next_items, next_users ? 2 * n_next : 0, s.num_users, s.num_items,
+        const int64_t mc = next_users ? 2 * n_next : 0;
+        const unsigned ncount = mc > 0 ? (unsigned)((mc + kBlock - 1) / kBlock < 512 ? (mc + kBlock - 1) / kBlock
+                                                                                      : 512) : 0u;
+        CountAhead ca{(int)nupd, (int)ncount, next_users, next_items, mc, s.num_users, s.num_items,
                       at<int32_t>(ws, L.cnt)};
-        const unsigned ncount = ca.m > 0 ? (unsigned)((ca.m + kBlock - 1) / kBlock < 512 ? (ca.m + kBlock - 1) / kBlock
-                                                                                             : 512) : 0u;
-        launch(k_emb_adam_touched, nupd + ncount, kBlock, 0, st,
+        MlpTail mt{};
+        if (mlp) {
+            mt = MlpTail{(s.mlp_params + kBlock - 1) / kBlock, mlp->p, mlp->m, mlp->v, s.mlp_params, mlp->slabs,
+                         mlp->nslab, step, h.lr, h.beta_1, h.beta_2, h.epsilon, make_l2_table(s, h),
+                         at<float>(ws, L.part_reg) + kUpdateGrid};
+        }
+        launch(k_emb_adam_touched, nupd + ncount + (unsigned)mt.nblocks, kBlock, 0, st,
                (float4*)emb, (float4*)m, (float4*)v, w4, at<const int32_t>(ws, L.touched),
                at<const int32_t>(ws, L.nuniq), offs, list, gs, row_step, (const int32_t*)step, h.lr, h.beta_1, h.beta_2,
-               h.epsilon, ca);
+               h.epsilon, ca, mt);
     } else
         launch(k_emb_sgd_hot, kUpdateGrid, kBlock, 0, st, (float4*)emb, n4, w4, offs, list, gs, h.lr);
     return hipGetLastError();
@@ -784,7 +823,8 @@ hipError_t launch_emb_reg(const ncf_shape_t& s, const WsLayout& L, void* ws, con
 hipError_t launch_mlp_update(const ncf_shape_t& s, const WsLayout& L, void* ws, float* mlp, float* m, float* v,
                              const int32_t* step, const ncf_hyper_t& h, int nslab, const float* grad_in,
                              float* grad_out, bool do_update, int* nreg, hipStream_t st, bool want_reg,
-                             int summary_nbce, int summary_nmet, float n_groups, float* summary) {
+                             int summary_nbce, int summary_nmet, float n_groups, float* summary,
+                             MlpDeferred* defer) {
     const int P = s.mlp_params;
     const int grid = (P + kBlock - 1) / kBlock;
     float* part = at<float>(ws, L.part_reg) + kUpdateGrid;
@@ -808,6 +848,13 @@ hipError_t launch_mlp_update(const ncf_shape_t& s, const WsLayout& L, void* ws, 
         hipError_t e = launch_summary(L, ws, summary_nbce, summary_nmet, n_groups, 0, 0, summary, st);
         if (e != hipSuccess) return e;
     }
+    if (defer && h.optimizer == NCF_OPT_ADAM && do_update && !grad_out && !want_reg && nslab > 0) {
+        // the caller runs the Adam step of the dense layers inside the touched-row update launch
+        *defer = MlpDeferred{mlp, m, v, slabs, nslab};
+        *nreg = t.n > 0 ? grid : 0;
+        return hipGetLastError();
+    }
+    if (defer) defer->p = nullptr;
     if (h.optimizer == NCF_OPT_ADAM)
         launch(k_mlp_update<NCF_OPT_ADAM>, grid, kBlock, 0, st, mlp, m, v, P, slabs, nslab, grad_in,
                                                             grad_out, do_update ? 1 : 0, want_reg ? 1 : 0, step,
