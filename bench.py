@@ -19,8 +19,9 @@ replicated`` keeps whole tables on every rank (reduce-scatter of the dense
 embedding gradient, sharded Adam, all-gather).
 
 Prints ONE JSON line (rank 0).  ``roofline`` is the embedding scatter-add +
-Adam sweep (the dominant, HBM-bound kernel), timed live with HIP events on
-the launch stream; ``cpu_baseline`` times the numpy CPU restatement
+Adam (the HBM-bound kernel the north star's >= 50 % target names) and
+``roofline_fwd_bwd`` the fused forward/backward (the step's longest kernel,
+MFMA-bound), both timed live with HIP events on the launch stream; ``cpu_baseline`` times the numpy CPU restatement
 (oracle/) of the same step on a bounded sample, rank 0, N=1 only.
 """
 
