@@ -80,6 +80,11 @@ def parse():
                          "(per-rank compute of the N-GPU step without its all-reduce; a diagnostic, not a result)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse N ranks sharing one GPU (correctness only, not a measurement)")
+    ap.add_argument("--time-every", type=int, default=10,
+                    help="kernel durations: HIP events on every k-th step of the timed region (events in the "
+                         "dispatch packets lengthen the step they ride on)")
+    ap.add_argument("--no-kernel-timing", action="store_true",
+                    help="diagnostic: no HIP events on the profiled launches (the roofline fields are then null)")
     ap.add_argument("--dp", default="auto", choices=["auto", "user", "sharded", "replicated"],
                     help="multi-GPU layout (auto: single engine at N=1, user-partitioned at N>1)")
     return ap.parse_args()
@@ -448,17 +453,25 @@ def main():
     for i in range(args.warmup):
         step(i)
     barrier()
-    # timed region.  The profiled launch groups carry HIP events in their dispatch packets
-    # (hipExtLaunchKernel): per-kernel durations with no marker packets added to the stream.
-    N.profile_enable([N.K_EMB_UPDATE, N.K_FWD_BWD, N.K_INDEX, N.K_SAMPLE, N.K_CATCHUP], 2 * args.steps)
     eng.flush() if hasattr(eng, "flush") else None
     barrier()
+    # timed region.  The profiled launch groups carry HIP events in their dispatch packets
+    # (hipExtLaunchKernel): per-kernel durations with no marker packets added to the stream.
+    if not args.no_kernel_timing:
+        N.profile_enable([N.K_EMB_UPDATE, N.K_FWD_BWD, N.K_INDEX, N.K_SAMPLE, N.K_CATCHUP], 2 * args.steps)
     t0 = time.perf_counter()
+    every = max(1, min(args.time_every, args.steps // 5))   # at least 5 timed steps
     for i in range(args.steps):
+        if not args.no_kernel_timing and every > 1:
+            N.profile_pause(i % every != 0)
         step(args.warmup + i)
+    if not args.no_kernel_timing:
+        N.profile_pause(True)    # the end-of-region flush is not a step's catch-up
     if hasattr(eng, "flush"):
         eng.flush()   # deferred decay settled inside the timed region: the table ends in the dense state
     barrier()
+    if not args.no_kernel_timing:
+        N.profile_pause(False)
     elapsed = time.perf_counter() - t0
     ms_emb, nl = N.profile_read(N.K_EMB_UPDATE)
     ms_fb, nfb = N.profile_read(N.K_FWD_BWD)
@@ -471,8 +484,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     value = args.steps * B * world / elapsed
-    kern_ms = ms_emb / max(nl, 1)
-    fb_ms = ms_fb / max(nfb, 1)
+    kern_ms = ms_emb / nl if nl else float("nan")
+    fb_ms = ms_fb / nfb if nfb else float("nan")
     fb_flops = fwd_bwd_flops(cfg) * B
     fb_bytes = fwd_bwd_bytes(eng.shape, B)
     train_exchange = dp.last_exchange if mode == "sharded" else None
@@ -483,9 +496,15 @@ def main():
         nbytes = emb_update_bytes(eng.shape, B, touched_rows=touched)
         if sampler is None:
             nbytes += 2 * B * (4 + 8)   # the launch also counts the next batch: id reads + counter atomics
+    elif mode == "user":
+        # two launches per step: the own users' scatter-add + Adam over the B user contributions
+        # (ncf_update_rows), then Adam over the item rows with the all-reduced dense gradient
+        # (ncf_apply_update); bytes per launch = the step's bytes / 2, time per launch = the average
+        Uloc, W = eng.num_users, eng.shape.row_width
+        own = 24 * Uloc * W + B * W * 4 + B * 4 + (Uloc + 1) * 4
+        nbytes = (own + 28 * (eng.num_rows - Uloc) * W) / 2.0
     else:
-        nbytes = emb_update_bytes(eng.shape, B, dense_rows=(dp.row_count if mode == "replicated" else
-                                                            eng.num_rows if mode == "user" else None))
+        nbytes = emb_update_bytes(eng.shape, B, dense_rows=(dp.row_count if mode == "replicated" else None))
     achieved = nbytes / (kern_ms * 1e-3) / 1e9
 
     # HR@10 on a synthetic validation set (1 positive + 99 sampled items per user), per rank
@@ -545,10 +564,16 @@ def main():
                                                     + ("; its launch also counts the next batch's index "
                                                        "contributions)" if sampler is None else ")")
                                                     if getattr(eng, "lazy", False) else
+                                                    "embedding Adam, 2 launches per step (k_emb_update: own-user "
+                                                    "rows with their scatter-add; item rows with the all-reduced "
+                                                    "gradient)" if mode == "user" else
                                                     "embedding scatter-add + Adam sweep (k_emb_update)"),
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "algorithmic_bytes_per_launch": nbytes, "avg_launch_ms": round(kern_ms, 5),
+                         "launches_per_step": round(nl / len(range(0, args.steps, every)), 2),
+                         "timed_steps": "every %d-th step of the timed region (HIP events in the dispatch packets)"
+                                        % every,
                          "traffic_source": "rocprofv3 --pmc FETCH_SIZE(x2 gfx950) + WRITE_SIZE, "
                                            "profiles/traffic_emb_update.json (per launch)"},
             "roofline_fwd_bwd": {"bound": "mfma", "kernel": {

@@ -360,6 +360,11 @@ int ncf_sample_batch(const ncf_sampler_data_t* data, const int32_t* order, int64
                              * (NCF_K_EMB_UPDATE then times the touched-row update only) */
 int ncf_profile_enable(int32_t kernel_mask, int32_t capacity);
 int ncf_profile_read(int32_t kernel_id, double* total_ms, int64_t* launches);
+/* paused != 0: launches carry no events (and take no slots) until resumed; the
+ * slots already taken are kept.  bench.py times a sample of the steps of its
+ * timed region this way, because the events in the dispatch packets lengthen a
+ * step (measured 16 us on the config-C step). */
+int ncf_profile_pause(int32_t paused);
 
 #ifdef __cplusplus
 }

@@ -76,6 +76,7 @@ struct ProfSlot {
 };
 struct Profiler {
     uint32_t mask = 0;  // bit k set: time launch group k
+    bool paused = false;
     ProfSlot slot[16];
 };
 thread_local Profiler g_prof;
@@ -83,7 +84,7 @@ thread_local Profiler g_prof;
 // A profiled launch group's events ride on its kernels' dispatch packets (ncf::launch).
 void prof_begin(int k, hipStream_t) {
     ProfSlot& p = g_prof.slot[k & 15];
-    if (!(g_prof.mask >> k & 1u) || p.used >= p.start.size()) return;
+    if (g_prof.paused || !(g_prof.mask >> k & 1u) || p.used >= p.start.size()) return;
     ncf::LaunchEvents& ev = ncf::launch_events();
     ev.start = p.start[p.used];
     ev.stop = p.stop[p.used];
@@ -91,7 +92,7 @@ void prof_begin(int k, hipStream_t) {
 }
 void prof_end(int k, hipStream_t) {
     ProfSlot& p = g_prof.slot[k & 15];
-    if (!(g_prof.mask >> k & 1u) || p.used >= p.start.size()) return;
+    if (g_prof.paused || !(g_prof.mask >> k & 1u) || p.used >= p.start.size()) return;
     ncf::LaunchEvents& ev = ncf::launch_events();
     if (ev.launches > 0) ++p.used;
     ev = ncf::LaunchEvents{};
@@ -549,6 +550,13 @@ static int forward_backward_rows(const ncf_shape_t* s, const ncf_model_t* model,
     if (int r = run_fb(*s, L, model, h, users, items, labels, n, ws, probs_out, &fb, st)) return r;
     // the index (side stream) must be complete before the side stream takes the dense tail
     if (int r = index_join(st, fb)) return r;
+    if (side_stream_mode() == 0 && ncf::part_tail_foldable(*s, *h, fb.nslab)) {
+        // L2 off, one stream: slab partials + summary, then the dense embedding gradient with the
+        // dense-layer gradient in extra workgroups: 2 launches instead of 4
+        hipError_t e = ncf::launch_part_tail(*s, L, ws, emb_grad, grad_row_begin, mlp_grad, fb.nslab, fb.nbce, fb.nmet,
+                                             fb.n_groups, summary, st);
+        return hip_check(e, "gradient tail");
+    }
     SideStream* ss = nullptr;
     hipStream_t st2 = fork_side(st, &ss);
     int nreg_mlp = 0, nreg_emb = 0;
@@ -673,6 +681,17 @@ int ncf_apply_update(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* opti
     ncf::WsLayout L;
     if (int r = check_ws(*s, 1, ws, ws_bytes, &L)) return r;
     hipStream_t st = (hipStream_t)stream;
+    if (row_count > 0 && side_stream_mode() == 0 && h->l2[0] == 0.0f && ncf::part_tail_foldable(*s, *h, 1 << 30)) {
+        // L2 off, one stream: the dense layers' step runs in extra workgroups of the row update
+        prof_begin(NCF_K_EMB_UPDATE, st);
+        hipError_t e = ncf::launch_apply_fused(*s, model->emb + row_begin * s->row_width, optim->emb_m, optim->emb_v,
+                                               emb_grad, row_count, model->mlp, optim->mlp_m, optim->mlp_v, mlp_grad,
+                                               optim->step, *h, st);
+        prof_end(NCF_K_EMB_UPDATE, st);
+        if (e != hipSuccess) return hip_check(e, "embedding + dense update");
+        e = ncf::launch_stats(L, ws, summary, 0, 0, h->inv_batch, stats, optim->step, true, st);
+        return hip_check(e, "stats");
+    }
     SideStream* ss = nullptr;
     hipStream_t st2 = fork_side(st, &ss);
     int nreg_mlp = 0;
@@ -952,6 +971,7 @@ int ncf_score_topk(const ncf_shape_t* s, const ncf_model_t* model, const int32_t
 
 int ncf_profile_enable(int32_t kernel_mask, int32_t capacity) {
     g_prof.mask = kernel_mask < 0 ? 0u : (uint32_t)kernel_mask;
+    g_prof.paused = false;
     for (int k = 0; k < 16; ++k) {
         ProfSlot& p = g_prof.slot[k];
         p.used = 0;
@@ -965,6 +985,11 @@ int ncf_profile_enable(int32_t kernel_mask, int32_t capacity) {
             p.stop.push_back(b);
         }
     }
+    return 0;
+}
+
+int ncf_profile_pause(int32_t paused) {
+    g_prof.paused = paused != 0;
     return 0;
 }
 

@@ -329,6 +329,18 @@ hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, vo
 // dense gradient of rows [row_begin, num_rows) into out (indexed from row_begin)
 hipError_t launch_emb_grad_dense(const ncf_shape_t& s, const WsLayout& L, void* ws, float* out, hipStream_t st,
                                   int64_t row_begin = 0);
+// Launch folding of the data-parallel gradient/update tails (every L2 factor zero and the slab
+// count large enough for the two-level reduction): launch_part_tail = slab partials + batch
+// summary, then dense embedding gradient of rows [row_begin, num_rows) + dense-layer gradient in
+// one launch; launch_apply_fused = table-row update with a dense gradient + dense-layer update in
+// one launch.  Bitwise the unfolded sequences.
+bool part_tail_foldable(const ncf_shape_t& s, const ncf_hyper_t& h, int nslab);
+hipError_t launch_part_tail(const ncf_shape_t& s, const WsLayout& L, void* ws, float* emb_grad, int64_t row_begin,
+                            float* mlp_grad, int nslab, int nbce, int nmet, float n_groups, float* summary,
+                            hipStream_t st);
+hipError_t launch_apply_fused(const ncf_shape_t& s, float* emb, float* m, float* v, const float* emb_grad,
+                              int64_t rows, float* mlp, float* mlp_m, float* mlp_v, const float* mlp_grad,
+                              const int32_t* step, const ncf_hyper_t& h, hipStream_t st);
 // mlp: reduce slabs (if nslab > 0) or read grad_in; optionally write grad_out; optionally update
 // summary_nbce >= 0: the first-level slab reduction also writes the batch summary (what
 // launch_summary(L, ws, summary_nbce, summary_nmet, n_groups, 0, 0, summary) does)

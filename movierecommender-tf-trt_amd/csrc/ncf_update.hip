@@ -98,20 +98,20 @@ __device__ __forceinline__ void decay4(float4& m, float4& v, float b1, float b2)
     v.x = b2 * v.x + 0.0f; v.y = b2 * v.y + 0.0f; v.z = b2 * v.z + 0.0f; v.w = b2 * v.w + 0.0f;
 }
 
+// blocks blk of nblk stride over the table's float4 elements
 template <int OPT, int SRC, bool L2>
-__global__ __launch_bounds__(kBlock) void k_emb_update(float4* __restrict__ emb, float4* __restrict__ m4,
-                                                       float4* __restrict__ v4, uint32_t n4, uint32_t w4,
-                                                       const int32_t* __restrict__ offs,
-                                                       const int32_t* __restrict__ list,
-                                                       const float4* __restrict__ gs,
-                                                       const float4* __restrict__ dgrad,
-                                                       const int32_t* __restrict__ step, float lr, float b1,
-                                                       float b2, float eps, float lam, float* __restrict__ part_reg) {
+__device__ __forceinline__ void emb_update_body(float4* __restrict__ emb, float4* __restrict__ m4,
+                                                float4* __restrict__ v4, uint32_t n4, uint32_t w4,
+                                                const int32_t* __restrict__ offs, const int32_t* __restrict__ list,
+                                                const float4* __restrict__ gs, const float4* __restrict__ dgrad,
+                                                const int32_t* __restrict__ step, float lr, float b1, float b2,
+                                                float eps, float lam, float* __restrict__ part_reg, uint32_t blk,
+                                                uint32_t nblk) {
     __shared__ float red[4];
     const int t = *step + 1;
     const float lr_t = (OPT == NCF_OPT_ADAM) ? adam_lr_t(lr, b1, b2, t) : lr;
     float reg = 0.0f;
-    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n4; e += gridDim.x * blockDim.x) {
+    for (uint32_t e = blk * blockDim.x + threadIdx.x; e < n4; e += nblk * blockDim.x) {
         float4 p = emb[e];
         float4 g;
         if (SRC == kGradSparse) {
@@ -150,8 +150,21 @@ __global__ __launch_bounds__(kBlock) void k_emb_update(float4* __restrict__ emb,
     }
     if (L2) {
         reg = block_sum_256(reg, red);
-        if (threadIdx.x == 0) part_reg[blockIdx.x] = reg;
+        if (threadIdx.x == 0) part_reg[blk] = reg;
     }
+}
+
+template <int OPT, int SRC, bool L2>
+__global__ __launch_bounds__(kBlock) void k_emb_update(float4* __restrict__ emb, float4* __restrict__ m4,
+                                                       float4* __restrict__ v4, uint32_t n4, uint32_t w4,
+                                                       const int32_t* __restrict__ offs,
+                                                       const int32_t* __restrict__ list,
+                                                       const float4* __restrict__ gs,
+                                                       const float4* __restrict__ dgrad,
+                                                       const int32_t* __restrict__ step, float lr, float b1,
+                                                       float b2, float eps, float lam, float* __restrict__ part_reg) {
+    emb_update_body<OPT, SRC, L2>(emb, m4, v4, n4, w4, offs, list, gs, dgrad, step, lr, b1, b2, eps, lam, part_reg,
+                                  blockIdx.x, gridDim.x);
 }
 
 #ifndef NCF_CATCHUP_P_ONLY
@@ -445,12 +458,13 @@ __global__ __launch_bounds__(kBlock) void k_emb_reg(const float4* __restrict__ e
     if (threadIdx.x == 0) part_reg[blockIdx.x] = reg;
 }
 
-// Dense embedding gradient (data-parallel path): every row written.
-__global__ __launch_bounds__(kBlock) void k_emb_grad_dense(float4* __restrict__ out, uint32_t n4, uint32_t w4,
-                                                           const int32_t* __restrict__ offs,
-                                                           const int32_t* __restrict__ list,
-                                                           const float4* __restrict__ gs) {
-    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n4; e += gridDim.x * blockDim.x) {
+// Dense embedding gradient (data-parallel path): every row written.  Blocks stride over the
+// elements with `nblk` blocks (the folded launch below adds blocks of other work after them).
+__device__ __forceinline__ void emb_grad_dense_body(float4* __restrict__ out, uint32_t n4, uint32_t w4,
+                                                    const int32_t* __restrict__ offs,
+                                                    const int32_t* __restrict__ list,
+                                                    const float4* __restrict__ gs, uint32_t blk, uint32_t nblk) {
+    for (uint32_t e = blk * blockDim.x + threadIdx.x; e < n4; e += nblk * blockDim.x) {
         const uint32_t r = e / w4;
         const uint32_t q = e - r * w4;
         const int o = offs[r];
@@ -468,6 +482,54 @@ __global__ __launch_bounds__(kBlock) void k_emb_grad_dense(float4* __restrict__ 
         for (; j < c; ++j) g = f4add(g, gs[(size_t)list[o + j] * w4 + q]);
         out[e] = g;
     }
+}
+
+__global__ __launch_bounds__(kBlock) void k_emb_grad_dense(float4* __restrict__ out, uint32_t n4, uint32_t w4,
+                                                           const int32_t* __restrict__ offs,
+                                                           const int32_t* __restrict__ list,
+                                                           const float4* __restrict__ gs) {
+    emb_grad_dense_body(out, n4, w4, offs, list, gs, blockIdx.x, gridDim.x);
+}
+
+// The data-parallel gradient tail in one launch: blocks [0, ngrad) write the dense embedding
+// gradient, blocks >= ngrad reduce the first-level slab partials into the dense-layer gradient
+// (k_mlp_update's work with no update and no L2; same order, bitwise).
+__global__ __launch_bounds__(kBlock) void k_emb_grad_dense_mlp(float4* __restrict__ out, uint32_t n4, uint32_t w4,
+                                                               const int32_t* __restrict__ offs,
+                                                               const int32_t* __restrict__ list,
+                                                               const float4* __restrict__ gs, uint32_t ngrad,
+                                                               int P, const float* __restrict__ slabs, int nslab,
+                                                               float* __restrict__ mlp_grad) {
+    if (blockIdx.x >= ngrad) {
+        const L2Table none{};
+        mlp_update_body<NCF_OPT_ADAM>(nullptr, nullptr, nullptr, P, slabs, nslab, nullptr, mlp_grad, 0, 0, nullptr,
+                                      0.f, 0.f, 0.f, 0.f, none, nullptr, (int)(blockIdx.x - ngrad));
+        return;
+    }
+    emb_grad_dense_body(out, n4, w4, offs, list, gs, blockIdx.x, ngrad);
+}
+
+// Replicated-row Adam/SGD with the all-reduced gradient in one launch: blocks [0, nupd) sweep the
+// table rows with their dense gradient (k_emb_update<OPT, kGradDense, false>'s work), blocks
+// >= nupd step the dense layers with theirs (k_mlp_update's work, no L2).  Used only with every
+// L2 factor zero; bitwise the two separate launches.
+template <int OPT>
+__global__ __launch_bounds__(kBlock) void k_emb_update_mlp(float4* __restrict__ emb, float4* __restrict__ m4,
+                                                           float4* __restrict__ v4, uint32_t n4, uint32_t w4,
+                                                           const float4* __restrict__ dgrad, uint32_t nupd,
+                                                           float* __restrict__ mp, float* __restrict__ mm,
+                                                           float* __restrict__ mv, int P,
+                                                           const float* __restrict__ mlp_grad,
+                                                           const int32_t* __restrict__ step, float lr, float b1,
+                                                           float b2, float eps) {
+    if (blockIdx.x >= nupd) {
+        const L2Table none{};
+        mlp_update_body<OPT>(mp, mm, mv, P, nullptr, 0, mlp_grad, nullptr, 1, 0, step, lr, b1, b2, eps, none, nullptr,
+                             (int)(blockIdx.x - nupd));
+        return;
+    }
+    emb_update_body<OPT, kGradDense, false>(emb, m4, v4, n4, w4, nullptr, nullptr, nullptr, dgrad, step, lr, b1, b2,
+                                            eps, 0.f, nullptr, blockIdx.x, nupd);
 }
 
 // Compact gradient of a row-sharded plan: out[u] = sum of unique row u's contributions
@@ -789,6 +851,49 @@ hipError_t launch_emb_grad_dense(const ncf_shape_t& s, const WsLayout& L, void* 
     if (n4 == 0) return hipSuccess;
     launch(k_emb_grad_dense, kUpdateGrid, kBlock, 0, st, (float4*)out, n4, w4, at<int32_t>(ws, L.offs) + row_begin,
                                                      at<int32_t>(ws, L.list), at<const float4>(ws, L.gs));
+    return hipGetLastError();
+}
+
+bool part_tail_foldable(const ncf_shape_t& s, const ncf_hyper_t& h, int nslab) {
+    return h.l2[0] == 0.0f && make_l2_table(s, h).n == 0 && nslab > 2 * kSlabSplit;
+}
+
+hipError_t launch_part_tail(const ncf_shape_t& s, const WsLayout& L, void* ws, float* emb_grad, int64_t row_begin,
+                            float* mlp_grad, int nslab, int nbce, int nmet, float n_groups, float* summary,
+                            hipStream_t st) {
+    const int P = s.mlp_params;
+    const int gridp = (P + kBlock - 1) / kBlock;
+    const int per = (nslab + kSlabSplit - 1) / kSlabSplit;
+    const int nch = (nslab + per - 1) / per;
+    float* sp = at<float>(ws, L.slab_part);
+    SummaryArgs sa{summary, at<float>(ws, L.part_bce), at<float>(ws, L.part_hit), at<float>(ws, L.part_dcg), nbce,
+                   nmet, n_groups};
+    launch(k_slab_partial, dim3(gridp + 1, nch), kBlock, 0, st, at<const float>(ws, L.slabs), P, nslab, per, sp, sa);
+    const uint32_t w4 = (uint32_t)(s.row_width / 4);
+    const uint32_t n4 = (uint32_t)((s.num_rows - row_begin) * w4);
+    const uint32_t ngrad = n4 ? (uint32_t)kUpdateGrid : 0u;
+    launch(k_emb_grad_dense_mlp, ngrad + (uint32_t)gridp, kBlock, 0, st, (float4*)emb_grad, n4, w4,
+           at<int32_t>(ws, L.offs) + row_begin, at<int32_t>(ws, L.list), at<const float4>(ws, L.gs), ngrad, P,
+           (const float*)sp, nch, mlp_grad);
+    return hipGetLastError();
+}
+
+hipError_t launch_apply_fused(const ncf_shape_t& s, float* emb, float* m, float* v, const float* emb_grad,
+                              int64_t rows, float* mlp, float* mlp_m, float* mlp_v, const float* mlp_grad,
+                              const int32_t* step, const ncf_hyper_t& h, hipStream_t st) {
+    const uint32_t w4 = (uint32_t)(s.row_width / 4);
+    const uint32_t n4 = (uint32_t)(rows * w4);
+    const int P = s.mlp_params;
+    const unsigned gridp = (unsigned)((P + kBlock - 1) / kBlock);
+    const uint32_t nupd = n4 ? (uint32_t)kUpdateGrid : 0u;
+    if (h.optimizer == NCF_OPT_ADAM)
+        launch(k_emb_update_mlp<NCF_OPT_ADAM>, nupd + gridp, kBlock, 0, st, (float4*)emb, (float4*)m, (float4*)v, n4,
+               w4, (const float4*)emb_grad, nupd, mlp, mlp_m, mlp_v, P, mlp_grad, step, h.lr, h.beta_1, h.beta_2,
+               h.epsilon);
+    else
+        launch(k_emb_update_mlp<NCF_OPT_SGD>, nupd + gridp, kBlock, 0, st, (float4*)emb, (float4*)m, (float4*)v, n4,
+               w4, (const float4*)emb_grad, nupd, mlp, mlp_m, mlp_v, P, mlp_grad, step, h.lr, h.beta_1, h.beta_2,
+               h.epsilon);
     return hipGetLastError();
 }
 

@@ -65,8 +65,8 @@ def _batch(shape, B, group, seed, dup_items=None):
     return users.astype(np.int32), items.astype(np.int32), y.astype(np.float32)
 
 
-def _engine(shape, w, **kw):
-    eng = NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=4096, **kw)
+def _engine(shape, w, max_batch=4096, **kw):
+    eng = NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=max_batch, **kw)
     eng.set_keras_weights(w)
     return eng
 
@@ -156,18 +156,48 @@ def test_clipped_samples_have_zero_gradient():
     assert grads[2][0].item() == pytest.approx(O.bce_per_sample(p, y).sum(), rel=1e-5)
 
 
-def test_apply_update_equals_train_step():
+@pytest.mark.parametrize("batch", [512, 8192])
+def test_apply_update_equals_train_step(batch):
+    """forward_backward + apply_update (the data-parallel split of a step) is bitwise the fused
+    train_step.  At batch 8192 the fused kernel writes more than 2 x kSlabSplit slabs, so the
+    folded tails run (slab partials + summary, dense embedding gradient + dense-layer gradient
+    in one launch; row update + dense-layer Adam in one launch)."""
     shape = O.NCFShape(200, 150, [128, 64, 32, 16], 64)
     w = _weights(shape, 7)
-    a = _engine(shape, w)
-    b = _engine(shape, w)
-    users, items, y = _batch(shape, 512, 4, 8)
+    a = _engine(shape, w, max_batch=batch)
+    b = _engine(shape, w, max_batch=batch)
+    users, items, y = _batch(shape, batch, 4, 8)
     a.train_step(users, items, y, group=4, k=2)
     grads = b.alloc_grads()
-    b.forward_backward(users, items, y, group=4, k=2, inv_batch=1.0 / 512, grads=grads)
-    b.apply_update(grads, inv_batch=1.0 / 512)
+    b.forward_backward(users, items, y, group=4, k=2, inv_batch=1.0 / batch, grads=grads)
+    b.apply_update(grads, inv_batch=1.0 / batch)
+    sa, sb = NCFEngine.read_stats(a.stats), NCFEngine.read_stats(b.stats)
+    assert sa["loss"] == sb["loss"] and sa["hr"] == sb["hr"] and sa["steps"] == sb["steps"]
     assert torch.equal(a.emb, b.emb) and torch.equal(a.mlp, b.mlp)
     assert torch.equal(a.emb_m, b.emb_m) and torch.equal(a.emb_v, b.emb_v)
+
+
+def test_user_partitioned_split_equals_train_step():
+    """The user-partitioned step at world 1 (forward_backward_part -> update_rows of the user rows
+    -> apply_update of the item rows and dense layers), at a batch where every folded tail
+    runs, is bitwise the single-device train_step."""
+    shape = O.NCFShape(3000, 700, [128, 64, 32, 16], 64)
+    w = _weights(shape, 9)
+    B, U = 8192, shape.num_users
+    a = _engine(shape, w, max_batch=B)
+    b = _engine(shape, w, max_batch=B)
+    grads = (torch.zeros(shape.num_items, b.row_width, device="cuda"), torch.zeros(b.mlp_params, device="cuda"),
+             torch.zeros(8, device="cuda"))
+    for s in range(3):
+        users, items, y = _batch(shape, B, 4, 60 + s)
+        a.train_step(users, items, y, group=4, k=2)
+        u, it, yy = (torch.from_numpy(x).cuda() for x in (users, items, y))
+        b.forward_backward_part(u, it, yy, group=4, k=2, inv_batch=1.0 / B, shared_row_begin=U, grads=grads)
+        b.update_rows(0, U, 1.0 / B)
+        b.apply_update(grads, 1.0 / B, rows=(U, shape.num_items), moments_by_row=True)
+    torch.cuda.synchronize()
+    for x, z in ((a.emb, b.emb), (a.mlp, b.mlp), (a.emb_m, b.emb_m), (a.emb_v, b.emb_v), (a.mlp_v, b.mlp_v)):
+        assert torch.equal(x, z)
 
 
 def test_rank_and_metrics_kats():
