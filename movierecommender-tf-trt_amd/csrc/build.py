@@ -42,7 +42,9 @@ def build(force=False, verbose=False, defines=(), out=None):
 
     def compile_one(src):
         obj = os.path.join(obj_dir, src.replace(".hip", ".o"))
-        cmd = ([HIPCC] + CFLAGS + EXTRA.get(src, []) + ["-D" + d for d in defines] +
+        # NCF_EXTRA_<SOURCE STEM>: extra compiler flags of one source (experiment variants)
+        env_extra = os.environ.get("NCF_EXTRA_" + src.replace(".hip", "").upper(), "").split()
+        cmd = ([HIPCC] + CFLAGS + EXTRA.get(src, []) + env_extra + ["-D" + d for d in defines] +
                ["-c", os.path.join(HERE, src), "-o", obj])
         if verbose:
             print(" ".join(cmd))

@@ -72,13 +72,16 @@ template <int MODE>
 __global__ __launch_bounds__(kBlock) void k_count(KeySrc ks, int64_t m, int32_t* __restrict__ cnt, int32_t* heavy_n,
                                                   int32_t* err) {
     if (blockIdx.x == 0 && threadIdx.x == 0) *heavy_n = 0;
-    for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < m; c += (int64_t)gridDim.x * blockDim.x) {
-        bool ok;
-        const int key = contrib_key<MODE>(c, ks, &ok);
-        if (ok)
-            atomicAdd(&cnt[key], 1);
-        else
-            atomicOr(err, 1);
+    const int64_t gstride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t cb = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); cb < m; cb += gstride) {
+        const int64_t c = cb + (threadIdx.x & 63);
+        bool ok = false;
+        int key = 0;
+        if (c < m) {
+            key = contrib_key<MODE>(c, ks, &ok);
+            if (!ok) atomicOr(err, 1);
+        }
+        wave_run_count(cnt, key, ok);
     }
 }
 
@@ -167,16 +170,34 @@ __global__ __launch_bounds__(kBlock) void k_fill(KeySrc ks, int64_t m, int32_t* 
             }
         }
     }
-    for (int64_t c = gt; c < m; c += gstride) {
-        bool ok;
-        const int key = contrib_key<MODE>(c, ks, &ok);
-        if constexpr (UNIQ) {
-            const int u = ok ? po.uloc[key] + upre[key / kScanBlock] : -1;
-            ((c & 1) ? po.cid_i : po.cid_u)[c >> 1] = u;
+    // Contributions a wave at a time (lane l takes c = base + l).  Equal keys two lanes apart
+    // (a user group's samples: c = 2i, 2i+2, ...) form runs; the run's head takes all of its
+    // slots with one atomic and hands them out, so a group's user contributions do not queue on
+    // one counter.  Slot order within a key does not matter: the lists are sorted afterwards.
+    const int lane = threadIdx.x & 63;
+    const uint64_t par = (lane & 1) ? 0xAAAAAAAAAAAAAAAAull : 0x5555555555555555ull;
+    const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+    for (int64_t cb = gt - lane; cb < m; cb += gstride) {
+        const int64_t c = cb + lane;
+        bool ok = false;
+        int key = 0;
+        if (c < m) {
+            key = contrib_key<MODE>(c, ks, &ok);
+            if constexpr (UNIQ) {
+                const int u = ok ? po.uloc[key] + upre[key / kScanBlock] : -1;
+                ((c & 1) ? po.cid_i : po.cid_u)[c >> 1] = u;
+            }
         }
-        if (!ok) continue;
-        const int slot = atomicSub(&cnt[key], 1) - 1;
-        list[local[key] + pre[key / kScanBlock] + slot] = (int)c;
+        const int kk = ok ? key : -2 - lane;                 // inactive lanes: unique keys
+        const int prev = __shfl_up(kk, 2, 64);
+        const uint64_t heads = ~__ballot(lane >= 2 && prev == kk) & par;
+        const int head = 63 - __clzll(heads & upto);
+        const uint64_t later = heads & ~upto;
+        const int next = later ? __ffsll((unsigned long long)later) - 1 : 64 + (lane & 1);
+        int top = 0;
+        if (ok && lane == head) top = atomicSub(&cnt[key], (next - head) >> 1);
+        top = __shfl(top, head, 64);
+        if (ok) list[local[key] + pre[key / kScanBlock] + top - 1 - ((lane - head) >> 1)] = (int)c;
     }
 }
 

@@ -72,6 +72,21 @@ struct WsLayout {
 
 // Per-kScanBlock-key exclusive scan of cnt into offs (+ block total), and for UNIQ of the flags
 // cnt > 0 into uloc / utot: the body of k_scan_local for scan block `blk` (whole workgroup).
+// cnt[key] += 1 for every lane with ok, called by all 64 lanes of a wave together.  Equal keys
+// two lanes apart (a user group's contributions c = 2i, 2i+2, ...) form runs: the run's head
+// adds the run length with one atomic, so a group does not queue on one counter.
+__device__ __forceinline__ void wave_run_count(int32_t* __restrict__ cnt, int key, bool ok) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t par = (lane & 1) ? 0xAAAAAAAAAAAAAAAAull : 0x5555555555555555ull;
+    const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+    const int kk = ok ? key : -2 - lane;
+    const int prev = __shfl_up(kk, 2, 64);
+    const uint64_t heads = ~__ballot(lane >= 2 && prev == kk) & par;
+    const uint64_t later = heads & ~upto;
+    const int next = later ? __ffsll((unsigned long long)later) - 1 : 64 + (lane & 1);
+    if (ok && ((heads >> lane) & 1ull)) atomicAdd(&cnt[key], (next - lane) >> 1);
+}
+
 template <bool UNIQ>
 __device__ inline void scan_local_body(const int32_t* __restrict__ cnt, int64_t r1, int32_t* __restrict__ offs,
                                        int32_t* __restrict__ tot, int32_t* __restrict__ uloc,

@@ -368,13 +368,20 @@ __global__ __launch_bounds__(kBlock) void k_emb_adam_touched(float4* __restrict_
     if ((int)blockIdx.x >= ca.nupd) {
         // extra blocks: count the NEXT batch's contributions (k_count's work) while this step's
         // rows stream; the counters are free here (the fill of this step's index emptied them)
-        const int64_t first = (int64_t)(blockIdx.x - ca.nupd) * kBlock + threadIdx.x;
+        const int64_t first = (int64_t)(blockIdx.x - ca.nupd) * kBlock + (threadIdx.x & ~63);
         const int64_t cstride = (int64_t)ca.ncount * kBlock;
-        for (int64_t c = first; c < ca.m; c += cstride) {
-            const int64_t i = c >> 1;
-            const int id = (c & 1) ? ca.items[i] : ca.users[i];
-            const int bound = (c & 1) ? ca.I : ca.U;
-            if ((unsigned)id < (unsigned)bound) atomicAdd(&ca.cnt[(c & 1) ? ca.U + id : id], 1);
+        for (int64_t cb = first; cb < ca.m; cb += cstride) {   // wave-uniform trip count
+            const int64_t c = cb + (threadIdx.x & 63);
+            bool ok = false;
+            int key = 0;
+            if (c < ca.m) {
+                const int64_t i = c >> 1;
+                const int id = (c & 1) ? ca.items[i] : ca.users[i];
+                const int bound = (c & 1) ? ca.I : ca.U;
+                ok = (unsigned)id < (unsigned)bound;
+                key = (c & 1) ? ca.U + id : id;
+            }
+            wave_run_count(ca.cnt, key, ok);
         }
         return;
     }
