@@ -223,7 +223,16 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
     for (int m = 0; m < S::MAXT; ++m)
 #pragma unroll
         for (int r = 0; r < 16; ++r) dwacc[m][r] = 0.f;
-    float acc_bias = 0.f, acc_h3 = 0.f, acc_dbo = 0.f, acc_bce = 0.f, acc_hit = 0.f, acc_dcg = 0.f;
+    // bias-gradient rows (L1 + L2 + L3 of them): when the dW tiles leave wave 0 one tile short
+    // (3 dW2/dW3 tiles after the dW1 groups, config C) wave 0 sums them all, NBR rows per lane;
+    // otherwise thread tid sums row tid.  Same per-row order either way.
+    constexpr int NB = L1 + L2 + L3;
+    constexpr bool BW0 = S::NSLOT1 > 0 && (S::NDW - S::NDW1) % 4 != 0;
+    constexpr int NBR = BW0 ? cdiv(NB, 64) : 1;
+    float acc_bias[NBR];
+#pragma unroll
+    for (int q = 0; q < NBR; ++q) acc_bias[q] = 0.f;
+    float acc_h3 = 0.f, acc_dbo = 0.f, acc_bce = 0.f, acc_hit = 0.f, acc_dcg = 0.f;
     const bool metrics = part_hit != nullptr;  // groups never straddle a 32-sample block (group | 32)
     // output-kernel gradients, accumulated per lane (its own samples) across tiles and reduced
     // across lanes once, in the epilogue: a per-tile transpose-reduction is a chain of 16
@@ -669,15 +678,19 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
         }
         NCF_T(10);
         // ---- bias gradients: one G row per thread, summed over the 128 samples
-        if (tid < L1 + L2 + L3) {
-            const int rr = tid < L1 ? S::RG1 + tid : tid < L1 + L2 ? S::RG2 + (tid - L1) : S::RG3 + (tid - L1 - L2);
-            float sacc = 0.f;
-            for (int b = 0; b < 4; ++b) {
-                const float* bb = stg + b * S::RB * LS + rr * LS;
 #pragma unroll
-                for (int c = 0; c < 32; ++c) sacc += bb[c];
+        for (int q = 0; q < NBR; ++q) {
+            const int br = BW0 ? (tid & 63) + 64 * q : tid;
+            if ((!BW0 || w == 0) && br < NB) {
+                const int rr = br < L1 ? S::RG1 + br : br < L1 + L2 ? S::RG2 + (br - L1) : S::RG3 + (br - L1 - L2);
+                float sacc = 0.f;
+                for (int b = 0; b < 4; ++b) {
+                    const float* bb = stg + b * S::RB * LS + rr * LS;
+#pragma unroll
+                    for (int c = 0; c < 32; ++c) sacc += bb[c];
+                }
+                acc_bias[q] += sacc;
             }
-            acc_bias += sacc;
         }
         NCF_T(11);
         __syncthreads();
@@ -705,9 +718,15 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
             if (ir < lin && oc < lout) slab[off + ir * lout + oc] = dwacc[m][r];
         }
     }
-    if (tid < L1) slab[S::OB1 + tid] = acc_bias;
-    else if (tid < L1 + L2) slab[S::OB2 + (tid - L1)] = acc_bias;
-    else if (tid < L1 + L2 + L3) slab[S::OB3 + (tid - L1 - L2)] = acc_bias;
+#pragma unroll
+    for (int q = 0; q < NBR; ++q) {
+        const int br = BW0 ? (tid & 63) + 64 * q : tid;
+        if (!BW0 || w == 0) {
+            if (br < L1) slab[S::OB1 + br] = acc_bias[q];
+            else if (br < L1 + L2) slab[S::OB2 + (br - L1)] = acc_bias[q];
+            else if (br < NB) slab[S::OB3 + (br - L1 - L2)] = acc_bias[q];
+        }
+    }
 
     // output layer: reduce the per-lane partials across each wave half, then combine the 4
     // waves in fixed order through LDS
