@@ -134,6 +134,7 @@ def profile_read(kernel):
     return ms.value, n.value
 
 _lib = None
+ABI_VERSION = 3   # include/movierec_ncf.h ncf_abi_version()
 
 
 def lib():
@@ -148,6 +149,10 @@ def lib():
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args
+        got = handle.ncf_abi_version()
+        if got != ABI_VERSION:
+            raise RuntimeError("libmovierec_ncf.so at %s has ABI %d, this binding expects %d: rebuild it "
+                               "(__graft_entry__.build())" % (LIB_PATH, got, ABI_VERSION))
         _lib = handle
     return _lib
 
