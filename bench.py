@@ -66,7 +66,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="C", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: the config's)")
-    ap.add_argument("--pool", type=int, default=8, help="distinct synthetic batches cycled through")
+    ap.add_argument("--pool", type=int, default=None,
+                    help="distinct synthetic batches cycled through (default: one per warmup + timed step, at "
+                         "most 1024: every step trains on fresh uniform ids, as epochs over real data do; a "
+                         "small pool leaves the users it never draws to owe the Keras dense decay of every step)")
     ap.add_argument("--generic", action="store_true", help="force the generic (non-MFMA) kernel")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
@@ -417,7 +420,8 @@ def main():
         else:
             raise SystemExit("--e2e supports the single-table and user-partitioned layouts")
     pool = []
-    for _ in range(args.pool):
+    npool = args.pool if args.pool else max(8, min(1024, args.warmup + args.steps + 1))
+    for _ in range(npool):
         # user-partitioned data: this rank's users only, as local ids (u // world)
         u = torch.randint(0, eng.num_users if mode == "user" else cfg["num_users"], (B // g,), generator=gen,
                           device="cuda", dtype=torch.int32)
@@ -492,7 +496,7 @@ def main():
     if mode == "sharded":
         nbytes = emb_update_bytes(eng.shape, B, sparse_rows=(eng.shard_rows, train_exchange[1]))
     elif getattr(eng, "lazy", False):
-        touched = float(np.mean([torch.unique(u).numel() + torch.unique(it).numel() for u, it, _ in pool]))
+        touched = float(np.mean([torch.unique(u).numel() + torch.unique(it).numel() for u, it, _ in pool[:16]]))
         nbytes = emb_update_bytes(eng.shape, B, touched_rows=touched)
         if sampler is None:
             nbytes += 2 * B * (4 + 8)   # the launch also counts the next batch: id reads + counter atomics
@@ -555,7 +559,7 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
             "data": ("synthetic ml-20m-shaped ratings (%d positives), negatives sampled on the device each step"
                      % len(sampler.data) if sampler is not None else
-                     "synthetic (uniform ids, seeded; random-init weights)"),
+                     "synthetic (uniform ids, seeded; %d distinct batches cycled; random-init weights)" % len(pool)),
             "config": {"workload": cfg["workload"], "global_batch": B * world, "per_gpu_batch": B,
                        "negatives_per_positive": cfg["negs"], "parallelism": par,
                        "kernel_path": getattr(eng, "kernel_path", "fused-mfma" if eng.fast_path else "generic")},

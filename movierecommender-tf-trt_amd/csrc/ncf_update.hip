@@ -196,7 +196,10 @@ struct RowLanes {
     }
 };
 
-constexpr int kLrLut = 64;  // bias-corrected lr of the last kLrLut steps, per block in LDS
+// bias-corrected lr of the last kLrLut steps, per block in LDS (one entry per thread).  Older
+// steps fall back to adam_lr_t (two powf per element-step): with fresh uniform batches a row's
+// gap exceeds 64 steps often enough that the few such rows set the launch's tail
+constexpr int kLrLut = kBlock;
 
 // replay the zero-gradient steps (s, t] of the touched rows list[0..*nlist) (ALL: every row,
 // ncf_lazy_flush)
