@@ -5,24 +5,35 @@ ml-20m"; config C of SURVEY §8(d)): ml-20m table sizes (138,493 users,
 27,278 items), NeuMF with gmf_dim 64 and MLP layers [128, 64, 32, 16],
 3 negatives per positive (groups of 4: [neg, neg, neg, pos], user repeated
 per group as the data pipeline emits them), batch 65,536 per GPU, Adam
-(lr 1e-3) applied densely to every parameter (Keras semantics), fp32.
-Synthetic, seeded ids resident in HBM before the timed region (a pool of
-batches cycled through); random-init weights.
+(lr 1e-3) with Keras' dense semantics (every row moves every step), fp32.
+Synthetic, seeded ids resident in HBM before the timed region (a fresh
+batch per step); random-init weights.
 
-One step = ncf_train_step on 1 GPU.  On N GPUs (torchrun, one process per GPU,
-RCCL over xGMI; per-GPU batch fixed = weak scaling) the default is the
-row-sharded layout (``--dp sharded``): each rank owns 1/N of the
-table rows and their Adam state; per step the batch's unique rows are fetched
-from their owners and their gradients returned (all_to_all), the dense-layer
-gradient is all-reduced, and each rank sweeps only its shard.  ``--dp
-replicated`` keeps whole tables on every rank (reduce-scatter of the dense
-embedding gradient, sharded Adam, all-gather).
+One step = ncf_train_step on 1 GPU (one table, deferred exact decay).  On N
+GPUs (one process per GPU, RCCL over xGMI, per-GPU batch fixed = weak
+scaling) the default layout is user-partitioned (``--dp user``): rank r trains
+the users u % N == r and alone holds their rows and Adam state, the item table
+and the dense layers are replicated, and ONE all-reduce per step carries
+[item-row gradient | dense-layer gradient | summary].  ``--dp sharded`` (row-
+sharded tables, all_to_all of rows) and ``--dp replicated`` (reduce-scatter +
+all-gather) are the other layouts.
 
-Prints ONE JSON line (rank 0).  ``roofline`` is the embedding scatter-add +
-Adam (the HBM-bound kernel the north star's >= 50 % target names) and
-``roofline_fwd_bwd`` the fused forward/backward (the step's longest kernel,
-MFMA-bound), both timed live with HIP events on the launch stream; ``cpu_baseline`` times the numpy CPU restatement
-(oracle/) of the same step on a bounded sample, rank 0, N=1 only.
+``python bench.py --gpus N`` with N > 1 and no torchrun environment launches
+the N ranks itself (``torch.distributed.run`` as a child process, before any
+GPU call) and exits with its status; under torchrun, ``--gpus`` must equal
+WORLD_SIZE.
+
+Prints ONE JSON line (rank 0).  ``roofline`` is the step's dominant kernel
+(config C: the fused forward/backward, MFMA-bound), ``roofline_emb_update``
+the embedding scatter-add + Adam (the HBM-bound kernel the north star's
+>= 50 % target names), both timed live with HIP events in the dispatch packets
+of the launch stream.  ``traffic`` comes from a committed rocprofv3 PMC
+measurement of the same config and batch (profiles/traffic/), else null.
+``cpu_baseline`` times the torch-CPU restatement of the reference's Keras step
+(oracle/ncf_torch_cpu.py) on rank 0 at N=1 only: BASELINE.md's protocol
+(20 warm-up steps, median of 5 timed runs, threads = the host cores this
+process may use), the run length bounded by ``--cpu-seconds`` unless
+``--cpu-protocol full`` (200 steps per run).
 """
 
 import argparse
@@ -72,7 +83,13 @@ def parse():
                          "small pool leaves the users it never draws to owe the Keras dense decay of every step)")
     ap.add_argument("--generic", action="store_true", help="force the generic (non-MFMA) kernel")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0,
+                    help="budget of the timed CPU baseline runs (the 5 runs share it)")
+    ap.add_argument("--cpu-protocol", default="bounded", choices=["bounded", "full"],
+                    help="full: BASELINE.md's 20 warm-up + 5 x 200 timed steps, whatever it takes")
+    ap.add_argument("--selftest-launch", action="store_true",
+                    help="launcher self-test (CPU, gloo): ranks start, synchronise and report without any "
+                         "GPU work; the JSON line names the rank count")
     ap.add_argument("--e2e", action="store_true",
                     help="end-to-end: each step also samples its batch on the device (ncf_sample_batch) from an "
                          "ml-20m-shaped synthetic ratings set (20M positives)")
@@ -132,33 +149,21 @@ def fwd_bwd_bytes(shape, batch):
     return batch * (12 + 2 * shape.row_width * 4 * 2 + 4)
 
 
-def cpu_baseline(cfg, budget_s):
-    """numpy restatement (oracle/) of one training step, fp32, bounded sample."""
-    from oracle import ncf_oracle as O
-    try:
-        from threadpoolctl import threadpool_info
-        threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
-    except Exception:
-        threads = 1
-    shape = O.NCFShape(cfg["num_users"], cfg["num_items"], cfg["layers"], cfg["gmf_dim"])
-    w = O.init_weights(shape, seed=0, dtype=np.float32)
-    st = O.new_opt_state(w)
-    B = cfg["batch"]
-    g = cfg["negs"] + 1
-    rng = np.random.RandomState(1)
-    hyper = dict(optimizer="adam", lr=0.001, beta_1=0.9, beta_2=0.999, layers_l2reg=[0] * len(cfg["layers"]))
-    steps, t_total = 0, 0.0
-    while t_total < budget_s and steps < 50:
-        users = rng.randint(0, cfg["num_users"], B // g).repeat(g)
-        items = rng.randint(0, cfg["num_items"], B)
-        y = np.tile([0] * (g - 1) + [1], B // g).astype(np.float32)
-        t0 = time.perf_counter()
-        O.train_step(shape, w, st, users, items, y, hyper)
-        t_total += time.perf_counter() - t0
-        steps += 1
-    return dict(value=round(steps * B / t_total, 1), unit="samples/s", cores=int(threads), kind="port",
-                sample="%d full training steps of batch %d (dense Adam over every table row), numpy fp32, "
-                       "%.1f s" % (steps, B, t_total))
+def cpu_baseline(cfg, budget_s, protocol="bounded"):
+    """torch-CPU restatement (oracle/ncf_torch_cpu.py) of the reference's Keras training step,
+    timed with BASELINE.md's protocol: 20 warm-up steps, 5 timed runs, median; threads = the
+    host cores this process may use.  ``bounded``: the 5 runs share ``budget_s`` seconds (at most
+    200 steps each); ``full``: 200 steps each."""
+    from oracle import ncf_torch_cpu as T
+    full = protocol == "full"
+    med, rates, threads, steps = T.time_protocol(cfg["num_users"], cfg["num_items"], cfg["layers"], cfg["gmf_dim"],
+                                                 cfg["batch"], cfg["negs"], warmup=20, steps=200, repeats=5,
+                                                 budget_s=None if full else budget_s)
+    return dict(value=round(med, 1), unit="samples/s", cores=int(threads), kind="port",
+                runs=[round(r, 1) for r in rates],
+                sample="torch-CPU fp32 Keras-equivalent step (autograd, dense embedding gradient, dense Adam "
+                       "over every table row), batch %d: 20 warm-up steps, median of 5 runs of %d steps "
+                       "(protocol %s)" % (cfg["batch"], steps, protocol))
 
 
 def cpu_sampler_baseline(cfg, budget_s):
@@ -314,15 +319,16 @@ def device_glorot_init(eng, w_small, seed):
     torch.cuda.synchronize()
 
 
-def pmc_traffic(name, kernel=None):
-    """HBM bytes per launch measured by tools/gpu_profile.sh (separate --pmc passes), if the
-    committed measurement is of ``kernel``."""
-    path = os.path.join(ROOT, "profiles", name)
+def pmc_traffic(kernel, config, batch, mode):
+    """HBM bytes per launch of ``kernel`` measured by tools/gpu_profile.sh (separate FETCH_SIZE /
+    WRITE_SIZE rocprofv3 passes) for exactly this config, per-GPU batch and layout; None when no
+    such measurement is committed under profiles/traffic/."""
+    path = os.path.join(ROOT, "profiles", "traffic", "%s_b%d_%s_%s.json" % (config, batch, mode, kernel))
     try:
         d = json.load(open(path))
     except (OSError, ValueError):
         return None
-    if kernel is not None and d.get("kernel") != kernel:
+    if (d.get("kernel"), d.get("config"), d.get("batch"), d.get("mode")) != (kernel, config, batch, mode):
         return None
     return d.get("bytes_per_launch")
 
@@ -345,12 +351,63 @@ def emit(text):
     _RESULT_OUT.flush()
 
 
+def _free_port():
+    import socket
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    return port
+
+
+def launch_ranks(nproc):
+    """``--gpus N`` outside torchrun: run this same command as N ranks under
+    torch.distributed.run (a child process, started before this process touches the GPU) and
+    return its exit status.  The ranks' stdout is this process's stdout: rank 0 prints the one
+    JSON line, the others print nothing there."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "1")   # torchrun's default; keeps its warning off stderr
+    sys.stdout.flush()
+    return subprocess.call(cmd, env=env)
+
+
+def selftest_main(args, world, rank):
+    """Launcher self-test: the process group forms (gloo, CPU), the ranks time a trivial region
+    between barriers, the max over ranks reaches rank 0, rank 0 prints the line."""
+    if world > 1:
+        dist.init_process_group("gloo")
+    t0 = time.perf_counter()
+    x = torch.zeros(1)
+    for _ in range(max(args.steps, 1)):
+        x += 1
+    if dist.is_initialized():
+        dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    if dist.is_initialized():
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        emit(json.dumps({"metric": "launcher self-test", "value": None, "n_gpus": world, "ranks": world,
+                         "steps": args.steps, "warmup": args.warmup, "elapsed_max_s": float(t.item()),
+                         "backend": dist.get_backend() if dist.is_initialized() else None}))
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
 def main():
-    _keep_stdout_for_result()
     args = parse()
+    if args.gpus > 1 and "RANK" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
+    _keep_stdout_for_result()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world:
+        raise SystemExit("--gpus %d but the launcher started %d rank(s) (WORLD_SIZE)" % (args.gpus, world))
+    if args.selftest_launch:
+        return selftest_main(args, world, rank)
     torch.cuda.set_device(local if args.dist_backend == "nccl" else 0)
     mode = args.dp if args.dp != "auto" else ("single" if world == 1 else "user")
     if world > 1:
@@ -530,9 +587,10 @@ def main():
         dist.all_reduce(hd)
     hr = {"hr": float(hd[0]) / (ev_users * world), "dcg": float(hd[1]) / (ev_users * world)}
 
-    traffic = pmc_traffic("traffic_emb_update.json", "k_emb_adam_touched" if getattr(eng, "lazy", False)
-                          else "k_emb_update") if mode == "single" else None
-    fb_traffic = pmc_traffic("traffic_fb_fused.json") if mode == "single" and eng.fast_path else None
+    emb_kernel = "k_emb_adam_touched" if getattr(eng, "lazy", False) else "k_emb_update"
+    traffic = pmc_traffic(emb_kernel, args.config, B, mode)
+    fb_kernel = {"fused-mfma": "k_fb_fused"}.get(getattr(eng, "kernel_path", ""), None)
+    fb_traffic = pmc_traffic(fb_kernel, args.config, B, mode) if fb_kernel else None
     par = {"single": "dp1 (one table)",
            "user": "dp%d user-partitioned data (rank r trains users u %% %d == r and alone holds their rows + "
                    "Adam state); item table replicated; ONE all-reduce per step of [item-row grad | dense-layer "
@@ -542,11 +600,66 @@ def main():
            "replicated": "dp%d replicated tables (reduce-scatter of the dense embedding grad, sharded Adam, "
                          "all-gather of the table; all-reduce of the dense-layer grad)" % world}[mode]
 
+    exchange = None
+    if mode == "user":
+        # the step's one collective, timed alone after the timed region (same buffer size, same
+        # communicator): how long the all-reduce the step overlaps with its own-user update takes
+        buf = dp.shared.clone()
+        for _ in range(3):
+            dist.all_reduce(buf)
+        torch.cuda.synchronize()
+        t_ar = time.perf_counter()
+        for _ in range(10):
+            dist.all_reduce(buf)
+        torch.cuda.synchronize()
+        ar_ms = (time.perf_counter() - t_ar) / 10 * 1e3
+        exchange = {"allreduce_bytes_per_step": dp.shared.numel() * dp.shared.element_size(),
+                    "allreduce_ms_standalone": round(ar_ms, 4), "collectives_per_step": 1,
+                    "local_users": eng.num_users}
+    elif mode == "sharded":
+        exchange = {"unique_rows_per_rank": train_exchange[0], "rows_served_per_rank": train_exchange[1],
+                    "shard_rows": eng.shard_rows}
+    if exchange is not None:
+        exchange.update(ranks=world, backend=dist.get_backend(),
+                        transport="RCCL over xGMI" if dist.get_backend() == "nccl" else dist.get_backend())
+
+    emb_roof = {"bound": "hbm", "kernel": ("embedding scatter-add + Adam on the batch's touched rows "
+                                           "(k_emb_adam_touched; deferred exact decay"
+                                           + ("; its launch also counts the next batch's index "
+                                              "contributions)" if sampler is None else ")")
+                                           if getattr(eng, "lazy", False) else
+                                           "embedding Adam, 2 launches per step (k_emb_update: own-user "
+                                           "rows with their scatter-add; item rows with the all-reduced "
+                                           "gradient)" if mode == "user" else
+                                           "embedding scatter-add + Adam sweep (k_emb_update)"),
+                "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "algorithmic_bytes_per_launch": nbytes, "avg_launch_ms": round(kern_ms, 5),
+                "launches_per_step": round(nl / len(range(0, args.steps, every)), 2),
+                "timed_steps": "every %d-th step of the timed region (HIP events in the dispatch packets)" % every,
+                "traffic_source": "rocprofv3 --pmc FETCH_SIZE(x2 gfx950) + WRITE_SIZE, profiles/traffic/ "
+                                  "(this config, batch and layout only; null if not measured)"}
+    fb_achieved = fb_flops / (fb_ms * 1e-3) / 1e12
+    fb_roof = {"bound": "mfma", "kernel": {
+                   "fused-mfma": "fused NeuMF forward+backward (k_fb_fused, fp32 MFMA)",
+                   "layered-rocblas": "layer-by-layer forward+backward (rocBLAS fp32 GEMMs + glue kernels, "
+                                      "ncf_layered.hip)"}.get(getattr(eng, "kernel_path", ""),
+                                                              "generic forward+backward"),
+               "achieved": round(fb_achieved, 2), "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+               "frac": round(fb_achieved / FP32_MFMA_PEAK_TFS, 4), "traffic": fb_traffic,
+               "traffic_unit": "HBM bytes per launch",
+               "algorithmic_flops_per_launch": fb_flops, "avg_launch_ms": round(fb_ms, 5),
+               "hbm_GBs": round(fb_bytes / (fb_ms * 1e-3) / 1e9, 1), "algorithmic_bytes_per_launch": fb_bytes}
+    # `roofline` = the step's dominant kernel (longest average time per step)
+    fb_per_step = fb_ms * nfb / max(len(range(0, args.steps, every)), 1)
+    emb_per_step = kern_ms * nl / max(len(range(0, args.steps, every)), 1)
+    dominant_fb = not (emb_per_step > fb_per_step)
+
     if rank == 0:
         cpu = None
         cpu_e2e = None
         if world == 1 and not args.no_cpu_baseline and not big:
-            cpu = cpu_baseline(cfg, args.cpu_seconds)
+            cpu = cpu_baseline(cfg, args.cpu_seconds, args.cpu_protocol)
             smp, smp_desc = cpu_sampler_baseline(cfg, min(6.0, args.cpu_seconds))
             # model step and sampler back to back on the host (the reference's Keras loop, workers=1)
             cpu_e2e = dict(value=round(1.0 / (1.0 / cpu["value"] + 1.0 / smp), 1), unit="samples/s",
@@ -563,34 +676,8 @@ def main():
             "config": {"workload": cfg["workload"], "global_batch": B * world, "per_gpu_batch": B,
                        "negatives_per_positive": cfg["negs"], "parallelism": par,
                        "kernel_path": getattr(eng, "kernel_path", "fused-mfma" if eng.fast_path else "generic")},
-            "roofline": {"bound": "hbm", "kernel": ("embedding scatter-add + Adam on the batch's touched rows "
-                                                    "(k_emb_adam_touched; deferred exact decay"
-                                                    + ("; its launch also counts the next batch's index "
-                                                       "contributions)" if sampler is None else ")")
-                                                    if getattr(eng, "lazy", False) else
-                                                    "embedding Adam, 2 launches per step (k_emb_update: own-user "
-                                                    "rows with their scatter-add; item rows with the all-reduced "
-                                                    "gradient)" if mode == "user" else
-                                                    "embedding scatter-add + Adam sweep (k_emb_update)"),
-                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "algorithmic_bytes_per_launch": nbytes, "avg_launch_ms": round(kern_ms, 5),
-                         "launches_per_step": round(nl / len(range(0, args.steps, every)), 2),
-                         "timed_steps": "every %d-th step of the timed region (HIP events in the dispatch packets)"
-                                        % every,
-                         "traffic_source": "rocprofv3 --pmc FETCH_SIZE(x2 gfx950) + WRITE_SIZE, "
-                                           "profiles/traffic_emb_update.json (per launch)"},
-            "roofline_fwd_bwd": {"bound": "mfma", "kernel": {
-                                     "fused-mfma": "fused NeuMF forward+backward (k_fb_fused, fp32 MFMA)",
-                                     "layered-rocblas": "layer-by-layer forward+backward (rocBLAS fp32 GEMMs + glue "
-                                                        "kernels, ncf_layered.hip)"}.get(
-                                     getattr(eng, "kernel_path", ""), "generic forward+backward"), "achieved": round(
-                                     fb_flops / (fb_ms * 1e-3) / 1e12, 2), "peak": FP32_MFMA_PEAK_TFS,
-                                 "unit": "TFLOP/s", "frac": round(fb_flops / (fb_ms * 1e-3) / 1e12 /
-                                                                  FP32_MFMA_PEAK_TFS, 4),
-                                 "algorithmic_flops_per_launch": fb_flops, "avg_launch_ms": round(fb_ms, 5),
-                                 "hbm_GBs": round(fb_bytes / (fb_ms * 1e-3) / 1e9, 1),
-                                 "algorithmic_bytes_per_launch": fb_bytes, "traffic": fb_traffic},
+            "roofline": fb_roof if dominant_fb else emb_roof,
+            "roofline_emb_update" if dominant_fb else "roofline_fwd_bwd": emb_roof if dominant_fb else fb_roof,
             "index_build_ms": round(ms_idx / max(nidx, 1), 5),
             "sampler_ms": round(ms_smp / nsmp, 5) if nsmp else None,
             "catchup_ms": round(ms_cu / ncu, 5) if ncu else None,
@@ -602,13 +689,8 @@ def main():
             "hr_at_10": {"value": round(hr["hr"], 4), "ndcg_at_10": round(hr["dcg"], 4),
                          "data": "synthetic eval groups (random ids; ~0.1 expected for an untrained model)"},
         }
-        if mode == "user":
-            line["exchange"] = {"allreduce_bytes_per_step": dp.shared.numel() * dp.shared.element_size(),
-                                "local_users": eng.num_users, "collectives_per_step": 1}
-        if mode == "sharded":
-            line["exchange"] = {"unique_rows_per_rank": train_exchange[0],
-                                "rows_served_per_rank": train_exchange[1],
-                                "shard_rows": eng.shard_rows}
+        if exchange is not None:
+            line["exchange"] = exchange
         emit(json.dumps(line))
     if dist.is_initialized():
         dist.destroy_process_group()

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define NCF_ABI_VERSION 3
+#define NCF_ABI_VERSION 4
 #define NCF_MAX_LAYERS 8
 #define NCF_EINVAL (-1)
 #define NCF_EHIP (-2)
@@ -137,6 +137,19 @@ int ncf_shape_init(ncf_shape_t* shape, int32_t num_users, int32_t num_items, con
 int ncf_workspace_size(const ncf_shape_t* shape, int64_t max_batch, size_t* bytes);
 /* Zero the workspace's persistent region (call once after allocating it). */
 int ncf_workspace_init(const ncf_shape_t* shape, int64_t max_batch, void* ws, size_t ws_bytes, void* stream);
+
+/* Sticky error flags of the workspace's index builds, copied to flags (device int32) and cleared:
+ *   NCF_WSERR_ID_RANGE     an index build met a user/item id outside the table (the kernels mask
+ *                          such samples; the Python layer raises ValueError, like TF's gather)
+ *   NCF_WSERR_STALE_COUNT  a batch passed with hyper->index_ready = 2 differed from the ids
+ *                          ncf_train_step_ahead counted (their contents changed in between): the
+ *                          index build wrote no slot outside its keys' ranges and cleared the
+ *                          counters, but that step's embedding gradient is wrong.
+ * Nothing else in the library synchronises on them. */
+#define NCF_WSERR_ID_RANGE 1
+#define NCF_WSERR_STALE_COUNT 4
+int ncf_workspace_flags(const ncf_shape_t* shape, int64_t max_batch, void* ws, size_t ws_bytes, int32_t* flags,
+                        void* stream);
 
 /* Forward only: probs[n] = sigmoid output for (users[i], items[i]).
  * Replaces Model.predict_on_batch output[0] (model.py:184-194). */

@@ -306,6 +306,18 @@ int ncf_workspace_init(const ncf_shape_t* s, int64_t max_batch, void* ws, size_t
     return hip_check(hipMemsetAsync(ws, 0, L.persistent_end, (hipStream_t)stream), "hipMemsetAsync");
 }
 
+int ncf_workspace_flags(const ncf_shape_t* s, int64_t max_batch, void* ws, size_t ws_bytes, int32_t* flags,
+                        void* stream) {
+    if (int r = check_shape(s)) return r;
+    if (!flags) return fail(NCF_EINVAL, "flags is NULL");
+    ncf::WsLayout L = ncf::make_layout(*s, max_batch);
+    if (!ws || ws_bytes < L.total) return fail(NCF_EINVAL, "workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    if (hipError_t e = hipMemcpyAsync(flags, ncf::at<int32_t>(ws, L.err), 4, hipMemcpyDeviceToDevice, st))
+        return hip_check(e, "flags copy");
+    return hip_check(hipMemsetAsync(ncf::at<int32_t>(ws, L.err), 0, 4, st), "flags clear");
+}
+
 int ncf_predict(const ncf_shape_t* s, const ncf_model_t* model, const int32_t* users, const int32_t* items,
                 int64_t n, float* probs, void* ws, size_t ws_bytes, void* stream) {
     if (int r = check_shape(s)) return r;

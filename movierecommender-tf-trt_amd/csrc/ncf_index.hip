@@ -79,7 +79,7 @@ __global__ __launch_bounds__(kBlock) void k_count(KeySrc ks, int64_t m, int32_t*
         int key = 0;
         if (c < m) {
             key = contrib_key<MODE>(c, ks, &ok);
-            if (!ok) atomicOr(err, 1);
+            if (!ok) atomicOr(err, kErrIdRange);
         }
         wave_run_count(cnt, key, ok);
     }
@@ -128,7 +128,7 @@ template <int MODE, bool UNIQ, bool LIST>
 __global__ __launch_bounds__(kBlock) void k_fill(KeySrc ks, int64_t m, int32_t* __restrict__ cnt,
                                                  const int32_t* __restrict__ local, const int32_t* __restrict__ tot,
                                                  int nscan, int64_t r1, int32_t* __restrict__ offs_g,
-                                                 int32_t* __restrict__ list, PlanOut po) {
+                                                 int32_t* __restrict__ list, PlanOut po, int32_t* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) int pre[];  // [nscan] (+ [nscan] unique prefix)
     __shared__ int sw[4];
     int* upre = pre + nscan;
@@ -197,7 +197,11 @@ __global__ __launch_bounds__(kBlock) void k_fill(KeySrc ks, int64_t m, int32_t* 
         int top = 0;
         if (ok && lane == head) top = atomicSub(&cnt[key], (next - head) >> 1);
         top = __shfl(top, head, 64);
-        if (ok) list[local[key] + pre[key / kScanBlock] + top - 1 - ((lane - head) >> 1)] = (int)c;
+        // a slot below the key's range means the key was counted fewer times than it occurs
+        // (counted-ahead ids changed since): flagged, never written outside the key's slots
+        const int slot = top - 1 - ((lane - head) >> 1);
+        if (ok && slot >= 0) list[local[key] + pre[key / kScanBlock] + slot] = (int)c;
+        else if (ok) atomicOr(err, kErrStaleCount);
     }
 }
 
@@ -205,8 +209,9 @@ __global__ __launch_bounds__(kBlock) void k_fill(KeySrc ks, int64_t m, int32_t* 
 // odd-even network in registers.  Longer keys: queued in LDS and sorted by the whole
 // workgroup with a bitmap over the contribution ids (set bits, popcount scan, write back).
 __global__ __launch_bounds__(kBlock) void k_sort(const int32_t* __restrict__ offs, int64_t R,
-                                                 int32_t* __restrict__ list, int nwords) {
-    sort_rows_body(offs, R, list, nwords, (int)blockIdx.x);
+                                                 int32_t* __restrict__ list, int nwords, int32_t* __restrict__ cnt,
+                                                 int32_t* __restrict__ err) {
+    sort_rows_body(offs, R, list, nwords, (int)blockIdx.x, cnt, err);
 }
 
 static int grid_for(int64_t work, int cap) {
@@ -249,10 +254,12 @@ static hipError_t build(const WsLayout& L, void* ws, const KeySrc& ks, int64_t m
                                                    U2 ? at<int32_t>(ws, L.utot) : nullptr);
     const size_t pre_bytes = (size_t)nscan * 4 * (U2 ? 2 : 1);
     launch(k_fill<MODE, UNIQ, LIST>, grid_for(m > r1 ? m : r1, 1024), kBlock, pre_bytes, st, ks, m, cnt, local, tot,
-                                                                                         nscan, r1, offs, list, po);
+                                                                                         nscan, r1, offs, list, po,
+                                                                                         at<int32_t>(ws, L.err));
     if (skip_sort) return hipGetLastError();
     if (hipError_t e = set_sort_lds(nwords)) return e;
-    launch(k_sort, (unsigned)((K + kBlock - 1) / kBlock), kBlock, (size_t)nwords * 4, st, offs, K, list, nwords);
+    launch(k_sort, (unsigned)((K + kBlock - 1) / kBlock), kBlock, (size_t)nwords * 4, st, offs, K, list, nwords, cnt,
+           at<int32_t>(ws, L.err));
     return hipGetLastError();
 }
 

@@ -121,9 +121,17 @@ __device__ inline void scan_local_body(const int32_t* __restrict__ cnt, int64_t 
     }
 }
 
+// Workspace error flags (L.err, sticky until ncf_workspace_flags reads them).
+constexpr int kErrIdRange = 1;     // an index build met an id outside the table
+constexpr int kErrStaleCount = 4;  // a counted-ahead index met ids that differ from the counted ones
+
+// cnt/err (optional): every row's counter must be back at zero after k_fill; a residue means the
+// ids changed after they were counted ahead (ncf_train_step_ahead) — flagged, and the counter
+// cleared so that the next build starts from zero.
 template <int UNUSED = 0>
 __device__ inline void sort_rows_body(const int32_t* __restrict__ offs, int64_t R, int32_t* __restrict__ list,
-                                      int nwords, int blk) {
+                                      int nwords, int blk, int32_t* __restrict__ cnt = nullptr,
+                                      int32_t* __restrict__ err = nullptr) {
     extern __shared__ __attribute__((aligned(16))) unsigned bm[];
     __shared__ int hrows[kBlock];
     __shared__ int mrows[kBlock];
@@ -132,6 +140,10 @@ __device__ inline void sort_rows_body(const int32_t* __restrict__ offs, int64_t 
     if (threadIdx.x == 0) nh = nm = 0;
     __syncthreads();
     const int64_t r = (int64_t)blk * kBlock + threadIdx.x;
+    if (cnt && r < R && cnt[r] != 0) {
+        atomicOr(err, kErrStaleCount);
+        cnt[r] = 0;
+    }
     if (r < R) {
         const int o = offs[r];
         const int c = offs[r + 1] - o;

@@ -209,6 +209,8 @@ struct SortAhead {
     int64_t keys;
     int32_t* list;
     int nwords;
+    int32_t* cnt;              // residue check of the counters (sort_rows_body)
+    int32_t* err;
 };
 
 template <bool ALL>
@@ -222,7 +224,7 @@ __global__ __launch_bounds__(kBlock) void k_emb_catchup(float4* __restrict__ emb
     if (!ALL && (int)blockIdx.x >= so.ncatch) {
         // the contribution lists of this step's index, sorted while the rows replay (k_sort's work;
         // only the touched-row update after the forward pass reads them)
-        sort_rows_body(so.offs, so.keys, so.list, so.nwords, (int)blockIdx.x - so.ncatch);
+        sort_rows_body(so.offs, so.keys, so.list, so.nwords, (int)blockIdx.x - so.ncatch, so.cnt, so.err);
         return;
     }
     __shared__ float lut[kLrLut];
@@ -778,11 +780,12 @@ hipError_t launch_emb_catchup(const ncf_shape_t& s, const WsLayout& L, void* ws,
     const uint32_t w4 = (uint32_t)(s.row_width / 4);
     const int64_t R = s.num_rows;
     const int64_t nmax = R < 2 * L.max_batch ? R : 2 * L.max_batch;
-    SortAhead so{0, nullptr, 0, nullptr, 0};
+    SortAhead so{0, nullptr, 0, nullptr, 0, nullptr, nullptr};
     unsigned nsort = 0;
     size_t lds = 0;
     if (sort_lists && !all_rows) {
-        so = SortAhead{0, at<const int32_t>(ws, L.offs), R, at<int32_t>(ws, L.list), (int)((2 * n + 31) / 32)};
+        so = SortAhead{0, at<const int32_t>(ws, L.offs), R, at<int32_t>(ws, L.list), (int)((2 * n + 31) / 32),
+                       at<int32_t>(ws, L.cnt), at<int32_t>(ws, L.err)};
         nsort = (unsigned)((R + kBlock - 1) / kBlock);
         lds = (size_t)so.nwords * 4;
         static bool lds_cfg = false;

@@ -22,6 +22,7 @@ NCF_OPT_ADAM = 0
 NCF_OPT_SGD = 1
 NCF_NUM_STATS = 8
 NCF_NUM_SUMMARY = 8
+NCF_WSERR_ID_RANGE, NCF_WSERR_STALE_COUNT = 1, 4
 SUM_BCE, SUM_HIT, SUM_DCG, SUM_GROUPS, SUM_REG = range(5)
 STAT_LOSS_SUM, STAT_HR_SUM, STAT_DCG_SUM, STAT_STEPS, STAT_LAST_LOSS, STAT_LAST_HR, STAT_LAST_DCG = range(7)
 
@@ -68,6 +69,7 @@ _SIGNATURES = {
     "ncf_shape_init": (ctypes.c_int, [_P(NcfShape), _i32, _i32, _P(_i32), _i32, _i32]),
     "ncf_workspace_size": (ctypes.c_int, [_P(NcfShape), _i64, _P(ctypes.c_size_t)]),
     "ncf_workspace_init": (ctypes.c_int, [_P(NcfShape), _i64, _vp, ctypes.c_size_t, _vp]),
+    "ncf_workspace_flags": (ctypes.c_int, [_P(NcfShape), _i64, _vp, ctypes.c_size_t, _vp, _vp]),
     "ncf_predict": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _vp, _vp, _i64, _vp, _vp, ctypes.c_size_t, _vp]),
     "ncf_rank": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp]),
     "ncf_group_metrics": (ctypes.c_int, [_vp, _vp, _i64, _i32, _i32, _vp, _vp, _vp]),
@@ -134,7 +136,7 @@ def profile_read(kernel):
     return ms.value, n.value
 
 _lib = None
-ABI_VERSION = 3   # include/movierec_ncf.h ncf_abi_version()
+ABI_VERSION = 4   # include/movierec_ncf.h ncf_abi_version()
 
 
 def lib():

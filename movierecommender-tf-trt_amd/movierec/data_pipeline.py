@@ -25,6 +25,7 @@ reference's RNG stream; used for throughput runs.  Documented in DESIGN.md.
 """
 
 import logging
+import os
 
 import numpy as np
 
@@ -218,7 +219,18 @@ def split_leave_two_out(ratings_df):
     return take(train_pos), take(val_pos), take(test_pos)
 
 
-def load_ratings_train_test_sets(dataset_name, data_dir, download=True):
+def load_ratings_train_test_sets(dataset_name, data_dir, download=True, remap_items=None):
+    """Reference ``data_pipeline.py:157-200``.  ``remap_items`` (new, default: ml-20m only) gives
+    the items dense ids before the split (DESIGN deviation 5): the order of the
+    dataset's movies file when it is present (ml-20m's 27,278 movies), else ascending raw id.
+    Without it ml-20m's raw movieIds (up to 131,262) fall outside the 27,278-row item table."""
     _check_dataset_name(dataset_name)
     ratings_df = load_ratings_data(data_dir, dataset_name, COL_USER_ID, COL_ITEM_ID, COL_RATING, download)
+    if remap_items is None:
+        remap_items = dataset_name == ml.ML_20M
+    if remap_items:
+        movies_df = None
+        if os.path.exists(ml.get_movies_path(data_dir, dataset_name)):
+            movies_df = ml.load_movies_data(data_dir, dataset_name, COL_ITEM_ID, download=False)
+        ratings_df, _raw = ml.remap_item_ids(ratings_df, COL_ITEM_ID, movies_df)
     return split_leave_two_out(ratings_df)

@@ -31,6 +31,14 @@ def keras_weight_names(layers, gmf_dim):
     return names + ["output/kernel", "output/bias"]
 
 
+def _same_ids(held, u, i, n):
+    """An index prepared for (users, items) tensors ``held`` = (u, i, n, u_version, i_version)
+    applies to this call's ids: same tensors (storage), same size, not modified in place since."""
+    hu, hi, hn, vu, vi = held
+    return (hu.data_ptr() == u.data_ptr() and hi.data_ptr() == i.data_ptr() and hn == n and
+            hu._version == vu and hi._version == vi)
+
+
 class NCFEngine(object):
     """Model + optimizer state of one replica on one device."""
 
@@ -228,8 +236,7 @@ class NCFEngine(object):
         h.group, h.k = int(group), int(k)
         h.inv_batch = 1.0 / n if inv_batch is None else float(inv_batch)
         pc = self._counted
-        ready = pc is not None and pc[0].data_ptr() == u.data_ptr() and pc[1].data_ptr() == i.data_ptr() and \
-            pc[2] == n
+        ready = pc is not None and _same_ids(pc, u, i, n)
         if pc is not None and not ready:
             self._discard_counted()
         nu = ni = None
@@ -247,7 +254,11 @@ class NCFEngine(object):
                     ctypes.byref(self.shape), ctypes.byref(self.model_s), ctypes.byref(self.optim_s), ctypes.byref(h),
                     N.ptr(u), N.ptr(i), N.ptr(y), n, N.ptr(nu), N.ptr(ni), nu.numel(), N.ptr(self.stats),
                     N.ptr(probs_out), N.ptr(self.ws), self.ws_bytes, N.stream_handle(self.device)))
-                self._counted = (nu, ni, nu.numel())   # holds the tensors: their memory stays theirs
+                # holds the tensors (their memory stays theirs) and their versions: an in-place
+                # refill through torch (copy_, fill_, index assignment) bumps _version and the next
+                # call rebuilds the index; writes that bypass torch's version counter are caught on
+                # the device (NCF_WSERR_STALE_COUNT, check_errors)
+                self._counted = (nu, ni, nu.numel(), nu._version, ni._version)
             else:
                 N.check(N.lib().ncf_train_step(ctypes.byref(self.shape), ctypes.byref(self.model_s),
                                                ctypes.byref(self.optim_s), ctypes.byref(h), N.ptr(u), N.ptr(i),
@@ -256,6 +267,22 @@ class NCFEngine(object):
         finally:
             h.index_ready = 0
         self._dirty = self.row_step is not None
+
+    def check_errors(self):
+        """Raise if an index build since the last call met an id outside the table (ValueError,
+        like TF's gather) or a counted-ahead batch whose ids changed after they were counted
+        (RuntimeError: that step's embedding update is wrong).  Synchronises the stream."""
+        if self.ws is None:
+            return
+        flags = torch.zeros(1, dtype=torch.int32, device=self.device)
+        N.check(N.lib().ncf_workspace_flags(ctypes.byref(self.shape), self.max_batch, N.ptr(self.ws), self.ws_bytes,
+                                            N.ptr(flags), N.stream_handle(self.device)))
+        f = int(flags.item())
+        if f & N.NCF_WSERR_STALE_COUNT:
+            raise RuntimeError("a batch counted ahead (train_step next_batch=) changed its ids before its step: "
+                               "that step's embedding update used a stale index")
+        if f & N.NCF_WSERR_ID_RANGE:
+            raise ValueError("an id outside the embedding table reached the device (those samples were masked)")
 
     def _discard_counted(self):
         """Clear the index counters holding a next batch's counts (ncf_train_step_ahead) before any
@@ -376,8 +403,7 @@ class NCFEngine(object):
         h.group, h.k, h.inv_batch = int(group), int(k), float(inv_batch)
         # an index prebuilt by build_index is used only for the very tensors it was built from
         pb = self._prebuilt
-        ready = pb is not None and pb[0].data_ptr() == u.data_ptr() and pb[1].data_ptr() == i.data_ptr() and \
-            pb[2] == n
+        ready = pb is not None and _same_ids(pb, u, i, n)
         h.index_ready = 1 if ready else 0
         eg, mg, sm = grads
         r0, rc = (0, self.num_rows) if reg_rows is None else reg_rows
@@ -407,7 +433,7 @@ class NCFEngine(object):
             return
         N.check(N.lib().ncf_build_index(ctypes.byref(self.shape), N.ptr(u), N.ptr(i), n, N.ptr(self.ws),
                                         self.ws_bytes, N.stream_handle(self.device)))
-        self._prebuilt = (u, i, n)   # holds the tensors: their memory cannot be reused meanwhile
+        self._prebuilt = (u, i, n, u._version, i._version)   # holds the tensors: their memory stays theirs
 
     def update_rows(self, row_begin, row_count, inv_batch):
         """Optimizer step of rows [row_begin, row_begin + row_count) from the per-sample gradient

@@ -312,6 +312,7 @@ class MovierecModel(object):
                 eng.train_step(xu, xi, y, group=group_t, k=self._k)
             if hasattr(train_data_generator, "check_errors"):
                 train_data_generator.check_errors()
+            eng.check_errors()
             train_data_generator.on_epoch_end()
             tr = eng.read_stats(eng.stats)
             self.model.learning_phase = 0

@@ -8,7 +8,11 @@ tests, which patch ``os.path.exists`` / ``pd.read_csv`` / ``download_movielens``
 in this module) work unchanged.
 
 Additions (documented in DESIGN.md): ``remap_item_ids`` — dense 0-based item
-ids for ml-20m, whose raw movieIds are non-contiguous.
+ids for ml-20m, whose raw movieIds are non-contiguous, applied by
+``data_pipeline.load_ratings_train_test_sets``; movie titles are decoded with each
+file's own encoding (``MOVIES_ENCODING``: the ml-100k ``u.item`` and ml-1m
+``movies.dat`` files are latin-1, ml-20m's ``movies.csv`` is utf-8), which the
+reference's ``load_movies_data`` (``:85-101``) leaves to pandas' utf-8 default.
 """
 
 import logging
@@ -43,6 +47,9 @@ HAS_HEADER = {name: spec[3] for name, spec in _LAYOUT.items()}
 # data_pipeline.py:60-61, trainer.py:72-73).
 NUM_USERS = {ML_100K: 943, ML_1M: 6040, ML_20M: 138493}
 NUM_ITEMS = {ML_100K: 1682, ML_1M: 3952, ML_20M: 27278}
+
+# text encoding of each dataset's movies file (titles such as "Misérables" in latin-1)
+MOVIES_ENCODING = {ML_100K: "latin-1", ML_1M: "latin-1", ML_20M: "utf-8"}
 
 
 def get_path(data_dir, dataset_name, file_name):
@@ -87,7 +94,7 @@ def load_movies_data(data_dir, dataset_name, col_item_id="itemId", col_movie_tit
                      download=True):
     path = _resolve_or_fetch(data_dir, dataset_name, MOVIES_FILE_NAME[dataset_name], download)
     movies = _read_table(path, dataset_name, (col_item_id, col_movie_title),
-                         {col_item_id: np.int32}, (0, 1))
+                         {col_item_id: np.int32}, (0, 1), encoding=MOVIES_ENCODING[dataset_name])
     movies[col_item_id] = movies[col_item_id] - 1  # 1-based → 0-based
     return movies
 
@@ -108,13 +115,21 @@ def remap_item_ids(ratings_df, col_item_id="itemId", movies_df=None):
     """Dense 0-based item ids (new).  ml-20m movieIds reach ~131k
     while NUM_ITEMS['ml-20m'] is 27278, so the reference cannot gather them.
     Ids are mapped in the order of ``movies_df`` when given (27278 movies for
-    ml-20m), else in ascending raw-id order.  Returns (new_df, raw_ids)."""
+    ml-20m), else in ascending raw-id order.  Returns (new_df, raw_ids):
+    ``raw_ids[dense] = raw``.  A rating of a movie absent from ``movies_df``
+    raises ValueError."""
     raw = (np.asarray(movies_df[col_item_id]) if movies_df is not None
            else np.unique(np.asarray(ratings_df[col_item_id])))
-    lut = {int(r): i for i, r in enumerate(raw)}
+    ids = np.asarray(ratings_df[col_item_id])
+    order = np.argsort(raw, kind="stable")
+    pos = np.searchsorted(raw[order], ids)
+    pos = np.minimum(pos, max(len(raw) - 1, 0))
+    dense = order[pos] if len(raw) else pos
+    if ids.size and (len(raw) == 0 or not np.array_equal(raw[dense], ids)):
+        bad = ids[raw[dense] != ids] if len(raw) else ids
+        raise ValueError("item id {} not in the movies list".format(int(bad[0])))
     out = ratings_df.copy()
-    out[col_item_id] = np.asarray([lut[int(r)] for r in ratings_df[col_item_id]],
-                                  dtype=ratings_df[col_item_id].dtype)
+    out[col_item_id] = dense.astype(ratings_df[col_item_id].dtype)
     return out, raw
 
 

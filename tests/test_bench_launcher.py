@@ -1,0 +1,41 @@
+"""bench.py's multi-rank launch (CPU, gloo): ``python bench.py --gpus N`` outside torchrun
+starts N ranks itself and the one JSON line on stdout names N; under a launcher whose
+WORLD_SIZE differs from --gpus it refuses to run instead of benching the wrong rank count."""
+
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, env=None):
+    e = dict(os.environ)
+    e.update(env or {})
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        if env is None or k not in env:
+            e.pop(k, None)
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                          env=e, timeout=240, cwd=ROOT)
+
+
+def test_gpus_2_launches_two_ranks():
+    r = _run(["--gpus", "2", "--selftest-launch", "--steps", "3", "--warmup", "1"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, r.stdout          # exactly one line on stdout: rank 0's result
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["ranks"] == 2 and d["backend"] == "gloo"
+
+
+def test_gpus_must_match_world_size():
+    r = _run(["--gpus", "2", "--selftest-launch"], env={"RANK": "0", "WORLD_SIZE": "1", "LOCAL_RANK": "0"})
+    assert r.returncode != 0
+    assert "WORLD_SIZE" in r.stderr
+
+
+def test_single_rank_selftest():
+    r = _run(["--selftest-launch", "--steps", "2"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert json.loads(r.stdout.strip())["n_gpus"] == 1

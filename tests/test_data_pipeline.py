@@ -215,3 +215,68 @@ def test_remap_item_ids_dense():
     out, raw = ml.remap_item_ids(df)
     np.testing.assert_array_equal(out["itemId"].values, np.array([2, 0, 1], np.int32))
     np.testing.assert_array_equal(raw, np.array([1, 28, 131261]))
+
+
+def _write_ml20m(base, n_users=60, per_user=8, seed=0):
+    """ml-20m-format files (csv with headers; raw movieIds sparse up to 131262, 1-based)."""
+    rng = np.random.RandomState(seed)
+    movie_ids = np.unique(np.concatenate([rng.choice(np.arange(1, 131263), 300, replace=False), [131262, 1]]))
+    d = os.path.join(base, "ml-20m")
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, "movies.csv"), "w", encoding="utf-8") as f:
+        f.write("movieId,title,genres\n")
+        for m in movie_ids:
+            f.write('%d,Movie %d (1999),Drama\n' % (m, m))
+    rows = ["userId,movieId,rating,timestamp"]
+    ts = 0
+    for u in range(1, n_users + 1):
+        for m in rng.choice(movie_ids, per_user, replace=False):
+            ts += 1
+            rows.append("%d,%d,%.1f,%d" % (u, m, rng.randint(1, 11) / 2.0, ts))
+    with open(os.path.join(d, "ratings.csv"), "w") as f:
+        f.write("\n".join(rows) + "\n")
+    return movie_ids
+
+
+def test_ml20m_split_has_dense_item_ids(tmp_path):
+    """load_ratings_train_test_sets remaps ml-20m's raw movieIds (up to 131262) to dense ids in
+    movies.csv order, so every id fits NUM_ITEMS['ml-20m'] = 27278."""
+    from movierec.data_pipeline import load_ratings_train_test_sets
+    movie_ids = _write_ml20m(str(tmp_path))
+    raw = load_ratings_data(str(tmp_path), "ml-20m", download=False)
+    assert raw["itemId"].max() == 131261 or raw["itemId"].max() > 27278
+    train, val, test = load_ratings_train_test_sets("ml-20m", str(tmp_path), download=False)
+    lut = {int(m) - 1: i for i, m in enumerate(movie_ids)}       # 0-based raw -> position in movies.csv
+    both = pd.concat([train, val, test])
+    assert both["itemId"].max() < ml.NUM_ITEMS["ml-20m"]
+    # the split itself is unchanged: same rows, items renamed through the movies order
+    tr0, va0, te0 = __import__("movierec.data_pipeline", fromlist=["x"]).split_leave_two_out(raw)
+    for a, b in ((train, tr0), (val, va0), (test, te0)):
+        np.testing.assert_array_equal(a["userId"].values, b["userId"].values)
+        np.testing.assert_array_equal(a["itemId"].values, [lut[int(x)] for x in b["itemId"].values])
+    # remap_items=False keeps the reference's raw ids
+    tr, _, _ = load_ratings_train_test_sets("ml-20m", str(tmp_path), download=False, remap_items=False)
+    np.testing.assert_array_equal(tr["itemId"].values, tr0["itemId"].values)
+
+
+def test_remap_rejects_unknown_movie():
+    df = pd.DataFrame({"userId": np.array([0], np.int32), "itemId": np.array([5], np.int32)})
+    movies = pd.DataFrame({"itemId": np.array([1, 2], np.int32)})
+    with pytest.raises(ValueError):
+        ml.remap_item_ids(df, movies_df=movies)
+
+
+def test_movie_titles_decoded_latin1(tmp_path):
+    """ml-100k u.item and ml-1m movies.dat are latin-1 files; their titles decode (the
+    reference's load_movies_data, movielens_utils.py:85-101, reads them as utf-8 and fails)."""
+    d = tmp_path / "ml-1m"
+    d.mkdir()
+    (d / "movies.dat").write_bytes("1::Misérables, Les (1995)::Drama\n2::Señorita (2001)::Comedy\n".encode("latin-1"))
+    m = ml.load_movies_data(str(tmp_path), "ml-1m", download=False)
+    assert list(m["itemId"]) == [0, 1]
+    assert m["movieTitle"][0] == "Misérables, Les (1995)" and m["movieTitle"][1] == "Señorita (2001)"
+    d = tmp_path / "ml-100k"
+    d.mkdir()
+    (d / "u.item").write_bytes("1|Très Bien (1996)|01-Jan-1996||http://x|0|1\n".encode("latin-1"))
+    m = ml.load_movies_data(str(tmp_path), "ml-100k", download=False)
+    assert m["movieTitle"][0] == "Très Bien (1996)"

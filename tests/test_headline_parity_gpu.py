@@ -1,0 +1,148 @@
+"""Oracle parity of the benched code path at its real size (BASELINE config C).
+
+``bench.py`` trains config C (ml-20m tables: 138,493 users x 27,278 items, NeuMF gmf 64 + MLP
+[128, 64, 32, 16], 3 negatives per positive) at batch 65,536 with deferred-decay Adam and the
+next batch's index counted ahead.  At that batch the fused kernel runs 512 tiles of 128 samples
+on 256 workgroups, so every workgroup carries its weight-gradient, GMF and bias accumulators
+across tiles — a path the small-batch tests never reach.  These tests drive exactly that call
+sequence (``NCFEngine.train_step(..., next_batch=...)`` on device ids) and compare it with the
+numpy oracle (reference ``movierec/model.py:154-215``, Keras Adam v1 dense semantics).
+
+Tolerances (fp32 device vs float64 oracle, as in test_native_gpu.py):
+  * probabilities of each step's forward pass: |dp| <= 2e-6
+  * batch loss: relative 2e-5
+  * every weight tensor after k steps: |dw| <= k * 2e-6 + 2e-6 * max|w|
+"""
+
+import numpy as np
+import pytest
+
+from conftest import gpu_available
+from oracle import ncf_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+if gpu_available():
+    import torch
+    from movierec.engine import NCFEngine
+
+U, I, LAYERS, GMF = 138493, 27278, [128, 64, 32, 16], 64
+GROUP = 4
+HYPER = dict(optimizer="adam", lr=0.001, beta_1=0.9, beta_2=0.999, layers_l2reg=[0.0] * 4)
+
+
+def _batch(rng, B):
+    users = rng.randint(0, U, B // GROUP).repeat(GROUP).astype(np.int32)
+    items = rng.randint(0, I, B).astype(np.int32)
+    y = np.tile([0.0] * (GROUP - 1) + [1.0], B // GROUP).astype(np.float32)
+    return users, items, y
+
+
+def _dev(*arrays):
+    return tuple(torch.from_numpy(a).cuda().contiguous() for a in arrays)
+
+
+def test_config_c_full_size_matches_oracle():
+    """3 steps on the full ml-20m tables: two of batch 65,536 (the second counted ahead inside
+    the first, as bench.py runs them), then one of 40,964 = 320 x 128 + 4 samples (a partial
+    last tile, 321 tiles over 256 workgroups)."""
+    shape = O.NCFShape(U, I, LAYERS, GMF)
+    w = {k: v.astype(np.float32).astype(np.float64) for k, v in O.init_weights(shape, seed=17).items()}
+    rng = np.random.RandomState(18)
+    batches = [_batch(rng, 65536), _batch(rng, 65536), _batch(rng, 40964)]
+    dev = [_dev(*b) for b in batches]
+
+    eng = NCFEngine(U, I, LAYERS, GMF, max_batch=65536, lazy_adam=True)
+    assert eng.fast_path and eng.lazy
+    eng.set_keras_weights(w)
+    ref = {k: v.copy() for k, v in w.items()}
+    st = O.new_opt_state(ref)
+
+    losses = []
+    for s, (u, it, y) in enumerate(dev):
+        B = u.numel()
+        probs = torch.empty(B, dtype=torch.float32, device="cuda")
+        nxt = (dev[s + 1][0], dev[s + 1][1]) if s + 1 < len(dev) and dev[s + 1][0].numel() == B else None
+        eng.train_step(u, it, y, group=GROUP, k=2, probs_out=probs, next_batch=nxt)
+        loss, p_ref = O.train_step(shape, ref, st, *batches[s], HYPER)
+        losses.append(loss)
+        err = float(np.max(np.abs(probs.cpu().numpy() - p_ref)))
+        assert err <= 2e-6, "step %d probs: max err %g" % (s, err)
+    stats = NCFEngine.read_stats(eng.stats)
+    assert stats["steps"] == 3
+    assert stats["loss"] == pytest.approx(np.mean(losses), rel=2e-5)
+    got = eng.keras_weights()     # flushes the deferred decay first
+    steps = len(batches)
+    for name in O.weight_names(shape):
+        tol = steps * 2e-6 + 2e-6 * float(np.max(np.abs(ref[name])))
+        err = float(np.max(np.abs(got[name] - ref[name])))
+        assert err <= tol, "%s: max err %g > %g" % (name, err, tol)
+    assert int(eng.step.item()) == steps
+
+
+def test_config_c_full_size_grads_match_oracle():
+    """forward/backward gradients of one 65,536-sample batch on the full tables (the
+    multi-tile accumulators of every dense-layer and output-layer gradient), fp32 vs float64."""
+    shape = O.NCFShape(U, I, LAYERS, GMF)
+    w = {k: v.astype(np.float32).astype(np.float64) for k, v in O.init_weights(shape, seed=23).items()}
+    users, items, y = _batch(np.random.RandomState(24), 65536)
+    eng = NCFEngine(U, I, LAYERS, GMF, max_batch=65536)
+    eng.set_keras_weights(w)
+    grads = eng.alloc_grads()
+    eng.forward_backward(users, items, y, group=GROUP, k=2, inv_batch=1.0 / 65536, grads=grads)
+    _, g, _ = O.loss_and_grads(shape, w, users, items, y, [0.0] * 4)
+    got = eng.keras_weights(grads[0], grads[1])
+    for name in O.weight_names(shape):
+        scale = float(np.max(np.abs(g[name]))) + 1e-12
+        err = float(np.max(np.abs(got[name] - g[name])))
+        assert err <= 1e-5 * scale + 1e-12, "%s: max err %g (scale %g)" % (name, err, scale)
+
+
+def test_deferred_decay_long_gaps_bitwise():
+    """Deferred decay against the dense Keras sweep over 310 steps: rows whose gaps between
+    touches are 255, 256, 257 and 300 steps (the catch-up's per-block lr table covers the last
+    256 steps; longer gaps evaluate lr_t directly), rows touched once and then only settled by
+    the final flush, and a read (flush) in the middle.  Bitwise: emb, Adam moments, dense
+    layers, row_step."""
+    shape = O.NCFShape(200, 150, [128, 64, 32, 16], 64)
+    w = {k: v.astype(np.float32).astype(np.float64) for k, v in O.init_weights(shape, seed=31).items()}
+    dense = NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=64)
+    lazy = NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=64, lazy_adam=True)
+    ahead = NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=64, lazy_adam=True)
+    for e in (dense, lazy, ahead):
+        e.set_keras_weights(w)
+    # special rows: user -> steps at which it is touched
+    touches = {10: (0, 255), 11: (0, 256), 12: (0, 257), 13: (1, 301), 14: (0,), 15: (2, 150, 290)}
+    item_touches = {100: (0, 256), 101: (3, 260), 102: (1,)}
+    steps = 310
+    rng = np.random.RandomState(32)
+    batches = []
+    for s in range(steps):
+        # group 1: a filler user (rows 0..3, touched every few steps) with filler items 0..7
+        users = [s % 4] * GROUP
+        items = list(rng.randint(0, 8, GROUP))
+        # group 2: the special user of this step, if any, else filler user 5
+        su = [u for u, ts in touches.items() if s in ts]
+        users += [su[0] if su else 5] * GROUP
+        si = [v for v, ts in item_touches.items() if s in ts]
+        items += ([si[0]] if si else [int(rng.randint(0, 8))]) + list(rng.randint(0, 8, GROUP - 1))
+        y = [0.0] * (GROUP - 1) + [1.0]
+        batches.append(_dev(np.array(users, np.int32), np.array(items, np.int32), np.array(y * 2, np.float32)))
+    for s, (u, it, y) in enumerate(batches):
+        dense.train_step(u, it, y, group=GROUP, k=2)
+        lazy.train_step(u, it, y, group=GROUP, k=2)
+        nxt = (batches[s + 1][0], batches[s + 1][1]) if s + 1 < steps else None
+        ahead.train_step(u, it, y, group=GROUP, k=2, next_batch=nxt)
+        if s == 150:   # a read in the middle: flush (gaps < 256 at this point)
+            for e in (lazy, ahead):
+                e.predict(u, it)
+    for e in (lazy, ahead):
+        e.flush()
+    torch.cuda.synchronize()
+    for e in (lazy, ahead):
+        assert torch.equal(dense.emb, e.emb)
+        assert torch.equal(dense.emb_m, e.emb_m) and torch.equal(dense.emb_v, e.emb_v)
+        assert torch.equal(dense.mlp, e.mlp) and torch.equal(dense.mlp_m, e.mlp_m)
+        assert int(e.row_step.min()) == int(e.row_step.max()) == steps == int(e.step.item())
+    assert NCFEngine.read_stats(dense.stats) == NCFEngine.read_stats(lazy.stats)
+    assert gpu_available()

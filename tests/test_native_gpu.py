@@ -422,3 +422,44 @@ def test_count_ahead_equals_plain_steps():
     torch.cuda.synchronize()
     for x, y in ((a.emb, b.emb), (a.emb_m, b.emb_m), (a.emb_v, b.emb_v), (a.mlp, b.mlp), (a.stats, b.stats)):
         assert torch.equal(x, y)
+
+
+def test_counted_ahead_ids_changed_in_place():
+    """A counted-ahead batch refilled in place before its step (a staging pattern): through torch
+    (version bump) the engine rebuilds the index — bitwise the plain steps; behind torch's back
+    (.data writes, or a kernel writing the pointer) the device guard keeps every list write inside
+    its key's slots, clears the counters and reports NCF_WSERR_STALE_COUNT (check_errors raises);
+    the engine keeps working afterwards."""
+    shape = O.NCFShape(*SHAPES[3])
+    w = _weights(shape, 60)
+    bt = []
+    for s in range(4):
+        users, items, y = _batch(shape, 256, 4, 61 + s)
+        bt.append((torch.from_numpy(users).cuda(), torch.from_numpy(items).cuda(), torch.from_numpy(y).cuda()))
+    a = _engine(shape, w, lazy_adam=True)
+    b = _engine(shape, w, lazy_adam=True)
+    stage = (bt[1][0].clone(), bt[1][1].clone())
+    a.train_step(*bt[0], group=4, k=2, next_batch=stage)
+    stage[1].copy_(bt[2][1])             # refill through torch: _version moves
+    stage[0].copy_(bt[2][0])
+    a.train_step(stage[0], stage[1], bt[2][2], group=4, k=2)
+    b.train_step(*bt[0], group=4, k=2)
+    b.train_step(*bt[2], group=4, k=2)
+    a.check_errors()                     # nothing flagged
+    a.flush()
+    b.flush()
+    assert torch.equal(a.emb, b.emb) and torch.equal(a.emb_m, b.emb_m) and torch.equal(a.mlp, b.mlp)
+    # behind torch's back: the version counter does not move
+    stage2 = (bt[3][0].clone(), bt[3][1].clone())
+    a.train_step(*bt[1], group=4, k=2, next_batch=stage2)
+    v = stage2[1]._version
+    stage2[1].data.copy_(bt[0][1])
+    assert stage2[1]._version == v
+    a.train_step(stage2[0], stage2[1], bt[3][2], group=4, k=2)
+    with pytest.raises(RuntimeError):
+        a.check_errors()
+    a.check_errors()                     # cleared by the read
+    for s in range(2):                   # counters were cleared on the device: later builds are sound
+        a.train_step(*bt[s], group=4, k=2)
+    a.check_errors()
+    assert torch.isfinite(a.emb).all()

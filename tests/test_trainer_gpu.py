@@ -63,3 +63,26 @@ def test_trainer_end_to_end(tmp_path):
     p1, _ = loaded.model.predict_on_batch([users, items])
     np.testing.assert_array_equal(p0, p1)
     assert gpu_available()
+
+
+def test_trainer_ml20m_format(tmp_path):
+    """trainer.train(..., "ml-20m") on ml-20m-format files whose raw movieIds reach 131262
+    (csv with headers, movies.csv in movieId order): the split remaps the items to dense ids
+     and training runs to completion over the full 138,493 x 27,278 tables."""
+    import random
+    from movierec import trainer
+    from movierec.model import MovierecModel
+    from test_data_pipeline import _write_ml20m
+    data_dir, out_dir = str(tmp_path / "data"), str(tmp_path / "models")
+    _write_ml20m(data_dir, n_users=300, per_user=12, seed=3)
+    np.random.seed(1)
+    random.seed(1)
+    params = dict(trainer.DEFAULT_PARAMS)
+    params.update(batch_size=400, num_negs_per_pos=3, batch_size_eval=200, num_negs_per_pos_eval=99, k=4,
+                  epochs=2, gmf_dim=8, seed=2)
+    model, history = trainer.train("ml20m", "ml-20m", data_dir, out_dir, params, verbose=0)
+    assert params["num_users"] == 138493 and params["num_items"] == 27278
+    h = history.history
+    assert len(h["loss"]) == 2 and all(np.isfinite(h["loss"])) and all(np.isfinite(h["val_output_hr"]))
+    assert os.path.exists(MovierecModel.get_model_weights_path(out_dir, "ml20m"))
+    assert gpu_available()

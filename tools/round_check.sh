@@ -18,4 +18,4 @@ import csv
 for r in csv.DictReader(open("$OUT/trace/run_kernel_stats.csv")):
     print("%-60s %5s %10.1f" % (r["Name"][:60], r["Calls"], float(r["AverageNs"]) / 1e3))
 PY
-cat $OUT/traffic_*.json
+cat $OUT/traffic/*.json
