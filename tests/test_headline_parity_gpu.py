@@ -11,7 +11,19 @@ numpy oracle (reference ``movierec/model.py:154-215``, Keras Adam v1 dense seman
 Tolerances (fp32 device vs float64 oracle, as in test_native_gpu.py):
   * probabilities of each step's forward pass: |dp| <= 2e-6
   * batch loss: relative 2e-5
+  * gradients: |dg| <= 1e-5 * max|g|
   * every weight tensor after k steps: |dw| <= k * 2e-6 + 2e-6 * max|w|
+
+Batches are drawn away from the ReLU kinks.  A hidden unit whose pre-activation lies within
+fp32 rounding of zero (~3e-9 here) can take the other side of the kink on the device than in
+float64; its backward gradient (and so the sample's embedding-gradient rows and its share of
+the dense-layer gradients) then legitimately differs while its forward contribution (~z) does
+not.  At 65,536 samples x 112 hidden units (pre-activations ~1e-2 at Keras initialisation) a
+uniform batch has ~100 such samples, and they dominate the deviations: measured on MI355X with
+tools/parity_debug.py on unfiltered batches, every element above tolerance belonged to a row
+of such a sample (or of a sample reading such a row later), every other element was within
+5e-9.  So, as a finite-difference check would, the tests keep only user groups whose samples
+all have |z| >= 1e-6 for every hidden unit under the oracle's weights of that step.
 """
 
 import numpy as np
@@ -31,11 +43,42 @@ GROUP = 4
 HYPER = dict(optimizer="adam", lr=0.001, beta_1=0.9, beta_2=0.999, layers_l2reg=[0.0] * 4)
 
 
-def _batch(rng, B):
-    users = rng.randint(0, U, B // GROUP).repeat(GROUP).astype(np.int32)
-    items = rng.randint(0, I, B).astype(np.int32)
-    y = np.tile([0.0] * (GROUP - 1) + [1.0], B // GROUP).astype(np.float32)
-    return users, items, y
+def _pre_activations(shape, w, users, items):
+    h = np.concatenate([w["user_embedding"][users], w["item_embedding"][items]], axis=1)
+    m = np.full(len(users), np.inf)
+    for l in range(1, shape.n):
+        z = h @ w["hidden_%d/kernel" % l] + w["hidden_%d/bias" % l]
+        m = np.minimum(m, np.abs(z).min(axis=1))
+        h = np.maximum(z, 0)
+    return m
+
+
+def _batch_off_kinks(shape, w, rng, B, margin=1e-6):
+    """A batch of B samples (groups of GROUP sharing a user) whose every hidden pre-activation
+    under weights ``w`` is at least ``margin`` away from 0; returns it and the count of groups
+    dropped."""
+    need = B // GROUP
+    ku, ki = [], []
+    dropped = 0
+    while sum(len(x) for x in ku) < need:
+        n = need + need // 8
+        users = rng.randint(0, U, n).repeat(GROUP)
+        items = rng.randint(0, I, n * GROUP)
+        ok = (_pre_activations(shape, w, users, items) >= margin).reshape(n, GROUP).all(axis=1)
+        dropped += int((~ok).sum())
+        ku.append(users.reshape(n, GROUP)[ok])
+        ki.append(items.reshape(n, GROUP)[ok])
+    users = np.concatenate(ku)[:need].reshape(-1).astype(np.int32)
+    items = np.concatenate(ki)[:need].reshape(-1).astype(np.int32)
+    y = np.tile([0.0] * (GROUP - 1) + [1.0], need).astype(np.float32)
+    return (users, items, y), dropped
+
+
+def _check_weights(shape, got, ref, steps):
+    for name in O.weight_names(shape):
+        tol = steps * 2e-6 + 2e-6 * float(np.max(np.abs(ref[name])))
+        err = float(np.max(np.abs(np.asarray(got[name], np.float64) - ref[name])))
+        assert err <= tol, "%s: max err %g > %g" % (name, err, tol)
 
 
 def _dev(*arrays):
@@ -49,35 +92,33 @@ def test_config_c_full_size_matches_oracle():
     shape = O.NCFShape(U, I, LAYERS, GMF)
     w = {k: v.astype(np.float32).astype(np.float64) for k, v in O.init_weights(shape, seed=17).items()}
     rng = np.random.RandomState(18)
-    batches = [_batch(rng, 65536), _batch(rng, 65536), _batch(rng, 40964)]
+    # the oracle runs first: each batch is drawn off the kinks of the weights it will meet
+    ref = {k: v.copy() for k, v in w.items()}
+    st = O.new_opt_state(ref)
+    batches, outs = [], []
+    for B in (65536, 65536, 40964):
+        b, dropped = _batch_off_kinks(shape, ref, rng, B)
+        assert dropped < 0.1 * B / GROUP, dropped
+        batches.append(b)
+        outs.append(O.train_step(shape, ref, st, *b, HYPER))
     dev = [_dev(*b) for b in batches]
 
     eng = NCFEngine(U, I, LAYERS, GMF, max_batch=65536, lazy_adam=True)
     assert eng.fast_path and eng.lazy
     eng.set_keras_weights(w)
-    ref = {k: v.copy() for k, v in w.items()}
-    st = O.new_opt_state(ref)
-
-    losses = []
     for s, (u, it, y) in enumerate(dev):
         B = u.numel()
         probs = torch.empty(B, dtype=torch.float32, device="cuda")
         nxt = (dev[s + 1][0], dev[s + 1][1]) if s + 1 < len(dev) and dev[s + 1][0].numel() == B else None
         eng.train_step(u, it, y, group=GROUP, k=2, probs_out=probs, next_batch=nxt)
-        loss, p_ref = O.train_step(shape, ref, st, *batches[s], HYPER)
-        losses.append(loss)
-        err = float(np.max(np.abs(probs.cpu().numpy() - p_ref)))
+        err = float(np.max(np.abs(probs.cpu().numpy() - outs[s][1])))
         assert err <= 2e-6, "step %d probs: max err %g" % (s, err)
     stats = NCFEngine.read_stats(eng.stats)
     assert stats["steps"] == 3
-    assert stats["loss"] == pytest.approx(np.mean(losses), rel=2e-5)
+    assert stats["loss"] == pytest.approx(np.mean([o[0] for o in outs]), rel=2e-5)
     got = eng.keras_weights()     # flushes the deferred decay first
-    steps = len(batches)
-    for name in O.weight_names(shape):
-        tol = steps * 2e-6 + 2e-6 * float(np.max(np.abs(ref[name])))
-        err = float(np.max(np.abs(got[name] - ref[name])))
-        assert err <= tol, "%s: max err %g > %g" % (name, err, tol)
-    assert int(eng.step.item()) == steps
+    _check_weights(shape, got, ref, len(batches))
+    assert int(eng.step.item()) == len(batches)
 
 
 def test_config_c_full_size_grads_match_oracle():
@@ -85,7 +126,7 @@ def test_config_c_full_size_grads_match_oracle():
     multi-tile accumulators of every dense-layer and output-layer gradient), fp32 vs float64."""
     shape = O.NCFShape(U, I, LAYERS, GMF)
     w = {k: v.astype(np.float32).astype(np.float64) for k, v in O.init_weights(shape, seed=23).items()}
-    users, items, y = _batch(np.random.RandomState(24), 65536)
+    (users, items, y), _ = _batch_off_kinks(shape, w, np.random.RandomState(24), 65536)
     eng = NCFEngine(U, I, LAYERS, GMF, max_batch=65536)
     eng.set_keras_weights(w)
     grads = eng.alloc_grads()
