@@ -55,6 +55,9 @@ HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 FP32_MFMA_PEAK_TFS = 157.3   # dense fp32 MFMA peak (v_mfma_f32_32x32x2_f32), MI355X_MICROARCH.md
 
 CONFIGS = {
+    "A": dict(workload="ml-100k GMF-only (config A): 943 users x 1682 items, GMF d=8 (no MLP), 3 neg/pos, "
+                       "batch 256 (the reference's CPU plumbing case; generic per-sample kernel)",
+              num_users=943, num_items=1682, layers=[], gmf_dim=8, negs=3, batch=256),
     "C": dict(workload="ml-20m NeuMF (config C): 138493 users x 27278 items, gmf 64 + MLP [128,64,32,16], "
                        "3 neg/pos, Adam dense",
               num_users=138493, num_items=27278, layers=[128, 64, 32, 16], gmf_dim=64, negs=3, batch=65536),
@@ -136,7 +139,7 @@ def fwd_bwd_flops(cfg):
     weight gradients (dW_l, output kernel)."""
     L, G = cfg["layers"], cfg["gmf_dim"]
     mlp = sum(a * b for a, b in zip(L[:-1], L[1:]))
-    out = G + L[-1]
+    out = G + (L[-1] if L else 0)
     fwd = mlp + out + G
     bwd_data = mlp + G * 2 + out
     dw = mlp + out
@@ -570,6 +573,7 @@ def main():
 
     # HR@10 on a synthetic validation set (1 positive + 99 sampled items per user), per rank
     ev_users = 2000
+    eval_ms = None
     ev_base = 0 if mode == "user" else rank * ev_users   # user mode: this rank's own (local) users
     ev_u = (torch.arange(ev_users, device="cuda", dtype=torch.int32) + ev_base).repeat_interleave(100)
     ev_i = torch.randint(0, cfg["num_items"], (ev_users * 100,), generator=gen, device="cuda", dtype=torch.int32)
@@ -581,6 +585,12 @@ def main():
     else:
         st = eng.val_stats.new_zeros(eng.val_stats.shape)
         eng.evaluate(ev_u, ev_i, ev_y, group=100, k=10, stats=st)
+        torch.cuda.synchronize()
+        t_ev = time.perf_counter()
+        for _ in range(5):
+            eng.evaluate(ev_u, ev_i, ev_y, group=100, k=10, stats=eng.val_stats.new_zeros(eng.val_stats.shape))
+        torch.cuda.synchronize()
+        eval_ms = (time.perf_counter() - t_ev) / 5 * 1e3
         r = NCFEngine.read_stats(st)
         hd = torch.tensor([r["hr"] * ev_users, r["dcg"] * ev_users], dtype=torch.float64, device="cuda")
     if dist.is_initialized():
@@ -687,7 +697,9 @@ def main():
             "cpu_baseline": cpu,
             "cpu_baseline_with_sampler": cpu_e2e,
             "hr_at_10": {"value": round(hr["hr"], 4), "ndcg_at_10": round(hr["dcg"], 4),
-                         "data": "synthetic eval groups (random ids; ~0.1 expected for an untrained model)"},
+                         "data": "synthetic eval groups (random ids; ~0.1 expected for an untrained model)",
+                         "eval_samples": ev_users * 100,
+                         "eval_ms": round(eval_ms, 4) if eval_ms is not None else None},
         }
         if exchange is not None:
             line["exchange"] = exchange

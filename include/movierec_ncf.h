@@ -57,6 +57,7 @@ extern "C" {
 #define NCF_STAT_LAST_LOSS 4
 #define NCF_STAT_LAST_HR 5
 #define NCF_STAT_LAST_DCG 6
+#define NCF_STAT_BCE_SUM 7    /* sum over steps of the batch BCE mean alone (Keras' output_loss) */
 #define NCF_NUM_STATS 8
 
 /* summary of one forward/backward (float[NCF_NUM_SUMMARY], device);
@@ -72,7 +73,7 @@ typedef struct ncf_shape {
     /* inputs (MovierecModel params: num_users, num_items, layers_sizes; gmf_dim = NeuMF extension) */
     int32_t num_users;
     int32_t num_items;
-    int32_t num_layers;                 /* len(layers_sizes) >= 1 */
+    int32_t num_layers;                 /* len(layers_sizes); 0 = GMF-only model (needs gmf_dim > 0) */
     int32_t gmf_dim;                    /* 0 = the reference's MLP-only model */
     int32_t layers[NCF_MAX_LAYERS];
     /* derived by ncf_shape_init */
@@ -129,7 +130,9 @@ int ncf_abi_version(void);
 const char* ncf_last_error(void);
 
 /* Validate the model dimensions and fill the derived fields.
- * Replaces the shape checks of MovierecModel.__init__ (model.py:73-80). */
+ * Replaces the shape checks of MovierecModel.__init__ (model.py:73-80).  num_layers == 0 with
+ * gmf_dim > 0 is the GMF-only model (BASELINE config A; an extension like the GMF branch):
+ * p = sigmoid(w . (u_gmf * i_gmf) + b); `layers` may then be NULL. */
 int ncf_shape_init(ncf_shape_t* shape, int32_t num_users, int32_t num_items, const int32_t* layers,
                    int32_t num_layers, int32_t gmf_dim);
 

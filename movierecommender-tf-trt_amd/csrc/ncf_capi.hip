@@ -157,6 +157,14 @@ bool use_fused(const ncf_shape_t& s, const ncf_hyper_t* h) {
     return s.fast_path && !(h && h->force_generic) && ncf::fused_supported(s);
 }
 
+// forward only: the fused MFMA forward when the shape has it, else the generic per-sample kernel
+hipError_t launch_predict(const ncf_shape_t& s, const ncf_hyper_t* h, const ncf::WsLayout& L, void* ws,
+                          const float* emb, const float* mlp, const int32_t* users, const int32_t* items,
+                          const float* labels, int64_t n, float* probs, ncf::IdSpace ids, int* nbce, hipStream_t st) {
+    if (use_fused(s, h)) return ncf::launch_fwd_fused(s, L, ws, emb, mlp, users, items, labels, n, probs, ids, nbce, st);
+    return ncf::launch_predict_generic(s, L, ws, emb, mlp, users, items, labels, n, probs, ids, nbce, st);
+}
+
 // Shapes the fused kernel does not hold: the layer-by-layer GEMM path when the dense weights
 // outgrow the generic kernel's LDS staging (config D), or when asked for (force_generic == 2);
 // the per-sample generic kernel for small models (the reference's test shapes) or force_generic == 1.
@@ -250,27 +258,31 @@ const char* ncf_last_error(void) { return g_err.c_str(); }
 
 int ncf_shape_init(ncf_shape_t* s, int32_t num_users, int32_t num_items, const int32_t* layers, int32_t num_layers,
                    int32_t gmf_dim) {
-    if (!s || !layers) return fail(NCF_EINVAL, "NULL argument");
-    if (num_layers < 1 || num_layers > NCF_MAX_LAYERS)
-        return fail(NCF_EINVAL, "num_layers must be in [1, %d], got %d", NCF_MAX_LAYERS, num_layers);
+    if (!s || (num_layers > 0 && !layers)) return fail(NCF_EINVAL, "NULL argument");
+    if (num_layers < 0 || num_layers > NCF_MAX_LAYERS)
+        return fail(NCF_EINVAL, "num_layers must be in [0, %d], got %d", NCF_MAX_LAYERS, num_layers);
+    if (num_layers == 0 && gmf_dim <= 0)
+        return fail(NCF_EINVAL, "a model needs an MLP (layers_sizes) or a GMF branch (gmf_dim > 0)");
     if (num_users <= 0 || num_items <= 0) return fail(NCF_EINVAL, "num_users and num_items must be > 0");
     if (gmf_dim < 0) return fail(NCF_EINVAL, "gmf_dim must be >= 0");
     for (int l = 0; l < num_layers; ++l)
         if (layers[l] <= 0) return fail(NCF_EINVAL, "layers_sizes[%d] must be > 0", l);
-    if (layers[0] < 2) return fail(NCF_EINVAL, "layers_sizes[0] must be >= 2 (user and item halves)");
+    if (num_layers > 0 && layers[0] < 2) return fail(NCF_EINVAL, "layers_sizes[0] must be >= 2 (user and item halves)");
     memset(s, 0, sizeof(*s));
     s->num_users = num_users;
     s->num_items = num_items;
     s->num_layers = num_layers;
     s->gmf_dim = gmf_dim;
     for (int l = 0; l < num_layers; ++l) s->layers[l] = layers[l];
-    s->du = layers[0] / 2;
-    s->di = layers[0] - s->du;
+    // GMF-only model (num_layers == 0, BASELINE config A): no MLP embedding halves, the output
+    // layer reads the GMF product alone
+    s->du = num_layers > 0 ? layers[0] / 2 : 0;
+    s->di = num_layers > 0 ? layers[0] - s->du : 0;
     s->gmf_stride = (gmf_dim + 3) / 4 * 4;
     const int mlpw = ((s->du > s->di ? s->du : s->di) + 3) / 4 * 4;
     s->row_width = s->gmf_stride + mlpw;
     s->num_rows = (int64_t)num_users + num_items;
-    s->out_features = gmf_dim + layers[num_layers - 1];
+    s->out_features = gmf_dim + (num_layers > 0 ? layers[num_layers - 1] : 0);
     int off = 0;
     for (int l = 1; l < num_layers; ++l) {
         s->layer_off[l] = off;
@@ -326,8 +338,8 @@ int ncf_predict(const ncf_shape_t* s, const ncf_model_t* model, const int32_t* u
     if (!model || !model->emb || !model->mlp || !users || !items || !probs)
         return fail(NCF_EINVAL, "NULL device pointer");
     int nbce = 0;
-    return hip_check(ncf::launch_predict_generic(*s, L, ws, model->emb, model->mlp, users, items, nullptr, n, probs,
-                                                 ncf::table_ids(*s), &nbce, (hipStream_t)stream),
+    return hip_check(launch_predict(*s, nullptr, L, ws, model->emb, model->mlp, users, items, nullptr, n, probs,
+                                    ncf::table_ids(*s), &nbce, (hipStream_t)stream),
                      "ncf_predict");
 }
 
@@ -650,8 +662,8 @@ int ncf_evaluate(const ncf_shape_t* s, const ncf_model_t* model, const ncf_hyper
     hipStream_t st = (hipStream_t)stream;
     float* probs = ncf::at<float>(ws, L.probs);
     int nbce = 0;
-    hipError_t e = ncf::launch_predict_generic(*s, L, ws, model->emb, model->mlp, users, items, labels, n, probs,
-                                               ncf::table_ids(*s), &nbce, st);
+    hipError_t e = launch_predict(*s, h, L, ws, model->emb, model->mlp, users, items, labels, n, probs,
+                                  ncf::table_ids(*s), &nbce, st);
     if (e != hipSuccess) return hip_check(e, "forward");
     const int64_t ng = n / h->group;
     int nmet = 0;
@@ -972,8 +984,8 @@ int ncf_score_topk(const ncf_shape_t* s, const ncf_model_t* model, const int32_t
         e = ncf::launch_score_pairs(users + q0, nq, I, pu, pi, st);
         if (e != hipSuccess) return hip_check(e, "score pairs");
         int nbce = 0;
-        e = ncf::launch_predict_generic(*s, PL, pws, model->emb, model->mlp, pu, pi, nullptr, nq * I, probs,
-                                        ncf::table_ids(*s), &nbce, st);
+        e = launch_predict(*s, nullptr, PL, pws, model->emb, model->mlp, pu, pi, nullptr, nq * I, probs,
+                           ncf::table_ids(*s), &nbce, st);
         if (e != hipSuccess) return hip_check(e, "score forward");
         e = ncf::launch_topk_rows(probs, nq, I, k, top_items + q0 * k, top_scores + q0 * k, st);
         if (e != hipSuccess) return hip_check(e, "score top-k");

@@ -776,6 +776,161 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
 }
 
 // ---------------------------------------------------------------------------
+// Forward only (ncf_predict / ncf_evaluate: Model.predict_on_batch output[0], the validation
+// pass of fit_generator, model.py:184-194, 329-333): the forward chain of k_fb_fused with no
+// staging, no masks and no backward.  LDS holds the dense weights only (WLDS floats), so two
+// workgroups share a CU; 128-sample tiles, persistent grid.  With labels: one Keras-BCE partial
+// per workgroup (fixed order: wave sums, then the 4 waves in order).
+
+template <class S>
+__global__ __launch_bounds__(kBlock, 2) void k_fwd_fused(const float* __restrict__ emb, const float* __restrict__ mlp,
+                                                         const int32_t* __restrict__ users,
+                                                         const int32_t* __restrict__ items,
+                                                         const float* __restrict__ labels, int64_t n, IdSpace ids,
+                                                         float* __restrict__ probs, float* __restrict__ part_bce) {
+    constexpr int L1 = S::L1, L2 = S::L2, L3 = S::L3, G = S::G, D0 = S::D0, W = S::W;
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    float* wl = lds;
+    __shared__ float red[4];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const float eps = 1e-7f, hi_clip = 1.0f - eps;
+    for (int e = tid; e < S::L0 * L1; e += kBlock) wl[S::SW1 + (e / L1) * S::LW1 + e % L1] = mlp[S::OW1 + e];
+    for (int e = tid; e < L1 * L2; e += kBlock) wl[S::SW2 + (e / L2) * S::LW2 + e % L2] = mlp[S::OW2 + e];
+    for (int e = tid; e < L2 * L3; e += kBlock) wl[S::SW3 + (e / L3) * S::LW3 + e % L3] = mlp[S::OW3 + e];
+    for (int e = tid; e < L1; e += kBlock) wl[S::SB1 + e] = mlp[S::OB1 + e];
+    for (int e = tid; e < L2; e += kBlock) wl[S::SB2 + e] = mlp[S::OB2 + e];
+    for (int e = tid; e < L3; e += kBlock) wl[S::SB3 + e] = mlp[S::OB3 + e];
+    for (int e = tid; e < G + L3 + 1; e += kBlock) wl[S::SWO + e] = mlp[S::OWO + e];
+    __syncthreads();
+
+    float acc_bce = 0.f;
+    const int64_t niter = (n + 127) / 128;
+    for (int64_t it = blockIdx.x; it < niter; it += gridDim.x) {
+        int lane_t = lane;
+        asm volatile("" : "+v"(lane_t));
+        const int j = lane_t & 31, h = lane_t >> 5;
+        const int64_t si = it * 128 + 32 * w + j;
+        const bool inb = si < n;
+        int u = 0, v = 0;
+        if (inb) {
+            u = users[si];
+            v = items[si];
+        }
+        const bool ok = inb && (unsigned)u < (unsigned)ids.ubound && (unsigned)v < (unsigned)ids.ibound;
+        const float* eu = emb + (size_t)(ok ? u : 0) * W;
+        const float* ei = emb + (size_t)(ok ? ids.ibase + v : 0) * W;
+        float4 xv[D0 / 4];
+        {
+            const float4* src = reinterpret_cast<const float4*>((h ? ei : eu) + G);
+#pragma unroll
+            for (int q = 0; q < D0 / 4; ++q) xv[q] = src[q];
+        }
+        float zp = 0.f;
+        if constexpr (G > 0) {
+            const float4* us = reinterpret_cast<const float4*>(eu + h * S::GH);
+            const float4* is = reinterpret_cast<const float4*>(ei + h * S::GH);
+            const float* wo = wl + S::SWO + h * S::GH;
+#pragma unroll
+            for (int q = 0; q < S::GH / 4; ++q) {
+                const float4 a = us[q], b = is[q];
+                zp += wo[4 * q] * (a.x * b.x) + wo[4 * q + 1] * (a.y * b.y) + wo[4 * q + 2] * (a.z * b.z) +
+                      wo[4 * q + 3] * (a.w * b.w);
+            }
+        }
+        // layer 1 (A = W1[k][out] from LDS, B = the gathered MLP vector, K order h*D0 + s)
+        f32x16 h1[S::NT1];
+        {
+            f32x16 acc[S::NT1];
+#pragma unroll
+            for (int to = 0; to < S::NT1; ++to) acc[to] = f32x16{};
+            float ab[2][4][S::NT1];
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int to = 0; to < S::NT1; ++to) {
+                    const int oc = 32 * to + j;
+                    ab[0][e][to] = oc < L1 ? wl[S::SW1 + (h * D0 + e) * S::LW1 + oc] : 0.f;
+                }
+#pragma unroll
+            for (int c = 0; c < D0 / 4; ++c) {
+                if (c + 1 < D0 / 4) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+#pragma unroll
+                        for (int to = 0; to < S::NT1; ++to) {
+                            const int oc = 32 * to + j;
+                            ab[(c + 1) & 1][e][to] =
+                                oc < L1 ? wl[S::SW1 + (h * D0 + 4 * (c + 1) + e) * S::LW1 + oc] : 0.f;
+                        }
+                }
+                NCF_SB();
+                const float xs[4] = {xv[c].x, xv[c].y, xv[c].z, xv[c].w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+#pragma unroll
+                    for (int to = 0; to < S::NT1; ++to) acc[to] = mfma32(ab[c & 1][e][to], xs[e], acc[to]);
+                NCF_SB();
+            }
+#pragma unroll
+            for (int to = 0; to < S::NT1; ++to)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int f = 32 * to + drow(r, h);
+                    h1[to][r] = (f < L1) ? fmaxf(acc[to][r] + wl[S::SB1 + f], 0.f) : 0.f;
+                }
+        }
+        f32x16 h2[S::NT2];
+#pragma unroll
+        for (int to = 0; to < S::NT2; ++to) {
+            const int oc = 32 * to + j;
+            const f32x16 acc = mchain<S::NS1, 4>(
+                f32x16{},
+                [&](int t) {
+                    const int k = 32 * (t / 16) + drow(t % 16, h);
+                    return (oc < L2 && k < L1) ? wl[S::SW2 + k * S::LW2 + oc] : 0.f;
+                },
+                [&](int t) { return h1[t / 16][t % 16]; });
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int f = 32 * to + drow(r, h);
+                h2[to][r] = (f < L2) ? fmaxf(acc[r] + wl[S::SB2 + f], 0.f) : 0.f;
+            }
+        }
+#pragma unroll
+        for (int to = 0; to < S::NT3; ++to) {
+            const int oc = 32 * to + j;
+            const f32x16 acc = mchain<S::NS2, 4>(
+                f32x16{},
+                [&](int t) {
+                    const int k = 32 * (t / 16) + drow(t % 16, h);
+                    return (oc < L3 && k < L2) ? wl[S::SW3 + k * S::LW3 + oc] : 0.f;
+                },
+                [&](int t) { return h2[t / 16][t % 16]; });
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int f = 32 * to + drow(r, h);
+                if (f < L3) zp += wl[S::SWO + G + f] * fmaxf(acc[r] + wl[S::SB3 + f], 0.f);
+            }
+        }
+        const float z = (zp + __shfl_xor(zp, 32, 64)) + wl[S::SBO];
+        const float p = 1.0f / (1.0f + expf(-z));
+        if (h == 0 && inb) {
+            probs[si] = ok ? p : __int_as_float(0x7fc00000);
+            if (labels && ok) {
+                const float y = labels[si];
+                const float pc = fminf(fmaxf(p, eps), hi_clip);
+                const float logit = logf(pc / (1.0f - pc));
+                acc_bce += fmaxf(logit, 0.0f) - logit * y + log1pf(expf(-fabsf(logit)));
+            }
+        }
+    }
+    if (part_bce) {
+        const float b = block_sum_256(acc_bce, red);
+        if (tid == 0) part_bce[blockIdx.x] = b;
+    }
+}
+
+// ---------------------------------------------------------------------------
 
 using ShapeC = FShape<128, 64, 32, 16, 64>;   // ml-20m NeuMF (config C)
 using ShapeB = FShape<64, 32, 16, 8, 8>;      // ml-1m NeuMF (config B)
@@ -827,6 +982,33 @@ hipError_t launch_fb_fused(const ncf_shape_t& s, const WsLayout& L, void* ws, co
     if (matches<SH>(s))                                                                                         \
     return launch_one<SH>(s, L, ws, emb, mlp, users, items, labels, n, inv_batch, ids, group, topk, nslab, nbce, \
                           nmet, st)
+    NCF_TRY(ShapeC);
+    NCF_TRY(ShapeB);
+    NCF_TRY(ShapeR);
+    NCF_TRY(ShapeC0);
+#undef NCF_TRY
+    return hipErrorNotSupported;
+}
+
+template <class S>
+static hipError_t launch_fwd_one(const float* emb, const float* mlp, const int32_t* users, const int32_t* items,
+                                 const float* labels, int64_t n, IdSpace ids, float* probs, float* part_bce,
+                                 int* nbce, hipStream_t st) {
+    const int64_t niter = (n + 127) / 128;
+    int grid = (int)(niter < 512 ? niter : 512);  // two workgroups per CU, persistent
+    if (grid > kMaxSlabs) grid = kMaxSlabs;
+    launch(k_fwd_fused<S>, grid, kBlock, (size_t)S::WLDS * 4, st, emb, mlp, users, items, labels, n, ids, probs,
+           labels ? part_bce : nullptr);
+    *nbce = labels ? grid : 0;
+    return hipGetLastError();
+}
+
+hipError_t launch_fwd_fused(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, const float* mlp,
+                            const int32_t* users, const int32_t* items, const float* labels, int64_t n,
+                            float* probs, IdSpace ids, int* nbce, hipStream_t st) {
+    float* part = at<float>(ws, L.part_bce);
+#define NCF_TRY(SH) \
+    if (matches<SH>(s)) return launch_fwd_one<SH>(emb, mlp, users, items, labels, n, ids, probs, part, nbce, st)
     NCF_TRY(ShapeC);
     NCF_TRY(ShapeB);
     NCF_TRY(ShapeR);

@@ -112,8 +112,10 @@ __global__ __launch_bounds__(kBlock) void k_fb_generic(GenShape S, const float* 
                 a[S.gmf_off + f] = gm;
                 z += gm * wo[f];
             }
-            const float* hl = a + S.act_off[S.n - 1];
-            for (int o = 0; o < S.L[S.n - 1]; ++o) z += hl[o] * wo[S.G + o];
+            if (S.n > 0) {  // n == 0: GMF-only model
+                const float* hl = a + S.act_off[S.n - 1];
+                for (int o = 0; o < S.L[S.n - 1]; ++o) z += hl[o] * wo[S.G + o];
+            }
             z += wo[S.F];
             p = 1.0f / (1.0f + expf(-z));
         } else {
@@ -162,7 +164,7 @@ __global__ __launch_bounds__(kBlock) void k_fb_generic(GenShape S, const float* 
                             gi[S.G4 + k - S.du] = s;
                     }
                 }
-            } else {
+            } else if (S.n == 1) {
                 for (int k = 0; k < S.L[0]; ++k) {
                     const float s = dzo * wo[S.G + k];
                     if (k < S.du) gu[S.G4 + k] = s;
@@ -205,7 +207,7 @@ __global__ __launch_bounds__(kBlock) void k_dw_generic(GenShape S, const float* 
         const int q = p - S.off[0];
         dcol = S.D - 1;
         if (q < S.F)
-            ain = (q < S.G) ? S.gmf_off + q : S.act_off[S.n - 1] + (q - S.G);
+            ain = (q < S.G || S.n == 0) ? S.gmf_off + q : S.act_off[S.n - 1] + (q - S.G);
         else
             ain = -1;
     }

@@ -308,6 +308,11 @@ hipError_t launch_fb_fused(const ncf_shape_t& s, const WsLayout& L, void* ws, co
                            int64_t n, float inv_batch, IdSpace ids, int group, int topk, int* nslab, int* nbce,
                            int* nmet, hipStream_t st);
 bool fused_supported(const ncf_shape_t& s);
+// fused MFMA forward only (shapes with s.fast_path): probs; with labels also one BCE partial per
+// workgroup in ws part_bce (*nbce of them)
+hipError_t launch_fwd_fused(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, const float* mlp,
+                            const int32_t* users, const int32_t* items, const float* labels, int64_t n,
+                            float* probs, IdSpace ids, int* nbce, hipStream_t st);
 // layer-by-layer path (ncf_layered.hip): rocBLAS fp32 GEMMs + HBM-bound glue kernels, same
 // outputs as launch_fb_generic (probs, gs, part_bce, one slab)
 bool layered_supported(const ncf_shape_t& s);

@@ -86,6 +86,7 @@ __device__ inline void stats_body(const float* __restrict__ summary, const float
             stats[NCF_STAT_LAST_LOSS] = loss;
             stats[NCF_STAT_LAST_HR] = hr;
             stats[NCF_STAT_LAST_DCG] = dc;
+            stats[NCF_STAT_BCE_SUM] += (double)(summary[NCF_SUM_BCE] * inv_batch);
         }
         if (bump) *step += 1;
     }

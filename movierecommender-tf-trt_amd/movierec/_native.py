@@ -24,7 +24,8 @@ NCF_NUM_STATS = 8
 NCF_NUM_SUMMARY = 8
 NCF_WSERR_ID_RANGE, NCF_WSERR_STALE_COUNT = 1, 4
 SUM_BCE, SUM_HIT, SUM_DCG, SUM_GROUPS, SUM_REG = range(5)
-STAT_LOSS_SUM, STAT_HR_SUM, STAT_DCG_SUM, STAT_STEPS, STAT_LAST_LOSS, STAT_LAST_HR, STAT_LAST_DCG = range(7)
+STAT_LOSS_SUM, STAT_HR_SUM, STAT_DCG_SUM, STAT_STEPS, STAT_LAST_LOSS, STAT_LAST_HR, STAT_LAST_DCG, STAT_BCE_SUM = \
+    range(8)
 
 LIB_PATH = os.environ.get("NCF_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib",
                                                       "libmovierec_ncf.so")

@@ -23,7 +23,7 @@ KERAS_EPSILON = 1e-7
 
 
 def keras_weight_names(layers, gmf_dim):
-    names = ["user_embedding", "item_embedding"]
+    names = ["user_embedding", "item_embedding"] if len(layers) else []
     if gmf_dim > 0:
         names += ["user_gmf_embedding", "item_gmf_embedding"]
     for l in range(1, len(layers)):
@@ -58,7 +58,7 @@ class NCFEngine(object):
         self.layers = [int(x) for x in layers_sizes]
         self.gmf_dim = int(gmf_dim)
         self.shape = N.NcfShape()
-        arr = (ctypes.c_int32 * len(self.layers))(*self.layers)
+        arr = (ctypes.c_int32 * max(len(self.layers), 1))(*self.layers)
         N.check(L.ncf_shape_init(ctypes.byref(self.shape), int(num_users), int(num_items), arr, len(self.layers),
                                  self.gmf_dim))
         s = self.shape
@@ -134,7 +134,7 @@ class NCFEngine(object):
     def set_hyper(self, optimizer, lr, beta_1=0.9, beta_2=0.999, layers_l2reg=None, group=None, k=None):
         if getattr(self, "row_step", None) is not None:
             self.flush()  # pending decay is owed under the previous hyper-parameters
-            if layers_l2reg is not None and float(layers_l2reg[0]) != 0.0:
+            if layers_l2reg is not None and len(layers_l2reg) and float(layers_l2reg[0]) != 0.0:
                 self.disable_lazy()
         h = self.hyper
         opt = {"adam": N.NCF_OPT_ADAM, "sgd": N.NCF_OPT_SGD}.get(optimizer)
@@ -488,4 +488,4 @@ class NCFEngine(object):
         s = t.detach().cpu().numpy()
         steps = max(s[N.STAT_STEPS], 1.0)
         return dict(loss=s[N.STAT_LOSS_SUM] / steps, hr=s[N.STAT_HR_SUM] / steps, dcg=s[N.STAT_DCG_SUM] / steps,
-                    steps=int(s[N.STAT_STEPS]))
+                    steps=int(s[N.STAT_STEPS]), bce=s[N.STAT_BCE_SUM] / steps)

@@ -21,16 +21,17 @@ class Layout(object):
         self.num_items = int(num_items)
         self.layers = [int(x) for x in layers]
         self.gmf_dim = int(gmf_dim)
-        self.du = self.layers[0] // 2                 # model.py:159-160
-        self.di = self.layers[0] - self.du
+        # model.py:159-160; no MLP (layers_sizes == []) = the GMF-only model (BASELINE config A)
+        self.du = self.layers[0] // 2 if self.layers else 0
+        self.di = self.layers[0] - self.du if self.layers else 0
         self.gmf_stride = _round4(self.gmf_dim)
         self.row_width = self.gmf_stride + _round4(max(self.du, self.di))
         self.num_rows = self.num_users + self.num_items
-        self.out_features = self.gmf_dim + self.layers[-1]
+        self.out_features = self.gmf_dim + (self.layers[-1] if self.layers else 0)
         self.mlp_params = sum(a * b + b for a, b in zip(self.layers[:-1], self.layers[1:])) + self.out_features + 1
 
     def weight_names(self):
-        names = ["user_embedding", "item_embedding"]
+        names = ["user_embedding", "item_embedding"] if self.layers else []
         if self.gmf_dim > 0:
             names += ["user_gmf_embedding", "item_gmf_embedding"]
         for l in range(1, len(self.layers)):
@@ -41,8 +42,9 @@ class Layout(object):
         """Keras-layout dict -> (emb [num_rows x row_width], flat dense vector)."""
         U, G, G4 = self.num_users, self.gmf_dim, self.gmf_stride
         emb = np.zeros((self.num_rows, self.row_width), dtype=dtype)
-        emb[:U, G4:G4 + self.du] = w["user_embedding"]
-        emb[U:, G4:G4 + self.di] = w["item_embedding"]
+        if self.layers:
+            emb[:U, G4:G4 + self.du] = w["user_embedding"]
+            emb[U:, G4:G4 + self.di] = w["item_embedding"]
         if G > 0:
             emb[:U, :G] = w["user_gmf_embedding"]
             emb[U:, :G] = w["item_gmf_embedding"]
@@ -59,7 +61,10 @@ class Layout(object):
         U, G, G4 = self.num_users, self.gmf_dim, self.gmf_stride
         e = np.asarray(emb)[:self.num_rows]
         f = np.asarray(flat)
-        w = {"user_embedding": e[:U, G4:G4 + self.du].copy(), "item_embedding": e[U:, G4:G4 + self.di].copy()}
+        w = {}
+        if self.layers:
+            w["user_embedding"] = e[:U, G4:G4 + self.du].copy()
+            w["item_embedding"] = e[U:, G4:G4 + self.di].copy()
         if G > 0:
             w["user_gmf_embedding"] = e[:U, :G].copy()
             w["item_gmf_embedding"] = e[U:, :G].copy()

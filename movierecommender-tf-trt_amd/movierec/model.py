@@ -87,12 +87,13 @@ class NCFNetwork(object):
         self.outputs = [OUTPUT_PRED, OUTPUT_RANK]
         self.trainable = True
         L = list(layers_sizes)
-        du, di = L[0] // 2, L[0] - L[0] // 2
-        ly = [_Layer("user_input", "InputLayer", (None, 1)), _Layer("item_input", "InputLayer", (None, 1)),
-              _Layer("user_embedding", "Embedding", (None, 1, du), ["user_embedding"]),
-              _Layer("item_embedding", "Embedding", (None, 1, di), ["item_embedding"]),
-              _Layer("flatten", "Flatten", (None, du)), _Layer("flatten_1", "Flatten", (None, di)),
-              _Layer("concatenate", "Concatenate", (None, L[0]))]
+        ly = [_Layer("user_input", "InputLayer", (None, 1)), _Layer("item_input", "InputLayer", (None, 1))]
+        if L:   # layers_sizes == [] with gmf_dim > 0: the GMF-only model (BASELINE config A)
+            du, di = L[0] // 2, L[0] - L[0] // 2
+            ly += [_Layer("user_embedding", "Embedding", (None, 1, du), ["user_embedding"]),
+                   _Layer("item_embedding", "Embedding", (None, 1, di), ["item_embedding"]),
+                   _Layer("flatten", "Flatten", (None, du)), _Layer("flatten_1", "Flatten", (None, di)),
+                   _Layer("concatenate", "Concatenate", (None, L[0]))]
         if gmf_dim > 0:
             ly += [_Layer("user_gmf_embedding", "Embedding", (None, 1, gmf_dim), ["user_gmf_embedding"]),
                    _Layer("item_gmf_embedding", "Embedding", (None, 1, gmf_dim), ["item_gmf_embedding"]),
@@ -100,7 +101,7 @@ class NCFNetwork(object):
                    _Layer("gmf_multiply", "Multiply", (None, gmf_dim))]
         for l in range(1, len(L)):
             ly.append(_Layer("hidden_%d" % l, "Dense", (None, L[l]), ["hidden_%d/kernel" % l, "hidden_%d/bias" % l]))
-        if gmf_dim > 0:
+        if gmf_dim > 0 and L:
             ly.append(_Layer("neumf_concatenate", "Concatenate", (None, gmf_dim + L[-1])))
         ly.append(_Layer(OUTPUT_PRED, "Dense", (None, 1), ["output/kernel", "output/bias"]))
         ly.append(_Layer(OUTPUT_RANK, "RankLayer", (None, None)))
@@ -322,9 +323,12 @@ class MovierecModel(object):
                 eng.check_ids(xu, xi)
                 eng.evaluate(xu, xi, y, group=group_v, k=self._k)
             va = eng.read_stats(eng.val_stats)
-            logs = {"loss": tr["loss"], "output_loss": tr["loss"], "output_hr": tr["hr"], "output_dcg": tr["dcg"]}
+            # Keras' History keys of this two-output model: `loss` is the total (BCE + the L2
+            # regularisers), `output_loss` the BCE of the `output` head alone; batch means averaged
+            # over the epoch's batches (all of one size)
+            logs = {"loss": tr["loss"], "output_loss": tr["bce"], "output_hr": tr["hr"], "output_dcg": tr["dcg"]}
             if n_val:
-                logs.update({"val_loss": va["loss"], "val_output_loss": va["loss"], "val_output_hr": va["hr"],
+                logs.update({"val_loss": va["loss"], "val_output_loss": va["bce"], "val_output_hr": va["hr"],
                              METRIC_VAL_DCG: va["dcg"]})
             hist.epoch.append(epoch)
             for key, val in logs.items():
@@ -408,20 +412,23 @@ def initial_weights(num_users, num_items, layers_sizes, gmf_dim=0, seed=None):
     """Keras initialisers (glorot_uniform / lecun_uniform / zeros) on the host."""
     rng = np.random.RandomState(seed) if seed is not None else np.random.RandomState()
     L = list(layers_sizes)
-    du, di = L[0] // 2, L[0] - L[0] // 2
 
     def glorot(r, c):
         lim = math.sqrt(6.0 / (r + c))
         return rng.uniform(-lim, lim, size=(r, c)).astype(np.float32)
 
-    w = {"user_embedding": glorot(num_users, du), "item_embedding": glorot(num_items, di)}
+    w = {}
+    if L:   # GMF-only model (layers_sizes == []): no MLP embeddings
+        du, di = L[0] // 2, L[0] - L[0] // 2
+        w["user_embedding"] = glorot(num_users, du)
+        w["item_embedding"] = glorot(num_items, di)
     if gmf_dim > 0:
         w["user_gmf_embedding"] = glorot(num_users, gmf_dim)
         w["item_gmf_embedding"] = glorot(num_items, gmf_dim)
     for l in range(1, len(L)):
         w["hidden_%d/kernel" % l] = glorot(L[l - 1], L[l])
         w["hidden_%d/bias" % l] = np.zeros(L[l], np.float32)
-    f = gmf_dim + L[-1]
+    f = gmf_dim + (L[-1] if L else 0)
     lim = math.sqrt(3.0 / f)
     w["output/kernel"] = rng.uniform(-lim, lim, size=(f, 1)).astype(np.float32)
     w["output/bias"] = np.zeros(1, np.float32)
@@ -478,7 +485,7 @@ def discounted_cumulative_gain(y_true, _, k, pred_rank_idx):
 
 def params_lazy(layers_l2reg):
     """Deferred exact decay is used whenever the embedding L2 is off (trainer default)."""
-    return float(layers_l2reg[0]) == 0.0
+    return len(layers_l2reg) == 0 or float(layers_l2reg[0]) == 0.0
 
 
 def params_copy(params):

@@ -40,7 +40,7 @@ class ShardedNCFEngine(object):
         if not 0 <= self.rank < self.world:
             raise ValueError("rank %d outside world %d" % (self.rank, self.world))
         self.shape = N.NcfShape()
-        arr = (ctypes.c_int32 * len(self.layers))(*self.layers)
+        arr = (ctypes.c_int32 * max(len(self.layers), 1))(*self.layers)
         N.check(L.ncf_shape_init(ctypes.byref(self.shape), int(num_users), int(num_items), arr, len(self.layers),
                                  self.gmf_dim))
         s = self.shape

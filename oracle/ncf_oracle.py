@@ -57,14 +57,15 @@ class NCFShape(object):
         self.num_items = int(num_items)
         self.layers = [int(x) for x in layers]
         self.gmf_dim = int(gmf_dim)
-        # model.py:159-160
-        self.du = self.layers[0] // 2
-        self.di = self.layers[0] - self.du
+        # model.py:159-160; layers == [] is the GMF-only model (BASELINE config A, an extension:
+        # p = sigmoid(w . (u_gmf * i_gmf) + b), He et al. 2017 eq. 10)
+        self.du = self.layers[0] // 2 if self.layers else 0
+        self.di = self.layers[0] - self.du if self.layers else 0
         self.n = len(self.layers)
 
     @property
     def out_features(self):
-        return self.gmf_dim + self.layers[-1]
+        return self.gmf_dim + (self.layers[-1] if self.layers else 0)
 
 
 def init_weights(shape, seed=0, dtype=np.float64):
@@ -78,8 +79,9 @@ def init_weights(shape, seed=0, dtype=np.float64):
         return rng.uniform(-lim, lim, size=(rows, cols)).astype(dtype)
 
     w = {}
-    w["user_embedding"] = glorot(shape.num_users, shape.du)
-    w["item_embedding"] = glorot(shape.num_items, shape.di)
+    if shape.n > 0:
+        w["user_embedding"] = glorot(shape.num_users, shape.du)
+        w["item_embedding"] = glorot(shape.num_items, shape.di)
     if shape.gmf_dim > 0:
         w["user_gmf_embedding"] = glorot(shape.num_users, shape.gmf_dim)
         w["item_gmf_embedding"] = glorot(shape.num_items, shape.gmf_dim)
@@ -94,7 +96,7 @@ def init_weights(shape, seed=0, dtype=np.float64):
 
 
 def weight_names(shape):
-    names = ["user_embedding", "item_embedding"]
+    names = ["user_embedding", "item_embedding"] if shape.n > 0 else []
     if shape.gmf_dim > 0:
         names += ["user_gmf_embedding", "item_gmf_embedding"]
     for l in range(1, shape.n):
@@ -107,7 +109,8 @@ def l2_of(shape, name, layers_l2reg):
     """Which l2 factor applies to a weight (model.py:163,168,178; the output
     layer and all biases carry none, model.py:184-187)."""
     if name.endswith("embedding"):
-        return float(layers_l2reg[0])
+        # the GMF-only model has no layers_l2reg entries: no embedding L2
+        return float(layers_l2reg[0]) if len(layers_l2reg) else 0.0
     if name.startswith("hidden_") and name.endswith("/kernel"):
         return float(layers_l2reg[int(name.split("_")[1].split("/")[0])])
     return 0.0
@@ -121,8 +124,12 @@ def forward(shape, w, users, items):
     """Per-sample forward; returns probabilities (B,) and a cache."""
     users = np.asarray(users).reshape(-1).astype(np.int64)
     items = np.asarray(items).reshape(-1).astype(np.int64)
-    dt = w["user_embedding"].dtype
-    h = [np.concatenate([w["user_embedding"][users], w["item_embedding"][items]], axis=1)]
+    if shape.n > 0:
+        dt = w["user_embedding"].dtype
+        h = [np.concatenate([w["user_embedding"][users], w["item_embedding"][items]], axis=1)]
+    else:
+        dt = w["user_gmf_embedding"].dtype
+        h = [np.zeros((len(users), 0), dtype=dt)]
     for l in range(1, shape.n):
         z = h[-1] @ w["hidden_%d/kernel" % l] + w["hidden_%d/bias" % l]
         h.append(np.maximum(z, 0))
@@ -199,8 +206,9 @@ def loss_and_grads(shape, w, users, items, labels, layers_l2reg, batch_norm=None
         g["hidden_%d/kernel" % l] = h[l - 1].T @ dzl
         g["hidden_%d/bias" % l] = dzl.sum(axis=0)
         dh = dzl @ w["hidden_%d/kernel" % l].T
-    g["user_embedding"] = _segment_sum(c["users"], dh[:, :shape.du], shape.num_users)
-    g["item_embedding"] = _segment_sum(c["items"], dh[:, shape.du:], shape.num_items)
+    if shape.n > 0:
+        g["user_embedding"] = _segment_sum(c["users"], dh[:, :shape.du], shape.num_users)
+        g["item_embedding"] = _segment_sum(c["items"], dh[:, shape.du:], shape.num_items)
     for name in weight_names(shape):
         lam = l2_of(shape, name, layers_l2reg)
         if lam != 0.0:

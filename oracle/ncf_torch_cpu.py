@@ -43,13 +43,16 @@ class TorchCPUTrainer(object):
     def __init__(self, num_users, num_items, layers, gmf_dim, lr=0.001, beta_1=0.9, beta_2=0.999, seed=0):
         g = torch.Generator().manual_seed(seed)
         L = [int(x) for x in layers]
-        du, di = L[0] // 2, L[0] - L[0] // 2
 
         def glorot(r, c):
             lim = math.sqrt(6.0 / (r + c))
             return ((torch.rand(r, c, generator=g) * 2 - 1) * lim).requires_grad_()
 
-        self.params = {"user_embedding": glorot(num_users, du), "item_embedding": glorot(num_items, di)}
+        self.params = {}
+        if L:   # layers == []: the GMF-only model (BASELINE config A)
+            du, di = L[0] // 2, L[0] - L[0] // 2
+            self.params["user_embedding"] = glorot(num_users, du)
+            self.params["item_embedding"] = glorot(num_items, di)
         if gmf_dim > 0:
             self.params["user_gmf_embedding"] = glorot(num_users, gmf_dim)
             self.params["item_gmf_embedding"] = glorot(num_items, gmf_dim)
@@ -59,7 +62,8 @@ class TorchCPUTrainer(object):
             b = torch.zeros(L[l], requires_grad=True)
             self.params["hidden_%d/kernel" % l], self.params["hidden_%d/bias" % l] = k, b
             self.hidden.append((k, b))
-        f = gmf_dim + L[-1]
+        f = gmf_dim + (L[-1] if L else 0)
+        self.has_mlp = bool(L)
         lim = math.sqrt(3.0 / f)
         self.params["output/kernel"] = ((torch.rand(f, 1, generator=g) * 2 - 1) * lim).requires_grad_()
         self.params["output/bias"] = torch.zeros(1, requires_grad=True)
@@ -71,9 +75,12 @@ class TorchCPUTrainer(object):
 
     def train_step(self, users, items, labels):
         P = self.params
-        h = torch.cat([P["user_embedding"][users], P["item_embedding"][items]], dim=1)
-        for k, b in self.hidden:
-            h = torch.relu(h @ k + b)
+        if self.has_mlp:
+            h = torch.cat([P["user_embedding"][users], P["item_embedding"][items]], dim=1)
+            for k, b in self.hidden:
+                h = torch.relu(h @ k + b)
+        else:
+            h = torch.zeros(len(users), 0)
         if self.gmf_dim > 0:
             h = torch.cat([P["user_gmf_embedding"][users] * P["item_gmf_embedding"][items], h], dim=1)
         p = torch.sigmoid(h @ P["output/kernel"] + P["output/bias"]).reshape(-1)

@@ -46,6 +46,21 @@ def test_shape_init_derivations():
     assert (s.du, s.di, s.gmf_stride, s.row_width) == (3, 4, 4, 8)
 
 
+def test_shape_init_gmf_only():
+    """BASELINE config A: ml-100k GMF-only (layers_sizes == [], gmf_dim 8): rows hold the GMF
+    vectors only, the output layer reads the product alone; the host Layout agrees."""
+    from movierec.layout import Layout
+    s = _shape(943, 1682, [], 8)
+    assert (s.num_layers, s.du, s.di, s.gmf_stride, s.row_width) == (0, 0, 0, 8, 8)
+    assert (s.out_features, s.mlp_params, s.fast_path) == (8, 9, 0)
+    lay = Layout(943, 1682, [], 8)
+    assert (lay.row_width, lay.mlp_params, lay.out_features) == (s.row_width, s.mlp_params, s.out_features)
+    assert lay.weight_names() == ["user_gmf_embedding", "item_gmf_embedding", "output/kernel", "output/bias"]
+    assert N.lib().ncf_score_supported(ctypes.byref(s), N.NCF_SCORE_FP16) == 0
+    s = _shape(10, 12, [], 5)   # gmf not a multiple of 4: padded rows
+    assert (s.gmf_stride, s.row_width, s.mlp_params) == (8, 8, 6)
+
+
 def test_shape_init_rejects_bad_dims():
     s = N.NcfShape()
     arr = (ctypes.c_int32 * 2)(0, 4)

@@ -31,6 +31,7 @@ SHAPES = [
     (200, 150, [128, 64, 32, 16], 64),  # config C shape (ml-20m NeuMF)
     (31, 17, [7, 5], 3),                # odd widths: du != di, gmf not a multiple of 4
     (40, 30, [256, 128, 64, 32], 128),  # config D shape: weights outgrow LDS -> layered GEMM path
+    (943, 1682, [], 8),                 # config A: ml-100k GMF-only (no MLP; generic kernel)
 ]
 
 
@@ -463,3 +464,36 @@ def test_counted_ahead_ids_changed_in_place():
         a.train_step(*bt[s], group=4, k=2)
     a.check_errors()
     assert torch.isfinite(a.emb).all()
+
+
+def test_evaluate_full_protocol_fused_forward():
+    """ncf_evaluate on a 200,000-sample validation pass (2,000 users x [99 negatives + the
+    held-out positive], k = 10) over config C's full tables: the fused MFMA forward against the
+    oracle (probabilities |dp| <= 2e-6; HR@10 / NDCG@10 of the device's own probabilities equal
+    the oracle's metric functions applied to them, and within the north star's +-0.002 of the
+    oracle's fp64 forward)."""
+    U, I = 138493, 27278
+    shape = O.NCFShape(U, I, [128, 64, 32, 16], 64)
+    w = {k: v.astype(np.float32).astype(np.float64) for k, v in O.init_weights(shape, seed=70).items()}
+    for k in w:   # spread the logits (Keras init gives ~0.5 everywhere): realistic ranking margins
+        if not k.endswith("bias"):
+            w[k] = (w[k] * (20.0 if k.endswith("embedding") else 2.0)).astype(np.float32).astype(np.float64)
+    rng = np.random.RandomState(71)
+    users = rng.choice(U, 2000, replace=False).repeat(100).astype(np.int32)
+    items = rng.randint(0, I, 200000).astype(np.int32)
+    y = np.tile([0.0] * 99 + [1.0], 2000).astype(np.float32)
+    eng = _engine(shape, w, max_batch=200000)
+    assert eng.fast_path
+    probs = torch.empty(200000, dtype=torch.float32, device="cuda")
+    eng.evaluate(users, items, y, group=100, k=10, probs_out=probs)
+    st = NCFEngine.read_stats(eng.val_stats)
+    p = probs.cpu().numpy()
+    pref, _ = O.forward(shape, w, users, items)
+    _close(p, pref, 2e-6, "probs")
+    hr_dev, dcg_dev = O.group_metrics(p, y, 100, 10)
+    assert st["hr"] == pytest.approx(hr_dev, abs=1e-7) and st["dcg"] == pytest.approx(dcg_dev, abs=1e-6)
+    hr_ref, dcg_ref = O.group_metrics(pref, y, 100, 10)
+    assert abs(st["hr"] - hr_ref) <= 0.002 and abs(st["dcg"] - dcg_ref) <= 0.002
+    assert st["loss"] == pytest.approx(O.bce_per_sample(pref, y).mean(), rel=1e-5)
+    # predict() takes the same fused forward
+    np.testing.assert_array_equal(eng.predict(users[:4096], items[:4096]).cpu().numpy(), p[:4096])

@@ -49,7 +49,7 @@ def test_rank_layer_kat():
                             np.array([[0, 1, 2, 3], [1, 2, 3, 0]]))
 
 
-@pytest.mark.parametrize("layers,gmf", [([6, 4], 0), ([8, 6, 4], 4), ([5, 3], 2)])
+@pytest.mark.parametrize("layers,gmf", [([6, 4], 0), ([8, 6, 4], 4), ([5, 3], 2), ([], 8)])
 def test_gradients_finite_difference(layers, gmf):
     shape = O.NCFShape(7, 9, layers, gmf)
     w = O.init_weights(shape, seed=1)

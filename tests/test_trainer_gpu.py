@@ -86,3 +86,29 @@ def test_trainer_ml20m_format(tmp_path):
     assert len(h["loss"]) == 2 and all(np.isfinite(h["loss"])) and all(np.isfinite(h["val_output_hr"]))
     assert os.path.exists(MovierecModel.get_model_weights_path(out_dir, "ml20m"))
     assert gpu_available()
+
+
+def test_trainer_gmf_only_config_a(tmp_path):
+    """BASELINE config A through the reference entry point: ml-100k, GMF-only model
+    (layers_sizes == [], gmf_dim 8), batch 256 with 3 negatives per positive."""
+    import random
+    from movierec import trainer
+    from movierec.model import MovierecModel
+    data_dir, out_dir = str(tmp_path / "data"), str(tmp_path / "models")
+    _write_ml100k(data_dir, seed=4)
+    np.random.seed(2)
+    random.seed(2)
+    params = dict(trainer.DEFAULT_PARAMS)
+    params.update(layers_sizes=[], layers_l2reg=[], batch_size=256, num_negs_per_pos=3, batch_size_eval=200,
+                  num_negs_per_pos_eval=99, k=4, epochs=3, gmf_dim=8, seed=5, lr=0.01)
+    model, history = trainer.train("gmf", "ml-100k", data_dir, out_dir, params, verbose=0)
+    h = history.history
+    assert h["loss"][-1] < h["loss"][0]
+    assert sorted(model.model.get_weights()) == ["item_gmf_embedding", "output/bias", "output/kernel",
+                                                 "user_gmf_embedding"]
+    loaded = MovierecModel.load_from_dir(out_dir, "gmf", verbose=0)
+    users = np.arange(10, dtype=np.int32).repeat(4)
+    items = np.tile(np.arange(4, dtype=np.int32), 10)
+    np.testing.assert_array_equal(model.model.predict_on_batch([users, items])[0],
+                                  loaded.model.predict_on_batch([users, items])[0])
+    assert gpu_available()
