@@ -379,8 +379,10 @@ struct CatchupCtx {
 static int catchup_touched(void* p) {
     const CatchupCtx& c = *static_cast<CatchupCtx*>(p);
     prof_begin(NCF_K_CATCHUP, c.st);
+    // counted ahead (index_ready == 2): the previous step's update launch also caught these rows up
     hipError_t e = ncf::launch_emb_catchup(*c.s, *c.L, c.ws, c.model->emb, c.optim->emb_m, c.optim->emb_v,
-                                           c.optim->row_step, c.optim->step, *c.h, false, c.st, true, c.n);
+                                           c.optim->row_step, c.optim->step, *c.h, false, c.st, true, c.n,
+                                           c.h->index_ready == 2);
     prof_end(NCF_K_CATCHUP, c.st);
     return hip_check(e, "touched-row catch-up");
 }

@@ -340,12 +340,15 @@ hipError_t launch_emb_update(const ncf_shape_t& s, const WsLayout& L, void* ws, 
 // the touched rows, which records row_step[r] = *step + 1.  Bitwise the dense sweep.
 // sort_lists (touched rows only): extra blocks of the same launch run k_sort over the index the
 // build left unsorted (launch_index_build(..., skip_sort = true)), for batch size n
+// rows_current: the batch's rows were caught up ahead by the previous step's update launch
+// (launch_emb_update_touched with next ids): only the sort blocks run
 hipError_t launch_emb_catchup(const ncf_shape_t& s, const WsLayout& L, void* ws, float* emb, float* m, float* v,
                               const int32_t* row_step, const int32_t* step, const ncf_hyper_t& h, bool all_rows,
-                              hipStream_t st, bool sort_lists = false, int64_t n = 0);
+                              hipStream_t st, bool sort_lists = false, int64_t n = 0, bool rows_current = false);
 hipError_t launch_row_step_fill(int32_t* row_step, int64_t R, const int32_t* step, hipStream_t st);
 // next_users/next_items (optional, n_next samples): extra blocks of the same launch count the NEXT
-// batch's contributions into the index counters (the next build skips its k_count)
+// batch's contributions into the index counters (the next build skips its k_count) and replay the
+// missed zero-gradient steps of its rows that this step does not touch (catch-up ahead)
 // The dense layers' Adam step handed from launch_mlp_update to launch_emb_update_touched
 // (same stream): it then runs in extra workgroups of the touched-row update launch.
 struct MlpDeferred {

@@ -92,6 +92,17 @@ __device__ inline void stats_body(const float* __restrict__ summary, const float
     }
 }
 
+// One component of adam4, the same expression: the replay below runs one element per lane and
+// rounds exactly like the float4 sweeps.
+__device__ __forceinline__ void adam1(float& p, float& m, float& v, float g, float lr_t, float b1, float b2,
+                                      float eps) {
+#pragma clang fp contract(off)
+    const float c1 = 1.0f - b1, c2 = 1.0f - b2;
+    m = b1 * m + c1 * g;
+    v = b2 * v + c2 * (g * g);
+    p -= lr_t * m / (sqrtf(v) + eps);
+}
+
 // adam4's moment updates with g = 0: b1*m + c1*0 and b2*v + c2*0 round like b1*m + 0, b2*v + 0
 __device__ __forceinline__ void decay4(float4& m, float4& v, float b1, float b2) {
 #pragma clang fp contract(off)
@@ -171,6 +182,20 @@ __global__ __launch_bounds__(kBlock) void k_emb_update(float4* __restrict__ emb,
 #ifndef NCF_CATCHUP_P_ONLY
 #define NCF_CATCHUP_P_ONLY 1
 #endif
+#ifndef NCF_CATCHUP_SCALAR
+#define NCF_CATCHUP_SCALAR 1
+#endif
+#ifndef NCF_CATCHUP_AHEAD
+#define NCF_CATCHUP_AHEAD 1
+#endif
+#ifndef NCF_AHEAD_REP
+#define NCF_AHEAD_REP 2
+#endif
+// occupancy floor of the touched-row update launch (its HBM-bound rows want many waves; the
+// catch-up-ahead blocks in the same launch must not raise its register count)
+#ifndef NCF_TOUCHED_MIN_BLOCKS
+#define NCF_TOUCHED_MIN_BLOCKS 7
+#endif
 
 // Deferred exact decay ("lazy" dense Adam, L2 off).  Keras' dense Adam (F5) moves EVERY row
 // every step; a row no sample touches gets g = 0, so its update is a pure function of
@@ -232,11 +257,42 @@ __global__ __launch_bounds__(kBlock) void k_emb_catchup(float4* __restrict__ emb
     const int t = *step;  // steps every row should have received
     if (threadIdx.x < kLrLut) lut[threadIdx.x] = t - (int)threadIdx.x >= 1 ? adam_lr_t(lr, b1, b2, t - threadIdx.x) : 0.f;
     __syncthreads();
+    const int64_t n = ALL ? R : (int64_t)*nlist;
+    const int64_t nblk = ALL ? gridDim.x : so.ncatch;
+#if NCF_CATCHUP_SCALAR
+    // One ELEMENT per lane (a row of W floats spans W lanes, 2 waves at config C): a row's replay
+    // is a sequential chain per element, so the longest debt of the batch — rows untouched since
+    // the start of the run — sets the launch's tail; spreading a row over 4x the lanes of the
+    // float4 form cuts that tail 4x (measured: the float4 form's time grew with the longest debt
+    // while the total work stayed flat, tools/catchup_probe.py).
+    const int W = 4 * (int)w4;
+    const int lanes_per_row = W < kBlock ? (W + 63) / 64 * 64 : kBlock;   // whole waves per row
+    const int rpb = kBlock / lanes_per_row;                                // rows per block pass
+    const int sub = threadIdx.x / lanes_per_row, q0 = threadIdx.x % lanes_per_row;
+    float* embf = reinterpret_cast<float*>(emb);
+    float* mf = reinterpret_cast<float*>(m4);
+    float* vf = reinterpret_cast<float*>(v4);
+    for (int64_t i = (int64_t)blockIdx.x * rpb + sub; i < n; i += nblk * rpb) {
+        const int64_t r = ALL ? i : list[i];
+        const int s = row_step[r];
+        if (s >= t) continue;
+        for (int q = q0; q < W; q += lanes_per_row) {
+            const size_t e = (size_t)r * W + q;
+            float p = embf[e], m = mf[e], v = vf[e];
+            for (int j = s + 1; j <= t; ++j)
+                adam1(p, m, v, 0.0f, t - j < kLrLut ? lut[t - j] : adam_lr_t(lr, b1, b2, j), b1, b2, eps);
+            embf[e] = p;
+            if (ALL || !NCF_CATCHUP_P_ONLY) {
+                mf[e] = m;
+                vf[e] = v;
+            }
+        }
+    }
+#else
     const RowLanes rl(w4);
     if (!rl.on) return;
-    const int64_t n = ALL ? R : (int64_t)*nlist;
     const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
-    const int64_t waves = ((int64_t)(ALL ? gridDim.x : so.ncatch) * kBlock) >> 6;
+    const int64_t waves = ((int64_t)nblk * kBlock) >> 6;
     const float4 zero = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int64_t i = wave * rl.rpw + rl.sub; i < n; i += waves * rl.rpw) {
         const int64_t r = ALL ? i : list[i];
@@ -256,6 +312,7 @@ __global__ __launch_bounds__(kBlock) void k_emb_catchup(float4* __restrict__ emb
             }
         }
     }
+#endif
 }
 
 // row_step[r] = *step for every row (after a flush: the replay kernel above only reads row_step)
@@ -340,6 +397,7 @@ struct CountAhead {
     int64_t m;
     int32_t U, I;
     int32_t* cnt;
+    int replay;                // 1: also catch the next batch's stale rows up (catch-up ahead)
 };
 
 // the dense layers' Adam (k_mlp_update<ADAM>'s work) in blocks >= nupd + ncount of the same launch
@@ -355,7 +413,7 @@ struct MlpTail {
     float* part_reg;
 };
 
-__global__ __launch_bounds__(kBlock) void k_emb_adam_touched(float4* __restrict__ emb, float4* __restrict__ m4,
+__global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_touched(float4* __restrict__ emb, float4* __restrict__ m4,
                                                              float4* __restrict__ v4, uint32_t w4,
                                                              const int32_t* __restrict__ list,
                                                              const int32_t* __restrict__ nlist,
@@ -365,38 +423,102 @@ __global__ __launch_bounds__(kBlock) void k_emb_adam_touched(float4* __restrict_
                                                              int32_t* __restrict__ row_step, const int32_t* step,
                                                              float lr, float b1, float b2, float eps,
                                                              CountAhead ca, MlpTail mt) {
+    // block order: [count (+ catch-up ahead)] [touched-row update] [dense-layer Adam]: the
+    // latency-bound replay blocks are dispatched first, so they run under the HBM-bound update
     if ((int)blockIdx.x >= ca.nupd + ca.ncount) {
         mlp_update_body<NCF_OPT_ADAM>(mt.p, mt.m, mt.v, mt.P, mt.slabs, mt.nslab, nullptr, nullptr, 1, 0, mt.step,
                                       mt.lr, mt.b1, mt.b2, mt.eps, mt.l2t, mt.part_reg,
                                       (int)blockIdx.x - ca.nupd - ca.ncount);
         return;
     }
-    if ((int)blockIdx.x >= ca.nupd) {
-        // extra blocks: count the NEXT batch's contributions (k_count's work) while this step's
-        // rows stream; the counters are free here (the fill of this step's index emptied them)
-        const int64_t first = (int64_t)(blockIdx.x - ca.nupd) * kBlock + (threadIdx.x & ~63);
-        const int64_t cstride = (int64_t)ca.ncount * kBlock;
-        for (int64_t cb = first; cb < ca.m; cb += cstride) {   // wave-uniform trip count
-            const int64_t c = cb + (threadIdx.x & 63);
-            bool ok = false;
-            int key = 0;
-            if (c < ca.m) {
-                const int64_t i = c >> 1;
-                const int id = (c & 1) ? ca.items[i] : ca.users[i];
-                const int bound = (c & 1) ? ca.I : ca.U;
-                ok = (unsigned)id < (unsigned)bound;
-                key = (c & 1) ? ca.U + id : id;
+    if ((int)blockIdx.x < ca.ncount) {
+        // count the NEXT batch's contributions (k_count's work) while this step's rows stream; the
+        // counters are free here (the fill of this step's index emptied them).
+        // Catch-up ahead (ca.replay): a row of the next batch that this step does not touch owes
+        // the zero-gradient steps (row_step, t] — this step's included — and nothing else in this
+        // launch reads or writes it, so it is replayed here (k_emb_catchup's work, same per-step
+        // arithmetic: bitwise) under the touched-row update, instead of in a launch of its own
+        // before the next forward pass.  One lane claims a row (CAS on row_step: a user's
+        // repeated contributions replay it once); the wave replays its claimed rows, kRep at a
+        // time with all their loads in flight and the rows' chains interleaved, one element per
+        // lane, and leaves p, m, v and row_step at step t.
+        __shared__ float lut[kLrLut];
+        const int t = *step + 1;
+        if (ca.replay) {
+            if (threadIdx.x < kLrLut)
+                lut[threadIdx.x] = t - (int)threadIdx.x >= 1 ? adam_lr_t(lr, b1, b2, t - threadIdx.x) : 0.f;
+            __syncthreads();
+        }
+        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+        const int W = 4 * (int)w4;
+        float* embf = reinterpret_cast<float*>(emb);
+        float* mf = reinterpret_cast<float*>(m4);
+        float* vf = reinterpret_cast<float*>(v4);
+        // a block takes 64 contributions per pass: wave 0 counts them and claims the stale rows,
+        // then the block's 4 waves share the claimed rows' replay (one row per wave at a time,
+        // one element per lane) — many short replay chains in flight instead of a few long ones
+        __shared__ int crow[64], cstep[64], ncl;
+        for (int64_t cb = (int64_t)blockIdx.x * 64; cb < ca.m; cb += (int64_t)ca.ncount * 64) {
+            if (wv == 0) {
+                const int64_t c = cb + lane;
+                bool ok = false;
+                int key = 0;
+                if (c < ca.m) {
+                    const int64_t i = c >> 1;
+                    const int id = (c & 1) ? ca.items[i] : ca.users[i];
+                    const int bound = (c & 1) ? ca.I : ca.U;
+                    ok = (unsigned)id < (unsigned)bound;
+                    key = (c & 1) ? ca.U + id : id;
+                }
+                wave_run_count(ca.cnt, key, ok);
+                bool claim = false;
+                int s0 = 0;
+                if (ca.replay && ok && offs[key + 1] == offs[key]) {   // not in this step's batch
+                    int sv = row_step[key];
+                    while (sv < t) {
+                        const int prev = atomicCAS(&row_step[key], sv, t);
+                        if (prev == sv) {
+                            claim = true;
+                            s0 = sv;
+                            break;
+                        }
+                        sv = prev;
+                    }
+                }
+                const uint64_t cm = __ballot(claim);
+                if (claim) {
+                    const int slot = __popcll(cm & ((1ull << lane) - 1));
+                    crow[slot] = key;
+                    cstep[slot] = s0;
+                }
+                if (lane == 0) ncl = __popcll(cm);
             }
-            wave_run_count(ca.cnt, key, ok);
+            __syncthreads();
+            const int nc = ncl;
+            for (int k = wv; k < nc; k += kBlock / 64) {
+                const int64_t r = crow[k];
+                const int sr = cstep[k];
+                for (int q = lane; q < W; q += 64) {
+                    const size_t e = (size_t)r * W + q;
+                    float p = embf[e], mm = mf[e], vv = vf[e];
+                    for (int j = sr + 1; j <= t; ++j)
+                        adam1(p, mm, vv, 0.0f, t - j < kLrLut ? lut[t - j] : adam_lr_t(lr, b1, b2, j), b1, b2, eps);
+                    embf[e] = p;
+                    mf[e] = mm;
+                    vf[e] = vv;
+                }
+            }
+            __syncthreads();
         }
         return;
     }
+    const int ublk = (int)blockIdx.x - ca.ncount;   // this block's index among the update blocks
     const RowLanes rl(w4);
     const int t = *step + 1;
     if (rl.on) {
         const float lr_t = adam_lr_t(lr, b1, b2, t);
         const int64_t n = *nlist;
-        const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+        const int64_t wave = ((int64_t)ublk * kBlock + threadIdx.x) >> 6;
         const int64_t stride = (((int64_t)ca.nupd * kBlock) >> 6) * rl.rpw;
         int64_t i = wave * rl.rpw + rl.sub;
         // software pipeline over this lane group's rows: the next row's id is loaded while the
@@ -777,7 +899,7 @@ static unsigned row_grid(int64_t rows, uint32_t w4, int64_t cap) {
 
 hipError_t launch_emb_catchup(const ncf_shape_t& s, const WsLayout& L, void* ws, float* emb, float* m, float* v,
                               const int32_t* row_step, const int32_t* step, const ncf_hyper_t& h, bool all_rows,
-                              hipStream_t st, bool sort_lists, int64_t n) {
+                              hipStream_t st, bool sort_lists, int64_t n, bool rows_current) {
     const uint32_t w4 = (uint32_t)(s.row_width / 4);
     const int64_t R = s.num_rows;
     const int64_t nmax = R < 2 * L.max_batch ? R : 2 * L.max_batch;
@@ -798,7 +920,9 @@ hipError_t launch_emb_catchup(const ncf_shape_t& s, const WsLayout& L, void* ws,
             lds_cfg = true;
         }
     }
-    if (h.optimizer != NCF_OPT_ADAM) {  // SGD: an untouched row does not move; only the sort remains
+    // rows_current: the previous step's update launch caught this batch's rows up ahead
+    if (h.optimizer != NCF_OPT_ADAM || (rows_current && NCF_CATCHUP_AHEAD)) {
+        // SGD (an untouched row does not move) or rows already current: only the sort remains
         if (nsort) {
             so.ncatch = 0;
             launch(k_emb_catchup<false>, nsort, kBlock, lds, st, (float4*)emb, (float4*)m, (float4*)v, w4,
@@ -807,12 +931,23 @@ hipError_t launch_emb_catchup(const ncf_shape_t& s, const WsLayout& L, void* ws,
         }
         return hipGetLastError();
     }
+#if NCF_CATCHUP_SCALAR
+    auto cgrid = [&](int64_t rows, int64_t cap) {
+        const int W = 4 * (int)w4;
+        const int64_t lanes = W < kBlock ? (W + 63) / 64 * 64 : kBlock;
+        const int64_t rpb = kBlock / lanes;
+        int64_t g = (rows + rpb - 1) / rpb;
+        return (unsigned)(g < 1 ? 1 : (g > cap ? cap : g));
+    };
+#else
+    auto cgrid = [&](int64_t rows, int64_t cap) { return row_grid(rows, w4, cap); };
+#endif
     if (all_rows) {
-        launch(k_emb_catchup<true>, row_grid(R, w4, 8192), kBlock, 0, st, (float4*)emb, (float4*)m, (float4*)v, w4,
+        launch(k_emb_catchup<true>, cgrid(R, 8192), kBlock, 0, st, (float4*)emb, (float4*)m, (float4*)v, w4,
                (const int32_t*)nullptr, (const int32_t*)nullptr, R, row_step, step, h.lr, h.beta_1, h.beta_2,
                h.epsilon, so);
     } else {
-        const unsigned ncatch = row_grid(nmax, w4, NCF_CATCHUP_GRID_MAX);
+        const unsigned ncatch = cgrid(nmax, NCF_CATCHUP_GRID_MAX);
         so.ncatch = (int)ncatch;
         launch(k_emb_catchup<false>, ncatch + nsort, kBlock, lds, st, (float4*)emb, (float4*)m, (float4*)v, w4,
                at<const int32_t>(ws, L.touched), at<const int32_t>(ws, L.nuniq), R, row_step, step, h.lr, h.beta_1,
@@ -830,6 +965,7 @@ hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, vo
                                      float* v, int32_t* row_step, int32_t* step, const ncf_hyper_t& h,
                                      hipStream_t st, const int32_t* next_users, const int32_t* next_items,
                                      int64_t n_next, const MlpDeferred* mlp) {
+    const bool replay_ahead = next_users != nullptr && NCF_CATCHUP_AHEAD;
     const uint32_t w4 = (uint32_t)(s.row_width / 4);
     const uint32_t n4 = (uint32_t)(s.num_rows * w4);
     const int32_t* offs = at<int32_t>(ws, L.offs);
@@ -839,10 +975,10 @@ hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, vo
     if (h.optimizer == NCF_OPT_ADAM) {
         const unsigned nupd = row_grid(R < 2 * L.max_batch ? R : 2 * L.max_batch, w4, NCF_TOUCHED_GRID_MAX);
         const int64_t mc = next_users ? 2 * n_next : 0;
-        const unsigned ncount = mc > 0 ? (unsigned)((mc + kBlock - 1) / kBlock < 512 ? (mc + kBlock - 1) / kBlock
-                                                                                      : 512) : 0u;
+        // count (+ catch-up ahead) blocks: 64 contributions per block and pass
+        const unsigned ncount = mc > 0 ? (unsigned)((mc + 63) / 64 < 4096 ? (mc + 63) / 64 : 4096) : 0u;
         CountAhead ca{(int)nupd, (int)ncount, next_users, next_items, mc, s.num_users, s.num_items,
-                      at<int32_t>(ws, L.cnt)};
+                      at<int32_t>(ws, L.cnt), replay_ahead ? 1 : 0};
         MlpTail mt{};
         if (mlp) {
             mt = MlpTail{(s.mlp_params + kBlock - 1) / kBlock, mlp->p, mlp->m, mlp->v, s.mlp_params, mlp->slabs,

@@ -317,7 +317,11 @@ class NCFEngine(object):
 
     def rank(self, probs, group):
         probs = probs.reshape(-1).contiguous()
+        if probs.numel() % group:   # RankLayer's reshape (-1, n+1) fails the same way in TF
+            raise ValueError("cannot rank %d predictions in groups of %d" % (probs.numel(), group))
         ng = probs.numel() // group
+        if ng == 0:
+            return torch.empty(0, group, dtype=torch.int32, device=self.device)
         out = torch.empty(ng, group, dtype=torch.int32, device=self.device)
         N.check(N.lib().ncf_rank(N.ptr(probs), ng, int(group), N.ptr(out), N.stream_handle(self.device)))
         return out

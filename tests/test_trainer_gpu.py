@@ -107,8 +107,8 @@ def test_trainer_gmf_only_config_a(tmp_path):
     assert sorted(model.model.get_weights()) == ["item_gmf_embedding", "output/bias", "output/kernel",
                                                  "user_gmf_embedding"]
     loaded = MovierecModel.load_from_dir(out_dir, "gmf", verbose=0)
-    users = np.arange(10, dtype=np.int32).repeat(4)
-    items = np.tile(np.arange(4, dtype=np.int32), 10)
+    users = np.arange(2, dtype=np.int32).repeat(100)     # two evaluation groups of 100
+    items = np.tile(np.arange(100, dtype=np.int32), 2)
     np.testing.assert_array_equal(model.model.predict_on_batch([users, items])[0],
                                   loaded.model.predict_on_batch([users, items])[0])
     assert gpu_available()
