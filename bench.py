@@ -113,24 +113,34 @@ def parse():
     return ap.parse_args()
 
 
-def emb_update_bytes(cfg_shape, batch, dense_rows=None, sparse_rows=None, touched_rows=None):
+def grad_rows(eng, batch, group):
+    """Per-sample gradient rows one batch produces: B item rows plus the user rows — one per
+    group when the fused kernel folds a group's user rows (include/movierec_ncf.h "User-row
+    folding"; the synthetic batches share the user within a group), else B."""
+    fused = bool(eng.shape.fast_path) and not eng.hyper.force_generic
+    fold = group if (fused and group in (2, 4, 8) and os.environ.get("NCF_FOLD_USERS", "1") != "0") else 1
+    return batch + batch // fold
+
+
+def emb_update_bytes(cfg_shape, batch, dense_rows=None, sparse_rows=None, touched_rows=None, contribs=None):
     """Algorithmic HBM bytes of one embedding scatter-add + Adam sweep launch:
     read+write p, m, v of every swept table element (24 B/param), plus the
-    gradient.  Single table: the 2B per-sample gradient rows (W floats) + list
-    (4 B per contribution) + row offsets (4 B/row).  Replicated DP
+    gradient.  Single table: the per-sample gradient rows (``contribs`` of them, W floats;
+    default 2B) + list (4 B per contribution) + row offsets (4 B/row).  Replicated DP
     (``dense_rows`` = this rank's shard): the reduce-scattered dense gradient
     (4 B/param).  Row-sharded DP (``sparse_rows`` = (shard rows, received
     gradient rows m)): the m received rows + list + offsets of the shard."""
     R, W = cfg_shape.num_rows, cfg_shape.row_width
+    c = 2 * batch if contribs is None else contribs
     if touched_rows is not None:
         # deferred exact decay: only the batch's touched rows are read and written
-        return 24 * touched_rows * W + 2 * batch * W * 4 + 2 * batch * 4 + (R + 1) * 4
+        return 24 * touched_rows * W + c * W * 4 + c * 4 + (R + 1) * 4
     if dense_rows is not None:
         return 28 * dense_rows * W
     if sparse_rows is not None:
         S, m = sparse_rows
         return 24 * S * W + m * W * 4 + m * 4 + (S + 1) * 4
-    return 24 * R * W + 2 * batch * W * 4 + 2 * batch * 4 + (R + 1) * 4
+    return 24 * R * W + c * W * 4 + c * 4 + (R + 1) * 4
 
 
 def fwd_bwd_flops(cfg):
@@ -146,10 +156,12 @@ def fwd_bwd_flops(cfg):
     return 2 * (fwd + bwd_data + dw)
 
 
-def fwd_bwd_bytes(shape, batch):
+def fwd_bwd_bytes(shape, batch, contribs=None):
     """Algorithmic HBM bytes of the fused kernel: ids+label (12 B), both gathered rows
-    (2W floats), both per-sample gradient rows written (2W floats), the probability."""
-    return batch * (12 + 2 * shape.row_width * 4 * 2 + 4)
+    (2W floats), the per-sample gradient rows written (``contribs`` rows of W floats, default
+    2B), the probability."""
+    c = 2 * batch if contribs is None else contribs
+    return batch * (12 + 2 * shape.row_width * 4 + 4) + c * shape.row_width * 4
 
 
 def cpu_baseline(cfg, budget_s, protocol="bounded"):
@@ -551,13 +563,14 @@ def main():
     kern_ms = ms_emb / nl if nl else float("nan")
     fb_ms = ms_fb / nfb if nfb else float("nan")
     fb_flops = fwd_bwd_flops(cfg) * B
-    fb_bytes = fwd_bwd_bytes(eng.shape, B)
+    contribs = grad_rows(eng, B, g) if mode != "sharded" else 2 * B
+    fb_bytes = fwd_bwd_bytes(eng.shape, B, contribs)
     train_exchange = dp.last_exchange if mode == "sharded" else None
     if mode == "sharded":
         nbytes = emb_update_bytes(eng.shape, B, sparse_rows=(eng.shard_rows, train_exchange[1]))
     elif getattr(eng, "lazy", False):
         touched = float(np.mean([torch.unique(u).numel() + torch.unique(it).numel() for u, it, _ in pool[:16]]))
-        nbytes = emb_update_bytes(eng.shape, B, touched_rows=touched)
+        nbytes = emb_update_bytes(eng.shape, B, touched_rows=touched, contribs=contribs)
         if sampler is None:
             nbytes += 2 * B * (4 + 8)   # the launch also counts the next batch: id reads + counter atomics
     elif mode == "user":
@@ -565,10 +578,12 @@ def main():
         # (ncf_update_rows), then Adam over the item rows with the all-reduced dense gradient
         # (ncf_apply_update); bytes per launch = the step's bytes / 2, time per launch = the average
         Uloc, W = eng.num_users, eng.shape.row_width
-        own = 24 * Uloc * W + B * W * 4 + B * 4 + (Uloc + 1) * 4
+        cu = contribs - B   # the own users' gradient rows
+        own = 24 * Uloc * W + cu * W * 4 + cu * 4 + (Uloc + 1) * 4
         nbytes = (own + 28 * (eng.num_rows - Uloc) * W) / 2.0
     else:
-        nbytes = emb_update_bytes(eng.shape, B, dense_rows=(dp.row_count if mode == "replicated" else None))
+        nbytes = emb_update_bytes(eng.shape, B, dense_rows=(dp.row_count if mode == "replicated" else None),
+                                  contribs=contribs)
     achieved = nbytes / (kern_ms * 1e-3) / 1e9
 
     # HR@10 on a synthetic validation set (1 positive + 99 sampled items per user), per rank
@@ -645,6 +660,7 @@ def main():
                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "algorithmic_bytes_per_launch": nbytes, "avg_launch_ms": round(kern_ms, 5),
+                "gradient_rows_per_step": contribs,
                 "launches_per_step": round(nl / len(range(0, args.steps, every)), 2),
                 "timed_steps": "every %d-th step of the timed region (HIP events in the dispatch packets)" % every,
                 "traffic_source": "rocprofv3 --pmc FETCH_SIZE(x2 gfx950) + WRITE_SIZE, profiles/traffic/ "

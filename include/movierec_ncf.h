@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define NCF_ABI_VERSION 4
+#define NCF_ABI_VERSION 5
 #define NCF_MAX_LAYERS 8
 #define NCF_EINVAL (-1)
 #define NCF_EHIP (-2)
@@ -148,9 +148,19 @@ int ncf_workspace_init(const ncf_shape_t* shape, int64_t max_batch, void* ws, si
  *                          ncf_train_step_ahead counted (their contents changed in between): the
  *                          index build wrote no slot outside its keys' ranges and cleared the
  *                          counters, but that step's embedding gradient is wrong.
- * Nothing else in the library synchronises on them. */
+ *   NCF_WSERR_FOLD         an index built by an earlier call (ncf_build_index, ncf_shard_plan)
+ *                          folds user rows differently than the step that used it (their hypers'
+ *                          group / force_generic differ): that step's embedding gradient is wrong.
+ * Nothing else in the library synchronises on them.
+ *
+ * User-row folding: when the fused kernel runs and hyper->group is a power of two <= 32, the
+ * user-row gradients of a group's samples that share the group head's user (the reference's
+ * batches: one positive + negs per user, data_pipeline.py:141) are summed inside the kernel and
+ * written once; the index lists that one contribution.  Any batch stays exact (a sample with
+ * another user keeps its own row); only the fp32 summation order of those rows changes. */
 #define NCF_WSERR_ID_RANGE 1
 #define NCF_WSERR_STALE_COUNT 4
+#define NCF_WSERR_FOLD 8
 int ncf_workspace_flags(const ncf_shape_t* shape, int64_t max_batch, void* ws, size_t ws_bytes, int32_t* flags,
                         void* stream);
 
@@ -257,9 +267,10 @@ int ncf_update_rows(const ncf_shape_t* shape, ncf_model_t* model, ncf_optim_t* o
  * e.g. while the current step's all-reduce is in flight: the call replaces the index of the
  * previous batch, so it must follow that batch's ncf_update_rows on the stream.  The next
  * ncf_forward_backward_part / ncf_forward_backward with hyper->index_ready = 1 then skips its own
- * index build (the caller guarantees it passes the same ids). */
-int ncf_build_index(const ncf_shape_t* shape, const int32_t* users, const int32_t* items, int64_t n, void* ws,
-                    size_t ws_bytes, void* stream);
+ * index build (the caller guarantees it passes the same ids).  hyper: that call's hyper (its group
+ * and force_generic decide the user-row folding; NULL = none); a mismatch sets NCF_WSERR_FOLD. */
+int ncf_build_index(const ncf_shape_t* shape, const ncf_hyper_t* hyper, const int32_t* users, const int32_t* items,
+                    int64_t n, void* ws, size_t ws_bytes, void* stream);
 
 /* Row-sharded data parallelism (no reference counterpart — the
  * reference trains on one CPU).  Rank r of `world` (1..16) owns the table rows g
@@ -288,9 +299,12 @@ int ncf_shard_rows(const ncf_shape_t* shape, int32_t world, int64_t* rows);
 int ncf_shard_workspace_size(const ncf_shape_t* shape, int64_t max_batch, int32_t world, size_t* bytes);
 int ncf_shard_workspace_init(const ncf_shape_t* shape, int64_t max_batch, int32_t world, void* ws, size_t ws_bytes,
                              void* stream);
-/* uniq_rows: int32[2n] capacity, send_counts: int32[world] (device). */
-int ncf_shard_plan(const ncf_shape_t* shape, int32_t world, const int32_t* users, const int32_t* items, int64_t n,
-                   int32_t* uniq_rows, int32_t* send_counts, void* ws, size_t ws_bytes, void* stream);
+/* uniq_rows: int32[2n] capacity, send_counts: int32[world] (device).  hyper: the hyper of the
+ * ncf_shard_forward_backward that follows (user-row folding, as ncf_build_index); NULL for a
+ * plan that only feeds ncf_shard_predict. */
+int ncf_shard_plan(const ncf_shape_t* shape, const ncf_hyper_t* hyper, int32_t world, const int32_t* users,
+                   const int32_t* items, int64_t n, int32_t* uniq_rows, int32_t* send_counts, void* ws,
+                   size_t ws_bytes, void* stream);
 /* out[j] = table[rows[j]] for j < m (rows outside [0, table_rows) give zero rows). */
 int ncf_gather_rows(const ncf_shape_t* shape, const float* table, int64_t table_rows, const int32_t* rows, int64_t m,
                     float* out, void* stream);

@@ -168,6 +168,16 @@ hipError_t launch_predict(const ncf_shape_t& s, const ncf_hyper_t* h, const ncf:
 // Shapes the fused kernel does not hold: the layer-by-layer GEMM path when the dense weights
 // outgrow the generic kernel's LDS staging (config D), or when asked for (force_generic == 2);
 // the per-sample generic kernel for small models (the reference's test shapes) or force_generic == 1.
+// user-row folding of a step's index and fused kernel (ncf_internal.h fold_of); h NULL: none.
+// NCF_FOLD_USERS=0 turns it off (A/B measurements)
+int index_fold(const ncf_shape_t& s, const ncf_hyper_t* h) {
+    static const bool on = [] {
+        const char* e = getenv("NCF_FOLD_USERS");
+        return !e || atoi(e) != 0;
+    }();
+    return h && on ? ncf::fold_of(h->group, use_fused(s, h)) : 0;
+}
+
 bool use_layered(const ncf_shape_t& s, const ncf_hyper_t* h) {
     if (!ncf::layered_supported(s)) return false;
     if (h && h->force_generic == 2) return true;
@@ -202,6 +212,7 @@ WsLayout make_layout(const ncf_shape_t& s, int64_t B, int world) {
     L.cnt = take((size_t)(K + 1) * 4);
     L.heavy_n = take(4);
     L.err = take(4);
+    L.ifold = take(4);
     L.persistent_end = off;
     L.nscan = (int)((K + 1 + kScanBlock - 1) / kScanBlock);
     L.nmetric = (int)((B + kBlock - 1) / kBlock);
@@ -404,13 +415,18 @@ static int run_fb(const ncf_shape_t& s, const ncf::WsLayout& L, const ncf_model_
                   int (*after_index)(void*) = nullptr, void* ctx = nullptr) {
     hipError_t e = hipSuccess;
     ncf::IdSpace ids = ncf::table_ids(s);
-    if (sharded) {
-        users = ncf::at<int32_t>(ws, L.cid_u);
-        items = ncf::at<int32_t>(ws, L.cid_i);
-        ids = ncf::compact_ids(n);
-    } else if (h->index_ready == 1 && !after_index) {
-        // ncf_build_index already built this batch's index on `st` (the deferred-decay step needs
-        // the touched-row list too and always builds its own)
+    const int fold = index_fold(s, h);
+    if (sharded || (h->index_ready == 1 && !after_index)) {
+        // the index was built by an earlier call — ncf_shard_plan (compact ids) or ncf_build_index
+        // (the deferred-decay step needs the touched-row list too and always builds its own): it
+        // must fold the user rows as this step's kernel does
+        if (sharded) {
+            users = ncf::at<int32_t>(ws, L.cid_u);
+            items = ncf::at<int32_t>(ws, L.cid_i);
+            ids = ncf::compact_ids(n);
+        }
+        e = ncf::launch_fold_check(L, ws, fold, st);
+        if (e != hipSuccess) return hip_check(e, "fold check");
     } else {
         // the index depends only on the ids: it is built on the side stream while the
         // forward/backward runs (the fused kernel leaves registers and a little LDS free on every
@@ -421,7 +437,7 @@ static int run_fb(const ncf_shape_t& s, const ncf::WsLayout& L, const ncf_model_
         prof_begin(NCF_K_INDEX, sti);
         // deferred decay: the catch-up launch (after_index) sorts the lists in extra workgroups
         e = ncf::launch_index_build(s, L, ws, users, items, n, sti, after_index != nullptr, h->index_ready == 2,
-                                    after_index != nullptr);
+                                    after_index != nullptr, fold);
         prof_end(NCF_K_INDEX, sti);
         if (e != hipSuccess) return hip_check(e, "index build");
         out->index_side = ss;
@@ -433,7 +449,7 @@ static int run_fb(const ncf_shape_t& s, const ncf::WsLayout& L, const ncf_model_
     prof_begin(NCF_K_FWD_BWD, st);
     if (use_fused(s, h))
         e = ncf::launch_fb_fused(s, L, ws, model->emb, model->mlp, users, items, labels, n, h->inv_batch, ids,
-                                 h->group, h->k, &out->nslab, &out->nbce, &out->nmet, st);
+                                 h->group, h->k, &out->nslab, &out->nbce, &out->nmet, st, fold);
     else if (use_layered(s, h))
         e = ncf::launch_fb_layered(s, L, ws, model->emb, model->mlp, users, items, labels, n, h->inv_batch, ids,
                                    &out->nslab, &out->nbce, st);
@@ -522,7 +538,7 @@ static int train_step_impl(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t
     if (lazy)
         e = ncf::launch_emb_update_touched(*s, L, ws, model->emb, optim->emb_m, optim->emb_v, optim->row_step,
                                            optim->step, *h, st, next_users, next_items, n_next,
-                                           mlp_def.p ? &mlp_def : nullptr);
+                                           mlp_def.p ? &mlp_def : nullptr, index_fold(*s, h));
     else
         e = ncf::launch_emb_update(*s, L, ws, model->emb, optim->emb_m, optim->emb_v, optim->step, *h, nullptr,
                                    s->num_rows, st);
@@ -620,15 +636,17 @@ int ncf_forward_backward_part(const ncf_shape_t* s, const ncf_model_t* model, co
                                  probs_out, reg_row_begin, reg_row_count, include_dense_reg, ws, ws_bytes, stream);
 }
 
-int ncf_build_index(const ncf_shape_t* s, const int32_t* users, const int32_t* items, int64_t n, void* ws,
-                    size_t ws_bytes, void* stream) {
+int ncf_build_index(const ncf_shape_t* s, const ncf_hyper_t* h, const int32_t* users, const int32_t* items,
+                    int64_t n, void* ws, size_t ws_bytes, void* stream) {
     if (int r = check_shape(s)) return r;
+    if (h)
+        if (int r = check_hyper(h)) return r;
     if (!users || !items) return fail(NCF_EINVAL, "NULL device pointer");
     ncf::WsLayout L;
     if (int r = check_ws(*s, n, ws, ws_bytes, &L)) return r;
     hipStream_t st = (hipStream_t)stream;
     prof_begin(NCF_K_INDEX, st);
-    hipError_t e = ncf::launch_index_build(*s, L, ws, users, items, n, st, false);
+    hipError_t e = ncf::launch_index_build(*s, L, ws, users, items, n, st, false, false, false, index_fold(*s, h));
     prof_end(NCF_K_INDEX, st);
     return hip_check(e, "index build");
 }
@@ -769,16 +787,19 @@ int ncf_shard_workspace_init(const ncf_shape_t* s, int64_t max_batch, int32_t wo
     return hip_check(hipMemsetAsync(ws, 0, L.persistent_end, (hipStream_t)stream), "hipMemsetAsync");
 }
 
-int ncf_shard_plan(const ncf_shape_t* s, int32_t world, const int32_t* users, const int32_t* items, int64_t n,
-                   int32_t* uniq_rows, int32_t* send_counts, void* ws, size_t ws_bytes, void* stream) {
+int ncf_shard_plan(const ncf_shape_t* s, const ncf_hyper_t* h, int32_t world, const int32_t* users,
+                   const int32_t* items, int64_t n, int32_t* uniq_rows, int32_t* send_counts, void* ws, size_t ws_bytes,
+                   void* stream) {
     if (int r = check_shape(s)) return r;
+    if (h)
+        if (int r = check_hyper(h)) return r;
     if (int r = check_world(world)) return r;
     if (!users || !items || !uniq_rows || !send_counts) return fail(NCF_EINVAL, "NULL device pointer");
     ncf::WsLayout L;
     if (int r = check_ws(*s, n, ws, ws_bytes, &L, world)) return r;
     hipStream_t st = (hipStream_t)stream;
     prof_begin(NCF_K_INDEX, st);
-    hipError_t e = ncf::launch_shard_plan(*s, L, ws, users, items, n, uniq_rows, send_counts, st);
+    hipError_t e = ncf::launch_shard_plan(*s, L, ws, users, items, n, uniq_rows, send_counts, st, index_fold(*s, h));
     prof_end(NCF_K_INDEX, st);
     return hip_check(e, "shard plan");
 }

@@ -28,6 +28,10 @@
 // Outputs match the generic kernel: probs, per-sample embedding gradient rows
 // gs[2i] (user) / gs[2i+1] (item), one dense-gradient slab per workgroup and
 // one BCE partial per workgroup.  Reference semantics: movierec/model.py:154-214.
+// With user-row folding (fold > 1, ncf_internal.h fold_of) the user rows of a
+// group's samples that share the head's user are summed across their lanes
+// (fixed butterfly order) and only the head writes gs[2 head]: a batch of
+// (1 positive + negs) per user writes one user row per group instead of fold.
 
 #include <cmath>
 
@@ -186,6 +190,19 @@ __device__ __forceinline__ f32x16 mchain2(f32x16 acc, FA fa, FB fb) {
     return acc;
 }
 
+// x summed over the FOLD consecutive lanes of its lane group (FOLD = 2, 4 or 8; all lanes
+// active): xor butterfly, the quad steps as DPP adds, the third on ds_swizzle (within 32 lanes).
+// Every lane of the group ends with the same value.
+template <int FOLD>
+__device__ __forceinline__ float fold_sum(float x) {
+    static_assert(FOLD == 2 || FOLD == 4 || FOLD == 8, "fold width");
+    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xB1, 0xF, 0xF, false));  // [1,0,3,2]
+    if constexpr (FOLD >= 4)
+        x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x4E, 0xF, 0xF, false));  // [2,3,0,1]
+    if constexpr (FOLD >= 8) x += __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(x), 0x1F | (4 << 10)));
+    return x;
+}
+
 // Phase timestamps of waves 0 and 3 (lane 0) for the first two tiles of every workgroup:
 // a profiling build (-DNCF_FUSED_TIMING) only; read with ncf_debug_fused_timing.
 #ifdef NCF_FUSED_TIMING
@@ -199,7 +216,7 @@ __device__ unsigned long long g_fused_t[256 * 2 * 2 * 16];
 #define NCF_T(ph) ((void)0)
 #endif
 
-template <class S>
+template <class S, int FOLD>
 __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict__ emb, const float* __restrict__ mlp,
                                                         const int32_t* __restrict__ users,
                                                         const int32_t* __restrict__ items,
@@ -290,6 +307,13 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
         // Masked samples read row 0 (a valid address) and get dz = 0: they contribute nothing.
         const bool ok = inb && (unsigned)u < (unsigned)ids.ubound && (unsigned)v < (unsigned)ids.ibound;
         const int urow = ok ? u : 0, irow = ok ? ids.ibase + v : 0;
+        // user-row folding: fmatch = this sample's user row joins its group head's sum; the head
+        // writes the sum, a sample with another user (any batch stays exact) its own row
+        constexpr int fm = FOLD > 1 ? FOLD - 1 : 0;
+        const int uhead = FOLD > 1 ? __shfl(u, lane_t - (j & fm), 64) : u;
+        const bool fmatch = FOLD > 1 && inb && u == uhead;
+        const bool fhead = (j & fm) == 0;
+        const bool ustore = inb && (fhead || !fmatch);
         if (h == 0) {
             srow[32 * w + j] = ok ? urow : -1;
             srow[128 + 32 * w + j] = ok ? irow : -1;
@@ -486,12 +510,20 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
                     contrib[4 * q + 1] = dz * (a.y * b.y);
                     contrib[4 * q + 2] = dz * (a.z * b.z);
                     contrib[4 * q + 3] = dz * (a.w * b.w);
-                    if (inb) {  // masked samples (dz = 0) write zero rows: the index may count their other, valid id
-                        const float4 gu4 = make_float4(dz * wo[f] * b.x, dz * wo[f + 1] * b.y, dz * wo[f + 2] * b.z,
-                                                       dz * wo[f + 3] * b.w);
+                    float4 gu4 = make_float4(dz * wo[f] * b.x, dz * wo[f + 1] * b.y, dz * wo[f + 2] * b.z,
+                                             dz * wo[f + 3] * b.w);
+                    if constexpr (FOLD > 1) {
+                        const float4 s = make_float4(fold_sum<FOLD>(fmatch ? gu4.x : 0.f),
+                                                     fold_sum<FOLD>(fmatch ? gu4.y : 0.f),
+                                                     fold_sum<FOLD>(fmatch ? gu4.z : 0.f),
+                                                     fold_sum<FOLD>(fmatch ? gu4.w : 0.f));
+                        if (fhead) gu4 = s;
+                    }
+                    // masked samples (dz = 0) write zero rows: the index may count their other, valid id
+                    if (ustore) st_stream(reinterpret_cast<float4*>(gu + h * S::GH + f), gu4);
+                    if (inb) {
                         const float4 gi4 = make_float4(dz * wo[f] * a.x, dz * wo[f + 1] * a.y, dz * wo[f + 2] * a.z,
                                                        dz * wo[f + 3] * a.w);
-                        st_stream(reinterpret_cast<float4*>(gu + h * S::GH + f), gu4);
                         st_stream(reinterpret_cast<float4*>(gi + h * S::GH + f), gi4);
                     }
                 }
@@ -567,15 +599,22 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_fused(const float* __restrict_
                     return (oc < L0 && k < L1) ? wl[S::SW1 + oc * S::LW1 + k] : 0.f;
                 },
                 [&](int t) { return g1[t / 16][t % 16]; });
-            if (inb) {  // masked samples (dz = 0) write zero rows: the index may count their other, valid id
+            f32x16 dx = acc;
+            if constexpr (FOLD > 1) if (32 * to < D0) {  // user-half rows: folded like the GMF part
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int f = 32 * to + 8 * q + 4 * h;  // rows drow(4q..4q+3, h) are f..f+3
-                    if (f < L0) {
-                        float* dst = (f < D0) ? gu + G + f : gi + G + (f - D0);
-                        st_stream(reinterpret_cast<float4*>(dst),
-                                  make_float4(acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]));
-                    }
+                for (int r = 0; r < 16; ++r) {
+                    const float s = fold_sum<FOLD>(fmatch ? acc[r] : 0.f);
+                    if (fhead && 32 * to + drow(r, h) < D0) dx[r] = s;
+                }
+            }
+            // masked samples (dz = 0) write zero rows: the index may count their other, valid id
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int f = 32 * to + 8 * q + 4 * h;  // rows drow(4q..4q+3, h) are f..f+3
+                if (f < L0 && (f < D0 ? ustore : inb)) {
+                    float* dst = (f < D0) ? gu + G + f : gi + G + (f - D0);
+                    st_stream(reinterpret_cast<float4*>(dst),
+                              make_float4(dx[4 * q], dx[4 * q + 1], dx[4 * q + 2], dx[4 * q + 3]));
                 }
             }
         }
@@ -951,23 +990,32 @@ template <class S>
 static hipError_t launch_one(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, const float* mlp,
                              const int32_t* users, const int32_t* items, const float* labels, int64_t n,
                              float inv_batch, IdSpace ids, int group, int topk, int* nslab, int* nbce, int* nmet,
-                             hipStream_t st) {
+                             hipStream_t st, int fold) {
     static bool configured = false;
     if (!configured) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_fb_fused<S>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)S::LDS_BYTES);
-        if (e != hipSuccess) return e;
+        for (const void* k : {(const void*)k_fb_fused<S, 0>, (const void*)k_fb_fused<S, 2>,
+                              (const void*)k_fb_fused<S, 4>, (const void*)k_fb_fused<S, 8>}) {
+            hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)S::LDS_BYTES);
+            if (e != hipSuccess) return e;
+        }
         configured = true;
     }
     const int64_t niter = (n + 127) / 128;
     int grid = (int)(niter < 256 ? niter : 256);
     if (grid > kMaxSlabs) grid = kMaxSlabs;
     const bool in_kernel = group > 0 && group <= 32 && 32 % group == 0;
-    launch(k_fb_fused<S>, grid, kBlock, S::LDS_BYTES, st, emb, mlp, users, items, labels, n, ids, inv_batch, at<float>(ws, L.probs),
-                                                      at<float>(ws, L.gs), at<float>(ws, L.slabs),
-                                                      at<float>(ws, L.part_bce), group, topk,
-                                                      in_kernel ? at<float>(ws, L.part_hit) : nullptr,
-                                                      in_kernel ? at<float>(ws, L.part_dcg) : nullptr);
+    auto go = [&](auto kern) {
+        launch(kern, grid, kBlock, S::LDS_BYTES, st, emb, mlp, users, items, labels, n, ids, inv_batch,
+               at<float>(ws, L.probs), at<float>(ws, L.gs), at<float>(ws, L.slabs), at<float>(ws, L.part_bce), group,
+               topk, in_kernel ? at<float>(ws, L.part_hit) : nullptr, in_kernel ? at<float>(ws, L.part_dcg) : nullptr);
+    };
+    switch (fold) {
+        case 0: go(k_fb_fused<S, 0>); break;
+        case 2: go(k_fb_fused<S, 2>); break;
+        case 4: go(k_fb_fused<S, 4>); break;
+        case 8: go(k_fb_fused<S, 8>); break;
+        default: return hipErrorInvalidValue;
+    }
     *nslab = grid;
     *nbce = grid;
     *nmet = in_kernel ? grid : 0;
@@ -977,11 +1025,13 @@ static hipError_t launch_one(const ncf_shape_t& s, const WsLayout& L, void* ws, 
 hipError_t launch_fb_fused(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, const float* mlp,
                            const int32_t* users, const int32_t* items, const float* labels, int64_t n,
                            float inv_batch, IdSpace ids, int group, int topk, int* nslab, int* nbce, int* nmet,
-                           hipStream_t st) {
+                           hipStream_t st, int fold) {
+    // the lanes of a fold group are consecutive samples of one 32-sample block
+    if (fold != 0 && (fold < 2 || fold > 8 || (fold & (fold - 1)) != 0 || n % fold != 0)) return hipErrorInvalidValue;
 #define NCF_TRY(SH)                                                                                             \
     if (matches<SH>(s))                                                                                         \
     return launch_one<SH>(s, L, ws, emb, mlp, users, items, labels, n, inv_batch, ids, group, topk, nslab, nbce, \
-                          nmet, st)
+                          nmet, st, fold)
     NCF_TRY(ShapeC);
     NCF_TRY(ShapeB);
     NCF_TRY(ShapeR);

@@ -39,11 +39,15 @@ struct KeySrc {
     const int32_t* keys;
     int32_t U, I;
     int32_t world;
-    int32_t S;  // shard rows (kKeyPairPerm) / key count (kKeyList)
+    int32_t S;     // shard rows (kKeyPairPerm) / key count (kKeyList)
+    int32_t fold;  // > 1: user rows folded per group of this size (fold_of, ncf_internal.h)
 };
 
+// Key of contribution c; *ok = the id is inside its table.  *own = false: a user contribution
+// folded into its group head's (it has a key — the plan's compact ids need it — but no slot).
 template <int MODE>
-__device__ inline int contrib_key(int64_t c, const KeySrc& k, bool* ok) {
+__device__ inline int contrib_key(int64_t c, const KeySrc& k, bool* ok, bool* own) {
+    *own = true;
     if constexpr (MODE == kKeyList) {
         const int v = k.keys[c];
         *ok = (unsigned)v < (unsigned)k.S;
@@ -58,6 +62,7 @@ __device__ inline int contrib_key(int64_t c, const KeySrc& k, bool* ok) {
         } else {
             const int u = k.users[i];
             *ok = (unsigned)u < (unsigned)k.U;
+            *own = !folded_user(k.users, i, k.fold);
             g = u;
         }
         if constexpr (MODE == kKeyPairPerm) {
@@ -75,13 +80,13 @@ __global__ __launch_bounds__(kBlock) void k_count(KeySrc ks, int64_t m, int32_t*
     const int64_t gstride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t cb = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); cb < m; cb += gstride) {
         const int64_t c = cb + (threadIdx.x & 63);
-        bool ok = false;
+        bool ok = false, own = true;
         int key = 0;
         if (c < m) {
-            key = contrib_key<MODE>(c, ks, &ok);
+            key = contrib_key<MODE>(c, ks, &ok, &own);
             if (!ok) atomicOr(err, kErrIdRange);
         }
-        wave_run_count(cnt, key, ok);
+        wave_run_count(cnt, key, ok && own);
     }
 }
 
@@ -128,7 +133,8 @@ template <int MODE, bool UNIQ, bool LIST>
 __global__ __launch_bounds__(kBlock) void k_fill(KeySrc ks, int64_t m, int32_t* __restrict__ cnt,
                                                  const int32_t* __restrict__ local, const int32_t* __restrict__ tot,
                                                  int nscan, int64_t r1, int32_t* __restrict__ offs_g,
-                                                 int32_t* __restrict__ list, PlanOut po, int32_t* __restrict__ err) {
+                                                 int32_t* __restrict__ list, PlanOut po, int32_t* __restrict__ err,
+                                                 int32_t* __restrict__ ifold) {
     extern __shared__ __attribute__((aligned(16))) int pre[];  // [nscan] (+ [nscan] unique prefix)
     __shared__ int sw[4];
     int* upre = pre + nscan;
@@ -137,6 +143,7 @@ __global__ __launch_bounds__(kBlock) void k_fill(KeySrc ks, int64_t m, int32_t* 
     const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t gstride = (int64_t)gridDim.x * blockDim.x;
     const int64_t K = r1 - 1;
+    if (gt == 0) *ifold = ks.fold;
     for (int64_t r = gt; r < r1; r += gstride) {
         const int o = local[r] + pre[r / kScanBlock];
         offs_g[r] = o;
@@ -166,7 +173,7 @@ __global__ __launch_bounds__(kBlock) void k_fill(KeySrc ks, int64_t m, int32_t* 
             if (threadIdx.x == 0) {
                 const int nu = uprefix(K);
                 *po.nuniq = nu;
-                po.uoffs[nu] = (int)m;
+                po.uoffs[nu] = local[K] + pre[K / kScanBlock];  // listed contributions (folded ones are not)
             }
         }
     }
@@ -179,14 +186,15 @@ __global__ __launch_bounds__(kBlock) void k_fill(KeySrc ks, int64_t m, int32_t* 
     const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
     for (int64_t cb = gt - lane; cb < m; cb += gstride) {
         const int64_t c = cb + lane;
-        bool ok = false;
+        bool ok = false, own = true;
         int key = 0;
         if (c < m) {
-            key = contrib_key<MODE>(c, ks, &ok);
+            key = contrib_key<MODE>(c, ks, &ok, &own);
             if constexpr (UNIQ) {
                 const int u = ok ? po.uloc[key] + upre[key / kScanBlock] : -1;
                 ((c & 1) ? po.cid_i : po.cid_u)[c >> 1] = u;
             }
+            ok = ok && own;
         }
         const int kk = ok ? key : -2 - lane;                 // inactive lanes: unique keys
         const int prev = __shfl_up(kk, 2, 64);
@@ -255,7 +263,8 @@ static hipError_t build(const WsLayout& L, void* ws, const KeySrc& ks, int64_t m
     const size_t pre_bytes = (size_t)nscan * 4 * (U2 ? 2 : 1);
     launch(k_fill<MODE, UNIQ, LIST>, grid_for(m > r1 ? m : r1, 1024), kBlock, pre_bytes, st, ks, m, cnt, local, tot,
                                                                                          nscan, r1, offs, list, po,
-                                                                                         at<int32_t>(ws, L.err));
+                                                                                         at<int32_t>(ws, L.err),
+                                                                                         at<int32_t>(ws, L.ifold));
     if (skip_sort) return hipGetLastError();
     if (hipError_t e = set_sort_lds(nwords)) return e;
     launch(k_sort, (unsigned)((K + kBlock - 1) / kBlock), kBlock, (size_t)nwords * 4, st, offs, K, list, nwords, cnt,
@@ -265,8 +274,8 @@ static hipError_t build(const WsLayout& L, void* ws, const KeySrc& ks, int64_t m
 
 hipError_t launch_index_build(const ncf_shape_t& s, const WsLayout& L, void* ws, const int32_t* users,
                               const int32_t* items, int64_t n, hipStream_t st, bool touched_list, bool counted,
-                              bool skip_sort) {
-    KeySrc ks{users, items, nullptr, s.num_users, s.num_items, 1, 0};
+                              bool skip_sort, int fold) {
+    KeySrc ks{users, items, nullptr, s.num_users, s.num_items, 1, 0, fold};
     if (touched_list) {
         PlanOut po{};
         po.uloc = at<int32_t>(ws, L.uloc);
@@ -281,15 +290,24 @@ hipError_t launch_index_build(const ncf_shape_t& s, const WsLayout& L, void* ws,
 
 hipError_t launch_shard_plan(const ncf_shape_t& s, const WsLayout& L, void* ws, const int32_t* users,
                              const int32_t* items, int64_t n, int32_t* uniq_rows, int32_t* send_counts,
-                             hipStream_t st) {
-    KeySrc ks{users, items, nullptr, s.num_users, s.num_items, L.world, (int32_t)L.shard_rows};
+                             hipStream_t st, int fold) {
+    KeySrc ks{users, items, nullptr, s.num_users, s.num_items, L.world, (int32_t)L.shard_rows, fold};
     PlanOut po{at<int32_t>(ws, L.uloc), at<int32_t>(ws, L.utot), uniq_rows, send_counts, at<int32_t>(ws, L.cid_u),
                at<int32_t>(ws, L.cid_i), at<int32_t>(ws, L.uoffs), at<int32_t>(ws, L.nuniq)};
     return build<kKeyPairPerm, true>(L, ws, ks, 2 * n, L.keys, po, (int)((2 * n + 31) / 32), st);
 }
 
+__global__ void k_fold_check(const int32_t* __restrict__ ifold, int fold, int32_t* __restrict__ err) {
+    if (threadIdx.x == 0 && *ifold != fold) atomicOr(err, kErrFold);
+}
+
+hipError_t launch_fold_check(const WsLayout& L, void* ws, int fold, hipStream_t st) {
+    launch(k_fold_check, 1, 64, 0, st, at<const int32_t>(ws, L.ifold), fold, at<int32_t>(ws, L.err));
+    return hipGetLastError();
+}
+
 hipError_t launch_owner_index(const WsLayout& L, void* ws, const int32_t* keys, int64_t m, hipStream_t st) {
-    KeySrc ks{nullptr, nullptr, keys, 0, 0, L.world, (int32_t)L.shard_rows};
+    KeySrc ks{nullptr, nullptr, keys, 0, 0, L.world, (int32_t)L.shard_rows, 0};
     // every source sends a row at most once: a key has <= world entries, so keys longer than
     // kSmallSeg (bitmap sort over m ids) exist only for world > kSmallSeg
     const int nwords = L.world > kSmallSeg ? (int)((m + 31) / 32) : 0;

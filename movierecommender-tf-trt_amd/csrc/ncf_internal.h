@@ -50,6 +50,7 @@ struct WsLayout {
     // row-sharded plan (world > 0 only; else empty): unique table rows of the batch
     size_t uloc;      // int32[K+1]  per-2048-key local exclusive scan of (cnt > 0)
     size_t utot;      // int32[nscan]
+    size_t ifold;     // int32       user-row folding of the last index build (persistent)
     size_t cid_u;     // int32[B]    compact (unique-row) id of each sample's user row
     size_t cid_i;     // int32[B]    compact id of each sample's item row
     size_t uoffs;     // int32[2B+1] compact row -> first list slot
@@ -121,9 +122,26 @@ __device__ inline void scan_local_body(const int32_t* __restrict__ cnt, int64_t 
     }
 }
 
+// User-row folding (the north star's duplicate-index reduction, done where the gradients are
+// made): the reference's batches are groups of group = negs + 1 samples sharing one user
+// (data_pipeline.py:141).  With fold = group (a power of two <= 32, fused kernel only), the
+// user-gradient rows of a group's samples whose user equals the group head's are summed inside
+// the kernel (lanes of one wave, fixed butterfly order) and written once, as the head's
+// contribution c = 2 * head; the others' user contributions do not exist.  Samples whose user
+// differs from the head's keep their own contribution, so any batch stays exact.  Fold widths
+// 2, 4 (the reference's default: 3 negatives) and 8 have fused-kernel variants.
+inline int fold_of(int group, bool fused) { return fused && (group == 2 || group == 4 || group == 8) ? group : 0; }
+__device__ __forceinline__ bool folded_user(const int32_t* __restrict__ users, int64_t i, int fold) {
+    if (fold <= 1) return false;
+    const int64_t hd = i - i % fold;
+    return i != hd && users[i] == users[hd];
+}
+
 // Workspace error flags (L.err, sticky until ncf_workspace_flags reads them).
 constexpr int kErrIdRange = 1;     // an index build met an id outside the table
 constexpr int kErrStaleCount = 4;  // a counted-ahead index met ids that differ from the counted ones
+constexpr int kErrFold = 8;        // an index built ahead folds user rows differently than the step
+                                   // using it (ncf_build_index / ncf_shard_plan hyper mismatch)
 
 // cnt/err (optional): every row's counter must be back at zero after k_fill; a residue means the
 // ids changed after they were counted ahead (ncf_train_step_ahead) — flagged, and the counter
@@ -273,14 +291,17 @@ __host__ __device__ inline T* at(void* base, size_t off) {
 
 // index build: contribution c = 2*i + side (0 user row, 1 item row) grouped by table row
 // touched_list: also the ascending list of the touched rows (ws touched, count in nuniq)
+// fold: user-row folding group (fold_of), 0 = every sample's user row is a contribution
 hipError_t launch_index_build(const ncf_shape_t& s, const WsLayout& L, void* ws, const int32_t* users,
                               const int32_t* items, int64_t n, hipStream_t st, bool touched_list = false,
-                              bool counted = false, bool skip_sort = false);
+                              bool counted = false, bool skip_sort = false, int fold = 0);
 // row-sharded plan: index over owner-major keys + unique-row compaction (uniq_rows = local row
 // ids grouped by owner, send_counts[world], cid_u/cid_i/uoffs/nuniq in the workspace)
+// flags kErrFold unless the last index build folded with `fold` (an index built in another call)
+hipError_t launch_fold_check(const WsLayout& L, void* ws, int fold, hipStream_t st);
 hipError_t launch_shard_plan(const ncf_shape_t& s, const WsLayout& L, void* ws, const int32_t* users,
                              const int32_t* items, int64_t n, int32_t* uniq_rows, int32_t* send_counts,
-                             hipStream_t st);
+                             hipStream_t st, int fold = 0);
 // owner index: m received local row ids keys[j] grouped by row (ascending j), S = L.shard_rows keys
 hipError_t launch_owner_index(const WsLayout& L, void* ws, const int32_t* keys, int64_t m, hipStream_t st);
 // compact gradient: out[u] = sum over the plan's contributions of unique row u (ascending c)
@@ -303,10 +324,11 @@ hipError_t launch_predict_generic(const ncf_shape_t& s, const WsLayout& L, void*
 
 // fused MFMA forward+backward (shapes with s.fast_path); same outputs as the generic kernel
 // also computes the hr/dcg group metrics in-kernel when group divides 32 (*nmet = partial count, else 0)
+// fold (fold_of(group, true) or 0): user-row folding, as the index was built with
 hipError_t launch_fb_fused(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb,
                            const float* mlp, const int32_t* users, const int32_t* items, const float* labels,
                            int64_t n, float inv_batch, IdSpace ids, int group, int topk, int* nslab, int* nbce,
-                           int* nmet, hipStream_t st);
+                           int* nmet, hipStream_t st, int fold = 0);
 bool fused_supported(const ncf_shape_t& s);
 // fused MFMA forward only (shapes with s.fast_path): probs; with labels also one BCE partial per
 // workgroup in ws part_bce (*nbce of them)
@@ -360,7 +382,7 @@ hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, vo
                                      float* v, int32_t* row_step, int32_t* step, const ncf_hyper_t& h,
                                      hipStream_t st, const int32_t* next_users = nullptr,
                                      const int32_t* next_items = nullptr, int64_t n_next = 0,
-                                     const MlpDeferred* mlp = nullptr);
+                                     const MlpDeferred* mlp = nullptr, int next_fold = 0);
 // dense gradient of rows [row_begin, num_rows) into out (indexed from row_begin)
 hipError_t launch_emb_grad_dense(const ncf_shape_t& s, const WsLayout& L, void* ws, float* out, hipStream_t st,
                                   int64_t row_begin = 0);

@@ -398,6 +398,7 @@ struct CountAhead {
     int32_t U, I;
     int32_t* cnt;
     int replay;                // 1: also catch the next batch's stale rows up (catch-up ahead)
+    int fold;                  // user-row folding of the next batch's index (fold_of)
 };
 
 // the dense layers' Adam (k_mlp_update<ADAM>'s work) in blocks >= nupd + ncount of the same launch
@@ -467,7 +468,7 @@ __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_tou
                     const int64_t i = c >> 1;
                     const int id = (c & 1) ? ca.items[i] : ca.users[i];
                     const int bound = (c & 1) ? ca.I : ca.U;
-                    ok = (unsigned)id < (unsigned)bound;
+                    ok = (unsigned)id < (unsigned)bound && ((c & 1) || !folded_user(ca.users, i, ca.fold));
                     key = (c & 1) ? ca.U + id : id;
                 }
                 wave_run_count(ca.cnt, key, ok);
@@ -964,7 +965,7 @@ hipError_t launch_row_step_fill(int32_t* row_step, int64_t R, const int32_t* ste
 hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, void* ws, float* emb, float* m,
                                      float* v, int32_t* row_step, int32_t* step, const ncf_hyper_t& h,
                                      hipStream_t st, const int32_t* next_users, const int32_t* next_items,
-                                     int64_t n_next, const MlpDeferred* mlp) {
+                                     int64_t n_next, const MlpDeferred* mlp, int next_fold) {
     const bool replay_ahead = next_users != nullptr && NCF_CATCHUP_AHEAD;
     const uint32_t w4 = (uint32_t)(s.row_width / 4);
     const uint32_t n4 = (uint32_t)(s.num_rows * w4);
@@ -978,7 +979,7 @@ hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, vo
         // count (+ catch-up ahead) blocks: 64 contributions per block and pass
         const unsigned ncount = mc > 0 ? (unsigned)((mc + 63) / 64 < 4096 ? (mc + 63) / 64 : 4096) : 0u;
         CountAhead ca{(int)nupd, (int)ncount, next_users, next_items, mc, s.num_users, s.num_items,
-                      at<int32_t>(ws, L.cnt), replay_ahead ? 1 : 0};
+                      at<int32_t>(ws, L.cnt), replay_ahead ? 1 : 0, next_fold};
         MlpTail mt{};
         if (mlp) {
             mt = MlpTail{(s.mlp_params + kBlock - 1) / kBlock, mlp->p, mlp->m, mlp->v, s.mlp_params, mlp->slabs,

@@ -22,7 +22,7 @@ NCF_OPT_ADAM = 0
 NCF_OPT_SGD = 1
 NCF_NUM_STATS = 8
 NCF_NUM_SUMMARY = 8
-NCF_WSERR_ID_RANGE, NCF_WSERR_STALE_COUNT = 1, 4
+NCF_WSERR_ID_RANGE, NCF_WSERR_STALE_COUNT, NCF_WSERR_FOLD = 1, 4, 8
 SUM_BCE, SUM_HIT, SUM_DCG, SUM_GROUPS, SUM_REG = range(5)
 STAT_LOSS_SUM, STAT_HR_SUM, STAT_DCG_SUM, STAT_STEPS, STAT_LAST_LOSS, STAT_LAST_HR, STAT_LAST_DCG, STAT_BCE_SUM = \
     range(8)
@@ -87,7 +87,7 @@ _SIGNATURES = {
                                                  _vp]),
     "ncf_update_rows": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _i64, _i64, _i64, _vp,
                                        ctypes.c_size_t, _vp]),
-    "ncf_build_index": (ctypes.c_int, [_P(NcfShape), _vp, _vp, _i64, _vp, ctypes.c_size_t, _vp]),
+    "ncf_build_index": (ctypes.c_int, [_P(NcfShape), _P(NcfHyper), _vp, _vp, _i64, _vp, ctypes.c_size_t, _vp]),
     "ncf_lazy_flush": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _vp, ctypes.c_size_t,
                                       _vp]),
     "ncf_apply_update": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _i64, _i64, _vp, _vp,
@@ -95,7 +95,8 @@ _SIGNATURES = {
     "ncf_shard_rows": (ctypes.c_int, [_P(NcfShape), _i32, _P(_i64)]),
     "ncf_shard_workspace_size": (ctypes.c_int, [_P(NcfShape), _i64, _i32, _P(ctypes.c_size_t)]),
     "ncf_shard_workspace_init": (ctypes.c_int, [_P(NcfShape), _i64, _i32, _vp, ctypes.c_size_t, _vp]),
-    "ncf_shard_plan": (ctypes.c_int, [_P(NcfShape), _i32, _vp, _vp, _i64, _vp, _vp, _vp, ctypes.c_size_t, _vp]),
+    "ncf_shard_plan": (ctypes.c_int, [_P(NcfShape), _P(NcfHyper), _i32, _vp, _vp, _i64, _vp, _vp, _vp,
+                                      ctypes.c_size_t, _vp]),
     "ncf_gather_rows": (ctypes.c_int, [_P(NcfShape), _vp, _i64, _vp, _i64, _vp, _vp]),
     "ncf_shard_forward_backward": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfHyper), _i32, _vp, _i64, _vp,
                                                   _vp, _vp, _vp, _vp, _i64, _i32, _vp, ctypes.c_size_t, _vp]),
@@ -137,7 +138,7 @@ def profile_read(kernel):
     return ms.value, n.value
 
 _lib = None
-ABI_VERSION = 4   # include/movierec_ncf.h ncf_abi_version()
+ABI_VERSION = 5   # include/movierec_ncf.h ncf_abi_version()
 
 
 def lib():

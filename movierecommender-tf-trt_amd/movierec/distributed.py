@@ -136,9 +136,9 @@ class RowShardedDataParallel(object):
         else:
             dist.broadcast(self.eng.mlp, src, group=self.group)
 
-    def _fetch_rows(self, users, items):
+    def _fetch_rows(self, users, items, group=None):
         eng = self.eng
-        uniq, send_counts = eng.plan(users, items)
+        uniq, send_counts = eng.plan(users, items, group)
         _all_to_all(self.recv_counts, send_counts, None, None, self.group)
         counts = torch.cat([send_counts, self.recv_counts]).cpu().tolist()
         send, recv = counts[:self.world], counts[self.world:]
@@ -154,7 +154,7 @@ class RowShardedDataParallel(object):
         gb = n * self.world if global_batch is None else int(global_batch)
         inv = 1.0 / gb
         eng = self.eng
-        send, recv, nu, m = self._fetch_rows(users, items)
+        send, recv, nu, m = self._fetch_rows(users, items, group)
         eng.forward_backward(labels, group=group, k=k, inv_batch=inv, include_dense_reg=self.rank == 0)
         _all_to_all(eng.recv_grad[:m], eng.uniq_grad[:nu], recv, send, self.group)
         _all_reduce(eng.dense_buf, self.group)
@@ -298,7 +298,7 @@ class UserPartitionedDataParallel(object):
         work = _all_reduce_async(self.shared, self.group)
         eng.update_rows(0, U, inv)               # own users: overlaps the all-reduce
         if next_batch is not None and hasattr(eng, "build_index"):
-            eng.build_index(*next_batch)         # so does the next step's index
+            eng.build_index(*next_batch, group)  # so does the next step's index
         if work is not None:
             work.wait()
         eng.apply_update(self.grads, inv, rows=(U, R - U), moments_by_row=True)

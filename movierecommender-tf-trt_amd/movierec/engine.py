@@ -31,12 +31,13 @@ def keras_weight_names(layers, gmf_dim):
     return names + ["output/kernel", "output/bias"]
 
 
-def _same_ids(held, u, i, n):
-    """An index prepared for (users, items) tensors ``held`` = (u, i, n, u_version, i_version)
-    applies to this call's ids: same tensors (storage), same size, not modified in place since."""
-    hu, hi, hn, vu, vi = held
+def _same_ids(held, u, i, n, group):
+    """An index prepared for (users, items) tensors ``held`` = (u, i, n, u_version, i_version,
+    group) applies to this call's ids: same tensors (storage), same size, not modified in place
+    since, and the same sample group (the index folds a group's user rows, ncf_internal.h)."""
+    hu, hi, hn, vu, vi, hg = held
     return (hu.data_ptr() == u.data_ptr() and hi.data_ptr() == i.data_ptr() and hn == n and
-            hu._version == vu and hi._version == vi)
+            hu._version == vu and hi._version == vi and hg == group)
 
 
 class NCFEngine(object):
@@ -236,7 +237,7 @@ class NCFEngine(object):
         h.group, h.k = int(group), int(k)
         h.inv_batch = 1.0 / n if inv_batch is None else float(inv_batch)
         pc = self._counted
-        ready = pc is not None and _same_ids(pc, u, i, n)
+        ready = pc is not None and _same_ids(pc, u, i, n, h.group)
         if pc is not None and not ready:
             self._discard_counted()
         nu = ni = None
@@ -258,7 +259,7 @@ class NCFEngine(object):
                 # refill through torch (copy_, fill_, index assignment) bumps _version and the next
                 # call rebuilds the index; writes that bypass torch's version counter are caught on
                 # the device (NCF_WSERR_STALE_COUNT, check_errors)
-                self._counted = (nu, ni, nu.numel(), nu._version, ni._version)
+                self._counted = (nu, ni, nu.numel(), nu._version, ni._version, h.group)
             else:
                 N.check(N.lib().ncf_train_step(ctypes.byref(self.shape), ctypes.byref(self.model_s),
                                                ctypes.byref(self.optim_s), ctypes.byref(h), N.ptr(u), N.ptr(i),
@@ -278,6 +279,8 @@ class NCFEngine(object):
         N.check(N.lib().ncf_workspace_flags(ctypes.byref(self.shape), self.max_batch, N.ptr(self.ws), self.ws_bytes,
                                             N.ptr(flags), N.stream_handle(self.device)))
         f = int(flags.item())
+        if f & N.NCF_WSERR_FOLD:
+            raise RuntimeError("an index built ahead (build_index / plan) used another sample group than the step")
         if f & N.NCF_WSERR_STALE_COUNT:
             raise RuntimeError("a batch counted ahead (train_step next_batch=) changed its ids before its step: "
                                "that step's embedding update used a stale index")
@@ -407,7 +410,7 @@ class NCFEngine(object):
         h.group, h.k, h.inv_batch = int(group), int(k), float(inv_batch)
         # an index prebuilt by build_index is used only for the very tensors it was built from
         pb = self._prebuilt
-        ready = pb is not None and _same_ids(pb, u, i, n)
+        ready = pb is not None and _same_ids(pb, u, i, n, h.group)
         h.index_ready = 1 if ready else 0
         eg, mg, sm = grads
         r0, rc = (0, self.num_rows) if reg_rows is None else reg_rows
@@ -421,10 +424,10 @@ class NCFEngine(object):
             self._prebuilt = None
         self._part_n = n
 
-    def build_index(self, users, items):
+    def build_index(self, users, items, group):
         """Build the contribution index of the NEXT ``forward_backward_part`` batch now (e.g. under
         the current step's all-reduce); call after this step's ``update_rows``.  That call must
-        pass the same id tensors (checked by identity, else the index is rebuilt), and their
+        pass the same id tensors and ``group`` (checked, else the index is rebuilt), and the ids'
         contents must not change in between (a sampler that refills one buffer in place must not
         use this)."""
         self._discard_counted()
@@ -435,9 +438,12 @@ class NCFEngine(object):
         n = u.numel()
         if n > self.max_batch or u.data_ptr() != users.data_ptr() or i.data_ptr() != items.data_ptr():
             return
-        N.check(N.lib().ncf_build_index(ctypes.byref(self.shape), N.ptr(u), N.ptr(i), n, N.ptr(self.ws),
-                                        self.ws_bytes, N.stream_handle(self.device)))
-        self._prebuilt = (u, i, n, u._version, i._version)   # holds the tensors: their memory stays theirs
+        h = self.hyper
+        h.group = int(group)
+        N.check(N.lib().ncf_build_index(ctypes.byref(self.shape), ctypes.byref(h), N.ptr(u), N.ptr(i), n,
+                                        N.ptr(self.ws), self.ws_bytes, N.stream_handle(self.device)))
+        # holds the tensors: their memory stays theirs
+        self._prebuilt = (u, i, n, u._version, i._version, h.group)
 
     def update_rows(self, row_begin, row_count, inv_batch):
         """Optimizer step of rows [row_begin, row_begin + row_count) from the per-sample gradient

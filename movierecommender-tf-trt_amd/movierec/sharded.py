@@ -141,17 +141,24 @@ class ShardedNCFEngine(object):
             y = torch.from_numpy(np.ascontiguousarray(np.asarray(y).reshape(-1), dtype=np.float32))
         return y.reshape(-1).to(device=self.device, dtype=torch.float32, non_blocking=True).contiguous()
 
-    def plan(self, users, items):
-        """Unique rows of the batch grouped by owner: (uniq local-row ids, send_counts) on device."""
+    def plan(self, users, items, group=None):
+        """Unique rows of the batch grouped by owner: (uniq local-row ids, send_counts) on device.
+        ``group``: the sample group of the ``forward_backward`` that follows (its index folds a
+        group's user rows); None for a plan that only feeds ``predict_planned``."""
         u, i = self._ids(users), self._ids(items)
         n = u.numel()
         if i.numel() != n:
             raise ValueError("users and items differ in length")
         self._ensure_ws(n)
         self._n = n
-        N.check(N.lib().ncf_shard_plan(ctypes.byref(self.shape), self.world, N.ptr(u), N.ptr(i), n, N.ptr(self.uniq),
-                                       N.ptr(self.send_counts), N.ptr(self.ws), self.ws_bytes,
-                                       N.stream_handle(self.device)))
+        h = None
+        if group is not None:
+            h = self.hyper
+            h.group = int(group)
+        self._plan_group = None if group is None else int(group)
+        N.check(N.lib().ncf_shard_plan(ctypes.byref(self.shape), ctypes.byref(h) if h is not None else None,
+                                       self.world, N.ptr(u), N.ptr(i), n, N.ptr(self.uniq), N.ptr(self.send_counts),
+                                       N.ptr(self.ws), self.ws_bytes, N.stream_handle(self.device)))
         return self.uniq, self.send_counts
 
     def gather_rows(self, rows, m):
@@ -166,6 +173,9 @@ class ShardedNCFEngine(object):
         y = self._labels(labels)
         if y.numel() != self._n:
             raise ValueError("labels do not match the planned batch")
+        if getattr(self, "_plan_group", None) != int(group):
+            raise ValueError("the batch was planned for group %r, not %d: pass group= to plan()"
+                             % (getattr(self, "_plan_group", None), int(group)))
         h = self.hyper
         h.group, h.k, h.inv_batch = int(group), int(k), float(inv_batch)
         model = N.NcfModel(self.uniq_vals.data_ptr(), self.mlp.data_ptr())

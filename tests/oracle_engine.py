@@ -153,7 +153,7 @@ class OracleShardedEngine(object):
         g[g >= self.num_rows] = -1
         return g
 
-    def plan(self, users, items):
+    def plan(self, users, items, group=None):
         u = np.asarray(users, dtype=np.int64)
         v = np.asarray(items, dtype=np.int64)
         rows = np.stack([u, self.shape.num_users + v], 1).reshape(-1)   # c = 2i + side

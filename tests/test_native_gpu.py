@@ -387,7 +387,7 @@ def test_prebuilt_index_equals_inline_build():
             e.forward_backward_part(u, it, y, group=4, k=2, inv_batch=1.0 / 256, shared_row_begin=U, grads=grads)
             e.update_rows(0, U, 1.0 / 256)
             if ahead and s + 1 < len(batches):
-                e.build_index(batches[s + 1][0], batches[s + 1][1])
+                e.build_index(batches[s + 1][0], batches[s + 1][1], 4)
                 assert e._prebuilt is not None
             e.apply_update(grads, 1.0 / 256, rows=(U, shape.num_items), moments_by_row=True)
         torch.cuda.synchronize()
