@@ -117,7 +117,7 @@ def grad_rows(eng, batch, group):
     """Per-sample gradient rows one batch produces: B item rows plus the user rows — one per
     group when the fused kernel folds a group's user rows (include/movierec_ncf.h "User-row
     folding"; the synthetic batches share the user within a group), else B."""
-    fused = bool(eng.shape.fast_path) and not eng.hyper.force_generic
+    fused = bool(eng.fast_path)
     fold = group if (fused and group in (2, 4, 8) and os.environ.get("NCF_FOLD_USERS", "1") != "0") else 1
     return batch + batch // fold
 
@@ -614,7 +614,8 @@ def main():
 
     emb_kernel = "k_emb_adam_touched" if getattr(eng, "lazy", False) else "k_emb_update"
     traffic = pmc_traffic(emb_kernel, args.config, B, mode)
-    fb_kernel = {"fused-mfma": "k_fb_fused"}.get(getattr(eng, "kernel_path", ""), None)
+    kpath = eng.kernel_for(B) if hasattr(eng, "kernel_for") else ("fused-mfma-tile" if eng.fast_path else "generic")
+    fb_kernel = {"fused-mfma-tile": "k_fb_fused", "fused-mfma-unit": "k_fb_unit"}.get(kpath)
     fb_traffic = pmc_traffic(fb_kernel, args.config, B, mode) if fb_kernel else None
     par = {"single": "dp1 (one table)",
            "user": "dp%d user-partitioned data (rank r trains users u %% %d == r and alone holds their rows + "
@@ -667,10 +668,12 @@ def main():
                                   "(this config, batch and layout only; null if not measured)"}
     fb_achieved = fb_flops / (fb_ms * 1e-3) / 1e12
     fb_roof = {"bound": "mfma", "kernel": {
-                   "fused-mfma": "fused NeuMF forward+backward (k_fb_fused, fp32 MFMA)",
+                   "fused-mfma-tile": "fused NeuMF forward+backward, 128-sample tiles (k_fb_fused, fp32 MFMA "
+                                      "32x32x2)",
+                   "fused-mfma-unit": "fused NeuMF forward+backward, 32-sample units split by output feature "
+                                      "over a workgroup's waves (k_fb_unit, fp32 MFMA 16x16x4)",
                    "layered-rocblas": "layer-by-layer forward+backward (rocBLAS fp32 GEMMs + glue kernels, "
-                                      "ncf_layered.hip)"}.get(getattr(eng, "kernel_path", ""),
-                                                              "generic forward+backward"),
+                                      "ncf_layered.hip)"}.get(kpath, "generic forward+backward"),
                "achieved": round(fb_achieved, 2), "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                "frac": round(fb_achieved / FP32_MFMA_PEAK_TFS, 4), "traffic": fb_traffic,
                "traffic_unit": "HBM bytes per launch",
@@ -701,7 +704,7 @@ def main():
                      "synthetic (uniform ids, seeded; %d distinct batches cycled; random-init weights)" % len(pool)),
             "config": {"workload": cfg["workload"], "global_batch": B * world, "per_gpu_batch": B,
                        "negatives_per_positive": cfg["negs"], "parallelism": par,
-                       "kernel_path": getattr(eng, "kernel_path", "fused-mfma" if eng.fast_path else "generic")},
+                       "kernel_path": kpath},
             "roofline": fb_roof if dominant_fb else emb_roof,
             "roofline_emb_update" if dominant_fb else "roofline_fwd_bwd": emb_roof if dominant_fb else fb_roof,
             "index_build_ms": round(ms_idx / max(nidx, 1), 5),

@@ -118,7 +118,10 @@ typedef struct ncf_hyper {
     int32_t force_generic;              /* 1: the generic per-sample kernel even if fast_path;
                                            2: the layer-by-layer GEMM path (default for shapes the
                                            fused kernel does not hold whose dense weights exceed
-                                           12288 floats, e.g. config D) */
+                                           12288 floats, e.g. config D);
+                                           3 / 4: (fast_path shapes) the 128-sample tile kernel /
+                                           the 32-sample unit kernel whatever the batch size
+                                           (default: units up to 32768 samples, tiles above) */
     int32_t index_ready;                /* 1: the contribution index of this call's batch was built
                                            beforehand by ncf_build_index (same ids, same ws): skip it;
                                            2: its contributions were counted and scanned by the
@@ -127,6 +130,13 @@ typedef struct ncf_hyper {
 } ncf_hyper_t;
 
 int ncf_abi_version(void);
+
+/* The forward/backward kernel a training call with n samples runs (for reporting). */
+#define NCF_FB_GENERIC 0
+#define NCF_FB_LAYERED 1
+#define NCF_FB_TILE 2
+#define NCF_FB_UNIT 3
+int ncf_fb_kernel(const ncf_shape_t* shape, const ncf_hyper_t* hyper, int64_t n);
 const char* ncf_last_error(void);
 
 /* Validate the model dimensions and fill the derived fields.

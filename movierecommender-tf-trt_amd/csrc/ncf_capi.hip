@@ -107,6 +107,10 @@ struct SideStream {
     hipEvent_t fork = nullptr, join = nullptr;
 };
 
+#ifndef NCF_UNIT_MAX_BATCH
+#define NCF_UNIT_MAX_BATCH 32768  // batches up to this run the sample-unit kernel (measured crossover)
+#endif
+
 int side_stream_mode() {
     static const int mode = [] {
         const char* e = getenv("NCF_SIDE_STREAM");
@@ -154,7 +158,7 @@ hipError_t join_side(hipStream_t st, SideStream* ss) {
 }
 
 bool use_fused(const ncf_shape_t& s, const ncf_hyper_t* h) {
-    return s.fast_path && !(h && h->force_generic) && ncf::fused_supported(s);
+    return s.fast_path && !(h && (h->force_generic == 1 || h->force_generic == 2)) && ncf::fused_supported(s);
 }
 
 // forward only: the fused MFMA forward when the shape has it, else the generic per-sample kernel
@@ -168,6 +172,22 @@ hipError_t launch_predict(const ncf_shape_t& s, const ncf_hyper_t* h, const ncf:
 // Shapes the fused kernel does not hold: the layer-by-layer GEMM path when the dense weights
 // outgrow the generic kernel's LDS staging (config D), or when asked for (force_generic == 2);
 // the per-sample generic kernel for small models (the reference's test shapes) or force_generic == 1.
+// MFMA forward/backward kernel for a fused shape: the sample-unit kernel (ncf_unit.hip) or the
+// 128-sample tile kernel (ncf_fused.hip).  NCF_FB_KERNEL=unit|tile forces one.
+// hyper->force_generic 3 / 4 pick the tile / unit kernel per call.
+bool use_unit(const ncf_shape_t& s, const ncf_hyper_t* h, int64_t n) {
+    static const int mode = [] {
+        const char* e = getenv("NCF_FB_KERNEL");
+        if (!e) return 0;
+        return strcmp(e, "unit") == 0 ? 1 : strcmp(e, "tile") == 0 ? 2 : 0;
+    }();
+    if (!ncf::unit_supported(s)) return false;
+    if (h && h->force_generic == 3) return false;
+    if (h && h->force_generic == 4) return true;
+    if (mode) return mode == 1;
+    return n <= NCF_UNIT_MAX_BATCH;
+}
+
 // user-row folding of a step's index and fused kernel (ncf_internal.h fold_of); h NULL: none.
 // NCF_FOLD_USERS=0 turns it off (A/B measurements)
 int index_fold(const ncf_shape_t& s, const ncf_hyper_t* h) {
@@ -230,8 +250,9 @@ WsLayout make_layout(const ncf_shape_t& s, int64_t B, int world) {
     L.offs = take((size_t)(K + 1) * 4);
     L.tot = take((size_t)L.nscan * 4);
     L.part_bce = take((size_t)kMaxSlabs * 4 + (size_t)L.nmetric * 4);
-    L.part_hit = take((size_t)L.nmetric * 4);
-    L.part_dcg = take((size_t)L.nmetric * 4);
+    // one partial per metrics block or per fused workgroup (up to kMaxSlabs)
+    L.part_hit = take((size_t)(L.nmetric > kMaxSlabs ? L.nmetric : kMaxSlabs) * 4);
+    L.part_dcg = take((size_t)(L.nmetric > kMaxSlabs ? L.nmetric : kMaxSlabs) * 4);
     L.part_reg = take((size_t)(kUpdateGrid + (s.mlp_params + kBlock - 1) / kBlock) * 4);
     L.summary = take(NCF_NUM_SUMMARY * 4);
     L.slabs = take((size_t)kMaxSlabs * s.mlp_params * 4);
@@ -264,6 +285,12 @@ LaunchEvents& launch_events() {
 extern "C" {
 
 int ncf_abi_version(void) { return NCF_ABI_VERSION; }
+
+int ncf_fb_kernel(const ncf_shape_t* s, const ncf_hyper_t* h, int64_t n) {
+    if (int r = check_shape(s)) return r;
+    if (use_fused(*s, h)) return use_unit(*s, h, n) ? NCF_FB_UNIT : NCF_FB_TILE;
+    return use_layered(*s, h) ? NCF_FB_LAYERED : NCF_FB_GENERIC;
+}
 
 const char* ncf_last_error(void) { return g_err.c_str(); }
 
@@ -447,7 +474,10 @@ static int run_fb(const ncf_shape_t& s, const ncf::WsLayout& L, const ncf_model_
         }
     }
     prof_begin(NCF_K_FWD_BWD, st);
-    if (use_fused(s, h))
+    if (use_fused(s, h) && use_unit(s, h, n))
+        e = ncf::launch_fb_unit(s, L, ws, model->emb, model->mlp, users, items, labels, n, h->inv_batch, ids,
+                                h->group, h->k, &out->nslab, &out->nbce, &out->nmet, st, fold);
+    else if (use_fused(s, h))
         e = ncf::launch_fb_fused(s, L, ws, model->emb, model->mlp, users, items, labels, n, h->inv_batch, ids,
                                  h->group, h->k, &out->nslab, &out->nbce, &out->nmet, st, fold);
     else if (use_layered(s, h))

@@ -23,6 +23,7 @@ NCF_OPT_SGD = 1
 NCF_NUM_STATS = 8
 NCF_NUM_SUMMARY = 8
 NCF_WSERR_ID_RANGE, NCF_WSERR_STALE_COUNT, NCF_WSERR_FOLD = 1, 4, 8
+FB_KERNELS = {0: "generic", 1: "layered-rocblas", 2: "fused-mfma-tile", 3: "fused-mfma-unit"}
 SUM_BCE, SUM_HIT, SUM_DCG, SUM_GROUPS, SUM_REG = range(5)
 STAT_LOSS_SUM, STAT_HR_SUM, STAT_DCG_SUM, STAT_STEPS, STAT_LAST_LOSS, STAT_LAST_HR, STAT_LAST_DCG, STAT_BCE_SUM = \
     range(8)
@@ -87,6 +88,7 @@ _SIGNATURES = {
                                                  _vp]),
     "ncf_update_rows": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _i64, _i64, _i64, _vp,
                                        ctypes.c_size_t, _vp]),
+    "ncf_fb_kernel": (ctypes.c_int, [_P(NcfShape), _P(NcfHyper), _i64]),
     "ncf_build_index": (ctypes.c_int, [_P(NcfShape), _P(NcfHyper), _vp, _vp, _i64, _vp, ctypes.c_size_t, _vp]),
     "ncf_lazy_flush": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _vp, ctypes.c_size_t,
                                       _vp]),
@@ -159,6 +161,13 @@ def lib():
                                "(__graft_entry__.build())" % (LIB_PATH, got, ABI_VERSION))
         _lib = handle
     return _lib
+
+
+def check_value(rc):
+    """A call that returns a non-negative value or a negative status."""
+    if rc < 0:
+        check(rc)
+    return rc
 
 
 def check(rc):

@@ -45,7 +45,7 @@ class NCFEngine(object):
 
     def __init__(self, num_users, num_items, layers_sizes, gmf_dim=0, max_batch=65536, device=None,
                  optimizer="adam", lr=0.001, beta_1=0.9, beta_2=0.999, layers_l2reg=None,
-                 force_generic=False, force_layered=False, lazy_adam=False):
+                 force_generic=False, force_layered=False, lazy_adam=False, fb_kernel=None):
         """``lazy_adam``: deferred exact decay (``ncf_optim_t.row_step``) — a training step updates
         only the batch's rows, the others catch up on their missed zero-gradient steps when next
         touched or read; bitwise the dense Keras sweep (F5).  Needs layers_l2reg[0] == 0; the
@@ -91,23 +91,26 @@ class NCFEngine(object):
         self.hyper = N.NcfHyper()
         self._bind_optim()
         self.set_hyper(optimizer, lr, beta_1, beta_2, layers_l2reg or [0.0] * len(self.layers))
-        self.hyper.force_generic = 1 if force_generic else (2 if force_layered else 0)
+        if fb_kernel not in (None, "tile", "unit"):
+            raise ValueError("fb_kernel must be None, 'tile' or 'unit'")
+        self.hyper.force_generic = (1 if force_generic else 2 if force_layered else
+                                    {None: 0, "tile": 3, "unit": 4}[fb_kernel])
 
     # ------------------------------------------------------------------ setup
     @property
     def fast_path(self):
-        return bool(self.shape.fast_path) and not self.hyper.force_generic
+        return bool(self.shape.fast_path) and self.hyper.force_generic not in (1, 2)
+
+    def kernel_for(self, n):
+        """Forward/backward kernel a training call with n samples runs (ncf_fb_kernel):
+        "fused-mfma-unit", "fused-mfma-tile", "layered-rocblas" or "generic"."""
+        k = N.check_value(N.lib().ncf_fb_kernel(ctypes.byref(self.shape), ctypes.byref(self.hyper), int(n)))
+        return N.FB_KERNELS[k]
 
     @property
     def kernel_path(self):
-        """Forward/backward path the library takes for this shape (ncf_capi.hip use_fused /
-        use_layered): "fused-mfma", "layered-rocblas" or "generic"."""
-        fg = self.hyper.force_generic
-        if self.fast_path:
-            return "fused-mfma"
-        if len(self.layers) >= 2 and (fg == 2 or (fg == 0 and self.mlp_params > 12288)):
-            return "layered-rocblas"
-        return "generic"
+        """Forward/backward path at the engine's batch capacity (see kernel_for)."""
+        return self.kernel_for(max(self.max_batch, 1))
 
     def _bind_optim(self):
         self.optim_s = N.NcfOptim(self.emb_m.data_ptr(), self.emb_v.data_ptr(), self.mlp_m.data_ptr(),

@@ -77,7 +77,12 @@ class ShardedNCFEngine(object):
     # ------------------------------------------------------------------ setup
     @property
     def fast_path(self):
-        return bool(self.shape.fast_path) and not self.hyper.force_generic
+        return bool(self.shape.fast_path) and self.hyper.force_generic not in (1, 2)
+
+    def kernel_for(self, n):
+        """Forward/backward kernel a call with n samples runs (ncf_fb_kernel)."""
+        k = N.check_value(N.lib().ncf_fb_kernel(ctypes.byref(self.shape), ctypes.byref(self.hyper), int(n)))
+        return N.FB_KERNELS[k]
 
     def set_hyper(self, optimizer, lr, beta_1=0.9, beta_2=0.999, layers_l2reg=None):
         h = self.hyper

@@ -1,0 +1,152 @@
+"""The two MFMA forward/backward kernels of the fused shapes — the 32-sample unit kernel
+(ncf_unit.hip, batches up to 32768 by default) and the 128-sample tile kernel (ncf_fused.hip,
+larger batches) — each against the oracle (reference movierec/model.py:154-214 restated) on the
+same batches, forced per engine (``fb_kernel=``) so both run at every size here.
+
+Tolerances as tests/test_native_gpu.py: gradients |dg| <= 1e-5 max|g|, probabilities 2e-6,
+weights after k steps k * 2e-6 + 2e-6 max|w|, BCE sum relative 1e-5, hr/dcg of the device
+probabilities exact.
+"""
+
+import numpy as np
+import pytest
+
+from conftest import gpu_available
+from oracle import ncf_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+if gpu_available():
+    import torch
+    from movierec.engine import NCFEngine
+
+FUSED_SHAPES = [
+    (200, 150, [128, 64, 32, 16], 64),  # config C
+    (120, 90, [64, 32, 16, 8], 8),      # config B
+    (120, 90, [64, 32, 16, 8], 0),      # reference trainer default (MLP-only)
+    (200, 150, [128, 64, 32, 16], 0),
+]
+IDS = ["configC", "configB", "mlp64", "mlp128"]
+
+
+def _weights(shape, seed):
+    from test_native_gpu import _weights as w
+    return w(shape, seed)
+
+
+def _batch(shape, B, group, seed):
+    rng = np.random.RandomState(seed)
+    users = rng.randint(0, shape.num_users, -(-B // group)).repeat(group)[:B]
+    items = rng.randint(0, shape.num_items, B)
+    y = np.tile([0] * (group - 1) + [1], -(-B // group))[:B].astype(np.float32)
+    return users.astype(np.int32), items.astype(np.int32), y
+
+
+def _engine(shape, w, kernel, max_batch=4096, **kw):
+    eng = NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=max_batch,
+                    fb_kernel=kernel, **kw)
+    eng.set_keras_weights(w)
+    return eng
+
+
+@pytest.mark.parametrize("dims", FUSED_SHAPES, ids=IDS)
+@pytest.mark.parametrize("kernel", ["unit", "tile"])
+@pytest.mark.parametrize("B,group", [(32, 4), (100, 4), (1000, 5), (2050, 2)])
+def test_grads_match_oracle(dims, kernel, B, group):
+    shape = O.NCFShape(*dims)
+    w = _weights(shape, 11)
+    users, items, y = _batch(shape, B, group, 12 + B)
+    eng = _engine(shape, w, kernel)
+    assert eng.kernel_for(B) == "fused-mfma-" + kernel
+    grads = eng.alloc_grads()
+    probs = torch.empty(B, dtype=torch.float32, device="cuda")
+    eng.forward_backward(users, items, y, group=group, k=2, inv_batch=1.0 / B, grads=grads, probs_out=probs)
+    _, g, _ = O.loss_and_grads(shape, w, users, items, y, [0.0] * len(shape.layers))
+    got = eng.keras_weights(grads[0], grads[1])
+    for name in O.weight_names(shape):
+        scale = np.max(np.abs(g[name])) + 1e-12
+        err = np.max(np.abs(got[name] - g[name]))
+        assert err <= 1e-5 * scale + 1e-9, (name, err, scale)
+    pref, _ = O.forward(shape, w, users, items)
+    assert np.max(np.abs(probs.cpu().numpy() - pref)) <= 2e-6
+    bce = O.bce_per_sample(pref, y).sum()
+    assert grads[2][0].item() == pytest.approx(bce, rel=1e-5)
+
+
+@pytest.mark.parametrize("dims", FUSED_SHAPES[:2], ids=IDS[:2])
+@pytest.mark.parametrize("lazy", [False, True], ids=["dense", "deferred"])
+def test_unit_train_steps_match_oracle(dims, lazy):
+    shape = O.NCFShape(*dims)
+    w = _weights(shape, 21)
+    eng = _engine(shape, w, "unit", lazy_adam=lazy)
+    ref = {k: v.copy() for k, v in w.items()}
+    st = O.new_opt_state(ref)
+    hyper = dict(optimizer="adam", lr=0.001, beta_1=0.9, beta_2=0.999, layers_l2reg=[0.0] * 4)
+    for s in range(3):
+        users, items, y = _batch(shape, 512, 4, 22 + s)
+        eng.train_step(users, items, y, group=4, k=2)
+        loss, _ = O.train_step(shape, ref, st, users, items, y, hyper)
+    got = eng.keras_weights()
+    for name in O.weight_names(shape):
+        tol = 3 * 2e-6 + 2e-6 * np.max(np.abs(ref[name]))
+        err = np.max(np.abs(got[name] - ref[name]))
+        assert err <= tol, (name, err, tol)
+    assert NCFEngine.read_stats(eng.stats)["loss"] > 0
+
+
+def test_unit_masked_ids_and_metrics():
+    """Ids outside the table: NaN probability, no gradient; in-kernel hr/dcg (group | 32) equal
+    the metric of the device probabilities."""
+    shape = O.NCFShape(*FUSED_SHAPES[0])
+    w = _weights(shape, 31)
+    users, items, y = _batch(shape, 256, 4, 32)
+    bad = np.zeros(256, bool)
+    bad[[5, 66, 200]] = True
+    users[5], items[66], users[200] = shape.num_users + 3, -2, -1
+    eng = _engine(shape, w, "unit")
+    grads = eng.alloc_grads()
+    probs = torch.empty(256, dtype=torch.float32, device="cuda")
+    eng.forward_backward(users, items, y, group=4, k=2, inv_batch=1.0 / 256, grads=grads, probs_out=probs)
+    p = probs.cpu().numpy()
+    assert np.isnan(p[bad]).all() and np.isfinite(p[~bad]).all()
+    ok = ~bad
+    _, g, _ = O.loss_and_grads(shape, w, users[ok], items[ok], y[ok], [0.0] * 4, batch_norm=256)
+    got = eng.keras_weights(grads[0], grads[1])
+    for name in O.weight_names(shape):
+        scale = np.max(np.abs(g[name])) + 1e-12
+        assert np.max(np.abs(got[name] - g[name])) <= 1e-5 * scale + 1e-9, name
+    # metrics: a clean batch through train_step, stats vs the oracle metric of the device probs
+    users, items, y = _batch(shape, 512, 4, 33)
+    eng2 = _engine(shape, w, "unit")
+    probs = torch.empty(512, dtype=torch.float32, device="cuda")
+    eng2.train_step(users, items, y, group=4, k=2, probs_out=probs)
+    hr, dcg = O.group_metrics(probs.cpu().numpy().astype(np.float64), y, 4, 2)
+    r = NCFEngine.read_stats(eng2.stats)
+    assert r["hr"] == pytest.approx(hr, abs=1e-6) and r["dcg"] == pytest.approx(dcg, abs=1e-6)
+
+
+def test_unit_deterministic_and_close_to_tile():
+    shape = O.NCFShape(*FUSED_SHAPES[0])
+    w = _weights(shape, 41)
+    users, items, y = _batch(shape, 4096, 4, 42)
+    outs = {}
+    for kernel in ("unit", "unit", "tile"):
+        eng = _engine(shape, w, kernel)
+        for _ in range(2):
+            eng.train_step(users, items, y, group=4, k=2)
+        torch.cuda.synchronize()
+        outs.setdefault(kernel, []).append((eng.emb.clone(), eng.mlp.clone()))
+    a, b = outs["unit"]
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    t = outs["tile"][0]
+    assert torch.max(torch.abs(a[0] - t[0])).item() <= 1e-6
+    assert torch.max(torch.abs(a[1] - t[1])).item() <= 1e-6
+
+
+def test_kernel_selection_by_batch():
+    shape = O.NCFShape(*FUSED_SHAPES[0])
+    eng = NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=256)
+    assert eng.kernel_for(8192) == "fused-mfma-unit"
+    assert eng.kernel_for(65536) == "fused-mfma-tile"
+    assert NCFEngine(5, 10, [6, 4], 0, max_batch=64).kernel_for(64) == "generic"
+    assert gpu_available()

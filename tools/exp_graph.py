@@ -1,6 +1,6 @@
 """Experiment: host cost of the eager training step vs hipGraph replay (torch.cuda.graph),
-config C, single table with deferred decay.  Checks that replay is bitwise the eager step.
-Usage (GPU box): python tools/exp_graph.py"""
+config C or B, single table with deferred decay (or the dense sweep).  Checks that replay is
+bitwise the eager step.  Usage (GPU box): python tools/exp_graph.py [lazy|dense] [C|B]"""
 import os
 import sys
 import time
@@ -13,8 +13,11 @@ import torch  # noqa: E402
 from movierec.engine import NCFEngine  # noqa: E402
 from movierec.model import initial_weights  # noqa: E402
 
-U, I, LAYERS, G, B, g = 138493, 27278, [128, 64, 32, 16], 64, 65536, 4
 mode = sys.argv[1] if len(sys.argv) > 1 else "lazy"
+cfg = sys.argv[2] if len(sys.argv) > 2 else "C"
+U, I, LAYERS, G, B, g = {"C": (138493, 27278, [128, 64, 32, 16], 64, 65536, 4),
+                         "B": (6040, 3952, [64, 32, 16, 8], 8, 4095, 5)}[cfg]
+print("config", cfg, mode, flush=True)
 w0 = initial_weights(U, I, LAYERS, G, seed=0)
 
 
