@@ -120,8 +120,7 @@ typedef struct ncf_hyper {
                                            fused kernel does not hold whose dense weights exceed
                                            12288 floats, e.g. config D);
                                            3 / 4: (fast_path shapes) the 128-sample tile kernel /
-                                           the 32-sample unit kernel whatever the batch size
-                                           (default: units up to 32768 samples, tiles above) */
+                                           the sample-unit kernel (the default) */
     int32_t index_ready;                /* 1: the contribution index of this call's batch was built
                                            beforehand by ncf_build_index (same ids, same ws): skip it;
                                            2: its contributions were counted and scanned by the

@@ -108,7 +108,9 @@ struct SideStream {
 };
 
 #ifndef NCF_UNIT_MAX_BATCH
-#define NCF_UNIT_MAX_BATCH 32768  // batches up to this run the sample-unit kernel (measured crossover)
+// batches up to this run the sample-unit kernel: it is the faster one at every size measured
+// (config C: 8192 22.4 vs 42.3 us, 65536 72 vs 80 us; profiles/r02_unit), so by default all
+#define NCF_UNIT_MAX_BATCH (1LL << 40)
 #endif
 
 int side_stream_mode() {

@@ -44,13 +44,19 @@ constexpr int cdiv(int a, int b) { return (a + b - 1) / b; }
 // (lanes: 16 consecutive rows x 4 columns), for ds_read_b32's 32-lane halves.
 constexpr int wstride(int lout) { return lout <= 16 ? 18 : lout <= 32 ? 36 : lout <= 64 ? 82 : 146; }
 
-template <int L0_, int L1_, int L2_, int L3_, int G_>
+template <int L0_, int L1_, int L2_, int L3_, int G_, int U_, int NG_>
 struct UShape {
-    static constexpr int L0 = L0_, L1 = L1_, L2 = L2_, L3 = L3_, G = G_;
+    static constexpr int L0 = L0_, L1 = L1_, L2 = L2_, L3 = L3_, G = G_, U = U_;
+    // NG unit groups of 4 waves per workgroup, each on its own unit (2: two waves per SIMD, the
+    // dense parameters in LDS once for both)
+    static constexpr int NG = NG_, NT = 256 * NG_;
     static_assert(L0 % 16 == 0 && L1 % 16 == 0 && L2 % 16 == 0 && L3 % 8 == 0 && L3 <= 16 && G % 8 == 0,
                   "unit-kernel shapes");
+    static_assert(U == 32 || U == 64, "unit size");
     static constexpr int D0 = L0 / 2, W = G + D0;
     static constexpr int B0 = L0 / 16, B1 = L1 / 16, B2 = L2 / 16, B3 = 1, P3 = 16;
+    static constexpr int NC = U / 16;  // 16-sample column blocks of a unit
+    static constexpr int NQ = U / 32;  // 32-sample halves (each its own [row][36] buffer)
     // flat dense-parameter offsets (include/movierec_ncf.h layout)
     static constexpr int OW1 = 0, OB1 = L0 * L1, OW2 = OB1 + L1, OB2 = OW2 + L1 * L2, OW3 = OB2 + L2,
                          OB3 = OW3 + L2 * L3, OWO = OB3 + L3, OBO = OWO + G + L3, P = OBO + 1;
@@ -59,29 +65,52 @@ struct UShape {
     static constexpr int SW1 = 0, SW2 = SW1 + L0 * LW1, SW3 = SW2 + L1 * LW2, SB1 = SW3 + L2 * LW3,
                          SB2 = SB1 + L1, SB3 = SB2 + L2, SWO = SB3 + P3, SBO = SWO + G + P3,
                          WLDS = (SBO + 1 + 3) / 4 * 4;
-    static constexpr int LA = 36;  // activation row stride (floats)
-    static constexpr int RX = 0, RH1 = RX + L0, RH2 = RH1 + L1, RH3 = RH2 + L2, RG1 = RH3 + P3, RG2 = RG1 + L1,
-                         RG3 = RG2 + L2, RN = RG3 + P3;
-    static constexpr int XP = L0 / 8;  // MLP-input floats gathered per thread (8 threads per sample)
-    static constexpr int GP = G / 8;   // GMF floats per thread
+    static constexpr int LA = 36;  // activation row stride (floats) of a 32-sample half
+    // (H3 never leaves registers: layer 3, the output and G3 share one phase)
+    static constexpr int RX = 0, RH1 = RX + L0, RH2 = RH1 + L1, RG1 = RH2 + L2, RG2 = RG1 + L1, RG3 = RG2 + L2,
+                         RN = RG3 + P3;
+    static constexpr int HS = RN * LA;  // floats per half
+    static constexpr int XP = L0 / 8;   // MLP-input floats gathered per thread and sample (8 threads per sample)
+    static constexpr int GP = G / 8;    // GMF floats per thread and sample
     static_assert(XP % 4 == 0, "float4 gather");
     static constexpr int NBIAS = L1 + L2 + L3;
-    static_assert(NBIAS <= 128, "bias rows: one per thread of waves 2-3");
-    static constexpr size_t LDS_BYTES = (size_t)(WLDS + RN * LA + 8 * 32 + 32 + 32) * 4;
+    static_assert(NBIAS <= 128, "bias rows: one per lane of roles 0-1");
+    static constexpr int GREG = NQ * HS + 8 * U + 5 * U;  // floats of one group's unit buffers
+    static constexpr size_t LDS_BYTES = (size_t)(WLDS + NG * GREG) * 4;
     static_assert(LDS_BYTES <= 163840, "LDS budget");
 };
 
-// A phase's Bo 16-row output blocks x 2 sample blocks over the 4 waves: Bo % 4 == 0 — wave w
-// takes blocks w, w+4, ... and both sample blocks (the A operand is read once for both);
-// Bo == 2 — one (block, sample block) pair per wave; Bo == 1 — waves 0-1, one sample block each.
-template <int Bo>
+// element (row, sample 32 half + c) of the activation buffers: 32-sample halves, [row][LA] each.
+// `half` is always known at compile time or wave-uniform at the call sites, so an operand read
+// is one ds_read with an immediate offset from a per-lane base.
+template <class S>
+__device__ __forceinline__ int aidx(int half, int row, int c) {
+    return half * S::HS + row * S::LA + c;
+}
+// sample column of 16-column block cb, lane li
+template <class S>
+__device__ __forceinline__ int cidx(int row, int cb, int li) {
+    return aidx<S>(cb >> 1, row, 16 * (cb & 1) + li);
+}
+// sample 4 t + lq (a K step of a weight-gradient chain; t < U / 4)
+template <class S>
+__device__ __forceinline__ int kidx(int row, int t, int lq) {
+    return aidx<S>(t >> 3, row, 4 * (t & 7) + lq);
+}
+
+// A phase's Bo 16-row output blocks x NC sample blocks over the 4 waves: Bo % 4 == 0 — wave w
+// takes blocks w, w+4, ... and every sample block (the A operand is read once for all);
+// Bo == 2 — one block, half the sample blocks per wave; Bo == 1 — the sample blocks split.
+template <int Bo, int NC>
 struct OutSplit {
     static_assert(Bo == 1 || Bo == 2 || Bo % 4 == 0, "output blocks");
     static constexpr int NA = Bo % 4 == 0 ? Bo / 4 : 1;
-    static constexpr int NB = Bo % 4 == 0 ? 2 : 1;
-    __device__ static bool active(int w) { return Bo != 1 || w < 2; }
+    static constexpr int NB = Bo % 4 == 0 ? NC : Bo == 2 ? NC / 2 : (NC >= 4 ? NC / 4 : 1);
+    __device__ static bool active(int w) { return Bo != 1 || NC >= 4 || w < 2; }
     __device__ static int ob(int w, int a) { return Bo % 4 == 0 ? w + 4 * a : Bo == 2 ? (w >> 1) : 0; }
-    __device__ static int cb(int w, int b) { return Bo % 4 == 0 ? b : (w & 1); }
+    __device__ static int cb(int w, int b) {
+        return Bo % 4 == 0 ? b : Bo == 2 ? (w & 1) * NB + b : (NC >= 4 ? w * NB + b : (w & 1));
+    }
 };
 
 // Weight-gradient tiles: Bi input blocks x Bo output blocks, each owned by one wave.
@@ -99,10 +128,12 @@ struct DwSplit {
 };
 
 // acc[a][b] += sum over NS steps of A(a, t) x B(b, t): NA x NB independent 16x16 chains, the
-// operands of the next 4 steps read (LDS) while the current 4 steps' MFMAs issue.
+// operands of the next CH steps read (LDS) while the current CH steps' MFMAs issue.  CH keeps a
+// chunk's reads within the 15 that lgkmcnt can count (more would force a full drain per chunk).
 template <int NS, int NA, int NB, class FA, class FB>
 __device__ __forceinline__ void mma_grid(f32x4 (&acc)[NA][NB], FA fa, FB fb) {
-    constexpr int CH = NS < 4 ? NS : 4;
+    constexpr int CHM = 15 / (NA + NB) >= 4 ? 4 : 15 / (NA + NB) >= 2 ? 2 : 1;
+    constexpr int CH = NS < CHM ? NS : CHM;
     static_assert(NS % CH == 0, "steps");
     float a[2][CH][NA], b[2][CH][NB];
 #pragma unroll
@@ -152,11 +183,11 @@ __device__ __forceinline__ float wave_half_sum(float x) {
 }
 
 // forward layer phase: out[o][s] = relu(sum_k W[k][o] in[k][s] + b[o]) (NS = K / 4 steps)
-template <int Bo, int NS, int LW, int LA>
+template <class S, int Bo, int NS, int LW>
 __device__ __forceinline__ void fwd_phase(const float* __restrict__ wt, const float* __restrict__ bias, int lout,
-                                          const float* __restrict__ in, float* __restrict__ out, int w, int li,
-                                          int lq) {
-    using A = OutSplit<Bo>;
+                                          const float* __restrict__ act, int rin, int rout, float* __restrict__ actw,
+                                          int w, int li, int lq) {
+    using A = OutSplit<Bo, S::NC>;
     if (!A::active(w)) return;
     f32x4 acc[A::NA][A::NB];
 #pragma unroll
@@ -165,7 +196,7 @@ __device__ __forceinline__ void fwd_phase(const float* __restrict__ wt, const fl
         for (int k = 0; k < A::NB; ++k) acc[i][k] = f32x4{0.f, 0.f, 0.f, 0.f};
     mma_grid<NS, A::NA, A::NB>(
         acc, [&](int a, int t) { return wt[(4 * t + lq) * LW + 16 * A::ob(w, a) + li]; },
-        [&](int b, int t) { return in[(4 * t + lq) * LA + 16 * A::cb(w, b) + li]; });
+        [&](int b, int t) { return act[cidx<S>(rin + 4 * t + lq, A::cb(w, b), li)]; });
 #pragma unroll
     for (int i = 0; i < A::NA; ++i)
 #pragma unroll
@@ -173,16 +204,16 @@ __device__ __forceinline__ void fwd_phase(const float* __restrict__ wt, const fl
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int row = 16 * A::ob(w, i) + 4 * lq + r;
-                out[row * LA + 16 * A::cb(w, k) + li] = row < lout ? fmaxf(acc[i][k][r] + bias[row], 0.f) : 0.f;
+                actw[cidx<S>(rout + row, A::cb(w, k), li)] =
+                    row < lout ? fmaxf(acc[i][k][r] + bias[row], 0.f) : 0.f;
             }
 }
 
 // backward data phase: gin[k][s] = (hin[k][s] > 0) ? sum_o W[k][o] gout[o][s] : 0
-template <int Bo, int NS, int LW, int LA>
-__device__ __forceinline__ void bwd_phase(const float* __restrict__ wt, const float* __restrict__ gout,
-                                          const float* __restrict__ hin, float* __restrict__ gin, int w, int li,
-                                          int lq) {
-    using A = OutSplit<Bo>;
+template <class S, int Bo, int NS, int LW>
+__device__ __forceinline__ void bwd_phase(const float* __restrict__ wt, const float* __restrict__ act, int rgout,
+                                          int rhin, int rgin, float* __restrict__ actw, int w, int li, int lq) {
+    using A = OutSplit<Bo, S::NC>;
     if (!A::active(w)) return;
     f32x4 acc[A::NA][A::NB];
 #pragma unroll
@@ -191,27 +222,27 @@ __device__ __forceinline__ void bwd_phase(const float* __restrict__ wt, const fl
         for (int k = 0; k < A::NB; ++k) acc[i][k] = f32x4{0.f, 0.f, 0.f, 0.f};
     mma_grid<NS, A::NA, A::NB>(
         acc, [&](int a, int t) { return wt[(16 * A::ob(w, a) + li) * LW + 4 * t + lq]; },
-        [&](int b, int t) { return gout[(4 * t + lq) * LA + 16 * A::cb(w, b) + li]; });
+        [&](int b, int t) { return act[cidx<S>(rgout + 4 * t + lq, A::cb(w, b), li)]; });
 #pragma unroll
     for (int i = 0; i < A::NA; ++i)
 #pragma unroll
         for (int k = 0; k < A::NB; ++k)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int o = (16 * A::ob(w, i) + 4 * lq + r) * LA + 16 * A::cb(w, k) + li;
-                gin[o] = hin[o] > 0.f ? acc[i][k][r] : 0.f;
+                const int row = 16 * A::ob(w, i) + 4 * lq + r, cb = A::cb(w, k);
+                actw[cidx<S>(rgin + row, cb, li)] = act[cidx<S>(rhin + row, cb, li)] > 0.f ? acc[i][k][r] : 0.f;
             }
 }
 
-// weight-gradient phase: acc[a][b] += in[kb-block][s] x g[ob-block][s] over the unit's 32 samples
-template <int Bi, int Bo, int LA, class ACC>
-__device__ __forceinline__ void dw_phase(ACC& acc, const float* __restrict__ in, const float* __restrict__ g, int w, int li,
+// weight-gradient phase: acc[a][b] += in[kb-block][s] x g[ob-block][s] over the unit's samples
+template <class S, int Bi, int Bo, class ACC>
+__device__ __forceinline__ void dw_phase(ACC& acc, const float* __restrict__ act, int rin, int rg, int w, int li,
                                          int lq) {
     using D = DwSplit<Bi, Bo>;
     if (!D::active(w)) return;
-    mma_grid<8, D::NA, D::NB>(
-        acc, [&](int a, int t) { return in[(16 * D::kb(w, a) + li) * LA + 4 * t + lq]; },
-        [&](int b, int t) { return g[(16 * D::ob(w, b) + li) * LA + 4 * t + lq]; });
+    mma_grid<S::U / 4, D::NA, D::NB>(
+        acc, [&](int a, int t) { return act[kidx<S>(rin + 16 * D::kb(w, a) + li, t, lq)]; },
+        [&](int b, int t) { return act[kidx<S>(rg + 16 * D::ob(w, b) + li, t, lq)]; });
 }
 
 template <int Bi, int Bo, class ACC>
@@ -237,7 +268,7 @@ __device__ __forceinline__ void dw_store(const ACC& acc, float* __restrict__ dst
 __device__ unsigned long long g_unit_t[256 * 2 * 4 * 20];
 #define NCF_UT(ph)                                                                                  \
     do {                                                                                            \
-        if (lane == 0 && blockIdx.x < 256 && itl < 2)                                               \
+        if (lane == 0 && gq == 0 && blockIdx.x < 256 && itl < 2)                                    \
             g_unit_t[((blockIdx.x * 2 + itl) * 4 + w) * 20 + (ph)] = __builtin_readcyclecounter(); \
     } while (0)
 #else
@@ -245,7 +276,7 @@ __device__ unsigned long long g_unit_t[256 * 2 * 4 * 20];
 #endif
 
 template <class S, int FOLD>
-__global__ __launch_bounds__(kBlock, 1) void k_fb_unit(const float* __restrict__ emb, const float* __restrict__ mlp,
+__global__ __launch_bounds__(S::NT, 1) void k_fb_unit(const float* __restrict__ emb, const float* __restrict__ mlp,
                                                        const int32_t* __restrict__ users,
                                                        const int32_t* __restrict__ items,
                                                        const float* __restrict__ labels, int64_t n, IdSpace ids,
@@ -253,33 +284,40 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_unit(const float* __restrict__
                                                        float* __restrict__ gs, float* __restrict__ slabs,
                                                        float* __restrict__ part_bce, int group, int topk,
                                                        float* __restrict__ part_hit, float* __restrict__ part_dcg) {
-    constexpr int L0 = S::L0, L1 = S::L1, L2 = S::L2, L3 = S::L3, G = S::G, D0 = S::D0, W = S::W, LA = S::LA;
-    constexpr int XP = S::XP, GP = S::GP, GPA = GP > 0 ? GP : 1;
+    constexpr int L0 = S::L0, L1 = S::L1, L2 = S::L2, L3 = S::L3, G = S::G, D0 = S::D0, W = S::W, U = S::U;
+    constexpr int XP = S::XP, GP = S::GP, GPA = GP > 0 ? GP : 1, NQ = S::NQ;
     extern __shared__ __attribute__((aligned(16))) float lds[];
     float* wl = lds;
-    float* act = lds + S::WLDS;                 // [RN][LA]
-    float* zpart = act + S::RN * LA;            // [8][32] GMF partial dots
-    float* dzb = zpart + 256;                   // [32] dz of the unit's samples
-    int* su = reinterpret_cast<int*>(dzb + 32);  // [32] their user ids (-1: past n)
+    const int gq = threadIdx.x >> 8;                 // this thread's unit group
+    float* act = lds + S::WLDS + gq * S::GREG;       // NQ halves of [RN][LA]
+    float* zpart = act + NQ * S::HS;                 // [8][U] GMF partial dots
+    float* dzb = zpart + 8 * U;                      // [U] dz of the unit's samples
+    int* su = reinterpret_cast<int*>(dzb + U);       // [U] their user ids (-1: past n)
+    float* prb = dzb + 2 * U;                        // [U] their probabilities (metrics, BCE)
+    float* yb = dzb + 3 * U;                         // [U] their labels
+    int* okb = reinterpret_cast<int*>(dzb + 4 * U);  // [U] id check passed
 
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int tid = threadIdx.x & 255, lane = tid & 63;
+    // the wave's role in its group; group 1 rotates the roles by two so that the two waves
+    // sharing a SIMD (waves i and i + 4) never both hold the output / metric / bias extras
+    const int w = ((tid >> 6) + 2 * gq) & 3;
     const int li = lane & 15, lq = lane >> 4;  // 16x16x4 operand coordinates
-    const int sj = lane & 31, p = tid >> 5;    // gather / GMF / output role: sample sj, part p
+    const int sj = lane & 31, p = tid >> 5;    // gather / GMF role: samples sj + 32 q, part p
     const float eps = 1e-7f, hi_clip = 1.0f - eps;
     const bool metrics = part_hit != nullptr;
 
     // dense parameters -> LDS (padding zeroed first: the L3 < 16 columns are read as zeros)
-    for (int e = tid; e < S::WLDS; e += kBlock) wl[e] = 0.f;
+    for (int e = threadIdx.x; e < S::WLDS; e += S::NT) wl[e] = 0.f;
     __syncthreads();
-    for (int e = tid; e < L0 * L1; e += kBlock) wl[S::SW1 + (e / L1) * S::LW1 + e % L1] = mlp[S::OW1 + e];
-    for (int e = tid; e < L1 * L2; e += kBlock) wl[S::SW2 + (e / L2) * S::LW2 + e % L2] = mlp[S::OW2 + e];
-    for (int e = tid; e < L2 * L3; e += kBlock) wl[S::SW3 + (e / L3) * S::LW3 + e % L3] = mlp[S::OW3 + e];
-    for (int e = tid; e < L1; e += kBlock) wl[S::SB1 + e] = mlp[S::OB1 + e];
-    for (int e = tid; e < L2; e += kBlock) wl[S::SB2 + e] = mlp[S::OB2 + e];
-    for (int e = tid; e < L3; e += kBlock) wl[S::SB3 + e] = mlp[S::OB3 + e];
-    for (int e = tid; e < G; e += kBlock) wl[S::SWO + e] = mlp[S::OWO + e];
-    for (int e = tid; e < L3; e += kBlock) wl[S::SWO + G + e] = mlp[S::OWO + G + e];
-    if (tid == 0) wl[S::SBO] = mlp[S::OBO];
+    for (int e = threadIdx.x; e < L0 * L1; e += S::NT) wl[S::SW1 + (e / L1) * S::LW1 + e % L1] = mlp[S::OW1 + e];
+    for (int e = threadIdx.x; e < L1 * L2; e += S::NT) wl[S::SW2 + (e / L2) * S::LW2 + e % L2] = mlp[S::OW2 + e];
+    for (int e = threadIdx.x; e < L2 * L3; e += S::NT) wl[S::SW3 + (e / L3) * S::LW3 + e % L3] = mlp[S::OW3 + e];
+    for (int e = threadIdx.x; e < L1; e += S::NT) wl[S::SB1 + e] = mlp[S::OB1 + e];
+    for (int e = threadIdx.x; e < L2; e += S::NT) wl[S::SB2 + e] = mlp[S::OB2 + e];
+    for (int e = threadIdx.x; e < L3; e += S::NT) wl[S::SB3 + e] = mlp[S::OB3 + e];
+    for (int e = threadIdx.x; e < G; e += S::NT) wl[S::SWO + e] = mlp[S::OWO + e];
+    for (int e = threadIdx.x; e < L3; e += S::NT) wl[S::SWO + G + e] = mlp[S::OWO + G + e];
+    if (threadIdx.x == 0) wl[S::SBO] = mlp[S::OBO];
     __syncthreads();
 
     using S1 = DwSplit<S::B0, S::B1>;
@@ -298,225 +336,240 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_unit(const float* __restrict__
     for (int a = 0; a < S3::NA; ++a)
 #pragma unroll
         for (int b = 0; b < S3::NB; ++b) dw3[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float acc_gmf[GPA], acc_h3[2];
+    float acc_gmf[GPA], acc_h3[4];  // acc_h3: output-kernel rows 4 lq + r of this lane's H3 samples
 #pragma unroll
     for (int e = 0; e < GPA; ++e) acc_gmf[e] = 0.f;
-    acc_h3[0] = acc_h3[1] = 0.f;
-    float acc_bias = 0.f, acc_bce = 0.f, acc_dbo = 0.f, acc_hit = 0.f, acc_dcg = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc_h3[e] = 0.f;
+    float acc_bias[1] = {0.f};
+    float acc_bce = 0.f, acc_dbo = 0.f, acc_hit = 0.f, acc_dcg = 0.f;
 
-    const int64_t nunits = (n + 31) / 32;
+    // ---- gather: thread (sj, p) brings part p of the MLP input of samples sj + 32 q (parts 0-3:
+    // the user half, 4-7: the item half) and part p of both GMF slices.  Masked samples read row
+    // 0 (a valid address) and get dz = 0: they contribute nothing.  The ids run two units ahead
+    // and the rows one unit ahead: the next unit's rows are in flight during this unit's dW phase.
+    const int64_t nunits = (n + U - 1) / U;
+    int cu[NQ], cv[NQ], nu[NQ], nv[NQ];
+    float cy[NQ], ny[NQ];
+    auto load_ids = [&](int64_t un, int (&u)[NQ], int (&v)[NQ], float (&y)[NQ]) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int64_t si = un * U + 32 * q + sj;
+            u[q] = 0, v[q] = 0, y[q] = 0.f;
+            if (un < nunits && si < n) {
+                u[q] = users[si];
+                v[q] = items[si];
+                y[q] = labels[si];
+            }
+        }
+    };
+    float4 xv[NQ][XP / 4];
+    float ug[NQ][GPA], ig[NQ][GPA];
+    auto load_rows = [&](int64_t un) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const bool okr = un * U + 32 * q + sj < n && (unsigned)cu[q] < (unsigned)ids.ubound &&
+                             (unsigned)cv[q] < (unsigned)ids.ibound;
+            const int urow = okr ? cu[q] : 0, irow = okr ? ids.ibase + cv[q] : 0;
+            const float4* xs =
+                reinterpret_cast<const float4*>(emb + (size_t)(p < 4 ? urow : irow) * W + G + (p & 3) * XP);
+#pragma unroll
+            for (int k = 0; k < XP / 4; ++k) xv[q][k] = xs[k];
+            if constexpr (G > 0) {
+                const float* us = emb + (size_t)urow * W + p * GP;
+                const float* is = emb + (size_t)irow * W + p * GP;
+                if constexpr (GP % 4 == 0) {
+#pragma unroll
+                    for (int k = 0; k < GP / 4; ++k) {
+                        const float4 a = reinterpret_cast<const float4*>(us)[k];
+                        const float4 b = reinterpret_cast<const float4*>(is)[k];
+                        ug[q][4 * k] = a.x, ug[q][4 * k + 1] = a.y, ug[q][4 * k + 2] = a.z, ug[q][4 * k + 3] = a.w;
+                        ig[q][4 * k] = b.x, ig[q][4 * k + 1] = b.y, ig[q][4 * k + 2] = b.z, ig[q][4 * k + 3] = b.w;
+                    }
+                } else {
+#pragma unroll
+                    for (int e = 0; e < GP; ++e) {
+                        ug[q][e] = us[e];
+                        ig[q][e] = is[e];
+                    }
+                }
+            }
+        }
+    };
+    // units of group gq: u0 + r * ustride; every group runs the workgroup's round count (the
+    // barriers are shared), a group past the end works on masked samples and adds nothing
+    const int64_t u0 = (int64_t)blockIdx.x * S::NG + gq, ustride = (int64_t)gridDim.x * S::NG;
+    const int64_t first = (int64_t)blockIdx.x * S::NG;
+    const int64_t rounds = nunits > first ? (nunits - first + ustride - 1) / ustride : 0;
+    load_ids(u0, cu, cv, cy);
+    load_rows(u0);
+    load_ids(u0 + ustride, nu, nv, ny);
+
+    const int fm = FOLD > 1 ? FOLD - 1 : 0;
     int itl = -1;
-    for (int64_t un = blockIdx.x; un < nunits; un += gridDim.x) {
+    for (int64_t r = 0; r < rounds; ++r) {
+        const int64_t un = u0 + r * ustride;
         ++itl;
         NCF_UT(0);
-        const int64_t s0 = un * 32;
-        // ---- gather: thread (sj, p) brings part p of its sample's MLP input (parts 0-3: the user
-        // half, 4-7: the item half) and part p of both GMF slices.  Masked samples read row 0 (a
-        // valid address) and get dz = 0: they contribute nothing.
-        const int64_t si = s0 + sj;
-        const bool inb = si < n;
-        int u = 0, v = 0;
-        float y = 0.f;
-        if (inb) {
-            u = users[si];
-            v = items[si];
-            y = labels[si];
-        }
-        const bool ok = inb && (unsigned)u < (unsigned)ids.ubound && (unsigned)v < (unsigned)ids.ibound;
-        const int urow = ok ? u : 0, irow = ok ? ids.ibase + v : 0;
-        {
-            const float4* xs = reinterpret_cast<const float4*>(emb + (size_t)(p < 4 ? urow : irow) * W + G + (p & 3) * XP);
-            float4 xv[XP / 4];
+        // lane coordinates re-derived opaquely every unit: keeps the compiler from hoisting the
+        // hundreds of lane-dependent LDS addresses out of the loop (and spilling them)
+        int lane_t = lane;
+        asm volatile("" : "+v"(lane_t));
+        const int li = lane_t & 15, lq = lane_t >> 4, sj = lane_t & 31;
+        const int64_t s0 = un * U;
+        bool inb[NQ], ok[NQ];
 #pragma unroll
-            for (int q = 0; q < XP / 4; ++q) xv[q] = xs[q];
+        for (int q = 0; q < NQ; ++q) {
+            inb[q] = s0 + 32 * q + sj < n;
+            ok[q] = inb[q] && (unsigned)cu[q] < (unsigned)ids.ubound && (unsigned)cv[q] < (unsigned)ids.ibound;
 #pragma unroll
-            for (int q = 0; q < XP / 4; ++q) {
-                float* dst = act + (S::RX + p * XP + 4 * q) * LA + sj;
-                dst[0] = xv[q].x;
-                dst[LA] = xv[q].y;
-                dst[2 * LA] = xv[q].z;
-                dst[3 * LA] = xv[q].w;
+            for (int k = 0; k < XP / 4; ++k) {
+                float* dst = act + aidx<S>(q, S::RX + p * XP + 4 * k, sj);
+                dst[0] = xv[q][k].x;
+                dst[S::LA] = xv[q][k].y;
+                dst[2 * S::LA] = xv[q][k].z;
+                dst[3 * S::LA] = xv[q][k].w;
+            }
+            if constexpr (G > 0) {
+                float zg = 0.f;
+#pragma unroll
+                for (int e = 0; e < GP; ++e) zg += wl[S::SWO + p * GP + e] * (ug[q][e] * ig[q][e]);
+                zpart[p * U + 32 * q + sj] = zg;
+            }
+            if (p == 0) {
+                su[32 * q + sj] = inb[q] ? cu[q] : -1;
+                yb[32 * q + sj] = cy[q];
+                okb[32 * q + sj] = ok[q] ? 1 : 0;
             }
         }
-        float ug[GPA], ig[GPA];
-        if constexpr (G > 0) {
-            const float* us = emb + (size_t)urow * W + p * GP;
-            const float* is = emb + (size_t)irow * W + p * GP;
-            if constexpr (GP % 4 == 0) {
-#pragma unroll
-                for (int q = 0; q < GP / 4; ++q) {
-                    const float4 a = reinterpret_cast<const float4*>(us)[q];
-                    const float4 b = reinterpret_cast<const float4*>(is)[q];
-                    ug[4 * q] = a.x, ug[4 * q + 1] = a.y, ug[4 * q + 2] = a.z, ug[4 * q + 3] = a.w;
-                    ig[4 * q] = b.x, ig[4 * q + 1] = b.y, ig[4 * q + 2] = b.z, ig[4 * q + 3] = b.w;
-                }
-            } else {
-#pragma unroll
-                for (int e = 0; e < GP; ++e) {
-                    ug[e] = us[e];
-                    ig[e] = is[e];
-                }
-            }
-            float zg = 0.f;
-#pragma unroll
-            for (int e = 0; e < GP; ++e) zg += wl[S::SWO + p * GP + e] * (ug[e] * ig[e]);
-            zpart[p * 32 + sj] = zg;
-        }
-        if (p == 0) su[sj] = inb ? u : -1;
         NCF_UT(1);
         __syncthreads();
         NCF_UT(2);
 
         // ---- forward
-        fwd_phase<S::B1, L0 / 4, S::LW1, LA>(wl + S::SW1, wl + S::SB1, L1, act + S::RX * LA, act + S::RH1 * LA, w,
-                                             li, lq);
+        fwd_phase<S, S::B1, L0 / 4, S::LW1>(wl + S::SW1, wl + S::SB1, L1, act, S::RX, S::RH1, act, w, li, lq);
         NCF_UT(3);
         __syncthreads();
         NCF_UT(4);
-        fwd_phase<S::B2, L1 / 4, S::LW2, LA>(wl + S::SW2, wl + S::SB2, L2, act + S::RH1 * LA, act + S::RH2 * LA, w,
-                                             li, lq);
+        fwd_phase<S, S::B2, L1 / 4, S::LW2>(wl + S::SW2, wl + S::SB2, L2, act, S::RH1, S::RH2, act, w, li, lq);
         NCF_UT(5);
         __syncthreads();
         NCF_UT(6);
-        fwd_phase<S::B3, L2 / 4, S::LW3, LA>(wl + S::SW3, wl + S::SB3, L3, act + S::RH2 * LA, act + S::RH3 * LA, w,
-                                             li, lq);
+        // ---- layer 3, output, dz and G3 in one phase: the roles holding an H3 block keep it in
+        // registers; z sums the block's 16 rows (4 per lane, then across the 4 lane groups)
+        {
+            using A = OutSplit<S::B3, S::NC>;
+            if (A::active(w)) {
+                f32x4 acc[1][A::NB];
+#pragma unroll
+                for (int k = 0; k < A::NB; ++k) acc[0][k] = f32x4{0.f, 0.f, 0.f, 0.f};
+                mma_grid<L2 / 4, 1, A::NB>(
+                    acc, [&](int, int t) { return wl[S::SW3 + (4 * t + lq) * S::LW3 + li]; },
+                    [&](int b, int t) { return act[cidx<S>(S::RH2 + 4 * t + lq, A::cb(w, b), li)]; });
+#pragma unroll
+                for (int k = 0; k < A::NB; ++k) {
+                    const int cb = A::cb(w, k), s = 16 * cb + li;
+                    float h[4], zp = 0.f;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int f = 4 * lq + r;
+                        h[r] = f < L3 ? fmaxf(acc[0][k][r] + wl[S::SB3 + f], 0.f) : 0.f;
+                        zp += wl[S::SWO + G + f] * h[r];
+                    }
+                    zp += __shfl_xor(zp, 16, 64);
+                    zp += __shfl_xor(zp, 32, 64);
+                    float z = zp;
+                    if constexpr (G > 0) {
+                        float zg = 0.f;
+#pragma unroll
+                        for (int q = 0; q < 8; ++q) zg += zpart[q * U + s];
+                        z += zg;
+                    }
+                    z += wl[S::SBO];
+                    const float pr = 1.0f / (1.0f + expf(-z));
+                    const bool okv = okb[s] != 0;
+                    const float dz = okv && pr >= eps && pr <= hi_clip ? (pr - yb[s]) * inv_batch : 0.0f;
+                    if (lq == 0) {
+                        if (s0 + s < n) probs[s0 + s] = okv ? pr : __int_as_float(0x7fc00000);
+                        dzb[s] = dz;
+                        prb[s] = pr;
+                        acc_dbo += dz;
+                    }
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int f = 4 * lq + r;
+                        act[cidx<S>(S::RG3 + f, cb, li)] = (f < L3 && h[r] > 0.f) ? dz * wl[S::SWO + G + f] : 0.f;
+                        acc_h3[r] += dz * h[r];
+                    }
+                }
+            }
+        }
         NCF_UT(7);
         __syncthreads();
         NCF_UT(8);
 
-        // ---- output, BCE, dz, hr/dcg (wave 0: lane half h sums every other H3 row)
-        if (w == 0) {
-            const int h = lane >> 5;
-            float zp = 0.f;
-#pragma unroll
-            for (int f = h; f < L3; f += 2) zp += wl[S::SWO + G + f] * act[(S::RH3 + f) * LA + sj];
-            float z = (zp + __shfl_xor(zp, 32, 64));
-            if constexpr (G > 0) {
-                float zg = 0.f;
-#pragma unroll
-                for (int q = 0; q < 8; ++q) zg += zpart[q * 32 + sj];
-                z += zg;
-            }
-            z += wl[S::SBO];
-            const float pr = 1.0f / (1.0f + expf(-z));
-            float dz = 0.f, bce = 0.f;
-            if (ok) {
-                const float pc = fminf(fmaxf(pr, eps), hi_clip);
-                const float logit = logf(pc / (1.0f - pc));
-                bce = fmaxf(logit, 0.0f) - logit * y + log1pf(expf(-fabsf(logit)));
-                dz = (pr >= eps && pr <= hi_clip) ? (pr - y) * inv_batch : 0.0f;
-            }
-            if (h == 0) {
-                if (inb) probs[si] = ok ? pr : __int_as_float(0x7fc00000);
-                dzb[sj] = dz;
-                acc_bce += bce;
-                acc_dbo += dz;
-            }
-            // RankLayer + _get_hits_per_user (model.py:344-455): label = first max of y;
-            // position = #(p > p_lab) + #(earlier ties)
-            if (metrics) {
-                const int e = sj % group;
-                const int base = 32 * h + sj - e;
-                int lab = 0;
-                float best = __shfl(y, base, 64);
-                for (int q = 1; q < group; ++q) {
-                    const float yq = __shfl(y, base + q, 64);
-                    if (yq > best) {
-                        best = yq;
-                        lab = q;
-                    }
-                }
-                const float pl = __shfl(pr, base + lab, 64);
-                int pos = 0;
-                for (int q = 0; q < group; ++q) {
-                    const float pq = __shfl(pr, base + q, 64);
-                    pos += (pq > pl) || (pq == pl && q < lab);
-                }
-                if (h == 0 && e == 0 && inb) {
-                    const float hit = pos < topk ? 1.f : 0.f;
-                    acc_hit += hit;
-                    acc_dcg += hit * (logf(2.0f) / logf((float)pos + 2.0f));
-                }
-            }
-        }
-        NCF_UT(9);
-        __syncthreads();
-        NCF_UT(10);
-
-        // ---- G3 and the output-kernel gradient of H3 (element slots e = tid, tid + 256)
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const int e = tid + 256 * q, f = e >> 5, s = e & 31;
-            const float h3 = act[(S::RH3 + f) * LA + s];
-            const float dz = dzb[s];
-            act[(S::RG3 + f) * LA + s] = (f < L3 && h3 > 0.f) ? dz * wl[S::SWO + G + f] : 0.f;
-            acc_h3[q] += dz * h3;
-        }
-        // ---- GMF backward: thread (sj, p), features [p GP, (p+1) GP) of its sample
-        const int fm = FOLD > 1 ? FOLD - 1 : 0;
+        // ---- GMF backward: thread (sj, p), features [p GP, (p+1) GP) of samples sj + 32 q
         if constexpr (G > 0) {
-            const float dz = dzb[sj];
-            const bool fmatch = FOLD > 1 && inb && su[sj] == su[sj & ~fm];
-            const bool fhead = (sj & fm) == 0;
-            float gu[GP], gi[GP];
 #pragma unroll
-            for (int e = 0; e < GP; ++e) {
-                const float wo = wl[S::SWO + p * GP + e];
-                gu[e] = dz * wo * ig[e];
-                gi[e] = dz * wo * ug[e];
-                acc_gmf[e] += dz * (ug[e] * ig[e]);
-            }
-            if constexpr (FOLD > 1) {
+            for (int q = 0; q < NQ; ++q) {
+                const int s = 32 * q + sj;
+                const float dz = dzb[s];
+                const bool fmatch = FOLD > 1 && inb[q] && su[s] == su[s & ~fm];
+                const bool fhead = (s & fm) == 0;
+                float gu[GP], gi[GP];
 #pragma unroll
                 for (int e = 0; e < GP; ++e) {
-                    const float sm = fold_sum<FOLD>(fmatch ? gu[e] : 0.f);
-                    if (fhead) gu[e] = sm;
+                    const float wo = wl[S::SWO + p * GP + e];
+                    gu[e] = dz * wo * ig[q][e];
+                    gi[e] = dz * wo * ug[q][e];
+                    acc_gmf[e] += dz * (ug[q][e] * ig[q][e]);
                 }
-            }
-            // masked samples (dz = 0) write zero rows: the index may count their other, valid id
-            float* gur = gs + (size_t)(2 * si) * W + p * GP;
-            float* gir = gur + W;
-            if (inb && (fhead || !fmatch)) {
-                if constexpr (GP % 4 == 0) {
+                if constexpr (FOLD > 1) {
 #pragma unroll
-                    for (int q = 0; q < GP / 4; ++q)
-                        st_stream(reinterpret_cast<float4*>(gur) + q,
-                                  make_float4(gu[4 * q], gu[4 * q + 1], gu[4 * q + 2], gu[4 * q + 3]));
-                } else {
-#pragma unroll
-                    for (int e = 0; e < GP; ++e) gur[e] = gu[e];
+                    for (int e = 0; e < GP; ++e) {
+                        const float sm = fold_sum<FOLD>(fmatch ? gu[e] : 0.f);
+                        if (fhead) gu[e] = sm;
+                    }
                 }
-            }
-            if (inb) {
-                if constexpr (GP % 4 == 0) {
+                // masked samples (dz = 0) write zero rows: the index may count their other, valid id
+                float* gur = gs + (size_t)(2 * (s0 + s)) * W + p * GP;
+                float* gir = gur + W;
+                if (inb[q] && (fhead || !fmatch)) {
+                    if constexpr (GP % 4 == 0) {
 #pragma unroll
-                    for (int q = 0; q < GP / 4; ++q)
-                        st_stream(reinterpret_cast<float4*>(gir) + q,
-                                  make_float4(gi[4 * q], gi[4 * q + 1], gi[4 * q + 2], gi[4 * q + 3]));
-                } else {
+                        for (int k = 0; k < GP / 4; ++k)
+                            st_stream(reinterpret_cast<float4*>(gur) + k,
+                                      make_float4(gu[4 * k], gu[4 * k + 1], gu[4 * k + 2], gu[4 * k + 3]));
+                    } else {
 #pragma unroll
-                    for (int e = 0; e < GP; ++e) gir[e] = gi[e];
+                        for (int e = 0; e < GP; ++e) gur[e] = gu[e];
+                    }
+                }
+                if (inb[q]) {
+                    if constexpr (GP % 4 == 0) {
+#pragma unroll
+                        for (int k = 0; k < GP / 4; ++k)
+                            st_stream(reinterpret_cast<float4*>(gir) + k,
+                                      make_float4(gi[4 * k], gi[4 * k + 1], gi[4 * k + 2], gi[4 * k + 3]));
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < GP; ++e) gir[e] = gi[e];
+                    }
                 }
             }
         }
-        NCF_UT(11);
-        __syncthreads();
-        NCF_UT(12);
-
-        // ---- backward data chain
-        bwd_phase<S::B2, S::P3 / 4, S::LW3, LA>(wl + S::SW3, act + S::RG3 * LA, act + S::RH2 * LA, act + S::RG2 * LA,
-                                                w, li, lq);
+        // ---- backward data chain (G2 shares the phase with the GMF backward)
+        bwd_phase<S, S::B2, S::P3 / 4, S::LW3>(wl + S::SW3, act, S::RG3, S::RH2, S::RG2, act, w, li, lq);
         NCF_UT(13);
         __syncthreads();
         NCF_UT(14);
-        bwd_phase<S::B1, L2 / 4, S::LW2, LA>(wl + S::SW2, act + S::RG2 * LA, act + S::RH1 * LA, act + S::RG1 * LA, w,
-                                             li, lq);
+        bwd_phase<S, S::B1, L2 / 4, S::LW2>(wl + S::SW2, act, S::RG2, S::RH1, S::RG1, act, w, li, lq);
         NCF_UT(15);
         __syncthreads();
         NCF_UT(16);
         // dX = W1 G1 -> the per-sample gradient rows (user half folded like the GMF part)
         {
-            using A = OutSplit<S::B0>;
+            using A = OutSplit<S::B0, S::NC>;
             f32x4 acc[A::NA][A::NB];
 #pragma unroll
             for (int i = 0; i < A::NA; ++i)
@@ -524,7 +577,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_unit(const float* __restrict__
                 for (int k = 0; k < A::NB; ++k) acc[i][k] = f32x4{0.f, 0.f, 0.f, 0.f};
             mma_grid<L1 / 4, A::NA, A::NB>(
                 acc, [&](int a, int t) { return wl[S::SW1 + (16 * A::ob(w, a) + li) * S::LW1 + 4 * t + lq]; },
-                [&](int b, int t) { return act[(S::RG1 + 4 * t + lq) * LA + 16 * A::cb(w, b) + li]; });
+                [&](int b, int t) { return act[cidx<S>(S::RG1 + 4 * t + lq, A::cb(w, b), li)]; });
 #pragma unroll
             for (int k = 0; k < A::NB; ++k) {
                 const int s = 16 * A::cb(w, k) + li;
@@ -538,7 +591,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_unit(const float* __restrict__
                     const int f0 = 16 * A::ob(w, i) + 4 * lq;
                     f32x4 d = acc[i][k];
                     if constexpr (FOLD > 1) {
-                        if (16 * A::ob(w, i) < D0) {  // uniform per wave: user-half block
+                        if (16 * A::ob(w, i) < D0) {  // uniform per wave: a user-half block
 #pragma unroll
                             for (int r = 0; r < 4; ++r) {
                                 const float sm = fold_sum<FOLD>(fmatch ? d[r] : 0.f);
@@ -554,18 +607,61 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_unit(const float* __restrict__
             }
         }
         NCF_UT(19);
-        // ---- weight gradients (operands in LDS) and bias rows
-        dw_phase<S::B0, S::B1, LA>(dw1, act + S::RX * LA, act + S::RG1 * LA, w, li, lq);
-        dw_phase<S::B1, S::B2, LA>(dw2, act + S::RH1 * LA, act + S::RG2 * LA, w, li, lq);
-        dw_phase<S::B2, S::B3, LA>(dw3, act + S::RH2 * LA, act + S::RG3 * LA, w, li, lq);
-        if (tid >= 128 && tid - 128 < S::NBIAS) {
-            const int br = tid - 128;
-            const int rr = br < L1 ? S::RG1 + br : br < L1 + L2 ? S::RG2 + (br - L1) : S::RG3 + (br - L1 - L2);
-            const float* row = act + rr * LA;
-            float sacc = 0.f;
+        // the next unit's rows (ids loaded a unit ago), and the ids of the one after
+        {
+            const int64_t un1 = un + ustride;
 #pragma unroll
-            for (int c = 0; c < 32; ++c) sacc += row[c];
-            acc_bias += sacc;
+            for (int q = 0; q < NQ; ++q) cu[q] = nu[q], cv[q] = nv[q], cy[q] = ny[q];
+            if (un1 < nunits) load_rows(un1);
+            load_ids(un1 + ustride, nu, nv, ny);
+        }
+        // ---- weight gradients (operands in LDS); bias rows (wave 3); BCE + hr/dcg (wave 2)
+        dw_phase<S, S::B0, S::B1>(dw1, act, S::RX, S::RG1, w, li, lq);
+        dw_phase<S, S::B1, S::B2>(dw2, act, S::RH1, S::RG2, w, li, lq);
+        dw_phase<S, S::B2, S::B3>(dw3, act, S::RH2, S::RG3, w, li, lq);
+        // extras beside the MFMA chains, one per role: bias rows 0-63 (role 0) and 64- (role 1),
+        // hr/dcg (role 2), BCE (role 3)
+        if (w < 2) {
+            const int br = lane + 64 * w;
+            if (br < S::NBIAS) {
+                const int rr = br < L1 ? S::RG1 + br : br < L1 + L2 ? S::RG2 + (br - L1) : S::RG3 + (br - L1 - L2);
+                float sacc = 0.f;
+#pragma unroll
+                for (int c = 0; c < U; ++c) sacc += act[aidx<S>(c >> 5, rr, c & 31)];
+                acc_bias[0] += sacc;
+            }
+        }
+        if (w == 3 && lane < U && okb[lane]) {
+            // Keras BCE of the clipped probability (binary_crossentropy through the logit); a
+            // masked sample adds nothing
+            const float pc = fminf(fmaxf(prb[lane], eps), hi_clip);
+            const float logit = logf(pc / (1.0f - pc));
+            acc_bce += fmaxf(logit, 0.0f) - logit * yb[lane] + log1pf(expf(-fabsf(logit)));
+        }
+        // RankLayer + _get_hits_per_user (model.py:344-455): label = first max of y; position =
+        // #(p > p_lab) + #(earlier ties)
+        if (metrics && w == 2 && lane < U) {
+            const int s = lane, e = s % group, base = s - e;
+            int lab = 0;
+            float best = yb[base];
+            for (int q = 1; q < group; ++q) {
+                const float yq = yb[base + q];
+                if (yq > best) {
+                    best = yq;
+                    lab = q;
+                }
+            }
+            const float pl = prb[base + lab];
+            int pos = 0;
+            for (int q = 0; q < group; ++q) {
+                const float pq = prb[base + q];
+                pos += (pq > pl) || (pq == pl && q < lab);
+            }
+            if (e == 0 && s0 + s < n) {
+                const float hit = pos < topk ? 1.f : 0.f;
+                acc_hit += hit;
+                acc_dcg += hit * (logf(2.0f) / logf((float)pos + 2.0f));
+            }
         }
         NCF_UT(17);
         __syncthreads();
@@ -573,18 +669,19 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_unit(const float* __restrict__
     }
 
     // ---- epilogue: this workgroup's dense-gradient slab and BCE / metric partials
-    float* slab = slabs + (size_t)blockIdx.x * S::P;
+    const int slot = blockIdx.x * S::NG + gq;  // this group's slab and partials
+    float* slab = slabs + (size_t)slot * S::P;
     dw_store<S::B0, S::B1>(dw1, slab + S::OW1, L0, L1, w, li, lq);
     dw_store<S::B1, S::B2>(dw2, slab + S::OW2, L1, L2, w, li, lq);
     dw_store<S::B2, S::B3>(dw3, slab + S::OW3, L2, L3, w, li, lq);
-    if (tid >= 128 && tid - 128 < S::NBIAS) {
-        const int br = tid - 128;
-        if (br < L1) slab[S::OB1 + br] = acc_bias;
-        else if (br < L1 + L2) slab[S::OB2 + (br - L1)] = acc_bias;
-        else slab[S::OB3 + (br - L1 - L2)] = acc_bias;
+    if (w < 2) {
+        const int br = lane + 64 * w;
+        if (br < L1) slab[S::OB1 + br] = acc_bias[0];
+        else if (br < L1 + L2) slab[S::OB2 + (br - L1)] = acc_bias[0];
+        else if (br < S::NBIAS) slab[S::OB3 + (br - L1 - L2)] = acc_bias[0];
     }
-    // output kernel: GMF entries (thread (sj, p): features p GP + e) and H3 entries (slot q:
-    // feature p + 8q), each summed over the 32 samples of a wave half
+    // output kernel, GMF entries: thread (sj, p) holds features p GP + e of its samples, summed
+    // over the 32 lanes of its wave half
     if constexpr (G > 0) {
 #pragma unroll
         for (int e = 0; e < GP; ++e) {
@@ -592,36 +689,48 @@ __global__ __launch_bounds__(kBlock, 1) void k_fb_unit(const float* __restrict__
             if (sj == 0) slab[S::OWO + p * GP + e] = v;
         }
     }
+    // H3 output-kernel rows, output bias, BCE, hr, dcg: summed over each role's lanes, then over
+    // the roles in role order through LDS (this group's GMF scratch: [role][20])
+    {
+        float* xr = zpart;
+        float v[4];
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const float v = wave_half_sum(acc_h3[q]);
-        const int f = p + 8 * q;
-        if (sj == 0 && f < L3) slab[S::OWO + G + f] = v;
-    }
-    if (w == 0) {
-        float dbo = acc_dbo, bce = acc_bce, hit = acc_hit, dcg = acc_dcg;
+        for (int r = 0; r < 4; ++r) {
+            v[r] = acc_h3[r];
 #pragma unroll
-        for (int m = 32; m >= 1; m >>= 1) {
-            dbo += __shfl_xor(dbo, m, 64);
-            bce += __shfl_xor(bce, m, 64);
-            hit += __shfl_xor(hit, m, 64);
-            dcg += __shfl_xor(dcg, m, 64);
+            for (int m = 8; m >= 1; m >>= 1) v[r] += __shfl_xor(v[r], m, 64);
+        }
+        float x[4] = {acc_dbo, acc_bce, acc_hit, acc_dcg};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int m = 32; m >= 1; m >>= 1) x[k] += __shfl_xor(x[k], m, 64);
+        if (li == 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) xr[w * 20 + 4 * lq + r] = v[r];
         }
         if (lane == 0) {
-            slab[S::OBO] = dbo;
-            part_bce[blockIdx.x] = bce;
-            if (metrics) {
-                part_hit[blockIdx.x] = hit;
-                part_dcg[blockIdx.x] = dcg;
-            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) xr[w * 20 + 16 + k] = x[k];
+        }
+        __syncthreads();
+        if (tid < 20) {
+            float t = 0.f;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) t += xr[r * 20 + tid];
+            if (tid < L3) slab[S::OWO + G + tid] = t;
+            else if (tid == 16) slab[S::OBO] = t;
+            else if (tid == 17) part_bce[slot] = t;
+            else if (tid == 18 && metrics) part_hit[slot] = t;
+            else if (tid == 19 && metrics) part_dcg[slot] = t;
         }
     }
 }
 
-using UShapeC = UShape<128, 64, 32, 16, 64>;  // ml-20m NeuMF (config C)
-using UShapeB = UShape<64, 32, 16, 8, 8>;     // ml-1m NeuMF (config B)
-using UShapeR = UShape<64, 32, 16, 8, 0>;     // reference trainer default (MLP-only)
-using UShapeC0 = UShape<128, 64, 32, 16, 0>;
+template <int U, int NG> using UShapeC = UShape<128, 64, 32, 16, 64, U, NG>;  // ml-20m NeuMF (config C)
+template <int U, int NG> using UShapeB = UShape<64, 32, 16, 8, 8, U, NG>;     // ml-1m NeuMF (config B)
+template <int U, int NG> using UShapeR = UShape<64, 32, 16, 8, 0, U, NG>;     // trainer default (MLP-only)
+template <int U, int NG> using UShapeC0 = UShape<128, 64, 32, 16, 0, U, NG>;
 
 template <class S>
 bool umatches(const ncf_shape_t& s) {
@@ -642,12 +751,13 @@ hipError_t launch_unit_one(const WsLayout& L, void* ws, const float* emb, const 
         }
         configured = true;
     }
-    const int64_t nunits = (n + 31) / 32;
-    int grid = (int)(nunits < 256 ? nunits : 256);
+    const int64_t nunits = (n + S::U - 1) / S::U;
+    const int64_t wgs = (nunits + S::NG - 1) / S::NG;
+    int grid = (int)(wgs < 256 ? wgs : 256);
     if (grid < 1) grid = 1;
     const bool in_kernel = group > 0 && group <= 32 && 32 % group == 0;
     auto go = [&](auto kern) {
-        launch(kern, grid, kBlock, S::LDS_BYTES, st, emb, mlp, users, items, labels, n, ids, inv_batch,
+        launch(kern, grid, S::NT, S::LDS_BYTES, st, emb, mlp, users, items, labels, n, ids, inv_batch,
                at<float>(ws, L.probs), at<float>(ws, L.gs), at<float>(ws, L.slabs), at<float>(ws, L.part_bce), group,
                topk, in_kernel ? at<float>(ws, L.part_hit) : nullptr, in_kernel ? at<float>(ws, L.part_dcg) : nullptr);
     };
@@ -658,10 +768,22 @@ hipError_t launch_unit_one(const WsLayout& L, void* ws, const float* emb, const 
         case 8: go(k_fb_unit<S, 8>); break;
         default: return hipErrorInvalidValue;
     }
-    *nslab = grid;
-    *nbce = grid;
-    *nmet = in_kernel ? grid : 0;
+    *nslab = grid * S::NG;
+    *nbce = grid * S::NG;
+    *nmet = in_kernel ? grid * S::NG : 0;
     return hipGetLastError();
+}
+
+// Schedule: one group of 32-sample units per workgroup while the units do not fill every CU
+// twice over, then two groups per workgroup (two waves per SIMD, one unit each);
+// NCF_UNIT_SCHED=1|2|64 forces one (64: one group of 64-sample units)
+int unit_sched(int64_t n) {
+    static const int forced = [] {
+        const char* e = getenv("NCF_UNIT_SCHED");
+        return e ? atoi(e) : 0;
+    }();
+    if (forced == 1 || forced == 2 || forced == 64) return forced;
+    return n >= 256 * 32 * 2 ? 2 : 1;
 }
 
 }  // namespace
@@ -674,7 +796,8 @@ extern "C" int ncf_debug_unit_timing(unsigned long long* out, size_t count) {
 #endif
 
 bool unit_supported(const ncf_shape_t& s) {
-    return umatches<UShapeC>(s) || umatches<UShapeB>(s) || umatches<UShapeR>(s) || umatches<UShapeC0>(s);
+    return umatches<UShapeC<32, 1>>(s) || umatches<UShapeB<32, 1>>(s) || umatches<UShapeR<32, 1>>(s) ||
+           umatches<UShapeC0<32, 1>>(s);
 }
 
 hipError_t launch_fb_unit(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, const float* mlp,
@@ -682,15 +805,18 @@ hipError_t launch_fb_unit(const ncf_shape_t& s, const WsLayout& L, void* ws, con
                           float inv_batch, IdSpace ids, int group, int topk, int* nslab, int* nbce, int* nmet,
                           hipStream_t st, int fold) {
     if (fold != 0 && (fold < 2 || fold > 8 || (fold & (fold - 1)) != 0 || n % fold != 0)) return hipErrorInvalidValue;
-#define NCF_TRY(SH)                                                                                                  \
-    if (umatches<SH>(s))                                                                                             \
-    return launch_unit_one<SH>(L, ws, emb, mlp, users, items, labels, n, inv_batch, ids, group, topk, nslab, nbce, \
-                               nmet, st, fold)
-    NCF_TRY(UShapeC);
-    NCF_TRY(UShapeB);
-    NCF_TRY(UShapeR);
-    NCF_TRY(UShapeC0);
+    const int sched = unit_sched(n);
+#define NCF_ARGS L, ws, emb, mlp, users, items, labels, n, inv_batch, ids, group, topk, nslab, nbce, nmet, st, fold
+#define NCF_TRY(SH)                                                                                 \
+    if (umatches<SH<32, 1>>(s))                                                                     \
+        return sched == 2 ? launch_unit_one<SH<32, 2>>(NCF_ARGS)                                    \
+                          : sched == 64 ? launch_unit_one<SH<64, 1>>(NCF_ARGS) : launch_unit_one<SH<32, 1>>(NCF_ARGS);
+    NCF_TRY(UShapeC)
+    NCF_TRY(UShapeB)
+    NCF_TRY(UShapeR)
+    NCF_TRY(UShapeC0)
 #undef NCF_TRY
+#undef NCF_ARGS
     return hipErrorInvalidValue;
 }
 

@@ -1,6 +1,6 @@
-"""The two MFMA forward/backward kernels of the fused shapes — the 32-sample unit kernel
-(ncf_unit.hip, batches up to 32768 by default) and the 128-sample tile kernel (ncf_fused.hip,
-larger batches) — each against the oracle (reference movierec/model.py:154-214 restated) on the
+"""The two MFMA forward/backward kernels of the fused shapes — the sample-unit kernel
+(ncf_unit.hip, the default) and the 128-sample tile kernel (ncf_fused.hip, hyper.force_generic 3)
+— each against the oracle (reference movierec/model.py:154-214 restated) on the
 same batches, forced per engine (``fb_kernel=``) so both run at every size here.
 
 Tolerances as tests/test_native_gpu.py: gradients |dg| <= 1e-5 max|g|, probabilities 2e-6,
@@ -94,6 +94,27 @@ def test_unit_train_steps_match_oracle(dims, lazy):
     assert NCFEngine.read_stats(eng.stats)["loss"] > 0
 
 
+@pytest.mark.parametrize("B", [16384 + 100, 20000])
+def test_two_group_schedule_matches_oracle(B):
+    """Batches of >= 16384 run two unit groups per workgroup (two waves per SIMD); uneven rounds
+    leave the last group of some workgroups on masked samples."""
+    shape = O.NCFShape(*FUSED_SHAPES[0])
+    w = _weights(shape, 51)
+    users, items, y = _batch(shape, B, 4, 52)
+    eng = _engine(shape, w, "unit", max_batch=B)
+    grads = eng.alloc_grads()
+    probs = torch.empty(B, dtype=torch.float32, device="cuda")
+    eng.forward_backward(users, items, y, group=4, k=2, inv_batch=1.0 / B, grads=grads, probs_out=probs)
+    _, g, _ = O.loss_and_grads(shape, w, users, items, y, [0.0] * 4)
+    got = eng.keras_weights(grads[0], grads[1])
+    for name in O.weight_names(shape):
+        scale = np.max(np.abs(g[name])) + 1e-12
+        assert np.max(np.abs(got[name] - g[name])) <= 1e-5 * scale + 1e-9, name
+    pref, _ = O.forward(shape, w, users, items)
+    assert np.max(np.abs(probs.cpu().numpy() - pref)) <= 2e-6
+    assert grads[2][0].item() == pytest.approx(O.bce_per_sample(pref, y).sum(), rel=1e-5)
+
+
 def test_unit_masked_ids_and_metrics():
     """Ids outside the table: NaN probability, no gradient; in-kernel hr/dcg (group | 32) equal
     the metric of the device probabilities."""
@@ -147,6 +168,8 @@ def test_kernel_selection_by_batch():
     shape = O.NCFShape(*FUSED_SHAPES[0])
     eng = NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=256)
     assert eng.kernel_for(8192) == "fused-mfma-unit"
-    assert eng.kernel_for(65536) == "fused-mfma-tile"
+    assert eng.kernel_for(65536) == "fused-mfma-unit"
+    assert NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=256,
+                     fb_kernel="tile").kernel_for(65536) == "fused-mfma-tile"
     assert NCFEngine(5, 10, [6, 4], 0, max_batch=64).kernel_for(64) == "generic"
     assert gpu_available()

@@ -21,11 +21,10 @@ from movierec import _native as N  # noqa: E402
 from movierec.engine import NCFEngine  # noqa: E402
 from movierec.model import initial_weights  # noqa: E402
 
-# stamp k: 0 unit start; odd = before barrier (k+1)/2, even = after it; 19 = dX done
+# stamps: 0 unit start, then before/after each barrier; 19 = dX done
 SEG = [("gather", 0, 1), ("bar1", 1, 2), ("L1", 2, 3), ("bar2", 3, 4), ("L2", 4, 5), ("bar3", 5, 6),
-       ("L3", 6, 7), ("bar4", 7, 8), ("out", 8, 9), ("bar5", 9, 10), ("g3+gmf_bwd", 10, 11), ("bar6", 11, 12),
-       ("G2", 12, 13), ("bar7", 13, 14), ("G1", 14, 15), ("bar8", 15, 16), ("dX", 16, 19), ("dW+bias", 19, 17),
-       ("bar9", 17, 18)]
+       ("L3+out+G3", 6, 7), ("bar4", 7, 8), ("gmf_bwd+G2", 8, 13), ("bar5", 13, 14), ("G1", 14, 15),
+       ("bar6", 15, 16), ("dX", 16, 19), ("dW+extras", 19, 17), ("bar7", 17, 18)]
 
 
 def main():
@@ -52,7 +51,8 @@ def main():
         res["wave%d" % w] = {name: round(float(np.mean(t[:, :, w, b] - t[:, :, w, a])), 1) for name, a, b in SEG}
     span = t[:, 1, 0, 18] - t[:, 0, 0, 0]
     res["two_units_cycles_mean"] = float(span.mean())
-    res["cycles_per_us_est"] = float(span.mean()) / 2 * (B // 32 / 256) / (ms / max(cnt, 1) * 1e3)
+    U = int(os.environ.get("NCF_UNIT_SIZE", "64" if B >= 16384 else "32"))
+    res["cycles_per_us_est"] = float(span.mean()) / 2 * (B // U / 256) / (ms / max(cnt, 1) * 1e3)
     print(json.dumps(res, indent=1))
 
 
