@@ -61,8 +61,9 @@ CONFIGS = {
     "C": dict(workload="ml-20m NeuMF (config C): 138493 users x 27278 items, gmf 64 + MLP [128,64,32,16], "
                        "3 neg/pos, Adam dense",
               num_users=138493, num_items=27278, layers=[128, 64, 32, 16], gmf_dim=64, negs=3, batch=65536),
-    "B": dict(workload="ml-1m NeuMF (config B shape): 6040 users x 3952 items, gmf 8 + MLP [64,32,16,8], 4 neg/pos",
-              num_users=6040, num_items=3952, layers=[64, 32, 16, 8], gmf_dim=8, negs=4, batch=4095),
+    "B": dict(workload="ml-1m NeuMF (config B shape): 6040 users x 3952 items, gmf 8 + MLP [64,32,16,8], 4 neg/pos, "
+                       "bf16 MLP operands (fp32 accumulation, master weights and Adam)",
+              num_users=6040, num_items=3952, layers=[64, 32, 16, 8], gmf_dim=8, negs=4, batch=4095, precision="bf16"),
     "D": dict(workload="synthetic 10M users x 1M items (config D): gmf 128 + MLP [256,128,64,32], 3 neg/pos, "
                        "Adam dense semantics via deferred exact decay, one GPU (layered rocBLAS GEMM path)",
               num_users=10000000, num_items=1000000, layers=[256, 128, 64, 32], gmf_dim=128, negs=3, batch=65536),
@@ -85,6 +86,8 @@ def parse():
                          "most 1024: every step trains on fresh uniform ids, as epochs over real data do; a "
                          "small pool leaves the users it never draws to owe the Keras dense decay of every step)")
     ap.add_argument("--generic", action="store_true", help="force the generic (non-MFMA) kernel")
+    ap.add_argument("--precision", default=None, choices=["fp32", "bf16"],
+                    help="MLP operand precision (default: the config's; bf16 = BASELINE config B)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0,
                     help="budget of the timed CPU baseline runs (the 5 runs share it)")
@@ -449,6 +452,9 @@ def main():
     if args.batch:
         cfg["batch"] = args.batch
     B, g = cfg["batch"], cfg["negs"] + 1
+    prec = args.precision or cfg.get("precision", "fp32")
+    if prec == "bf16" and mode == "sharded":
+        raise SystemExit("bf16 MLP operands run on the single-table and user-partitioned layouts")
     assert B % g == 0, "batch must be divisible by negs+1"
     big = args.config == "D"   # 11 GB table: initialised on the device, not through host numpy
     if big and mode != "single":
@@ -468,13 +474,14 @@ def main():
         ew = max(world, args.emulate_world)
         n_loc = (cfg["num_users"] - rank + ew - 1) // ew
         eng = NCFEngine(n_loc, cfg["num_items"], cfg["layers"], cfg["gmf_dim"], max_batch=B,
-                        force_generic=args.generic)
+                        force_generic=args.generic, precision=prec)
         eng.set_keras_weights(partition_keras_weights(w0, ew, rank))
         dp = UserPartitionedDataParallel(eng)
         dp.broadcast_parameters()
     else:
         eng = NCFEngine(cfg["num_users"], cfg["num_items"], cfg["layers"], cfg["gmf_dim"], max_batch=B,
-                        force_generic=args.generic, lazy_adam=(mode == "single" and not args.dense_sweep))
+                        force_generic=args.generic, lazy_adam=(mode == "single" and not args.dense_sweep),
+                        precision=prec)
         if big:
             device_glorot_init(eng, w0, seed=0)
         else:
@@ -698,7 +705,8 @@ def main():
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16 MLP operands, fp32 accumulate/master/Adam" if prec == "bf16" else "fp32",
             "data": ("synthetic ml-20m-shaped ratings (%d positives), negatives sampled on the device each step"
                      % len(sampler.data) if sampler is not None else
                      "synthetic (uniform ids, seeded; %d distinct batches cycled; random-init weights)" % len(pool)),

@@ -125,7 +125,12 @@ typedef struct ncf_hyper {
                                            beforehand by ncf_build_index (same ids, same ws): skip it;
                                            2: its contributions were counted and scanned by the
                                            previous ncf_train_step_ahead (same ids, same ws) */
-    int32_t reserved[5];
+    int32_t mlp_bf16;                   /* 1: the MLP tower's matrix products (forward, data and
+                                           weight gradients) take bf16 operands with fp32
+                                           accumulation; embeddings, GMF, loss, master weights
+                                           and Adam stay fp32 (BASELINE config B; fast_path
+                                           shapes, unit kernel only) */
+    int32_t reserved[4];
 } ncf_hyper_t;
 
 int ncf_abi_version(void);

@@ -476,9 +476,11 @@ static int run_fb(const ncf_shape_t& s, const ncf::WsLayout& L, const ncf_model_
         }
     }
     prof_begin(NCF_K_FWD_BWD, st);
+    if (h->mlp_bf16 && !(use_fused(s, h) && use_unit(s, h, n)))
+        return fail(NCF_EINVAL, "bf16 MLP operands need a fused-kernel shape and the unit kernel");
     if (use_fused(s, h) && use_unit(s, h, n))
         e = ncf::launch_fb_unit(s, L, ws, model->emb, model->mlp, users, items, labels, n, h->inv_batch, ids,
-                                h->group, h->k, &out->nslab, &out->nbce, &out->nmet, st, fold);
+                                h->group, h->k, &out->nslab, &out->nbce, &out->nmet, st, fold, h->mlp_bf16 != 0);
     else if (use_fused(s, h))
         e = ncf::launch_fb_fused(s, L, ws, model->emb, model->mlp, users, items, labels, n, h->inv_batch, ids,
                                  h->group, h->k, &out->nslab, &out->nbce, &out->nmet, st, fold);

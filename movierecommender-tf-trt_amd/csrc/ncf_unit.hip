@@ -92,11 +92,6 @@ template <class S>
 __device__ __forceinline__ int cidx(int row, int cb, int li) {
     return aidx<S>(cb >> 1, row, 16 * (cb & 1) + li);
 }
-// sample 4 t + lq (a K step of a weight-gradient chain; t < U / 4)
-template <class S>
-__device__ __forceinline__ int kidx(int row, int t, int lq) {
-    return aidx<S>(t >> 3, row, 4 * (t & 7) + lq);
-}
 
 // A phase's Bo 16-row output blocks x NC sample blocks over the 4 waves: Bo % 4 == 0 — wave w
 // takes blocks w, w+4, ... and every sample block (the A operand is read once for all);
@@ -127,21 +122,27 @@ struct DwSplit {
     __device__ static int ob(int w, int b) { return BYI ? b : HALF ? (w >> 1) * NB + b : QUART ? w * NB + b : b; }
 };
 
-// acc[a][b] += sum over NS steps of A(a, t) x B(b, t): NA x NB independent 16x16 chains, the
-// operands of the next CH steps read (LDS) while the current CH steps' MFMAs issue.  CH keeps a
-// chunk's reads within the 15 that lgkmcnt can count (more would force a full drain per chunk).
-template <int NS, int NA, int NB, class FA, class FB>
-__device__ __forceinline__ void mma_grid(f32x4 (&acc)[NA][NB], FA fa, FB fb) {
+// acc[a][b] += sum over the K steps of A(a, k) x B(b, k): NA x NB independent 16x16 chains.
+// The operand functions take (block, kc, kr) with k = kc + kr: kc known at compile time, kr the
+// lane's offset (lq for the fp32 16x16x4 form, 4 lq for bf16 16x16x16), so an LDS operand is a
+// read at an immediate offset from a per-lane base.
+//
+// fp32 (v_mfma_f32_16x16x4_f32): lane (li, lq) supplies k = 4 t + lq.  The operands of the next CH
+// steps are read while the current CH steps' MFMAs issue; CH keeps a chunk's reads within the 15
+// that lgkmcnt can count (more would force a full drain per chunk).
+template <int K, int NA, int NB, class FA, class FB>
+__device__ __forceinline__ void mma_grid(f32x4 (&acc)[NA][NB], FA fa, FB fb, int lq) {
+    constexpr int NS = K / 4;
     constexpr int CHM = 15 / (NA + NB) >= 4 ? 4 : 15 / (NA + NB) >= 2 ? 2 : 1;
     constexpr int CH = NS < CHM ? NS : CHM;
-    static_assert(NS % CH == 0, "steps");
+    static_assert(K % 4 == 0 && NS % CH == 0, "steps");
     float a[2][CH][NA], b[2][CH][NB];
 #pragma unroll
     for (int e = 0; e < CH; ++e) {
 #pragma unroll
-        for (int i = 0; i < NA; ++i) a[0][e][i] = fa(i, e);
+        for (int i = 0; i < NA; ++i) a[0][e][i] = fa(i, 4 * e, lq);
 #pragma unroll
-        for (int i = 0; i < NB; ++i) b[0][e][i] = fb(i, e);
+        for (int i = 0; i < NB; ++i) b[0][e][i] = fb(i, 4 * e, lq);
     }
 #pragma unroll
     for (int c = 0; c < NS / CH; ++c) {
@@ -149,9 +150,9 @@ __device__ __forceinline__ void mma_grid(f32x4 (&acc)[NA][NB], FA fa, FB fb) {
 #pragma unroll
             for (int e = 0; e < CH; ++e) {
 #pragma unroll
-                for (int i = 0; i < NA; ++i) a[(c + 1) & 1][e][i] = fa(i, CH * (c + 1) + e);
+                for (int i = 0; i < NA; ++i) a[(c + 1) & 1][e][i] = fa(i, 4 * (CH * (c + 1) + e), lq);
 #pragma unroll
-                for (int i = 0; i < NB; ++i) b[(c + 1) & 1][e][i] = fb(i, CH * (c + 1) + e);
+                for (int i = 0; i < NB; ++i) b[(c + 1) & 1][e][i] = fb(i, 4 * (CH * (c + 1) + e), lq);
             }
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -163,6 +164,51 @@ __device__ __forceinline__ void mma_grid(f32x4 (&acc)[NA][NB], FA fa, FB fb) {
                 for (int ib = 0; ib < NB; ++ib) acc[ia][ib] = mfma16(a[c & 1][e][ia], b[c & 1][e][ib], acc[ia][ib]);
         __builtin_amdgcn_sched_barrier(0);
     }
+}
+
+// bf16 operands, fp32 accumulation (v_mfma_f32_16x16x16_bf16): lane (li, lq) supplies
+// k = 16 t + 4 lq + j, j = 0..3, rounded to bf16 (RNE, v_cvt_pk_bf16_f32) as they are read.
+// The next step's operands are read while the current step's MFMAs issue.
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+template <int K, int NA, int NB, class FA, class FB>
+__device__ __forceinline__ void mma_grid_bf(f32x4 (&acc)[NA][NB], FA fa, FB fb, int lq) {
+    constexpr int NS = K / 16;
+    static_assert(K % 16 == 0, "bf16 steps cover 16 k");
+    s16x4 a[2][NA], b[2][NB];
+    auto load = [&](int t, s16x4 (&aa)[NA], s16x4 (&bb)[NB]) {
+#pragma unroll
+        for (int i = 0; i < NA; ++i) {
+            const bf16x4 v = {(__bf16)fa(i, 16 * t, 4 * lq), (__bf16)fa(i, 16 * t + 1, 4 * lq),
+                              (__bf16)fa(i, 16 * t + 2, 4 * lq), (__bf16)fa(i, 16 * t + 3, 4 * lq)};
+            aa[i] = __builtin_bit_cast(s16x4, v);
+        }
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+            const bf16x4 v = {(__bf16)fb(i, 16 * t, 4 * lq), (__bf16)fb(i, 16 * t + 1, 4 * lq),
+                              (__bf16)fb(i, 16 * t + 2, 4 * lq), (__bf16)fb(i, 16 * t + 3, 4 * lq)};
+            bb[i] = __builtin_bit_cast(s16x4, v);
+        }
+    };
+    load(0, a[0], b[0]);
+#pragma unroll
+    for (int t = 0; t < NS; ++t) {
+        if (t + 1 < NS) load(t + 1, a[(t + 1) & 1], b[(t + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int ia = 0; ia < NA; ++ia)
+#pragma unroll
+            for (int ib = 0; ib < NB; ++ib)
+                acc[ia][ib] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[t & 1][ia], b[t & 1][ib], acc[ia][ib], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+template <bool BF, int K, int NA, int NB, class FA, class FB>
+__device__ __forceinline__ void mma(f32x4 (&acc)[NA][NB], FA fa, FB fb, int lq) {
+    if constexpr (BF) mma_grid_bf<K, NA, NB>(acc, fa, fb, lq);
+    else mma_grid<K, NA, NB>(acc, fa, fb, lq);
 }
 
 // x summed over the FOLD consecutive lanes of its group (FOLD 2, 4, 8; all lanes active)
@@ -183,7 +229,7 @@ __device__ __forceinline__ float wave_half_sum(float x) {
 }
 
 // forward layer phase: out[o][s] = relu(sum_k W[k][o] in[k][s] + b[o]) (NS = K / 4 steps)
-template <class S, int Bo, int NS, int LW>
+template <class S, bool BF, int Bo, int K, int LW>
 __device__ __forceinline__ void fwd_phase(const float* __restrict__ wt, const float* __restrict__ bias, int lout,
                                           const float* __restrict__ act, int rin, int rout, float* __restrict__ actw,
                                           int w, int li, int lq) {
@@ -194,9 +240,9 @@ __device__ __forceinline__ void fwd_phase(const float* __restrict__ wt, const fl
     for (int i = 0; i < A::NA; ++i)
 #pragma unroll
         for (int k = 0; k < A::NB; ++k) acc[i][k] = f32x4{0.f, 0.f, 0.f, 0.f};
-    mma_grid<NS, A::NA, A::NB>(
-        acc, [&](int a, int t) { return wt[(4 * t + lq) * LW + 16 * A::ob(w, a) + li]; },
-        [&](int b, int t) { return act[cidx<S>(rin + 4 * t + lq, A::cb(w, b), li)]; });
+    mma<BF, K, A::NA, A::NB>(
+        acc, [&](int a, int kc, int kr) { return wt[(kc + kr) * LW + 16 * A::ob(w, a) + li]; },
+        [&](int b, int kc, int kr) { return act[cidx<S>(rin + kc + kr, A::cb(w, b), li)]; }, lq);
 #pragma unroll
     for (int i = 0; i < A::NA; ++i)
 #pragma unroll
@@ -210,7 +256,7 @@ __device__ __forceinline__ void fwd_phase(const float* __restrict__ wt, const fl
 }
 
 // backward data phase: gin[k][s] = (hin[k][s] > 0) ? sum_o W[k][o] gout[o][s] : 0
-template <class S, int Bo, int NS, int LW>
+template <class S, bool BF, int Bo, int K, int LW>
 __device__ __forceinline__ void bwd_phase(const float* __restrict__ wt, const float* __restrict__ act, int rgout,
                                           int rhin, int rgin, float* __restrict__ actw, int w, int li, int lq) {
     using A = OutSplit<Bo, S::NC>;
@@ -220,9 +266,9 @@ __device__ __forceinline__ void bwd_phase(const float* __restrict__ wt, const fl
     for (int i = 0; i < A::NA; ++i)
 #pragma unroll
         for (int k = 0; k < A::NB; ++k) acc[i][k] = f32x4{0.f, 0.f, 0.f, 0.f};
-    mma_grid<NS, A::NA, A::NB>(
-        acc, [&](int a, int t) { return wt[(16 * A::ob(w, a) + li) * LW + 4 * t + lq]; },
-        [&](int b, int t) { return act[cidx<S>(rgout + 4 * t + lq, A::cb(w, b), li)]; });
+    mma<BF, K, A::NA, A::NB>(
+        acc, [&](int a, int kc, int kr) { return wt[(16 * A::ob(w, a) + li) * LW + kc + kr]; },
+        [&](int b, int kc, int kr) { return act[cidx<S>(rgout + kc + kr, A::cb(w, b), li)]; }, lq);
 #pragma unroll
     for (int i = 0; i < A::NA; ++i)
 #pragma unroll
@@ -235,14 +281,16 @@ __device__ __forceinline__ void bwd_phase(const float* __restrict__ wt, const fl
 }
 
 // weight-gradient phase: acc[a][b] += in[kb-block][s] x g[ob-block][s] over the unit's samples
-template <class S, int Bi, int Bo, class ACC>
+template <class S, bool BF, int Bi, int Bo, class ACC>
 __device__ __forceinline__ void dw_phase(ACC& acc, const float* __restrict__ act, int rin, int rg, int w, int li,
                                          int lq) {
     using D = DwSplit<Bi, Bo>;
     if (!D::active(w)) return;
-    mma_grid<S::U / 4, D::NA, D::NB>(
-        acc, [&](int a, int t) { return act[kidx<S>(rin + 16 * D::kb(w, a) + li, t, lq)]; },
-        [&](int b, int t) { return act[kidx<S>(rg + 16 * D::ob(w, b) + li, t, lq)]; });
+    // K = the unit's samples, k = kc + kr: 32-sample half kc >> 5 (the lane offset never carries)
+    mma<BF, S::U, D::NA, D::NB>(
+        acc,
+        [&](int a, int kc, int kr) { return act[aidx<S>(kc >> 5, rin + 16 * D::kb(w, a) + li, (kc & 31) + kr)]; },
+        [&](int b, int kc, int kr) { return act[aidx<S>(kc >> 5, rg + 16 * D::ob(w, b) + li, (kc & 31) + kr)]; }, lq);
 }
 
 template <int Bi, int Bo, class ACC>
@@ -275,7 +323,7 @@ __device__ unsigned long long g_unit_t[256 * 2 * 4 * 20];
 #define NCF_UT(ph) ((void)0)
 #endif
 
-template <class S, int FOLD>
+template <class S, int FOLD, bool BF>
 __global__ __launch_bounds__(S::NT, 1) void k_fb_unit(const float* __restrict__ emb, const float* __restrict__ mlp,
                                                        const int32_t* __restrict__ users,
                                                        const int32_t* __restrict__ items,
@@ -447,11 +495,11 @@ __global__ __launch_bounds__(S::NT, 1) void k_fb_unit(const float* __restrict__ 
         NCF_UT(2);
 
         // ---- forward
-        fwd_phase<S, S::B1, L0 / 4, S::LW1>(wl + S::SW1, wl + S::SB1, L1, act, S::RX, S::RH1, act, w, li, lq);
+        fwd_phase<S, BF, S::B1, L0, S::LW1>(wl + S::SW1, wl + S::SB1, L1, act, S::RX, S::RH1, act, w, li, lq);
         NCF_UT(3);
         __syncthreads();
         NCF_UT(4);
-        fwd_phase<S, S::B2, L1 / 4, S::LW2>(wl + S::SW2, wl + S::SB2, L2, act, S::RH1, S::RH2, act, w, li, lq);
+        fwd_phase<S, BF, S::B2, L1, S::LW2>(wl + S::SW2, wl + S::SB2, L2, act, S::RH1, S::RH2, act, w, li, lq);
         NCF_UT(5);
         __syncthreads();
         NCF_UT(6);
@@ -463,9 +511,9 @@ __global__ __launch_bounds__(S::NT, 1) void k_fb_unit(const float* __restrict__ 
                 f32x4 acc[1][A::NB];
 #pragma unroll
                 for (int k = 0; k < A::NB; ++k) acc[0][k] = f32x4{0.f, 0.f, 0.f, 0.f};
-                mma_grid<L2 / 4, 1, A::NB>(
-                    acc, [&](int, int t) { return wl[S::SW3 + (4 * t + lq) * S::LW3 + li]; },
-                    [&](int b, int t) { return act[cidx<S>(S::RH2 + 4 * t + lq, A::cb(w, b), li)]; });
+                mma<BF, L2, 1, A::NB>(
+                    acc, [&](int, int kc, int kr) { return wl[S::SW3 + (kc + kr) * S::LW3 + li]; },
+                    [&](int b, int kc, int kr) { return act[cidx<S>(S::RH2 + kc + kr, A::cb(w, b), li)]; }, lq);
 #pragma unroll
                 for (int k = 0; k < A::NB; ++k) {
                     const int cb = A::cb(w, k), s = 16 * cb + li;
@@ -559,11 +607,11 @@ __global__ __launch_bounds__(S::NT, 1) void k_fb_unit(const float* __restrict__ 
             }
         }
         // ---- backward data chain (G2 shares the phase with the GMF backward)
-        bwd_phase<S, S::B2, S::P3 / 4, S::LW3>(wl + S::SW3, act, S::RG3, S::RH2, S::RG2, act, w, li, lq);
+        bwd_phase<S, BF, S::B2, S::P3, S::LW3>(wl + S::SW3, act, S::RG3, S::RH2, S::RG2, act, w, li, lq);
         NCF_UT(13);
         __syncthreads();
         NCF_UT(14);
-        bwd_phase<S, S::B1, L2 / 4, S::LW2>(wl + S::SW2, act, S::RG2, S::RH1, S::RG1, act, w, li, lq);
+        bwd_phase<S, BF, S::B1, L2, S::LW2>(wl + S::SW2, act, S::RG2, S::RH1, S::RG1, act, w, li, lq);
         NCF_UT(15);
         __syncthreads();
         NCF_UT(16);
@@ -575,9 +623,9 @@ __global__ __launch_bounds__(S::NT, 1) void k_fb_unit(const float* __restrict__ 
             for (int i = 0; i < A::NA; ++i)
 #pragma unroll
                 for (int k = 0; k < A::NB; ++k) acc[i][k] = f32x4{0.f, 0.f, 0.f, 0.f};
-            mma_grid<L1 / 4, A::NA, A::NB>(
-                acc, [&](int a, int t) { return wl[S::SW1 + (16 * A::ob(w, a) + li) * S::LW1 + 4 * t + lq]; },
-                [&](int b, int t) { return act[cidx<S>(S::RG1 + 4 * t + lq, A::cb(w, b), li)]; });
+            mma<BF, L1, A::NA, A::NB>(
+                acc, [&](int a, int kc, int kr) { return wl[S::SW1 + (16 * A::ob(w, a) + li) * S::LW1 + kc + kr]; },
+                [&](int b, int kc, int kr) { return act[cidx<S>(S::RG1 + kc + kr, A::cb(w, b), li)]; }, lq);
 #pragma unroll
             for (int k = 0; k < A::NB; ++k) {
                 const int s = 16 * A::cb(w, k) + li;
@@ -616,9 +664,9 @@ __global__ __launch_bounds__(S::NT, 1) void k_fb_unit(const float* __restrict__ 
             load_ids(un1 + ustride, nu, nv, ny);
         }
         // ---- weight gradients (operands in LDS); bias rows (wave 3); BCE + hr/dcg (wave 2)
-        dw_phase<S, S::B0, S::B1>(dw1, act, S::RX, S::RG1, w, li, lq);
-        dw_phase<S, S::B1, S::B2>(dw2, act, S::RH1, S::RG2, w, li, lq);
-        dw_phase<S, S::B2, S::B3>(dw3, act, S::RH2, S::RG3, w, li, lq);
+        dw_phase<S, BF, S::B0, S::B1>(dw1, act, S::RX, S::RG1, w, li, lq);
+        dw_phase<S, BF, S::B1, S::B2>(dw2, act, S::RH1, S::RG2, w, li, lq);
+        dw_phase<S, BF, S::B2, S::B3>(dw3, act, S::RH2, S::RG3, w, li, lq);
         // extras beside the MFMA chains, one per role: bias rows 0-63 (role 0) and 64- (role 1),
         // hr/dcg (role 2), BCE (role 3)
         if (w < 2) {
@@ -738,14 +786,14 @@ bool umatches(const ncf_shape_t& s) {
            s.layers[3] == S::L3 && s.gmf_dim == S::G && s.row_width == S::W && s.gmf_stride == S::G;
 }
 
-template <class S>
+template <class S, bool BF>
 hipError_t launch_unit_one(const WsLayout& L, void* ws, const float* emb, const float* mlp, const int32_t* users,
                            const int32_t* items, const float* labels, int64_t n, float inv_batch, IdSpace ids,
                            int group, int topk, int* nslab, int* nbce, int* nmet, hipStream_t st, int fold) {
     static bool configured = false;  // one-time attribute set per shape (idempotent)
     if (!configured) {
-        for (const void* k : {(const void*)k_fb_unit<S, 0>, (const void*)k_fb_unit<S, 2>,
-                              (const void*)k_fb_unit<S, 4>, (const void*)k_fb_unit<S, 8>}) {
+        for (const void* k : {(const void*)k_fb_unit<S, 0, BF>, (const void*)k_fb_unit<S, 2, BF>,
+                              (const void*)k_fb_unit<S, 4, BF>, (const void*)k_fb_unit<S, 8, BF>}) {
             hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)S::LDS_BYTES);
             if (e != hipSuccess) return e;
         }
@@ -762,10 +810,10 @@ hipError_t launch_unit_one(const WsLayout& L, void* ws, const float* emb, const 
                topk, in_kernel ? at<float>(ws, L.part_hit) : nullptr, in_kernel ? at<float>(ws, L.part_dcg) : nullptr);
     };
     switch (fold) {
-        case 0: go(k_fb_unit<S, 0>); break;
-        case 2: go(k_fb_unit<S, 2>); break;
-        case 4: go(k_fb_unit<S, 4>); break;
-        case 8: go(k_fb_unit<S, 8>); break;
+        case 0: go(k_fb_unit<S, 0, BF>); break;
+        case 2: go(k_fb_unit<S, 2, BF>); break;
+        case 4: go(k_fb_unit<S, 4, BF>); break;
+        case 8: go(k_fb_unit<S, 8, BF>); break;
         default: return hipErrorInvalidValue;
     }
     *nslab = grid * S::NG;
@@ -803,14 +851,17 @@ bool unit_supported(const ncf_shape_t& s) {
 hipError_t launch_fb_unit(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, const float* mlp,
                           const int32_t* users, const int32_t* items, const float* labels, int64_t n,
                           float inv_batch, IdSpace ids, int group, int topk, int* nslab, int* nbce, int* nmet,
-                          hipStream_t st, int fold) {
+                          hipStream_t st, int fold, bool bf16) {
     if (fold != 0 && (fold < 2 || fold > 8 || (fold & (fold - 1)) != 0 || n % fold != 0)) return hipErrorInvalidValue;
     const int sched = unit_sched(n);
+    // bf16 operands: one 32-sample unit group per workgroup at every size (config B's path)
 #define NCF_ARGS L, ws, emb, mlp, users, items, labels, n, inv_batch, ids, group, topk, nslab, nbce, nmet, st, fold
-#define NCF_TRY(SH)                                                                                 \
-    if (umatches<SH<32, 1>>(s))                                                                     \
-        return sched == 2 ? launch_unit_one<SH<32, 2>>(NCF_ARGS)                                    \
-                          : sched == 64 ? launch_unit_one<SH<64, 1>>(NCF_ARGS) : launch_unit_one<SH<32, 1>>(NCF_ARGS);
+#define NCF_TRY(SH)                                                                                           \
+    if (umatches<SH<32, 1>>(s))                                                                               \
+        return bf16 ? launch_unit_one<SH<32, 1>, true>(NCF_ARGS)                                              \
+                    : sched == 2 ? launch_unit_one<SH<32, 2>, false>(NCF_ARGS)                                \
+                                 : sched == 64 ? launch_unit_one<SH<64, 1>, false>(NCF_ARGS)                  \
+                                               : launch_unit_one<SH<32, 1>, false>(NCF_ARGS);
     NCF_TRY(UShapeC)
     NCF_TRY(UShapeB)
     NCF_TRY(UShapeR)

@@ -56,7 +56,7 @@ class NcfOptim(ctypes.Structure):
 class NcfHyper(ctypes.Structure):
     _fields_ = [("optimizer", _i32), ("lr", _f32), ("beta_1", _f32), ("beta_2", _f32), ("epsilon", _f32),
                 ("l2", _f32 * NCF_MAX_LAYERS), ("group", _i32), ("k", _i32), ("inv_batch", _f32),
-                ("force_generic", _i32), ("index_ready", _i32), ("reserved", _i32 * 5)]
+                ("force_generic", _i32), ("index_ready", _i32), ("mlp_bf16", _i32), ("reserved", _i32 * 4)]
 
 
 class NcfSamplerData(ctypes.Structure):

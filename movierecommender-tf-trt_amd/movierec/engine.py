@@ -45,7 +45,7 @@ class NCFEngine(object):
 
     def __init__(self, num_users, num_items, layers_sizes, gmf_dim=0, max_batch=65536, device=None,
                  optimizer="adam", lr=0.001, beta_1=0.9, beta_2=0.999, layers_l2reg=None,
-                 force_generic=False, force_layered=False, lazy_adam=False, fb_kernel=None):
+                 force_generic=False, force_layered=False, lazy_adam=False, fb_kernel=None, precision="fp32"):
         """``lazy_adam``: deferred exact decay (``ncf_optim_t.row_step``) — a training step updates
         only the batch's rows, the others catch up on their missed zero-gradient steps when next
         touched or read; bitwise the dense Keras sweep (F5).  Needs layers_l2reg[0] == 0; the
@@ -93,8 +93,15 @@ class NCFEngine(object):
         self.set_hyper(optimizer, lr, beta_1, beta_2, layers_l2reg or [0.0] * len(self.layers))
         if fb_kernel not in (None, "tile", "unit"):
             raise ValueError("fb_kernel must be None, 'tile' or 'unit'")
+        if precision not in ("fp32", "bf16"):
+            raise ValueError("precision must be 'fp32' or 'bf16'")
         self.hyper.force_generic = (1 if force_generic else 2 if force_layered else
                                     {None: 0, "tile": 3, "unit": 4}[fb_kernel])
+        # bf16 MLP operands (fp32 accumulation, master weights and Adam): BASELINE config B
+        self.precision = precision
+        self.hyper.mlp_bf16 = 1 if precision == "bf16" else 0
+        if precision == "bf16" and self.kernel_for(max(self.max_batch, 1)) != "fused-mfma-unit":
+            raise ValueError("precision='bf16' needs a model shape the fused unit kernel holds")
 
     # ------------------------------------------------------------------ setup
     @property

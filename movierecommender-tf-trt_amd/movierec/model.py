@@ -210,6 +210,9 @@ class MovierecModel(object):
         self._gmf_dim = int(params.get("gmf_dim", 0))
         self._seed = params.get("seed", None)
         self._max_batch = int(params.get("max_batch", max(self._batch_size, self._batch_size_eval)))
+        # "bf16": the MLP tower's matrix products take bf16 operands (fp32 accumulation, master
+        # weights and Adam) — BASELINE config B's precision; default fp32 (the reference's)
+        self._precision = params.get("precision", "fp32")
 
         try:
             os.makedirs(output_dir)
@@ -235,7 +238,7 @@ class MovierecModel(object):
         eng = NCFEngine(self._num_users, self._num_items, self._layers_sizes, self._gmf_dim,
                         max_batch=self._max_batch, optimizer=self._optimizer, lr=self._lr, beta_1=self._beta_1,
                         beta_2=self._beta_2, layers_l2reg=self._layers_l2reg,
-                        lazy_adam=bool(params_lazy(self._layers_l2reg)))
+                        lazy_adam=bool(params_lazy(self._layers_l2reg)), precision=self._precision)
         eng.set_keras_weights(initial_weights(self._num_users, self._num_items, self._layers_sizes, self._gmf_dim,
                                               self._seed))
         return NCFNetwork(eng, self._layers_sizes, self._gmf_dim, self._num_negs_per_pos,

@@ -120,8 +120,21 @@ def l2_of(shape, name, layers_l2reg):
 # forward / loss / backward
 # ---------------------------------------------------------------------------
 
-def forward(shape, w, users, items):
-    """Per-sample forward; returns probabilities (B,) and a cache."""
+def bf16_round(x):
+    """Round to bfloat16 (round-to-nearest-even on the float32 value, v_cvt_pk_bf16_f32), back
+    as float64: the operand rounding of the bf16 MLP mode (include/movierec_ncf.h mlp_bf16)."""
+    b = np.ascontiguousarray(np.asarray(x, dtype=np.float32)).view(np.uint32).astype(np.uint64)
+    r = ((b + 0x7FFF + ((b >> 16) & 1)) & 0xFFFF0000).astype(np.uint32)
+    return r.view(np.float32).astype(np.float64)
+
+
+def _identity(x):
+    return x
+
+
+def forward(shape, w, users, items, mm_round=_identity):
+    """Per-sample forward; returns probabilities (B,) and a cache.  ``mm_round`` is applied to
+    both operands of every hidden-layer matrix product (bf16_round: the bf16 MLP mode)."""
     users = np.asarray(users).reshape(-1).astype(np.int64)
     items = np.asarray(items).reshape(-1).astype(np.int64)
     if shape.n > 0:
@@ -131,7 +144,7 @@ def forward(shape, w, users, items):
         dt = w["user_gmf_embedding"].dtype
         h = [np.zeros((len(users), 0), dtype=dt)]
     for l in range(1, shape.n):
-        z = h[-1] @ w["hidden_%d/kernel" % l] + w["hidden_%d/bias" % l]
+        z = mm_round(h[-1]) @ mm_round(w["hidden_%d/kernel" % l]) + w["hidden_%d/bias" % l]
         h.append(np.maximum(z, 0))
     if shape.gmf_dim > 0:
         gu = w["user_gmf_embedding"][users]
@@ -172,13 +185,14 @@ def reg_loss(shape, w, layers_l2reg):
     return tot
 
 
-def loss_and_grads(shape, w, users, items, labels, layers_l2reg, batch_norm=None):
+def loss_and_grads(shape, w, users, items, labels, layers_l2reg, batch_norm=None, mm_round=_identity):
     """Total loss (mean BCE + L2) and dense gradients for every weight.
 
     ``batch_norm`` overrides the divisor of the mean (data-parallel global
-    batch); default = this batch's size.
+    batch); default = this batch's size.  ``mm_round``: as ``forward``, also on the
+    backward's matrix products.
     """
-    p, c = forward(shape, w, users, items)
+    p, c = forward(shape, w, users, items, mm_round)
     y = np.asarray(labels, dtype=np.float64).reshape(-1)
     B = p.shape[0]
     nb = float(B if batch_norm is None else batch_norm)
@@ -203,9 +217,9 @@ def loss_and_grads(shape, w, users, items, labels, layers_l2reg, batch_norm=None
     h = c["h"]
     for l in range(shape.n - 1, 0, -1):
         dzl = dh * (h[l] > 0)
-        g["hidden_%d/kernel" % l] = h[l - 1].T @ dzl
+        g["hidden_%d/kernel" % l] = mm_round(h[l - 1]).T @ mm_round(dzl)
         g["hidden_%d/bias" % l] = dzl.sum(axis=0)
-        dh = dzl @ w["hidden_%d/kernel" % l].T
+        dh = mm_round(dzl) @ mm_round(w["hidden_%d/kernel" % l]).T
     if shape.n > 0:
         g["user_embedding"] = _segment_sum(c["users"], dh[:, :shape.du], shape.num_users)
         g["item_embedding"] = _segment_sum(c["items"], dh[:, shape.du:], shape.num_items)
