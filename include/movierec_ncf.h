@@ -19,7 +19,13 @@
  *    raises ValueError, like the reference's parameter checks model.py:77-112),
  *    NCF_EHIP (-2) = HIP error (RuntimeError).  The message is available from
  *    ncf_last_error() (thread-local).  No C++ exception crosses the ABI.
- *  - Reentrant: no global mutable state besides the thread-local error text.
+ *  - Process-wide state, all of it set once and idempotent: the kernels' dynamic-LDS
+ *    attributes (set on first launch of each kernel variant), the NCF_* tuning knobs read from
+ *    the environment on first use (NCF_SIDE_STREAM, NCF_FB_KERNEL, NCF_FOLD_USERS,
+ *    NCF_UNIT_SCHED; experiments only), and the side streams of NCF_SIDE_STREAM (one per
+ *    device, mutex-guarded).  Thread-local: the error text, the profiling events, the
+ *    layered path's rocBLAS handle.  Calls on different workspaces may run concurrently from
+ *    different threads.
  *
  * Device data layout (DESIGN.md §Data layout)
  *  - One combined embedding table `emb`: rows [0, num_users) are users, rows

@@ -13,10 +13,11 @@ print("sched", sys.argv[2], 'kernel_ms', round(d['kernel_ms'], 4), 'two units', 
 for n in d['wave0']: print('%-12s' % n, ' '.join('%7.0f' % d['wave%d' % w][n] for w in range(4)))
 PY
 done
-for args in "--config C" "--config C --batch 16384" "--config C --batch 8192"; do
+for args in "--config C" "--config C --batch 16384" "--config C --batch 8192" "--config B"; do
   for k in tile unit; do
-    NCF_FB_KERNEL=$k timeout -k 10 300 python bench.py $args --no-cpu-baseline > $OUT/b.json 2> $OUT/b.err || { tail -20 $OUT/b.err; exit 1; }
-    python - $OUT/b.json "$args $k" <<'PY'
+    tag=$(echo "$args $k" | tr ' ' '_' | tr -d '-')
+    NCF_FB_KERNEL=$k timeout -k 10 300 python bench.py $args --no-cpu-baseline > $OUT/bench_$tag.json 2> $OUT/b.err || { tail -20 $OUT/b.err; exit 1; }
+    python - $OUT/bench_$tag.json "$args $k" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 r = {v["bound"]: v for k, v in d.items() if k.startswith("roofline")}
