@@ -571,6 +571,7 @@ def main():
     fb_ms = ms_fb / nfb if nfb else float("nan")
     fb_flops = fwd_bwd_flops(cfg) * B
     contribs = grad_rows(eng, B, g) if mode != "sharded" else 2 * B
+    replay_rows = 0.0
     fb_bytes = fwd_bwd_bytes(eng.shape, B, contribs)
     train_exchange = dp.last_exchange if mode == "sharded" else None
     if mode == "sharded":
@@ -580,6 +581,15 @@ def main():
         nbytes = emb_update_bytes(eng.shape, B, touched_rows=touched, contribs=contribs)
         if sampler is None:
             nbytes += 2 * B * (4 + 8)   # the launch also counts the next batch: id reads + counter atomics
+            # ... and catches the next batch's stale rows up (the rows it touches that this step
+            # did not): their p, m, v read and written once more before the next forward pass
+            stale = []
+            for (u0, i0, _), (u1, i1, _) in zip(pool[:16], pool[1:17]):
+                r0 = torch.cat([torch.unique(u0.long()), eng.num_users + torch.unique(i0.long())])
+                r1 = torch.cat([torch.unique(u1.long()), eng.num_users + torch.unique(i1.long())])
+                stale.append(int((~torch.isin(r1, r0)).sum()))
+            replay_rows = float(np.mean(stale)) if stale else 0.0
+            nbytes += 24 * replay_rows * eng.shape.row_width
     elif mode == "user":
         # two launches per step: the own users' scatter-add + Adam over the B user contributions
         # (ncf_update_rows), then Adam over the item rows with the all-reduced dense gradient
@@ -668,7 +678,7 @@ def main():
                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "algorithmic_bytes_per_launch": nbytes, "avg_launch_ms": round(kern_ms, 5),
-                "gradient_rows_per_step": contribs,
+                "gradient_rows_per_step": contribs, "replayed_rows_per_step": replay_rows,
                 "launches_per_step": round(nl / len(range(0, args.steps, every)), 2),
                 "timed_steps": "every %d-th step of the timed region (HIP events in the dispatch packets)" % every,
                 "traffic_source": "rocprofv3 --pmc FETCH_SIZE(x2 gfx950) + WRITE_SIZE, profiles/traffic/ "

@@ -445,6 +445,8 @@ static int run_fb(const ncf_shape_t& s, const ncf::WsLayout& L, const ncf_model_
     hipError_t e = hipSuccess;
     ncf::IdSpace ids = ncf::table_ids(s);
     const int fold = index_fold(s, h);
+    const bool unit = use_fused(s, h) && use_unit(s, h, n);
+    bool check_fold = false;  // the unit kernel checks an earlier call's index fold itself
     if (sharded || (h->index_ready == 1 && !after_index)) {
         // the index was built by an earlier call — ncf_shard_plan (compact ids) or ncf_build_index
         // (the deferred-decay step needs the touched-row list too and always builds its own): it
@@ -454,8 +456,12 @@ static int run_fb(const ncf_shape_t& s, const ncf::WsLayout& L, const ncf_model_
             items = ncf::at<int32_t>(ws, L.cid_i);
             ids = ncf::compact_ids(n);
         }
-        e = ncf::launch_fold_check(L, ws, fold, st);
-        if (e != hipSuccess) return hip_check(e, "fold check");
+        if (unit) {
+            check_fold = true;
+        } else {
+            e = ncf::launch_fold_check(L, ws, fold, st);
+            if (e != hipSuccess) return hip_check(e, "fold check");
+        }
     } else {
         // the index depends only on the ids: it is built on the side stream while the
         // forward/backward runs (the fused kernel leaves registers and a little LDS free on every
@@ -476,11 +482,12 @@ static int run_fb(const ncf_shape_t& s, const ncf::WsLayout& L, const ncf_model_
         }
     }
     prof_begin(NCF_K_FWD_BWD, st);
-    if (h->mlp_bf16 && !(use_fused(s, h) && use_unit(s, h, n)))
+    if (h->mlp_bf16 && !unit)
         return fail(NCF_EINVAL, "bf16 MLP operands need a fused-kernel shape and the unit kernel");
-    if (use_fused(s, h) && use_unit(s, h, n))
+    if (unit)
         e = ncf::launch_fb_unit(s, L, ws, model->emb, model->mlp, users, items, labels, n, h->inv_batch, ids,
-                                h->group, h->k, &out->nslab, &out->nbce, &out->nmet, st, fold, h->mlp_bf16 != 0);
+                                h->group, h->k, &out->nslab, &out->nbce, &out->nmet, st, fold, h->mlp_bf16 != 0,
+                                check_fold);
     else if (use_fused(s, h))
         e = ncf::launch_fb_fused(s, L, ws, model->emb, model->mlp, users, items, labels, n, h->inv_batch, ids,
                                  h->group, h->k, &out->nslab, &out->nbce, &out->nmet, st, fold);

@@ -336,7 +336,7 @@ bool unit_supported(const ncf_shape_t& s);
 hipError_t launch_fb_unit(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, const float* mlp,
                           const int32_t* users, const int32_t* items, const float* labels, int64_t n,
                           float inv_batch, IdSpace ids, int group, int topk, int* nslab, int* nbce, int* nmet,
-                          hipStream_t st, int fold, bool bf16);
+                          hipStream_t st, int fold, bool bf16, bool check_fold = false);
 // fused MFMA forward only (shapes with s.fast_path): probs; with labels also one BCE partial per
 // workgroup in ws part_bce (*nbce of them)
 hipError_t launch_fwd_fused(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, const float* mlp,

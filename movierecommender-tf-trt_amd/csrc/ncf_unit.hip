@@ -331,8 +331,11 @@ __global__ __launch_bounds__(S::NT, 1) void k_fb_unit(const float* __restrict__ 
                                                        float inv_batch, float* __restrict__ probs,
                                                        float* __restrict__ gs, float* __restrict__ slabs,
                                                        float* __restrict__ part_bce, int group, int topk,
-                                                       float* __restrict__ part_hit, float* __restrict__ part_dcg) {
+                                                       float* __restrict__ part_hit, float* __restrict__ part_dcg,
+                                                       const int32_t* __restrict__ ifold, int32_t* __restrict__ ferr) {
     constexpr int L0 = S::L0, L1 = S::L1, L2 = S::L2, L3 = S::L3, G = S::G, D0 = S::D0, W = S::W, U = S::U;
+    // an index built by an earlier call (ncf_build_index / ncf_shard_plan) must fold as this kernel does
+    if (ifold && blockIdx.x == 0 && threadIdx.x == 0 && *ifold != FOLD) atomicOr(ferr, kErrFold);
     constexpr int XP = S::XP, GP = S::GP, GPA = GP > 0 ? GP : 1, NQ = S::NQ;
     extern __shared__ __attribute__((aligned(16))) float lds[];
     float* wl = lds;
@@ -789,7 +792,8 @@ bool umatches(const ncf_shape_t& s) {
 template <class S, bool BF>
 hipError_t launch_unit_one(const WsLayout& L, void* ws, const float* emb, const float* mlp, const int32_t* users,
                            const int32_t* items, const float* labels, int64_t n, float inv_batch, IdSpace ids,
-                           int group, int topk, int* nslab, int* nbce, int* nmet, hipStream_t st, int fold) {
+                           int group, int topk, int* nslab, int* nbce, int* nmet, hipStream_t st, int fold,
+                           bool check_fold) {
     static bool configured = false;  // one-time attribute set per shape (idempotent)
     if (!configured) {
         for (const void* k : {(const void*)k_fb_unit<S, 0, BF>, (const void*)k_fb_unit<S, 2, BF>,
@@ -807,7 +811,8 @@ hipError_t launch_unit_one(const WsLayout& L, void* ws, const float* emb, const 
     auto go = [&](auto kern) {
         launch(kern, grid, S::NT, S::LDS_BYTES, st, emb, mlp, users, items, labels, n, ids, inv_batch,
                at<float>(ws, L.probs), at<float>(ws, L.gs), at<float>(ws, L.slabs), at<float>(ws, L.part_bce), group,
-               topk, in_kernel ? at<float>(ws, L.part_hit) : nullptr, in_kernel ? at<float>(ws, L.part_dcg) : nullptr);
+               topk, in_kernel ? at<float>(ws, L.part_hit) : nullptr, in_kernel ? at<float>(ws, L.part_dcg) : nullptr,
+               check_fold ? at<const int32_t>(ws, L.ifold) : nullptr, at<int32_t>(ws, L.err));
     };
     switch (fold) {
         case 0: go(k_fb_unit<S, 0, BF>); break;
@@ -851,11 +856,12 @@ bool unit_supported(const ncf_shape_t& s) {
 hipError_t launch_fb_unit(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, const float* mlp,
                           const int32_t* users, const int32_t* items, const float* labels, int64_t n,
                           float inv_batch, IdSpace ids, int group, int topk, int* nslab, int* nbce, int* nmet,
-                          hipStream_t st, int fold, bool bf16) {
+                          hipStream_t st, int fold, bool bf16, bool check_fold) {
     if (fold != 0 && (fold < 2 || fold > 8 || (fold & (fold - 1)) != 0 || n % fold != 0)) return hipErrorInvalidValue;
     const int sched = unit_sched(n);
     // bf16 operands: one 32-sample unit group per workgroup at every size (config B's path)
-#define NCF_ARGS L, ws, emb, mlp, users, items, labels, n, inv_batch, ids, group, topk, nslab, nbce, nmet, st, fold
+#define NCF_ARGS \
+    L, ws, emb, mlp, users, items, labels, n, inv_batch, ids, group, topk, nslab, nbce, nmet, st, fold, check_fold
 #define NCF_TRY(SH)                                                                                           \
     if (umatches<SH<32, 1>>(s))                                                                               \
         return bf16 ? launch_unit_one<SH<32, 1>, true>(NCF_ARGS)                                              \
