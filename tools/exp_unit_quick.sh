@@ -13,7 +13,7 @@ print("sched", sys.argv[2], 'kernel_ms', round(d['kernel_ms'], 4), 'two units', 
 for n in d['wave0']: print('%-12s' % n, ' '.join('%7.0f' % d['wave%d' % w][n] for w in range(4)))
 PY
 done
-for args in "--config C" "--config C --batch 16384" "--config C --batch 8192" "--config B"; do
+for args in "--config C" "--config C --batch 16384" "--config C --batch 8192" "--config B --precision fp32"; do
   for k in tile unit; do
     tag=$(echo "$args $k" | tr ' ' '_' | tr -d '-')
     NCF_FB_KERNEL=$k timeout -k 10 300 python bench.py $args --no-cpu-baseline > $OUT/bench_$tag.json 2> $OUT/b.err || { tail -20 $OUT/b.err; exit 1; }
