@@ -632,7 +632,8 @@ def main():
     emb_kernel = "k_emb_adam_touched" if getattr(eng, "lazy", False) else "k_emb_update"
     traffic = pmc_traffic(emb_kernel, args.config, B, mode)
     kpath = eng.kernel_for(B) if hasattr(eng, "kernel_for") else ("fused-mfma-tile" if eng.fast_path else "generic")
-    fb_kernel = {"fused-mfma-tile": "k_fb_fused", "fused-mfma-unit": "k_fb_unit"}.get(kpath)
+    fb_kernel = {"fused-mfma-tile": "k_fb_fused", "fused-mfma-unit": "k_fb_unit",
+                 "fused-mfma-wave": "k_fb_wave"}.get(kpath)
     fb_traffic = pmc_traffic(fb_kernel, args.config, B, mode) if fb_kernel else None
     par = {"single": "dp1 (one table)",
            "user": "dp%d user-partitioned data (rank r trains users u %% %d == r and alone holds their rows + "
@@ -689,6 +690,8 @@ def main():
                                       "32x32x2)",
                    "fused-mfma-unit": "fused NeuMF forward+backward, 32-sample units split by output feature "
                                       "over a workgroup's waves (k_fb_unit, fp32 MFMA 16x16x4)",
+                   "fused-mfma-wave": "fused NeuMF forward+backward, 16-sample units, the whole chain in one "
+                                      "wave (k_fb_wave, fp32 MFMA 16x16x4)",
                    "layered-rocblas": "layer-by-layer forward+backward (rocBLAS fp32 GEMMs + glue kernels, "
                                       "ncf_layered.hip)"}.get(kpath, "generic forward+backward"),
                "achieved": round(fb_achieved, 2), "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",

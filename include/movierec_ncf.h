@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define NCF_ABI_VERSION 5
+#define NCF_ABI_VERSION 6
 #define NCF_MAX_LAYERS 8
 #define NCF_EINVAL (-1)
 #define NCF_EHIP (-2)
@@ -125,8 +125,9 @@ typedef struct ncf_hyper {
                                            2: the layer-by-layer GEMM path (default for shapes the
                                            fused kernel does not hold whose dense weights exceed
                                            12288 floats, e.g. config D);
-                                           3 / 4: (fast_path shapes) the 128-sample tile kernel /
-                                           the sample-unit kernel (the default) */
+                                           3 / 4 / 5: (fast_path shapes) the 128-sample tile
+                                           kernel / the sample-unit kernel (the default) / the
+                                           wave-chain kernel (fp32 operands; else the unit one) */
     int32_t index_ready;                /* 1: the contribution index of this call's batch was built
                                            beforehand by ncf_build_index (same ids, same ws): skip it;
                                            2: its contributions were counted and scanned by the
@@ -146,6 +147,7 @@ int ncf_abi_version(void);
 #define NCF_FB_LAYERED 1
 #define NCF_FB_TILE 2
 #define NCF_FB_UNIT 3
+#define NCF_FB_WAVE 4
 int ncf_fb_kernel(const ncf_shape_t* shape, const ncf_hyper_t* hyper, int64_t n);
 const char* ncf_last_error(void);
 

@@ -174,20 +174,26 @@ hipError_t launch_predict(const ncf_shape_t& s, const ncf_hyper_t* h, const ncf:
 // Shapes the fused kernel does not hold: the layer-by-layer GEMM path when the dense weights
 // outgrow the generic kernel's LDS staging (config D), or when asked for (force_generic == 2);
 // the per-sample generic kernel for small models (the reference's test shapes) or force_generic == 1.
-// MFMA forward/backward kernel for a fused shape: the sample-unit kernel (ncf_unit.hip) or the
-// 128-sample tile kernel (ncf_fused.hip).  NCF_FB_KERNEL=unit|tile forces one.
-// hyper->force_generic 3 / 4 pick the tile / unit kernel per call.
-bool use_unit(const ncf_shape_t& s, const ncf_hyper_t* h, int64_t n) {
+// MFMA forward/backward kernel for a fused shape: the sample-unit kernel (ncf_unit.hip), the
+// wave-chain kernel (ncf_wave.hip) or the 128-sample tile kernel (ncf_fused.hip).
+// NCF_FB_KERNEL=unit|wave|tile forces one; hyper->force_generic 3 / 4 / 5 pick tile / unit / wave
+// per call.  bf16 operands run on the unit kernel only.
+int fb_variant(const ncf_shape_t& s, const ncf_hyper_t* h, int64_t n) {
     static const int mode = [] {
         const char* e = getenv("NCF_FB_KERNEL");
         if (!e) return 0;
-        return strcmp(e, "unit") == 0 ? 1 : strcmp(e, "tile") == 0 ? 2 : 0;
+        return strcmp(e, "tile") == 0 ? NCF_FB_TILE : strcmp(e, "unit") == 0 ? NCF_FB_UNIT
+                                                    : strcmp(e, "wave") == 0 ? NCF_FB_WAVE : 0;
     }();
-    if (!ncf::unit_supported(s)) return false;
-    if (h && h->force_generic == 3) return false;
-    if (h && h->force_generic == 4) return true;
-    if (mode) return mode == 1;
-    return n <= NCF_UNIT_MAX_BATCH;
+    const bool bf16 = h && h->mlp_bf16;
+    const int fg = h ? h->force_generic : 0;
+    if (!ncf::unit_supported(s)) return NCF_FB_TILE;
+    if (fg == 3) return NCF_FB_TILE;
+    if (fg == 4) return NCF_FB_UNIT;
+    if (fg == 5) return ncf::wave_supported(s) && !bf16 ? NCF_FB_WAVE : NCF_FB_UNIT;
+    int v = mode ? mode : n <= NCF_UNIT_MAX_BATCH ? NCF_FB_UNIT : NCF_FB_TILE;
+    if (v == NCF_FB_WAVE && (bf16 || !ncf::wave_supported(s))) v = NCF_FB_UNIT;
+    return v;
 }
 
 // user-row folding of a step's index and fused kernel (ncf_internal.h fold_of); h NULL: none.
@@ -290,7 +296,7 @@ int ncf_abi_version(void) { return NCF_ABI_VERSION; }
 
 int ncf_fb_kernel(const ncf_shape_t* s, const ncf_hyper_t* h, int64_t n) {
     if (int r = check_shape(s)) return r;
-    if (use_fused(*s, h)) return use_unit(*s, h, n) ? NCF_FB_UNIT : NCF_FB_TILE;
+    if (use_fused(*s, h)) return fb_variant(*s, h, n);
     return use_layered(*s, h) ? NCF_FB_LAYERED : NCF_FB_GENERIC;
 }
 
@@ -445,8 +451,9 @@ static int run_fb(const ncf_shape_t& s, const ncf::WsLayout& L, const ncf_model_
     hipError_t e = hipSuccess;
     ncf::IdSpace ids = ncf::table_ids(s);
     const int fold = index_fold(s, h);
-    const bool unit = use_fused(s, h) && use_unit(s, h, n);
-    bool check_fold = false;  // the unit kernel checks an earlier call's index fold itself
+    const int variant = use_fused(s, h) ? fb_variant(s, h, n) : -1;
+    const bool unit = variant == NCF_FB_UNIT || variant == NCF_FB_WAVE;
+    bool check_fold = false;  // the unit / wave kernels check an earlier call's index fold themselves
     if (sharded || (h->index_ready == 1 && !after_index)) {
         // the index was built by an earlier call — ncf_shard_plan (compact ids) or ncf_build_index
         // (the deferred-decay step needs the touched-row list too and always builds its own): it
@@ -482,9 +489,12 @@ static int run_fb(const ncf_shape_t& s, const ncf::WsLayout& L, const ncf_model_
         }
     }
     prof_begin(NCF_K_FWD_BWD, st);
-    if (h->mlp_bf16 && !unit)
+    if (h->mlp_bf16 && variant != NCF_FB_UNIT)
         return fail(NCF_EINVAL, "bf16 MLP operands need a fused-kernel shape and the unit kernel");
-    if (unit)
+    if (variant == NCF_FB_WAVE)
+        e = ncf::launch_fb_wave(s, L, ws, model->emb, model->mlp, users, items, labels, n, h->inv_batch, ids,
+                                h->group, h->k, &out->nslab, &out->nbce, &out->nmet, st, fold, check_fold);
+    else if (unit)
         e = ncf::launch_fb_unit(s, L, ws, model->emb, model->mlp, users, items, labels, n, h->inv_batch, ids,
                                 h->group, h->k, &out->nslab, &out->nbce, &out->nmet, st, fold, h->mlp_bf16 != 0,
                                 check_fold);

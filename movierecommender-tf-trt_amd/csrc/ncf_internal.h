@@ -333,6 +333,12 @@ bool fused_supported(const ncf_shape_t& s);
 // sample-unit kernel (ncf_unit.hip): the fused shapes, 32-sample units split across a
 // workgroup's waves by output feature; same outputs and folding as launch_fb_fused
 bool unit_supported(const ncf_shape_t& s);
+// wave-chain kernel (ncf_wave.hip): outputs as launch_fb_unit (fp32 operands only)
+bool wave_supported(const ncf_shape_t& s);
+hipError_t launch_fb_wave(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, const float* mlp,
+                          const int32_t* users, const int32_t* items, const float* labels, int64_t n,
+                          float inv_batch, IdSpace ids, int group, int topk, int* nslab, int* nbce, int* nmet,
+                          hipStream_t st, int fold, bool check_fold);
 hipError_t launch_fb_unit(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, const float* mlp,
                           const int32_t* users, const int32_t* items, const float* labels, int64_t n,
                           float inv_batch, IdSpace ids, int group, int topk, int* nslab, int* nbce, int* nmet,

@@ -1,0 +1,825 @@
+// Wave-chain fused NeuMF forward + backward on CDNA4 fp32 MFMA (v_mfma_f32_16x16x4_f32).
+//
+// One 256-thread workgroup (4 waves, one per SIMD) per CU; every wave works ALONE on its own
+// 16-sample units, so the per-unit loop has no workgroup barrier at all.  The unit kernel
+// (ncf_unit.hip) splits each layer's output features over 4 waves and pays 7 barriers and the
+// imbalance of the narrow layers per 32 samples; here each wave runs the whole chain:
+//
+//   forward:  H1 = relu(W1^T X + b1), H2, H3 as 16x16 MFMA tiles [feature][sample] — the output
+//             registers of one layer ARE the B operand of the next (the k order of a layer's
+//             contraction is free, so k-step (tile t, register r) takes feature 16 t + 4 lq + r
+//             from lane group lq), no LDS round trip between layers
+//   output:   z = wo . [u_gmf * i_gmf | H3] + bo (in-lane partial sums + two cross-group adds),
+//             Keras-clipped BCE, dz = (p - y) / B
+//   backward: G3 = dz wo ⊙ relu'(H3); G2 = (W3 G3) ⊙ relu'(H2); G1 = (W2 G2) ⊙ relu'(H1);
+//             dX = W1 G1 -> per-sample gradient rows gs (users folded as in the unit kernel)
+//   weights:  dW_l += H_{l-1} G_l^T over the unit's 16 samples (K = 16: 4 MFMA steps per tile).
+//             The contraction runs over samples, so the wave writes X, H1, H2, G1, G2, G3
+//             transposed ([sample][feature]) into its own LDS buffers and reads them back in the
+//             operand layout; every dW tile of the model lives in this wave's accumulators
+//             (168 registers at config C — one wave per SIMD has 512).
+//
+// Dense weights sit in LDS once per workgroup in an operand-friendly layout: column c of a
+// matrix with NB 16-column blocks is stored at position (c mod 16) NB + c / 16, so one
+// ds_read_b32/b64/b128 returns the A operands of all NB output tiles of a forward k-step, or NB
+// k-steps of the backward contraction.  Per 16-sample unit a wave issues 504 MFMAs (config C)
+// and ~134 LDS reads.  The next unit's MLP input is loaded into the registers layer 1 has just
+// consumed; a unit's GMF slices are loaded as it starts (first needed after layer 3).
+//
+// Epilogue: each wave reduces its per-lane bias / output-kernel / loss sums over its 16 sample
+// lanes, the four waves' contributions are added in LDS in a fixed order ((w0 + w2) + (w1 + w3))
+// and the workgroup writes one dense-gradient slab and one BCE / hit / dcg partial — the outputs
+// of k_fb_unit, so the index, update and reduction launches do not care which kernel ran.
+// Bitwise reproducible.  Reference semantics: movierec/model.py:154-214.
+
+#include <cmath>
+
+#include "ncf_common.h"
+#include "ncf_internal.h"
+
+namespace ncf {
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// NB contiguous floats from / to LDS as one (or two, NB = 8) ds_read / ds_write
+template <int NB>
+__device__ __forceinline__ void ldsv(const float* p, float (&o)[NB]) {
+    if constexpr (NB == 8) {
+        const f32x4 x = *reinterpret_cast<const f32x4*>(p), y = *reinterpret_cast<const f32x4*>(p + 4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = x[i], o[4 + i] = y[i];
+    } else if constexpr (NB == 4) {
+        const f32x4 x = *reinterpret_cast<const f32x4*>(p);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = x[i];
+    } else if constexpr (NB == 2) {
+        const f32x2 x = *reinterpret_cast<const f32x2*>(p);
+        o[0] = x[0], o[1] = x[1];
+    } else {
+        static_assert(NB == 1, "vector width");
+        o[0] = p[0];
+    }
+}
+template <int NB>
+__device__ __forceinline__ void stsv(float* p, const float (&v)[NB]) {
+    if constexpr (NB == 4) {
+        *reinterpret_cast<f32x4*>(p) = f32x4{v[0], v[1], v[2], v[3]};
+    } else if constexpr (NB == 2) {
+        *reinterpret_cast<f32x2*>(p) = f32x2{v[0], v[1]};
+    } else {
+        static_assert(NB == 1, "vector width");
+        p[0] = v[0];
+    }
+}
+
+template <int L0_, int L1_, int L2_, int L3_, int G_>
+struct WShape {
+    static constexpr int L0 = L0_, L1 = L1_, L2 = L2_, L3 = L3_, G = G_;
+    static constexpr int D0 = L0 / 2, W = G + D0;
+    static constexpr int B0 = L0 / 16, B1 = L1 / 16, B2 = L2 / 16;
+    static_assert(L0 % 64 == 0 && L1 % 16 == 0 && L2 % 16 == 0 && L3 <= 16 && L3 % 4 == 0 && G % 4 == 0,
+                  "wave-kernel shapes");
+    static_assert((B0 == 4 || B0 == 8) && (B1 == 1 || B1 == 2 || B1 == 4) && (B2 == 1 || B2 == 2 || B2 == 4),
+                  "16-column blocks per layer");
+    static constexpr int XQ = L0 / 4;  // MLP-input floats per lane: features XQ lq + q of sample li
+    static constexpr int GQ = G / 4;   // GMF floats per lane: dims GQ lq + e
+    // flat dense-parameter offsets (include/movierec_ncf.h layout)
+    static constexpr int OW1 = 0, OB1 = L0 * L1, OW2 = OB1 + L1, OB2 = OW2 + L1 * L2, OW3 = OB2 + L2,
+                         OB3 = OW3 + L2 * L3, OWO = OB3 + L3, OBO = OWO + G + L3, P = OBO + 1;
+    // LDS: weights [in][pos] with row strides 16 NB + 4 (bank-conflict-free for the forward
+    // reads, at most 2-way for the backward ones under MI355X_MICROARCH.md's LDS model); layer 3
+    // padded to 16 output columns (zeros)
+    static constexpr int S1 = 16 * B1 + 4, S2 = 16 * B2 + 4, S3 = 20;
+    static constexpr int SW1 = 0, SW2 = SW1 + L0 * S1, SW3 = SW2 + L1 * S2, SB1 = SW3 + L2 * S3,
+                         SB2 = SB1 + L1, SB3 = SB2 + L2, SWO = SB3 + 16, SBO = SWO + G + 16,
+                         WLDS = (SBO + 1 + 3) / 4 * 4;
+    // per-wave transposed buffers [sample][pos], pos = (f mod 16) NT + f / 16, row stride ts(NT)
+    static constexpr int ts(int nt) { return nt == 8 ? 132 : 16 * nt; }
+    static constexpr int TX = 0, TH1 = TX + 16 * ts(B0), TG1 = TH1 + 16 * ts(B1), TH2 = TG1 + 16 * ts(B1),
+                         TG2 = TH2 + 16 * ts(B2), TG3 = TG2 + 16 * ts(B2), WREG = TG3 + 16 * 16;
+    static constexpr size_t LDS_BYTES = (size_t)(WLDS + 4 * WREG) * 4;
+    static_assert(LDS_BYTES <= 163840, "LDS budget");
+    // epilogue: two reduction rows of P gradient entries + BCE, hit, dcg
+    static constexpr int PR = (P + 3 + 3) / 4 * 4;
+    static_assert((size_t)2 * PR * 4 <= LDS_BYTES, "epilogue rows");
+};
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// Operand registers of one pipelined step
+template <int N>
+struct Ops {
+    float v[N];
+};
+template <int M, int N>
+struct Ops2 {
+    float v[M][N];
+};
+template <int B0, int B1, int B2>
+struct DwOps {
+    float x[B0], g1[B1], h1[B1], g2[B2], h2[B2], g3;
+};
+
+// NSTEP steps of LDS operand reads + MFMAs with the reads PD steps ahead (a ring of PD operand
+// sets): step s issues its MFMAs, then the reads of step s + PD into the set it just used.  The
+// scheduling barriers keep that order (a single wave per SIMD has no other wave to hide a read
+// behind), and lgkmcnt counts the reads each step waits for.
+template <int NSTEP, int PD, class OPS, class LD, class MM>
+__device__ __forceinline__ void pipe(LD ld, MM mm) {
+    OPS ring[PD];
+#pragma unroll
+    for (int s = 0; s < PD && s < NSTEP; ++s) ld(s, ring[s]);
+#pragma unroll
+    for (int s = 0; s < NSTEP; ++s) {
+        __builtin_amdgcn_sched_barrier(0);
+        mm(s, ring[s % PD]);
+        if (s + PD < NSTEP) ld(s + PD, ring[s % PD]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+// x summed over the FOLD consecutive sample lanes of its group (FOLD 2, 4, 8; all lanes active)
+template <int FOLD>
+__device__ __forceinline__ float fold_sum(float x) {
+    static_assert(FOLD == 2 || FOLD == 4 || FOLD == 8, "fold width");
+    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xB1, 0xF, 0xF, false));  // [1,0,3,2]
+    if constexpr (FOLD >= 4)
+        x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x4E, 0xF, 0xF, false));  // [2,3,0,1]
+    if constexpr (FOLD >= 8) x += __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(x), 0x1F | (4 << 10)));
+    return x;
+}
+
+// sum over the 16 sample lanes of a lane group
+__device__ __forceinline__ float row_sum(float x) {
+#pragma unroll
+    for (int m = 1; m <= 8; m <<= 1) x += __shfl_xor(x, m, 64);
+    return x;
+}
+
+// Phase timestamps (lane 0 of every wave, first two units; stamp 8 = prologue done, 9 = end): a
+// profiling build (-DNCF_WAVE_TIMING) only; read with ncf_debug_wave_timing (tools/wave_timing.py).
+#ifdef NCF_WAVE_TIMING
+__device__ unsigned long long g_wave_t[256 * 4 * 2 * 10];
+#define NCF_WT(it, ph)                                                                                 \
+    do {                                                                                               \
+        if (lane == 0 && blockIdx.x < 256 && (it) < 2)                                                 \
+            g_wave_t[((blockIdx.x * 4 + wv) * 2 + (it)) * 10 + (ph)] = __builtin_readcyclecounter(); \
+    } while (0)
+#else
+#define NCF_WT(it, ph) ((void)0)
+#endif
+
+template <class S, int FOLD, bool MET>
+__global__ __launch_bounds__(256, 1) void k_fb_wave(const float* __restrict__ emb, const float* __restrict__ mlp,
+                                                     const int32_t* __restrict__ users,
+                                                     const int32_t* __restrict__ items,
+                                                     const float* __restrict__ labels, int64_t n, IdSpace ids,
+                                                     float inv_batch, float* __restrict__ probs,
+                                                     float* __restrict__ gs, float* __restrict__ slabs,
+                                                     float* __restrict__ part_bce, int group, int topk,
+                                                     float* __restrict__ part_hit, float* __restrict__ part_dcg,
+                                                     const int32_t* __restrict__ ifold, int32_t* __restrict__ ferr) {
+    constexpr int L0 = S::L0, L1 = S::L1, L2 = S::L2, L3 = S::L3, G = S::G, D0 = S::D0, W = S::W;
+    constexpr int B0 = S::B0, B1 = S::B1, B2 = S::B2, XQ = S::XQ, GQ = S::GQ, GQA = GQ > 0 ? GQ : 1;
+    constexpr int T0 = S::ts(B0), T1 = S::ts(B1), T2 = S::ts(B2);
+    // an index built by an earlier call (ncf_build_index / ncf_shard_plan) must fold as this kernel does
+    if (ifold && blockIdx.x == 0 && threadIdx.x == 0 && *ifold != FOLD) atomicOr(ferr, kErrFold);
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    float* wl = lds;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    float* tb = lds + S::WLDS + wv * S::WREG;
+    const float eps = 1e-7f, hi_clip = 1.0f - eps;
+    static_assert(!MET || FOLD > 1, "in-kernel metrics for groups of FOLD samples");
+
+    // dense parameters -> LDS in the operand layout (padding zeroed first)
+    for (int e = threadIdx.x; e < S::WLDS; e += 256) wl[e] = 0.f;
+    __syncthreads();
+#pragma unroll 8
+    for (int e = threadIdx.x; e < L0 * L1; e += 256) {
+        const int i = e / L1, c = e % L1;
+        wl[S::SW1 + i * S::S1 + (c & 15) * B1 + (c >> 4)] = mlp[S::OW1 + e];
+    }
+#pragma unroll 8
+    for (int e = threadIdx.x; e < L1 * L2; e += 256) {
+        const int i = e / L2, c = e % L2;
+        wl[S::SW2 + i * S::S2 + (c & 15) * B2 + (c >> 4)] = mlp[S::OW2 + e];
+    }
+    for (int e = threadIdx.x; e < L2 * L3; e += 256) wl[S::SW3 + (e / L3) * S::S3 + e % L3] = mlp[S::OW3 + e];
+    for (int e = threadIdx.x; e < L1; e += 256) wl[S::SB1 + e] = mlp[S::OB1 + e];
+    for (int e = threadIdx.x; e < L2; e += 256) wl[S::SB2 + e] = mlp[S::OB2 + e];
+    for (int e = threadIdx.x; e < L3; e += 256) wl[S::SB3 + e] = mlp[S::OB3 + e];
+    for (int e = threadIdx.x; e < G; e += 256) wl[S::SWO + e] = mlp[S::OWO + e];
+    for (int e = threadIdx.x; e < L3; e += 256) wl[S::SWO + G + e] = mlp[S::OWO + G + e];
+    if (threadIdx.x == 0) wl[S::SBO] = mlp[S::OBO];
+    __syncthreads();
+
+    f32x4 dw1[B0][B1], dw2[B1][B2], dw3[B2];
+#pragma unroll
+    for (int a = 0; a < B0; ++a)
+#pragma unroll
+        for (int b = 0; b < B1; ++b) dw1[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int a = 0; a < B1; ++a)
+#pragma unroll
+        for (int b = 0; b < B2; ++b) dw2[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int a = 0; a < B2; ++a) dw3[a] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // bias gradients: summed from the dW phase's G operands (lane: output feature 16 t + li,
+    // samples 4 q + lq), so a layer costs one register per 16-column block
+    float ab1[B1], ab2[B2], ab3 = 0.f, ah3[4], agmf[GQA];
+#pragma unroll
+    for (int t = 0; t < B1; ++t) ab1[t] = 0.f;
+#pragma unroll
+    for (int t = 0; t < B2; ++t) ab2[t] = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ah3[r] = 0.f;
+#pragma unroll
+    for (int e = 0; e < GQA; ++e) agmf[e] = 0.f;
+    float acc_bce = 0.f, acc_dbo = 0.f, acc_hit = 0.f, acc_dcg = 0.f;
+
+    const int li = lane & 15, g = lane >> 4;  // sample lane, lane group (the MFMA k index)
+    const int64_t nunits = (n + 15) / 16;
+    const int64_t ustride = (int64_t)gridDim.x * 4;
+    int64_t un = (int64_t)blockIdx.x * 4 + wv;
+
+    // ids run two units ahead, rows one unit ahead.  A masked sample (past n or an id outside the
+    // table) reads row 0 (a valid address) and gets dz = 0: it contributes nothing.
+    // (buffer loads: a lane past n reads 0 without a branch)
+    const uint32_t nbytes = (uint32_t)(n * 4);
+    const __amdgpu_buffer_rsrc_t us_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)users, (short)0, (int)nbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t it_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)items, (short)0, (int)nbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t lb_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)labels, (short)0, (int)nbytes, 0x00020000);
+    auto load_ids = [&](int64_t u, int& cu, int& cv, float& cy) {
+        const int64_t si = u * 16 + li;
+        const uint32_t off = si < n ? (uint32_t)si * 4u : 0x80000000u;
+        cu = (int)__builtin_amdgcn_raw_buffer_load_b32(us_rsrc, off, 0, 0);
+        cv = (int)__builtin_amdgcn_raw_buffer_load_b32(it_rsrc, off, 0, 0);
+        cy = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(lb_rsrc, off, 0, 0));
+    };
+    auto rows_of = [&](int64_t u, int cu, int cv, int& urow, int& irow) {
+        const bool okr = u * 16 + li < n && (unsigned)cu < (unsigned)ids.ubound && (unsigned)cv < (unsigned)ids.ibound;
+        urow = okr ? cu : 0;
+        irow = okr ? ids.ibase + cv : 0;
+    };
+    float xr[XQ], gu[GQA], gi[GQA];
+    auto load_x = [&](int64_t u, int cu, int cv) {
+        int urow, irow;
+        rows_of(u, cu, cv, urow, irow);
+        const float4* xs = reinterpret_cast<const float4*>(emb + (size_t)(g < 2 ? urow : irow) * W + G + (g & 1) * XQ);
+#pragma unroll
+        for (int k = 0; k < XQ / 4; ++k) {
+            const float4 v = xs[k];
+            xr[4 * k] = v.x, xr[4 * k + 1] = v.y, xr[4 * k + 2] = v.z, xr[4 * k + 3] = v.w;
+        }
+    };
+    auto load_g = [&](int64_t u, int cu, int cv) {
+        if constexpr (G > 0) {
+            int urow, irow;
+            rows_of(u, cu, cv, urow, irow);
+            const float* us = emb + (size_t)urow * W + g * GQ;
+            const float* is = emb + (size_t)irow * W + g * GQ;
+            if constexpr (GQ % 4 == 0) {
+#pragma unroll
+                for (int k = 0; k < GQ / 4; ++k) {
+                    const float4 a = reinterpret_cast<const float4*>(us)[k];
+                    const float4 b = reinterpret_cast<const float4*>(is)[k];
+                    gu[4 * k] = a.x, gu[4 * k + 1] = a.y, gu[4 * k + 2] = a.z, gu[4 * k + 3] = a.w;
+                    gi[4 * k] = b.x, gi[4 * k + 1] = b.y, gi[4 * k + 2] = b.z, gi[4 * k + 3] = b.w;
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < GQ; ++e) gu[e] = us[e], gi[e] = is[e];
+            }
+        }
+    };
+    int cu, cv, nu, nv;
+    float cy, ny;
+    load_ids(un, cu, cv, cy);
+    load_x(un, cu, cv);
+    load_ids(un + ustride, nu, nv, ny);
+
+    const int fm = FOLD > 1 ? FOLD - 1 : 0;
+    // stores through buffer resources: a lane whose sample is past n (or whose user row is folded
+    // into its group head) gets an offset past the buffer and the hardware drops the store, so
+    // the unit body has no branches and the scheduler sees it as one block
+    constexpr uint32_t kDrop = 0x80000000u;
+    const __amdgpu_buffer_rsrc_t gs_rsrc =
+        __builtin_amdgcn_make_buffer_rsrc(gs, (short)0, (int)(uint32_t)(2 * n * W * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t pr_rsrc = __builtin_amdgcn_make_buffer_rsrc(probs, (short)0, (int)(uint32_t)(n * 4), 0x00020000);
+    auto st4 = [&](uint32_t off, float a, float b, float c, float d) {
+        const f32x4 v = {a, b, c, d};
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), gs_rsrc, off, 0, 0);
+    };
+    NCF_WT(0, 8);
+    int itw = -1;
+    for (; un < nunits; un += ustride) {
+        ++itw;
+        NCF_WT(itw, 0);
+        const int64_t s0 = un * 16, sg = s0 + li, un1 = un + ustride;
+        const bool inb = sg < n;
+        const bool ok = inb && (unsigned)cu < (unsigned)ids.ubound && (unsigned)cv < (unsigned)ids.ibound;
+
+        // ---- X^T for dW1 (row li: features XQ lq + q), then layer 1: k-step q takes feature
+        // XQ lq + q from lane group lq (A: W1 row XQ lq + q, all B1 output blocks in one read)
+#pragma unroll
+        for (int q = 0; q < XQ; ++q)
+            tb[S::TX + li * T0 + (XQ / 16) * g + (q & 15) * B0 + (q >> 4)] = xr[q];
+        f32x4 h1[B1];
+#pragma unroll
+        for (int t = 0; t < B1; ++t) h1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        pipe<XQ, 4, Ops<B1>>(
+            [&](int q, Ops<B1>& o) { ldsv<B1>(wl + S::SW1 + (XQ * g + q) * S::S1 + li * B1, o.v); },
+            [&](int q, const Ops<B1>& o) {
+#pragma unroll
+                for (int t = 0; t < B1; ++t) h1[t] = mfma16(o.v[t], xr[q], h1[t]);
+            });
+        // the next unit's MLP input into the registers layer 1 has consumed; this unit's GMF
+        // slices (first used by the output, after layers 2-3)
+        if (un1 < nunits) load_x(un1, nu, nv);
+        load_g(un, cu, cv);
+#pragma unroll
+        for (int t = 0; t < B1; ++t) {
+            float b[4];
+            ldsv<4>(wl + S::SB1 + 16 * t + 4 * g, b);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) h1[t][r] = fmaxf(h1[t][r] + b[r], 0.f);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float v[B1];
+#pragma unroll
+            for (int t = 0; t < B1; ++t) v[t] = h1[t][r];
+            stsv<B1>(tb + S::TH1 + li * T1 + (4 * g + r) * B1, v);
+        }
+
+        NCF_WT(itw, 1);
+        // ---- layer 2: k-step (t, r) takes H1 feature 16 t + 4 lq + r (this lane's register)
+        f32x4 h2[B2];
+#pragma unroll
+        for (int t = 0; t < B2; ++t) h2[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        pipe<4 * B1, 4, Ops<B2>>(
+            [&](int k, Ops<B2>& o) { ldsv<B2>(wl + S::SW2 + (16 * (k >> 2) + 4 * g + (k & 3)) * S::S2 + li * B2, o.v); },
+            [&](int k, const Ops<B2>& o) {
+#pragma unroll
+                for (int t2 = 0; t2 < B2; ++t2) h2[t2] = mfma16(o.v[t2], h1[k >> 2][k & 3], h2[t2]);
+            });
+#pragma unroll
+        for (int t = 0; t < B2; ++t) {
+            float b[4];
+            ldsv<4>(wl + S::SB2 + 16 * t + 4 * g, b);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) h2[t][r] = fmaxf(h2[t][r] + b[r], 0.f);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float v[B2];
+#pragma unroll
+            for (int t = 0; t < B2; ++t) v[t] = h2[t][r];
+            stsv<B2>(tb + S::TH2 + li * T2 + (4 * g + r) * B2, v);
+        }
+
+        // ---- layer 3 (one 16-row block, padded): two accumulation chains, then added
+        f32x4 h3c[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+        pipe<4 * B2, 4, Ops<1>>(
+            [&](int k, Ops<1>& o) { o.v[0] = wl[S::SW3 + (16 * (k >> 2) + 4 * g + (k & 3)) * S::S3 + li]; },
+            [&](int k, const Ops<1>& o) { h3c[k & 1] = mfma16(o.v[0], h2[k >> 2][k & 3], h3c[k & 1]); });
+        float h3[4], wo3[4];
+        {
+            float b[4];
+            ldsv<4>(wl + S::SB3 + 4 * g, b);
+            ldsv<4>(wl + S::SWO + G + 4 * g, wo3);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) h3[r] = fmaxf(h3c[0][r] + h3c[1][r] + b[r], 0.f);
+        }
+
+        NCF_WT(itw, 2);
+        // ---- output: this lane's 4 H3 features and GQ GMF dims, then the 4 lane groups
+        float wg[GQA];
+        float zp = 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) zp += wo3[r] * h3[r];
+        if constexpr (G > 0) {
+            if constexpr (GQ % 4 == 0) {
+#pragma unroll
+                for (int k = 0; k < GQ / 4; ++k) {
+                    float v[4];
+                    ldsv<4>(wl + S::SWO + GQ * g + 4 * k, v);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) wg[4 * k + i] = v[i];
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < GQ; ++e) wg[e] = wl[S::SWO + GQ * g + e];
+            }
+#pragma unroll
+            for (int e = 0; e < GQ; ++e) zp += wg[e] * (gu[e] * gi[e]);
+        }
+        zp += __shfl_xor(zp, 16, 64);
+        zp += __shfl_xor(zp, 32, 64);
+        const float z = zp + wl[S::SBO];
+        // v_exp_f32 / v_rcp_f32 (about 1 ulp each): the probability stays within ~1e-7 of the
+        // correctly rounded sigmoid, far inside the 2e-6 the tests hold it to
+        const float pr = __builtin_amdgcn_rcpf(1.0f + __expf(-z));
+        const float dz = ok && pr >= eps && pr <= hi_clip ? (pr - cy) * inv_batch : 0.0f;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ok ? pr : __int_as_float(0x7fc00000)), pr_rsrc,
+                                              g == 0 && inb ? (uint32_t)sg * 4u : kDrop, 0, 0);
+        {
+            // Keras BCE of the clipped probability: binary_crossentropy through the logit,
+            // max(l, 0) - l y + log(1 + e^-|l|) with l = log(pc / (1 - pc)), equals
+            // -y log(pc) - (1 - y) log(1 - pc) (v_log_f32, ~1 ulp); one lane group counts each
+            // sample, a masked one adds nothing
+            const float pc = fminf(fmaxf(pr, eps), hi_clip);
+            const float bce = -(cy * __logf(pc) + (1.0f - cy) * __logf(1.0f - pc));
+            acc_bce += g == 0 && ok ? bce : 0.f;
+            acc_dbo += g == 0 ? dz : 0.f;
+        }
+        // RankLayer + _get_hits_per_user (model.py:344-455) for groups of FOLD samples (the
+        // launch asks for it when group == FOLD): label = first max of y; position =
+        // #(p > p_lab) + #(earlier ties)
+        if constexpr (MET) {
+            const int e = li & fm, base = lane - e;
+            int lab = 0;
+            float best = __shfl(cy, base, 64);
+#pragma unroll
+            for (int q = 1; q < FOLD; ++q) {
+                const float yq = __shfl(cy, base + q, 64);
+                lab = yq > best ? q : lab;
+                best = fmaxf(best, yq);
+            }
+            const float pl = __shfl(pr, base + lab, 64);
+            int pos = 0;
+#pragma unroll
+            for (int q = 0; q < FOLD; ++q) {
+                const float pq = __shfl(pr, base + q, 64);
+                pos += (pq > pl) || (pq == pl && q < lab);
+            }
+            const float hit = g == 0 && e == 0 && inb && pos < topk ? 1.f : 0.f;
+            acc_hit += hit;
+            acc_dcg += hit * (0.69314718f * __builtin_amdgcn_rcpf(__logf((float)pos + 2.0f)));
+        }
+
+        NCF_WT(itw, 3);
+        // ---- G3 (registers; padded features have h3 = 0 -> 0) and its transposed copy
+        float g3[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            g3[r] = h3[r] > 0.f ? dz * wo3[r] : 0.f;
+            ah3[r] += dz * h3[r];
+        }
+        stsv<4>(tb + S::TG3 + li * 16 + 4 * g, g3);
+
+        // ---- GMF backward; user rows of a fold group summed into its head sample
+        const int su = inb ? cu : -1;
+        const bool fmatch = FOLD > 1 && inb && su == __shfl(su, lane & ~fm, 64);
+        const bool fhead = (li & fm) == 0;
+        // byte offsets of this sample's user / item gradient rows (or dropped)
+        const uint32_t urow_off = inb && (fhead || !fmatch) ? (uint32_t)(2 * sg * W) * 4u : kDrop;
+        const uint32_t irow_off = inb ? (uint32_t)((2 * sg + 1) * W) * 4u : kDrop;
+        if constexpr (G > 0) {
+            float gug[GQ], gig[GQ];
+#pragma unroll
+            for (int e = 0; e < GQ; ++e) {
+                gug[e] = dz * wg[e] * gi[e];
+                gig[e] = dz * wg[e] * gu[e];
+                agmf[e] += dz * (gu[e] * gi[e]);
+            }
+            if constexpr (FOLD > 1) {
+#pragma unroll
+                for (int e = 0; e < GQ; ++e) {
+                    const float sm = fold_sum<FOLD>(fmatch ? gug[e] : 0.f);
+                    gug[e] = fhead ? sm : gug[e];
+                }
+            }
+            // masked samples (dz = 0) write zero rows: the index may count their other, valid id
+            if constexpr (GQ % 4 == 0) {
+#pragma unroll
+                for (int k = 0; k < GQ / 4; ++k) {
+                    st4(urow_off == kDrop ? kDrop : urow_off + (GQ * g + 4 * k) * 4, gug[4 * k], gug[4 * k + 1],
+                        gug[4 * k + 2], gug[4 * k + 3]);
+                    st4(irow_off == kDrop ? kDrop : irow_off + (GQ * g + 4 * k) * 4, gig[4 * k], gig[4 * k + 1],
+                        gig[4 * k + 2], gig[4 * k + 3]);
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < GQ; ++e) {
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(gug[e]), gs_rsrc,
+                                                          urow_off == kDrop ? kDrop : urow_off + (GQ * g + e) * 4, 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(gig[e]), gs_rsrc,
+                                                          irow_off == kDrop ? kDrop : irow_off + (GQ * g + e) * 4, 0, 0);
+                }
+            }
+        }
+
+        NCF_WT(itw, 4);
+        // ---- G2 = (W3 G3) ⊙ relu'(H2): k-step r takes G3 feature 4 lq + r; one b128 read gives
+        // the 4 steps' A operands (W3 row 16 ti + li, columns 4 lq .. 4 lq + 3).  relu' of H2 and
+        // H1 from the transposed copies: their registers are free after layer 3
+        float g2[B2][4];
+        {
+            float hv[4][B2], a[B2][4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) ldsv<B2>(tb + S::TH2 + li * T2 + (4 * g + r) * B2, hv[r]);
+#pragma unroll
+            for (int ti = 0; ti < B2; ++ti) ldsv<4>(wl + S::SW3 + (16 * ti + li) * S::S3 + 4 * g, a[ti]);
+            f32x4 acc[B2];
+#pragma unroll
+            for (int ti = 0; ti < B2; ++ti) acc[ti] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int ti = 0; ti < B2; ++ti) acc[ti] = mfma16(a[ti][r], g3[r], acc[ti]);
+#pragma unroll
+            for (int ti = 0; ti < B2; ++ti)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) g2[ti][r] = hv[r][ti] > 0.f ? acc[ti][r] : 0.f;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float v[B2];
+#pragma unroll
+            for (int t = 0; t < B2; ++t) v[t] = g2[t][r];
+            stsv<B2>(tb + S::TG2 + li * T2 + (4 * g + r) * B2, v);
+        }
+
+        // ---- G1 = (W2 G2) ⊙ relu'(H1): k-step (t, r) takes G2 feature 16 t + 4 lq + r; the B1
+        // output blocks' chains interleaved
+        float g1[B1][4];
+        {
+            f32x4 acc[B1];
+#pragma unroll
+            for (int ti = 0; ti < B1; ++ti) acc[ti] = f32x4{0.f, 0.f, 0.f, 0.f};
+            pipe<4, 2, Ops2<B1, B2>>(
+                [&](int r, Ops2<B1, B2>& o) {
+#pragma unroll
+                    for (int ti = 0; ti < B1; ++ti)
+                        ldsv<B2>(wl + S::SW2 + (16 * ti + li) * S::S2 + (4 * g + r) * B2, o.v[ti]);
+                },
+                [&](int r, const Ops2<B1, B2>& o) {
+#pragma unroll
+                    for (int t = 0; t < B2; ++t)
+#pragma unroll
+                        for (int ti = 0; ti < B1; ++ti) acc[ti] = mfma16(o.v[ti][t], g2[t][r], acc[ti]);
+                });
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float hv[B1];
+                ldsv<B1>(tb + S::TH1 + li * T1 + (4 * g + r) * B1, hv);
+#pragma unroll
+                for (int ti = 0; ti < B1; ++ti) g1[ti][r] = hv[ti] > 0.f ? acc[ti][r] : 0.f;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float v[B1];
+#pragma unroll
+            for (int t = 0; t < B1; ++t) v[t] = g1[t][r];
+            stsv<B1>(tb + S::TG1 + li * T1 + (4 * g + r) * B1, v);
+        }
+
+        NCF_WT(itw, 5);
+        // ---- dX = W1 G1 -> the per-sample gradient rows: block ti holds input features
+        // 16 ti + 4 lq .. + 3 of sample li (user half folded like the GMF part); two blocks'
+        // chains interleaved, k-step (t, r) takes G1 feature 16 t + 4 lq + r
+#pragma unroll
+        for (int tp = 0; tp < B0 / 2; ++tp) {
+            f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+            pipe<4, 2, Ops2<2, B1>>(
+                [&](int r, Ops2<2, B1>& o) {
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        ldsv<B1>(wl + S::SW1 + (16 * (2 * tp + j) + li) * S::S1 + (4 * g + r) * B1, o.v[j]);
+                },
+                [&](int r, const Ops2<2, B1>& o) {
+#pragma unroll
+                    for (int t = 0; t < B1; ++t)
+#pragma unroll
+                        for (int j = 0; j < 2; ++j) acc[j] = mfma16(o.v[j][t], g1[t][r], acc[j]);
+                });
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int ti = 2 * tp + j;
+                const int f0 = 16 * ti + 4 * g;
+                const bool user = 16 * ti < D0;  // compile time: D0 is a multiple of 16
+                f32x4 d = acc[j];
+                if constexpr (FOLD > 1) {
+                    if (user) {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const float sm = fold_sum<FOLD>(fmatch ? d[r] : 0.f);
+                            d[r] = fhead ? sm : d[r];
+                        }
+                    }
+                }
+                const uint32_t base = user ? urow_off : irow_off;
+                st4(base == kDrop ? kDrop : base + (G + (user ? f0 : f0 - D0)) * 4, d[0], d[1], d[2], d[3]);
+            }
+        }
+
+        // ---- weight gradients over the unit's 16 samples: k-step q takes sample 4 q + lq
+        NCF_WT(itw, 6);
+        pipe<4, 2, DwOps<B0, B1, B2>>(
+            [&](int q, DwOps<B0, B1, B2>& o) {
+                const int srow = 4 * q + g;
+                ldsv<B0>(tb + S::TX + srow * T0 + li * B0, o.x);
+                ldsv<B1>(tb + S::TG1 + srow * T1 + li * B1, o.g1);
+                ldsv<B1>(tb + S::TH1 + srow * T1 + li * B1, o.h1);
+                ldsv<B2>(tb + S::TG2 + srow * T2 + li * B2, o.g2);
+                ldsv<B2>(tb + S::TH2 + srow * T2 + li * B2, o.h2);
+                o.g3 = tb[S::TG3 + srow * 16 + li];
+            },
+            [&](int, const DwOps<B0, B1, B2>& o) {
+#pragma unroll
+                for (int a = 0; a < B0; ++a)
+#pragma unroll
+                    for (int b = 0; b < B1; ++b) dw1[a][b] = mfma16(o.x[a], o.g1[b], dw1[a][b]);
+#pragma unroll
+                for (int a = 0; a < B1; ++a)
+#pragma unroll
+                    for (int b = 0; b < B2; ++b) dw2[a][b] = mfma16(o.h1[a], o.g2[b], dw2[a][b]);
+#pragma unroll
+                for (int a = 0; a < B2; ++a) dw3[a] = mfma16(o.h2[a], o.g3, dw3[a]);
+#pragma unroll
+                for (int b = 0; b < B1; ++b) ab1[b] += o.g1[b];
+#pragma unroll
+                for (int b = 0; b < B2; ++b) ab2[b] += o.g2[b];
+                ab3 += o.g3;
+            });
+
+        cu = nu, cv = nv, cy = ny;
+        load_ids(un1 + ustride, nu, nv, ny);
+        NCF_WT(itw, 7);
+    }
+
+    // ---- epilogue: per-lane sums over the 16 sample lanes, then the four waves in LDS
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ah3[r] = row_sum(ah3[r]);
+    // bias sums: over the 4 lane groups (samples 4 q + lq)
+    auto group_sum = [](float x) {
+        x += __shfl_xor(x, 16, 64);
+        return x + __shfl_xor(x, 32, 64);
+    };
+#pragma unroll
+    for (int t = 0; t < B1; ++t) ab1[t] = group_sum(ab1[t]);
+#pragma unroll
+    for (int t = 0; t < B2; ++t) ab2[t] = group_sum(ab2[t]);
+    ab3 = group_sum(ab3);
+#pragma unroll
+    for (int e = 0; e < GQ; ++e) agmf[e] = row_sum(agmf[e]);
+    acc_dbo = wave_sum(acc_dbo);
+    acc_bce = wave_sum(acc_bce);
+    acc_hit = wave_sum(acc_hit);
+    acc_dcg = wave_sum(acc_dcg);
+    __syncthreads();  // every wave is done with the weights and its buffers
+    float* R = lds + (wv & 1) * S::PR;
+    auto put = [&](float* dst, float v, bool add) { *dst = add ? *dst + v : v; };
+    auto contribute = [&](bool add) {
+#pragma unroll
+        for (int a = 0; a < B0; ++a)
+#pragma unroll
+            for (int b = 0; b < B1; ++b)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    put(R + S::OW1 + (16 * a + 4 * g + r) * L1 + 16 * b + li, dw1[a][b][r], add);
+#pragma unroll
+        for (int a = 0; a < B1; ++a)
+#pragma unroll
+            for (int b = 0; b < B2; ++b)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    put(R + S::OW2 + (16 * a + 4 * g + r) * L2 + 16 * b + li, dw2[a][b][r], add);
+        if (li < L3) {
+#pragma unroll
+            for (int a = 0; a < B2; ++a)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) put(R + S::OW3 + (16 * a + 4 * g + r) * L3 + li, dw3[a][r], add);
+        }
+        if (g == 0) {
+#pragma unroll
+            for (int t = 0; t < B1; ++t) put(R + S::OB1 + 16 * t + li, ab1[t], add);
+#pragma unroll
+            for (int t = 0; t < B2; ++t) put(R + S::OB2 + 16 * t + li, ab2[t], add);
+            if (li < L3) put(R + S::OB3 + li, ab3, add);
+        }
+        if (li == 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (4 * g + r < L3) put(R + S::OWO + G + 4 * g + r, ah3[r], add);
+#pragma unroll
+            for (int e = 0; e < GQ; ++e) put(R + S::OWO + GQ * g + e, agmf[e], add);
+        }
+        if (lane == 0) {
+            put(R + S::OBO, acc_dbo, add);
+            put(R + S::P, acc_bce, add);
+            put(R + S::P + 1, acc_hit, add);
+            put(R + S::P + 2, acc_dcg, add);
+        }
+    };
+    if (wv < 2) contribute(false);
+    __syncthreads();
+    if (wv >= 2) contribute(true);
+    __syncthreads();
+    float* slab = slabs + (size_t)blockIdx.x * S::P;
+    const float* R0 = lds;
+    const float* R1 = lds + S::PR;
+    for (int e = threadIdx.x; e < S::P; e += 256) slab[e] = R0[e] + R1[e];
+    NCF_WT(0, 9);
+    if (threadIdx.x == 0) {
+        part_bce[blockIdx.x] = R0[S::P] + R1[S::P];
+        if constexpr (MET) {
+            part_hit[blockIdx.x] = R0[S::P + 1] + R1[S::P + 1];
+            part_dcg[blockIdx.x] = R0[S::P + 2] + R1[S::P + 2];
+        }
+    }
+}
+
+using WShapeC = WShape<128, 64, 32, 16, 64>;  // ml-20m NeuMF (config C)
+using WShapeB = WShape<64, 32, 16, 8, 8>;     // ml-1m NeuMF (config B)
+using WShapeR = WShape<64, 32, 16, 8, 0>;     // trainer default (MLP-only)
+using WShapeC0 = WShape<128, 64, 32, 16, 0>;
+
+template <class S>
+bool wmatches(const ncf_shape_t& s) {
+    return s.num_layers == 4 && s.layers[0] == S::L0 && s.layers[1] == S::L1 && s.layers[2] == S::L2 &&
+           s.layers[3] == S::L3 && s.gmf_dim == S::G && s.row_width == S::W && s.gmf_stride == S::G;
+}
+
+template <class S>
+hipError_t launch_wave_one(const WsLayout& L, void* ws, const float* emb, const float* mlp, const int32_t* users,
+                           const int32_t* items, const float* labels, int64_t n, float inv_batch, IdSpace ids,
+                           int group, int topk, int* nslab, int* nbce, int* nmet, hipStream_t st, int fold,
+                           bool check_fold) {
+    static bool configured = false;  // one-time attribute set per shape (idempotent)
+    if (!configured) {
+        for (const void* k : {(const void*)k_fb_wave<S, 0, false>, (const void*)k_fb_wave<S, 2, false>,
+                              (const void*)k_fb_wave<S, 4, false>, (const void*)k_fb_wave<S, 8, false>,
+                              (const void*)k_fb_wave<S, 2, true>, (const void*)k_fb_wave<S, 4, true>,
+                              (const void*)k_fb_wave<S, 8, true>}) {
+            hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)S::LDS_BYTES);
+            if (e != hipSuccess) return e;
+        }
+        configured = true;
+    }
+    const int64_t nunits = (n + 15) / 16;
+    const int64_t wgs = (nunits + 3) / 4;
+    int grid = (int)(wgs < 256 ? wgs : 256);
+    if (grid < 1) grid = 1;
+    // hr/dcg in the kernel when the metric groups are the fold groups (group 2, 4, 8); other
+    // groups get the separate metrics launch
+    const bool in_kernel = fold > 1 && group == fold;
+    auto go = [&](auto kern) {
+        launch(kern, grid, 256, S::LDS_BYTES, st, emb, mlp, users, items, labels, n, ids, inv_batch,
+               at<float>(ws, L.probs), at<float>(ws, L.gs), at<float>(ws, L.slabs), at<float>(ws, L.part_bce), group,
+               topk, at<float>(ws, L.part_hit), at<float>(ws, L.part_dcg),
+               check_fold ? at<const int32_t>(ws, L.ifold) : nullptr, at<int32_t>(ws, L.err));
+    };
+    switch (fold * 2 + (in_kernel ? 1 : 0)) {
+        case 0: go(k_fb_wave<S, 0, false>); break;
+        case 4: go(k_fb_wave<S, 2, false>); break;
+        case 8: go(k_fb_wave<S, 4, false>); break;
+        case 16: go(k_fb_wave<S, 8, false>); break;
+        case 5: go(k_fb_wave<S, 2, true>); break;
+        case 9: go(k_fb_wave<S, 4, true>); break;
+        case 17: go(k_fb_wave<S, 8, true>); break;
+        default: return hipErrorInvalidValue;
+    }
+    *nslab = grid;
+    *nbce = grid;
+    *nmet = in_kernel ? grid : 0;
+    return hipGetLastError();
+}
+
+}  // namespace
+
+#ifdef NCF_WAVE_TIMING
+extern "C" int ncf_debug_wave_timing(unsigned long long* out, size_t count) {
+    size_t m = count < sizeof(g_wave_t) / 8 ? count : sizeof(g_wave_t) / 8;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_t), m * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -2;
+}
+#endif
+
+bool wave_supported(const ncf_shape_t& s) {
+    return wmatches<WShapeC>(s) || wmatches<WShapeB>(s) || wmatches<WShapeR>(s) || wmatches<WShapeC0>(s);
+}
+
+hipError_t launch_fb_wave(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, const float* mlp,
+                          const int32_t* users, const int32_t* items, const float* labels, int64_t n,
+                          float inv_batch, IdSpace ids, int group, int topk, int* nslab, int* nbce, int* nmet,
+                          hipStream_t st, int fold, bool check_fold) {
+    if (fold != 0 && (fold < 2 || fold > 8 || (fold & (fold - 1)) != 0 || n % fold != 0)) return hipErrorInvalidValue;
+#define NCF_ARGS \
+    L, ws, emb, mlp, users, items, labels, n, inv_batch, ids, group, topk, nslab, nbce, nmet, st, fold, check_fold
+    if (wmatches<WShapeC>(s)) return launch_wave_one<WShapeC>(NCF_ARGS);
+    if (wmatches<WShapeB>(s)) return launch_wave_one<WShapeB>(NCF_ARGS);
+    if (wmatches<WShapeR>(s)) return launch_wave_one<WShapeR>(NCF_ARGS);
+    if (wmatches<WShapeC0>(s)) return launch_wave_one<WShapeC0>(NCF_ARGS);
+#undef NCF_ARGS
+    return hipErrorInvalidValue;
+}
+
+}  // namespace ncf

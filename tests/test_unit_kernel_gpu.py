@@ -1,7 +1,8 @@
-"""The two MFMA forward/backward kernels of the fused shapes — the sample-unit kernel
-(ncf_unit.hip, the default) and the 128-sample tile kernel (ncf_fused.hip, hyper.force_generic 3)
-— each against the oracle (reference movierec/model.py:154-214 restated) on the
-same batches, forced per engine (``fb_kernel=``) so both run at every size here.
+"""The MFMA forward/backward kernels of the fused shapes — the sample-unit kernel (ncf_unit.hip,
+the default), the wave-chain kernel (ncf_wave.hip, hyper.force_generic 5) and the 128-sample
+tile kernel (ncf_fused.hip, hyper.force_generic 3) — each against the oracle (reference
+movierec/model.py:154-214 restated) on the same batches, forced per engine (``fb_kernel=``) so
+every one runs at every size here.
 
 Tolerances as tests/test_native_gpu.py: gradients |dg| <= 1e-5 max|g|, probabilities 2e-6,
 weights after k steps k * 2e-6 + 2e-6 max|w|, BCE sum relative 1e-5, hr/dcg of the device
@@ -50,8 +51,8 @@ def _engine(shape, w, kernel, max_batch=4096, **kw):
 
 
 @pytest.mark.parametrize("dims", FUSED_SHAPES, ids=IDS)
-@pytest.mark.parametrize("kernel", ["unit", "tile"])
-@pytest.mark.parametrize("B,group", [(32, 4), (100, 4), (1000, 5), (2050, 2)])
+@pytest.mark.parametrize("kernel", ["unit", "wave", "tile"])
+@pytest.mark.parametrize("B,group", [(32, 4), (100, 4), (1000, 5), (2050, 2), (4099, 1)])
 def test_grads_match_oracle(dims, kernel, B, group):
     shape = O.NCFShape(*dims)
     w = _weights(shape, 11)
@@ -75,10 +76,11 @@ def test_grads_match_oracle(dims, kernel, B, group):
 
 @pytest.mark.parametrize("dims", FUSED_SHAPES[:2], ids=IDS[:2])
 @pytest.mark.parametrize("lazy", [False, True], ids=["dense", "deferred"])
-def test_unit_train_steps_match_oracle(dims, lazy):
+@pytest.mark.parametrize("kernel", ["unit", "wave"])
+def test_unit_train_steps_match_oracle(dims, lazy, kernel):
     shape = O.NCFShape(*dims)
     w = _weights(shape, 21)
-    eng = _engine(shape, w, "unit", lazy_adam=lazy)
+    eng = _engine(shape, w, kernel, lazy_adam=lazy)
     ref = {k: v.copy() for k, v in w.items()}
     st = O.new_opt_state(ref)
     hyper = dict(optimizer="adam", lr=0.001, beta_1=0.9, beta_2=0.999, layers_l2reg=[0.0] * 4)
@@ -95,13 +97,15 @@ def test_unit_train_steps_match_oracle(dims, lazy):
 
 
 @pytest.mark.parametrize("B", [16384 + 100, 20000])
-def test_two_group_schedule_matches_oracle(B):
+@pytest.mark.parametrize("kernel", ["unit", "wave"])
+def test_two_group_schedule_matches_oracle(B, kernel):
     """Batches of >= 16384 run two unit groups per workgroup (two waves per SIMD); uneven rounds
-    leave the last group of some workgroups on masked samples."""
+    leave the last group of some workgroups on masked samples.  The wave kernel: several units
+    per wave, the last ones partly or wholly past n."""
     shape = O.NCFShape(*FUSED_SHAPES[0])
     w = _weights(shape, 51)
     users, items, y = _batch(shape, B, 4, 52)
-    eng = _engine(shape, w, "unit", max_batch=B)
+    eng = _engine(shape, w, kernel, max_batch=B)
     grads = eng.alloc_grads()
     probs = torch.empty(B, dtype=torch.float32, device="cuda")
     eng.forward_backward(users, items, y, group=4, k=2, inv_batch=1.0 / B, grads=grads, probs_out=probs)
@@ -115,16 +119,17 @@ def test_two_group_schedule_matches_oracle(B):
     assert grads[2][0].item() == pytest.approx(O.bce_per_sample(pref, y).sum(), rel=1e-5)
 
 
-def test_unit_masked_ids_and_metrics():
-    """Ids outside the table: NaN probability, no gradient; in-kernel hr/dcg (group | 32) equal
-    the metric of the device probabilities."""
+@pytest.mark.parametrize("kernel", ["unit", "wave"])
+def test_unit_masked_ids_and_metrics(kernel):
+    """Ids outside the table: NaN probability, no gradient; in-kernel hr/dcg (group | 32, wave
+    kernel group | 16) equal the metric of the device probabilities."""
     shape = O.NCFShape(*FUSED_SHAPES[0])
     w = _weights(shape, 31)
     users, items, y = _batch(shape, 256, 4, 32)
     bad = np.zeros(256, bool)
     bad[[5, 66, 200]] = True
     users[5], items[66], users[200] = shape.num_users + 3, -2, -1
-    eng = _engine(shape, w, "unit")
+    eng = _engine(shape, w, kernel)
     grads = eng.alloc_grads()
     probs = torch.empty(256, dtype=torch.float32, device="cuda")
     eng.forward_backward(users, items, y, group=4, k=2, inv_batch=1.0 / 256, grads=grads, probs_out=probs)
@@ -138,7 +143,7 @@ def test_unit_masked_ids_and_metrics():
         assert np.max(np.abs(got[name] - g[name])) <= 1e-5 * scale + 1e-9, name
     # metrics: a clean batch through train_step, stats vs the oracle metric of the device probs
     users, items, y = _batch(shape, 512, 4, 33)
-    eng2 = _engine(shape, w, "unit")
+    eng2 = _engine(shape, w, kernel)
     probs = torch.empty(512, dtype=torch.float32, device="cuda")
     eng2.train_step(users, items, y, group=4, k=2, probs_out=probs)
     hr, dcg = O.group_metrics(probs.cpu().numpy().astype(np.float64), y, 4, 2)
@@ -151,17 +156,18 @@ def test_unit_deterministic_and_close_to_tile():
     w = _weights(shape, 41)
     users, items, y = _batch(shape, 4096, 4, 42)
     outs = {}
-    for kernel in ("unit", "unit", "tile"):
+    for kernel in ("unit", "unit", "wave", "wave", "tile"):
         eng = _engine(shape, w, kernel)
         for _ in range(2):
             eng.train_step(users, items, y, group=4, k=2)
         torch.cuda.synchronize()
         outs.setdefault(kernel, []).append((eng.emb.clone(), eng.mlp.clone()))
-    a, b = outs["unit"]
-    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
     t = outs["tile"][0]
-    assert torch.max(torch.abs(a[0] - t[0])).item() <= 1e-6
-    assert torch.max(torch.abs(a[1] - t[1])).item() <= 1e-6
+    for kernel in ("unit", "wave"):
+        a, b = outs[kernel]
+        assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+        assert torch.max(torch.abs(a[0] - t[0])).item() <= 1e-6
+        assert torch.max(torch.abs(a[1] - t[1])).item() <= 1e-6
 
 
 def test_kernel_selection_by_batch():
@@ -171,5 +177,10 @@ def test_kernel_selection_by_batch():
     assert eng.kernel_for(65536) == "fused-mfma-unit"
     assert NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=256,
                      fb_kernel="tile").kernel_for(65536) == "fused-mfma-tile"
+    assert NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=256,
+                     fb_kernel="wave").kernel_for(65536) == "fused-mfma-wave"
+    # bf16 operands are the unit kernel's: a forced wave kernel falls back to it
+    assert NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=256,
+                     fb_kernel="wave", precision="bf16").kernel_for(65536) == "fused-mfma-unit"
     assert NCFEngine(5, 10, [6, 4], 0, max_batch=64).kernel_for(64) == "generic"
     assert gpu_available()

@@ -49,13 +49,14 @@ def _mixed_batch(shape, B, group, seed):
     return users.astype(np.int32), items.astype(np.int32), y
 
 
+@pytest.mark.parametrize("kernel", [None, "wave"], ids=["default", "wave"])
 @pytest.mark.parametrize("group", [2, 4, 8, 16, 32])
-def test_mixed_groups_grads_match_oracle(group):
+def test_mixed_groups_grads_match_oracle(group, kernel):
     shape = O.NCFShape(*CONFIG_C)
     w = _weights(shape, 60 + group)
     B = 1024
     users, items, y = _mixed_batch(shape, B, group, 61 + group)
-    eng = NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=B)
+    eng = NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=B, fb_kernel=kernel)
     eng.set_keras_weights(w)
     grads = eng.alloc_grads()
     probs = torch.empty(B, dtype=torch.float32, device="cuda")
@@ -70,11 +71,13 @@ def test_mixed_groups_grads_match_oracle(group):
     assert np.max(np.abs(probs.cpu().numpy() - pref)) <= 2e-6
 
 
+@pytest.mark.parametrize("kernel", [None, "wave"], ids=["default", "wave"])
 @pytest.mark.parametrize("lazy", [False, True], ids=["dense", "deferred"])
-def test_mixed_groups_train_steps_match_oracle(lazy):
+def test_mixed_groups_train_steps_match_oracle(lazy, kernel):
     shape = O.NCFShape(*CONFIG_C)
     w = _weights(shape, 70)
-    eng = NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=512, lazy_adam=lazy)
+    eng = NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=512, lazy_adam=lazy,
+                    fb_kernel=kernel)
     eng.set_keras_weights(w)
     ref = {k: v.copy() for k, v in w.items()}
     st = O.new_opt_state(ref)
@@ -92,13 +95,15 @@ def test_mixed_groups_train_steps_match_oracle(lazy):
         assert err <= tol, (name, err, tol)
 
 
-def test_folded_step_is_deterministic():
+@pytest.mark.parametrize("kernel", [None, "wave"], ids=["default", "wave"])
+def test_folded_step_is_deterministic(kernel):
     shape = O.NCFShape(*CONFIG_C)
     w = _weights(shape, 80)
     users, items, y = _mixed_batch(shape, 2048, 4, 81)
     outs = []
     for _ in range(2):
-        eng = NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=2048)
+        eng = NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=2048,
+                        fb_kernel=kernel)
         eng.set_keras_weights(w)
         for _ in range(2):
             eng.train_step(users, items, y, group=4, k=2)
@@ -108,13 +113,14 @@ def test_folded_step_is_deterministic():
         assert torch.equal(a, b)
 
 
-def test_index_built_with_another_group_is_flagged():
+@pytest.mark.parametrize("kernel", [None, "wave"], ids=["default", "wave"])
+def test_index_built_with_another_group_is_flagged(kernel):
     """An index built ahead (ncf_build_index) with group 4 (fold 4) used by a step with group 2
     (fold 2): the step's fold check sets NCF_WSERR_FOLD and check_errors raises."""
     shape = O.NCFShape(*CONFIG_C)
     w = _weights(shape, 90)
     users, items, y = [torch.from_numpy(x).cuda() for x in _mixed_batch(shape, 256, 4, 91)]
-    eng = NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=256)
+    eng = NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=256, fb_kernel=kernel)
     eng.set_keras_weights(w)
     U = shape.num_users
     grads = (torch.zeros(shape.num_items, eng.row_width, device="cuda"), torch.zeros(eng.mlp_params, device="cuda"),

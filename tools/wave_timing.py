@@ -1,0 +1,60 @@
+"""Phase timing of the wave-chain forward/backward kernel (profiling build).
+
+Build:  python movierecommender-tf-trt_amd/csrc/build.py -D NCF_WAVE_TIMING \
+            --out movierecommender-tf-trt_amd/movierec/_lib/var/wtiming.so
+Run:    NCF_LIB=<that .so> BATCH=65536 python tools/wave_timing.py   (GPU box)
+Prints the mean cycles of each segment of the per-unit loop over all waves (first two units),
+the prologue and the epilogue, from __builtin_readcyclecounter stamps.
+"""
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "movierecommender-tf-trt_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from movierec import _native as N  # noqa: E402
+from movierec.engine import NCFEngine  # noqa: E402
+from movierec.model import initial_weights  # noqa: E402
+
+# stamps per unit: 0 start, 1 layer 1 done, 2 layers 2-3, 3 output + metrics, 4 G3 + GMF backward,
+# 5 G2 + G1, 6 dX, 7 dW; per kernel: unit 0 slot 8 = prologue done, slot 9 = epilogue done
+SEG = [("L1", 0, 1), ("L2+L3", 1, 2), ("output", 2, 3), ("G3+gmf_bwd", 3, 4), ("G2+G1", 4, 5), ("dX", 5, 6),
+       ("dW", 6, 7)]
+
+
+def main():
+    B = int(os.environ.get("BATCH", "65536"))
+    eng = NCFEngine(138493, 27278, [128, 64, 32, 16], 64, max_batch=B, fb_kernel="wave")
+    eng.set_keras_weights(initial_weights(138493, 27278, [128, 64, 32, 16], 64, seed=0))
+    g = torch.Generator(device="cuda").manual_seed(1)
+    u = torch.randint(0, 138493, (B // 4,), generator=g, device="cuda", dtype=torch.int32).repeat_interleave(4)
+    it = torch.randint(0, 27278, (B,), generator=g, device="cuda", dtype=torch.int32)
+    y = torch.tensor([0., 0., 0., 1.], device="cuda").repeat(B // 4)
+    for _ in range(5):
+        eng.train_step(u, it, y, group=4, k=3)
+    N.profile_enable([N.K_FWD_BWD], 4)
+    eng.train_step(u, it, y, group=4, k=3)
+    torch.cuda.synchronize()
+    ms, cnt = N.profile_read(N.K_FWD_BWD)
+    fn = N.lib().ncf_debug_wave_timing
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    buf = np.zeros(256 * 4 * 2 * 10, dtype=np.uint64)
+    assert fn(buf.ctypes.data, buf.size) == 0
+    t = buf.reshape(256, 4, 2, 10).astype(np.int64)
+    res = {"kernel_ms": ms / max(cnt, 1)}
+    res["segments"] = {name: round(float(np.mean(t[:, :, :, b] - t[:, :, :, a])), 1) for name, a, b in SEG}
+    res["unit_total"] = round(float(np.mean(t[:, :, :, 7] - t[:, :, :, 0])), 1)
+    res["unit_to_unit"] = round(float(np.mean(t[:, :, 1, 0] - t[:, :, 0, 0])), 1)
+    start = t[:, :, 0, 0].min(axis=1)
+    res["prologue_to_first_unit"] = round(float(np.mean(t[:, :, 0, 0] - t[:, :, 0, 8])), 1)
+    res["wg_span"] = round(float(np.mean(t[:, 0, 0, 9] - start)), 1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
