@@ -108,9 +108,15 @@ struct SideStream {
 };
 
 #ifndef NCF_UNIT_MAX_BATCH
-// batches up to this run the sample-unit kernel: it is the faster one at every size measured
-// (config C: 8192 22.4 vs 42.3 us, 65536 72 vs 80 us; profiles/r02_unit), so by default all
+// batches up to this run the sample-unit kernel: it is faster than the tile kernel at every size
+// measured (config C: 8192 22.4 vs 42.3 us, 65536 72 vs 80 us; profiles/r02_unit), so by default all
 #define NCF_UNIT_MAX_BATCH (1LL << 40)
+#endif
+#ifndef NCF_WAVE_MIN_BATCH
+// fp32 batches from this size run the wave-chain kernel instead (config C: 16384 28.2 vs 29.3 us,
+// 65536 63.7 vs 73.4, 131072 108.7 vs 130.2; 8192 26.5 vs 23.1 — too few 16-sample units to give
+// every SIMD work; profiles/r02_wave)
+#define NCF_WAVE_MIN_BATCH 16384
 #endif
 
 int side_stream_mode() {
@@ -191,7 +197,10 @@ int fb_variant(const ncf_shape_t& s, const ncf_hyper_t* h, int64_t n) {
     if (fg == 3) return NCF_FB_TILE;
     if (fg == 4) return NCF_FB_UNIT;
     if (fg == 5) return ncf::wave_supported(s) && !bf16 ? NCF_FB_WAVE : NCF_FB_UNIT;
-    int v = mode ? mode : n <= NCF_UNIT_MAX_BATCH ? NCF_FB_UNIT : NCF_FB_TILE;
+    int v = mode                      ? mode
+            : n > NCF_UNIT_MAX_BATCH      ? NCF_FB_TILE
+            : n >= NCF_WAVE_MIN_BATCH     ? NCF_FB_WAVE
+                                          : NCF_FB_UNIT;
     if (v == NCF_FB_WAVE && (bf16 || !ncf::wave_supported(s))) v = NCF_FB_UNIT;
     return v;
 }

@@ -174,7 +174,11 @@ def test_kernel_selection_by_batch():
     shape = O.NCFShape(*FUSED_SHAPES[0])
     eng = NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=256)
     assert eng.kernel_for(8192) == "fused-mfma-unit"
-    assert eng.kernel_for(65536) == "fused-mfma-unit"
+    assert eng.kernel_for(16384) == "fused-mfma-wave"
+    assert eng.kernel_for(65536) == "fused-mfma-wave"
+    # bf16 operands: the unit kernel at every size
+    assert NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=256,
+                     precision="bf16").kernel_for(65536) == "fused-mfma-unit"
     assert NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=256,
                      fb_kernel="tile").kernel_for(65536) == "fused-mfma-tile"
     assert NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=256,
