@@ -105,8 +105,17 @@ struct WShape {
                          TG2 = TH2 + 16 * ts(B2), TG3 = TG2 + 16 * ts(B2), WREG = TG3 + 16 * 16;
     static constexpr size_t LDS_BYTES = (size_t)(WLDS + 4 * WREG) * 4;
     static_assert(LDS_BYTES <= 163840, "LDS budget");
-    // epilogue: two reduction rows of P gradient entries + BCE, hit, dcg
-    static constexpr int PR = (P + 3 + 3) / 4 * 4;
+    // the prologue moves the flat parameters as float4 groups: no group straddles two segments,
+    // and the contiguous segments land on 16-byte-aligned LDS positions
+    static_assert(OB1 % 4 == 0 && OW2 % 4 == 0 && OB2 % 4 == 0 && OW3 % 4 == 0 && OB3 % 4 == 0 && OWO % 4 == 0 &&
+                      OBO % 4 == 0 && SW3 % 4 == 0 && S3 % 4 == 0 && SB1 % 4 == 0 && SB2 % 4 == 0 && SB3 % 4 == 0 &&
+                      SWO % 4 == 0,
+                  "float4 parameter groups");
+    // epilogue: two reduction rows, each NT dW tiles in the accumulator layout ([tile][lane][4],
+    // one ds_write_b128 per tile and lane) followed by the bias / output-kernel / loss entries
+    static constexpr int NT1 = B0 * B1, NT2 = B1 * B2, NT = NT1 + NT2 + B2;
+    static constexpr int RB1 = NT * 256, RB2 = RB1 + L1, RB3 = RB2 + L2, RWO = RB3 + L3, RBO = RWO + G + L3,
+                         RX = RBO + 1, PR = (RX + 3 + 3) / 4 * 4;
     static_assert((size_t)2 * PR * 4 <= LDS_BYTES, "epilogue rows");
 };
 
@@ -164,15 +173,26 @@ __device__ __forceinline__ float row_sum(float x) {
 
 // Phase timestamps (lane 0 of every wave, first two units; stamp 8 = prologue done, 9 = end): a
 // profiling build (-DNCF_WAVE_TIMING) only; read with ncf_debug_wave_timing (tools/wave_timing.py).
+// Span stamps (g_wave_s, 16 per wave): 0/1 entry (s_memrealtime / cycles), 2 weights in LDS,
+// 3 + k start of the wave's unit k (k < 8), 11 loop done, 14 epilogue's first barrier passed,
+// 15 the four waves' sums in LDS, 12 end (cycles), 13 end (s_memrealtime).
 #ifdef NCF_WAVE_TIMING
 __device__ unsigned long long g_wave_t[256 * 4 * 2 * 10];
+__device__ unsigned long long g_wave_s[256 * 4 * 16];
 #define NCF_WT(it, ph)                                                                                 \
     do {                                                                                               \
         if (lane == 0 && blockIdx.x < 256 && (it) < 2)                                                 \
             g_wave_t[((blockIdx.x * 4 + wv) * 2 + (it)) * 10 + (ph)] = __builtin_readcyclecounter(); \
+        if (lane == 0 && blockIdx.x < 256 && (ph) == 0 && (it) < 8)                                    \
+            g_wave_s[(blockIdx.x * 4 + wv) * 16 + 3 + (it)] = __builtin_readcyclecounter();            \
+    } while (0)
+#define NCF_WS(slot, v)                                                                                \
+    do {                                                                                               \
+        if ((threadIdx.x & 63) == 0 && blockIdx.x < 256) g_wave_s[blockIdx.x * 64 + (threadIdx.x >> 6) * 16 + (slot)] = (v); \
     } while (0)
 #else
 #define NCF_WT(it, ph) ((void)0)
+#define NCF_WS(slot, v) ((void)0)
 #endif
 
 template <class S, int FOLD, bool MET>
@@ -188,6 +208,8 @@ __global__ __launch_bounds__(256, 1) void k_fb_wave(const float* __restrict__ em
     constexpr int L0 = S::L0, L1 = S::L1, L2 = S::L2, L3 = S::L3, G = S::G, D0 = S::D0, W = S::W;
     constexpr int B0 = S::B0, B1 = S::B1, B2 = S::B2, XQ = S::XQ, GQ = S::GQ, GQA = GQ > 0 ? GQ : 1;
     constexpr int T0 = S::ts(B0), T1 = S::ts(B1), T2 = S::ts(B2);
+    NCF_WS(0, __builtin_amdgcn_s_memrealtime());
+    NCF_WS(1, __builtin_readcyclecounter());
     // an index built by an earlier call (ncf_build_index / ncf_shard_plan) must fold as this kernel does
     if (ifold && blockIdx.x == 0 && threadIdx.x == 0 && *ifold != FOLD) atomicOr(ferr, kErrFold);
     extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -196,52 +218,6 @@ __global__ __launch_bounds__(256, 1) void k_fb_wave(const float* __restrict__ em
     float* tb = lds + S::WLDS + wv * S::WREG;
     const float eps = 1e-7f, hi_clip = 1.0f - eps;
     static_assert(!MET || FOLD > 1, "in-kernel metrics for groups of FOLD samples");
-
-    // dense parameters -> LDS in the operand layout (padding zeroed first)
-    for (int e = threadIdx.x; e < S::WLDS; e += 256) wl[e] = 0.f;
-    __syncthreads();
-#pragma unroll 8
-    for (int e = threadIdx.x; e < L0 * L1; e += 256) {
-        const int i = e / L1, c = e % L1;
-        wl[S::SW1 + i * S::S1 + (c & 15) * B1 + (c >> 4)] = mlp[S::OW1 + e];
-    }
-#pragma unroll 8
-    for (int e = threadIdx.x; e < L1 * L2; e += 256) {
-        const int i = e / L2, c = e % L2;
-        wl[S::SW2 + i * S::S2 + (c & 15) * B2 + (c >> 4)] = mlp[S::OW2 + e];
-    }
-    for (int e = threadIdx.x; e < L2 * L3; e += 256) wl[S::SW3 + (e / L3) * S::S3 + e % L3] = mlp[S::OW3 + e];
-    for (int e = threadIdx.x; e < L1; e += 256) wl[S::SB1 + e] = mlp[S::OB1 + e];
-    for (int e = threadIdx.x; e < L2; e += 256) wl[S::SB2 + e] = mlp[S::OB2 + e];
-    for (int e = threadIdx.x; e < L3; e += 256) wl[S::SB3 + e] = mlp[S::OB3 + e];
-    for (int e = threadIdx.x; e < G; e += 256) wl[S::SWO + e] = mlp[S::OWO + e];
-    for (int e = threadIdx.x; e < L3; e += 256) wl[S::SWO + G + e] = mlp[S::OWO + G + e];
-    if (threadIdx.x == 0) wl[S::SBO] = mlp[S::OBO];
-    __syncthreads();
-
-    f32x4 dw1[B0][B1], dw2[B1][B2], dw3[B2];
-#pragma unroll
-    for (int a = 0; a < B0; ++a)
-#pragma unroll
-        for (int b = 0; b < B1; ++b) dw1[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int a = 0; a < B1; ++a)
-#pragma unroll
-        for (int b = 0; b < B2; ++b) dw2[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int a = 0; a < B2; ++a) dw3[a] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // bias gradients: summed from the dW phase's G operands (lane: output feature 16 t + li,
-    // samples 4 q + lq), so a layer costs one register per 16-column block
-    float ab1[B1], ab2[B2], ab3 = 0.f, ah3[4], agmf[GQA];
-#pragma unroll
-    for (int t = 0; t < B1; ++t) ab1[t] = 0.f;
-#pragma unroll
-    for (int t = 0; t < B2; ++t) ab2[t] = 0.f;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) ah3[r] = 0.f;
-#pragma unroll
-    for (int e = 0; e < GQA; ++e) agmf[e] = 0.f;
-    float acc_bce = 0.f, acc_dbo = 0.f, acc_hit = 0.f, acc_dcg = 0.f;
 
     const int li = lane & 15, g = lane >> 4;  // sample lane, lane group (the MFMA k index)
     const int64_t nunits = (n + 15) / 16;
@@ -300,15 +276,87 @@ __global__ __launch_bounds__(256, 1) void k_fb_wave(const float* __restrict__ em
     };
     int cu, cv, nu, nv;
     float cy, ny;
+    constexpr uint32_t kDrop = 0x80000000u;
+
+    // Prologue.  The first unit's ids, then every dense parameter (one b128 buffer load per 4
+    // floats, all issued before any is used), are in flight while the operand layout's padding is
+    // zeroed; the first unit's MLP input follows the ids; then the parameters go to LDS.  Every
+    // segment of the flat layout starts at a multiple of 4 floats, so a float4 never straddles two.
     load_ids(un, cu, cv, cy);
+    constexpr int NV4 = S::OBO / 4, NVT = (NV4 + 255) / 256;
+    const __amdgpu_buffer_rsrc_t ml_rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)mlp, (short)0, (int)(S::P * 4), 0x00020000);
+    f32x4 pv[NVT];
+#pragma unroll
+    for (int j = 0; j < NVT; ++j) {
+        const int q = (int)threadIdx.x + 256 * j;
+        pv[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ml_rsrc, q < NV4 ? (uint32_t)q * 16u : kDrop, 0, 0));
+    }
+    const float pbo = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ml_rsrc, (uint32_t)S::OBO * 4u, 0, 0));
+    for (int e = threadIdx.x; e < S::WLDS / 4; e += 256) reinterpret_cast<f32x4*>(wl)[e] = f32x4{0.f, 0.f, 0.f, 0.f};
+    __syncthreads();
     load_x(un, cu, cv);
     load_ids(un + ustride, nu, nv, ny);
+    // float4 group at flat offset e0 -> its LDS operand-layout positions
+    auto put4 = [&](int e0, const f32x4& v) {
+        if (e0 < S::OB1) {
+            const int i = e0 / L1, c0 = e0 % L1, base = S::SW1 + i * S::S1 + (c0 & 15) * B1 + (c0 >> 4);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) wl[base + k * B1] = v[k];
+        } else if (e0 < S::OW2) {
+            *reinterpret_cast<f32x4*>(wl + S::SB1 + (e0 - S::OB1)) = v;
+        } else if (e0 < S::OB2) {
+            const int e = e0 - S::OW2, i = e / L2, c0 = e % L2, base = S::SW2 + i * S::S2 + (c0 & 15) * B2 + (c0 >> 4);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) wl[base + k * B2] = v[k];
+        } else if (e0 < S::OW3) {
+            *reinterpret_cast<f32x4*>(wl + S::SB2 + (e0 - S::OB2)) = v;
+        } else if (e0 < S::OB3) {
+            const int e = e0 - S::OW3;
+            *reinterpret_cast<f32x4*>(wl + S::SW3 + (e / L3) * S::S3 + e % L3) = v;
+        } else if (e0 < S::OWO) {
+            *reinterpret_cast<f32x4*>(wl + S::SB3 + (e0 - S::OB3)) = v;
+        } else {
+            *reinterpret_cast<f32x4*>(wl + S::SWO + (e0 - S::OWO)) = v;  // [gmf | layer 3] output kernel
+        }
+    };
+#pragma unroll
+    for (int j = 0; j < NVT; ++j) {
+        const int q = (int)threadIdx.x + 256 * j;
+        if (q < NV4) put4(4 * q, pv[j]);
+    }
+    if (threadIdx.x == 0) wl[S::SBO] = pbo;
+    __syncthreads();
+    NCF_WS(2, __builtin_readcyclecounter());
+
+    f32x4 dw1[B0][B1], dw2[B1][B2], dw3[B2];
+#pragma unroll
+    for (int a = 0; a < B0; ++a)
+#pragma unroll
+        for (int b = 0; b < B1; ++b) dw1[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int a = 0; a < B1; ++a)
+#pragma unroll
+        for (int b = 0; b < B2; ++b) dw2[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int a = 0; a < B2; ++a) dw3[a] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // bias gradients: summed from the dW phase's G operands (lane: output feature 16 t + li,
+    // samples 4 q + lq), so a layer costs one register per 16-column block
+    float ab1[B1], ab2[B2], ab3 = 0.f, ah3[4], agmf[GQA];
+#pragma unroll
+    for (int t = 0; t < B1; ++t) ab1[t] = 0.f;
+#pragma unroll
+    for (int t = 0; t < B2; ++t) ab2[t] = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ah3[r] = 0.f;
+#pragma unroll
+    for (int e = 0; e < GQA; ++e) agmf[e] = 0.f;
+    float acc_bce = 0.f, acc_dbo = 0.f, acc_hit = 0.f, acc_dcg = 0.f;
 
     const int fm = FOLD > 1 ? FOLD - 1 : 0;
     // stores through buffer resources: a lane whose sample is past n (or whose user row is folded
-    // into its group head) gets an offset past the buffer and the hardware drops the store, so
-    // the unit body has no branches and the scheduler sees it as one block
-    constexpr uint32_t kDrop = 0x80000000u;
+    // into its group head) gets an offset past the buffer (kDrop) and the hardware drops the
+    // store, so the unit body has no branches and the scheduler sees it as one block
     const __amdgpu_buffer_rsrc_t gs_rsrc =
         __builtin_amdgcn_make_buffer_rsrc(gs, (short)0, (int)(uint32_t)(2 * n * W * 4), 0x00020000);
     const __amdgpu_buffer_rsrc_t pr_rsrc = __builtin_amdgcn_make_buffer_rsrc(probs, (short)0, (int)(uint32_t)(n * 4), 0x00020000);
@@ -657,6 +705,7 @@ __global__ __launch_bounds__(256, 1) void k_fb_wave(const float* __restrict__ em
     }
 
     // ---- epilogue: per-lane sums over the 16 sample lanes, then the four waves in LDS
+    NCF_WS(11, __builtin_readcyclecounter());
 #pragma unroll
     for (int r = 0; r < 4; ++r) ah3[r] = row_sum(ah3[r]);
     // bias sums: over the 4 lane groups (samples 4 q + lq)
@@ -676,66 +725,94 @@ __global__ __launch_bounds__(256, 1) void k_fb_wave(const float* __restrict__ em
     acc_hit = wave_sum(acc_hit);
     acc_dcg = wave_sum(acc_dcg);
     __syncthreads();  // every wave is done with the weights and its buffers
+    NCF_WS(14, __builtin_readcyclecounter());
     float* R = lds + (wv & 1) * S::PR;
     auto put = [&](float* dst, float v, bool add) { *dst = add ? *dst + v : v; };
+    auto tput = [&](int tile, const f32x4& v, bool add) {
+        f32x4* dst = reinterpret_cast<f32x4*>(R + tile * 256 + lane * 4);
+        *dst = add ? *dst + v : v;
+    };
     auto contribute = [&](bool add) {
 #pragma unroll
         for (int a = 0; a < B0; ++a)
 #pragma unroll
-            for (int b = 0; b < B1; ++b)
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    put(R + S::OW1 + (16 * a + 4 * g + r) * L1 + 16 * b + li, dw1[a][b][r], add);
+            for (int b = 0; b < B1; ++b) tput(a * B1 + b, dw1[a][b], add);
 #pragma unroll
         for (int a = 0; a < B1; ++a)
 #pragma unroll
-            for (int b = 0; b < B2; ++b)
+            for (int b = 0; b < B2; ++b) tput(S::NT1 + a * B2 + b, dw2[a][b], add);
 #pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    put(R + S::OW2 + (16 * a + 4 * g + r) * L2 + 16 * b + li, dw2[a][b][r], add);
-        if (li < L3) {
-#pragma unroll
-            for (int a = 0; a < B2; ++a)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) put(R + S::OW3 + (16 * a + 4 * g + r) * L3 + li, dw3[a][r], add);
-        }
+        for (int a = 0; a < B2; ++a) tput(S::NT1 + S::NT2 + a, dw3[a], add);
         if (g == 0) {
 #pragma unroll
-            for (int t = 0; t < B1; ++t) put(R + S::OB1 + 16 * t + li, ab1[t], add);
+            for (int t = 0; t < B1; ++t) put(R + S::RB1 + 16 * t + li, ab1[t], add);
 #pragma unroll
-            for (int t = 0; t < B2; ++t) put(R + S::OB2 + 16 * t + li, ab2[t], add);
-            if (li < L3) put(R + S::OB3 + li, ab3, add);
+            for (int t = 0; t < B2; ++t) put(R + S::RB2 + 16 * t + li, ab2[t], add);
+            if (li < L3) put(R + S::RB3 + li, ab3, add);
         }
         if (li == 0) {
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-                if (4 * g + r < L3) put(R + S::OWO + G + 4 * g + r, ah3[r], add);
+                if (4 * g + r < L3) put(R + S::RWO + G + 4 * g + r, ah3[r], add);
 #pragma unroll
-            for (int e = 0; e < GQ; ++e) put(R + S::OWO + GQ * g + e, agmf[e], add);
+            for (int e = 0; e < GQ; ++e) put(R + S::RWO + GQ * g + e, agmf[e], add);
         }
         if (lane == 0) {
-            put(R + S::OBO, acc_dbo, add);
-            put(R + S::P, acc_bce, add);
-            put(R + S::P + 1, acc_hit, add);
-            put(R + S::P + 2, acc_dcg, add);
+            put(R + S::RBO, acc_dbo, add);
+            put(R + S::RX, acc_bce, add);
+            put(R + S::RX + 1, acc_hit, add);
+            put(R + S::RX + 2, acc_dcg, add);
         }
     };
+    // fixed order: slab = (w0 + w2) + (w1 + w3)
     if (wv < 2) contribute(false);
     __syncthreads();
     if (wv >= 2) contribute(true);
     __syncthreads();
+    NCF_WS(15, __builtin_readcyclecounter());
     float* slab = slabs + (size_t)blockIdx.x * S::P;
     const float* R0 = lds;
     const float* R1 = lds + S::PR;
-    for (int e = threadIdx.x; e < S::P; e += 256) slab[e] = R0[e] + R1[e];
-    NCF_WT(0, 9);
-    if (threadIdx.x == 0) {
-        part_bce[blockIdx.x] = R0[S::P] + R1[S::P];
-        if constexpr (MET) {
-            part_hit[blockIdx.x] = R0[S::P + 1] + R1[S::P + 1];
-            part_dcg[blockIdx.x] = R0[S::P + 2] + R1[S::P + 2];
+    // dW tiles: a wave takes one tile (64 lanes x 4 rows) per pass, b128 reads; tile element
+    // (lane gq*16 + c, register r) is row 16 a + 4 gq + r, column 16 b + c of its matrix
+    for (int q = threadIdx.x; q < S::NT * 64; q += 256) {
+        const int tile = q >> 6;  // uniform per wave
+        const f32x4 v = *reinterpret_cast<const f32x4*>(R0 + 4 * q) + *reinterpret_cast<const f32x4*>(R1 + 4 * q);
+        int base, ld;
+        bool keep = true;
+        if (tile < S::NT1) {
+            base = S::OW1 + 16 * (tile / B1) * L1 + 16 * (tile % B1) + li, ld = L1;
+        } else if (tile < S::NT1 + S::NT2) {
+            const int t2 = tile - S::NT1;
+            base = S::OW2 + 16 * (t2 / B2) * L2 + 16 * (t2 % B2) + li, ld = L2;
+        } else {
+            base = S::OW3 + 16 * (tile - S::NT1 - S::NT2) * L3 + li, ld = L3;
+            keep = li < L3;
+        }
+        if (keep) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) slab[base + (4 * g + r) * ld] = v[r];
         }
     }
+    // biases, output kernel, output bias: back to back in the rows (RB1 .. RBO), segment by
+    // segment in the flat layout
+    for (int e = threadIdx.x; e <= S::RBO - S::RB1; e += 256) {
+        const int d = e < L1 ? S::OB1 + e
+                      : e < L1 + L2 ? S::OB2 + (e - L1)
+                      : e < L1 + L2 + L3 ? S::OB3 + (e - L1 - L2)
+                                         : S::OWO + (e - L1 - L2 - L3);
+        slab[d] = R0[S::RB1 + e] + R1[S::RB1 + e];
+    }
+    NCF_WT(0, 9);
+    if (threadIdx.x == 0) {
+        part_bce[blockIdx.x] = R0[S::RX] + R1[S::RX];
+        if constexpr (MET) {
+            part_hit[blockIdx.x] = R0[S::RX + 1] + R1[S::RX + 1];
+            part_dcg[blockIdx.x] = R0[S::RX + 2] + R1[S::RX + 2];
+        }
+    }
+    NCF_WS(12, __builtin_readcyclecounter());
+    NCF_WS(13, __builtin_amdgcn_s_memrealtime());
 }
 
 using WShapeC = WShape<128, 64, 32, 16, 64>;  // ml-20m NeuMF (config C)
@@ -800,6 +877,10 @@ hipError_t launch_wave_one(const WsLayout& L, void* ws, const float* emb, const 
 extern "C" int ncf_debug_wave_timing(unsigned long long* out, size_t count) {
     size_t m = count < sizeof(g_wave_t) / 8 ? count : sizeof(g_wave_t) / 8;
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_t), m * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -2;
+}
+extern "C" int ncf_debug_wave_spans(unsigned long long* out, size_t count) {
+    size_t m = count < sizeof(g_wave_s) / 8 ? count : sizeof(g_wave_s) / 8;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_s), m * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -2;
 }
 #endif
 

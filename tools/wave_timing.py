@@ -27,8 +27,46 @@ SEG = [("L1", 0, 1), ("L2+L3", 1, 2), ("output", 2, 3), ("G3+gmf_bwd", 3, 4), ("
        ("dW", 6, 7)]
 
 
+def spans(fn_name):
+    """Per-wave span stamps (g_wave_s): entry / end on the 100 MHz realtime clock (aligned across
+    CUs), prologue / units / epilogue in shader cycles."""
+    fn = getattr(N.lib(), fn_name)
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    buf = np.zeros(256 * 4 * 16, dtype=np.uint64)
+    assert fn(buf.ctypes.data, buf.size) == 0
+    s = buf.reshape(256, 4, 16).astype(np.int64)
+    rt0, rt1 = s[:, :, 0], s[:, :, 13]
+    units = s[:, :, 3:11]
+    nu = int(np.sum(units[0, 0] > 0))
+    out = {"entry_skew_us": round(float(rt0.max() - rt0.min()) / 100.0, 2),
+           "end_skew_us": round(float(rt1.max() - rt1.min()) / 100.0, 2),
+           "first_entry_to_last_end_us": round(float(rt1.max() - rt0.min()) / 100.0, 2),
+           "wave_span_us_mean": round(float(np.mean(rt1 - rt0)) / 100.0, 2),
+           "clock_ghz": round(float(np.mean((s[:, :, 12] - s[:, :, 1]) / np.maximum(rt1 - rt0, 1))) / 10.0, 3),
+           "prologue_cyc": round(float(np.mean(s[:, :, 2] - s[:, :, 1])), 1),
+           "to_first_unit_cyc": round(float(np.mean(s[:, :, 3] - s[:, :, 2])), 1),
+           "units": nu}
+    ends = [units[:, :, k + 1] if k + 1 < nu else s[:, :, 11] for k in range(nu)]
+    out["unit_cyc"] = [round(float(np.mean(ends[k] - units[:, :, k])), 1) for k in range(nu)]
+    out["epilogue_cyc"] = round(float(np.mean(s[:, :, 12] - s[:, :, 11])), 1)
+    out["epi_wait_first_barrier_cyc"] = round(float(np.mean(s[:, :, 14] - s[:, :, 11])), 1)
+    out["epi_wg_loop_end_spread_cyc"] = round(float(np.mean(s[:, :, 11].max(axis=1) - s[:, :, 11].min(axis=1))), 1)
+    out["epi_lds_sums_cyc"] = round(float(np.mean(s[:, :, 15] - s[:, :, 14])), 1)
+    out["epi_slab_write_cyc"] = round(float(np.mean(s[:, :, 12] - s[:, :, 15])), 1)
+    return out
+
+
 def main():
-    B = int(os.environ.get("BATCH", "65536"))
+    if os.environ.get("BATCHES"):
+        res = {}
+        for B in [int(b) for b in os.environ["BATCHES"].split(",")]:
+            res[B] = run(B)
+        print(json.dumps(res, indent=1))
+        return
+    print(json.dumps(run(int(os.environ.get("BATCH", "65536"))), indent=1))
+
+
+def run(B):
     eng = NCFEngine(138493, 27278, [128, 64, 32, 16], 64, max_batch=B, fb_kernel="wave")
     eng.set_keras_weights(initial_weights(138493, 27278, [128, 64, 32, 16], 64, seed=0))
     g = torch.Generator(device="cuda").manual_seed(1)
@@ -53,7 +91,8 @@ def main():
     start = t[:, :, 0, 0].min(axis=1)
     res["prologue_to_first_unit"] = round(float(np.mean(t[:, :, 0, 0] - t[:, :, 0, 8])), 1)
     res["wg_span"] = round(float(np.mean(t[:, 0, 0, 9] - start)), 1)
-    print(json.dumps(res, indent=1))
+    res["spans"] = spans("ncf_debug_wave_spans")
+    return res
 
 
 if __name__ == "__main__":
