@@ -727,22 +727,26 @@ __global__ __launch_bounds__(256, 1) void k_fb_wave(const float* __restrict__ em
     __syncthreads();  // every wave is done with the weights and its buffers
     NCF_WS(14, __builtin_readcyclecounter());
     float* R = lds + (wv & 1) * S::PR;
-    auto put = [&](float* dst, float v, bool add) { *dst = add ? *dst + v : v; };
-    auto tput = [&](int tile, const f32x4& v, bool add) {
-        f32x4* dst = reinterpret_cast<f32x4*>(R + tile * 256 + lane * 4);
-        *dst = add ? *dst + v : v;
+    const float* R0 = lds;
+    const float* R1 = lds + S::PR;
+    auto tile_at = [&](const float* row, int tile) {
+        return reinterpret_cast<const f32x4*>(row + tile * 256 + lane * 4);
     };
-    auto contribute = [&](bool add) {
+    // every dW tile of this wave with its tile number (rows: [tile][lane][4])
+    auto for_tiles = [&](auto f) {
 #pragma unroll
         for (int a = 0; a < B0; ++a)
 #pragma unroll
-            for (int b = 0; b < B1; ++b) tput(a * B1 + b, dw1[a][b], add);
+            for (int b = 0; b < B1; ++b) f(a * B1 + b, dw1[a][b]);
 #pragma unroll
         for (int a = 0; a < B1; ++a)
 #pragma unroll
-            for (int b = 0; b < B2; ++b) tput(S::NT1 + a * B2 + b, dw2[a][b], add);
+            for (int b = 0; b < B2; ++b) f(S::NT1 + a * B2 + b, dw2[a][b]);
 #pragma unroll
-        for (int a = 0; a < B2; ++a) tput(S::NT1 + S::NT2 + a, dw3[a], add);
+        for (int a = 0; a < B2; ++a) f(S::NT1 + S::NT2 + a, dw3[a]);
+    };
+    auto put = [&](float* dst, float v, bool add) { *dst = add ? *dst + v : v; };
+    auto scalars = [&](bool add) {
         if (g == 0) {
 #pragma unroll
             for (int t = 0; t < B1; ++t) put(R + S::RB1 + 16 * t + li, ab1[t], add);
@@ -764,47 +768,59 @@ __global__ __launch_bounds__(256, 1) void k_fb_wave(const float* __restrict__ em
             put(R + S::RX + 2, acc_dcg, add);
         }
     };
-    // fixed order: slab = (w0 + w2) + (w1 + w3)
-    if (wv < 2) contribute(false);
+    // Fixed order, slab = (w0 + w2) + (w1 + w3).  Waves 2, 3 put their sums in rows 0, 1; waves
+    // 0, 1 add them to their registers (all reads issued before the adds), wave 1 writes its
+    // total back; wave 0 adds it and writes the dW tiles to the slab straight from registers while
+    // the other waves write the bias / output entries.
+    if (wv >= 2) {
+        for_tiles([&](int t, f32x4& v) { *reinterpret_cast<f32x4*>(R + t * 256 + lane * 4) = v; });
+        scalars(false);
+    }
     __syncthreads();
-    if (wv >= 2) contribute(true);
+    if (wv < 2) {
+        f32x4 o[S::NT];
+        for_tiles([&](int t, f32x4&) { o[t] = *tile_at(R, t); });
+        for_tiles([&](int t, f32x4& v) { v += o[t]; });
+        scalars(true);
+        if (wv == 1) for_tiles([&](int t, f32x4& v) { *reinterpret_cast<f32x4*>(R + t * 256 + lane * 4) = v; });
+    }
     __syncthreads();
     NCF_WS(15, __builtin_readcyclecounter());
     float* slab = slabs + (size_t)blockIdx.x * S::P;
-    const float* R0 = lds;
-    const float* R1 = lds + S::PR;
-    // dW tiles: a wave takes one tile (64 lanes x 4 rows) per pass, b128 reads; tile element
-    // (lane gq*16 + c, register r) is row 16 a + 4 gq + r, column 16 b + c of its matrix
-    for (int q = threadIdx.x; q < S::NT * 64; q += 256) {
-        const int tile = q >> 6;  // uniform per wave
-        const f32x4 v = *reinterpret_cast<const f32x4*>(R0 + 4 * q) + *reinterpret_cast<const f32x4*>(R1 + 4 * q);
-        int base, ld;
-        bool keep = true;
-        if (tile < S::NT1) {
-            base = S::OW1 + 16 * (tile / B1) * L1 + 16 * (tile % B1) + li, ld = L1;
-        } else if (tile < S::NT1 + S::NT2) {
-            const int t2 = tile - S::NT1;
-            base = S::OW2 + 16 * (t2 / B2) * L2 + 16 * (t2 % B2) + li, ld = L2;
-        } else {
-            base = S::OW3 + 16 * (tile - S::NT1 - S::NT2) * L3 + li, ld = L3;
-            keep = li < L3;
-        }
-        if (keep) {
+    if (wv == 0) {
+        f32x4 o[S::NT];
+        for_tiles([&](int t, f32x4&) { o[t] = *tile_at(R1, t); });
+        // tile element (lane gq * 16 + c, register r) is row 16 a + 4 gq + r, column 16 b + c
+        for_tiles([&](int t, f32x4& v) {
+            const f32x4 x = v + o[t];
+            int base, ld;
+            bool keep = true;
+            if (t < S::NT1) {
+                base = S::OW1 + 16 * (t / B1) * L1 + 16 * (t % B1) + li, ld = L1;
+            } else if (t < S::NT1 + S::NT2) {
+                base = S::OW2 + 16 * ((t - S::NT1) / B2) * L2 + 16 * ((t - S::NT1) % B2) + li, ld = L2;
+            } else {
+                base = S::OW3 + 16 * (t - S::NT1 - S::NT2) * L3 + li, ld = L3;
+                keep = li < L3;
+            }
+            if (keep) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) slab[base + (4 * g + r) * ld] = v[r];
+                for (int r = 0; r < 4; ++r) slab[base + (4 * g + r) * ld] = x[r];
+            }
+        });
+    } else {
+        // biases, output kernel, output bias: back to back in the rows (RB1 .. RBO), segment by
+        // segment in the flat layout
+        for (int e = threadIdx.x - 64; e <= S::RBO - S::RB1; e += 192) {
+            const int d = e < L1 ? S::OB1 + e
+                          : e < L1 + L2 ? S::OB2 + (e - L1)
+                          : e < L1 + L2 + L3 ? S::OB3 + (e - L1 - L2)
+                                             : S::OWO + (e - L1 - L2 - L3);
+            slab[d] = R0[S::RB1 + e] + R1[S::RB1 + e];
         }
-    }
-    // biases, output kernel, output bias: back to back in the rows (RB1 .. RBO), segment by
-    // segment in the flat layout
-    for (int e = threadIdx.x; e <= S::RBO - S::RB1; e += 256) {
-        const int d = e < L1 ? S::OB1 + e
-                      : e < L1 + L2 ? S::OB2 + (e - L1)
-                      : e < L1 + L2 + L3 ? S::OB3 + (e - L1 - L2)
-                                         : S::OWO + (e - L1 - L2 - L3);
-        slab[d] = R0[S::RB1 + e] + R1[S::RB1 + e];
     }
     NCF_WT(0, 9);
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 64) {
         part_bce[blockIdx.x] = R0[S::RX] + R1[S::RX];
         if constexpr (MET) {
             part_hit[blockIdx.x] = R0[S::RX + 1] + R1[S::RX + 1];
