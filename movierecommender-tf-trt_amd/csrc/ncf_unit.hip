@@ -357,20 +357,6 @@ __global__ __launch_bounds__(S::NT, 1) void k_fb_unit(const float* __restrict__ 
     const float eps = 1e-7f, hi_clip = 1.0f - eps;
     const bool metrics = part_hit != nullptr;
 
-    // dense parameters -> LDS (padding zeroed first: the L3 < 16 columns are read as zeros)
-    for (int e = threadIdx.x; e < S::WLDS; e += S::NT) wl[e] = 0.f;
-    __syncthreads();
-    for (int e = threadIdx.x; e < L0 * L1; e += S::NT) wl[S::SW1 + (e / L1) * S::LW1 + e % L1] = mlp[S::OW1 + e];
-    for (int e = threadIdx.x; e < L1 * L2; e += S::NT) wl[S::SW2 + (e / L2) * S::LW2 + e % L2] = mlp[S::OW2 + e];
-    for (int e = threadIdx.x; e < L2 * L3; e += S::NT) wl[S::SW3 + (e / L3) * S::LW3 + e % L3] = mlp[S::OW3 + e];
-    for (int e = threadIdx.x; e < L1; e += S::NT) wl[S::SB1 + e] = mlp[S::OB1 + e];
-    for (int e = threadIdx.x; e < L2; e += S::NT) wl[S::SB2 + e] = mlp[S::OB2 + e];
-    for (int e = threadIdx.x; e < L3; e += S::NT) wl[S::SB3 + e] = mlp[S::OB3 + e];
-    for (int e = threadIdx.x; e < G; e += S::NT) wl[S::SWO + e] = mlp[S::OWO + e];
-    for (int e = threadIdx.x; e < L3; e += S::NT) wl[S::SWO + G + e] = mlp[S::OWO + G + e];
-    if (threadIdx.x == 0) wl[S::SBO] = mlp[S::OBO];
-    __syncthreads();
-
     using S1 = DwSplit<S::B0, S::B1>;
     using S2 = DwSplit<S::B1, S::B2>;
     using S3 = DwSplit<S::B2, S::B3>;
@@ -452,9 +438,56 @@ __global__ __launch_bounds__(S::NT, 1) void k_fb_unit(const float* __restrict__ 
     const int64_t u0 = (int64_t)blockIdx.x * S::NG + gq, ustride = (int64_t)gridDim.x * S::NG;
     const int64_t first = (int64_t)blockIdx.x * S::NG;
     const int64_t rounds = nunits > first ? (nunits - first + ustride - 1) / ustride : 0;
+    // Prologue.  The first unit's ids, then every dense parameter (one b128 buffer load per 4
+    // floats, all issued before any is used), are in flight while the LDS parameter block is
+    // zeroed (the L3 < 16 columns are read as zeros); the first unit's rows follow the ids; then
+    // the parameters go to LDS.  Every segment of the flat layout starts at a multiple of 4 floats.
     load_ids(u0, cu, cv, cy);
+    static_assert(S::OB1 % 4 == 0 && S::OW2 % 4 == 0 && S::OB2 % 4 == 0 && S::OW3 % 4 == 0 && S::OB3 % 4 == 0 &&
+                      S::OWO % 4 == 0 && S::OBO % 4 == 0,
+                  "float4 parameter groups");
+    constexpr int NV4 = S::OBO / 4, NVT = (NV4 + S::NT - 1) / S::NT;
+    const __amdgpu_buffer_rsrc_t ml_rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)mlp, (short)0, (int)(S::P * 4), 0x00020000);
+    f32x4 pv[NVT];
+#pragma unroll
+    for (int j = 0; j < NVT; ++j) {
+        const int q = (int)threadIdx.x + S::NT * j;
+        pv[j] = __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(ml_rsrc, q < NV4 ? (uint32_t)q * 16u : 0x80000000u, 0, 0));
+    }
+    const float pbo = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ml_rsrc, (uint32_t)S::OBO * 4u, 0, 0));
+    for (int e = threadIdx.x; e < S::WLDS / 4; e += S::NT) reinterpret_cast<f32x4*>(wl)[e] = f32x4{0.f, 0.f, 0.f, 0.f};
+    __syncthreads();
     load_rows(u0);
     load_ids(u0 + ustride, nu, nv, ny);
+#pragma unroll
+    for (int j = 0; j < NVT; ++j) {
+        const int q = (int)threadIdx.x + S::NT * j;
+        if (q < NV4) {
+            const int e0 = 4 * q;
+            int d;  // LDS position of element e0 (its 3 successors follow it)
+            if (e0 < S::OB1) {
+                d = S::SW1 + (e0 / L1) * S::LW1 + e0 % L1;
+            } else if (e0 < S::OW2) {
+                d = S::SB1 + (e0 - S::OB1);
+            } else if (e0 < S::OB2) {
+                d = S::SW2 + ((e0 - S::OW2) / L2) * S::LW2 + (e0 - S::OW2) % L2;
+            } else if (e0 < S::OW3) {
+                d = S::SB2 + (e0 - S::OB2);
+            } else if (e0 < S::OB3) {
+                d = S::SW3 + ((e0 - S::OW3) / L3) * S::LW3 + (e0 - S::OW3) % L3;
+            } else if (e0 < S::OWO) {
+                d = S::SB3 + (e0 - S::OB3);
+            } else {
+                d = S::SWO + (e0 - S::OWO);  // [gmf | layer 3] output kernel
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) wl[d + k] = pv[j][k];
+        }
+    }
+    if (threadIdx.x == 0) wl[S::SBO] = pbo;
+    __syncthreads();
 
     const int fm = FOLD > 1 ? FOLD - 1 : 0;
     int itl = -1;

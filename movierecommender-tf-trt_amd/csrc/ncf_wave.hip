@@ -111,12 +111,13 @@ struct WShape {
                       OBO % 4 == 0 && SW3 % 4 == 0 && S3 % 4 == 0 && SB1 % 4 == 0 && SB2 % 4 == 0 && SB3 % 4 == 0 &&
                       SWO % 4 == 0,
                   "float4 parameter groups");
-    // epilogue: two reduction rows, each NT dW tiles in the accumulator layout ([tile][lane][4],
-    // one ds_write_b128 per tile and lane) followed by the bias / output-kernel / loss entries
-    static constexpr int NT1 = B0 * B1, NT2 = B1 * B2, NT = NT1 + NT2 + B2;
-    static constexpr int RB1 = NT * 256, RB2 = RB1 + L1, RB3 = RB2 + L2, RWO = RB3 + L3, RBO = RWO + G + L3,
+    // epilogue: one reduction row per wave, holding half of its NT dW tiles at a time in the
+    // accumulator layout ([tile][lane][4], one ds_write_b128 per tile and lane) followed by the
+    // bias / output-kernel / loss entries
+    static constexpr int NT1 = B0 * B1, NT2 = B1 * B2, NT = NT1 + NT2 + B2, NTH = (NT + 1) / 2;
+    static constexpr int RB1 = NTH * 256, RB2 = RB1 + L1, RB3 = RB2 + L2, RWO = RB3 + L3, RBO = RWO + G + L3,
                          RX = RBO + 1, PR = (RX + 3 + 3) / 4 * 4;
-    static_assert((size_t)2 * PR * 4 <= LDS_BYTES, "epilogue rows");
+    static_assert((size_t)4 * PR * 4 <= LDS_BYTES, "epilogue rows");
 };
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
@@ -164,15 +165,16 @@ __device__ __forceinline__ float fold_sum(float x) {
     return x;
 }
 
-// sum over the 16 sample lanes of a lane group
+// sum over the 16 sample lanes of a lane group (DPP row rotations: full-rate VALU; each lane
+// associates differently, the callers read lane li == 0)
 __device__ __forceinline__ float row_sum(float x) {
-#pragma unroll
-    for (int m = 1; m <= 8; m <<= 1) x += __shfl_xor(x, m, 64);
+    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x128, 0xF, 0xF, false));  // row_ror:8
+    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x124, 0xF, 0xF, false));  // row_ror:4
+    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x122, 0xF, 0xF, false));  // row_ror:2
+    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x121, 0xF, 0xF, false));  // row_ror:1
     return x;
 }
 
-// Phase timestamps (lane 0 of every wave, first two units; stamp 8 = prologue done, 9 = end): a
-// profiling build (-DNCF_WAVE_TIMING) only; read with ncf_debug_wave_timing (tools/wave_timing.py).
 // Span stamps (g_wave_s, 16 per wave): 0/1 entry (s_memrealtime / cycles), 2 weights in LDS,
 // 3 + k start of the wave's unit k (k < 8), 11 loop done, 14 epilogue's first barrier passed,
 // 15 the four waves' sums in LDS, 12 end (cycles), 13 end (s_memrealtime).
@@ -726,13 +728,8 @@ __global__ __launch_bounds__(256, 1) void k_fb_wave(const float* __restrict__ em
     acc_dcg = wave_sum(acc_dcg);
     __syncthreads();  // every wave is done with the weights and its buffers
     NCF_WS(14, __builtin_readcyclecounter());
-    float* R = lds + (wv & 1) * S::PR;
-    const float* R0 = lds;
-    const float* R1 = lds + S::PR;
-    auto tile_at = [&](const float* row, int tile) {
-        return reinterpret_cast<const f32x4*>(row + tile * 256 + lane * 4);
-    };
-    // every dW tile of this wave with its tile number (rows: [tile][lane][4])
+    float* R = lds + wv * S::PR;
+    // every dW tile of this wave with its tile number
     auto for_tiles = [&](auto f) {
 #pragma unroll
         for (int a = 0; a < B0; ++a)
@@ -745,54 +742,44 @@ __global__ __launch_bounds__(256, 1) void k_fb_wave(const float* __restrict__ em
 #pragma unroll
         for (int a = 0; a < B2; ++a) f(S::NT1 + S::NT2 + a, dw3[a]);
     };
-    auto put = [&](float* dst, float v, bool add) { *dst = add ? *dst + v : v; };
-    auto scalars = [&](bool add) {
-        if (g == 0) {
+    if (g == 0) {
 #pragma unroll
-            for (int t = 0; t < B1; ++t) put(R + S::RB1 + 16 * t + li, ab1[t], add);
+        for (int t = 0; t < B1; ++t) R[S::RB1 + 16 * t + li] = ab1[t];
 #pragma unroll
-            for (int t = 0; t < B2; ++t) put(R + S::RB2 + 16 * t + li, ab2[t], add);
-            if (li < L3) put(R + S::RB3 + li, ab3, add);
-        }
-        if (li == 0) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                if (4 * g + r < L3) put(R + S::RWO + G + 4 * g + r, ah3[r], add);
-#pragma unroll
-            for (int e = 0; e < GQ; ++e) put(R + S::RWO + GQ * g + e, agmf[e], add);
-        }
-        if (lane == 0) {
-            put(R + S::RBO, acc_dbo, add);
-            put(R + S::RX, acc_bce, add);
-            put(R + S::RX + 1, acc_hit, add);
-            put(R + S::RX + 2, acc_dcg, add);
-        }
-    };
-    // Fixed order, slab = (w0 + w2) + (w1 + w3).  Waves 2, 3 put their sums in rows 0, 1; waves
-    // 0, 1 add them to their registers (all reads issued before the adds), wave 1 writes its
-    // total back; wave 0 adds it and writes the dW tiles to the slab straight from registers while
-    // the other waves write the bias / output entries.
-    if (wv >= 2) {
-        for_tiles([&](int t, f32x4& v) { *reinterpret_cast<f32x4*>(R + t * 256 + lane * 4) = v; });
-        scalars(false);
+        for (int t = 0; t < B2; ++t) R[S::RB2 + 16 * t + li] = ab2[t];
+        if (li < L3) R[S::RB3 + li] = ab3;
     }
-    __syncthreads();
-    if (wv < 2) {
-        f32x4 o[S::NT];
-        for_tiles([&](int t, f32x4&) { o[t] = *tile_at(R, t); });
-        for_tiles([&](int t, f32x4& v) { v += o[t]; });
-        scalars(true);
-        if (wv == 1) for_tiles([&](int t, f32x4& v) { *reinterpret_cast<f32x4*>(R + t * 256 + lane * 4) = v; });
+    if (li == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            if (4 * g + r < L3) R[S::RWO + G + 4 * g + r] = ah3[r];
+#pragma unroll
+        for (int e = 0; e < GQ; ++e) R[S::RWO + GQ * g + e] = agmf[e];
     }
-    __syncthreads();
-    NCF_WS(15, __builtin_readcyclecounter());
+    if (lane == 0) {
+        R[S::RBO] = acc_dbo;
+        R[S::RX] = acc_bce;
+        R[S::RX + 1] = acc_hit;
+        R[S::RX + 2] = acc_dcg;
+    }
+    // Two rounds of half the tiles: every wave puts its tiles in its own row (straight from the
+    // accumulators), then all 256 threads add the four rows in a fixed order,
+    // slab = (w0 + w2) + (w1 + w3), and write the flat slab; tile element (lane gq * 16 + c,
+    // register r) is row 16 a + 4 gq + r, column 16 b + c of its matrix
     float* slab = slabs + (size_t)blockIdx.x * S::P;
-    if (wv == 0) {
-        f32x4 o[S::NT];
-        for_tiles([&](int t, f32x4&) { o[t] = *tile_at(R1, t); });
-        // tile element (lane gq * 16 + c, register r) is row 16 a + 4 gq + r, column 16 b + c
+    const float* R0 = lds;
+    const float* R1 = lds + S::PR;
+    const float* R2 = lds + 2 * S::PR;
+    const float* R3 = lds + 3 * S::PR;
+    auto round = [&](int t0, int t1) {
         for_tiles([&](int t, f32x4& v) {
-            const f32x4 x = v + o[t];
+            if (t >= t0 && t < t1) *reinterpret_cast<f32x4*>(R + (t - t0) * 256 + lane * 4) = v;
+        });
+        __syncthreads();
+        for (int q = threadIdx.x; q < (t1 - t0) * 64; q += 256) {
+            auto at4 = [&](const float* row) { return *reinterpret_cast<const f32x4*>(row + 4 * q); };
+            const f32x4 x = (at4(R0) + at4(R2)) + (at4(R1) + at4(R3));
+            const int t = t0 + (q >> 6);  // uniform per wave
             int base, ld;
             bool keep = true;
             if (t < S::NT1) {
@@ -807,26 +794,29 @@ __global__ __launch_bounds__(256, 1) void k_fb_wave(const float* __restrict__ em
 #pragma unroll
                 for (int r = 0; r < 4; ++r) slab[base + (4 * g + r) * ld] = x[r];
             }
-        });
-    } else {
-        // biases, output kernel, output bias: back to back in the rows (RB1 .. RBO), segment by
-        // segment in the flat layout
-        for (int e = threadIdx.x - 64; e <= S::RBO - S::RB1; e += 192) {
-            const int d = e < L1 ? S::OB1 + e
-                          : e < L1 + L2 ? S::OB2 + (e - L1)
-                          : e < L1 + L2 + L3 ? S::OB3 + (e - L1 - L2)
-                                             : S::OWO + (e - L1 - L2 - L3);
-            slab[d] = R0[S::RB1 + e] + R1[S::RB1 + e];
         }
+    };
+    round(0, S::NTH);
+    // biases, output kernel, output bias: back to back in the rows (RB1 .. RBO), segment by
+    // segment in the flat layout
+    for (int e = threadIdx.x; e <= S::RBO - S::RB1; e += 256) {
+        const int d = e < L1 ? S::OB1 + e
+                      : e < L1 + L2 ? S::OB2 + (e - L1)
+                      : e < L1 + L2 + L3 ? S::OB3 + (e - L1 - L2)
+                                         : S::OWO + (e - L1 - L2 - L3);
+        slab[d] = (R0[S::RB1 + e] + R2[S::RB1 + e]) + (R1[S::RB1 + e] + R3[S::RB1 + e]);
     }
-    NCF_WT(0, 9);
-    if (threadIdx.x == 64) {
-        part_bce[blockIdx.x] = R0[S::RX] + R1[S::RX];
+    if (threadIdx.x == 0) {
+        part_bce[blockIdx.x] = (R0[S::RX] + R2[S::RX]) + (R1[S::RX] + R3[S::RX]);
         if constexpr (MET) {
-            part_hit[blockIdx.x] = R0[S::RX + 1] + R1[S::RX + 1];
-            part_dcg[blockIdx.x] = R0[S::RX + 2] + R1[S::RX + 2];
+            part_hit[blockIdx.x] = (R0[S::RX + 1] + R2[S::RX + 1]) + (R1[S::RX + 1] + R3[S::RX + 1]);
+            part_dcg[blockIdx.x] = (R0[S::RX + 2] + R2[S::RX + 2]) + (R1[S::RX + 2] + R3[S::RX + 2]);
         }
     }
+    NCF_WS(15, __builtin_readcyclecounter());
+    __syncthreads();  // the first round's rows are read before the second overwrites them
+    round(S::NTH, S::NT);
+    NCF_WT(0, 9);
     NCF_WS(12, __builtin_readcyclecounter());
     NCF_WS(13, __builtin_amdgcn_s_memrealtime());
 }
