@@ -99,19 +99,6 @@ __global__ __launch_bounds__(kBlock) void k_scan_local(const int32_t* __restrict
     scan_local_body<UNIQ>(cnt, r1, offs, tot, uloc, utot, (int)blockIdx.x);
 }
 
-// Exclusive prefix of the scan-block totals into LDS pre[0..nscan) (every thread participates).
-__device__ inline void block_prefix_of_totals(const int32_t* __restrict__ tot, int nscan, int* pre, int* sw) {
-    int carry = 0;
-    for (int base = 0; base < nscan; base += kBlock) {
-        const int x = base + (int)threadIdx.x < nscan ? tot[base + threadIdx.x] : 0;
-        int total;
-        const int ex = block_exscan_256(x, sw, &total);
-        if (base + (int)threadIdx.x < nscan) pre[base + threadIdx.x] = carry + ex;
-        carry += total;
-    }
-    __syncthreads();
-}
-
 // Plan outputs of k_fill (UNIQ only).
 struct PlanOut {
     const int32_t* uloc;
@@ -129,6 +116,12 @@ struct PlanOut {
 // (UNIQ) also numbers the occupied keys (compact ids) and writes the per-owner counts.
 // LIST (single table): also the compact list of the occupied keys (touched rows, ascending) and
 // its length, for the deferred-decay kernels.
+//
+// Latency: a thread's first row and first contribution are handled before the block prefixes
+// exist wherever they do not need them (single-table keys): the ids, the row's local offsets,
+// the block totals and — once the ids are in — the contribution's counter atomic and its key's
+// local offset all go out together, so the launch waits on two memory round trips instead of
+// five.  Later grid-stride passes (more keys or contributions than threads) take the plain path.
 template <int MODE, bool UNIQ, bool LIST>
 __global__ __launch_bounds__(kBlock) void k_fill(KeySrc ks, int64_t m, int32_t* __restrict__ cnt,
                                                  const int32_t* __restrict__ local, const int32_t* __restrict__ tot,
@@ -137,21 +130,86 @@ __global__ __launch_bounds__(kBlock) void k_fill(KeySrc ks, int64_t m, int32_t* 
                                                  int32_t* __restrict__ ifold) {
     extern __shared__ __attribute__((aligned(16))) int pre[];  // [nscan] (+ [nscan] unique prefix)
     __shared__ int sw[4];
+    constexpr bool U2 = UNIQ || LIST;
+    constexpr bool EARLY = MODE == kKeyPair && !UNIQ;
     int* upre = pre + nscan;
-    block_prefix_of_totals(tot, nscan, pre, sw);
-    if constexpr (UNIQ || LIST) block_prefix_of_totals(po.utot, nscan, upre, sw);
     const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t gstride = (int64_t)gridDim.x * blockDim.x;
     const int64_t K = r1 - 1;
+    const int lane = threadIdx.x & 63;
+    const uint64_t par = (lane & 1) ? 0xAAAAAAAAAAAAAAAAull : 0x5555555555555555ull;
+    const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+
+    // ---- early loads (EARLY): first contribution's key, first row's local offsets, the totals
+    int e_key = 0, e_top = 0, e_head = 0, e_loc = 0;
+    bool e_ok = false;
+    int r_loc = 0, r_loc1 = 0, r_uloc = 0;
+    int t_first = 0, u_first = 0;
+    if constexpr (EARLY) {
+        const int64_t c = gt;  // cb = gt - lane, c = cb + lane
+        bool own = true;
+        if (c < m) {
+            e_key = contrib_key<MODE>(c, ks, &e_ok, &own);
+            if (!e_ok) atomicOr(err, kErrIdRange);
+        }
+        if (gt < r1) {
+            r_loc = local[gt];
+            if constexpr (U2) {
+                if (gt < K) r_loc1 = local[gt + 1];
+                r_uloc = po.uloc[gt];
+            }
+        }
+        if ((int)threadIdx.x < nscan) {
+            t_first = tot[threadIdx.x];
+            if constexpr (U2) u_first = po.utot[threadIdx.x];
+        }
+        e_ok = e_ok && own;
+        const int kk = e_ok ? e_key : -2 - lane;  // inactive lanes: unique keys
+        const int prev = __shfl_up(kk, 2, 64);
+        const uint64_t heads = ~__ballot(lane >= 2 && prev == kk) & par;
+        e_head = 63 - __clzll(heads & upto);
+        const uint64_t later = heads & ~upto;
+        const int next = later ? __ffsll((unsigned long long)later) - 1 : 64 + (lane & 1);
+        if (e_ok && lane == e_head) e_top = atomicSub(&cnt[e_key], (next - e_head) >> 1);
+        if (e_ok) e_loc = local[e_key];
+    }
+
+    // ---- exclusive prefixes of the scan-block totals into LDS (pre, upre)
+    {
+        int carry = 0, ucarry = 0;
+        for (int base = 0; base < nscan; base += kBlock) {
+            const bool in = base + (int)threadIdx.x < nscan;
+            int x, y = 0;
+            if (EARLY && base == 0) {
+                x = t_first;
+                y = u_first;
+            } else {
+                x = in ? tot[base + threadIdx.x] : 0;
+                if constexpr (U2) y = in ? po.utot[base + threadIdx.x] : 0;
+            }
+            int total;
+            const int ex = block_exscan_256(x, sw, &total);
+            if (in) pre[base + threadIdx.x] = carry + ex;
+            carry += total;
+            if constexpr (U2) {
+                int utotal;
+                const int uex = block_exscan_256(y, sw, &utotal);
+                if (in) upre[base + threadIdx.x] = ucarry + uex;
+                ucarry += utotal;
+            }
+        }
+        __syncthreads();
+    }
     if (gt == 0) *ifold = ks.fold;
     for (int64_t r = gt; r < r1; r += gstride) {
-        const int o = local[r] + pre[r / kScanBlock];
+        const bool first = EARLY && r == gt;
+        const int o = (first ? r_loc : local[r]) + pre[r / kScanBlock];
         offs_g[r] = o;
-        if constexpr (UNIQ || LIST) {
+        if constexpr (U2) {
             if (r < K) {
-                const int o1 = local[r + 1] + pre[(r + 1) / kScanBlock];
+                const int o1 = (first ? r_loc1 : local[r + 1]) + pre[(r + 1) / kScanBlock];
                 if (o1 > o) {
-                    const int u = po.uloc[r] + upre[r / kScanBlock];
+                    const int u = (first ? r_uloc : po.uloc[r]) + upre[r / kScanBlock];
                     if constexpr (UNIQ) {
                         po.uniq_rows[u] = (int)(r % ks.S);
                         po.uoffs[u] = o;
@@ -181,15 +239,23 @@ __global__ __launch_bounds__(kBlock) void k_fill(KeySrc ks, int64_t m, int32_t* 
     // (a user group's samples: c = 2i, 2i+2, ...) form runs; the run's head takes all of its
     // slots with one atomic and hands them out, so a group's user contributions do not queue on
     // one counter.  Slot order within a key does not matter: the lists are sorted afterwards.
-    const int lane = threadIdx.x & 63;
-    const uint64_t par = (lane & 1) ? 0xAAAAAAAAAAAAAAAAull : 0x5555555555555555ull;
-    const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
-    for (int64_t cb = gt - lane; cb < m; cb += gstride) {
+    // A slot below the key's range means the key was counted fewer times than it occurs
+    // (counted-ahead ids changed since): flagged, never written outside the key's slots.
+    if constexpr (EARLY) {
+        if (gt - lane < m) {
+            const int top = __shfl(e_top, e_head, 64);
+            const int slot = top - 1 - ((lane - e_head) >> 1);
+            if (e_ok && slot >= 0) list[e_loc + pre[e_key / kScanBlock] + slot] = (int)gt;
+            else if (e_ok) atomicOr(err, kErrStaleCount);
+        }
+    }
+    for (int64_t cb = gt - lane + (EARLY ? gstride : 0); cb < m; cb += gstride) {
         const int64_t c = cb + lane;
         bool ok = false, own = true;
         int key = 0;
         if (c < m) {
             key = contrib_key<MODE>(c, ks, &ok, &own);
+            if (!ok) atomicOr(err, kErrIdRange);
             if constexpr (UNIQ) {
                 const int u = ok ? po.uloc[key] + upre[key / kScanBlock] : -1;
                 ((c & 1) ? po.cid_i : po.cid_u)[c >> 1] = u;
@@ -205,8 +271,6 @@ __global__ __launch_bounds__(kBlock) void k_fill(KeySrc ks, int64_t m, int32_t* 
         int top = 0;
         if (ok && lane == head) top = atomicSub(&cnt[key], (next - head) >> 1);
         top = __shfl(top, head, 64);
-        // a slot below the key's range means the key was counted fewer times than it occurs
-        // (counted-ahead ids changed since): flagged, never written outside the key's slots
         const int slot = top - 1 - ((lane - head) >> 1);
         if (ok && slot >= 0) list[local[key] + pre[key / kScanBlock] + slot] = (int)c;
         else if (ok) atomicOr(err, kErrStaleCount);
