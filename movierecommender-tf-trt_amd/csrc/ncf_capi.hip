@@ -284,6 +284,7 @@ WsLayout make_layout(const ncf_shape_t& s, int64_t B, int world) {
         L.uoffs = take((size_t)(2 * B + 1) * 4);
     } else {
         L.touched = take((size_t)(R < 2 * B ? R : 2 * B) * 4);
+        L.touched_oc = take((size_t)(R < 2 * B ? R : 2 * B) * 8);
     }
     L.act = take((size_t)B * A * 4);
     L.dz = take((size_t)B * D * 4);

@@ -109,6 +109,7 @@ struct PlanOut {
     int32_t* cid_i;        // [n]
     int32_t* uoffs;        // [nuniq + 1]
     int32_t* nuniq;
+    int2* uniq_oc;         // LIST: [nuniq] (list offset, contribution count) of each touched row
 };
 
 // Finalise the key offsets (offs_g = local scan + prefix of block totals) and scatter every
@@ -215,6 +216,7 @@ __global__ __launch_bounds__(kBlock) void k_fill(KeySrc ks, int64_t m, int32_t* 
                         po.uoffs[u] = o;
                     } else {
                         po.uniq_rows[u] = (int)r;
+                        po.uniq_oc[u] = make_int2(o, o1 - o);
                     }
                 }
             }
@@ -346,6 +348,7 @@ hipError_t launch_index_build(const ncf_shape_t& s, const WsLayout& L, void* ws,
         po.utot = at<int32_t>(ws, L.utot);
         po.uniq_rows = at<int32_t>(ws, L.touched);
         po.nuniq = at<int32_t>(ws, L.nuniq);
+        po.uniq_oc = at<int2>(ws, L.touched_oc);
         return build<kKeyPair, false, true>(L, ws, ks, 2 * n, s.num_rows, po, (int)((2 * n + 31) / 32), st,
                                             counted, skip_sort);
     }

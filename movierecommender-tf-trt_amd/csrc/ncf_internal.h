@@ -56,6 +56,7 @@ struct WsLayout {
     size_t uoffs;     // int32[2B+1] compact row -> first list slot
     size_t nuniq;     // int32       number of unique rows (single table: of touched rows)
     size_t touched;   // int32[min(R, 2B)] single table, deferred decay: the touched rows, ascending
+    size_t touched_oc;  // int2[min(R, 2B)] their (list offset, contribution count): the update needs no offs
     size_t act;       // float[B * A] generic kernel activations
     size_t dz;        // float[B * D] generic kernel pre-activation grad
     size_t ones;      // float[B] layered path: all-ones vector (column sums as GEMV)ients

@@ -189,8 +189,9 @@ __global__ __launch_bounds__(kBlock) void k_emb_update(float4* __restrict__ emb,
 #define NCF_CATCHUP_AHEAD 1
 #endif
 #ifndef NCF_AHEAD_REP
-#define NCF_AHEAD_REP 2
+#define NCF_AHEAD_REP 3   // catch-up-ahead replay items per wave with their loads in flight together (4 spills at 7 blocks/CU)
 #endif
+constexpr int kRep = NCF_AHEAD_REP;
 // occupancy floor of the touched-row update launch (its HBM-bound rows want many waves; the
 // catch-up-ahead blocks in the same launch must not raise its register count)
 #ifndef NCF_TOUCHED_MIN_BLOCKS
@@ -417,6 +418,7 @@ struct MlpTail {
 __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_touched(float4* __restrict__ emb, float4* __restrict__ m4,
                                                              float4* __restrict__ v4, uint32_t w4,
                                                              const int32_t* __restrict__ list,
+                                                             const int2* __restrict__ toc,
                                                              const int32_t* __restrict__ nlist,
                                                              const int32_t* __restrict__ offs,
                                                              const int32_t* __restrict__ clist,
@@ -426,13 +428,17 @@ __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_tou
                                                              CountAhead ca, MlpTail mt) {
     // block order: [count (+ catch-up ahead)] [touched-row update] [dense-layer Adam]: the
     // latency-bound replay blocks are dispatched first, so they run under the HBM-bound update
-    if ((int)blockIdx.x >= ca.nupd + ca.ncount) {
+    // (interleaving them one in every (nupd + ncount) / ncount blocks was measured slower: 60.2
+    // vs 53.3 us at config C — their chains are the launch's long pole)
+    const int b = (int)blockIdx.x;
+    if (b >= ca.nupd + ca.ncount) {
         mlp_update_body<NCF_OPT_ADAM>(mt.p, mt.m, mt.v, mt.P, mt.slabs, mt.nslab, nullptr, nullptr, 1, 0, mt.step,
                                       mt.lr, mt.b1, mt.b2, mt.eps, mt.l2t, mt.part_reg,
                                       (int)blockIdx.x - ca.nupd - ca.ncount);
         return;
     }
-    if ((int)blockIdx.x < ca.ncount) {
+    if (b < ca.ncount) {
+        const int cblk = b;  // this block's index among the count blocks
         // count the NEXT batch's contributions (k_count's work) while this step's rows stream; the
         // counters are free here (the fill of this step's index emptied them).
         // Catch-up ahead (ca.replay): a row of the next batch that this step does not touch owes
@@ -440,26 +446,23 @@ __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_tou
         // launch reads or writes it, so it is replayed here (k_emb_catchup's work, same per-step
         // arithmetic: bitwise) under the touched-row update, instead of in a launch of its own
         // before the next forward pass.  One lane claims a row (CAS on row_step: a user's
-        // repeated contributions replay it once); the wave replays its claimed rows, kRep at a
-        // time with all their loads in flight and the rows' chains interleaved, one element per
-        // lane, and leaves p, m, v and row_step at step t.
+        // repeated contributions replay it once) and leaves p, m, v and row_step at step t.
         __shared__ float lut[kLrLut];
         const int t = *step + 1;
-        if (ca.replay) {
-            if (threadIdx.x < kLrLut)
-                lut[threadIdx.x] = t - (int)threadIdx.x >= 1 ? adam_lr_t(lr, b1, b2, t - threadIdx.x) : 0.f;
-            __syncthreads();
-        }
+        if (ca.replay && threadIdx.x < kLrLut)
+            lut[threadIdx.x] = t - (int)threadIdx.x >= 1 ? adam_lr_t(lr, b1, b2, t - threadIdx.x) : 0.f;
         const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
         const int W = 4 * (int)w4;
         float* embf = reinterpret_cast<float*>(emb);
         float* mf = reinterpret_cast<float*>(m4);
         float* vf = reinterpret_cast<float*>(v4);
         // a block takes 64 contributions per pass: wave 0 counts them and claims the stale rows,
-        // then the block's 4 waves share the claimed rows' replay (one row per wave at a time,
-        // one element per lane) — many short replay chains in flight instead of a few long ones
+        // then the block's 4 waves share the claimed rows' replay, kRep (row, 64-element slice)
+        // items per wave at a time with all their loads in flight — many short replay chains in
+        // flight (many blocks), one memory round trip per batch of items instead of per row
         __shared__ int crow[64], cstep[64], ncl;
-        for (int64_t cb = (int64_t)blockIdx.x * 64; cb < ca.m; cb += (int64_t)ca.ncount * 64) {
+        for (int64_t cb = (int64_t)cblk * 64; cb < ca.m; cb += (int64_t)ca.ncount * 64) {
+            __syncthreads();  // lut ready, the previous pass's replay done
             if (wv == 0) {
                 const int64_t c = cb + lane;
                 bool ok = false;
@@ -474,8 +477,14 @@ __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_tou
                 wave_run_count(ca.cnt, key, ok);
                 bool claim = false;
                 int s0 = 0;
-                if (ca.replay && ok && offs[key + 1] == offs[key]) {   // not in this step's batch
-                    int sv = row_step[key];
+                // the row's step goes out with its offsets (one memory round trip, not two)
+                int o0 = 0, o1 = 0, sv = t;
+                if (ca.replay && ok) {
+                    o0 = offs[key];
+                    o1 = offs[key + 1];
+                    sv = row_step[key];
+                }
+                if (ca.replay && ok && o1 == o0) {   // not in this step's batch
                     while (sv < t) {
                         const int prev = atomicCAS(&row_step[key], sv, t);
                         if (prev == sv) {
@@ -495,25 +504,45 @@ __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_tou
                 if (lane == 0) ncl = __popcll(cm);
             }
             __syncthreads();
-            const int nc = ncl;
-            for (int k = wv; k < nc; k += kBlock / 64) {
-                const int64_t r = crow[k];
-                const int sr = cstep[k];
-                for (int q = lane; q < W; q += 64) {
-                    const size_t e = (size_t)r * W + q;
-                    float p = embf[e], mm = mf[e], vv = vf[e];
-                    for (int j = sr + 1; j <= t; ++j)
-                        adam1(p, mm, vv, 0.0f, t - j < kLrLut ? lut[t - j] : adam_lr_t(lr, b1, b2, j), b1, b2, eps);
-                    embf[e] = p;
-                    mf[e] = mm;
-                    vf[e] = vv;
+            const int per_row = (W + 63) >> 6;
+            const int items = ncl * per_row;
+            // item it = row it / per_row, elements (it % per_row) * 64 + lane; wave wv takes
+            // it = wv + 4 j (wave-uniform: the step loops do not diverge)
+            for (int i0 = wv; i0 < items; i0 += 4 * kRep) {
+                float p[kRep], mm[kRep], vv[kRep];
+                size_t e[kRep];
+                int sr[kRep];
+                bool act[kRep];
+#pragma unroll
+                for (int j = 0; j < kRep; ++j) {
+                    const int it = i0 + 4 * j;
+                    const int k = it < items ? it / per_row : 0;
+                    const int q = (it - k * per_row) * 64 + lane;
+                    act[j] = it < items && q < W;
+                    sr[j] = it < items ? cstep[k] : t;
+                    e[j] = (size_t)crow[k] * W + (act[j] ? q : 0);
+                    p[j] = act[j] ? embf[e[j]] : 0.f;
+                    mm[j] = act[j] ? mf[e[j]] : 0.f;
+                    vv[j] = act[j] ? vf[e[j]] : 0.f;
+                }
+#pragma unroll
+                for (int j = 0; j < kRep; ++j)
+                    for (int st = sr[j] + 1; st <= t; ++st)
+                        adam1(p[j], mm[j], vv[j], 0.0f, t - st < kLrLut ? lut[t - st] : adam_lr_t(lr, b1, b2, st), b1,
+                              b2, eps);
+#pragma unroll
+                for (int j = 0; j < kRep; ++j) {
+                    if (act[j]) {
+                        embf[e[j]] = p[j];
+                        mf[e[j]] = mm[j];
+                        vf[e[j]] = vv[j];
+                    }
                 }
             }
-            __syncthreads();
         }
         return;
     }
-    const int ublk = (int)blockIdx.x - ca.ncount;   // this block's index among the update blocks
+    const int ublk = b - ca.ncount;   // this block's index among the update blocks
     const RowLanes rl(w4);
     const int t = *step + 1;
     if (rl.on) {
@@ -522,14 +551,16 @@ __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_tou
         const int64_t wave = ((int64_t)ublk * kBlock + threadIdx.x) >> 6;
         const int64_t stride = (((int64_t)ca.nupd * kBlock) >> 6) * rl.rpw;
         int64_t i = wave * rl.rpw + rl.sub;
-        // software pipeline over this lane group's rows: the next row's id is loaded while the
-        // current row is processed, so the list -> offsets -> contribution chain of row i+1
-        // overlaps row i's state and gradient traffic
+        // software pipeline over this lane group's rows: the next row's id and (list offset,
+        // count) are loaded while the current row is processed, so the list -> contribution
+        // chain of row i+1 overlaps row i's state and gradient traffic
         int r = i < n ? list[i] : 0;
+        int2 oc = i < n ? toc[i] : make_int2(0, 0);
         for (; i < n; i += stride) {
             const int rn = i + stride < n ? list[i + stride] : 0;
-            const int o = offs[r];
-            const int c = offs[r + 1] - o;
+            const int2 ocn = i + stride < n ? toc[i + stride] : make_int2(0, 0);
+            const int o = oc.x;
+            const int c = oc.y;
             const int k = NCF_CATCHUP_P_ONLY ? t - 1 - row_step[r] : 0;  // m/v decay steps still owed
             for (uint32_t q = rl.q; q < w4; q += rl.qstep) {
                 const size_t e = (size_t)r * w4 + q;
@@ -558,6 +589,7 @@ __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_tou
             }
             if (rl.q == 0) row_step[r] = t;
             r = rn;
+            oc = ocn;
         }
     }
 }
@@ -988,7 +1020,7 @@ hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, vo
         }
         launch(k_emb_adam_touched, nupd + ncount + (unsigned)mt.nblocks, kBlock, 0, st,
                (float4*)emb, (float4*)m, (float4*)v, w4, at<const int32_t>(ws, L.touched),
-               at<const int32_t>(ws, L.nuniq), offs, list, gs, row_step, (const int32_t*)step, h.lr, h.beta_1, h.beta_2,
+               at<const int2>(ws, L.touched_oc), at<const int32_t>(ws, L.nuniq), offs, list, gs, row_step, (const int32_t*)step, h.lr, h.beta_1, h.beta_2,
                h.epsilon, ca, mt);
     } else
         launch(k_emb_sgd_hot, kUpdateGrid, kBlock, 0, st, (float4*)emb, n4, w4, offs, list, gs, h.lr);
