@@ -175,6 +175,40 @@ __device__ __forceinline__ float row_sum(float x) {
     return x;
 }
 
+// sum over the 4 lane groups (lanes l, l ^ 16, l ^ 32, l ^ 48): gfx950's permlane swaps (VALU),
+// every lane gets (g0 + g1) + (g2 + g3)
+__device__ __forceinline__ float group_allsum(float x) {
+    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    x = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+    const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
+// element q of this lane's group of FOLD consecutive lanes (DPP quad permutes for FOLD 2, 4;
+// q is a compile-time constant at every call site, the switch folds away)
+template <int CTRL>
+__device__ __forceinline__ int dpp_mov(int x) {
+    return __builtin_amdgcn_mov_dpp(x, CTRL, 0xF, 0xF, false);
+}
+template <int FOLD, class T>
+__device__ __forceinline__ T grp_bcast(T x, int q, int lane) {
+    static_assert(sizeof(T) == 4, "32-bit values");
+    const int v = __builtin_bit_cast(int, x);
+    if constexpr (FOLD == 4) {
+        switch (q) {
+            case 0: return __builtin_bit_cast(T, dpp_mov<0x00>(v));  // quad_perm [0,0,0,0]
+            case 1: return __builtin_bit_cast(T, dpp_mov<0x55>(v));  // [1,1,1,1]
+            case 2: return __builtin_bit_cast(T, dpp_mov<0xAA>(v));  // [2,2,2,2]
+            default: return __builtin_bit_cast(T, dpp_mov<0xFF>(v)); // [3,3,3,3]
+        }
+    } else if constexpr (FOLD == 2) {
+        return q == 0 ? __builtin_bit_cast(T, dpp_mov<0xA0>(v))   // [0,0,2,2]
+                      : __builtin_bit_cast(T, dpp_mov<0xF5>(v));  // [1,1,3,3]
+    } else {
+        return __shfl(x, (lane & ~(FOLD - 1)) + q, 64);
+    }
+}
+
 // Span stamps (g_wave_s, 16 per wave): 0/1 entry (s_memrealtime / cycles), 2 weights in LDS,
 // 3 + k start of the wave's unit k (k < 8), 11 loop done, 14 epilogue's first barrier passed,
 // 15 the four waves' sums in LDS, 12 end (cycles), 13 end (s_memrealtime).
@@ -470,9 +504,7 @@ __global__ __launch_bounds__(256, 1) void k_fb_wave(const float* __restrict__ em
 #pragma unroll
             for (int e = 0; e < GQ; ++e) zp += wg[e] * (gu[e] * gi[e]);
         }
-        zp += __shfl_xor(zp, 16, 64);
-        zp += __shfl_xor(zp, 32, 64);
-        const float z = zp + wl[S::SBO];
+        const float z = group_allsum(zp) + wl[S::SBO];
         // v_exp_f32 / v_rcp_f32 (about 1 ulp each): the probability stays within ~1e-7 of the
         // correctly rounded sigmoid, far inside the 2e-6 the tests hold it to
         const float pr = __builtin_amdgcn_rcpf(1.0f + __expf(-z));
@@ -493,22 +525,23 @@ __global__ __launch_bounds__(256, 1) void k_fb_wave(const float* __restrict__ em
         // launch asks for it when group == FOLD): label = first max of y; position =
         // #(p > p_lab) + #(earlier ties)
         if constexpr (MET) {
-            const int e = li & fm, base = lane - e;
+            const int e = li & fm;
             int lab = 0;
-            float best = __shfl(cy, base, 64);
+            float best = grp_bcast<FOLD>(cy, 0, lane), pq[FOLD];
 #pragma unroll
             for (int q = 1; q < FOLD; ++q) {
-                const float yq = __shfl(cy, base + q, 64);
+                const float yq = grp_bcast<FOLD>(cy, q, lane);
                 lab = yq > best ? q : lab;
                 best = fmaxf(best, yq);
             }
-            const float pl = __shfl(pr, base + lab, 64);
+#pragma unroll
+            for (int q = 0; q < FOLD; ++q) pq[q] = grp_bcast<FOLD>(pr, q, lane);
+            float pl = pq[0];
+#pragma unroll
+            for (int q = 1; q < FOLD; ++q) pl = lab == q ? pq[q] : pl;
             int pos = 0;
 #pragma unroll
-            for (int q = 0; q < FOLD; ++q) {
-                const float pq = __shfl(pr, base + q, 64);
-                pos += (pq > pl) || (pq == pl && q < lab);
-            }
+            for (int q = 0; q < FOLD; ++q) pos += (pq[q] > pl) || (pq[q] == pl && q < lab);
             const float hit = g == 0 && e == 0 && inb && pos < topk ? 1.f : 0.f;
             acc_hit += hit;
             acc_dcg += hit * (0.69314718f * __builtin_amdgcn_rcpf(__logf((float)pos + 2.0f)));
@@ -526,7 +559,7 @@ __global__ __launch_bounds__(256, 1) void k_fb_wave(const float* __restrict__ em
 
         // ---- GMF backward; user rows of a fold group summed into its head sample
         const int su = inb ? cu : -1;
-        const bool fmatch = FOLD > 1 && inb && su == __shfl(su, lane & ~fm, 64);
+        const bool fmatch = FOLD > 1 && inb && su == grp_bcast<(FOLD > 1 ? FOLD : 2)>(su, 0, lane);
         const bool fhead = (li & fm) == 0;
         // byte offsets of this sample's user / item gradient rows (or dropped)
         const uint32_t urow_off = inb && (fhead || !fmatch) ? (uint32_t)(2 * sg * W) * 4u : kDrop;
@@ -711,21 +744,17 @@ __global__ __launch_bounds__(256, 1) void k_fb_wave(const float* __restrict__ em
 #pragma unroll
     for (int r = 0; r < 4; ++r) ah3[r] = row_sum(ah3[r]);
     // bias sums: over the 4 lane groups (samples 4 q + lq)
-    auto group_sum = [](float x) {
-        x += __shfl_xor(x, 16, 64);
-        return x + __shfl_xor(x, 32, 64);
-    };
 #pragma unroll
-    for (int t = 0; t < B1; ++t) ab1[t] = group_sum(ab1[t]);
+    for (int t = 0; t < B1; ++t) ab1[t] = group_allsum(ab1[t]);
 #pragma unroll
-    for (int t = 0; t < B2; ++t) ab2[t] = group_sum(ab2[t]);
-    ab3 = group_sum(ab3);
+    for (int t = 0; t < B2; ++t) ab2[t] = group_allsum(ab2[t]);
+    ab3 = group_allsum(ab3);
 #pragma unroll
     for (int e = 0; e < GQ; ++e) agmf[e] = row_sum(agmf[e]);
-    acc_dbo = wave_sum(acc_dbo);
-    acc_bce = wave_sum(acc_bce);
-    acc_hit = wave_sum(acc_hit);
-    acc_dcg = wave_sum(acc_dcg);
+    acc_dbo = group_allsum(row_sum(acc_dbo));
+    acc_bce = group_allsum(row_sum(acc_bce));
+    acc_hit = group_allsum(row_sum(acc_hit));
+    acc_dcg = group_allsum(row_sum(acc_dcg));
     __syncthreads();  // every wave is done with the weights and its buffers
     NCF_WS(14, __builtin_readcyclecounter());
     float* R = lds + wv * S::PR;
