@@ -400,6 +400,7 @@ struct CountAhead {
     int32_t* cnt;
     int replay;                // 1: also catch the next batch's stale rows up (catch-up ahead)
     int fold;                  // user-row folding of the next batch's index (fold_of)
+    int per;                   // contributions per count block and pass (16, 32 or 64)
 };
 
 // the dense layers' Adam (k_mlp_update<ADAM>'s work) in blocks >= nupd + ncount of the same launch
@@ -456,18 +457,20 @@ __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_tou
         float* embf = reinterpret_cast<float*>(emb);
         float* mf = reinterpret_cast<float*>(m4);
         float* vf = reinterpret_cast<float*>(v4);
-        // a block takes 64 contributions per pass: wave 0 counts them and claims the stale rows,
-        // then the block's 4 waves share the claimed rows' replay, kRep (row, 64-element slice)
-        // items per wave at a time with all their loads in flight — many short replay chains in
-        // flight (many blocks), one memory round trip per batch of items instead of per row
+        // a block takes ca.per contributions per pass: wave 0 counts them and claims the stale
+        // rows, then the block's 4 waves share the claimed rows' replay, kRep (row, 64-element
+        // slice) items per wave at a time with all their loads in flight and their step chains
+        // interleaved — many short replay chains in flight (small batches get 16 contributions
+        // per block: their rows owe many steps each), one memory round trip per batch of items
         __shared__ int crow[64], cstep[64], ncl;
-        for (int64_t cb = (int64_t)cblk * 64; cb < ca.m; cb += (int64_t)ca.ncount * 64) {
+        const int per = ca.per;
+        for (int64_t cb = (int64_t)cblk * per; cb < ca.m; cb += (int64_t)ca.ncount * per) {
             __syncthreads();  // lut ready, the previous pass's replay done
             if (wv == 0) {
                 const int64_t c = cb + lane;
                 bool ok = false;
                 int key = 0;
-                if (c < ca.m) {
+                if (lane < per && c < ca.m) {
                     const int64_t i = c >> 1;
                     const int id = (c & 1) ? ca.items[i] : ca.users[i];
                     const int bound = (c & 1) ? ca.I : ca.U;
@@ -525,11 +528,16 @@ __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_tou
                     mm[j] = act[j] ? mf[e[j]] : 0.f;
                     vv[j] = act[j] ? vf[e[j]] : 0.f;
                 }
+                // the items' chains advance together (same per-element arithmetic, step by step)
+                int smin = t;
 #pragma unroll
-                for (int j = 0; j < kRep; ++j)
-                    for (int st = sr[j] + 1; st <= t; ++st)
-                        adam1(p[j], mm[j], vv[j], 0.0f, t - st < kLrLut ? lut[t - st] : adam_lr_t(lr, b1, b2, st), b1,
-                              b2, eps);
+                for (int j = 0; j < kRep; ++j) smin = sr[j] < smin ? sr[j] : smin;
+                for (int st = smin + 1; st <= t; ++st) {
+                    const float lrt = t - st < kLrLut ? lut[t - st] : adam_lr_t(lr, b1, b2, st);
+#pragma unroll
+                    for (int j = 0; j < kRep; ++j)
+                        if (st > sr[j]) adam1(p[j], mm[j], vv[j], 0.0f, lrt, b1, b2, eps);
+                }
 #pragma unroll
                 for (int j = 0; j < kRep; ++j) {
                     if (act[j]) {
@@ -1008,10 +1016,12 @@ hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, vo
     if (h.optimizer == NCF_OPT_ADAM) {
         const unsigned nupd = row_grid(R < 2 * L.max_batch ? R : 2 * L.max_batch, w4, NCF_TOUCHED_GRID_MAX);
         const int64_t mc = next_users ? 2 * n_next : 0;
-        // count (+ catch-up ahead) blocks: 64 contributions per block and pass
-        const unsigned ncount = mc > 0 ? (unsigned)((mc + 63) / 64 < 4096 ? (mc + 63) / 64 : 4096) : 0u;
+        // count (+ catch-up ahead) blocks: 64 contributions per block and pass, 32 / 16 below 65,536
+        // / 32,768 contributions (at least ~1,000 blocks of replay chains)
+        const int per = mc >= 65536 ? 64 : mc >= 32768 ? 32 : 16;
+        const unsigned ncount = mc > 0 ? (unsigned)((mc + per - 1) / per < 4096 ? (mc + per - 1) / per : 4096) : 0u;
         CountAhead ca{(int)nupd, (int)ncount, next_users, next_items, mc, s.num_users, s.num_items,
-                      at<int32_t>(ws, L.cnt), replay_ahead ? 1 : 0, next_fold};
+                      at<int32_t>(ws, L.cnt), replay_ahead ? 1 : 0, next_fold, per};
         MlpTail mt{};
         if (mlp) {
             mt = MlpTail{(s.mlp_params + kBlock - 1) / kBlock, mlp->p, mlp->m, mlp->v, s.mlp_params, mlp->slabs,
