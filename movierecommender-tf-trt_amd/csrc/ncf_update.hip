@@ -192,6 +192,9 @@ __global__ __launch_bounds__(kBlock) void k_emb_update(float4* __restrict__ emb,
 #define NCF_AHEAD_REP 3   // catch-up-ahead replay items per wave with their loads in flight together (4 spills at 7 blocks/CU)
 #endif
 constexpr int kRep = NCF_AHEAD_REP;
+#ifndef NCF_COUNT_PER_MAX
+#define NCF_COUNT_PER_MAX 64   // contributions per count block and pass from 65,536 contributions
+#endif
 // occupancy floor of the touched-row update launch (its HBM-bound rows want many waves; the
 // catch-up-ahead blocks in the same launch must not raise its register count)
 #ifndef NCF_TOUCHED_MIN_BLOCKS
@@ -1018,7 +1021,7 @@ hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, vo
         const int64_t mc = next_users ? 2 * n_next : 0;
         // count (+ catch-up ahead) blocks: 64 contributions per block and pass, 32 / 16 below 65,536
         // / 32,768 contributions (at least ~1,000 blocks of replay chains)
-        const int per = mc >= 65536 ? 64 : mc >= 32768 ? 32 : 16;
+        const int per = mc >= 65536 ? NCF_COUNT_PER_MAX : mc >= 32768 ? 32 : 16;
         const unsigned ncount = mc > 0 ? (unsigned)((mc + per - 1) / per < 4096 ? (mc + per - 1) / per : 4096) : 0u;
         CountAhead ca{(int)nupd, (int)ncount, next_users, next_items, mc, s.num_users, s.num_items,
                       at<int32_t>(ws, L.cnt), replay_ahead ? 1 : 0, next_fold, per};
