@@ -14,6 +14,7 @@
 // row's per-sample gradient contributions in ascending sample order through
 // the index built by ncf_index.hip (deterministic, no atomics).
 
+#include <climits>
 #include <cmath>
 
 #include "ncf_common.h"
@@ -1168,9 +1169,74 @@ hipError_t launch_mlp_update(const ncf_shape_t& s, const WsLayout& L, void* ws, 
     return hipGetLastError();
 }
 
+// Groups wider than 8 (evaluation: 1 positive + 99 negatives): one wave per group, its elements
+// on the lanes (coalesced reads, chunks of 64), label = first max of y and position = #(p > p_lab)
+// + #(earlier ties) from wave reductions — the per-group hit and dcg of k_group_metrics, with
+// every lane of the machine busy instead of one thread per group.  A block's 4 waves loop over
+// groups with the block's stride and add their sums into one partial per block.
+__global__ __launch_bounds__(kBlock) void k_group_metrics_wave(const float* __restrict__ probs,
+                                                               const float* __restrict__ labels, int64_t ng,
+                                                               int group, int k, float* __restrict__ hit,
+                                                               float* __restrict__ dcg, float* __restrict__ part_hit,
+                                                               float* __restrict__ part_dcg) {
+    __shared__ float red[4];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    float h_acc = 0.f, d_acc = 0.f;
+    for (int64_t g = (int64_t)blockIdx.x * 4 + wv; g < ng; g += (int64_t)gridDim.x * 4) {
+        const float* pr = probs + g * group;
+        const float* lb = labels + g * group;
+        float best = -INFINITY;
+        for (int j = lane; j < group; j += 64) best = fmaxf(best, lb[j]);
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) best = fmaxf(best, __shfl_xor(best, m, 64));
+        int first = INT_MAX;
+        for (int j = lane; j < group; j += 64) first = lb[j] == best && j < first ? j : first;
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) first = min(first, __shfl_xor(first, m, 64));
+        const int lab = first;
+        const float pl = pr[lab];
+        int cnt = 0;
+        for (int j = lane; j < group; j += 64) {
+            const float pj = pr[j];
+            cnt += (pj > pl) || (pj == pl && j < lab);
+        }
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) cnt += __shfl_xor(cnt, m, 64);
+        const float h = cnt < k ? 1.0f : 0.0f;
+        const float d = h * (logf(2.0f) / logf((float)cnt + 2.0f));
+        if (lane == 0) {
+            if (hit) hit[g] = h;
+            if (dcg) dcg[g] = d;
+        }
+        h_acc += h;
+        d_acc += d;
+    }
+    if (lane == 0) red[wv] = h_acc;
+    __syncthreads();
+    const float hs = (red[0] + red[1]) + (red[2] + red[3]);
+    __syncthreads();
+    if (lane == 0) red[wv] = d_acc;
+    __syncthreads();
+    const float ds = (red[0] + red[1]) + (red[2] + red[3]);
+    if (threadIdx.x == 0) {
+        if (part_hit) part_hit[blockIdx.x] = hs;
+        if (part_dcg) part_dcg[blockIdx.x] = ds;
+    }
+}
+
 hipError_t launch_group_metrics(const float* probs, const float* labels, int64_t n_groups, int group, int k,
                                 float* hit, float* dcg, float* part_hit, float* part_dcg, int* nparts,
                                 hipStream_t st) {
+    if (group > 8) {
+        // a wave per group; at most ceil(samples / kBlock) partials (the workspace's nmetric)
+        const int64_t by_groups = (n_groups + 3) / 4, cap = (n_groups * group + kBlock - 1) / kBlock;
+        const int grid = (int)(by_groups < cap ? by_groups : cap);
+        *nparts = grid;
+        if (grid == 0) return hipSuccess;
+        launch(k_group_metrics_wave, grid, kBlock, 0, st, probs, labels, n_groups, group, k, hit, dcg, part_hit,
+               part_dcg);
+        return hipGetLastError();
+    }
     const int grid = (int)((n_groups + kBlock - 1) / kBlock);
     *nparts = grid;
     if (grid == 0) return hipSuccess;

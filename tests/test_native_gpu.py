@@ -497,3 +497,27 @@ def test_evaluate_full_protocol_fused_forward():
     assert st["loss"] == pytest.approx(O.bce_per_sample(pref, y).mean(), rel=1e-5)
     # predict() takes the same fused forward
     np.testing.assert_array_equal(eng.predict(users[:4096], items[:4096]).cpu().numpy(), p[:4096])
+
+
+@pytest.mark.parametrize("group", [9, 100, 150])
+def test_group_metrics_wide_groups_match_oracle(group):
+    """Groups wider than 8 run one wave per group (k_group_metrics_wave, chunks of 64 lanes for
+    group > 64): per-group hit and dcg equal the reference's RankLayer + _get_hits_per_user
+    restatement (model.py:344-455), label ties (first max wins) and probability ties included."""
+    shape = O.NCFShape(5, 10, [6, 4], 0)
+    eng = _engine(shape, _weights(shape, 0))
+    rng = np.random.RandomState(group)
+    ng = 300
+    p = np.round(rng.rand(ng, group), 2).astype(np.float32)      # many probability ties
+    y = np.zeros((ng, group), np.float32)
+    lab = rng.randint(0, group, ng)
+    y[np.arange(ng), lab] = 1.0
+    y[::7, (lab[::7] + 3) % group] = 1.0                         # two positives: the first counts
+    p[::5, (lab[::5] + 1) % group] = p[::5, lab[::5]]             # a negative tied with the positive
+    for k in (1, 10, group):
+        hit, dcg = eng.group_metrics(torch.from_numpy(p.reshape(-1)).to(eng.device), y.reshape(-1), group, k)
+        rank = O.rank_layer(p.reshape(-1), group)
+        hits, pos = O.hits_per_user(y, rank, k)
+        np.testing.assert_array_equal(hit.cpu().numpy(), hits.astype(np.float32))
+        ref_dcg = np.where(hits, np.log(2.0) / np.log(pos + 2.0), 0.0)
+        np.testing.assert_allclose(dcg.cpu().numpy(), ref_dcg, rtol=1e-6, atol=0)
