@@ -27,6 +27,17 @@ __device__ inline float adam_lr_t(float lr, float b1, float b2, int t) {
     return lr * (sqrtf(1.0f - powf(b2, ft)) / (1.0f - powf(b1, ft)));
 }
 
+// lr_t * m / (sqrt(v) + eps) with the hardware square root and reciprocal (v_sqrt_f32,
+// v_rcp_f32: ~1 ulp each) instead of the correctly rounded sequences (~20 VALU instructions):
+// the zero-gradient replays of the deferred decay are VALU-bound chains of these.  Every
+// embedding Adam path (dense sweep, touched-row update, replays, flush, sharded update) goes
+// through it, so they still round identically; against the correctly rounded quotient the step
+// term differs by a few ulp (the oracle tolerances hold it).
+__device__ __forceinline__ float adam_term(float lr_t, float m, float v, float eps) {
+#pragma clang fp contract(off)
+    return (lr_t * m) * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(v) + eps);
+}
+
 // One Adam step of one float4 element (Keras v1 update, see top of file).  Every sweep of the
 // table goes through this one function, so the dense sweep, the touched-row update and the
 // zero-gradient replay round identically.
@@ -40,8 +51,8 @@ __device__ __forceinline__ void adam4(float4& p, float4& m, float4& v, const flo
     m.z = b1 * m.z + c1 * g.z; m.w = b1 * m.w + c1 * g.w;
     v.x = b2 * v.x + c2 * (g.x * g.x); v.y = b2 * v.y + c2 * (g.y * g.y);
     v.z = b2 * v.z + c2 * (g.z * g.z); v.w = b2 * v.w + c2 * (g.w * g.w);
-    p.x -= lr_t * m.x / (sqrtf(v.x) + eps); p.y -= lr_t * m.y / (sqrtf(v.y) + eps);
-    p.z -= lr_t * m.z / (sqrtf(v.z) + eps); p.w -= lr_t * m.w / (sqrtf(v.w) + eps);
+    p.x -= adam_term(lr_t, m.x, v.x, eps); p.y -= adam_term(lr_t, m.y, v.y, eps);
+    p.z -= adam_term(lr_t, m.z, v.z, eps); p.w -= adam_term(lr_t, m.w, v.w, eps);
 }
 
 __device__ inline float block_sum_array(const float* __restrict__ a, int n, float* red) {
@@ -101,7 +112,7 @@ __device__ __forceinline__ void adam1(float& p, float& m, float& v, float g, flo
     const float c1 = 1.0f - b1, c2 = 1.0f - b2;
     m = b1 * m + c1 * g;
     v = b2 * v + c2 * (g * g);
-    p -= lr_t * m / (sqrtf(v) + eps);
+    p -= adam_term(lr_t, m, v, eps);
 }
 
 // adam4's moment updates with g = 0: b1*m + c1*0 and b2*v + c2*0 round like b1*m + 0, b2*v + 0
@@ -277,19 +288,46 @@ __global__ __launch_bounds__(kBlock) void k_emb_catchup(float4* __restrict__ emb
     float* embf = reinterpret_cast<float*>(emb);
     float* mf = reinterpret_cast<float*>(m4);
     float* vf = reinterpret_cast<float*>(v4);
-    for (int64_t i = (int64_t)blockIdx.x * rpb + sub; i < n; i += nblk * rpb) {
-        const int64_t r = ALL ? i : list[i];
-        const int s = row_step[r];
-        if (s >= t) continue;
+    // kRep rows per pass: their steps, then their elements' loads in flight together, their step
+    // chains advancing together (same per-element arithmetic: bitwise the one-row form)
+    const int64_t pstride = nblk * rpb;
+    for (int64_t i0 = (int64_t)blockIdx.x * rpb + sub; i0 < n; i0 += pstride * kRep) {
+        int64_t r[kRep];
+        int sr[kRep];
+#pragma unroll
+        for (int j = 0; j < kRep; ++j) {
+            const int64_t i = i0 + j * pstride;
+            r[j] = i < n ? (ALL ? i : list[i]) : 0;
+            sr[j] = i < n ? row_step[r[j]] : t;
+        }
         for (int q = q0; q < W; q += lanes_per_row) {
-            const size_t e = (size_t)r * W + q;
-            float p = embf[e], m = mf[e], v = vf[e];
-            for (int j = s + 1; j <= t; ++j)
-                adam1(p, m, v, 0.0f, t - j < kLrLut ? lut[t - j] : adam_lr_t(lr, b1, b2, j), b1, b2, eps);
-            embf[e] = p;
-            if (ALL || !NCF_CATCHUP_P_ONLY) {
-                mf[e] = m;
-                vf[e] = v;
+            float p[kRep], m[kRep], v[kRep];
+            int smin = t;
+#pragma unroll
+            for (int j = 0; j < kRep; ++j) {
+                const size_t e = (size_t)r[j] * W + q;
+                const bool act = sr[j] < t;
+                p[j] = act ? embf[e] : 0.f;
+                m[j] = act ? mf[e] : 0.f;
+                v[j] = act ? vf[e] : 0.f;
+                smin = sr[j] < smin ? sr[j] : smin;
+            }
+            for (int st = smin + 1; st <= t; ++st) {
+                const float lrt = t - st < kLrLut ? lut[t - st] : adam_lr_t(lr, b1, b2, st);
+#pragma unroll
+                for (int j = 0; j < kRep; ++j)
+                    if (st > sr[j]) adam1(p[j], m[j], v[j], 0.0f, lrt, b1, b2, eps);
+            }
+#pragma unroll
+            for (int j = 0; j < kRep; ++j) {
+                if (sr[j] < t) {
+                    const size_t e = (size_t)r[j] * W + q;
+                    embf[e] = p[j];
+                    if (ALL || !NCF_CATCHUP_P_ONLY) {
+                        mf[e] = m[j];
+                        vf[e] = v[j];
+                    }
+                }
             }
         }
     }
