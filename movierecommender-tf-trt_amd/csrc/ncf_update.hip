@@ -115,6 +115,16 @@ __device__ __forceinline__ void adam1(float& p, float& m, float& v, float g, flo
     p -= adam_term(lr_t, m, v, eps);
 }
 
+// adam1 with g = 0 (the deferred decay's replayed steps): c1 * 0 and c2 * (0 * 0) are +0 for the
+// finite c1, c2 of any valid beta, so b1*m + c1*g rounds like b1*m + 0 — bitwise adam1(..., 0, ...)
+// with three multiplies less per replayed step
+__device__ __forceinline__ void adam1_zero(float& p, float& m, float& v, float lr_t, float b1, float b2, float eps) {
+#pragma clang fp contract(off)
+    m = b1 * m + 0.0f;
+    v = b2 * v + 0.0f;
+    p -= adam_term(lr_t, m, v, eps);
+}
+
 // adam4's moment updates with g = 0: b1*m + c1*0 and b2*v + c2*0 round like b1*m + 0, b2*v + 0
 __device__ __forceinline__ void decay4(float4& m, float4& v, float b1, float b2) {
 #pragma clang fp contract(off)
@@ -316,7 +326,7 @@ __global__ __launch_bounds__(kBlock) void k_emb_catchup(float4* __restrict__ emb
                 const float lrt = t - st < kLrLut ? lut[t - st] : adam_lr_t(lr, b1, b2, st);
 #pragma unroll
                 for (int j = 0; j < kRep; ++j)
-                    if (st > sr[j]) adam1(p[j], m[j], v[j], 0.0f, lrt, b1, b2, eps);
+                    if (st > sr[j]) adam1_zero(p[j], m[j], v[j], lrt, b1, b2, eps);
             }
 #pragma unroll
             for (int j = 0; j < kRep; ++j) {
@@ -578,7 +588,7 @@ __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_tou
                     const float lrt = t - st < kLrLut ? lut[t - st] : adam_lr_t(lr, b1, b2, st);
 #pragma unroll
                     for (int j = 0; j < kRep; ++j)
-                        if (st > sr[j]) adam1(p[j], mm[j], vv[j], 0.0f, lrt, b1, b2, eps);
+                        if (st > sr[j]) adam1_zero(p[j], mm[j], vv[j], lrt, b1, b2, eps);
                 }
 #pragma unroll
                 for (int j = 0; j < kRep; ++j) {
