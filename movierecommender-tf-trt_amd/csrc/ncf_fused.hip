@@ -833,13 +833,44 @@ __global__ __launch_bounds__(kBlock, 2) void k_fwd_fused(const float* __restrict
     __shared__ float red[4];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const float eps = 1e-7f, hi_clip = 1.0f - eps;
-    for (int e = tid; e < S::L0 * L1; e += kBlock) wl[S::SW1 + (e / L1) * S::LW1 + e % L1] = mlp[S::OW1 + e];
-    for (int e = tid; e < L1 * L2; e += kBlock) wl[S::SW2 + (e / L2) * S::LW2 + e % L2] = mlp[S::OW2 + e];
-    for (int e = tid; e < L2 * L3; e += kBlock) wl[S::SW3 + (e / L3) * S::LW3 + e % L3] = mlp[S::OW3 + e];
-    for (int e = tid; e < L1; e += kBlock) wl[S::SB1 + e] = mlp[S::OB1 + e];
-    for (int e = tid; e < L2; e += kBlock) wl[S::SB2 + e] = mlp[S::OB2 + e];
-    for (int e = tid; e < L3; e += kBlock) wl[S::SB3 + e] = mlp[S::OB3 + e];
-    for (int e = tid; e < G + L3 + 1; e += kBlock) wl[S::SWO + e] = mlp[S::OWO + e];
+    // dense parameters -> LDS: every float4 group of the flat layout loaded first (one b128 buffer
+    // load each, all in flight together; every segment starts at a multiple of 4 floats), then
+    // stored element by element into the padded rows
+    static_assert(S::OB1 % 4 == 0 && S::OW2 % 4 == 0 && S::OB2 % 4 == 0 && S::OW3 % 4 == 0 && S::OB3 % 4 == 0 &&
+                      S::OWO % 4 == 0 && S::OBO % 4 == 0,
+                  "float4 parameter groups");
+    {
+        constexpr int NV4 = S::OBO / 4, NVT = (NV4 + kBlock - 1) / kBlock;
+        const __amdgpu_buffer_rsrc_t ml_rsrc =
+            __builtin_amdgcn_make_buffer_rsrc((void*)mlp, (short)0, (int)(S::P * 4), 0x00020000);
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        f4v pv[NVT];
+#pragma unroll
+        for (int j = 0; j < NVT; ++j) {
+            const int q = tid + kBlock * j;
+            pv[j] = __builtin_bit_cast(
+                f4v, __builtin_amdgcn_raw_buffer_load_b128(ml_rsrc, q < NV4 ? (uint32_t)q * 16u : 0x80000000u, 0, 0));
+        }
+        const float pbo = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ml_rsrc, (uint32_t)S::OBO * 4u, 0, 0));
+#pragma unroll
+        for (int j = 0; j < NVT; ++j) {
+            const int q = tid + kBlock * j;
+            if (q < NV4) {
+                const int e0 = 4 * q;
+                int d;  // LDS position of element e0 (its 3 successors follow it in the same row)
+                if (e0 < S::OB1) d = S::SW1 + (e0 / L1) * S::LW1 + e0 % L1;
+                else if (e0 < S::OW2) d = S::SB1 + (e0 - S::OB1);
+                else if (e0 < S::OB2) d = S::SW2 + ((e0 - S::OW2) / L2) * S::LW2 + (e0 - S::OW2) % L2;
+                else if (e0 < S::OW3) d = S::SB2 + (e0 - S::OB2);
+                else if (e0 < S::OB3) d = S::SW3 + ((e0 - S::OW3) / L3) * S::LW3 + (e0 - S::OW3) % L3;
+                else if (e0 < S::OWO) d = S::SB3 + (e0 - S::OB3);
+                else d = S::SWO + (e0 - S::OWO);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) wl[d + k] = pv[j][k];
+            }
+        }
+        if (tid == 0) wl[S::SWO + G + L3] = pbo;
+    }
     __syncthreads();
 
     float acc_bce = 0.f;
