@@ -49,6 +49,14 @@ def spans(fn_name):
     ends = [units[:, :, k + 1] if k + 1 < nu else s[:, :, 11] for k in range(nu)]
     out["unit_cyc"] = [round(float(np.mean(ends[k] - units[:, :, k])), 1) for k in range(nu)]
     out["epilogue_cyc"] = round(float(np.mean(s[:, :, 12] - s[:, :, 11])), 1)
+    # where the end skew comes from: loop-end times (realtime clock, us after the first entry) by
+    # XCD (workgroup i runs on XCD i % 8) and by wave slot, and their spread
+    loop_end_rt = rt0 + (s[:, :, 11] - s[:, :, 1]) / np.maximum((s[:, :, 12] - s[:, :, 1]) / np.maximum(rt1 - rt0, 1), 1e-9)
+    le = (loop_end_rt - rt0.min()) / 100.0
+    out["loop_end_us_by_xcd"] = [round(float(le[x::8].mean()), 2) for x in range(8)]
+    out["loop_end_us_by_wave"] = [round(float(le[:, w].mean()), 2) for w in range(4)]
+    out["loop_end_us_pct"] = {q: round(float(np.percentile(le, q)), 2) for q in (0, 10, 50, 90, 100)}
+    out["entry_us_by_xcd"] = [round(float(((rt0 - rt0.min()) / 100.0)[x::8].mean()), 2) for x in range(8)]
     out["epi_wait_first_barrier_cyc"] = round(float(np.mean(s[:, :, 14] - s[:, :, 11])), 1)
     out["epi_wg_loop_end_spread_cyc"] = round(float(np.mean(s[:, :, 11].max(axis=1) - s[:, :, 11].min(axis=1))), 1)
     out["epi_lds_sums_cyc"] = round(float(np.mean(s[:, :, 15] - s[:, :, 14])), 1)
