@@ -406,6 +406,9 @@ __global__ __launch_bounds__(256, 1) void k_fb_wave(const float* __restrict__ em
         ++itw;
         NCF_WT(itw, 0);
         const int64_t s0 = un * 16, sg = s0 + li, un1 = un + ustride;
+        int tu, tv;
+        float ty;
+        load_ids(un1 + ustride, tu, tv, ty);  // ids two units ahead, consumed at this unit's end
         const bool inb = sg < n;
         const bool ok = inb && (unsigned)cu < (unsigned)ids.ubound && (unsigned)cv < (unsigned)ids.ibound;
 
@@ -486,6 +489,12 @@ __global__ __launch_bounds__(256, 1) void k_fb_wave(const float* __restrict__ em
         // ---- output: this lane's 4 H3 features and GQ GMF dims, then the 4 lane groups
         float wg[GQA];
         float zp = 0.f;
+        if constexpr (G > 0) {
+            // the GMF slices are first used here: without this fence the compiler hoists their
+            // products next to the loads (issued after layer 1) and the unit waits for them there
+#pragma unroll
+            for (int e = 0; e < GQ; ++e) asm volatile("" : "+v"(gu[e]), "+v"(gi[e]));
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) zp += wo3[r] * h3[r];
         if constexpr (G > 0) {
@@ -734,8 +743,11 @@ __global__ __launch_bounds__(256, 1) void k_fb_wave(const float* __restrict__ em
                 ab3 += o.g3;
             });
 
+        // rotate the ids: the loop-carried registers take values loaded a whole unit ago (a load
+        // issued here and carried into the next iteration got copied between registers at once,
+        // a memory round trip per unit spent waiting)
         cu = nu, cv = nv, cy = ny;
-        load_ids(un1 + ustride, nu, nv, ny);
+        nu = tu, nv = tv, ny = ty;
         NCF_WT(itw, 7);
     }
 
