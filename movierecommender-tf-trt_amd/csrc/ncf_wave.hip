@@ -409,6 +409,7 @@ __global__ __launch_bounds__(256, 1) void k_fb_wave(const float* __restrict__ em
         int tu, tv;
         float ty;
         load_ids(un1 + ustride, tu, tv, ty);  // ids two units ahead, consumed at this unit's end
+        load_g(un, cu, cv);                    // this unit's GMF slices, first used by the output
         const bool inb = sg < n;
         const bool ok = inb && (unsigned)cu < (unsigned)ids.ubound && (unsigned)cv < (unsigned)ids.ibound;
 
@@ -426,10 +427,8 @@ __global__ __launch_bounds__(256, 1) void k_fb_wave(const float* __restrict__ em
 #pragma unroll
                 for (int t = 0; t < B1; ++t) h1[t] = mfma16(o.v[t], xr[q], h1[t]);
             });
-        // the next unit's MLP input into the registers layer 1 has consumed; this unit's GMF
-        // slices (first used by the output, after layers 2-3)
+        // the next unit's MLP input into the registers layer 1 has consumed
         if (un1 < nunits) load_x(un1, nu, nv);
-        load_g(un, cu, cv);
 #pragma unroll
         for (int t = 0; t < B1; ++t) {
             float b[4];
