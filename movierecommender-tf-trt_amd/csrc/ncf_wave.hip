@@ -427,8 +427,7 @@ __global__ __launch_bounds__(256, 1) void k_fb_wave(const float* __restrict__ em
 #pragma unroll
                 for (int t = 0; t < B1; ++t) h1[t] = mfma16(o.v[t], xr[q], h1[t]);
             });
-        // the next unit's MLP input into the registers layer 1 has consumed
-        if (un1 < nunits) load_x(un1, nu, nv);
+
 #pragma unroll
         for (int t = 0; t < B1; ++t) {
             float b[4];
@@ -494,6 +493,9 @@ __global__ __launch_bounds__(256, 1) void k_fb_wave(const float* __restrict__ em
 #pragma unroll
             for (int e = 0; e < GQ; ++e) asm volatile("" : "+v"(gu[e]), "+v"(gi[e]));
         }
+        // the next unit's MLP input into the registers layer 1 has consumed (issued after the
+        // fence above, whose wait covers every load before it)
+        if (un1 < nunits) load_x(un1, nu, nv);
 #pragma unroll
         for (int r = 0; r < 4; ++r) zp += wo3[r] * h3[r];
         if constexpr (G > 0) {
