@@ -211,7 +211,8 @@ __global__ __launch_bounds__(kBlock) void k_emb_update(float4* __restrict__ emb,
 #define NCF_CATCHUP_AHEAD 1
 #endif
 #ifndef NCF_AHEAD_REP
-#define NCF_AHEAD_REP 3   // catch-up-ahead replay items per wave with their loads in flight together (4 spills at 7 blocks/CU)
+#define NCF_AHEAD_REP 3   // replay items (rows / row slices) per wave with their loads in flight together, in the
+                          // catch-up-ahead blocks and the catch-up / flush kernel (4 spills at 7 blocks/CU)
 #endif
 constexpr int kRep = NCF_AHEAD_REP;
 #ifndef NCF_COUNT_PER_MAX
