@@ -125,6 +125,19 @@ __device__ __forceinline__ void adam1_zero(float& p, float& m, float& v, float l
     p -= adam_term(lr_t, m, v, eps);
 }
 
+// adam1_zero on two neighbouring elements: the multiplies and adds as packed fp32 (v_pk_mul_f32,
+// v_pk_add_f32: IEEE per component, so bitwise adam1_zero per element), half the VALU issue of the
+// moment updates and the step term's products in the replays
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void adam2_zero(f32x2& p, f32x2& m, f32x2& v, float lr_t, float b1, float b2, float eps) {
+#pragma clang fp contract(off)
+    m = m * b1 + 0.0f;
+    v = v * b2 + 0.0f;
+    const f32x2 r = {__builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(v.x) + eps),
+                     __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(v.y) + eps)};
+    p -= (m * lr_t) * r;
+}
+
 // adam4's moment updates with g = 0: b1*m + c1*0 and b2*v + c2*0 round like b1*m + 0, b2*v + 0
 __device__ __forceinline__ void decay4(float4& m, float4& v, float b1, float b2) {
 #pragma clang fp contract(off)
@@ -293,7 +306,8 @@ __global__ __launch_bounds__(kBlock) void k_emb_catchup(float4* __restrict__ emb
     // float4 form cuts that tail 4x (measured: the float4 form's time grew with the longest debt
     // while the total work stayed flat, tools/catchup_probe.py).
     const int W = 4 * (int)w4;
-    const int lanes_per_row = W < kBlock ? (W + 63) / 64 * 64 : kBlock;   // whole waves per row
+    const int W2 = W / 2;                                                   // element pairs per row
+    const int lanes_per_row = W2 < kBlock ? (W2 + 63) / 64 * 64 : kBlock;  // whole waves per row
     const int rpb = kBlock / lanes_per_row;                                // rows per block pass
     const int sub = threadIdx.x / lanes_per_row, q0 = threadIdx.x % lanes_per_row;
     float* embf = reinterpret_cast<float*>(emb);
@@ -311,32 +325,33 @@ __global__ __launch_bounds__(kBlock) void k_emb_catchup(float4* __restrict__ emb
             r[j] = i < n ? (ALL ? i : list[i]) : 0;
             sr[j] = i < n ? row_step[r[j]] : t;
         }
-        for (int q = q0; q < W; q += lanes_per_row) {
-            float p[kRep], m[kRep], v[kRep];
+        for (int q = q0; q < W2; q += lanes_per_row) {  // element pair q: elements 2q, 2q + 1
+            const f32x2 z2 = {0.f, 0.f};
+            f32x2 p[kRep], m[kRep], v[kRep];
             int smin = t;
 #pragma unroll
             for (int j = 0; j < kRep; ++j) {
-                const size_t e = (size_t)r[j] * W + q;
+                const size_t e = (size_t)r[j] * W + 2 * q;
                 const bool act = sr[j] < t;
-                p[j] = act ? embf[e] : 0.f;
-                m[j] = act ? mf[e] : 0.f;
-                v[j] = act ? vf[e] : 0.f;
+                p[j] = act ? *reinterpret_cast<const f32x2*>(embf + e) : z2;
+                m[j] = act ? *reinterpret_cast<const f32x2*>(mf + e) : z2;
+                v[j] = act ? *reinterpret_cast<const f32x2*>(vf + e) : z2;
                 smin = sr[j] < smin ? sr[j] : smin;
             }
             for (int st = smin + 1; st <= t; ++st) {
                 const float lrt = t - st < kLrLut ? lut[t - st] : adam_lr_t(lr, b1, b2, st);
 #pragma unroll
                 for (int j = 0; j < kRep; ++j)
-                    if (st > sr[j]) adam1_zero(p[j], m[j], v[j], lrt, b1, b2, eps);
+                    if (st > sr[j]) adam2_zero(p[j], m[j], v[j], lrt, b1, b2, eps);
             }
 #pragma unroll
             for (int j = 0; j < kRep; ++j) {
                 if (sr[j] < t) {
-                    const size_t e = (size_t)r[j] * W + q;
-                    embf[e] = p[j];
+                    const size_t e = (size_t)r[j] * W + 2 * q;
+                    *reinterpret_cast<f32x2*>(embf + e) = p[j];
                     if (ALL || !NCF_CATCHUP_P_ONLY) {
-                        mf[e] = m[j];
-                        vf[e] = v[j];
+                        *reinterpret_cast<f32x2*>(mf + e) = m[j];
+                        *reinterpret_cast<f32x2*>(vf + e) = v[j];
                     }
                 }
             }
@@ -560,43 +575,45 @@ __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_tou
                 if (lane == 0) ncl = __popcll(cm);
             }
             __syncthreads();
-            const int per_row = (W + 63) >> 6;
+            const int per_row = (W + 127) >> 7;
             const int items = ncl * per_row;
-            // item it = row it / per_row, elements (it % per_row) * 64 + lane; wave wv takes
-            // it = wv + 4 j (wave-uniform: the step loops do not diverge)
-            for (int i0 = wv; i0 < items; i0 += 4 * kRep) {
-                float p[kRep], mm[kRep], vv[kRep];
-                size_t e[kRep];
-                int sr[kRep];
-                bool act[kRep];
+            // item it = row it / per_row, elements (it % per_row) * 128 + 2 lane + {0, 1} (W is a
+            // multiple of 4); wave wv takes it = wv + 4 j (wave-uniform: the step loops do not diverge)
+            const f32x2 z2 = {0.f, 0.f};
+            constexpr int kRepC = 2;  // float2 items: two per wave keep the launch's 72-VGPR cap unspilled
+            for (int i0 = wv; i0 < items; i0 += 4 * kRepC) {
+                f32x2 p[kRepC], mm[kRepC], vv[kRepC];
+                size_t e[kRepC];
+                int sr[kRepC];
+                bool act[kRepC];
 #pragma unroll
-                for (int j = 0; j < kRep; ++j) {
+                for (int j = 0; j < kRepC; ++j) {
                     const int it = i0 + 4 * j;
                     const int k = it < items ? it / per_row : 0;
-                    const int q = (it - k * per_row) * 64 + lane;
+                    const int q = (it - k * per_row) * 128 + 2 * lane;
                     act[j] = it < items && q < W;
                     sr[j] = it < items ? cstep[k] : t;
                     e[j] = (size_t)crow[k] * W + (act[j] ? q : 0);
-                    p[j] = act[j] ? embf[e[j]] : 0.f;
-                    mm[j] = act[j] ? mf[e[j]] : 0.f;
-                    vv[j] = act[j] ? vf[e[j]] : 0.f;
+                    p[j] = act[j] ? *reinterpret_cast<const f32x2*>(embf + e[j]) : z2;
+                    mm[j] = act[j] ? *reinterpret_cast<const f32x2*>(mf + e[j]) : z2;
+                    vv[j] = act[j] ? *reinterpret_cast<const f32x2*>(vf + e[j]) : z2;
                 }
                 // the items' chains advance together (same per-element arithmetic, step by step)
                 int smin = t;
 #pragma unroll
-                for (int j = 0; j < kRep; ++j) smin = sr[j] < smin ? sr[j] : smin;
+                for (int j = 0; j < kRepC; ++j) smin = sr[j] < smin ? sr[j] : smin;
                 for (int st = smin + 1; st <= t; ++st) {
                     const float lrt = t - st < kLrLut ? lut[t - st] : adam_lr_t(lr, b1, b2, st);
 #pragma unroll
-                    for (int j = 0; j < kRep; ++j)
-                        if (st > sr[j]) adam1_zero(p[j], mm[j], vv[j], lrt, b1, b2, eps);
+                    for (int j = 0; j < kRepC; ++j)
+                        if (st > sr[j]) adam2_zero(p[j], mm[j], vv[j], lrt, b1, b2, eps);
                 }
 #pragma unroll
-                for (int j = 0; j < kRep; ++j) {
+                for (int j = 0; j < kRepC; ++j) {
                     if (act[j]) {
-                        embf[e[j]] = p[j];
-                        mf[e[j]] = mm[j];
-                        vf[e[j]] = vv[j];
+                        *reinterpret_cast<f32x2*>(embf + e[j]) = p[j];
+                        *reinterpret_cast<f32x2*>(mf + e[j]) = mm[j];
+                        *reinterpret_cast<f32x2*>(vf + e[j]) = vv[j];
                     }
                 }
             }
@@ -1027,8 +1044,8 @@ hipError_t launch_emb_catchup(const ncf_shape_t& s, const WsLayout& L, void* ws,
     }
 #if NCF_CATCHUP_SCALAR
     auto cgrid = [&](int64_t rows, int64_t cap) {
-        const int W = 4 * (int)w4;
-        const int64_t lanes = W < kBlock ? (W + 63) / 64 * 64 : kBlock;
+        const int W2 = 2 * (int)w4;  // element pairs per row (one per lane)
+        const int64_t lanes = W2 < kBlock ? (W2 + 63) / 64 * 64 : kBlock;
         const int64_t rpb = kBlock / lanes;
         int64_t g = (rows + rpb - 1) / rpb;
         return (unsigned)(g < 1 ? 1 : (g > cap ? cap : g));
