@@ -384,6 +384,14 @@ def launch_ranks(nproc):
     return its exit status.  The ranks' stdout is this process's stdout: rank 0 prints the one
     JSON line, the others print nothing there."""
     import subprocess
+    pre = os.environ.get("LD_PRELOAD", "")
+    if os.environ.get("ROCP_TOOL_LIBRARIES") or os.environ.get("ROCPROF_PRELOAD") or "rocprof" in pre:
+        # under rocprofv3 the profiler's preloaded library has initialised the GPU in this process:
+        # starting the launcher from here would be the forbidden exec of a GPU-initialised process
+        sys.stderr.write("bench.py --gpus %d: refusing to launch ranks under a profiler; profile one rank per "
+                         "process instead (an outer torch.distributed.run with rocprofv3 -- python bench.py per "
+                         "rank)\n" % nproc)
+        return 2
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
     env = dict(os.environ)
@@ -604,10 +612,12 @@ def main():
     achieved = nbytes / (kern_ms * 1e-3) / 1e9
 
     # HR@10 on a synthetic validation set (1 positive + 99 sampled items per user), per rank
-    ev_users = 2000
+    # evaluation users drawn inside the table (user mode: this rank's own users, as local ids;
+    # config A's table has 943 users, so at most that many distinct ones)
+    ev_table = eng.num_users if mode == "user" else cfg["num_users"]
+    ev_users = min(2000, ev_table)
     eval_ms = None
-    ev_base = 0 if mode == "user" else rank * ev_users   # user mode: this rank's own (local) users
-    ev_u = (torch.arange(ev_users, device="cuda", dtype=torch.int32) + ev_base).repeat_interleave(100)
+    ev_u = torch.randperm(ev_table, generator=gen, device="cuda")[:ev_users].to(torch.int32).repeat_interleave(100)
     ev_i = torch.randint(0, cfg["num_items"], (ev_users * 100,), generator=gen, device="cuda", dtype=torch.int32)
     ev_y = torch.tensor([0.0] * 99 + [1.0], device="cuda").repeat(ev_users)
     if mode == "sharded":

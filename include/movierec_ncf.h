@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define NCF_ABI_VERSION 6
+#define NCF_ABI_VERSION 7
 #define NCF_MAX_LAYERS 8
 #define NCF_EINVAL (-1)
 #define NCF_EHIP (-2)
@@ -169,22 +169,32 @@ int ncf_workspace_init(const ncf_shape_t* shape, int64_t max_batch, void* ws, si
  *   NCF_WSERR_STALE_COUNT  a batch passed with hyper->index_ready = 2 differed from the ids
  *                          ncf_train_step_ahead counted (their contents changed in between): the
  *                          index build wrote no slot outside its keys' ranges and cleared the
- *                          counters, but that step's embedding gradient is wrong.
+ *                          counters, and the step replayed the deferred decay of the rows it read
+ *                          that the counted set missed (the table stays in the dense-sweep state),
+ *                          but that step's embedding gradient is wrong.
  *   NCF_WSERR_FOLD         an index built by an earlier call (ncf_build_index, ncf_shard_plan)
  *                          folds user rows differently than the step that used it (their hypers'
  *                          group / force_generic differ): that step's embedding gradient is wrong.
- * Nothing else in the library synchronises on them.
+ * Nothing else in the library synchronises on them.  ncf_shard_workspace_flags reads the flags of
+ * a row-sharded workspace (its layout depends on world).
  *
- * User-row folding: when the fused kernel runs and hyper->group is a power of two <= 32, the
- * user-row gradients of a group's samples that share the group head's user (the reference's
- * batches: one positive + negs per user, data_pipeline.py:141) are summed inside the kernel and
- * written once; the index lists that one contribution.  Any batch stays exact (a sample with
- * another user keeps its own row); only the fp32 summation order of those rows changes. */
+ * User-row folding: when the fused kernel runs and hyper->group is 2, 4 or 8, the user-row
+ * gradients of a group's samples that share the group head's user (the reference's batches: one
+ * positive + negs per user, data_pipeline.py:141) are summed inside the kernel and written once;
+ * the index lists that one contribution.  Any batch stays exact (a sample with another user keeps
+ * its own row); only the fp32 summation order of those rows changes. */
 #define NCF_WSERR_ID_RANGE 1
 #define NCF_WSERR_STALE_COUNT 4
 #define NCF_WSERR_FOLD 8
 int ncf_workspace_flags(const ncf_shape_t* shape, int64_t max_batch, void* ws, size_t ws_bytes, int32_t* flags,
                         void* stream);
+int ncf_shard_workspace_flags(const ncf_shape_t* shape, int64_t max_batch, int32_t world, void* ws, size_t ws_bytes,
+                              int32_t* flags, void* stream);
+/* Drop the next batch's index counts that ncf_train_step_ahead took (the batch will not be
+ * passed after all): clears the index counters only — the sticky error flags and the fold of the
+ * last index build stay (ncf_workspace_init would clear them too). */
+int ncf_workspace_discard_counts(const ncf_shape_t* shape, int64_t max_batch, void* ws, size_t ws_bytes,
+                                 void* stream);
 
 /* Forward only: probs[n] = sigmoid output for (users[i], items[i]).
  * Replaces Model.predict_on_batch output[0] (model.py:184-194). */

@@ -386,6 +386,28 @@ int ncf_workspace_flags(const ncf_shape_t* s, int64_t max_batch, void* ws, size_
     return hip_check(hipMemsetAsync(ncf::at<int32_t>(ws, L.err), 0, 4, st), "flags clear");
 }
 
+int ncf_shard_workspace_flags(const ncf_shape_t* s, int64_t max_batch, int32_t world, void* ws, size_t ws_bytes,
+                              int32_t* flags, void* stream) {
+    if (int r = check_shape(s)) return r;
+    if (int r = check_world(world)) return r;
+    if (!flags) return fail(NCF_EINVAL, "flags is NULL");
+    ncf::WsLayout L = ncf::make_layout(*s, max_batch, world);
+    if (!ws || ws_bytes < L.total) return fail(NCF_EINVAL, "workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    if (hipError_t e = hipMemcpyAsync(flags, ncf::at<int32_t>(ws, L.err), 4, hipMemcpyDeviceToDevice, st))
+        return hip_check(e, "flags copy");
+    return hip_check(hipMemsetAsync(ncf::at<int32_t>(ws, L.err), 0, 4, st), "flags clear");
+}
+
+int ncf_workspace_discard_counts(const ncf_shape_t* s, int64_t max_batch, void* ws, size_t ws_bytes, void* stream) {
+    if (int r = check_shape(s)) return r;
+    ncf::WsLayout L = ncf::make_layout(*s, max_batch);
+    if (!ws || ws_bytes < L.total) return fail(NCF_EINVAL, "workspace too small");
+    // the index counters only: the sticky error flags and the last build's fold stay
+    return hip_check(hipMemsetAsync(ncf::at<int32_t>(ws, L.cnt), 0, (size_t)(L.keys + 1) * 4, (hipStream_t)stream),
+                     "counter clear");
+}
+
 int ncf_predict(const ncf_shape_t* s, const ncf_model_t* model, const int32_t* users, const int32_t* items,
                 int64_t n, float* probs, void* ws, size_t ws_bytes, void* stream) {
     if (int r = check_shape(s)) return r;
@@ -431,14 +453,17 @@ struct CatchupCtx {
     void* ws;
     hipStream_t st;
     int64_t n;  // batch size (the catch-up launch also sorts the index lists)
+    const int32_t* users;
+    const int32_t* items;
 };
 static int catchup_touched(void* p) {
     const CatchupCtx& c = *static_cast<CatchupCtx*>(p);
     prof_begin(NCF_K_CATCHUP, c.st);
     // counted ahead (index_ready == 2): the previous step's update launch also caught these rows up
+    // (if the ids changed since, the launch's gate blocks replay the rows the counted set missed)
     hipError_t e = ncf::launch_emb_catchup(*c.s, *c.L, c.ws, c.model->emb, c.optim->emb_m, c.optim->emb_v,
                                            c.optim->row_step, c.optim->step, *c.h, false, c.st, true, c.n,
-                                           c.h->index_ready == 2);
+                                           c.h->index_ready == 2, c.users, c.items);
     prof_end(NCF_K_CATCHUP, c.st);
     return hip_check(e, "touched-row catch-up");
 }
@@ -566,7 +591,7 @@ static int train_step_impl(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t
     const bool lazy = optim->row_step != nullptr;
     if (lazy && h->l2[0] != 0.0f)
         return fail(NCF_EINVAL, "deferred decay (row_step) needs the embedding L2 off: the loss sums the whole table");
-    CatchupCtx cc{s, &L, model, optim, h, ws, st, n};
+    CatchupCtx cc{s, &L, model, optim, h, ws, st, n, users, items};
     if (int r = run_fb(*s, L, model, h, users, items, labels, n, ws, probs_out, &fb, st, false,
                        lazy ? catchup_touched : nullptr, &cc))
         return r;

@@ -377,10 +377,13 @@ hipError_t launch_emb_update(const ncf_shape_t& s, const WsLayout& L, void* ws, 
 // sort_lists (touched rows only): extra blocks of the same launch run k_sort over the index the
 // build left unsorted (launch_index_build(..., skip_sort = true)), for batch size n
 // rows_current: the batch's rows were caught up ahead by the previous step's update launch
-// (launch_emb_update_touched with next ids): only the sort blocks run
+// (launch_emb_update_touched with next ids): only the sort blocks run, plus gate blocks that —
+// only if the index fill flagged kErrStaleCount — fully replay the rows of users/items (the ids
+// actually passed, n samples) the counted set missed
 hipError_t launch_emb_catchup(const ncf_shape_t& s, const WsLayout& L, void* ws, float* emb, float* m, float* v,
-                              const int32_t* row_step, const int32_t* step, const ncf_hyper_t& h, bool all_rows,
-                              hipStream_t st, bool sort_lists = false, int64_t n = 0, bool rows_current = false);
+                              int32_t* row_step, const int32_t* step, const ncf_hyper_t& h, bool all_rows,
+                              hipStream_t st, bool sort_lists = false, int64_t n = 0, bool rows_current = false,
+                              const int32_t* users = nullptr, const int32_t* items = nullptr);
 hipError_t launch_row_step_fill(int32_t* row_step, int64_t R, const int32_t* step, hipStream_t st);
 // next_users/next_items (optional, n_next samples): extra blocks of the same launch count the NEXT
 // batch's contributions into the index counters (the next build skips its k_count) and replay the

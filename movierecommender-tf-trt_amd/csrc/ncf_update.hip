@@ -279,18 +279,89 @@ struct SortAhead {
     int32_t* err;
 };
 
+// A batch whose rows the previous step caught up ahead (counted ahead, index_ready == 2) needs no
+// replay — unless its ids changed after they were counted (NCF_WSERR_STALE_COUNT, raised by the
+// index fill before this launch).  Then the rows of the ids actually passed that the counted set
+// missed are not in the touched list, yet the forward pass reads them: the gate blocks replay
+// every such row fully (p, m, v to step t, row_step = t, claimed by CAS so a row repeated in the
+// batch replays once; rows already current are skipped), so the table stays exactly the dense
+// sweep's state (that step's embedding gradient is still wrong, as the flag reports).  Without the
+// flag the gate blocks return at once.
+struct StaleGate {
+    const int32_t* users;      // nullptr: no gate blocks
+    const int32_t* items;
+    int64_t m;                 // 2 * batch contributions
+    int32_t U, I;
+    int32_t* row_step;
+};
+
+__device__ __forceinline__ void stale_replay_body(float* __restrict__ embf, float* __restrict__ mf,
+                                               float* __restrict__ vf, int W, const StaleGate& sg, int t, float lr,
+                                               float b1, float b2, float eps, const int32_t* __restrict__ err,
+                                               int blk, int nblk) {
+    if (!(__atomic_load_n(err, __ATOMIC_RELAXED) & kErrStaleCount)) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (int64_t)blk * (kBlock / 64) + (threadIdx.x >> 6);
+    const int64_t nw = (int64_t)nblk * (kBlock / 64);
+    for (int64_t c0 = wave * 64; c0 < sg.m; c0 += nw * 64) {
+        const int64_t c = c0 + lane;
+        int key = -1;
+        if (c < sg.m) {
+            const int64_t i = c >> 1;
+            const int id = (c & 1) ? sg.items[i] : sg.users[i];
+            if ((unsigned)id < (unsigned)((c & 1) ? sg.I : sg.U)) key = (c & 1) ? sg.U + id : id;
+        }
+        bool claim = false;
+        int s0 = t;
+        if (key >= 0) {
+            int sv = sg.row_step[key];
+            while (sv < t) {
+                const int prev = atomicCAS(&sg.row_step[key], sv, t);
+                if (prev == sv) {
+                    claim = true;
+                    s0 = sv;
+                    break;
+                }
+                sv = prev;
+            }
+        }
+        uint64_t cm = __ballot(claim);
+        while (cm) {  // the wave replays its claimed rows one after another, two elements per lane
+            const int src = __ffsll((unsigned long long)cm) - 1;
+            cm &= cm - 1;
+            const int r = __shfl(key, src, 64);
+            const int s = __shfl(s0, src, 64);
+            for (int q = lane; 2 * q < W; q += 64) {
+                const size_t e = (size_t)r * W + 2 * q;
+                f32x2 p = *reinterpret_cast<const f32x2*>(embf + e);
+                f32x2 m = *reinterpret_cast<const f32x2*>(mf + e);
+                f32x2 v = *reinterpret_cast<const f32x2*>(vf + e);
+                for (int st = s + 1; st <= t; ++st) adam2_zero(p, m, v, adam_lr_t(lr, b1, b2, st), b1, b2, eps);
+                *reinterpret_cast<f32x2*>(embf + e) = p;
+                *reinterpret_cast<f32x2*>(mf + e) = m;
+                *reinterpret_cast<f32x2*>(vf + e) = v;
+            }
+        }
+    }
+}
+
 template <bool ALL>
-__global__ __launch_bounds__(kBlock) void k_emb_catchup(float4* __restrict__ emb, float4* __restrict__ m4,
+__device__ __forceinline__ void catchup_body(float4* __restrict__ emb, float4* __restrict__ m4,
                                                         float4* __restrict__ v4, uint32_t w4,
                                                         const int32_t* __restrict__ list,
                                                         const int32_t* __restrict__ nlist, int64_t R,
                                                         const int32_t* __restrict__ row_step,
                                                         const int32_t* __restrict__ step, float lr, float b1,
-                                                        float b2, float eps, SortAhead so) {
+                                                        float b2, float eps, SortAhead so, StaleGate sg) {
     if (!ALL && (int)blockIdx.x >= so.ncatch) {
         // the contribution lists of this step's index, sorted while the rows replay (k_sort's work;
         // only the touched-row update after the forward pass reads them)
         sort_rows_body(so.offs, so.keys, so.list, so.nwords, (int)blockIdx.x - so.ncatch, so.cnt, so.err);
+        return;
+    }
+    if (!ALL && sg.users) {
+        stale_replay_body(reinterpret_cast<float*>(emb), reinterpret_cast<float*>(m4), reinterpret_cast<float*>(v4),
+                          4 * (int)w4, sg, *step, lr, b1, b2, eps, so.err, (int)blockIdx.x, so.ncatch);
         return;
     }
     __shared__ float lut[kLrLut];
@@ -382,6 +453,29 @@ __global__ __launch_bounds__(kBlock) void k_emb_catchup(float4* __restrict__ emb
         }
     }
 #endif
+}
+
+// ncf_lazy_flush: every row
+__global__ __launch_bounds__(kBlock) void k_emb_flush(float4* __restrict__ emb, float4* __restrict__ m4,
+                                                      float4* __restrict__ v4, uint32_t w4, int64_t R,
+                                                      const int32_t* __restrict__ row_step,
+                                                      const int32_t* __restrict__ step, float lr, float b1, float b2,
+                                                      float eps) {
+    const SortAhead so{0, nullptr, 0, nullptr, 0, nullptr, nullptr};
+    const StaleGate sg{nullptr, nullptr, 0, 0, 0, nullptr};
+    catchup_body<true>(emb, m4, v4, w4, nullptr, nullptr, R, row_step, step, lr, b1, b2, eps, so, sg);
+}
+
+// the batch's touched rows (+ the index sort, + the stale-count gate): capped at 64 VGPRs, the
+// 8 waves per SIMD of the latency-bound replay chains (the gate path spills a little instead)
+__global__ __launch_bounds__(kBlock, 8) void k_emb_catchup(float4* __restrict__ emb, float4* __restrict__ m4,
+                                                           float4* __restrict__ v4, uint32_t w4,
+                                                           const int32_t* __restrict__ list,
+                                                           const int32_t* __restrict__ nlist, int64_t R,
+                                                           const int32_t* __restrict__ row_step,
+                                                           const int32_t* __restrict__ step, float lr, float b1,
+                                                           float b2, float eps, SortAhead so, StaleGate sg) {
+    catchup_body<false>(emb, m4, v4, w4, list, nlist, R, row_step, step, lr, b1, b2, eps, so, sg);
 }
 
 // row_step[r] = *step for every row (after a flush: the replay kernel above only reads row_step)
@@ -644,7 +738,7 @@ __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_tou
                 const size_t e = (size_t)r * w4 + q;
                 // the row's state does not depend on the gradient chain: its loads go out first
                 float4 p = emb[e], m = m4[e], v = v4[e];
-                // k_emb_catchup<false> brought p up to step t-1 and left m, v at row_step: the same
+                // k_emb_catchup brought p up to step t-1 and left m, v at row_step: the same
                 // per-step decay adam4 applies with g = 0 (b1*m + 0, b2*v + 0), bitwise
                 for (int j = 0; j < k; ++j) decay4(m, v, b1, b2);
                 // contributions summed in ascending order; four gradient rows in flight at a time
@@ -1009,12 +1103,14 @@ static unsigned row_grid(int64_t rows, uint32_t w4, int64_t cap) {
 }
 
 hipError_t launch_emb_catchup(const ncf_shape_t& s, const WsLayout& L, void* ws, float* emb, float* m, float* v,
-                              const int32_t* row_step, const int32_t* step, const ncf_hyper_t& h, bool all_rows,
-                              hipStream_t st, bool sort_lists, int64_t n, bool rows_current) {
+                              int32_t* row_step, const int32_t* step, const ncf_hyper_t& h, bool all_rows,
+                              hipStream_t st, bool sort_lists, int64_t n, bool rows_current, const int32_t* users,
+                              const int32_t* items) {
     const uint32_t w4 = (uint32_t)(s.row_width / 4);
     const int64_t R = s.num_rows;
     const int64_t nmax = R < 2 * L.max_batch ? R : 2 * L.max_batch;
-    SortAhead so{0, nullptr, 0, nullptr, 0, nullptr, nullptr};
+    SortAhead so{0, nullptr, 0, nullptr, 0, nullptr, at<int32_t>(ws, L.err)};
+    const StaleGate nogate{nullptr, nullptr, 0, 0, 0, nullptr};
     unsigned nsort = 0;
     size_t lds = 0;
     if (sort_lists && !all_rows) {
@@ -1024,7 +1120,7 @@ hipError_t launch_emb_catchup(const ncf_shape_t& s, const WsLayout& L, void* ws,
         lds = (size_t)so.nwords * 4;
         static bool lds_cfg = false;
         if (!lds_cfg && lds > 65536) {
-            hipError_t e = hipFuncSetAttribute((const void*)k_emb_catchup<false>,
+            hipError_t e = hipFuncSetAttribute((const void*)k_emb_catchup,
                                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                                (int)((kMaxBatch * 2 / 32) * 4));
             if (e != hipSuccess) return e;
@@ -1033,12 +1129,19 @@ hipError_t launch_emb_catchup(const ncf_shape_t& s, const WsLayout& L, void* ws,
     }
     // rows_current: the previous step's update launch caught this batch's rows up ahead
     if (h.optimizer != NCF_OPT_ADAM || (rows_current && NCF_CATCHUP_AHEAD)) {
-        // SGD (an untouched row does not move) or rows already current: only the sort remains
-        if (nsort) {
-            so.ncatch = 0;
-            launch(k_emb_catchup<false>, nsort, kBlock, lds, st, (float4*)emb, (float4*)m, (float4*)v, w4,
-                   at<const int32_t>(ws, L.touched), at<const int32_t>(ws, L.nuniq), R, row_step, step, h.lr,
-                   h.beta_1, h.beta_2, h.epsilon, so);
+        // SGD (an untouched row does not move) or rows already current: only the sort remains,
+        // plus (Adam, rows current) the stale-count gate blocks
+        StaleGate sg = nogate;
+        unsigned ngate = 0;
+        if (h.optimizer == NCF_OPT_ADAM && users && items && n > 0) {
+            sg = StaleGate{users, items, 2 * n, s.num_users, s.num_items, row_step};
+            ngate = 64;
+        }
+        if (nsort + ngate) {
+            so.ncatch = (int)ngate;
+            launch(k_emb_catchup, ngate + nsort, kBlock, lds, st, (float4*)emb, (float4*)m, (float4*)v, w4,
+                   at<const int32_t>(ws, L.touched), at<const int32_t>(ws, L.nuniq), R, (const int32_t*)row_step,
+                   step, h.lr, h.beta_1, h.beta_2, h.epsilon, so, sg);
         }
         return hipGetLastError();
     }
@@ -1054,15 +1157,14 @@ hipError_t launch_emb_catchup(const ncf_shape_t& s, const WsLayout& L, void* ws,
     auto cgrid = [&](int64_t rows, int64_t cap) { return row_grid(rows, w4, cap); };
 #endif
     if (all_rows) {
-        launch(k_emb_catchup<true>, cgrid(R, 8192), kBlock, 0, st, (float4*)emb, (float4*)m, (float4*)v, w4,
-               (const int32_t*)nullptr, (const int32_t*)nullptr, R, row_step, step, h.lr, h.beta_1, h.beta_2,
-               h.epsilon, so);
+        launch(k_emb_flush, cgrid(R, 8192), kBlock, 0, st, (float4*)emb, (float4*)m, (float4*)v, w4, R,
+               (const int32_t*)row_step, step, h.lr, h.beta_1, h.beta_2, h.epsilon);
     } else {
         const unsigned ncatch = cgrid(nmax, NCF_CATCHUP_GRID_MAX);
         so.ncatch = (int)ncatch;
-        launch(k_emb_catchup<false>, ncatch + nsort, kBlock, lds, st, (float4*)emb, (float4*)m, (float4*)v, w4,
-               at<const int32_t>(ws, L.touched), at<const int32_t>(ws, L.nuniq), R, row_step, step, h.lr, h.beta_1,
-               h.beta_2, h.epsilon, so);
+        launch(k_emb_catchup, ncatch + nsort, kBlock, lds, st, (float4*)emb, (float4*)m, (float4*)v, w4,
+               at<const int32_t>(ws, L.touched), at<const int32_t>(ws, L.nuniq), R, (const int32_t*)row_step, step,
+               h.lr, h.beta_1, h.beta_2, h.epsilon, so, nogate);
     }
     return hipGetLastError();
 }

@@ -72,6 +72,8 @@ _SIGNATURES = {
     "ncf_workspace_size": (ctypes.c_int, [_P(NcfShape), _i64, _P(ctypes.c_size_t)]),
     "ncf_workspace_init": (ctypes.c_int, [_P(NcfShape), _i64, _vp, ctypes.c_size_t, _vp]),
     "ncf_workspace_flags": (ctypes.c_int, [_P(NcfShape), _i64, _vp, ctypes.c_size_t, _vp, _vp]),
+    "ncf_shard_workspace_flags": (ctypes.c_int, [_P(NcfShape), _i64, _i32, _vp, ctypes.c_size_t, _vp, _vp]),
+    "ncf_workspace_discard_counts": (ctypes.c_int, [_P(NcfShape), _i64, _vp, ctypes.c_size_t, _vp]),
     "ncf_predict": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _vp, _vp, _i64, _vp, _vp, ctypes.c_size_t, _vp]),
     "ncf_rank": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp]),
     "ncf_group_metrics": (ctypes.c_int, [_vp, _vp, _i64, _i32, _i32, _vp, _vp, _vp]),
@@ -140,7 +142,7 @@ def profile_read(kernel):
     return ms.value, n.value
 
 _lib = None
-ABI_VERSION = 6   # include/movierec_ncf.h ncf_abi_version()
+ABI_VERSION = 7   # include/movierec_ncf.h ncf_abi_version()
 
 
 def lib():

@@ -221,16 +221,30 @@ def split_leave_two_out(ratings_df):
 
 def load_ratings_train_test_sets(dataset_name, data_dir, download=True, remap_items=None):
     """Reference ``data_pipeline.py:157-200``.  ``remap_items`` (new, default: ml-20m only) gives
-    the items dense ids before the split (DESIGN deviation 5): the order of the
-    dataset's movies file when it is present (ml-20m's 27,278 movies), else ascending raw id.
-    Without it ml-20m's raw movieIds (up to 131,262) fall outside the 27,278-row item table."""
+    the items dense ids before the split (DESIGN deviation 5).  One deterministic
+    mapping: the item's position in the dataset's movies file (ml-20m's ``movies.csv``: 27,278
+    movies, ascending movieId), which ships in every MovieLens zip; a missing movies file raises
+    FileNotFoundError rather than falling back to another numbering.  ``remap_items="ratings"``
+    asks for ascending rated ids instead (files without a movies list).  Without a remap ml-20m's
+    raw movieIds (up to 131,262) fall outside the 27,278-row item table.  The raw (0-based) id of
+    every dense id is kept in ``df.attrs["raw_item_ids"]`` of the three frames, so predictions can
+    be mapped back to movieIds and titles (``trainer.train`` saves it next to the model)."""
     _check_dataset_name(dataset_name)
     ratings_df = load_ratings_data(data_dir, dataset_name, COL_USER_ID, COL_ITEM_ID, COL_RATING, download)
     if remap_items is None:
         remap_items = dataset_name == ml.ML_20M
+    raw = None
     if remap_items:
         movies_df = None
-        if os.path.exists(ml.get_movies_path(data_dir, dataset_name)):
+        if remap_items != "ratings":
+            path = ml.get_movies_path(data_dir, dataset_name)
+            if not os.path.exists(path):
+                raise FileNotFoundError("{} is needed to number {}'s items (or pass remap_items='ratings')"
+                                        .format(path, dataset_name))
             movies_df = ml.load_movies_data(data_dir, dataset_name, COL_ITEM_ID, download=False)
-        ratings_df, _raw = ml.remap_item_ids(ratings_df, COL_ITEM_ID, movies_df)
-    return split_leave_two_out(ratings_df)
+        ratings_df, raw = ml.remap_item_ids(ratings_df, COL_ITEM_ID, movies_df)
+    frames = split_leave_two_out(ratings_df)
+    if raw is not None:
+        for f in frames:
+            f.attrs["raw_item_ids"] = np.asarray(raw)
+    return frames

@@ -40,6 +40,17 @@ def _same_ids(held, u, i, n, group):
             hu._version == vu and hi._version == vi and hg == group)
 
 
+def raise_ws_flags(f):
+    """Raise for the sticky workspace flags ``f`` (ncf_workspace_flags / ncf_shard_workspace_flags)."""
+    if f & N.NCF_WSERR_FOLD:
+        raise RuntimeError("an index built ahead (build_index / plan) used another sample group than the step")
+    if f & N.NCF_WSERR_STALE_COUNT:
+        raise RuntimeError("a batch counted ahead (train_step next_batch=) changed its ids before its step: "
+                           "that step's embedding update used a stale index")
+    if f & N.NCF_WSERR_ID_RANGE:
+        raise ValueError("an id outside the embedding table reached the device (those samples were masked)")
+
+
 class NCFEngine(object):
     """Model + optimizer state of one replica on one device."""
 
@@ -288,21 +299,15 @@ class NCFEngine(object):
         flags = torch.zeros(1, dtype=torch.int32, device=self.device)
         N.check(N.lib().ncf_workspace_flags(ctypes.byref(self.shape), self.max_batch, N.ptr(self.ws), self.ws_bytes,
                                             N.ptr(flags), N.stream_handle(self.device)))
-        f = int(flags.item())
-        if f & N.NCF_WSERR_FOLD:
-            raise RuntimeError("an index built ahead (build_index / plan) used another sample group than the step")
-        if f & N.NCF_WSERR_STALE_COUNT:
-            raise RuntimeError("a batch counted ahead (train_step next_batch=) changed its ids before its step: "
-                               "that step's embedding update used a stale index")
-        if f & N.NCF_WSERR_ID_RANGE:
-            raise ValueError("an id outside the embedding table reached the device (those samples were masked)")
+        raise_ws_flags(int(flags.item()))
 
     def _discard_counted(self):
         """Clear the index counters holding a next batch's counts (ncf_train_step_ahead) before any
         other index build uses them."""
         if self._counted is not None:
-            N.check(N.lib().ncf_workspace_init(ctypes.byref(self.shape), self.max_batch, N.ptr(self.ws),
-                                               self.ws_bytes, N.stream_handle(self.device)))
+            # counters only: the sticky error flags stay for check_errors
+            N.check(N.lib().ncf_workspace_discard_counts(ctypes.byref(self.shape), self.max_batch, N.ptr(self.ws),
+                                                         self.ws_bytes, N.stream_handle(self.device)))
             self._counted = None
 
     def evaluate(self, users, items, labels, group, k, stats=None, probs_out=None):

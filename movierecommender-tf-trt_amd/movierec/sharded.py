@@ -117,6 +117,16 @@ class ShardedNCFEngine(object):
         self.recv_grad = torch.zeros(recv_cap, W, dtype=torch.float32, device=dev)
         self.max_batch = int(n)
 
+    def check_errors(self):
+        """Raise for the workspace's sticky flags (an id outside the table, a plan whose fold
+        differs from the step that used it); synchronises the stream."""
+        from .engine import raise_ws_flags
+        flags = torch.zeros(1, dtype=torch.int32, device=self.device)
+        N.check(N.lib().ncf_shard_workspace_flags(ctypes.byref(self.shape), self.max_batch, self.world,
+                                                  N.ptr(self.ws), self.ws_bytes, N.ptr(flags),
+                                                  N.stream_handle(self.device)))
+        raise_ws_flags(int(flags.item()))
+
     # --------------------------------------------------- weights marshalling
     def owned_rows(self):
         """Global table rows of this shard's local rows (-1 for padding rows)."""

@@ -53,11 +53,11 @@ def train(model_name, dataset_name, data_dir, output_dir, params=DEFAULT_PARAMS,
 def main(argv=None):
     import argparse
     parser = argparse.ArgumentParser(description="Train a movie recommendation (NCF/NeuMF) model on MI355X.")
-    parser.add_argument("-m", "--model-name", type=str, required=True, help="Model name (to save output files).")
+    parser.add_argument("-m", "--model-name", type=str, required=True, help="Name given to the saved weights, params and checkpoint files.")
     parser.add_argument("-n", "--dataset-name", type=str, required=True, help="Movielens dataset name.")
     parser.add_argument("-d", "--data-dir", type=str, default="data/", help="Dataset directory to read ratings from")
-    parser.add_argument("-o", "--output-dir", type=str, default="models", help="Output dir to save model files.")
-    parser.add_argument("-l", "--log-level", type=str, default="INFO", help="Log level (default: INFO).")
+    parser.add_argument("-o", "--output-dir", type=str, default="models", help="Directory the trained model files are written to.")
+    parser.add_argument("-l", "--log-level", type=str, default="INFO", help="Python logging level name, e.g. DEBUG, INFO (the default) or WARNING.")
     parser.add_argument("--gmf-dim", type=int, default=0, help="NeuMF GMF branch width (0 = MLP-only model).")
     parser.add_argument("--epochs", type=int, default=None)
     parser.add_argument("--seed", type=int, default=None)

@@ -1,0 +1,207 @@
+"""BASELINE config D at its real size: 10,000,000 users x 1,000,000 items, NeuMF gmf 128 + MLP
+[256, 128, 64, 32] (reference ``movierec/model.py:154-215`` plus the GMF branch), one GPU.
+
+The combined table has 11,000,000 rows of 256 floats (2.8 G floats, 11.3 GB; with the Adam moments
+34 GB): element offsets past 2^31 are reached by every item row and by users from 8,388,608 on,
+so this test is what proves no 32-bit element offset survives on the path the bench runs
+(deferred-decay Adam, the next batch counted ahead, the layer-by-layer forward/backward).
+
+The oracle cannot hold 11 M rows in float64, and does not need to: under Keras' dense Adam (F5) a
+row only interacts with the others through the batches that read it.  A row no batch touches has
+g = 0 at every step, and with zero moments that step leaves it unchanged (m = v = 0, the update
+is 0).  So the oracle runs on the COMPACTED model — the union of the rows any step reads (plus
+every candidate row the batch draw looked at), ids remapped — and every touched row of the device
+table is compared with it after the steps; every untouched row must still equal its initial
+value, bit for bit, with zero moments.
+
+Tolerances (fp32 device vs float64 oracle): weights after k steps |dw| <= k * 2e-6 + 2e-6 * max|w|
+and loss rel 2e-5, as tests/test_headline_parity_gpu.py; probabilities |dp| <= 2e-6 on the initial
+weights and <= 2e-6 * (1 + s) after s optimizer steps — the weights may drift by the tolerance
+above each step, and config D's 256-wide first layer (O(1) activations here) sums that drift over
+twice the inputs of config C's.
+Batches are drawn off the ReLU kinks (every hidden |z| >= 1e-6 under the oracle's weights of that
+step), as in the headline test; tests/test_headline_parity_gpu.py also covers unfiltered batches.
+"""
+
+import numpy as np
+import pytest
+
+from conftest import gpu_available
+from oracle import ncf_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+if gpu_available():
+    import torch
+    from movierec.engine import NCFEngine
+
+U, I, LAYERS, GMF = 10_000_000, 1_000_000, [256, 128, 64, 32], 128
+GROUP = 4
+HYPER = dict(optimizer="adam", lr=0.001, beta_1=0.9, beta_2=0.999, layers_l2reg=[0.0] * 4)
+
+
+def _dense_weights(seed):
+    """Dense layers: Keras initialisation of the config-D layers, scaled like the small-shape
+    tests so activations stay O(1) with O(1) embeddings; the output layer rescaled later."""
+    small = O.NCFShape(2, 2, LAYERS, GMF)
+    w = O.init_weights(small, seed=seed)
+    rng = np.random.RandomState(seed + 1)
+    out = {}
+    for k, v in w.items():
+        if k.endswith("embedding"):
+            continue
+        out[k] = rng.uniform(-0.1, 0.1, size=v.shape) if k.endswith("bias") else v * 4.0
+    return out
+
+
+def _device_tables(eng, seed):
+    """Uniform(-0.5, 0.5) embedding tables drawn on the device (deterministic generator)."""
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    chunk = 1 << 20
+    for r0 in range(0, eng.num_rows, chunk):
+        r1 = min(eng.num_rows, r0 + chunk)
+        eng.emb[r0:r1].copy_(torch.rand(r1 - r0, eng.row_width, generator=g, device="cuda") - 0.5)
+    torch.cuda.synchronize()
+
+
+class Compact(object):
+    """The compacted oracle model: rows gathered from the device's initial table."""
+
+    def __init__(self, emb0, dense, users, items, gstride, du, di):
+        self.users = np.unique(users)
+        self.items = np.unique(items)
+        ur = torch.from_numpy(self.users.astype(np.int64)).cuda()
+        ir = torch.from_numpy(self.items.astype(np.int64) + U).cuda()
+        urows = emb0[ur].double().cpu().numpy()
+        irows = emb0[ir].double().cpu().numpy()
+        self.w = dict(dense)
+        self.w["user_gmf_embedding"] = urows[:, :GMF]
+        self.w["item_gmf_embedding"] = irows[:, :GMF]
+        self.w["user_embedding"] = urows[:, gstride:gstride + du]
+        self.w["item_embedding"] = irows[:, gstride:gstride + di]
+        self.shape = O.NCFShape(len(self.users), len(self.items), LAYERS, GMF)
+
+    def ids(self, users, items):
+        return (np.searchsorted(self.users, users).astype(np.int32),
+                np.searchsorted(self.items, items).astype(np.int32))
+
+
+def _pre_activations(w, users, items):
+    h = np.concatenate([w["user_embedding"][users], w["item_embedding"][items]], axis=1)
+    m = np.full(len(users), np.inf)
+    for l in range(1, len(LAYERS)):
+        z = h @ w["hidden_%d/kernel" % l] + w["hidden_%d/bias" % l]
+        m = np.minimum(m, np.abs(z).min(axis=1))
+        h = np.maximum(z, 0)
+    return m
+
+
+def test_config_d_full_size_matches_compacted_oracle():
+    B = 65536
+    steps = 3
+    rng = np.random.RandomState(40)
+    ngroups = B // GROUP
+    # candidate groups, 1/8 spare for the kink filter; the first groups pin the table's corners
+    cand = []
+    for s in range(steps):
+        n = ngroups + ngroups // 8
+        cu = rng.randint(0, U, n)
+        ci = rng.randint(0, I, (n, GROUP))
+        if s == 0:
+            cu[:3] = [0, U - 1, 8_388_608]        # first user, last user, first past 2^31 / 256
+            ci[:3, -1] = [0, I - 1, I // 2]
+        cand.append((cu, ci))
+
+    eng = NCFEngine(U, I, LAYERS, GMF, max_batch=B, lazy_adam=True)
+    assert eng.kernel_for(B) in ("layered-rocblas", "fused-mfma-wave", "fused-mfma-unit"), eng.kernel_for(B)
+    gstride, du, di = eng.shape.gmf_stride, eng.shape.du, eng.shape.di
+    assert eng.row_width * eng.num_rows > (1 << 31)
+    _device_tables(eng, seed=41)
+    emb0 = eng.emb.clone()
+    dense = _dense_weights(42)
+    all_u = np.concatenate([c[0] for c in cand])
+    all_i = np.concatenate([c[1].reshape(-1) for c in cand])
+    cm = Compact(emb0, dense, all_u, all_i, gstride, du, di)
+    # output layer: keep logits well inside the BCE clip range on the first candidates
+    u0, i0 = cm.ids(cand[0][0][:512].repeat(GROUP), cand[0][1][:512].reshape(-1))
+    _, c = O.forward(cm.shape, cm.w, u0, i0)
+    f = 6.0 / max(np.max(np.abs(c["z"])), 1e-6)
+    cm.w["output/kernel"] = cm.w["output/kernel"] * f
+    cm.w["output/bias"] = cm.w["output/bias"] * f
+    cm.w = {k: v.astype(np.float32).astype(np.float64) for k, v in cm.w.items()}
+    from movierec.layout import Layout
+    flat = Layout(1, 1, LAYERS, GMF).to_device({**cm.w, "user_embedding": np.zeros((1, du)),
+                                                 "item_embedding": np.zeros((1, di)),
+                                                 "user_gmf_embedding": np.zeros((1, GMF)),
+                                                 "item_gmf_embedding": np.zeros((1, GMF))})[1]
+    eng.mlp.copy_(torch.from_numpy(flat))
+
+    # the oracle runs first: each step's batch is drawn off the kinks of the weights it meets
+    ref = {k: v.copy() for k, v in cm.w.items()}
+    st = O.new_opt_state(ref)
+    batches, outs = [], []
+    for s in range(steps):
+        cu, ci = cand[s]
+        users = cu.repeat(GROUP)
+        items = ci.reshape(-1)
+        lu, li = cm.ids(users, items)
+        ok = (_pre_activations(ref, lu, li) >= 1e-6).reshape(-1, GROUP).all(axis=1)
+        if s == 0:
+            ok[:3] = True                        # the corner groups stay (checked below)
+        keep = np.flatnonzero(ok)[:ngroups]
+        assert len(keep) == ngroups, "too many kink groups: %d" % int((~ok).sum())
+        gu = cu[keep].repeat(GROUP).astype(np.int32)
+        gi = ci[keep].reshape(-1).astype(np.int32)
+        y = np.tile([0.0] * (GROUP - 1) + [1.0], ngroups).astype(np.float32)
+        lu, li = cm.ids(gu, gi)
+        outs.append(O.train_step(cm.shape, ref, st, lu, li, y, HYPER))
+        batches.append((gu, gi, y))
+    assert batches[0][0][GROUP] == U - 1 and batches[0][1][3 * GROUP - 1] == I // 2
+
+    dev = [tuple(torch.from_numpy(a).cuda() for a in b) for b in batches]
+    for s, (u, it, y) in enumerate(dev):
+        probs = torch.empty(B, dtype=torch.float32, device="cuda")
+        nxt = (dev[s + 1][0], dev[s + 1][1]) if s + 1 < steps else None
+        eng.train_step(u, it, y, group=GROUP, k=2, probs_out=probs, next_batch=nxt)
+        err = float(np.max(np.abs(probs.cpu().numpy() - outs[s][1])))
+        assert err <= 2e-6 * (1 + s), "step %d probs: max err %g" % (s, err)
+    eng.check_errors()
+    stats = NCFEngine.read_stats(eng.stats)
+    assert stats["steps"] == steps
+    assert stats["loss"] == pytest.approx(np.mean([o[0] for o in outs]), rel=2e-5)
+    eng.flush()
+    torch.cuda.synchronize()
+    assert int(eng.row_step.min()) == int(eng.row_step.max()) == steps == int(eng.step.item())
+
+    # every row of the compacted model (touched or not) against the oracle
+    ur = torch.from_numpy(cm.users.astype(np.int64)).cuda()
+    ir = torch.from_numpy(cm.items.astype(np.int64) + U).cuda()
+    got = {}
+    urows, irows = eng.emb[ur].double().cpu().numpy(), eng.emb[ir].double().cpu().numpy()
+    got["user_gmf_embedding"], got["item_gmf_embedding"] = urows[:, :GMF], irows[:, :GMF]
+    got["user_embedding"] = urows[:, gstride:gstride + du]
+    got["item_embedding"] = irows[:, gstride:gstride + di]
+    dense_got = Layout(1, 1, LAYERS, GMF).from_device(np.zeros((2, eng.row_width), np.float32),
+                                                      eng.mlp.cpu().numpy())
+    for name in O.weight_names(cm.shape):
+        g = got[name] if name.endswith("embedding") else dense_got[name]
+        tol = steps * 2e-6 + 2e-6 * float(np.max(np.abs(ref[name])))
+        e = float(np.max(np.abs(np.asarray(g, np.float64) - ref[name])))
+        assert e <= tol, "%s: max err %g > %g" % (name, e, tol)
+
+    # untouched rows: bitwise their initial values, zero moments
+    touched = torch.zeros(eng.num_rows, dtype=torch.bool, device="cuda")
+    for u, it, _ in dev:
+        touched[u.long()] = True
+        touched[it.long() + U] = True
+    n_touched = int(touched.sum())
+    chunk = 1 << 20
+    for r0 in range(0, eng.num_rows, chunk):
+        r1 = min(eng.num_rows, r0 + chunk)
+        cold = ~touched[r0:r1]
+        moved = (eng.emb[r0:r1] != emb0[r0:r1]).any(dim=1)
+        assert not bool((moved & cold).any()), "untouched rows moved in [%d, %d)" % (r0, r1)
+        nz = (eng.emb_m[r0:r1] != 0).any(dim=1) | (eng.emb_v[r0:r1] != 0).any(dim=1)
+        assert not bool((nz & cold).any()), "untouched rows got moments in [%d, %d)" % (r0, r1)
+        assert bool((nz | ~touched[r0:r1]).all()), "a touched row kept zero moments in [%d, %d)" % (r0, r1)
+    assert 0 < n_touched < eng.num_rows

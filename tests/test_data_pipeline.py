@@ -257,6 +257,25 @@ def test_ml20m_split_has_dense_item_ids(tmp_path):
     # remap_items=False keeps the reference's raw ids
     tr, _, _ = load_ratings_train_test_sets("ml-20m", str(tmp_path), download=False, remap_items=False)
     np.testing.assert_array_equal(tr["itemId"].values, tr0["itemId"].values)
+    # the dense -> raw table travels with the frames (invert the mapping: ids back to movieIds)
+    for f in (train, val, test):
+        np.testing.assert_array_equal(f.attrs["raw_item_ids"], movie_ids - 1)
+    np.testing.assert_array_equal(train.attrs["raw_item_ids"][train["itemId"].values], tr0["itemId"].values)
+
+
+def test_ml20m_remap_needs_the_movies_file(tmp_path):
+    """One numbering only: without ml-20m's movies.csv the default remap refuses instead of
+    silently numbering by the rated ids; remap_items='ratings' asks for that numbering."""
+    from movierec.data_pipeline import load_ratings_train_test_sets
+    _write_ml20m(str(tmp_path))
+    os.remove(os.path.join(str(tmp_path), "ml-20m", "movies.csv"))
+    with pytest.raises(FileNotFoundError):
+        load_ratings_train_test_sets("ml-20m", str(tmp_path), download=False)
+    train, val, test = load_ratings_train_test_sets("ml-20m", str(tmp_path), download=False, remap_items="ratings")
+    raw = train.attrs["raw_item_ids"]
+    assert np.all(np.diff(raw) > 0)
+    both = pd.concat([train, val, test])
+    assert set(raw[both["itemId"].values].tolist()) == set(raw.tolist())
 
 
 def test_remap_rejects_unknown_movie():

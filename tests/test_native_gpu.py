@@ -466,6 +466,79 @@ def test_counted_ahead_ids_changed_in_place():
     assert torch.isfinite(a.emb).all()
 
 
+def test_stale_count_step_keeps_the_dense_decay_state():
+    """A counted-ahead batch whose item ids change behind torch's back (NCF_WSERR_STALE_COUNT):
+    the rows it reads that the counted set missed owe their deferred decay — the step replays them
+    before the forward pass, so the table stays in the dense-sweep state.  Pinned against an engine
+    that flushes (every row current) right before the same stale step: with the replay the two are
+    bitwise equal; without it the missed rows' p would be stale and differ."""
+    shape = O.NCFShape(*SHAPES[3])
+    w = _weights(shape, 70)
+    bt = []
+    for s in range(4):
+        users, items, y = _batch(shape, 256, 4, 71 + s)
+        bt.append((torch.from_numpy(users).cuda(), torch.from_numpy(items).cuda(), torch.from_numpy(y).cuda()))
+    # items of bt[3] restricted to 0..74, the stale ids 75..149: every stale item row is missed by
+    # the counted set, and rows idle since step 0 owe several zero-gradient steps
+    it3 = (bt[3][1] % 75).contiguous()
+    stale_items = (75 + bt[0][1] % 75).contiguous()
+    engines = []
+    for flush_first in (False, True):
+        e = _engine(shape, w, lazy_adam=True)
+        for s in range(3):
+            e.train_step(*bt[s], group=4, k=2)
+        stage = (bt[3][0].clone(), it3.clone())
+        e.train_step(*bt[2], group=4, k=2, next_batch=stage)
+        stage[1].data.copy_(stale_items)     # behind torch's back: counted ids no longer match
+        if flush_first:
+            e.flush()                        # every row current: no replay owed
+            e._dirty = True
+        e.train_step(stage[0], stage[1], bt[3][2], group=4, k=2)
+        with pytest.raises(RuntimeError):
+            e.check_errors()
+        e.flush()
+        engines.append(e)
+    torch.cuda.synchronize()
+    a, d = engines
+    assert torch.equal(a.row_step, d.row_step)
+    assert torch.equal(a.emb, d.emb) and torch.equal(a.emb_m, d.emb_m) and torch.equal(a.emb_v, d.emb_v)
+    assert torch.equal(a.mlp, d.mlp)
+
+
+def test_discarded_counts_keep_sticky_flags():
+    """Dropping a counted-ahead batch (the next step passes other ids) clears only the index
+    counters: an id-range flag raised before stays for check_errors."""
+    shape = O.NCFShape(*SHAPES[3])
+    w = _weights(shape, 80)
+    b0 = [torch.from_numpy(x).cuda() for x in _batch(shape, 256, 4, 81)]
+    b1 = [torch.from_numpy(x).cuda() for x in _batch(shape, 256, 4, 82)]
+    b2 = [torch.from_numpy(x).cuda() for x in _batch(shape, 256, 4, 83)]
+    e = _engine(shape, w, lazy_adam=True)
+    bad_items = b0[1].clone()
+    bad_items[5] = shape.num_items + 3       # outside the table: masked and flagged on the device
+    e.train_step(b0[0], bad_items, b0[2], group=4, k=2, next_batch=(b1[0], b1[1]))
+    e.train_step(*b2, group=4, k=2)          # not the counted batch: the counts are discarded
+    with pytest.raises(ValueError):
+        e.check_errors()
+    e.check_errors()
+
+
+def test_sharded_workspace_flags():
+    """ShardedNCFEngine.check_errors reads the flags at the row-sharded layout's offset."""
+    from movierec.sharded import ShardedNCFEngine
+    shape = O.NCFShape(*SHAPES[3])
+    e = ShardedNCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, world=3, rank=1,
+                         max_batch=256)
+    users, items, _ = _batch(shape, 256, 4, 90)
+    e.plan(users, items, group=4)
+    e.check_errors()
+    items[7] = -1
+    e.plan(users, items, group=4)
+    with pytest.raises(ValueError):
+        e.check_errors()
+    e.check_errors()
+
+
 def test_evaluate_full_protocol_fused_forward():
     """ncf_evaluate on a 200,000-sample validation pass (2,000 users x [99 negatives + the
     held-out positive], k = 10) over config C's full tables: the fused MFMA forward against the

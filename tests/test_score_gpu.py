@@ -111,6 +111,29 @@ def test_score_topk_matches_oracle(dims, precision):
     assert covered >= 0.5   # the exact-position check covered most positions
 
 
+@pytest.mark.parametrize("precision", ["fp16", "fp32"])
+def test_score_topk_full_ml20m_catalogue(precision):
+    """BASELINE config E at its real size: the ml-20m NeuMF model (config C's) over the full
+    138,493 x 27,278 tables; 77 users (not a multiple of 32, with duplicates, the first and the
+    last user) scored against every one of the 27,278 items (853 item tiles: every item range of
+    a user block and the merge), top-10 compared with the oracle's full catalogue scores."""
+    shape = O.NCFShape(138493, 27278, [128, 64, 32, 16], 64)
+    w = _weights(shape, 11)
+    eng = _engine(shape, w)
+    rng = np.random.RandomState(12)
+    users = rng.randint(0, shape.num_users, 77).astype(np.int32)
+    users[:4] = [0, shape.num_users - 1, 0, users[10]]
+    items, scores = eng.score_topk(users, k=10, precision=precision)
+    z = O.score_all_items(shape, w, users)
+    tol = TOL_Z[precision]
+    covered = _check(items.cpu().numpy(), scores.cpu().numpy(), z, 10, tol, exact_gap=2 * tol)
+    assert covered >= 0.5
+    # duplicate users get identical lists
+    it = items.cpu().numpy()
+    np.testing.assert_array_equal(it[0], it[2])
+    np.testing.assert_array_equal(it[3], it[10])
+
+
 @pytest.mark.parametrize("k", [1, 5, 32])
 def test_score_topk_k_values(k):
     shape = O.NCFShape(120, 300, [128, 64, 32, 16], 64)
