@@ -81,6 +81,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="C", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: the config's)")
+    ap.add_argument("--global-batch", type=int, default=None,
+                    help="strong scaling: a fixed global batch split over the ranks (per-GPU batch = global / N; "
+                         "config C's BASELINE configuration is --global-batch 65536 on 8 GPUs); default: weak "
+                         "scaling, the per-GPU batch fixed")
     ap.add_argument("--pool", type=int, default=None,
                     help="distinct synthetic batches cycled through (default: one per warmup + timed step, at "
                          "most 1024: every step trains on fresh uniform ids, as epochs over real data do; a "
@@ -99,6 +103,10 @@ def parse():
     ap.add_argument("--e2e", action="store_true",
                     help="end-to-end: each step also samples its batch on the device (ncf_sample_batch) from an "
                          "ml-20m-shaped synthetic ratings set (20M positives)")
+    ap.add_argument("--fit-epochs", action="store_true",
+                    help="end to end through the reference's API: --steps whole MovierecModel.fit_generator epochs "
+                         "(after one warm-up epoch) over an ml-20m-shaped synthetic ratings set with the device "
+                         "sampler (trainer params sampler='device'; world_size = --gpus); samples/s of the epochs")
     ap.add_argument("--dense-sweep", action="store_true",
                     help="sweep every embedding row every step instead of the deferred exact decay (same result)")
     ap.add_argument("--emulate-world", type=int, default=1,
@@ -295,6 +303,61 @@ def score_main(args, cfg, world, rank):
         dist.destroy_process_group()
 
 
+def fit_main(args, cfg, world, rank):
+    """Trainer-style epochs: MovierecModel.fit_generator (the reference's model.py:305-333 loop:
+    every batch of the Sequence, on_epoch_end; no validation pass) over DeviceMovieLensDataGenerator
+    batches, timed whole — sampling, the H2D-free batch handoff, training steps, per-epoch error
+    checks and metric reads included."""
+    import tempfile
+    from movierec.model import MovierecModel
+    B, g = cfg["batch"], cfg["negs"] + 1
+    L = cfg["layers"]
+    params = dict(num_users=cfg["num_users"], num_items=cfg["num_items"], layers_sizes=L, layers_l2reg=[0] * len(L),
+                  optimizer="adam", lr=0.001, batch_size=B * world, num_negs_per_pos=cfg["negs"],
+                  batch_size_eval=100 * world, num_negs_per_pos_eval=99, k=min(10, g), seed=0,
+                  gmf_dim=cfg["gmf_dim"], world_size=world, precision=args.precision or cfg.get("precision", "fp32"),
+                  max_batch=B)
+    model = MovierecModel(params, "bench", tempfile.mkdtemp(), verbose=0)
+    eng = model.model.engine
+    gen = synthetic_device_generator(cfg, B, g, seed=1234 + rank, world=world,
+                                     num_users=eng.num_users if world > 1 else None)
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist.is_initialized():
+            dist.barrier()
+
+    model.fit_generator(gen, None, epochs=1)   # warm-up epoch
+    barrier()
+    t0 = time.perf_counter()
+    model.fit_generator(gen, None, epochs=args.steps)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist.is_initialized():
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    steps_per_epoch = len(gen)
+    if dist.is_initialized():
+        from movierec.distributed import all_reduce_min
+        steps_per_epoch = all_reduce_min(steps_per_epoch)
+    samples = args.steps * steps_per_epoch * B * world
+    if rank == 0:
+        emit(json.dumps({
+            "metric": "fit_generator epoch samples/sec (user-item pairs) NeuMF ml-20m, device sampler",
+            "value": round(samples / elapsed, 1), "unit": "samples/s", "n_gpus": world, "epochs": args.steps,
+            "warmup_epochs": 1, "steps_per_epoch": steps_per_epoch, "ms_per_step": round(elapsed / (args.steps *
+                                                                                               steps_per_epoch) * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "dtype": params["precision"],
+            "data": "synthetic ml-20m-shaped ratings (%d positives per rank), negatives sampled on the device"
+                    % len(gen.data),
+            "config": {"workload": cfg["workload"], "global_batch": B * world, "per_gpu_batch": B,
+                       "api": "MovierecModel.fit_generator (trainer params sampler='device', world_size=%d)" % world,
+                       "epoch_rule": "len = positives // batch (the reference's data_pipeline.py:97, SURVEY F4)"}}))
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
 def synthetic_device_generator(cfg, batch, group, seed, num_users=None, world=1):
     """ml-20m-shaped synthetic ratings (20M positives over the config's users x items, uniform)
     behind the on-device sampler: a step = sample one batch + train on it.  User-partitioned
@@ -453,12 +516,22 @@ def main():
     cfg = dict(CONFIGS[args.config])
     if args.config == "E":
         return score_main(args, cfg, world, rank)
+    if args.fit_epochs:
+        if args.batch:
+            cfg["batch"] = args.batch
+        return fit_main(args, cfg, world, rank)
     from movierec.engine import NCFEngine
     from movierec.model import initial_weights
     from movierec import _native as N
 
+    if args.batch and args.global_batch:
+        raise SystemExit("--batch (per GPU, weak scaling) and --global-batch (strong scaling) exclude each other")
     if args.batch:
         cfg["batch"] = args.batch
+    if args.global_batch:
+        if args.global_batch % world:
+            raise SystemExit("--global-batch %d does not split over %d ranks" % (args.global_batch, world))
+        cfg["batch"] = args.global_batch // world
     B, g = cfg["batch"], cfg["negs"] + 1
     prec = args.precision or cfg.get("precision", "fp32")
     if prec == "bf16" and mode == "sharded":
@@ -481,8 +554,10 @@ def main():
         from movierec.distributed import UserPartitionedDataParallel, partition_keras_weights
         ew = max(world, args.emulate_world)
         n_loc = (cfg["num_users"] - rank + ew - 1) // ew
+        # the own users under deferred exact decay (the replicated item rows are swept every step)
         eng = NCFEngine(n_loc, cfg["num_items"], cfg["layers"], cfg["gmf_dim"], max_batch=B,
-                        force_generic=args.generic, precision=prec)
+                        force_generic=args.generic, precision=prec, lazy_adam=not args.dense_sweep,
+                        lazy_rows=n_loc)
         eng.set_keras_weights(partition_keras_weights(w0, ew, rank))
         dp = UserPartitionedDataParallel(eng)
         dp.broadcast_parameters()
@@ -584,7 +659,7 @@ def main():
     train_exchange = dp.last_exchange if mode == "sharded" else None
     if mode == "sharded":
         nbytes = emb_update_bytes(eng.shape, B, sparse_rows=(eng.shard_rows, train_exchange[1]))
-    elif getattr(eng, "lazy", False):
+    elif getattr(eng, "lazy", False) and mode == "single":
         touched = float(np.mean([torch.unique(u).numel() + torch.unique(it).numel() for u, it, _ in pool[:16]]))
         nbytes = emb_update_bytes(eng.shape, B, touched_rows=touched, contribs=contribs)
         if sampler is None:
@@ -604,7 +679,17 @@ def main():
         # (ncf_apply_update); bytes per launch = the step's bytes / 2, time per launch = the average
         Uloc, W = eng.num_users, eng.shape.row_width
         cu = contribs - B   # the own users' gradient rows
-        own = 24 * Uloc * W + cu * W * 4 + cu * 4 + (Uloc + 1) * 4
+        if getattr(eng, "lazy", False):
+            # deferred decay of the own users: the touched ones only, plus (counting ahead) the next
+            # batch's id reads + counter atomics and the replay of its own rows this step missed
+            tu = float(np.mean([torch.unique(u).numel() for u, _, _ in pool[:16]]))
+            own = 24 * tu * W + cu * W * 4 + cu * 4 + 2 * B * (4 + 8)
+            stale = [int((~torch.isin(torch.unique(u1.long()), torch.unique(u0.long()))).sum())
+                     for (u0, _, _), (u1, _, _) in zip(pool[:16], pool[1:17])]
+            replay_rows = float(np.mean(stale)) if stale else 0.0
+            own += 24 * replay_rows * W
+        else:
+            own = 24 * Uloc * W + cu * W * 4 + cu * 4 + (Uloc + 1) * 4
         nbytes = (own + 28 * (eng.num_rows - Uloc) * W) / 2.0
     else:
         nbytes = emb_update_bytes(eng.shape, B, dense_rows=(dp.row_count if mode == "replicated" else None),
@@ -639,7 +724,7 @@ def main():
         dist.all_reduce(hd)
     hr = {"hr": float(hd[0]) / (ev_users * world), "dcg": float(hd[1]) / (ev_users * world)}
 
-    emb_kernel = "k_emb_adam_touched" if getattr(eng, "lazy", False) else "k_emb_update"
+    emb_kernel = "k_emb_adam_touched" if getattr(eng, "lazy", False) and mode == "single" else "k_emb_update"
     traffic = pmc_traffic(emb_kernel, args.config, B, mode)
     kpath = eng.kernel_for(B) if hasattr(eng, "kernel_for") else ("fused-mfma-tile" if eng.fast_path else "generic")
     fb_kernel = {"fused-mfma-tile": "k_fb_fused", "fused-mfma-unit": "k_fb_unit",
@@ -681,7 +766,12 @@ def main():
                                            "(k_emb_adam_touched; deferred exact decay"
                                            + ("; its launch also counts the next batch's index "
                                               "contributions)" if sampler is None else ")")
-                                           if getattr(eng, "lazy", False) else
+                                           if getattr(eng, "lazy", False) and mode == "single" else
+                                           "embedding Adam, 2 launches per step (k_emb_adam_touched: the "
+                                           "touched own-user rows with their scatter-add, deferred exact "
+                                           "decay, the next batch counted and its own rows caught up ahead; "
+                                           "k_emb_update_mlp: item rows with the all-reduced gradient + the "
+                                           "dense layers)" if mode == "user" and getattr(eng, "lazy", False) else
                                            "embedding Adam, 2 launches per step (k_emb_update: own-user "
                                            "rows with their scatter-add; item rows with the all-reduced "
                                            "gradient)" if mode == "user" else
@@ -728,7 +818,7 @@ def main():
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "higher_is_better": True, "scaling": "strong" if args.global_batch else "weak", "vs_baseline": None,
             "dtype": "bf16 MLP operands, fp32 accumulate/master/Adam" if prec == "bf16" else "fp32",
             "data": ("synthetic ml-20m-shaped ratings (%d positives), negatives sampled on the device each step"
                      % len(sampler.data) if sampler is not None else
@@ -743,6 +833,7 @@ def main():
             "catchup_ms": round(ms_cu / ncu, 5) if ncu else None,
             "adam": ("deferred exact decay (untouched rows replay their zero-gradient steps when next touched; "
                      "flushed inside the timed region; bitwise the dense Keras sweep)"
+                     + ("; the replicated item rows are swept every step" if mode == "user" else "")
                      if getattr(eng, "lazy", False) else "dense sweep of every row every step (Keras, F5)"),
             "cpu_baseline": cpu,
             "cpu_baseline_with_sampler": cpu_e2e,
@@ -753,6 +844,11 @@ def main():
         }
         if exchange is not None:
             line["exchange"] = exchange
+        if args.emulate_world > 1:
+            line["emulated_world"] = args.emulate_world
+            line["note"] = ("diagnostic: rank 0's per-rank compute of the %d-rank user-partitioned step on one GPU "
+                            "(local table of 1/%d of the users, a one-rank communicator); not a scaling result"
+                            % (args.emulate_world, args.emulate_world))
         emit(json.dumps(line))
     if dist.is_initialized():
         dist.destroy_process_group()

@@ -137,7 +137,12 @@ typedef struct ncf_hyper {
                                            accumulation; embeddings, GMF, loss, master weights
                                            and Adam stay fp32 (BASELINE config B; fast_path
                                            shapes, unit kernel only) */
-    int32_t reserved[4];
+    int32_t lazy_rows;                  /* deferred exact decay (optim->row_step) covers table rows
+                                           [0, lazy_rows) only, 0 = every row; the rows past it are
+                                           swept densely by the caller (the replicated item rows of
+                                           user-partitioned data parallelism), and row_step needs
+                                           lazy_rows entries */
+    int32_t reserved[3];
 } ncf_hyper_t;
 
 int ncf_abi_version(void);
@@ -303,6 +308,30 @@ int ncf_update_rows(const ncf_shape_t* shape, ncf_model_t* model, ncf_optim_t* o
  * and force_generic decide the user-row folding; NULL = none); a mismatch sets NCF_WSERR_FOLD. */
 int ncf_build_index(const ncf_shape_t* shape, const ncf_hyper_t* hyper, const int32_t* users, const int32_t* items,
                     int64_t n, void* ws, size_t ws_bytes, void* stream);
+
+/* The user-partitioned step with deferred exact decay of the own rows [0, hyper->lazy_rows) (the
+ * rank's users; optim->row_step has lazy_rows entries; embedding L2 off), the rest as above:
+ *   ncf_forward_backward_part_lazy  ncf_forward_backward_part with shared_row_begin =
+ *                              hyper->lazy_rows; the batch's own rows are caught up on their
+ *                              missed zero-gradient steps before the forward pass (nothing to do
+ *                              with hyper->index_ready = 2: the previous ncf_update_rows_lazy counted
+ *                              this batch and caught its rows up ahead)
+ *   all_reduce                 [shared_grad | mlp_grad | summary] (RCCL, async)
+ *   ncf_update_rows_lazy       meanwhile: the touched own rows' scatter-add + Adam at step
+ *                              *optim->step + 1 (row_step set; step not bumped); with next ids
+ *                              (n_next == n, Adam) the same launch counts the next batch's index
+ *                              and catches its own rows up ahead, then its key scan runs
+ *   ncf_apply_update           the replicated rows (dense sweep), dense layers, stats, step++.
+ * Bitwise the same table as the dense-sweep user-partitioned step after ncf_lazy_flush (which
+ * flushes rows [0, lazy_rows) only). */
+int ncf_forward_backward_part_lazy(const ncf_shape_t* shape, ncf_model_t* model, ncf_optim_t* optim,
+                                   const ncf_hyper_t* hyper, const int32_t* users, const int32_t* items,
+                                   const float* labels, int64_t n, float* shared_grad, float* mlp_grad, float* summary,
+                                   float* probs_out, int32_t include_dense_reg, void* ws, size_t ws_bytes,
+                                   void* stream);
+int ncf_update_rows_lazy(const ncf_shape_t* shape, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* hyper,
+                         int64_t n, const int32_t* next_users, const int32_t* next_items, int64_t n_next, void* ws,
+                         size_t ws_bytes, void* stream);
 
 /* Row-sharded data parallelism (no reference counterpart — the
  * reference trains on one CPU).  Rank r of `world` (1..16) owns the table rows g

@@ -589,6 +589,8 @@ static int train_step_impl(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t
     // Deferred exact decay (optim->row_step set, L2 off): untouched rows are not swept; the
     // batch's rows catch up on their missed zero-gradient steps right after the index build
     const bool lazy = optim->row_step != nullptr;
+    if (lazy && h->lazy_rows > 0 && h->lazy_rows < s->num_rows)
+        return fail(NCF_EINVAL, "hyper->lazy_rows < num_rows is the user-partitioned step's (ncf_*_lazy)");
     if (lazy && h->l2[0] != 0.0f)
         return fail(NCF_EINVAL, "deferred decay (row_step) needs the embedding L2 off: the loss sums the whole table");
     CatchupCtx cc{s, &L, model, optim, h, ws, st, n, users, items};
@@ -661,11 +663,14 @@ int ncf_train_step_ahead(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* 
                            probs_out, ws, ws_bytes, stream);
 }
 
+// lazy (optional): deferred exact decay of rows [0, h->lazy_rows) — the index carries the touched
+// list and the batch's stale rows are caught up before the forward pass (user-partitioned DP)
 static int forward_backward_rows(const ncf_shape_t* s, const ncf_model_t* model, const ncf_hyper_t* h,
                                  const int32_t* users, const int32_t* items, const float* labels, int64_t n,
                                  int64_t grad_row_begin, float* emb_grad, float* mlp_grad, float* summary,
                                  float* probs_out, int64_t reg_row_begin, int64_t reg_row_count,
-                                 int32_t include_dense_reg, void* ws, size_t ws_bytes, void* stream) {
+                                 int32_t include_dense_reg, void* ws, size_t ws_bytes, void* stream,
+                                 ncf_optim_t* lazy = nullptr) {
     if (int r = check_train_args(s, model, h, users, items, labels, n)) return r;
     if (!emb_grad || !mlp_grad || !summary) return fail(NCF_EINVAL, "NULL gradient output");
     if (reg_row_begin < 0 || reg_row_count < 0 || reg_row_begin > s->num_rows)
@@ -675,7 +680,10 @@ static int forward_backward_rows(const ncf_shape_t* s, const ncf_model_t* model,
     if (int r = check_ws(*s, n, ws, ws_bytes, &L)) return r;
     hipStream_t st = (hipStream_t)stream;
     FbOut fb;
-    if (int r = run_fb(*s, L, model, h, users, items, labels, n, ws, probs_out, &fb, st)) return r;
+    CatchupCtx cc{s, &L, const_cast<ncf_model_t*>(model), lazy, h, ws, st, n, users, items};
+    if (int r = run_fb(*s, L, model, h, users, items, labels, n, ws, probs_out, &fb, st, false,
+                       lazy ? catchup_touched : nullptr, &cc))
+        return r;
     // the index (side stream) must be complete before the side stream takes the dense tail
     if (int r = index_join(st, fb)) return r;
     if (side_stream_mode() == 0 && ncf::part_tail_foldable(*s, *h, fb.nslab)) {
@@ -720,6 +728,54 @@ int ncf_forward_backward_part(const ncf_shape_t* s, const ncf_model_t* model, co
     if (shared_row_begin < 0 || shared_row_begin > s->num_rows) return fail(NCF_EINVAL, "invalid shared row range");
     return forward_backward_rows(s, model, h, users, items, labels, n, shared_row_begin, shared_grad, mlp_grad, summary,
                                  probs_out, reg_row_begin, reg_row_count, include_dense_reg, ws, ws_bytes, stream);
+}
+
+static int check_lazy_dp(const ncf_shape_t* s, const ncf_model_t* model, const ncf_optim_t* optim,
+                         const ncf_hyper_t* h) {
+    if (int r = check_shape(s)) return r;
+    if (int r = check_hyper(h)) return r;
+    if (!model || !model->emb) return fail(NCF_EINVAL, "NULL device pointer");
+    if (!optim || !optim->step || !optim->row_step ||
+        (h->optimizer == NCF_OPT_ADAM && (!optim->emb_m || !optim->emb_v)))
+        return fail(NCF_EINVAL, "deferred decay needs the optimizer state and row_step");
+    if (h->lazy_rows <= 0 || h->lazy_rows > s->num_rows)
+        return fail(NCF_EINVAL, "hyper->lazy_rows must be in [1, num_rows], got %d", h->lazy_rows);
+    if (h->l2[0] != 0.0f)
+        return fail(NCF_EINVAL, "deferred decay (row_step) needs the embedding L2 off: the loss sums the whole table");
+    return 0;
+}
+
+int ncf_forward_backward_part_lazy(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* optim,
+                                   const ncf_hyper_t* h, const int32_t* users, const int32_t* items,
+                                   const float* labels, int64_t n, float* shared_grad, float* mlp_grad, float* summary,
+                                   float* probs_out, int32_t include_dense_reg, void* ws, size_t ws_bytes,
+                                   void* stream) {
+    if (int r = check_lazy_dp(s, model, optim, h)) return r;
+    if (h->index_ready == 1) return fail(NCF_EINVAL, "index_ready = 1 (ncf_build_index) is not used here: count ahead");
+    return forward_backward_rows(s, model, h, users, items, labels, n, h->lazy_rows, shared_grad, mlp_grad, summary,
+                                 probs_out, 0, 0, include_dense_reg, ws, ws_bytes, stream, optim);
+}
+
+int ncf_update_rows_lazy(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* h,
+                         int64_t n, const int32_t* next_users, const int32_t* next_items, int64_t n_next, void* ws,
+                         size_t ws_bytes, void* stream) {
+    if (int r = check_lazy_dp(s, model, optim, h)) return r;
+    if ((next_users || next_items) && (!next_users || !next_items || n_next != n || h->optimizer != NCF_OPT_ADAM))
+        return fail(NCF_EINVAL, "next batch: NULL ids, n_next != n, or not Adam");
+    ncf::WsLayout L;
+    if (int r = check_ws(*s, n, ws, ws_bytes, &L)) return r;
+    hipStream_t st = (hipStream_t)stream;
+    prof_begin(NCF_K_EMB_UPDATE, st);
+    hipError_t e = ncf::launch_emb_update_touched(*s, L, ws, model->emb, optim->emb_m, optim->emb_v, optim->row_step,
+                                                  optim->step, *h, st, next_users, next_items,
+                                                  next_users ? n_next : 0, nullptr, index_fold(*s, h));
+    prof_end(NCF_K_EMB_UPDATE, st);
+    if (e != hipSuccess) return hip_check(e, "touched-row update");
+    if (next_users) {
+        e = ncf::launch_scan_ahead(L, ws, s->num_rows, st);
+        if (e != hipSuccess) return hip_check(e, "scan ahead");
+    }
+    return 0;
 }
 
 int ncf_build_index(const ncf_shape_t* s, const ncf_hyper_t* h, const int32_t* users, const int32_t* items,
@@ -1009,7 +1065,8 @@ int ncf_lazy_flush(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* optim,
     hipError_t e = ncf::launch_emb_catchup(*s, L, ws, model->emb, optim->emb_m, optim->emb_v, optim->row_step,
                                            optim->step, *h, true, st);
     if (e != hipSuccess) return hip_check(e, "flush");
-    return hip_check(ncf::launch_row_step_fill(optim->row_step, s->num_rows, optim->step, st), "row-step fill");
+    return hip_check(ncf::launch_row_step_fill(optim->row_step, ncf::lazy_bound(*s, *h), optim->step, st),
+                     "row-step fill");
 }
 
 // ------------------------------------------------------------ negative sampling

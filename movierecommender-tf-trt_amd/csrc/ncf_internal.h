@@ -275,6 +275,11 @@ inline void launch(void (*k)(KArgs...), dim3 grid, dim3 block, size_t shmem, hip
 // rows by owner first: key = (g % world) * S + g / world.
 inline int64_t shard_rows_of(int64_t R, int world) { return world > 0 ? (R + world - 1) / world : R; }
 
+// Rows under deferred exact decay (hyper->lazy_rows; 0 = every row of the table).
+inline int64_t lazy_bound(const ncf_shape_t& s, const ncf_hyper_t& h) {
+    return h.lazy_rows > 0 && h.lazy_rows < s.num_rows ? (int64_t)h.lazy_rows : s.num_rows;
+}
+
 // Which ids a forward/backward kernel reads: table rows (user u -> row u, item v -> row
 // ibase + v, bounds ubound/ibound), or the compact unique-row ids of a row-sharded plan.
 struct IdSpace {
@@ -425,6 +430,8 @@ hipError_t launch_mlp_update(const ncf_shape_t& s, const WsLayout& L, void* ws, 
                              float* summary = nullptr, MlpDeferred* defer = nullptr);
 hipError_t launch_emb_reg(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, int64_t rows,
                           float lam, hipStream_t st);
+// the next batch's per-block key scan (k_scan_local<true>) over counts taken ahead, alone
+hipError_t launch_scan_ahead(const WsLayout& L, void* ws, int64_t keys, hipStream_t st);
 // scan_ahead: the same launch also runs the next batch's per-block key scan (k_scan_local<true>
 // over the counts the touched update took ahead)
 hipError_t launch_stats(const WsLayout& L, void* ws, const float* summary, int nreg_emb, int nreg_mlp,

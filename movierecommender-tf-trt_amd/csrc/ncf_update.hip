@@ -293,6 +293,7 @@ struct StaleGate {
     int64_t m;                 // 2 * batch contributions
     int32_t U, I;
     int32_t* row_step;
+    int64_t lazy_rows;         // rows [0, lazy_rows) are under deferred decay
 };
 
 __device__ __forceinline__ void stale_replay_body(float* __restrict__ embf, float* __restrict__ mf,
@@ -310,6 +311,7 @@ __device__ __forceinline__ void stale_replay_body(float* __restrict__ embf, floa
             const int64_t i = c >> 1;
             const int id = (c & 1) ? sg.items[i] : sg.users[i];
             if ((unsigned)id < (unsigned)((c & 1) ? sg.I : sg.U)) key = (c & 1) ? sg.U + id : id;
+            if (key >= sg.lazy_rows) key = -1;
         }
         bool claim = false;
         int s0 = t;
@@ -394,7 +396,8 @@ __device__ __forceinline__ void catchup_body(float4* __restrict__ emb, float4* _
         for (int j = 0; j < kRep; ++j) {
             const int64_t i = i0 + j * pstride;
             r[j] = i < n ? (ALL ? i : list[i]) : 0;
-            sr[j] = i < n ? row_step[r[j]] : t;
+            // R: rows [0, R) are under deferred decay (touched rows past it are swept densely)
+            sr[j] = i < n && (ALL || r[j] < R) ? row_step[r[j]] : t;
         }
         for (int q = q0; q < W2; q += lanes_per_row) {  // element pair q: elements 2q, 2q + 1
             const f32x2 z2 = {0.f, 0.f};
@@ -436,6 +439,7 @@ __device__ __forceinline__ void catchup_body(float4* __restrict__ emb, float4* _
     const float4 zero = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int64_t i = wave * rl.rpw + rl.sub; i < n; i += waves * rl.rpw) {
         const int64_t r = ALL ? i : list[i];
+        if (!ALL && r >= R) continue;
         const int s = row_step[r];
         if (s >= t) continue;
         for (uint32_t q = rl.q; q < w4; q += rl.qstep) {
@@ -462,7 +466,7 @@ __global__ __launch_bounds__(kBlock) void k_emb_flush(float4* __restrict__ emb, 
                                                       const int32_t* __restrict__ step, float lr, float b1, float b2,
                                                       float eps) {
     const SortAhead so{0, nullptr, 0, nullptr, 0, nullptr, nullptr};
-    const StaleGate sg{nullptr, nullptr, 0, 0, 0, nullptr};
+    const StaleGate sg{nullptr, nullptr, 0, 0, 0, nullptr, 0};
     catchup_body<true>(emb, m4, v4, w4, nullptr, nullptr, R, row_step, step, lr, b1, b2, eps, so, sg);
 }
 
@@ -563,6 +567,8 @@ struct CountAhead {
     int replay;                // 1: also catch the next batch's stale rows up (catch-up ahead)
     int fold;                  // user-row folding of the next batch's index (fold_of)
     int per;                   // contributions per count block and pass (16, 32 or 64)
+    int64_t lazy_rows;         // rows [0, lazy_rows) are under deferred decay: only they are
+                               // updated here and caught up ahead (the rest are swept densely)
 };
 
 // the dense layers' Adam (k_mlp_update<ADAM>'s work) in blocks >= nupd + ncount of the same launch
@@ -644,7 +650,7 @@ __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_tou
                 int s0 = 0;
                 // the row's step goes out with its offsets (one memory round trip, not two)
                 int o0 = 0, o1 = 0, sv = t;
-                if (ca.replay && ok) {
+                if (ca.replay && ok && key < ca.lazy_rows) {
                     o0 = offs[key];
                     o1 = offs[key + 1];
                     sv = row_step[key];
@@ -733,8 +739,10 @@ __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_tou
             const int2 ocn = i + stride < n ? toc[i + stride] : make_int2(0, 0);
             const int o = oc.x;
             const int c = oc.y;
-            const int k = NCF_CATCHUP_P_ONLY ? t - 1 - row_step[r] : 0;  // m/v decay steps still owed
-            for (uint32_t q = rl.q; q < w4; q += rl.qstep) {
+            // rows past lazy_rows (the list is ascending: its tail) are the caller's dense sweep's
+            const bool mine = r < ca.lazy_rows;
+            const int k = NCF_CATCHUP_P_ONLY && mine ? t - 1 - row_step[r] : 0;  // m/v decay steps still owed
+            for (uint32_t q = rl.q; mine && q < w4; q += rl.qstep) {
                 const size_t e = (size_t)r * w4 + q;
                 // the row's state does not depend on the gradient chain: its loads go out first
                 float4 p = emb[e], m = m4[e], v = v4[e];
@@ -759,7 +767,7 @@ __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_tou
                 st_stream(&m4[e], m);
                 st_stream(&v4[e], v);
             }
-            if (rl.q == 0) row_step[r] = t;
+            if (rl.q == 0 && mine) row_step[r] = t;
             r = rn;
             oc = ocn;
         }
@@ -1044,6 +1052,21 @@ __global__ __launch_bounds__(kBlock) void k_stats_scan(const float* __restrict__
     }
 }
 
+// The next batch's per-block key scan alone (k_stats_scan's blocks >= 1), for a counting-ahead
+// update that has no stats launch of its own behind it (user-partitioned data parallelism).
+__global__ __launch_bounds__(kBlock) void k_scan_ahead(ScanAhead sc) {
+    scan_local_body<true>(sc.cnt, sc.r1, sc.offs, sc.tot, sc.uloc, sc.utot, (int)blockIdx.x);
+}
+
+hipError_t launch_scan_ahead(const WsLayout& L, void* ws, int64_t keys, hipStream_t st) {
+    const int64_t r1 = keys + 1;
+    const int nscan = (int)((r1 + kScanBlock - 1) / kScanBlock);
+    ScanAhead sc{at<const int32_t>(ws, L.cnt), r1, at<int32_t>(ws, L.offs_local), at<int32_t>(ws, L.tot),
+                 at<int32_t>(ws, L.uloc), at<int32_t>(ws, L.utot)};
+    launch(k_scan_ahead, nscan, kBlock, 0, st, sc);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------
 
 static L2Table make_l2_table(const ncf_shape_t& s, const ncf_hyper_t& h) {
@@ -1110,7 +1133,8 @@ hipError_t launch_emb_catchup(const ncf_shape_t& s, const WsLayout& L, void* ws,
     const int64_t R = s.num_rows;
     const int64_t nmax = R < 2 * L.max_batch ? R : 2 * L.max_batch;
     SortAhead so{0, nullptr, 0, nullptr, 0, nullptr, at<int32_t>(ws, L.err)};
-    const StaleGate nogate{nullptr, nullptr, 0, 0, 0, nullptr};
+    const StaleGate nogate{nullptr, nullptr, 0, 0, 0, nullptr, 0};
+    const int64_t bound = lazy_bound(s, h);  // rows under deferred decay
     unsigned nsort = 0;
     size_t lds = 0;
     if (sort_lists && !all_rows) {
@@ -1134,13 +1158,13 @@ hipError_t launch_emb_catchup(const ncf_shape_t& s, const WsLayout& L, void* ws,
         StaleGate sg = nogate;
         unsigned ngate = 0;
         if (h.optimizer == NCF_OPT_ADAM && users && items && n > 0) {
-            sg = StaleGate{users, items, 2 * n, s.num_users, s.num_items, row_step};
+            sg = StaleGate{users, items, 2 * n, s.num_users, s.num_items, row_step, bound};
             ngate = 64;
         }
         if (nsort + ngate) {
             so.ncatch = (int)ngate;
             launch(k_emb_catchup, ngate + nsort, kBlock, lds, st, (float4*)emb, (float4*)m, (float4*)v, w4,
-                   at<const int32_t>(ws, L.touched), at<const int32_t>(ws, L.nuniq), R, (const int32_t*)row_step,
+                   at<const int32_t>(ws, L.touched), at<const int32_t>(ws, L.nuniq), bound, (const int32_t*)row_step,
                    step, h.lr, h.beta_1, h.beta_2, h.epsilon, so, sg);
         }
         return hipGetLastError();
@@ -1157,14 +1181,14 @@ hipError_t launch_emb_catchup(const ncf_shape_t& s, const WsLayout& L, void* ws,
     auto cgrid = [&](int64_t rows, int64_t cap) { return row_grid(rows, w4, cap); };
 #endif
     if (all_rows) {
-        launch(k_emb_flush, cgrid(R, 8192), kBlock, 0, st, (float4*)emb, (float4*)m, (float4*)v, w4, R,
+        launch(k_emb_flush, cgrid(bound, 8192), kBlock, 0, st, (float4*)emb, (float4*)m, (float4*)v, w4, bound,
                (const int32_t*)row_step, step, h.lr, h.beta_1, h.beta_2, h.epsilon);
     } else {
         const unsigned ncatch = cgrid(nmax, NCF_CATCHUP_GRID_MAX);
         so.ncatch = (int)ncatch;
         launch(k_emb_catchup, ncatch + nsort, kBlock, lds, st, (float4*)emb, (float4*)m, (float4*)v, w4,
-               at<const int32_t>(ws, L.touched), at<const int32_t>(ws, L.nuniq), R, (const int32_t*)row_step, step,
-               h.lr, h.beta_1, h.beta_2, h.epsilon, so, nogate);
+               at<const int32_t>(ws, L.touched), at<const int32_t>(ws, L.nuniq), bound, (const int32_t*)row_step,
+               step, h.lr, h.beta_1, h.beta_2, h.epsilon, so, nogate);
     }
     return hipGetLastError();
 }
@@ -1180,7 +1204,7 @@ hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, vo
                                      int64_t n_next, const MlpDeferred* mlp, int next_fold) {
     const bool replay_ahead = next_users != nullptr && NCF_CATCHUP_AHEAD;
     const uint32_t w4 = (uint32_t)(s.row_width / 4);
-    const uint32_t n4 = (uint32_t)(s.num_rows * w4);
+    const uint32_t n4 = (uint32_t)(lazy_bound(s, h) * w4);  // SGD: the rows under deferred decay
     const int32_t* offs = at<int32_t>(ws, L.offs);
     const int32_t* list = at<int32_t>(ws, L.list);
     const float4* gs = at<const float4>(ws, L.gs);
@@ -1193,7 +1217,7 @@ hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, vo
         const int per = mc >= 65536 ? NCF_COUNT_PER_MAX : mc >= 32768 ? 32 : 16;
         const unsigned ncount = mc > 0 ? (unsigned)((mc + per - 1) / per < 4096 ? (mc + per - 1) / per : 4096) : 0u;
         CountAhead ca{(int)nupd, (int)ncount, next_users, next_items, mc, s.num_users, s.num_items,
-                      at<int32_t>(ws, L.cnt), replay_ahead ? 1 : 0, next_fold, per};
+                      at<int32_t>(ws, L.cnt), replay_ahead ? 1 : 0, next_fold, per, lazy_bound(s, h)};
         MlpTail mt{};
         if (mlp) {
             mt = MlpTail{(s.mlp_params + kBlock - 1) / kBlock, mlp->p, mlp->m, mlp->v, s.mlp_params, mlp->slabs,

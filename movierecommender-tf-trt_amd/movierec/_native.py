@@ -56,7 +56,8 @@ class NcfOptim(ctypes.Structure):
 class NcfHyper(ctypes.Structure):
     _fields_ = [("optimizer", _i32), ("lr", _f32), ("beta_1", _f32), ("beta_2", _f32), ("epsilon", _f32),
                 ("l2", _f32 * NCF_MAX_LAYERS), ("group", _i32), ("k", _i32), ("inv_batch", _f32),
-                ("force_generic", _i32), ("index_ready", _i32), ("mlp_bf16", _i32), ("reserved", _i32 * 4)]
+                ("force_generic", _i32), ("index_ready", _i32), ("mlp_bf16", _i32), ("lazy_rows", _i32),
+                ("reserved", _i32 * 3)]
 
 
 class NcfSamplerData(ctypes.Structure):
@@ -92,6 +93,11 @@ _SIGNATURES = {
                                        ctypes.c_size_t, _vp]),
     "ncf_fb_kernel": (ctypes.c_int, [_P(NcfShape), _P(NcfHyper), _i64]),
     "ncf_build_index": (ctypes.c_int, [_P(NcfShape), _P(NcfHyper), _vp, _vp, _i64, _vp, ctypes.c_size_t, _vp]),
+    "ncf_forward_backward_part_lazy": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _vp,
+                                                      _vp, _vp, _i64, _vp, _vp, _vp, _vp, _i32, _vp, ctypes.c_size_t,
+                                                      _vp]),
+    "ncf_update_rows_lazy": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _i64, _vp, _vp,
+                                            _i64, _vp, ctypes.c_size_t, _vp]),
     "ncf_lazy_flush": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _vp, ctypes.c_size_t,
                                       _vp]),
     "ncf_apply_update": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _i64, _i64, _vp, _vp,

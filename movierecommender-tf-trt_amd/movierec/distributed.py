@@ -44,6 +44,46 @@ import torch
 import torch.distributed as dist
 
 
+def ensure_process_group(world_size, backend=None):
+    """The process group of a ``world_size``-rank run (``MovierecModel`` params ``world_size``):
+    the one already initialised, or one formed from torchrun's environment (RANK, WORLD_SIZE,
+    LOCAL_RANK, MASTER_ADDR/PORT).  Backend: ``nccl`` (RCCL over xGMI) when the GPUs are visible,
+    else ``gloo``; each rank drives GPU LOCAL_RANK.  Returns this process's rank."""
+    import os
+    if not dist.is_initialized():
+        env_world = int(os.environ.get("WORLD_SIZE", "1"))
+        if env_world != world_size:
+            raise ValueError("world_size %d but WORLD_SIZE=%d: launch one process per GPU, e.g. "
+                             "python -m torch.distributed.run --nproc-per-node %d ..." % (world_size, env_world,
+                                                                                        world_size))
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if torch.cuda.is_available():
+            torch.cuda.set_device(local if backend == "nccl" else 0)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    if dist.get_world_size() != world_size:
+        raise ValueError("world_size %d but the process group has %d ranks" % (world_size, dist.get_world_size()))
+    return dist.get_rank()
+
+
+def all_reduce_min(x, group=None):
+    """min over ranks of a host int (the number of steps every rank can run)."""
+    t = torch.tensor([int(x)], dtype=torch.int64)
+    if dist.get_backend(group) == "nccl":
+        t = t.cuda()
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return int(t.item())
+
+
+def all_reduce_sum_(t, group=None):
+    """In-place sum over ranks of a (device) tensor."""
+    _all_reduce(t, group)
+
+
 def _reduce_scatter(out, inp, group):
     try:
         dist.reduce_scatter_tensor(out, inp, op=dist.ReduceOp.SUM, group=group)
@@ -264,6 +304,10 @@ class UserPartitionedDataParallel(object):
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         U, R, W = int(engine.num_users), int(engine.num_rows), int(engine.row_width)
+        lazy = getattr(engine, "lazy_rows", None)
+        if getattr(engine, "row_step", None) is not None and lazy != U:
+            raise ValueError("a deferred-decay engine for user-partitioned training needs lazy_rows = its %d users "
+                             "(the replicated item rows are swept every step)" % U)
         _, mg0, sm0 = engine.alloc_grads(rows=0)
         P, S = mg0.numel(), sm0.numel()
         dev = engine.emb.device
@@ -296,9 +340,14 @@ class UserPartitionedDataParallel(object):
         eng.forward_backward_part(users, items, labels, group=group, k=k, inv_batch=inv, shared_row_begin=U,
                                   grads=self.grads, reg_rows=self.reg_rows, include_dense_reg=self.rank == 0)
         work = _all_reduce_async(self.shared, self.group)
-        eng.update_rows(0, U, inv)               # own users: overlaps the all-reduce
-        if next_batch is not None and hasattr(eng, "build_index"):
-            eng.build_index(*next_batch, group)  # so does the next step's index
+        if getattr(eng, "lazy_rows", None) == U and eng.row_step is not None:
+            # deferred decay of the own users: the touched ones' update, and the next batch's index
+            # counted + its own rows caught up ahead, in one launch under the all-reduce
+            eng.update_rows(0, U, inv, next_batch=next_batch)
+        else:
+            eng.update_rows(0, U, inv)               # own users: overlaps the all-reduce
+            if next_batch is not None and hasattr(eng, "build_index"):
+                eng.build_index(*next_batch, group)  # so does the next step's index
         if work is not None:
             work.wait()
         eng.apply_update(self.grads, inv, rows=(U, R - U), moments_by_row=True)

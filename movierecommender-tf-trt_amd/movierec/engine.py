@@ -56,11 +56,14 @@ class NCFEngine(object):
 
     def __init__(self, num_users, num_items, layers_sizes, gmf_dim=0, max_batch=65536, device=None,
                  optimizer="adam", lr=0.001, beta_1=0.9, beta_2=0.999, layers_l2reg=None,
-                 force_generic=False, force_layered=False, lazy_adam=False, fb_kernel=None, precision="fp32"):
+                 force_generic=False, force_layered=False, lazy_adam=False, fb_kernel=None, precision="fp32",
+                 lazy_rows=None):
         """``lazy_adam``: deferred exact decay (``ncf_optim_t.row_step``) — a training step updates
         only the batch's rows, the others catch up on their missed zero-gradient steps when next
         touched or read; bitwise the dense Keras sweep (F5).  Needs layers_l2reg[0] == 0; the
-        table is flushed before every read (predict, evaluate, scoring, weights export)."""
+        table is flushed before every read (predict, evaluate, scoring, weights export).
+        ``lazy_rows``: only rows [0, lazy_rows) are deferred (user-partitioned data parallelism:
+        the rank's own users; the replicated item rows are swept every step)."""
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device())
         self.device = torch.device(device)
@@ -89,7 +92,11 @@ class NCFEngine(object):
             self.mlp_m = torch.zeros_like(self.mlp)
             self.mlp_v = torch.zeros_like(self.mlp)
             self.step = torch.zeros(1, dtype=torch.int32, device=dev)
-            self.row_step = torch.zeros(s.num_rows, dtype=torch.int32, device=dev) if lazy_adam else None
+            self.lazy_rows = None if lazy_rows is None else int(lazy_rows)
+            if self.lazy_rows is not None and not 0 < self.lazy_rows <= s.num_rows:
+                raise ValueError("lazy_rows must be in [1, %d]" % s.num_rows)
+            nlazy = s.num_rows if self.lazy_rows is None else self.lazy_rows
+            self.row_step = torch.zeros(nlazy, dtype=torch.int32, device=dev) if lazy_adam else None
             self._dirty = False
             self.stats = torch.zeros(N.NCF_NUM_STATS, dtype=torch.float64, device=dev)
             self.val_stats = torch.zeros(N.NCF_NUM_STATS, dtype=torch.float64, device=dev)
@@ -100,6 +107,7 @@ class NCFEngine(object):
             self._ensure_ws(int(max_batch))
         self.model_s = N.NcfModel(self.emb.data_ptr(), self.mlp.data_ptr())
         self.hyper = N.NcfHyper()
+        self.hyper.lazy_rows = self.lazy_rows or 0
         self._bind_optim()
         self.set_hyper(optimizer, lr, beta_1, beta_2, layers_l2reg or [0.0] * len(self.layers))
         if fb_kernel not in (None, "tile", "unit", "wave"):
@@ -151,6 +159,8 @@ class NCFEngine(object):
         """Flush and return to the dense sweep (data-parallel paths update every row)."""
         self.flush()
         self.row_step = None
+        self.lazy_rows = None
+        self.hyper.lazy_rows = 0
         self._bind_optim()
 
     def set_hyper(self, optimizer, lr, beta_1=0.9, beta_2=0.999, layers_l2reg=None, group=None, k=None):
@@ -251,6 +261,10 @@ class NCFEngine(object):
         following call (deferred-decay Adam): their index counts are taken inside this step's
         touched-row update, and the next call skips its count kernel if it passes exactly these
         tensors (identity-checked; their contents must not change in between)."""
+        if self.lazy_rows is not None and self.lazy_rows < self.num_rows:
+            raise ValueError("this engine defers the decay of its first %d rows only (user-partitioned data "
+                             "parallelism): train it through forward_backward_part / update_rows / apply_update"
+                             % self.lazy_rows)
         u, i, y = self._ids(users), self._ids(items), self._labels(labels)
         n = u.numel()
         self._ensure_ws(n)
@@ -414,7 +428,12 @@ class NCFEngine(object):
                               probs_out=None, reg_rows=None, include_dense_reg=True):
         """``forward_backward`` with the dense embedding gradient written for the replicated rows
         [shared_row_begin, num_rows) only (``grads[0]`` indexed from that row); the own rows are
-        updated from the per-sample gradients by ``update_rows`` (user-partitioned DP)."""
+        updated from the per-sample gradients by ``update_rows`` (user-partitioned DP).  With
+        ``lazy_rows == shared_row_begin`` the own rows are under deferred decay: the batch's are
+        caught up first (or were, ahead, by the previous ``update_rows(..., next_batch=)``)."""
+        if self.row_step is not None and self.lazy_rows == int(shared_row_begin):
+            return self._forward_backward_part_lazy(users, items, labels, group, k, inv_batch, grads, probs_out,
+                                                    include_dense_reg)
         self._discard_counted()
         if self.row_step is not None:
             self.disable_lazy()
@@ -439,6 +458,30 @@ class NCFEngine(object):
             self._prebuilt = None
         self._part_n = n
 
+    def _forward_backward_part_lazy(self, users, items, labels, group, k, inv_batch, grads, probs_out,
+                                    include_dense_reg):
+        u, i, y = self._ids(users), self._ids(items), self._labels(labels)
+        n = u.numel()
+        self._ensure_ws(n)
+        h = self.hyper
+        h.group, h.k, h.inv_batch = int(group), int(k), float(inv_batch)
+        pc = self._counted
+        ready = pc is not None and _same_ids(pc, u, i, n, h.group)
+        if pc is not None and not ready:
+            self._discard_counted()
+        self._counted = None
+        h.index_ready = 2 if ready else 0
+        eg, mg, sm = grads
+        try:
+            N.check(N.lib().ncf_forward_backward_part_lazy(
+                ctypes.byref(self.shape), ctypes.byref(self.model_s), ctypes.byref(self.optim_s), ctypes.byref(h),
+                N.ptr(u), N.ptr(i), N.ptr(y), n, N.ptr(eg), N.ptr(mg), N.ptr(sm), N.ptr(probs_out),
+                1 if include_dense_reg else 0, N.ptr(self.ws), self.ws_bytes, N.stream_handle(self.device)))
+        finally:
+            h.index_ready = 0
+        self._part_n = n
+        self._dirty = True
+
     def build_index(self, users, items, group):
         """Build the contribution index of the NEXT ``forward_backward_part`` batch now (e.g. under
         the current step's all-reduce); call after this step's ``update_rows``.  That call must
@@ -460,13 +503,31 @@ class NCFEngine(object):
         # holds the tensors: their memory stays theirs
         self._prebuilt = (u, i, n, u._version, i._version, h.group)
 
-    def update_rows(self, row_begin, row_count, inv_batch):
+    def update_rows(self, row_begin, row_count, inv_batch, next_batch=None):
         """Optimizer step of rows [row_begin, row_begin + row_count) from the per-sample gradient
-        rows of the last ``forward_backward_part`` (step counter not advanced)."""
+        rows of the last ``forward_backward_part`` (step counter not advanced).  Deferred decay
+        (``lazy_rows == row_count``, ``row_begin == 0``): the batch's touched own rows only, and
+        ``next_batch`` = (users, items) device int32 tensors of the next step, whose index is counted
+        and whose own rows are caught up in the same launch (pass the same tensors next step)."""
         n = getattr(self, "_part_n", None)
         if n is None:
             raise RuntimeError("update_rows needs a preceding forward_backward_part")
         self.hyper.inv_batch = float(inv_batch)
+        if self.row_step is not None and self.lazy_rows == int(row_count) and int(row_begin) == 0:
+            nu = ni = None
+            if next_batch is not None and self.hyper.optimizer == N.NCF_OPT_ADAM:
+                nu, ni = next_batch
+                if not (torch.is_tensor(nu) and torch.is_tensor(ni) and nu.is_cuda and ni.is_cuda and
+                        nu.dtype == torch.int32 and ni.dtype == torch.int32 and nu.is_contiguous() and
+                        ni.is_contiguous() and nu.numel() == ni.numel() == n):
+                    nu = ni = None
+            N.check(N.lib().ncf_update_rows_lazy(ctypes.byref(self.shape), ctypes.byref(self.model_s),
+                                                 ctypes.byref(self.optim_s), ctypes.byref(self.hyper), int(n),
+                                                 N.ptr(nu), N.ptr(ni), n if nu is not None else 0, N.ptr(self.ws),
+                                                 self.ws_bytes, N.stream_handle(self.device)))
+            if nu is not None:
+                self._counted = (nu, ni, n, nu._version, ni._version, self.hyper.group)
+            return
         N.check(N.lib().ncf_update_rows(ctypes.byref(self.shape), ctypes.byref(self.model_s),
                                         ctypes.byref(self.optim_s), ctypes.byref(self.hyper), int(n), int(row_begin),
                                         int(row_count), N.ptr(self.ws), self.ws_bytes,
@@ -477,11 +538,11 @@ class NCFEngine(object):
         ``emb_grad`` (default grads[0]; indexed from ``begin``), every dense parameter.
         ``moments_by_row``: the Adam moments cover the whole table (indexed by row), not just
         the range (user-partitioned DP)."""
-        if self.row_step is not None:
-            self.disable_lazy()
         eg, mg, sm = grads
         eg = eg if emb_grad is None else emb_grad
         r0, rc = (0, self.num_rows) if rows is None else rows
+        if self.row_step is not None and not (self.lazy_rows is not None and r0 >= self.lazy_rows):
+            self.disable_lazy()   # a dense update of deferred rows: settle them first
         self.hyper.inv_batch = float(inv_batch)
         optim = self.optim_s
         if moments_by_row and r0:

@@ -59,6 +59,7 @@ OUTPUT_RANK = "rank"
 METRIC_VAL_DCG = "val_{}_{}".format(OUTPUT_PRED, DCG)
 
 WEIGHTS_SUFFIX = "_weights.safetensors"
+RUNTIME_KEYS = ("world_size", "dist_backend")
 
 
 class _Layer(object):
@@ -76,8 +77,9 @@ class NCFNetwork(object):
     """Stands where the reference's ``keras.Model`` stood (``model.py:194``):
     two int inputs (user, item), outputs ``[output (B,1), rank (B/(n+1), n+1)]``."""
 
-    def __init__(self, engine, layers_sizes, gmf_dim, num_negs_train, num_negs_eval, name):
+    def __init__(self, engine, layers_sizes, gmf_dim, num_negs_train, num_negs_eval, name, dp=None):
         self.engine = engine
+        self.dp = dp          # UserPartitionedDataParallel when world_size > 1
         self.name = name
         self._negs = (num_negs_train, num_negs_eval)
         self.learning_phase = 0
@@ -118,10 +120,27 @@ class NCFNetwork(object):
         raise ValueError("No such layer: " + name)
 
     def get_weights(self):
+        """The whole model's weights.  Data-parallel (world_size > 1): gathered from every rank's
+        users (a collective: every rank calls it)."""
+        if self.dp is not None:
+            return self.dp.keras_weights()
         return self.engine.keras_weights()
 
     def set_weights(self, w):
+        """Load the whole model's weights (data-parallel: this rank keeps its users' rows)."""
+        if self.dp is not None:
+            from .distributed import partition_keras_weights
+            w = partition_keras_weights(w, self.dp.world, self.dp.rank)
         self.engine.set_keras_weights(w)
+
+    def local_user_ids(self, users):
+        """Data-parallel: global ids of this rank's users (u % world == rank) -> local rows."""
+        if self.dp is None:
+            return users
+        u = np.asarray(users)
+        if u.size and np.any(u % self.dp.world != self.dp.rank):
+            raise ValueError("user ids not owned by rank %d of %d (u %% world != rank)" % (self.dp.rank, self.dp.world))
+        return u // self.dp.world
 
     def count_params(self):
         return sum(int(np.prod(a.shape)) for a in self.get_weights().values())
@@ -138,6 +157,7 @@ class NCFNetwork(object):
         """``[output (B,1) float32, rank (B/(n+1), n+1) int32]`` in the current
         learning phase (RankLayer group size, model.py:347)."""
         users, items = x
+        users = self.local_user_ids(users)
         self.engine.check_ids(users, items)
         p = self.engine.predict(users, items)
         group = self._negs[0 if self.learning_phase else 1] + 1
@@ -145,7 +165,9 @@ class NCFNetwork(object):
         return [p.cpu().numpy().reshape(-1, 1), rank.cpu().numpy()]
 
     def save_weights(self, path):
-        save_tensors(path, self.get_weights())
+        w = self.get_weights()          # collective when data-parallel
+        if self.dp is None or self.dp.rank == 0:
+            save_tensors(path, w)
 
     def load_weights(self, path):
         self.set_weights(load_tensors(path))
@@ -213,6 +235,16 @@ class MovierecModel(object):
         # "bf16": the MLP tower's matrix products take bf16 operands (fp32 accumulation, master
         # weights and Adam) — BASELINE config B's precision; default fp32 (the reference's)
         self._precision = params.get("precision", "fp32")
+        # data parallelism (new; SURVEY §5 "world_size"): one process per GPU under torchrun, the
+        # ratings partitioned by user (rank r trains users u % world == r, as local ids u // world,
+        # movierec.distributed.UserPartitionedDataParallel); 1 = the reference's single device
+        self._world_size = int(params.get("world_size", 1))
+        if self._world_size < 1:
+            raise ValueError("world_size must be >= 1, found {}".format(self._world_size))
+        self._rank = 0
+        if self._world_size > 1:
+            from .distributed import ensure_process_group
+            self._rank = ensure_process_group(self._world_size, params.get("dist_backend"))
 
         try:
             os.makedirs(output_dir)
@@ -221,7 +253,9 @@ class MovierecModel(object):
         self.name = model_name
         self._model_weights_path = self.get_model_weights_path(output_dir, model_name)
         self._params_path = self.get_params_json_path(output_dir, model_name)
-        self._serialized_params = json.dumps(params)
+        # the run's layout (world_size, dist_backend) is not part of the model: a saved model loads
+        # anywhere, on one device or another rank count
+        self._serialized_params = json.dumps({k: v for k, v in params.items() if k not in RUNTIME_KEYS})
         self._output_model_checkpoints = os.path.join(
             output_dir, "{}-checkpoint-{{epoch:02d}}-{{val_loss:.2f}}.safetensors".format(model_name))
         self.verbose = verbose
@@ -235,14 +269,26 @@ class MovierecModel(object):
         glorot_uniform embeddings and hidden kernels, lecun_uniform output
         kernel, zero biases (model.py:161-188)."""
         from .engine import NCFEngine
-        eng = NCFEngine(self._num_users, self._num_items, self._layers_sizes, self._gmf_dim,
+        world, rank = self._world_size, self._rank
+        lazy = bool(params_lazy(self._layers_l2reg))
+        # data-parallel: this rank's users only (local row u // world), every item
+        n_users = self._num_users if world == 1 else (self._num_users - rank + world - 1) // world
+        eng = NCFEngine(n_users, self._num_items, self._layers_sizes, self._gmf_dim,
                         max_batch=self._max_batch, optimizer=self._optimizer, lr=self._lr, beta_1=self._beta_1,
-                        beta_2=self._beta_2, layers_l2reg=self._layers_l2reg,
-                        lazy_adam=bool(params_lazy(self._layers_l2reg)), precision=self._precision)
-        eng.set_keras_weights(initial_weights(self._num_users, self._num_items, self._layers_sizes, self._gmf_dim,
-                                              self._seed))
+                        beta_2=self._beta_2, layers_l2reg=self._layers_l2reg, lazy_adam=lazy,
+                        precision=self._precision, lazy_rows=n_users if world > 1 and lazy else None)
+        w = initial_weights(self._num_users, self._num_items, self._layers_sizes, self._gmf_dim, self._seed)
+        dp = None
+        if world > 1:
+            from .distributed import UserPartitionedDataParallel, partition_keras_weights
+            w = partition_keras_weights(w, world, rank)
+            eng.set_keras_weights(w)
+            dp = UserPartitionedDataParallel(eng)
+            dp.broadcast_parameters()   # one replicated item table and dense layers (unseeded init)
+        else:
+            eng.set_keras_weights(w)
         return NCFNetwork(eng, self._layers_sizes, self._gmf_dim, self._num_negs_per_pos,
-                          self._num_negs_per_pos_eval, self.name)
+                          self._num_negs_per_pos_eval, self.name, dp=dp)
 
     def compile_model(self):
         """Optimizer and metrics (model.py:197-215): the optimizer state lives
@@ -272,7 +318,9 @@ class MovierecModel(object):
 
     # ------------------------------------------------------------ persistence
     def save(self):
-        self.model.save_weights(self._model_weights_path)
+        self.model.save_weights(self._model_weights_path)   # collective when data-parallel
+        if self._rank != 0:
+            return
         logging.info("Model weights saved to: {}".format(self._model_weights_path))
         with open(self._params_path, "w") as f_out:
             f_out.write(self._serialized_params)
@@ -299,21 +347,45 @@ class MovierecModel(object):
         of the Sequence (batch order shuffled with python ``random`` when
         ``shuffle``, as Keras' OrderedEnqueuer does), ``on_epoch_end``, then a
         validation pass; EarlyStopping(val_output_dcg, max, patience,
-        restore_best_weights) and best-only checkpoints.  Returns a History."""
+        restore_best_weights) and best-only checkpoints.  Returns a History.
+
+        Batches go to the device one step ahead: each step's launch counts the next batch's
+        index (and, under deferred decay, catches its rows up) while it updates the current one.
+        Data-parallel (``world_size`` > 1): every rank passes ITS generators (its users' ratings,
+        local user ids u // world); each step trains the ranks' batches together as one global
+        batch (UserPartitionedDataParallel: one all-reduce), all ranks run the same number of
+        steps (the smallest generator's), validation metrics are averaged over every rank's
+        batches, and the early-stopping / checkpoint decisions are the same on every rank."""
         eng = self.model.engine
+        dp = self.model.dp
         hist = History()
         best, wait, best_w = -math.inf, 0, None
         group_t = self._num_negs_per_pos + 1
         group_v = self._num_negs_per_pos_eval + 1
+        n_train = len(train_data_generator)
+        n_val = len(validation_data_generator) if validation_data_generator is not None else 0
+        if dp is not None:
+            from .distributed import all_reduce_min
+            n_train = all_reduce_min(n_train, dp.group)
+            n_val = all_reduce_min(n_val, dp.group) if validation_data_generator is not None else 0
         for epoch in range(epochs):
             self.model.learning_phase = 1
             eng.stats.zero_()
-            order = list(range(len(train_data_generator)))
+            order = list(range(n_train))
             if shuffle:
                 random.shuffle(order)
-            for (xu, xi), y in _prefetch(train_data_generator, order, prefetch):
-                eng.check_ids(xu, xi)
-                eng.train_step(xu, xi, y, group=group_t, k=self._k)
+            batches = _device_batches(train_data_generator, order, prefetch, eng)
+            cur = next(batches, None)
+            while cur is not None:
+                nxt = next(batches, None)
+                (xu, xi), y = cur
+                nb = (nxt[0][0], nxt[0][1]) if nxt is not None else None
+                if dp is not None:
+                    dp.train_step(xu, xi, y, group=group_t, k=self._k, global_batch=xu.numel() * dp.world,
+                                  next_batch=nb)
+                else:
+                    eng.train_step(xu, xi, y, group=group_t, k=self._k, next_batch=nb)
+                cur = nxt
             if hasattr(train_data_generator, "check_errors"):
                 train_data_generator.check_errors()
             eng.check_errors()
@@ -321,10 +393,11 @@ class MovierecModel(object):
             tr = eng.read_stats(eng.stats)
             self.model.learning_phase = 0
             eng.val_stats.zero_()
-            n_val = len(validation_data_generator) if validation_data_generator is not None else 0
-            for (xu, xi), y in _prefetch(validation_data_generator, list(range(n_val)), prefetch):
-                eng.check_ids(xu, xi)
+            for (xu, xi), y in _device_batches(validation_data_generator, list(range(n_val)), prefetch, eng):
                 eng.evaluate(xu, xi, y, group=group_v, k=self._k)
+            if dp is not None:
+                from .distributed import all_reduce_sum_
+                all_reduce_sum_(eng.val_stats, dp.group)
             va = eng.read_stats(eng.val_stats)
             # Keras' History keys of this two-output model: `loss` is the total (BCE + the L2
             # regularisers), `output_loss` the BCE of the `output` head alone; batch means averaged
@@ -336,7 +409,7 @@ class MovierecModel(object):
             hist.epoch.append(epoch)
             for key, val in logs.items():
                 hist.history.setdefault(key, []).append(float(val))
-            if self.verbose:
+            if self.verbose and self._rank == 0:
                 logging.info("Epoch %d/%d - %s", epoch + 1, epochs,
                              " - ".join("%s: %.4f" % kv for kv in logs.items()))
             current = logs.get(METRIC_VAL_DCG)
@@ -359,13 +432,18 @@ class MovierecModel(object):
         """Full-protocol evaluation (new): mean loss / HR@k / DCG@k (= NDCG@k,
         one relevant item per group) over every batch of ``generator``."""
         eng = self.model.engine
+        dp = self.model.dp
         k = self._k if k is None else int(k)
         group = generator.negatives_per_positive + 1
         stats = eng.val_stats.new_zeros(eng.val_stats.shape)
         n = len(generator) if batches is None else batches
-        for (xu, xi), y in _prefetch(generator, list(range(n)), 10):
-            eng.check_ids(xu, xi)
+        if dp is not None:
+            from .distributed import all_reduce_min, all_reduce_sum_
+            n = all_reduce_min(n, dp.group)
+        for (xu, xi), y in _device_batches(generator, list(range(n)), 10, eng):
             eng.evaluate(xu, xi, y, group=group, k=k, stats=stats)
+        if dp is not None:
+            all_reduce_sum_(stats, dp.group)   # every rank's batches: the mean over all of them
         return eng.read_stats(stats)
 
     def recommend(self, user_ids, k=10, precision="fp16"):
@@ -377,6 +455,7 @@ class MovierecModel(object):
         user_ids = np.asarray(user_ids).reshape(-1)
         if user_ids.size and (user_ids.min() < 0 or user_ids.max() >= self._num_users):
             raise ValueError("user id out of range [0, %d)" % self._num_users)
+        user_ids = self.model.local_user_ids(user_ids)   # data-parallel: this rank's users
         items, scores = self.model.engine.score_topk(user_ids, k=k, precision=precision)
         return items.cpu().numpy(), scores.cpu().numpy()
 
@@ -409,6 +488,26 @@ def _prefetch(gen, order, depth):
             raise item
         yield item
     t.join()
+
+
+def _device_batches(gen, order, depth, eng):
+    """``gen[i]`` for i in order, as device tensors ``([users int32, items int32], labels float32)``:
+    host batches are produced on one background thread (``_prefetch``), range-checked against the
+    engine's tables (TF's gather raises on out-of-range ids) and uploaded here; batches already on
+    the device (DeviceMovieLensDataGenerator) pass through."""
+    import torch
+    if gen is None:
+        return
+    dev = eng.device
+    for (xu, xi), y in _prefetch(gen, order, depth):
+        if not (torch.is_tensor(xu) and xu.is_cuda):
+            eng.check_ids(xu, xi)
+        up = [torch.as_tensor(np.ascontiguousarray(np.asarray(x).reshape(-1), dtype=np.int32)).to(dev)
+              if not (torch.is_tensor(x) and x.is_cuda and x.dtype == torch.int32) else x.reshape(-1).contiguous()
+              for x in (xu, xi)]
+        yy = y if torch.is_tensor(y) and y.is_cuda else torch.as_tensor(
+            np.ascontiguousarray(np.asarray(y).reshape(-1), dtype=np.float32)).to(dev)
+        yield up, yy.reshape(-1).to(torch.float32)
 
 
 def initial_weights(num_users, num_items, layers_sizes, gmf_dim=0, seed=None):

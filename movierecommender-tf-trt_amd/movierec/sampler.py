@@ -4,11 +4,10 @@ the HIP library (``ncf_sample_batch``).
 Same constructor, ``__len__`` (the F4 quirk included), ``on_epoch_end`` and batch layout as
 the reference generator (``data_pipeline.py:17-154``); ``__getitem__`` returns device tensors
 ``([x_user, x_item], y)`` (int32, int32, float32) ready for ``NCFEngine.train_step`` — no host
-sampling and no H2D copy per batch.  The epoch order is shuffled on the host with the same
-``np.random.shuffle`` call as the reference (``:152-154``) and uploaded once per epoch; the
-negatives come from the library's counter-based Philox stream (seed, epoch, batch), so they are
-reproducible but NOT numpy's stream: reference-exact batches remain available from the host
-``MovieLensDataGenerator``.
+sampling and no H2D copy per batch.  The epoch order (``:152-154``) is a device permutation
+(``torch.randperm``, seeded by (seed, epoch)); the negatives come from the library's
+counter-based Philox stream (seed, epoch, batch), so batches are reproducible but NOT numpy's
+stream: reference-exact batches remain available from the host ``MovieLensDataGenerator``.
 """
 
 import ctypes
@@ -58,9 +57,16 @@ class DeviceMovieLensDataGenerator(MovieLensDataGenerator):
                                       d["ptr"].data_ptr(), d["excl"].data_ptr(), self.num_users, self.num_items)
 
     def on_epoch_end(self):
-        super(DeviceMovieLensDataGenerator, self).on_epoch_end()
+        # the epoch's positive order (data_pipeline.py:152-154) is drawn on the device: numpy's
+        # shuffle of ml-20m's 20M positives takes about a second per epoch on the host (the
+        # batches are not the numpy stream anyway; the host generator keeps the exact mode)
         self.epoch += 1
-        self._order = torch.from_numpy(np.ascontiguousarray(self.indexes, dtype=np.int32)).to(self.device)
+        n = len(self.indexes)
+        if self.shuffle:
+            g = torch.Generator(device=self.device).manual_seed((self.seed * 1000003 + self.epoch) & 0x7FFFFFFFFFFF)
+            self._order = torch.randperm(n, generator=g, device=self.device).to(torch.int32)
+        else:
+            self._order = torch.arange(n, dtype=torch.int32, device=self.device)
 
     def __getitem__(self, idx):
         if self._dev is None:

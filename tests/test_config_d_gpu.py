@@ -19,8 +19,10 @@ and loss rel 2e-5, as tests/test_headline_parity_gpu.py; probabilities |dp| <= 2
 weights and <= 2e-6 * (1 + s) after s optimizer steps — the weights may drift by the tolerance
 above each step, and config D's 256-wide first layer (O(1) activations here) sums that drift over
 twice the inputs of config C's.
-Batches are drawn off the ReLU kinks (every hidden |z| >= 1e-6 under the oracle's weights of that
-step), as in the headline test; tests/test_headline_parity_gpu.py also covers unfiltered batches.
+Batches are drawn off the ReLU kinks (every hidden |z| beyond 64 fp32 ulps of its accumulation's
+magnitude under the oracle's weights of that step; config D's O(1) activations over 256 inputs
+put that near 1e-4), as the headline test does; tests/test_headline_parity_gpu.py also covers
+unfiltered batches.
 """
 
 import numpy as np
@@ -86,14 +88,19 @@ class Compact(object):
                 np.searchsorted(self.items, items).astype(np.int32))
 
 
-def _pre_activations(w, users, items):
+def _off_kinks(w, users, items, ulps=64):
+    """Samples whose every hidden pre-activation is more than ``ulps`` fp32 rounding units of its
+    accumulation's magnitude sum away from 0 (tests/test_headline_parity_gpu.py kink_samples):
+    fp32 and float64 then take the same side of every ReLU."""
     h = np.concatenate([w["user_embedding"][users], w["item_embedding"][items]], axis=1)
-    m = np.full(len(users), np.inf)
+    ok = np.ones(len(users), bool)
+    eps = float(np.finfo(np.float32).eps)
     for l in range(1, len(LAYERS)):
-        z = h @ w["hidden_%d/kernel" % l] + w["hidden_%d/bias" % l]
-        m = np.minimum(m, np.abs(z).min(axis=1))
+        W, b = w["hidden_%d/kernel" % l], w["hidden_%d/bias" % l]
+        z = h @ W + b
+        ok &= (np.abs(z) > ulps * eps * (np.abs(h) @ np.abs(W) + np.abs(b))).all(axis=1)
         h = np.maximum(z, 0)
-    return m
+    return ok
 
 
 def test_config_d_full_size_matches_compacted_oracle():
@@ -145,7 +152,7 @@ def test_config_d_full_size_matches_compacted_oracle():
         users = cu.repeat(GROUP)
         items = ci.reshape(-1)
         lu, li = cm.ids(users, items)
-        ok = (_pre_activations(ref, lu, li) >= 1e-6).reshape(-1, GROUP).all(axis=1)
+        ok = _off_kinks(ref, lu, li).reshape(-1, GROUP).all(axis=1)
         if s == 0:
             ok[:3] = True                        # the corner groups stay (checked below)
         keep = np.flatnonzero(ok)[:ngroups]
@@ -186,8 +193,10 @@ def test_config_d_full_size_matches_compacted_oracle():
     for name in O.weight_names(cm.shape):
         g = got[name] if name.endswith("embedding") else dense_got[name]
         tol = steps * 2e-6 + 2e-6 * float(np.max(np.abs(ref[name])))
-        e = float(np.max(np.abs(np.asarray(g, np.float64) - ref[name])))
-        assert e <= tol, "%s: max err %g > %g" % (name, e, tol)
+        d = np.abs(np.asarray(g, np.float64) - ref[name])
+        e = float(np.max(d))
+        assert e <= tol, "%s: max err %g > %g (%d elements in %d rows beyond)" % (
+            name, e, tol, int((d > tol).sum()), int((d > tol).reshape(len(d), -1).any(axis=1).sum()))
 
     # untouched rows: bitwise their initial values, zero moments
     touched = torch.zeros(eng.num_rows, dtype=torch.bool, device="cuda")

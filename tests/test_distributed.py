@@ -471,3 +471,170 @@ def test_row_sharded_dp_config_d_model_gpu():
         for a, b in zip(pr, rprobs):
             np.testing.assert_allclose(a, b[r * per:(r + 1) * per], rtol=0, atol=2e-6)
     assert gpu_available()
+
+
+# ------------------------------------------- user-partitioned, deferred decay (GPU)
+
+SHAPE_C = (200, 150, [128, 64, 32, 16], 64)   # config C's model, small tables (fused kernels)
+
+
+def _user_part_device_batches(dims, world, per, steps, seed):
+    shape = O.NCFShape(*dims)
+    rng = np.random.RandomState(seed)
+    out = []
+    for _ in range(steps):
+        parts = []
+        for r in range(world):
+            n_loc = (shape.num_users - r + world - 1) // world
+            users = (rng.randint(0, n_loc, per // GROUP) * world + r).repeat(GROUP).astype(np.int32)
+            items = rng.randint(0, shape.num_items, per).astype(np.int32)
+            y = np.tile([0] * (GROUP - 1) + [1], per // GROUP).astype(np.float32)
+            parts.append((users, items, y))
+        out.append(parts)
+    return out
+
+
+def _gpu_user_lazy_worker(rank, world, port, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [here, os.path.dirname(here), os.path.join(os.path.dirname(here), "movierecommender-tf-trt_amd")]
+    from movierec.engine import NCFEngine
+    from movierec.distributed import UserPartitionedDataParallel, partition_keras_weights
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    shape, w = _weights(SHAPE_C)
+    n_loc = (shape.num_users - rank + world - 1) // world
+    per = 256
+    out = []
+    for lazy in (False, True):
+        eng = NCFEngine(n_loc, shape.num_items, shape.layers, shape.gmf_dim, max_batch=per, lazy_adam=lazy,
+                        lazy_rows=n_loc if lazy else None)
+        eng.set_keras_weights(partition_keras_weights(w, world, rank))
+        dp = UserPartitionedDataParallel(eng)
+        dp.broadcast_parameters()
+        batches = _user_part_device_batches(SHAPE_C, world, per, 12, 21)
+        dev = [tuple(torch.from_numpy(x).cuda() for x in (p[rank][0] // world, p[rank][1], p[rank][2]))
+               for p in batches]
+        for s, (u, it, y) in enumerate(dev):
+            nxt = (dev[s + 1][0], dev[s + 1][1]) if s + 1 < len(dev) and s != 5 else None   # step 6: not counted
+            dp.train_step(u, it, y, group=GROUP, k=2, global_batch=per * world, next_batch=nxt)
+        eng.check_errors()
+        eng.flush()
+        torch.cuda.synchronize()
+        m, v, t = eng.optimizer_state()
+        out.append((dp.keras_weights(), m, v, t, NCFEngine.read_stats(eng.stats)))
+    q.put((rank, out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [1, 2])
+def test_user_partitioned_deferred_decay_bitwise_dense_gpu(world):
+    """The user-partitioned step with deferred decay of the own users (touched-row update, the next
+    batch counted and its rows caught up ahead under the all-reduce, one step not counted) against
+    the same layout's dense sweep of every own user row: bitwise equal weights, Adam moments,
+    iteration count and metrics after 12 steps (the item rows are swept every step in both)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_user_lazy_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, out = q.get(timeout=300)
+        res[r] = out
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for r in range(world):
+        (wd, md, vd, td, sd), (wl, ml, vl, tl, sl) = res[r]
+        for name in wd:
+            np.testing.assert_array_equal(wl[name], wd[name], err_msg=name)
+        for name in md:
+            np.testing.assert_array_equal(ml[name], md[name], err_msg="m " + name)
+            np.testing.assert_array_equal(vl[name], vd[name], err_msg="v " + name)
+        assert tl == td == 12
+        assert sl == sd
+    assert gpu_available()
+
+
+def _gpu_user_full_worker(rank, world, port, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [here, os.path.dirname(here), os.path.join(os.path.dirname(here), "movierecommender-tf-trt_amd")]
+    from movierec.engine import NCFEngine
+    from movierec.model import initial_weights
+    from movierec.distributed import UserPartitionedDataParallel, partition_keras_weights
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    U, I, layers, gmf = 138493, 27278, [128, 64, 32, 16], 64
+    per = 65536
+    n_loc = (U - rank + world - 1) // world
+    w = initial_weights(U, I, layers, gmf, seed=3)
+    eng = NCFEngine(n_loc, I, layers, gmf, max_batch=per, lazy_adam=True, lazy_rows=n_loc)
+    eng.set_keras_weights(partition_keras_weights(w, world, rank))
+    dp = UserPartitionedDataParallel(eng)
+    batches = _user_part_device_batches((U, I, layers, gmf), world, per, 3, 31)
+    dev = [tuple(torch.from_numpy(x).cuda() for x in (p[rank][0] // world, p[rank][1], p[rank][2]))
+           for p in batches]
+    for s, (u, it, y) in enumerate(dev):
+        nxt = (dev[s + 1][0], dev[s + 1][1]) if s + 1 < len(dev) else None
+        dp.train_step(u, it, y, group=GROUP, k=2, global_batch=per * world, next_batch=nxt)
+    eng.check_errors()
+    q.put((rank, eng.keras_weights(), NCFEngine.read_stats(eng.stats)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_user_partitioned_full_config_c_tables_gpu():
+    """The user layout at config C's full tables (138,493 x 27,278), 65,536 samples per rank at
+    world 2, deferred decay with counting ahead, 3 steps, against ncf_train_step on the
+    concatenated 131,072-sample batches.  The step is the same arithmetic up to fp32 summation
+    order of the item-row and dense-layer gradients; from step 2 on that order can move a sample
+    across a ReLU kink (a pre-activation within ~1e-9 of 0), which changes its rows by up to two
+    Adam steps.  So: dense layers within 1e-5; embedding rows beyond 1e-5 fewer than 0.1 % of the
+    table and every element within 3e-3 (two Adam steps of lr 1e-3); loss rel 1e-5."""
+    from movierec.engine import NCFEngine
+    from movierec.model import initial_weights
+    from movierec.distributed import partition_keras_weights
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_user_full_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, wts, st = q.get(timeout=600)
+        res[r] = (wts, st)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    U, I, layers, gmf = 138493, 27278, [128, 64, 32, 16], 64
+    ref = NCFEngine(U, I, layers, gmf, max_batch=2 * 65536, lazy_adam=True)
+    ref.set_keras_weights(initial_weights(U, I, layers, gmf, seed=3))
+    batches = _user_part_device_batches((U, I, layers, gmf), world, 65536, 3, 31)
+    dev = [tuple(torch.from_numpy(np.concatenate(x)).cuda() for x in zip(*parts)) for parts in batches]
+    for s, (u, it, y) in enumerate(dev):
+        nxt = (dev[s + 1][0], dev[s + 1][1]) if s + 1 < len(dev) else None
+        ref.train_step(u, it, y, group=GROUP, k=2, next_batch=nxt)
+    rw = ref.keras_weights()
+    rst = NCFEngine.read_stats(ref.stats)
+    for r in range(world):
+        wts, st = res[r]
+        loc = partition_keras_weights(rw, world, r)
+        for name in loc:
+            d = np.abs(np.asarray(wts[name], np.float64) - loc[name])
+            if name.endswith("embedding"):
+                rows_off = (d > 1e-5).any(axis=1).mean()
+                assert rows_off < 1e-3, "%s: %.4f of the rows beyond 1e-5" % (name, rows_off)
+                assert d.max() <= 3e-3, "%s: max err %g" % (name, d.max())
+            else:
+                assert d.max() <= 1e-5, "%s: max err %g" % (name, d.max())
+        assert st["loss"] == pytest.approx(rst["loss"], rel=1e-5)
+        assert st["steps"] == rst["steps"] == 3
+    assert gpu_available()

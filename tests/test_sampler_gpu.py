@@ -41,7 +41,7 @@ def test_device_batches_match_restatement(negs):
     extra = _frame(2, n=200)
     gen = DeviceMovieLensDataGenerator("ml-100k", data, (negs + 1) * 40, negs, extra_data_df=extra, seed=1234)
     ex = _excluded_dict(gen)
-    order = np.asarray(gen.indexes)
+    order = gen._order.cpu().numpy()   # the epoch's positive order (a device permutation)
     for idx in (0, 3, len(gen) - 1):
         (xu, xi), y = gen[idx]
         ru, ri, ry = O.sample_batch(gen._users, gen._items, ex, I, order, idx * 40, 40, negs, 1234,
@@ -59,12 +59,14 @@ def test_device_batches_invariants():
     gen = DeviceMovieLensDataGenerator("ml-100k", data, 10 * 100, negs, extra_data_df=extra, seed=7)
     ex = _excluded_dict(gen)
     assert len(gen) == len(data) // 1000   # data_pipeline.py:97 quirk kept
+    order = gen._order.cpu().numpy()
+    assert np.array_equal(np.sort(order), np.arange(len(data)))   # a permutation of the positives
     for idx in range(len(gen)):
         (xu, xi), y = gen[idx]
         xu, xi, y = xu.cpu().numpy().reshape(-1, negs + 1), xi.cpu().numpy().reshape(-1, negs + 1), y.cpu().numpy()
         np.testing.assert_array_equal(y, np.tile([0] * negs + [1], 100))
         assert (xu == xu[:, :1]).all()
-        pos = gen.indexes[idx * 100:(idx + 1) * 100]
+        pos = order[idx * 100:(idx + 1) * 100]
         np.testing.assert_array_equal(xi[:, -1], gen._items[pos])
         for row_u, row_i in zip(xu[:, 0], xi):
             negatives = row_i[:-1]
