@@ -131,7 +131,9 @@ typedef struct ncf_hyper {
     int32_t index_ready;                /* 1: the contribution index of this call's batch was built
                                            beforehand by ncf_build_index (same ids, same ws): skip it;
                                            2: its contributions were counted and scanned by the
-                                           previous ncf_train_step_ahead (same ids, same ws) */
+                                           previous ncf_train_step_ahead (same ids, same ws);
+                                           3: its index was finished (and its deferred rows
+                                           caught up) by the previous ncf_user_dp_step */
     int32_t mlp_bf16;                   /* 1: the MLP tower's matrix products (forward, data and
                                            weight gradients) take bf16 operands with fp32
                                            accumulation; embeddings, GMF, loss, master weights
@@ -315,7 +317,8 @@ int ncf_build_index(const ncf_shape_t* shape, const ncf_hyper_t* hyper, const in
  *                              hyper->lazy_rows; the batch's own rows are caught up on their
  *                              missed zero-gradient steps before the forward pass (nothing to do
  *                              with hyper->index_ready = 2: the previous ncf_update_rows_lazy counted
- *                              this batch and caught its rows up ahead)
+ *                              this batch and caught its rows up ahead; 3: the previous
+ *                              ncf_user_dp_step also finished its index)
  *   all_reduce                 [shared_grad | mlp_grad | summary] (RCCL, async)
  *   ncf_update_rows_lazy       meanwhile: the touched own rows' scatter-add + Adam at step
  *                              *optim->step + 1 (row_step set; step not bumped); with next ids
@@ -332,6 +335,32 @@ int ncf_forward_backward_part_lazy(const ncf_shape_t* shape, ncf_model_t* model,
 int ncf_update_rows_lazy(const ncf_shape_t* shape, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* hyper,
                          int64_t n, const int32_t* next_users, const int32_t* next_items, int64_t n_next, void* ws,
                          size_t ws_bytes, void* stream);
+
+/* Native communicator (RCCL inside the library; no reference counterpart).  The ranks come from
+ * the caller's process group: rank 0 takes an id with ncf_comm_unique_id (128 bytes), the caller
+ * broadcasts it, every rank calls ncf_comm_init on its device (a collective: it blocks until all
+ * ranks joined).  The communicator owns a side stream for its collective.
+ *   ncf_comm_allreduce   in-place fp32 sum over the ranks, ordered after the work enqueued on
+ *                        `stream` so far; `stream` waits for it.
+ *   ncf_user_dp_step     the user-partitioned step with deferred decay in ONE call:
+ *                        ncf_forward_backward_part_lazy, the all-reduce of shared =
+ *                        [item-row gradient (num_rows - lazy_rows rows) | dense-layer gradient |
+ *                        summary] on the side stream while the compute stream runs
+ *                        ncf_update_rows_lazy (next ids optional), then ncf_apply_update of the
+ *                        item rows (moments indexed by table row) and the dense layers, stats,
+ *                        step++.  With next ids the next batch's index is also filled and sorted
+ *                        under the collective: pass those very ids next call with
+ *                        hyper->index_ready = 3 (the index is trusted: contents must not change in
+ *                        between; 0 = build it now).  Bitwise the same as those calls made one by
+ *                        one with any other all-reduce of the same sums. */
+int ncf_comm_unique_id(void* id, size_t bytes);
+int ncf_comm_init(int32_t world, int32_t rank, const void* id, size_t bytes, void** comm);
+int ncf_comm_destroy(void* comm);
+int ncf_comm_allreduce(void* comm, float* buf, int64_t count, void* stream);
+int ncf_user_dp_step(const ncf_shape_t* shape, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* hyper,
+                     const int32_t* users, const int32_t* items, const float* labels, int64_t n,
+                     const int32_t* next_users, const int32_t* next_items, int64_t n_next, float* shared,
+                     int32_t include_dense_reg, void* comm, double* stats, void* ws, size_t ws_bytes, void* stream);
 
 /* Row-sharded data parallelism (no reference counterpart — the
  * reference trains on one CPU).  Rank r of `world` (1..16) owns the table rows g

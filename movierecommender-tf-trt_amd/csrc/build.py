@@ -15,7 +15,7 @@ ROOT = os.path.dirname(PKG)
 INCLUDE = os.path.join(ROOT, "include")
 OUT_DIR = os.path.join(PKG, "movierec", "_lib")
 LIB = os.path.join(OUT_DIR, "libmovierec_ncf.so")
-SOURCES = ["ncf_index.hip", "ncf_update.hip", "ncf_generic.hip", "ncf_fused.hip", "ncf_unit.hip", "ncf_wave.hip", "ncf_layered.hip", "ncf_score.hip", "ncf_sample.hip", "ncf_capi.hip"]
+SOURCES = ["ncf_index.hip", "ncf_update.hip", "ncf_generic.hip", "ncf_fused.hip", "ncf_unit.hip", "ncf_wave.hip", "ncf_layered.hip", "ncf_score.hip", "ncf_sample.hip", "ncf_comm.hip", "ncf_capi.hip"]
 # per-source extra flags: the scorer keeps its MFMA accumulators in VGPRs (no v_accvgpr_read
 # before every epilogue op; its 226 registers fit the unified file at 2 waves/SIMD)
 EXTRA = {"ncf_score.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
@@ -58,7 +58,8 @@ def build(force=False, verbose=False, defines=(), out=None):
     tmp = lib_path + ".tmp"
     # rocBLAS (plain fp32 GEMMs of the layered path): same soname as the copy torch loads, so one
     # rocBLAS serves the process
-    cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-o", tmp] + objs + ["-L/opt/rocm/lib", "-lrocblas"]
+    # RCCL (the data-parallel step's all-reduce, ncf_comm.hip): librccl.so.1, the soname torch loads too
+    cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-o", tmp] + objs + ["-L/opt/rocm/lib", "-lrocblas", "-lrccl"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError("link failed:\n%s\n%s" % (r.stdout, r.stderr))

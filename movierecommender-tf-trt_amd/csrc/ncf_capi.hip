@@ -169,11 +169,20 @@ bool use_fused(const ncf_shape_t& s, const ncf_hyper_t* h) {
     return s.fast_path && !(h && (h->force_generic == 1 || h->force_generic == 2)) && ncf::fused_supported(s);
 }
 
+bool use_layered(const ncf_shape_t& s, const ncf_hyper_t* h) {
+    if (!ncf::layered_supported(s)) return false;
+    if (h && h->force_generic == 2) return true;
+    if (h && h->force_generic == 1) return false;
+    return !use_fused(s, h) && s.mlp_params > 12288;
+}
+
 // forward only: the fused MFMA forward when the shape has it, else the generic per-sample kernel
 hipError_t launch_predict(const ncf_shape_t& s, const ncf_hyper_t* h, const ncf::WsLayout& L, void* ws,
                           const float* emb, const float* mlp, const int32_t* users, const int32_t* items,
                           const float* labels, int64_t n, float* probs, ncf::IdSpace ids, int* nbce, hipStream_t st) {
     if (use_fused(s, h)) return ncf::launch_fwd_fused(s, L, ws, emb, mlp, users, items, labels, n, probs, ids, nbce, st);
+    // shapes whose weights outgrow the fused kernels (config D): the layered GEMM forward
+    if (use_layered(s, h)) return ncf::launch_predict_layered(s, L, ws, emb, mlp, users, items, labels, n, probs, ids, nbce, st);
     return ncf::launch_predict_generic(s, L, ws, emb, mlp, users, items, labels, n, probs, ids, nbce, st);
 }
 
@@ -215,12 +224,6 @@ int index_fold(const ncf_shape_t& s, const ncf_hyper_t* h) {
     return h && on ? ncf::fold_of(h->group, use_fused(s, h)) : 0;
 }
 
-bool use_layered(const ncf_shape_t& s, const ncf_hyper_t* h) {
-    if (!ncf::layered_supported(s)) return false;
-    if (h && h->force_generic == 2) return true;
-    if (h && h->force_generic == 1) return false;
-    return !use_fused(s, h) && s.mlp_params > 12288;
-}
 
 }  // namespace
 
@@ -293,9 +296,41 @@ WsLayout make_layout(const ncf_shape_t& s, int64_t B, int world) {
     return L;
 }
 
+int set_error(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
 LaunchEvents& launch_events() {
     thread_local LaunchEvents ev;
     return ev;
+}
+
+}  // namespace ncf
+
+namespace ncf {
+// ncf_user_dp_step's tail: the next batch's index finished ahead (its counts were taken and
+// scanned by the ncf_update_rows_lazy just enqueued): fill, list sort (+ the stale-count gate), so
+// the next step starts at its forward/backward (index_ready = 3)
+int build_next_index(const ncf_shape_t& s, const ncf_hyper_t& h, ncf_model_t* model, ncf_optim_t* optim,
+                     const int32_t* next_users, const int32_t* next_items, int64_t n, void* ws, size_t ws_bytes,
+                     hipStream_t st) {
+    WsLayout L;
+    if (int r = check_ws(s, n, ws, ws_bytes, &L)) return r;
+    prof_begin(NCF_K_INDEX, st);
+    hipError_t e = launch_index_build(s, L, ws, next_users, next_items, n, st, true, true, true, index_fold(s, &h));
+    prof_end(NCF_K_INDEX, st);
+    if (e != hipSuccess) return hip_check(e, "next index");
+    prof_begin(NCF_K_CATCHUP, st);
+    e = launch_emb_catchup(s, L, ws, model->emb, optim->emb_m, optim->emb_v, optim->row_step, optim->step, h, false, st,
+                           true, n, true, next_users, next_items);
+    prof_end(NCF_K_CATCHUP, st);
+    return hip_check(e, "next index sort");
 }
 
 }  // namespace ncf
@@ -489,9 +524,10 @@ static int run_fb(const ncf_shape_t& s, const ncf::WsLayout& L, const ncf_model_
     const int variant = use_fused(s, h) ? fb_variant(s, h, n) : -1;
     const bool unit = variant == NCF_FB_UNIT || variant == NCF_FB_WAVE;
     bool check_fold = false;  // the unit / wave kernels check an earlier call's index fold themselves
-    if (sharded || (h->index_ready == 1 && !after_index)) {
-        // the index was built by an earlier call — ncf_shard_plan (compact ids) or ncf_build_index
-        // (the deferred-decay step needs the touched-row list too and always builds its own): it
+    if (sharded || (h->index_ready == 1 && !after_index) || h->index_ready == 3) {
+        // the index was built by an earlier call — ncf_shard_plan (compact ids), ncf_build_index
+        // (the deferred-decay step needs the touched-row list too and builds its own), or the
+        // previous ncf_user_dp_step (index_ready 3: list, touched rows and catch-up all done): it
         // must fold the user rows as this step's kernel does
         if (sharded) {
             users = ncf::at<int32_t>(ws, L.cid_u);

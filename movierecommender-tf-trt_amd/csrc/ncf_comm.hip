@@ -1,0 +1,150 @@
+// RCCL inside the library: the data-parallel step's one collective enqueued by the same host call
+// that enqueues its kernels (include/movierec_ncf.h "Native communicator").
+//
+// torch.distributed's process group forms the ranks and carries the RCCL unique id; the step's
+// all-reduce then goes straight to RCCL on a side stream of this library (fork/join by events),
+// beside the own-user update on the compute stream.  Per step that is one host call instead of
+// the five Python-level calls (and the c10d collective's own host work) of the same step driven
+// from Python — the user-partitioned step was host-issue-bound that way (a ~300 us host step
+// against ~150 us of kernels at an emulated 8 ranks, rocprofv3 timeline, profiles/r03_user).
+//
+// librccl.so.1 is the soname the PyTorch build loads too: one RCCL serves the process.
+
+#include <rccl/rccl.h>
+
+#include <cstring>
+
+#include "movierec_ncf.h"
+#include "ncf_internal.h"
+
+namespace {
+
+struct Comm {
+    ncclComm_t nccl = nullptr;
+    hipStream_t side = nullptr;   // the collective's stream
+    hipEvent_t fork = nullptr, join = nullptr;
+    int world = 0, rank = 0, device = 0;
+};
+
+int comm_fail(int code, const char* what, const char* detail) { return ncf::set_error(code, "%s: %s", what, detail); }
+
+int nccl_check(ncclResult_t r, const char* what) {
+    return r == ncclSuccess ? 0 : comm_fail(NCF_EHIP, what, ncclGetErrorString(r));
+}
+
+int hip_ok(hipError_t e, const char* what) { return e == hipSuccess ? 0 : comm_fail(NCF_EHIP, what, hipGetErrorString(e)); }
+
+}  // namespace
+
+extern "C" {
+
+int ncf_comm_unique_id(void* id, size_t bytes) {
+    if (!id || bytes < sizeof(ncclUniqueId)) return comm_fail(NCF_EINVAL, "ncf_comm_unique_id", "buffer < 128 bytes");
+    ncclUniqueId u;
+    if (int r = nccl_check(ncclGetUniqueId(&u), "ncclGetUniqueId")) return r;
+    memcpy(id, &u, sizeof(u));
+    return 0;
+}
+
+int ncf_comm_init(int32_t world, int32_t rank, const void* id, size_t bytes, void** comm) {
+    if (!comm || !id || bytes < sizeof(ncclUniqueId)) return comm_fail(NCF_EINVAL, "ncf_comm_init", "NULL argument");
+    if (world < 1 || rank < 0 || rank >= world) return comm_fail(NCF_EINVAL, "ncf_comm_init", "rank outside world");
+    Comm* c = new Comm();
+    c->world = world;
+    c->rank = rank;
+    if (int r = hip_ok(hipGetDevice(&c->device), "hipGetDevice")) {
+        delete c;
+        return r;
+    }
+    ncclUniqueId u;
+    memcpy(&u, id, sizeof(u));
+    int r = nccl_check(ncclCommInitRank(&c->nccl, world, u, rank), "ncclCommInitRank");
+    if (!r) r = hip_ok(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking), "hipStreamCreate");
+    if (!r) r = hip_ok(hipEventCreateWithFlags(&c->fork, hipEventDisableTiming), "hipEventCreate");
+    if (!r) r = hip_ok(hipEventCreateWithFlags(&c->join, hipEventDisableTiming), "hipEventCreate");
+    if (r) {
+        if (c->nccl) ncclCommDestroy(c->nccl);
+        delete c;
+        return r;
+    }
+    *comm = c;
+    return 0;
+}
+
+int ncf_comm_destroy(void* comm) {
+    Comm* c = static_cast<Comm*>(comm);
+    if (!c) return 0;
+    hipStreamSynchronize(c->side);
+    int r = c->nccl ? nccl_check(ncclCommDestroy(c->nccl), "ncclCommDestroy") : 0;
+    if (c->fork) hipEventDestroy(c->fork);
+    if (c->join) hipEventDestroy(c->join);
+    if (c->side) hipStreamDestroy(c->side);
+    delete c;
+    return r;
+}
+
+// in-place sum over the ranks on the communicator's stream, ordered after everything enqueued on
+// `stream` so far; `stream` waits for it before its next work
+int ncf_comm_allreduce(void* comm, float* buf, int64_t count, void* stream) {
+    Comm* c = static_cast<Comm*>(comm);
+    if (!c || (!buf && count > 0) || count < 0) return comm_fail(NCF_EINVAL, "ncf_comm_allreduce", "invalid argument");
+    hipStream_t st = (hipStream_t)stream;
+    if (int r = hip_ok(hipEventRecord(c->fork, st), "fork")) return r;
+    if (int r = hip_ok(hipStreamWaitEvent(c->side, c->fork, 0), "fork wait")) return r;
+    if (int r = nccl_check(ncclAllReduce(buf, buf, (size_t)count, ncclFloat32, ncclSum, c->nccl, c->side),
+                           "ncclAllReduce"))
+        return r;
+    if (int r = hip_ok(hipEventRecord(c->join, c->side), "join")) return r;
+    return hip_ok(hipStreamWaitEvent(st, c->join, 0), "join wait");
+}
+
+// The user-partitioned step with deferred decay (ncf_forward_backward_part_lazy, all-reduce,
+// ncf_update_rows_lazy, ncf_apply_update) in one call: the all-reduce of
+// shared = [item-row gradient | dense-layer gradient | summary] runs on the communicator's stream
+// while the compute stream applies the own-user update and prepares the next batch (counted,
+// own rows caught up, index filled and sorted: the next call passes hyper->index_ready = 3).
+int ncf_user_dp_step(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* h,
+                     const int32_t* users, const int32_t* items, const float* labels, int64_t n,
+                     const int32_t* next_users, const int32_t* next_items, int64_t n_next, float* shared,
+                     int32_t include_dense_reg, void* comm, double* stats, void* ws, size_t ws_bytes, void* stream) {
+    Comm* c = static_cast<Comm*>(comm);
+    if (!s || !model || !optim || !h || !shared || !c) return comm_fail(NCF_EINVAL, "ncf_user_dp_step", "NULL argument");
+    if (h->lazy_rows <= 0 || h->lazy_rows > s->num_rows)
+        return comm_fail(NCF_EINVAL, "ncf_user_dp_step", "hyper->lazy_rows must be the rank's user count");
+    const int64_t U = h->lazy_rows, R = s->num_rows, W = s->row_width, P = s->mlp_params;
+    float* item_grad = shared;
+    float* mlp_grad = shared + (R - U) * W;
+    float* summary = mlp_grad + P;
+    hipStream_t st = (hipStream_t)stream;
+    if (int r = ncf_forward_backward_part_lazy(s, model, optim, h, users, items, labels, n, item_grad, mlp_grad, summary,
+                                               nullptr, include_dense_reg, ws, ws_bytes, stream))
+        return r;   // the message is set
+    const int64_t count = (R - U) * W + P + NCF_NUM_SUMMARY;
+    hipStream_t side = c->side;
+    if (int r = hip_ok(hipEventRecord(c->fork, st), "fork")) return r;
+    if (int r = hip_ok(hipStreamWaitEvent(side, c->fork, 0), "fork wait")) return r;
+    if (int r = nccl_check(ncclAllReduce(shared, shared, (size_t)count, ncclFloat32, ncclSum, c->nccl, side),
+                           "ncclAllReduce"))
+        return r;
+    if (int r = hip_ok(hipEventRecord(c->join, side), "join")) return r;
+    // meanwhile on the compute stream: the own users' update (+ the next batch counted and its own
+    // rows caught up ahead), then the next batch's index finished — none of it reads an item row,
+    // so all of it runs under the collective; the next step starts at its forward/backward
+    if (int r = ncf_update_rows_lazy(s, model, optim, h, n, next_users, next_items, n_next, ws, ws_bytes, stream))
+        return r;
+    if (next_users)
+        if (int r = ncf::build_next_index(*s, *h, model, optim, next_users, next_items, n_next, ws, ws_bytes, st))
+            return r;
+    if (int r = hip_ok(hipStreamWaitEvent(st, c->join, 0), "join wait")) return r;
+    // the replicated item rows (their moments indexed by table row) and the dense layers
+    ncf_optim_t items_opt = *optim;
+    if (items_opt.emb_m) items_opt.emb_m += U * W;
+    if (items_opt.emb_v) items_opt.emb_v += U * W;
+    items_opt.row_step = nullptr;
+    if (int r = ncf_apply_update(s, model, &items_opt, h, U, R - U, item_grad, mlp_grad, summary, stats, ws, ws_bytes,
+                                 stream))
+        return r;
+    return 0;
+}
+
+}  // extern "C"

@@ -77,7 +77,10 @@ struct WsLayout {
 // cnt[key] += 1 for every lane with ok, called by all 64 lanes of a wave together.  Equal keys
 // two lanes apart (a user group's contributions c = 2i, 2i+2, ...) form runs: the run's head
 // adds the run length with one atomic, so a group does not queue on one counter.
-__device__ __forceinline__ void wave_run_count(int32_t* __restrict__ cnt, int key, bool ok) {
+// FIRST: the head lane returns whether its run is the key's first occurrence in the counted set
+// (the count it added to was 0: the counters start at zero for a batch), every other lane false.
+template <bool FIRST = false>
+__device__ __forceinline__ bool wave_run_count(int32_t* __restrict__ cnt, int key, bool ok) {
     const int lane = threadIdx.x & 63;
     const uint64_t par = (lane & 1) ? 0xAAAAAAAAAAAAAAAAull : 0x5555555555555555ull;
     const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
@@ -86,7 +89,11 @@ __device__ __forceinline__ void wave_run_count(int32_t* __restrict__ cnt, int ke
     const uint64_t heads = ~__ballot(lane >= 2 && prev == kk) & par;
     const uint64_t later = heads & ~upto;
     const int next = later ? __ffsll((unsigned long long)later) - 1 : 64 + (lane & 1);
-    if (ok && ((heads >> lane) & 1ull)) atomicAdd(&cnt[key], (next - lane) >> 1);
+    if (ok && ((heads >> lane) & 1ull)) {
+        if constexpr (FIRST) return atomicAdd(&cnt[key], (next - lane) >> 1) == 0;
+        atomicAdd(&cnt[key], (next - lane) >> 1);
+    }
+    return false;
 }
 
 template <bool UNIQ>
@@ -243,6 +250,14 @@ __device__ inline void sort_rows_body(const int32_t* __restrict__ offs, int64_t 
     }
 }
 
+// ncf_user_dp_step's helpers (ncf_capi.hip)
+int build_next_index(const ncf_shape_t& s, const ncf_hyper_t& h, ncf_model_t* model, ncf_optim_t* optim,
+                     const int32_t* next_users, const int32_t* next_items, int64_t n, void* ws, size_t ws_bytes,
+                     hipStream_t st);
+
+// the thread's ncf_last_error() text (printf format); returns code
+int set_error(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+
 // world == 0: single-table layout; world >= 1: row-sharded layout (ncf_shard_*)
 WsLayout make_layout(const ncf_shape_t& s, int64_t max_batch, int world = 0);
 
@@ -360,6 +375,10 @@ bool layered_supported(const ncf_shape_t& s);
 hipError_t launch_fb_layered(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, const float* mlp,
                              const int32_t* users, const int32_t* items, const float* labels, int64_t n,
                              float inv_batch, IdSpace ids, int* nslab, int* nbce, hipStream_t st);
+// its forward half alone (predict / evaluate): probs, and with labels the BCE partials
+hipError_t launch_predict_layered(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb,
+                                  const float* mlp, const int32_t* users, const int32_t* items, const float* labels,
+                                  int64_t n, float* probs, IdSpace ids, int* nbce, hipStream_t st);
 
 // metrics / summaries
 hipError_t launch_group_metrics(const float* probs, const float* labels, int64_t n_groups, int group, int k,

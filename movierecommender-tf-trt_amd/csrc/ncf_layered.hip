@@ -194,7 +194,7 @@ __global__ __launch_bounds__(kBlock) void k_lay_out2(const float* __restrict__ g
         z += wo[G + Ll];
         const float p = 1.0f / (1.0f + expf(-z));
         float d = 0.f;
-        if (ok) {
+        if (ok && labels) {   // forward only (ncf_predict): no labels, no loss
             const float y = labels[i];
             const float eps = 1e-7f, hi = 1.0f - eps;
             const float pc = fminf(fmaxf(p, eps), hi);
@@ -255,12 +255,61 @@ __global__ __launch_bounds__(kBlock) void k_lay_scatter(const float* __restrict_
 
 bool layered_supported(const ncf_shape_t& s) { return s.num_layers >= 2; }
 
-constexpr int kLayeredSlabs = 64;  // batch chunks of the weight-gradient GEMMs (<= kMaxSlabs)
-
 static unsigned grid_for(int64_t total) {
     int64_t g = (total + kBlock - 1) / kBlock;
     return (unsigned)(g < 1 ? 1 : (g > 8192 ? 8192 : g));
 }
+
+// Forward only (ncf_predict / ncf_evaluate on layered shapes): the gather, the dense layers as
+// GEMMs + bias/ReLU, the output layer with (labels given) the Keras BCE partials, one per
+// 256-sample block in part_bce (*nbce).  Same arithmetic as the forward half of
+// launch_fb_layered, so evaluation matches training's forward.
+hipError_t launch_predict_layered(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb,
+                                  const float* mlp, const int32_t* users, const int32_t* items, const float* labels,
+                                  int64_t n, float* probs, IdSpace ids, int* nbce, hipStream_t st) {
+    if (!layered_supported(s) || n > L.max_batch) return hipErrorInvalidValue;
+    rocblas_handle bh;
+    hipError_t e = blas(st, &bh);
+    if (e != hipSuccess) return e;
+    const int nl = s.num_layers, G = s.gmf_dim, G4 = s.gmf_stride, W = s.row_width;
+    const int du = s.du, di = s.di, Ll = s.layers[nl - 1];
+    float* act = at<float>(ws, L.act);
+    float* X[NCF_MAX_LAYERS];
+    int64_t o = 0;
+    for (int l = 0; l < nl; ++l) { X[l] = act + o; o += (int64_t)L.max_batch * s.layers[l]; }
+    float* gmf = act + o;
+    float* dzo = at<float>(ws, L.dz);
+    float* ones = at<float>(ws, L.ones);
+    const float one = 1.0f, zero = 0.0f;
+    const bool vec4 = du % 4 == 0 && di % 4 == 0 && G == G4 && W % 4 == 0;
+    if (vec4)
+        launch(k_lay_gather4, grid_for(n * (du + di + G) / 4), kBlock, 0, st, (const float4*)emb, users, items, n, ids,
+               W / 4, G / 4, du / 4, di / 4, (float4*)X[0], (float4*)gmf);
+    else
+        launch(k_lay_gather, grid_for(n * (du + di + G)), kBlock, 0, st, emb, users, items, n, ids, W, G, G4, du, di,
+               X[0], gmf);
+    for (int l = 1; l < nl; ++l) {
+        const int lin = s.layers[l - 1], lout = s.layers[l];
+        const float* Wl = mlp + s.layer_off[l];
+        e = blas_err(rocblas_sgemm(bh, rocblas_operation_none, rocblas_operation_none, lout, (int)n, lin, &one, Wl,
+                                   lout, X[l - 1], lin, &zero, X[l], lout));
+        if (e != hipSuccess) return e;
+        launch(k_bias_relu, grid_for(n * lout), kBlock, 0, st, X[l], n * lout, lout, Wl + (int64_t)lin * lout);
+    }
+    const unsigned gb = (unsigned)((n + kBlock - 1) / kBlock);
+    const int wo_off = s.layer_off[0];
+    if (G % 4 == 0 && Ll % 4 == 0)
+        launch(k_lay_out2<true>, gb, kBlock, 0, st, (const float*)gmf, (const float*)X[nl - 1], mlp + wo_off, G, Ll,
+               users, items, ids, labels, n, 1.0f, probs, dzo, ones, at<float>(ws, L.part_bce));
+    else
+        launch(k_lay_out2<false>, gb, kBlock, 0, st, (const float*)gmf, (const float*)X[nl - 1], mlp + wo_off, G, Ll,
+               users, items, ids, labels, n, 1.0f, probs, dzo, ones, at<float>(ws, L.part_bce));
+    *nbce = labels ? (int)gb : 0;
+    return hipGetLastError();
+}
+
+constexpr int kLayeredSlabs = 64;  // batch chunks of the weight-gradient GEMMs (<= kMaxSlabs)
+
 
 hipError_t launch_fb_layered(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, const float* mlp,
                              const int32_t* users, const int32_t* items, const float* labels, int64_t n,

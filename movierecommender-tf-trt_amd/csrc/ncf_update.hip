@@ -645,27 +645,20 @@ __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_tou
                     ok = (unsigned)id < (unsigned)bound && ((c & 1) || !folded_user(ca.users, i, ca.fold));
                     key = (c & 1) ? ca.U + id : id;
                 }
-                wave_run_count(ca.cnt, key, ok);
-                bool claim = false;
-                int s0 = 0;
-                // the row's step goes out with its offsets (one memory round trip, not two)
+                // the row's step and offsets go out before the count's atomic returns (one memory
+                // round trip); the lane whose run is the key's first occurrence in the next batch
+                // (its count was 0) owns the row's replay — no claim atomic of its own
                 int o0 = 0, o1 = 0, sv = t;
                 if (ca.replay && ok && key < ca.lazy_rows) {
                     o0 = offs[key];
                     o1 = offs[key + 1];
                     sv = row_step[key];
                 }
-                if (ca.replay && ok && o1 == o0) {   // not in this step's batch
-                    while (sv < t) {
-                        const int prev = atomicCAS(&row_step[key], sv, t);
-                        if (prev == sv) {
-                            claim = true;
-                            s0 = sv;
-                            break;
-                        }
-                        sv = prev;
-                    }
-                }
+                const bool first = wave_run_count<true>(ca.cnt, key, ok);
+                // not in this step's batch (this launch's update blocks do not touch it) and behind
+                const bool claim = ca.replay && first && key < ca.lazy_rows && o1 == o0 && sv < t;
+                const int s0 = sv;
+                if (claim) row_step[key] = t;
                 const uint64_t cm = __ballot(claim);
                 if (claim) {
                     const int slot = __popcll(cm & ((1ull << lane) - 1));

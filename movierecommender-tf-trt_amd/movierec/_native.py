@@ -98,6 +98,12 @@ _SIGNATURES = {
                                                       _vp]),
     "ncf_update_rows_lazy": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _i64, _vp, _vp,
                                             _i64, _vp, ctypes.c_size_t, _vp]),
+    "ncf_comm_unique_id": (ctypes.c_int, [_vp, ctypes.c_size_t]),
+    "ncf_comm_init": (ctypes.c_int, [_i32, _i32, _vp, ctypes.c_size_t, _P(_vp)]),
+    "ncf_comm_destroy": (ctypes.c_int, [_vp]),
+    "ncf_comm_allreduce": (ctypes.c_int, [_vp, _vp, _i64, _vp]),
+    "ncf_user_dp_step": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _vp, _vp, _vp, _i64,
+                                        _vp, _vp, _i64, _vp, _i32, _vp, _vp, _vp, ctypes.c_size_t, _vp]),
     "ncf_lazy_flush": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _vp, ctypes.c_size_t,
                                       _vp]),
     "ncf_apply_update": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _i64, _i64, _vp, _vp,

@@ -262,6 +262,42 @@ class ReplicatedDataParallel(object):
         _all_gather_inplace(eng.emb, self.shard_rows, self.group)
 
 
+class NativeComm(object):
+    """The library's RCCL communicator (ncf_comm_init) for this rank; destroyed with the object."""
+
+    def __init__(self, handle):
+        self.handle = handle
+
+    def close(self):
+        if self.handle:
+            from . import _native as N
+            N.check(N.lib().ncf_comm_destroy(self.handle))
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _native_comm(rank, world, group=None):
+    """Form the library's RCCL communicator over the ranks of ``group``: rank 0's unique id goes
+    to every rank through the process group, then every rank joins (a collective)."""
+    import ctypes
+    from . import _native as N
+    L = N.lib()
+    uid = (ctypes.c_char * 128)()
+    if rank == 0:
+        N.check(L.ncf_comm_unique_id(uid, 128))
+    box = [bytes(uid)]
+    dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+    uid = (ctypes.c_char * 128).from_buffer_copy(box[0])
+    handle = ctypes.c_void_p()
+    N.check(L.ncf_comm_init(world, rank, uid, 128, ctypes.byref(handle)))
+    return NativeComm(handle)
+
+
 def partition_keras_weights(w, world, rank):
     """Keras-layout weights of rank ``rank``'s local model under user partitioning: the user
     rows u % world == rank (local row u // world), every item row, the dense layers."""
@@ -298,7 +334,12 @@ class UserPartitionedDataParallel(object):
     device stepping on the concatenated global batch, up to fp32 order of the cross-rank sum.
     """
 
-    def __init__(self, engine, group=None):
+    def __init__(self, engine, group=None, native=None):
+        """``native``: drive the step through ``ncf_user_dp_step`` with the library's own RCCL
+        communicator (one host call per step, the all-reduce on its side stream); default: when the
+        process group is RCCL (``nccl``) and the engine defers its users' decay.  Otherwise the
+        step's calls and the torch.distributed all-reduce are issued one by one (gloo: ranks that
+        share one GPU in the tests)."""
         self.eng = engine
         self.group = group
         self.world = dist.get_world_size(group)
@@ -308,6 +349,10 @@ class UserPartitionedDataParallel(object):
         if getattr(engine, "row_step", None) is not None and lazy != U:
             raise ValueError("a deferred-decay engine for user-partitioned training needs lazy_rows = its %d users "
                              "(the replicated item rows are swept every step)" % U)
+        if native is None:
+            native = (dist.get_backend(group) == "nccl" and getattr(engine, "row_step", None) is not None and
+                      hasattr(engine, "user_dp_step"))
+        self.comm = _native_comm(self.rank, self.world, group) if native else None
         _, mg0, sm0 = engine.alloc_grads(rows=0)
         P, S = mg0.numel(), sm0.numel()
         dev = engine.emb.device
@@ -337,6 +382,10 @@ class UserPartitionedDataParallel(object):
         inv = 1.0 / gb
         eng = self.eng
         U, R = self.num_local_users, int(eng.num_rows)
+        if self.comm is not None and eng.row_step is not None:
+            eng.user_dp_step(users, items, labels, group=group, k=k, inv_batch=inv, shared=self.shared,
+                             comm=self.comm.handle, next_batch=next_batch, include_dense_reg=self.rank == 0)
+            return
         eng.forward_backward_part(users, items, labels, group=group, k=k, inv_batch=inv, shared_row_begin=U,
                                   grads=self.grads, reg_rows=self.reg_rows, include_dense_reg=self.rank == 0)
         work = _all_reduce_async(self.shared, self.group)

@@ -482,6 +482,44 @@ class NCFEngine(object):
         self._part_n = n
         self._dirty = True
 
+    def user_dp_step(self, users, items, labels, group, k, inv_batch, shared, comm, next_batch=None,
+                     include_dense_reg=True):
+        """The whole user-partitioned step with deferred decay in one library call
+        (ncf_user_dp_step): forward/backward, the RCCL all-reduce of ``shared`` = [item-row grad |
+        dense-layer grad | summary] on the native communicator ``comm`` beside the own-user update
+        (and the next batch counted ahead), then the item rows, dense layers and stats."""
+        u, i, y = self._ids(users), self._ids(items), self._labels(labels)
+        n = u.numel()
+        self._ensure_ws(n)
+        h = self.hyper
+        h.group, h.k, h.inv_batch = int(group), int(k), float(inv_batch)
+        pc = self._counted
+        # the previous step counted this batch AND built its index (ncf_user_dp_step): index_ready 3
+        ready = pc is not None and _same_ids(pc, u, i, n, h.group)
+        if pc is not None and not ready:
+            self._discard_counted()
+        self._counted = None
+        nu = ni = None
+        if next_batch is not None and h.optimizer == N.NCF_OPT_ADAM:
+            nu, ni = next_batch
+            if not (torch.is_tensor(nu) and torch.is_tensor(ni) and nu.is_cuda and ni.is_cuda and
+                    nu.dtype == torch.int32 and ni.dtype == torch.int32 and nu.is_contiguous() and
+                    ni.is_contiguous() and nu.numel() == ni.numel() == n):
+                nu = ni = None
+        h.index_ready = 3 if ready else 0
+        try:
+            N.check(N.lib().ncf_user_dp_step(
+                ctypes.byref(self.shape), ctypes.byref(self.model_s), ctypes.byref(self.optim_s), ctypes.byref(h),
+                N.ptr(u), N.ptr(i), N.ptr(y), n, N.ptr(nu), N.ptr(ni), n if nu is not None else 0, N.ptr(shared),
+                1 if include_dense_reg else 0, comm, N.ptr(self.stats), N.ptr(self.ws), self.ws_bytes,
+                N.stream_handle(self.device)))
+        finally:
+            h.index_ready = 0
+        if nu is not None:
+            self._counted = (nu, ni, n, nu._version, ni._version, h.group)
+        self._part_n = n
+        self._dirty = True
+
     def build_index(self, users, items, group):
         """Build the contribution index of the NEXT ``forward_backward_part`` batch now (e.g. under
         the current step's all-reduce); call after this step's ``update_rows``.  That call must

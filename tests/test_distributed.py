@@ -478,6 +478,27 @@ def test_row_sharded_dp_config_d_model_gpu():
 SHAPE_C = (200, 150, [128, 64, 32, 16], 64)   # config C's model, small tables (fused kernels)
 
 
+def _reporting(body, rank, world, port, q):
+    """Run a worker body; an exception goes to the parent through the queue (a worker that died
+    silently would leave the parent waiting for its result)."""
+    import traceback
+    try:
+        body(rank, world, port, q)
+    except BaseException:
+        q.put((rank, "worker failed:\n" + traceback.format_exc()))
+        raise
+
+
+def _get(q, n, timeout=150):
+    res = {}
+    for _ in range(n):
+        item = q.get(timeout=timeout)
+        if isinstance(item[1], str) and item[1].startswith("worker failed"):
+            pytest.fail(item[1])
+        res[item[0]] = item[1:] if len(item) > 2 else item[1]
+    return res
+
+
 def _user_part_device_batches(dims, world, per, steps, seed):
     shape = O.NCFShape(*dims)
     rng = np.random.RandomState(seed)
@@ -495,6 +516,10 @@ def _user_part_device_batches(dims, world, per, steps, seed):
 
 
 def _gpu_user_lazy_worker(rank, world, port, q):
+    _reporting(_gpu_user_lazy_worker_body, rank, world, port, q)
+
+
+def _gpu_user_lazy_worker_body(rank, world, port, q):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path[:0] = [here, os.path.dirname(here), os.path.join(os.path.dirname(here), "movierecommender-tf-trt_amd")]
@@ -541,10 +566,7 @@ def test_user_partitioned_deferred_decay_bitwise_dense_gpu(world):
     procs = [ctx.Process(target=_gpu_user_lazy_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = {}
-    for _ in range(world):
-        r, out = q.get(timeout=300)
-        res[r] = out
+    res = _get(q, world)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
@@ -561,6 +583,10 @@ def test_user_partitioned_deferred_decay_bitwise_dense_gpu(world):
 
 
 def _gpu_user_full_worker(rank, world, port, q):
+    _reporting(_gpu_user_full_worker_body, rank, world, port, q)
+
+
+def _gpu_user_full_worker_body(rank, world, port, q):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path[:0] = [here, os.path.dirname(here), os.path.join(os.path.dirname(here), "movierecommender-tf-trt_amd")]
@@ -607,10 +633,7 @@ def test_user_partitioned_full_config_c_tables_gpu():
     procs = [ctx.Process(target=_gpu_user_full_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = {}
-    for _ in range(world):
-        r, wts, st = q.get(timeout=600)
-        res[r] = (wts, st)
+    res = _get(q, world)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
@@ -637,4 +660,65 @@ def test_user_partitioned_full_config_c_tables_gpu():
                 assert d.max() <= 1e-5, "%s: max err %g" % (name, d.max())
         assert st["loss"] == pytest.approx(rst["loss"], rel=1e-5)
         assert st["steps"] == rst["steps"] == 3
+    assert gpu_available()
+
+
+def _gpu_native_comm_worker(rank, world, port, q):
+    _reporting(_gpu_native_comm_worker_body, rank, world, port, q)
+
+
+def _gpu_native_comm_worker_body(rank, world, port, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [here, os.path.dirname(here), os.path.join(os.path.dirname(here), "movierecommender-tf-trt_amd")]
+    from movierec.engine import NCFEngine
+    from movierec.distributed import UserPartitionedDataParallel, partition_keras_weights
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world,
+                            device_id=torch.device("cuda", 0))
+    shape, w = _weights(SHAPE_C)
+    per = 256
+    out = []
+    for native in (True, False):
+        eng = NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=per, lazy_adam=True,
+                        lazy_rows=shape.num_users)
+        eng.set_keras_weights(partition_keras_weights(w, world, rank))
+        dp = UserPartitionedDataParallel(eng, native=native)
+        assert (dp.comm is not None) == native
+        batches = _user_part_device_batches(SHAPE_C, world, per, 10, 41)
+        dev = [tuple(torch.from_numpy(x).cuda() for x in p[rank]) for p in batches]
+        for s, (u, it, y) in enumerate(dev):
+            nxt = (dev[s + 1][0], dev[s + 1][1]) if s + 1 < len(dev) and s != 4 else None
+            dp.train_step(u, it, y, group=GROUP, k=2, next_batch=nxt)
+        eng.check_errors()
+        eng.flush()
+        torch.cuda.synchronize()
+        m, v, t = eng.optimizer_state()
+        out.append((eng.keras_weights(), m, v, t, NCFEngine.read_stats(eng.stats)))
+        if dp.comm is not None:
+            dp.comm.close()
+    q.put((rank, out))
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_user_partitioned_native_comm_step_bitwise_gpu():
+    """ncf_user_dp_step (one library call per step, the all-reduce on the library's own RCCL
+    communicator and side stream) against the same step issued call by call from Python with
+    torch.distributed's all-reduce: one rank over RCCL (the box has one GPU), 10 steps with the next
+    batch counted ahead (one step not), bitwise equal weights, moments, iteration count, metrics."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    p = ctx.Process(target=_gpu_native_comm_worker, args=(0, 1, port, q))
+    p.start()
+    out = _get(q, 1)[0]
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    (wa, ma, va, ta, sa), (wb, mb, vb, tb, sb) = out
+    for name in wa:
+        np.testing.assert_array_equal(wa[name], wb[name], err_msg=name)
+        np.testing.assert_array_equal(ma[name], mb[name], err_msg="m " + name)
+        np.testing.assert_array_equal(va[name], vb[name], err_msg="v " + name)
+    assert ta == tb == 10 and sa == sb
     assert gpu_available()
