@@ -650,12 +650,16 @@ static int train_step_impl(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t
     int nreg_mlp = 0;
     // one stream + deferred decay: the dense layers' Adam step runs in extra workgroups of the
     // touched-row update launch (one launch fewer)
-    ncf::MlpDeferred mlp_def{nullptr, nullptr, nullptr, nullptr, 0};
+    ncf::MlpDeferred mlp_def{nullptr, nullptr, nullptr, nullptr, 0, 0};
     const bool defer_mlp = fold && lazy;
+    // every L2 factor zero and enough slabs: both slab-reduction levels run in the touched-row
+    // update launch too, and the batch summary in the stats launch (two launches fewer)
+    const bool two_level = defer_mlp && h->optimizer == NCF_OPT_ADAM && ncf::part_tail_foldable(*s, *h, fb.nslab);
+    mlp_def.two_level = two_level ? 1 : 0;
     prof_begin(NCF_K_MLP_UPDATE, st2);
     e = ncf::launch_mlp_update(*s, L, ws, model->mlp, optim->mlp_m, optim->mlp_v, optim->step, *h, fb.nslab, nullptr,
-                               nullptr, true, &nreg_mlp, st2, false, fold ? fb.nbce : -1, fb.nmet, fb.n_groups,
-                               fold ? summary : nullptr, defer_mlp ? &mlp_def : nullptr);
+                               nullptr, true, &nreg_mlp, st2, false, fold && !two_level ? fb.nbce : -1, fb.nmet,
+                               fb.n_groups, fold && !two_level ? summary : nullptr, defer_mlp ? &mlp_def : nullptr);
     prof_end(NCF_K_MLP_UPDATE, st2);
     if (e != hipSuccess) return hip_check(e, "dense update");
     prof_begin(NCF_K_EMB_UPDATE, st);
@@ -673,7 +677,8 @@ static int train_step_impl(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t
     const int nreg_emb = h->l2[0] != 0.0f ? ncf::kUpdateGrid : 0;
     // counting ahead: the stats launch also scans the next batch's counts
     e = ncf::launch_stats(L, ws, summary, nreg_emb, nreg_mlp, h->inv_batch, stats, optim->step, true, st,
-                          lazy && next_users != nullptr, s->num_rows);
+                          lazy && next_users != nullptr, s->num_rows,
+                          two_level ? ncf::SummaryFirst{fb.nbce, fb.nmet, fb.n_groups} : ncf::SummaryFirst{-1, 0, 0.f});
     return hip_check(e, "stats");
 }
 

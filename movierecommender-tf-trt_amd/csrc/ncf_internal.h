@@ -416,8 +416,10 @@ hipError_t launch_row_step_fill(int32_t* row_step, int64_t R, const int32_t* ste
 // (same stream): it then runs in extra workgroups of the touched-row update launch.
 struct MlpDeferred {
     float *p, *m, *v;          // p == nullptr: not deferred (launch_mlp_update launched it)
-    const float* slabs;        // reduced slab partials
+    const float* slabs;        // reduced slab partials (two_level: the raw slabs)
     int nslab;
+    int two_level;             // 1: the launch also does the first-level slab reduction
+                               // (k_slab_partial's work, same order: bitwise) — no launch of its own
 };
 hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, void* ws, float* emb, float* m,
                                      float* v, int32_t* row_step, int32_t* step, const ncf_hyper_t& h,
@@ -453,9 +455,15 @@ hipError_t launch_emb_reg(const ncf_shape_t& s, const WsLayout& L, void* ws, con
 hipError_t launch_scan_ahead(const WsLayout& L, void* ws, int64_t keys, hipStream_t st);
 // scan_ahead: the same launch also runs the next batch's per-block key scan (k_scan_local<true>
 // over the counts the touched update took ahead)
+// summary_first (nbce >= 0): block 0 first writes the batch summary (launch_summary's work with
+// no L2 partials) and then folds it into stats
+struct SummaryFirst {
+    int nbce, nmet;
+    float n_groups;
+};
 hipError_t launch_stats(const WsLayout& L, void* ws, const float* summary, int nreg_emb, int nreg_mlp,
                         float inv_batch, double* stats, int32_t* step, bool bump_step, hipStream_t st,
-                        bool scan_ahead = false, int64_t scan_keys = 0);
+                        bool scan_ahead = false, int64_t scan_keys = 0, SummaryFirst sf = SummaryFirst{-1, 0, 0.f});
 
 // on-device negative sampling (ncf_sample.hip)
 hipError_t launch_sample_batch(const int32_t* pos_users, const int32_t* pos_items, const int32_t* excl_ptr,

@@ -571,7 +571,8 @@ struct CountAhead {
                                // updated here and caught up ahead (the rest are swept densely)
 };
 
-// the dense layers' Adam (k_mlp_update<ADAM>'s work) in blocks >= nupd + ncount of the same launch
+// the dense layers' Adam (k_mlp_update<ADAM>'s work) in blocks >= nupd + ncount of the same launch;
+// two_level: in the FIRST blocks of the launch, 16 parameters per block, from the raw slabs
 struct MlpTail {
     int nblocks;               // 0: none
     float *p, *m, *v;
@@ -582,7 +583,64 @@ struct MlpTail {
     float lr, b1, b2, eps;
     L2Table l2t;
     float* part_reg;
+    int two_level;
 };
+
+// Both levels of the slab reduction for 16 parameters (16 P0 .. 16 P0 + 15, P0 = blk): thread
+// (c, j) sums chunk c of the slabs for parameter j (k_slab_partial's chunks and order), then the
+// threads c == 0 add the chunk sums (k_mlp_update's order) and return the gradient — bitwise the
+// k_slab_partial + k_mlp_update pair.  Whole block; the value is meaningful where c == 0, i < P.
+__device__ __forceinline__ float slab_grad16(const float* __restrict__ slabs, int P, int nslab, int blk) {
+    __shared__ float part[16][17];
+    const int c = threadIdx.x >> 4, j = threadIdx.x & 15, i = blk * 16 + j;
+    const int per = (nslab + kSlabSplit - 1) / kSlabSplit, nch = (nslab + per - 1) / per;
+    if (c < nch && i < P) {
+        const int s0 = c * per, s1 = min(nslab, s0 + per);
+        float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+        int s = s0;
+        for (; s + 4 <= s1; s += 4) {
+            a0 += slabs[(size_t)(s + 0) * P + i];
+            a1 += slabs[(size_t)(s + 1) * P + i];
+            a2 += slabs[(size_t)(s + 2) * P + i];
+            a3 += slabs[(size_t)(s + 3) * P + i];
+        }
+        for (; s < s1; ++s) a0 += slabs[(size_t)s * P + i];
+        part[c][j] = (a0 + a1) + (a2 + a3);
+    }
+    __syncthreads();
+    float g = 0.f;
+    if (c == 0 && i < P) {
+        float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+        int s = 0;
+        for (; s + 4 <= nch; s += 4) {
+            a0 += part[s + 0][j];
+            a1 += part[s + 1][j];
+            a2 += part[s + 2][j];
+            a3 += part[s + 3][j];
+        }
+        for (; s < nch; ++s) a0 += part[s][j];
+        g = (a0 + a1) + (a2 + a3);
+    }
+    return g;
+}
+
+// Dense-layer Adam straight from the fused kernel's slabs (every L2 factor zero), 16 parameters
+// per block: slab_grad16, then mlp_update_body's Adam (the same expressions)
+__device__ __forceinline__ void mlp_slabs_adam(const MlpTail& mt, int blk) {
+    const float g = slab_grad16(mt.slabs, mt.P, mt.nslab, blk);
+    const int i = blk * 16 + (threadIdx.x & 15);
+    if ((threadIdx.x >> 4) == 0 && i < mt.P) {
+        const int t = *mt.step + 1;
+        const float lr_t = adam_lr_t(mt.lr, mt.b1, mt.b2, t);
+        float w = mt.p[i];
+        const float mm = mt.b1 * mt.m[i] + (1.0f - mt.b1) * g;
+        const float vv = mt.b2 * mt.v[i] + (1.0f - mt.b2) * (g * g);
+        w -= lr_t * mm / (sqrtf(vv) + mt.eps);
+        mt.m[i] = mm;
+        mt.v[i] = vv;
+        mt.p[i] = w;
+    }
+}
 
 __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_touched(float4* __restrict__ emb, float4* __restrict__ m4,
                                                              float4* __restrict__ v4, uint32_t w4,
@@ -599,8 +657,16 @@ __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_tou
     // latency-bound replay blocks are dispatched first, so they run under the HBM-bound update
     // (interleaving them one in every (nupd + ncount) / ncount blocks was measured slower: 60.2
     // vs 53.3 us at config C — their chains are the launch's long pole)
-    const int b = (int)blockIdx.x;
-    if (b >= ca.nupd + ca.ncount) {
+    // (two_level: the dense-layer blocks come first — each waits one round of slab loads, under
+    // everything else)
+    int b = (int)blockIdx.x;
+    if (mt.two_level) {
+        if (b < mt.nblocks) {
+            mlp_slabs_adam(mt, b);
+            return;
+        }
+        b -= mt.nblocks;
+    } else if (b >= ca.nupd + ca.ncount) {
         mlp_update_body<NCF_OPT_ADAM>(mt.p, mt.m, mt.v, mt.P, mt.slabs, mt.nslab, nullptr, nullptr, 1, 0, mt.step,
                                       mt.lr, mt.b1, mt.b2, mt.eps, mt.l2t, mt.part_reg,
                                       (int)blockIdx.x - ca.nupd - ca.ncount);
@@ -832,24 +898,6 @@ __global__ __launch_bounds__(kBlock) void k_emb_grad_dense(float4* __restrict__ 
     emb_grad_dense_body(out, n4, w4, offs, list, gs, blockIdx.x, gridDim.x);
 }
 
-// The data-parallel gradient tail in one launch: blocks [0, ngrad) write the dense embedding
-// gradient, blocks >= ngrad reduce the first-level slab partials into the dense-layer gradient
-// (k_mlp_update's work with no update and no L2; same order, bitwise).
-__global__ __launch_bounds__(kBlock) void k_emb_grad_dense_mlp(float4* __restrict__ out, uint32_t n4, uint32_t w4,
-                                                               const int32_t* __restrict__ offs,
-                                                               const int32_t* __restrict__ list,
-                                                               const float4* __restrict__ gs, uint32_t ngrad,
-                                                               int P, const float* __restrict__ slabs, int nslab,
-                                                               float* __restrict__ mlp_grad) {
-    if (blockIdx.x >= ngrad) {
-        const L2Table none{};
-        mlp_update_body<NCF_OPT_ADAM>(nullptr, nullptr, nullptr, P, slabs, nslab, nullptr, mlp_grad, 0, 0, nullptr,
-                                      0.f, 0.f, 0.f, 0.f, none, nullptr, (int)(blockIdx.x - ngrad));
-        return;
-    }
-    emb_grad_dense_body(out, n4, w4, offs, list, gs, blockIdx.x, ngrad);
-}
-
 // Replicated-row Adam/SGD with the all-reduced gradient in one launch: blocks [0, nupd) sweep the
 // table rows with their dense gradient (k_emb_update<OPT, kGradDense, false>'s work), blocks
 // >= nupd step the dense layers with theirs (k_mlp_update's work, no L2).  Used only with every
@@ -940,6 +988,36 @@ __global__ __launch_bounds__(kBlock) void k_slab_partial(const float* __restrict
 }
 
 
+// The data-parallel gradient tail in one launch, both slab levels included: blocks [0, nmlp)
+// reduce the slabs of 16 dense-layer parameters each into their gradient (slab_grad16: the
+// k_slab_partial + k_mlp_update pair's order, bitwise), block nmlp writes the batch summary (when
+// asked), the rest write the dense embedding gradient (ngrad blocks).  Dispatch order puts the
+// short slab blocks first.
+__global__ __launch_bounds__(kBlock) void k_part_tail(float4* __restrict__ out, uint32_t n4, uint32_t w4,
+                                                      const int32_t* __restrict__ offs, const int32_t* __restrict__ list,
+                                                      const float4* __restrict__ gs, uint32_t ngrad, int P,
+                                                      const float* __restrict__ slabs, int nslab, int nmlp,
+                                                      float* __restrict__ mlp_grad, SummaryArgs sa) {
+    int b = (int)blockIdx.x;
+    if (b < nmlp) {
+        const float g = slab_grad16(slabs, P, nslab, b);
+        const int i = b * 16 + (threadIdx.x & 15);
+        if ((threadIdx.x >> 4) == 0 && i < P) mlp_grad[i] = g;
+        return;
+    }
+    b -= nmlp;
+    if (sa.summary) {
+        if (b == 0) {
+            __shared__ float red[4];
+            summary_body(sa.part_bce, sa.nbce, sa.part_hit, sa.part_dcg, sa.nmet, sa.n_groups, nullptr, 0, nullptr, 0,
+                         sa.summary, red);
+            return;
+        }
+        --b;
+    }
+    emb_grad_dense_body(out, n4, w4, offs, list, gs, (uint32_t)b, ngrad);
+}
+
 
 template <int OPT>
 __global__ __launch_bounds__(kBlock) void k_mlp_update(float* __restrict__ p, float* __restrict__ m,
@@ -1017,11 +1095,16 @@ __global__ __launch_bounds__(kBlock) void k_summary(const float* __restrict__ pa
                  red);
 }
 
-__global__ __launch_bounds__(kBlock) void k_stats(const float* __restrict__ summary,
+__global__ __launch_bounds__(kBlock) void k_stats(float* __restrict__ summary,
                                                   const float* __restrict__ reg_emb, int nreg_emb,
                                                   const float* __restrict__ reg_mlp, int nreg_mlp, float inv_batch,
-                                                  double* __restrict__ stats, int32_t* step, int bump) {
+                                                  double* __restrict__ stats, int32_t* step, int bump, SummaryArgs sa) {
     __shared__ float red[4];
+    if (sa.summary) {
+        summary_body(sa.part_bce, sa.nbce, sa.part_hit, sa.part_dcg, sa.nmet, sa.n_groups, nullptr, 0, nullptr, 0,
+                     summary, red);
+        __syncthreads();
+    }
     stats_body(summary, reg_emb, nreg_emb, reg_mlp, nreg_mlp, inv_batch, stats, step, bump, red);
 }
 
@@ -1032,13 +1115,18 @@ struct ScanAhead {
     int64_t r1;
     int32_t *offs, *tot, *uloc, *utot;
 };
-__global__ __launch_bounds__(kBlock) void k_stats_scan(const float* __restrict__ summary,
+__global__ __launch_bounds__(kBlock) void k_stats_scan(float* __restrict__ summary,
                                                        const float* __restrict__ reg_emb, int nreg_emb,
                                                        const float* __restrict__ reg_mlp, int nreg_mlp,
                                                        float inv_batch, double* __restrict__ stats, int32_t* step,
-                                                       int bump, ScanAhead sc) {
+                                                       int bump, ScanAhead sc, SummaryArgs sa) {
     if (blockIdx.x == 0) {
         __shared__ float red[4];
+        if (sa.summary) {   // the batch summary first (launch_summary's work), then the stats
+            summary_body(sa.part_bce, sa.nbce, sa.part_hit, sa.part_dcg, sa.nmet, sa.n_groups, nullptr, 0, nullptr, 0,
+                         summary, red);
+            __syncthreads();
+        }
         stats_body(summary, reg_emb, nreg_emb, reg_mlp, nreg_mlp, inv_batch, stats, step, bump, red);
     } else {
         scan_local_body<true>(sc.cnt, sc.r1, sc.offs, sc.tot, sc.uloc, sc.utot, (int)blockIdx.x - 1);
@@ -1213,9 +1301,9 @@ hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, vo
                       at<int32_t>(ws, L.cnt), replay_ahead ? 1 : 0, next_fold, per, lazy_bound(s, h)};
         MlpTail mt{};
         if (mlp) {
-            mt = MlpTail{(s.mlp_params + kBlock - 1) / kBlock, mlp->p, mlp->m, mlp->v, s.mlp_params, mlp->slabs,
-                         mlp->nslab, step, h.lr, h.beta_1, h.beta_2, h.epsilon, make_l2_table(s, h),
-                         at<float>(ws, L.part_reg) + kUpdateGrid};
+            mt = MlpTail{mlp->two_level ? (s.mlp_params + 15) / 16 : (s.mlp_params + kBlock - 1) / kBlock, mlp->p,
+                         mlp->m, mlp->v, s.mlp_params, mlp->slabs, mlp->nslab, step, h.lr, h.beta_1, h.beta_2,
+                         h.epsilon, make_l2_table(s, h), at<float>(ws, L.part_reg) + kUpdateGrid, mlp->two_level};
         }
         launch(k_emb_adam_touched, nupd + ncount + (unsigned)mt.nblocks, kBlock, 0, st,
                (float4*)emb, (float4*)m, (float4*)v, w4, at<const int32_t>(ws, L.touched),
@@ -1244,19 +1332,15 @@ hipError_t launch_part_tail(const ncf_shape_t& s, const WsLayout& L, void* ws, f
                             float* mlp_grad, int nslab, int nbce, int nmet, float n_groups, float* summary,
                             hipStream_t st) {
     const int P = s.mlp_params;
-    const int gridp = (P + kBlock - 1) / kBlock;
-    const int per = (nslab + kSlabSplit - 1) / kSlabSplit;
-    const int nch = (nslab + per - 1) / per;
-    float* sp = at<float>(ws, L.slab_part);
+    const int nmlp = (P + 15) / 16;
     SummaryArgs sa{summary, at<float>(ws, L.part_bce), at<float>(ws, L.part_hit), at<float>(ws, L.part_dcg), nbce,
                    nmet, n_groups};
-    launch(k_slab_partial, dim3(gridp + 1, nch), kBlock, 0, st, at<const float>(ws, L.slabs), P, nslab, per, sp, sa);
     const uint32_t w4 = (uint32_t)(s.row_width / 4);
     const uint32_t n4 = (uint32_t)((s.num_rows - row_begin) * w4);
     const uint32_t ngrad = n4 ? (uint32_t)kUpdateGrid : 0u;
-    launch(k_emb_grad_dense_mlp, ngrad + (uint32_t)gridp, kBlock, 0, st, (float4*)emb_grad, n4, w4,
+    launch(k_part_tail, ngrad + (uint32_t)nmlp + (summary ? 1u : 0u), kBlock, 0, st, (float4*)emb_grad, n4, w4,
            at<int32_t>(ws, L.offs) + row_begin, at<int32_t>(ws, L.list), at<const float4>(ws, L.gs), ngrad, P,
-           (const float*)sp, nch, mlp_grad);
+           at<const float>(ws, L.slabs), nslab, nmlp, mlp_grad, sa);
     return hipGetLastError();
 }
 
@@ -1318,6 +1402,14 @@ hipError_t launch_mlp_update(const ncf_shape_t& s, const WsLayout& L, void* ws, 
     const L2Table t = make_l2_table(s, h);
     const float* slabs = at<float>(ws, L.slabs);
     bool summary_done = summary == nullptr || summary_nbce < 0;
+    if (defer && defer->two_level && h.optimizer == NCF_OPT_ADAM && do_update && !grad_out && !want_reg &&
+        nslab > 2 * kSlabSplit && t.n == 0 && summary_done) {
+        // the touched-row update launch does both slab-reduction levels and the Adam step
+        *defer = MlpDeferred{mlp, m, v, slabs, nslab, 1};
+        *nreg = 0;
+        return hipSuccess;
+    }
+    if (defer) defer->two_level = 0;
     if (nslab > 2 * kSlabSplit) {
         const int per = (nslab + kSlabSplit - 1) / kSlabSplit;
         const int nch = (nslab + per - 1) / per;
@@ -1337,7 +1429,7 @@ hipError_t launch_mlp_update(const ncf_shape_t& s, const WsLayout& L, void* ws, 
     }
     if (defer && h.optimizer == NCF_OPT_ADAM && do_update && !grad_out && !want_reg && nslab > 0) {
         // the caller runs the Adam step of the dense layers inside the touched-row update launch
-        *defer = MlpDeferred{mlp, m, v, slabs, nslab};
+        *defer = MlpDeferred{mlp, m, v, slabs, nslab, 0};
         *nreg = t.n > 0 ? grid : 0;
         return hipGetLastError();
     }
@@ -1445,21 +1537,27 @@ hipError_t launch_summary(const WsLayout& L, void* ws, int nbce, int nmet, float
     return hipGetLastError();
 }
 
-hipError_t launch_stats(const WsLayout& L, void* ws, const float* summary, int nreg_emb, int nreg_mlp,
+hipError_t launch_stats(const WsLayout& L, void* ws, const float* summary_in, int nreg_emb, int nreg_mlp,
                         float inv_batch, double* stats, int32_t* step, bool bump_step, hipStream_t st,
-                        bool scan_ahead, int64_t scan_keys) {
+                        bool scan_ahead, int64_t scan_keys, SummaryFirst sf) {
     const float* reg = at<float>(ws, L.part_reg);
+    // written only by the summary_first block (the workspace's summary); read-only otherwise
+    float* summary = const_cast<float*>(summary_in);
+    SummaryArgs sa{nullptr, nullptr, nullptr, nullptr, 0, 0, 0.f};
+    if (sf.nbce >= 0)
+        sa = SummaryArgs{summary, at<float>(ws, L.part_bce), at<float>(ws, L.part_hit), at<float>(ws, L.part_dcg),
+                         sf.nbce, sf.nmet, sf.n_groups};
     if (scan_ahead) {
         const int64_t r1 = scan_keys + 1;
         const int nscan = (int)((r1 + kScanBlock - 1) / kScanBlock);
         ScanAhead sc{at<const int32_t>(ws, L.cnt), r1, at<int32_t>(ws, L.offs_local), at<int32_t>(ws, L.tot),
                      at<int32_t>(ws, L.uloc), at<int32_t>(ws, L.utot)};
         launch(k_stats_scan, 1 + nscan, kBlock, 0, st, summary, reg, nreg_emb, reg + kUpdateGrid, nreg_mlp, inv_batch,
-               stats, step, bump_step ? 1 : 0, sc);
+               stats, step, bump_step ? 1 : 0, sc, sa);
         return hipGetLastError();
     }
     launch(k_stats, 1, kBlock, 0, st, summary, reg, nreg_emb, reg + kUpdateGrid, nreg_mlp, inv_batch, stats, step,
-                                  bump_step ? 1 : 0);
+                                  bump_step ? 1 : 0, sa);
     return hipGetLastError();
 }
 
