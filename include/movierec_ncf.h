@@ -127,7 +127,9 @@ typedef struct ncf_hyper {
                                            12288 floats, e.g. config D);
                                            3 / 4 / 5: (fast_path shapes) the 128-sample tile
                                            kernel / the sample-unit kernel (the default) / the
-                                           wave-chain kernel (fp32 operands; else the unit one) */
+                                           wave-chain kernel (fp32 operands; else the unit one);
+                                           6: the wave-chain kernel in its one-wave form (no
+                                           separate weight-gradient waves) */
     int32_t index_ready;                /* 1: the contribution index of this call's batch was built
                                            beforehand by ncf_build_index (same ids, same ws): skip it;
                                            2: its contributions were counted and scanned by the

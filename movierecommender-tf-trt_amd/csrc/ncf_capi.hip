@@ -192,7 +192,7 @@ hipError_t launch_predict(const ncf_shape_t& s, const ncf_hyper_t* h, const ncf:
 // MFMA forward/backward kernel for a fused shape: the sample-unit kernel (ncf_unit.hip), the
 // wave-chain kernel (ncf_wave.hip) or the 128-sample tile kernel (ncf_fused.hip).
 // NCF_FB_KERNEL=unit|wave|tile forces one; hyper->force_generic 3 / 4 / 5 pick tile / unit / wave
-// per call.  bf16 operands run on the unit kernel only.
+// per call (6: the wave kernel's one-wave form).  bf16 operands run on the unit kernel only.
 int fb_variant(const ncf_shape_t& s, const ncf_hyper_t* h, int64_t n) {
     static const int mode = [] {
         const char* e = getenv("NCF_FB_KERNEL");
@@ -205,7 +205,7 @@ int fb_variant(const ncf_shape_t& s, const ncf_hyper_t* h, int64_t n) {
     if (!ncf::unit_supported(s)) return NCF_FB_TILE;
     if (fg == 3) return NCF_FB_TILE;
     if (fg == 4) return NCF_FB_UNIT;
-    if (fg == 5) return ncf::wave_supported(s) && !bf16 ? NCF_FB_WAVE : NCF_FB_UNIT;
+    if (fg == 5 || fg == 6) return ncf::wave_supported(s) && !bf16 ? NCF_FB_WAVE : NCF_FB_UNIT;
     int v = mode                      ? mode
             : n > NCF_UNIT_MAX_BATCH      ? NCF_FB_TILE
             : n >= NCF_WAVE_MIN_BATCH     ? NCF_FB_WAVE
@@ -475,6 +475,8 @@ int ncf_group_metrics(const float* probs, const float* labels, int64_t n_groups,
 struct FbOut {
     int nslab = 0, nbce = 0, nmet = 0;
     float n_groups = 0.f;
+    bool defer_metrics = false;         // in: groups <= 8 may leave their metrics to the update launch
+    ncf::MetricsDeferred met{0, nullptr, nullptr, 0, 0, 0};  // out: deferred (nblocks > 0)
     SideStream* index_side = nullptr;  // index built on this side stream: join before using it
 };
 
@@ -564,7 +566,8 @@ static int run_fb(const ncf_shape_t& s, const ncf::WsLayout& L, const ncf_model_
         return fail(NCF_EINVAL, "bf16 MLP operands need a fused-kernel shape and the unit kernel");
     if (variant == NCF_FB_WAVE)
         e = ncf::launch_fb_wave(s, L, ws, model->emb, model->mlp, users, items, labels, n, h->inv_batch, ids,
-                                h->group, h->k, &out->nslab, &out->nbce, &out->nmet, st, fold, check_fold);
+                                h->group, h->k, &out->nslab, &out->nbce, &out->nmet, st, fold, check_fold,
+                                h->force_generic == 6);
     else if (unit)
         e = ncf::launch_fb_unit(s, L, ws, model->emb, model->mlp, users, items, labels, n, h->inv_batch, ids,
                                 h->group, h->k, &out->nslab, &out->nbce, &out->nmet, st, fold, h->mlp_bf16 != 0,
@@ -583,7 +586,13 @@ static int run_fb(const ncf_shape_t& s, const ncf::WsLayout& L, const ncf_model_
     float* probs = ncf::at<float>(ws, L.probs);
     const int64_t ng = n / h->group;
     out->n_groups = (float)ng;
-    if (out->nmet == 0) {
+    if (out->nmet == 0 && out->defer_metrics && h->group <= 8 && ng > 0) {
+        // the touched-row update launch computes them (MetricsDeferred, when the batch summary
+        // is written after it; else the caller launches them): one launch fewer
+        const int grid = (int)((ng + ncf::kBlock - 1) / ncf::kBlock);
+        out->met = ncf::MetricsDeferred{grid, probs, labels, ng, h->group, h->k};
+        out->nmet = grid;
+    } else if (out->nmet == 0) {
         prof_begin(NCF_K_METRICS, st);
         e = ncf::launch_group_metrics(probs, labels, ng, h->group, h->k, nullptr, nullptr,
                                       ncf::at<float>(ws, L.part_hit), ncf::at<float>(ws, L.part_dcg), &out->nmet, st);
@@ -630,6 +639,9 @@ static int train_step_impl(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t
     if (lazy && h->l2[0] != 0.0f)
         return fail(NCF_EINVAL, "deferred decay (row_step) needs the embedding L2 off: the loss sums the whole table");
     CatchupCtx cc{s, &L, model, optim, h, ws, st, n, users, items};
+    // deferred decay on one stream: the group metrics (groups <= 8 the kernel does not compute)
+    // ride in the touched-row update launch
+    fb.defer_metrics = lazy && side_stream_mode() == 0;
     if (int r = run_fb(*s, L, model, h, users, items, labels, n, ws, probs_out, &fb, st, false,
                        lazy ? catchup_touched : nullptr, &cc))
         return r;
@@ -656,6 +668,16 @@ static int train_step_impl(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t
     // update launch too, and the batch summary in the stats launch (two launches fewer)
     const bool two_level = defer_mlp && h->optimizer == NCF_OPT_ADAM && ncf::part_tail_foldable(*s, *h, fb.nslab);
     mlp_def.two_level = two_level ? 1 : 0;
+    if (fb.met.nblocks > 0 && !two_level) {
+        // the summary is written before the touched-row update launch: the metrics go first
+        int nm = 0;
+        prof_begin(NCF_K_METRICS, st);
+        e = ncf::launch_group_metrics(fb.met.probs, fb.met.labels, fb.met.ng, fb.met.group, fb.met.k, nullptr, nullptr,
+                                      ncf::at<float>(ws, L.part_hit), ncf::at<float>(ws, L.part_dcg), &nm, st);
+        prof_end(NCF_K_METRICS, st);
+        if (e != hipSuccess) return hip_check(e, "metrics");
+        fb.met.nblocks = 0;
+    }
     prof_begin(NCF_K_MLP_UPDATE, st2);
     e = ncf::launch_mlp_update(*s, L, ws, model->mlp, optim->mlp_m, optim->mlp_v, optim->step, *h, fb.nslab, nullptr,
                                nullptr, true, &nreg_mlp, st2, false, fold && !two_level ? fb.nbce : -1, fb.nmet,
@@ -666,7 +688,8 @@ static int train_step_impl(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t
     if (lazy)
         e = ncf::launch_emb_update_touched(*s, L, ws, model->emb, optim->emb_m, optim->emb_v, optim->row_step,
                                            optim->step, *h, st, next_users, next_items, n_next,
-                                           mlp_def.p ? &mlp_def : nullptr, index_fold(*s, h));
+                                           mlp_def.p ? &mlp_def : nullptr, index_fold(*s, h),
+                                           fb.met.nblocks > 0 ? &fb.met : nullptr);
     else
         e = ncf::launch_emb_update(*s, L, ws, model->emb, optim->emb_m, optim->emb_v, optim->step, *h, nullptr,
                                    s->num_rows, st);

@@ -354,12 +354,13 @@ bool fused_supported(const ncf_shape_t& s);
 // sample-unit kernel (ncf_unit.hip): the fused shapes, 32-sample units split across a
 // workgroup's waves by output feature; same outputs and folding as launch_fb_fused
 bool unit_supported(const ncf_shape_t& s);
-// wave-chain kernel (ncf_wave.hip): outputs as launch_fb_unit (fp32 operands only)
+// wave-chain kernel (ncf_wave.hip): outputs as launch_fb_unit (fp32 operands only); one_wave: the
+// form without separate weight-gradient waves (else chosen by shape and NCF_WAVE_SPLIT)
 bool wave_supported(const ncf_shape_t& s);
 hipError_t launch_fb_wave(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, const float* mlp,
                           const int32_t* users, const int32_t* items, const float* labels, int64_t n,
                           float inv_batch, IdSpace ids, int group, int topk, int* nslab, int* nbce, int* nmet,
-                          hipStream_t st, int fold, bool check_fold);
+                          hipStream_t st, int fold, bool check_fold, bool one_wave = false);
 hipError_t launch_fb_unit(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, const float* mlp,
                           const int32_t* users, const int32_t* items, const float* labels, int64_t n,
                           float inv_batch, IdSpace ids, int group, int topk, int* nslab, int* nbce, int* nmet,
@@ -421,11 +422,21 @@ struct MlpDeferred {
     int two_level;             // 1: the launch also does the first-level slab reduction
                                // (k_slab_partial's work, same order: bitwise) — no launch of its own
 };
+// The step's group metrics handed from the forward/backward to the touched-row update launch
+// (groups <= 8 that the kernel did not compute): nblocks partials into ws part_hit / part_dcg
+struct MetricsDeferred {
+    int nblocks;
+    const float* probs;
+    const float* labels;
+    int64_t ng;
+    int group, k;
+};
 hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, void* ws, float* emb, float* m,
                                      float* v, int32_t* row_step, int32_t* step, const ncf_hyper_t& h,
                                      hipStream_t st, const int32_t* next_users = nullptr,
                                      const int32_t* next_items = nullptr, int64_t n_next = 0,
-                                     const MlpDeferred* mlp = nullptr, int next_fold = 0);
+                                     const MlpDeferred* mlp = nullptr, int next_fold = 0,
+                                     const MetricsDeferred* met = nullptr);
 // dense gradient of rows [row_begin, num_rows) into out (indexed from row_begin)
 hipError_t launch_emb_grad_dense(const ncf_shape_t& s, const WsLayout& L, void* ws, float* out, hipStream_t st,
                                   int64_t row_begin = 0);

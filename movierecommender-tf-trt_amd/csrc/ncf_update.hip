@@ -556,6 +556,11 @@ __device__ inline void mlp_update_body(float* __restrict__ p, float* __restrict_
     if (threadIdx.x == 0 && part_reg) part_reg[blk] = reg;
 }
 
+__device__ __forceinline__ void group_metrics_body(const float* __restrict__ probs, const float* __restrict__ labels,
+                                                   int64_t ng, int group, int k, float* __restrict__ hit,
+                                                   float* __restrict__ dcg, float* __restrict__ part_hit,
+                                                   float* __restrict__ part_dcg, int blk);
+
 struct CountAhead {
     int nupd;                  // blocks [0, nupd) update rows; [nupd, nupd + ncount) count
     int ncount;
@@ -573,6 +578,17 @@ struct CountAhead {
 
 // the dense layers' Adam (k_mlp_update<ADAM>'s work) in blocks >= nupd + ncount of the same launch;
 // two_level: in the FIRST blocks of the launch, 16 parameters per block, from the raw slabs
+// the step's group metrics (groups <= 8, not computed in the forward/backward kernel) in the
+// first blocks of the touched-row update launch: nblocks partials
+struct MetricsTail {
+    int nblocks;               // 0: none
+    const float* probs;
+    const float* labels;
+    int64_t ng;
+    int group, k;
+    float *part_hit, *part_dcg;
+};
+
 struct MlpTail {
     int nblocks;               // 0: none
     float *p, *m, *v;
@@ -652,7 +668,7 @@ __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_tou
                                                              const float4* __restrict__ gs,
                                                              int32_t* __restrict__ row_step, const int32_t* step,
                                                              float lr, float b1, float b2, float eps,
-                                                             CountAhead ca, MlpTail mt) {
+                                                             CountAhead ca, MlpTail mt, MetricsTail mm) {
     // block order: [count (+ catch-up ahead)] [touched-row update] [dense-layer Adam]: the
     // latency-bound replay blocks are dispatched first, so they run under the HBM-bound update
     // (interleaving them one in every (nupd + ncount) / ncount blocks was measured slower: 60.2
@@ -660,6 +676,13 @@ __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_tou
     // (two_level: the dense-layer blocks come first — each waits one round of slab loads, under
     // everything else)
     int b = (int)blockIdx.x;
+    // the step's hr/dcg partials (k_group_metrics' work, groups <= 8) in the first blocks: the
+    // probabilities are final once the forward/backward launch before this one is done
+    if (b < mm.nblocks) {
+        group_metrics_body(mm.probs, mm.labels, mm.ng, mm.group, mm.k, nullptr, nullptr, mm.part_hit, mm.part_dcg, b);
+        return;
+    }
+    b -= mm.nblocks;
     if (mt.two_level) {
         if (b < mt.nblocks) {
             mlp_slabs_adam(mt, b);
@@ -669,7 +692,7 @@ __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_tou
     } else if (b >= ca.nupd + ca.ncount) {
         mlp_update_body<NCF_OPT_ADAM>(mt.p, mt.m, mt.v, mt.P, mt.slabs, mt.nslab, nullptr, nullptr, 1, 0, mt.step,
                                       mt.lr, mt.b1, mt.b2, mt.eps, mt.l2t, mt.part_reg,
-                                      (int)blockIdx.x - ca.nupd - ca.ncount);
+                                      b - ca.nupd - ca.ncount);
         return;
     }
     if (b < ca.ncount) {
@@ -1033,12 +1056,12 @@ __global__ __launch_bounds__(kBlock) void k_mlp_update(float* __restrict__ p, fl
 // Per-group hit@k / dcg@k: the label's position in the stable descending
 // order equals #(p_j > p_lab) + #(j < lab with p_j == p_lab)  (top_k ties →
 // lower index first; test/test_model.py:121-149).
-__global__ __launch_bounds__(kBlock) void k_group_metrics(const float* __restrict__ probs,
-                                                          const float* __restrict__ labels, int64_t ng, int group,
-                                                          int k, float* __restrict__ hit, float* __restrict__ dcg,
-                                                          float* __restrict__ part_hit, float* __restrict__ part_dcg) {
+__device__ __forceinline__ void group_metrics_body(const float* __restrict__ probs, const float* __restrict__ labels,
+                                                   int64_t ng, int group, int k, float* __restrict__ hit,
+                                                   float* __restrict__ dcg, float* __restrict__ part_hit,
+                                                   float* __restrict__ part_dcg, int blk) {
     __shared__ float red[4];
-    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t g = (int64_t)blk * kBlock + threadIdx.x;
     float h = 0.f, d = 0.f;
     if (g < ng) {
         const float* pr = probs + g * group;
@@ -1061,9 +1084,15 @@ __global__ __launch_bounds__(kBlock) void k_group_metrics(const float* __restric
     h = block_sum_256(h, red);
     d = block_sum_256(d, red);
     if (threadIdx.x == 0) {
-        if (part_hit) part_hit[blockIdx.x] = h;
-        if (part_dcg) part_dcg[blockIdx.x] = d;
+        if (part_hit) part_hit[blk] = h;
+        if (part_dcg) part_dcg[blk] = d;
     }
+}
+__global__ __launch_bounds__(kBlock) void k_group_metrics(const float* __restrict__ probs,
+                                                          const float* __restrict__ labels, int64_t ng, int group,
+                                                          int k, float* __restrict__ hit, float* __restrict__ dcg,
+                                                          float* __restrict__ part_hit, float* __restrict__ part_dcg) {
+    group_metrics_body(probs, labels, ng, group, k, hit, dcg, part_hit, part_dcg, (int)blockIdx.x);
 }
 
 __global__ __launch_bounds__(kBlock) void k_rank(const float* __restrict__ probs, int64_t ng, int group,
@@ -1282,7 +1311,7 @@ hipError_t launch_row_step_fill(int32_t* row_step, int64_t R, const int32_t* ste
 hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, void* ws, float* emb, float* m,
                                      float* v, int32_t* row_step, int32_t* step, const ncf_hyper_t& h,
                                      hipStream_t st, const int32_t* next_users, const int32_t* next_items,
-                                     int64_t n_next, const MlpDeferred* mlp, int next_fold) {
+                                     int64_t n_next, const MlpDeferred* mlp, int next_fold, const MetricsDeferred* met) {
     const bool replay_ahead = next_users != nullptr && NCF_CATCHUP_AHEAD;
     const uint32_t w4 = (uint32_t)(s.row_width / 4);
     const uint32_t n4 = (uint32_t)(lazy_bound(s, h) * w4);  // SGD: the rows under deferred decay
@@ -1305,10 +1334,13 @@ hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, vo
                          mlp->m, mlp->v, s.mlp_params, mlp->slabs, mlp->nslab, step, h.lr, h.beta_1, h.beta_2,
                          h.epsilon, make_l2_table(s, h), at<float>(ws, L.part_reg) + kUpdateGrid, mlp->two_level};
         }
-        launch(k_emb_adam_touched, nupd + ncount + (unsigned)mt.nblocks, kBlock, 0, st,
+        MetricsTail mm{};
+        if (met) mm = MetricsTail{met->nblocks, met->probs, met->labels, met->ng, met->group, met->k,
+                                  at<float>(ws, L.part_hit), at<float>(ws, L.part_dcg)};
+        launch(k_emb_adam_touched, nupd + ncount + (unsigned)mt.nblocks + (unsigned)mm.nblocks, kBlock, 0, st,
                (float4*)emb, (float4*)m, (float4*)v, w4, at<const int32_t>(ws, L.touched),
                at<const int2>(ws, L.touched_oc), at<const int32_t>(ws, L.nuniq), offs, list, gs, row_step, (const int32_t*)step, h.lr, h.beta_1, h.beta_2,
-               h.epsilon, ca, mt);
+               h.epsilon, ca, mt, mm);
     } else
         launch(k_emb_sgd_hot, kUpdateGrid, kBlock, 0, st, (float4*)emb, n4, w4, offs, list, gs, h.lr);
     return hipGetLastError();

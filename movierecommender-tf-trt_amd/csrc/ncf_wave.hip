@@ -33,6 +33,7 @@
 // Bitwise reproducible.  Reference semantics: movierec/model.py:154-214.
 
 #include <cmath>
+#include <cstdlib>
 
 #include "ncf_common.h"
 #include "ncf_internal.h"
@@ -105,6 +106,11 @@ struct WShape {
                          TG2 = TH2 + 16 * ts(B2), TG3 = TG2 + 16 * ts(B2), WREG = TG3 + 16 * 16;
     static constexpr size_t LDS_BYTES = (size_t)(WLDS + 4 * WREG) * 4;
     static_assert(LDS_BYTES <= 163840, "LDS budget");
+    // split form (k_fb_wave<..., true>): no X^T buffer (the weight-gradient wave loads X from the
+    // table), two buffers per chain wave (the unit being written, the unit being contracted)
+    static constexpr int XSZ = 16 * ts(B0), WREG2 = WREG - XSZ;
+    static constexpr size_t LDS_BYTES2 = (size_t)(WLDS + 8 * WREG2) * 4;
+    static constexpr bool SPLIT_OK = LDS_BYTES2 <= 163840 && WLDS >= XSZ;
     // the prologue moves the flat parameters as float4 groups: no group straddles two segments,
     // and the contiguous segments land on 16-byte-aligned LDS positions
     static_assert(OB1 % 4 == 0 && OW2 % 4 == 0 && OB2 % 4 == 0 && OW3 % 4 == 0 && OB3 % 4 == 0 && OWO % 4 == 0 &&
@@ -224,15 +230,44 @@ __device__ unsigned long long g_wave_s[256 * 4 * 16];
     } while (0)
 #define NCF_WS(slot, v)                                                                                \
     do {                                                                                               \
-        if ((threadIdx.x & 63) == 0 && blockIdx.x < 256) g_wave_s[blockIdx.x * 64 + (threadIdx.x >> 6) * 16 + (slot)] = (v); \
+        if ((threadIdx.x & 63) == 0 && blockIdx.x < 256 && threadIdx.x < 256) g_wave_s[blockIdx.x * 64 + (threadIdx.x >> 6) * 16 + (slot)] = (v); \
     } while (0)
 #else
 #define NCF_WT(it, ph) ((void)0)
 #define NCF_WS(slot, v) ((void)0)
 #endif
 
-template <class S, int FOLD, bool MET>
-__global__ __launch_bounds__(256, 1) void k_fb_wave(const float* __restrict__ emb, const float* __restrict__ mlp,
+// SPLIT: 8 waves, two per SIMD.  Waves 0-3 run the chain of their units as above except the
+// weight gradients; wave 4 + p (the same SIMD as chain wave p) contracts chain wave p's units into
+// the dW accumulators: it reads G1, H1, G2, H2, G3 from the transposed buffers the chain wave
+// wrote (two per chain wave, by unit parity) and X from the table rows (lane li: features
+// B0 li .. B0 li + B0 - 1 of sample 4 q + lq, so dW1 tile a's row i is feature B0 i + a).  One
+// workgroup barrier per unit hands a unit over: barrier k follows chain unit k and precedes its
+// contraction, so barrier k + 1 also frees unit k's buffers for unit k + 2.  The chain's phases
+// that issue no MFMA now have the weight-gradient wave's 168 MFMAs per unit beside them on the
+// same SIMD.  Same MFMAs on the same operands in the same order as the one-wave form: bitwise.
+#ifndef NCF_SPLIT_PRIO
+#define NCF_SPLIT_PRIO 1
+#endif
+// experiment switches (wrong results, timing only): NCF_SPLIT_NODW 1 = the weight-gradient waves
+// skip their contraction; NCF_SPLIT_NOSYNC 1 = also no per-unit barrier
+#ifndef NCF_SPLIT_NODW
+#define NCF_SPLIT_NODW 0
+#endif
+#ifndef NCF_SPLIT_NOSYNC
+#define NCF_SPLIT_NOSYNC 0
+#endif
+// 1: a weight-gradient wave contracts unit k while its chain wave runs unit k + 1 past layer 1
+// (two barriers per unit); 0 (the default): right after unit k (one barrier, beside the chain's
+// layer 1).  Measured at config C (profiles/r03_b): 0 53.0-53.3 us, 1 54.4-55.3, the one-wave
+// form 55.0-55.2; phase stamps of 1 show the chain's MFMA-free output and G3 sections growing by
+// the partner's MFMA time (a SIMD's VALU / MFMA issue is shared, MI355X_MICROARCH.md "Two waves
+// per SIMD" item 3)
+#ifndef NCF_SPLIT_LATE
+#define NCF_SPLIT_LATE 0
+#endif
+template <class S, int FOLD, bool MET, bool SPLIT = false>
+__global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* __restrict__ emb, const float* __restrict__ mlp,
                                                      const int32_t* __restrict__ users,
                                                      const int32_t* __restrict__ items,
                                                      const float* __restrict__ labels, int64_t n, IdSpace ids,
@@ -251,14 +286,23 @@ __global__ __launch_bounds__(256, 1) void k_fb_wave(const float* __restrict__ em
     extern __shared__ __attribute__((aligned(16))) float lds[];
     float* wl = lds;
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    float* tb = lds + S::WLDS + wv * S::WREG;
+    const int pw = wv & 3;                     // the chain (split: chain / weight-gradient pair) index
+    const bool dwave = SPLIT && wv >= 4;       // split: the weight-gradient wave of pair pw
+    static_assert(!SPLIT || S::SPLIT_OK, "split form: LDS budget");
+    // split: chain wave pw's buffer for units of parity `par` (its TX offset is never used)
+    auto tbuf = [&](int par) {
+        return SPLIT ? lds + S::WLDS + (pw * 2 + par) * S::WREG2 - S::XSZ : lds + S::WLDS + wv * S::WREG;
+    };
+    float* tb = tbuf(0);
     const float eps = 1e-7f, hi_clip = 1.0f - eps;
     static_assert(!MET || FOLD > 1, "in-kernel metrics for groups of FOLD samples");
 
     const int li = lane & 15, g = lane >> 4;  // sample lane, lane group (the MFMA k index)
     const int64_t nunits = (n + 15) / 16;
     const int64_t ustride = (int64_t)gridDim.x * 4;
-    int64_t un = (int64_t)blockIdx.x * 4 + wv;
+    int64_t un = (int64_t)blockIdx.x * 4 + pw;
+    // split: units (barriers) of this workgroup = those of its chain wave 0, the one with the most
+    const int64_t nit = SPLIT ? (nunits - (int64_t)blockIdx.x * 4 + ustride - 1) / ustride : 0;
 
     // ids run two units ahead, rows one unit ahead.  A masked sample (past n or an id outside the
     // table) reads row 0 (a valid address) and gets dz = 0: it contributes nothing.
@@ -318,21 +362,27 @@ __global__ __launch_bounds__(256, 1) void k_fb_wave(const float* __restrict__ em
     // floats, all issued before any is used), are in flight while the operand layout's padding is
     // zeroed; the first unit's MLP input follows the ids; then the parameters go to LDS.  Every
     // segment of the flat layout starts at a multiple of 4 floats, so a float4 never straddles two.
-    load_ids(un, cu, cv, cy);
+    // (split: the chain waves load the parameters; the weight-gradient waves only pass the barriers)
     constexpr int NV4 = S::OBO / 4, NVT = (NV4 + 255) / 256;
     const __amdgpu_buffer_rsrc_t ml_rsrc =
         __builtin_amdgcn_make_buffer_rsrc((void*)mlp, (short)0, (int)(S::P * 4), 0x00020000);
     f32x4 pv[NVT];
+    float pbo = 0.f;
+    if (!dwave) {
+        load_ids(un, cu, cv, cy);
 #pragma unroll
-    for (int j = 0; j < NVT; ++j) {
-        const int q = (int)threadIdx.x + 256 * j;
-        pv[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ml_rsrc, q < NV4 ? (uint32_t)q * 16u : kDrop, 0, 0));
+        for (int j = 0; j < NVT; ++j) {
+            const int q = (int)threadIdx.x + 256 * j;
+            pv[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ml_rsrc, q < NV4 ? (uint32_t)q * 16u : kDrop, 0, 0));
+        }
+        pbo = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ml_rsrc, (uint32_t)S::OBO * 4u, 0, 0));
+        for (int e = threadIdx.x; e < S::WLDS / 4; e += 256) reinterpret_cast<f32x4*>(wl)[e] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    const float pbo = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ml_rsrc, (uint32_t)S::OBO * 4u, 0, 0));
-    for (int e = threadIdx.x; e < S::WLDS / 4; e += 256) reinterpret_cast<f32x4*>(wl)[e] = f32x4{0.f, 0.f, 0.f, 0.f};
     __syncthreads();
-    load_x(un, cu, cv);
-    load_ids(un + ustride, nu, nv, ny);
+    if (!dwave) {
+        load_x(un, cu, cv);
+        load_ids(un + ustride, nu, nv, ny);
+    }
     // float4 group at flat offset e0 -> its LDS operand-layout positions
     auto put4 = [&](int e0, const f32x4& v) {
         if (e0 < S::OB1) {
@@ -356,14 +406,221 @@ __global__ __launch_bounds__(256, 1) void k_fb_wave(const float* __restrict__ em
             *reinterpret_cast<f32x4*>(wl + S::SWO + (e0 - S::OWO)) = v;  // [gmf | layer 3] output kernel
         }
     };
+    if (!dwave) {
 #pragma unroll
-    for (int j = 0; j < NVT; ++j) {
-        const int q = (int)threadIdx.x + 256 * j;
-        if (q < NV4) put4(4 * q, pv[j]);
+        for (int j = 0; j < NVT; ++j) {
+            const int q = (int)threadIdx.x + 256 * j;
+            if (q < NV4) put4(4 * q, pv[j]);
+        }
+        if (threadIdx.x == 0) wl[S::SBO] = pbo;
     }
-    if (threadIdx.x == 0) wl[S::SBO] = pbo;
     __syncthreads();
     NCF_WS(2, __builtin_readcyclecounter());
+
+    // ---- epilogue pieces shared by both forms: row w (one per chain / pair) holds half of the dW
+    // tiles at a time in the accumulator layout ([tile][lane][4]) followed by the bias /
+    // output-kernel / loss entries; the rows are added in a fixed order ((w0 + w2) + (w1 + w3))
+    constexpr int NTHR = SPLIT ? 512 : 256;
+    float* slab = slabs + (size_t)blockIdx.x * S::P;
+    const float* R0 = lds;
+    const float* R1 = lds + S::PR;
+    const float* R2 = lds + 2 * S::PR;
+    const float* R3 = lds + 3 * S::PR;
+    float* R = lds + pw * S::PR;
+    static_assert((size_t)4 * S::PR * 4 <= (SPLIT ? S::LDS_BYTES2 : S::LDS_BYTES), "epilogue rows");
+    // tile element (lane gq * 16 + c, register r) is row 16 a + 4 gq + r (split dW1: row
+    // B0 (4 gq + r) + a), column 16 b + c of its matrix
+    auto reduce_tiles = [&](int t0, int t1) {
+        for (int q = threadIdx.x; q < (t1 - t0) * 64; q += NTHR) {
+            auto at4 = [&](const float* row) { return *reinterpret_cast<const f32x4*>(row + 4 * q); };
+            const f32x4 x = (at4(R0) + at4(R2)) + (at4(R1) + at4(R3));
+            const int t = t0 + (q >> 6);  // uniform per wave
+            int base, ld, rs = 1;
+            bool keep = true;
+            if (t < S::NT1) {
+                if constexpr (SPLIT) {
+                    base = S::OW1 + (t / B1) * L1 + 16 * (t % B1) + li, ld = L1, rs = B0;
+                } else {
+                    base = S::OW1 + 16 * (t / B1) * L1 + 16 * (t % B1) + li, ld = L1;
+                }
+            } else if (t < S::NT1 + S::NT2) {
+                base = S::OW2 + 16 * ((t - S::NT1) / B2) * L2 + 16 * ((t - S::NT1) % B2) + li, ld = L2;
+            } else {
+                base = S::OW3 + 16 * (t - S::NT1 - S::NT2) * L3 + li, ld = L3;
+                keep = li < L3;
+            }
+            if (keep) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) slab[base + (4 * g + r) * rs * ld] = x[r];
+            }
+        }
+    };
+    // biases, output kernel, output bias: back to back in the rows (RB1 .. RBO), segment by
+    // segment in the flat layout; the loss / hit / dcg partials
+    auto reduce_rest = [&]() {
+        for (int e = threadIdx.x; e <= S::RBO - S::RB1; e += NTHR) {
+            const int d = e < L1 ? S::OB1 + e
+                          : e < L1 + L2 ? S::OB2 + (e - L1)
+                          : e < L1 + L2 + L3 ? S::OB3 + (e - L1 - L2)
+                                             : S::OWO + (e - L1 - L2 - L3);
+            slab[d] = (R0[S::RB1 + e] + R2[S::RB1 + e]) + (R1[S::RB1 + e] + R3[S::RB1 + e]);
+        }
+        if (threadIdx.x == 0) {
+            part_bce[blockIdx.x] = (R0[S::RX] + R2[S::RX]) + (R1[S::RX] + R3[S::RX]);
+            if constexpr (MET) {
+                part_hit[blockIdx.x] = (R0[S::RX + 1] + R2[S::RX + 1]) + (R1[S::RX + 1] + R3[S::RX + 1]);
+                part_dcg[blockIdx.x] = (R0[S::RX + 2] + R2[S::RX + 2]) + (R1[S::RX + 2] + R3[S::RX + 2]);
+            }
+        }
+    };
+
+    if constexpr (SPLIT) {
+        if (dwave) {
+            // ---- the weight-gradient wave of pair pw
+            f32x4 dw1[B0][B1], dw2[B1][B2], dw3[B2];
+#pragma unroll
+            for (int a = 0; a < B0; ++a)
+#pragma unroll
+                for (int b = 0; b < B1; ++b) dw1[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int a = 0; a < B1; ++a)
+#pragma unroll
+                for (int b = 0; b < B2; ++b) dw2[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int a = 0; a < B2; ++a) dw3[a] = f32x4{0.f, 0.f, 0.f, 0.f};
+            float ab1[B1], ab2[B2], ab3 = 0.f;
+#pragma unroll
+            for (int t = 0; t < B1; ++t) ab1[t] = 0.f;
+#pragma unroll
+            for (int t = 0; t < B2; ++t) ab2[t] = 0.f;
+            // X operands of k-step q (sample 4 q + lq, MLP-input features B0 li .. + B0 - 1: lanes
+            // li < 8 the user half, else the item half) in slot q & 1: steps 0 and 1 are loaded
+            // before the unit's barrier, steps 2 and 3 once the MFMAs of steps 0 and 1 have read
+            // their slot.  A masked sample reads the chain's row 0 (its G rows are zero).
+            float xq[2][B0];
+            auto load_xq = [&](int64_t u, int q) {
+                const int64_t si = u * 16 + 4 * q + g;
+                const uint32_t off = si < n ? (uint32_t)si * 4u : kDrop;
+                const int xu = (int)__builtin_amdgcn_raw_buffer_load_b32(us_rsrc, off, 0, 0);
+                const int xv = (int)__builtin_amdgcn_raw_buffer_load_b32(it_rsrc, off, 0, 0);
+                const bool okr = si < n && (unsigned)xu < (unsigned)ids.ubound && (unsigned)xv < (unsigned)ids.ibound;
+                const int row = okr ? (li < 8 ? xu : ids.ibase + xv) : 0;
+                const float4* xs = reinterpret_cast<const float4*>(emb + (size_t)row * W + G + (li & 7) * B0);
+#pragma unroll
+                for (int k = 0; k < B0 / 4; ++k) {
+                    const float4 v = xs[k];
+                    xq[q & 1][4 * k] = v.x, xq[q & 1][4 * k + 1] = v.y, xq[q & 1][4 * k + 2] = v.z,
+                                 xq[q & 1][4 * k + 3] = v.w;
+                }
+            };
+            // unit u's contraction from chain buffer `par`
+            auto contract = [&](int64_t u, int par) {
+                const float* tq = tbuf(par);
+                pipe<4, 1, DwOps<1, B1, B2>>(
+                    [&](int q, DwOps<1, B1, B2>& o) {
+                        const int srow = 4 * q + g;
+                        ldsv<B1>(tq + S::TG1 + srow * T1 + li * B1, o.g1);
+                        ldsv<B1>(tq + S::TH1 + srow * T1 + li * B1, o.h1);
+                        ldsv<B2>(tq + S::TG2 + srow * T2 + li * B2, o.g2);
+                        ldsv<B2>(tq + S::TH2 + srow * T2 + li * B2, o.h2);
+                        o.g3 = tq[S::TG3 + srow * 16 + li];
+                    },
+                    [&](int q, const DwOps<1, B1, B2>& o) {
+#pragma unroll
+                        for (int a = 0; a < B0; ++a)
+#pragma unroll
+                            for (int b = 0; b < B1; ++b) dw1[a][b] = mfma16(xq[q & 1][a], o.g1[b], dw1[a][b]);
+#pragma unroll
+                        for (int a = 0; a < B1; ++a)
+#pragma unroll
+                            for (int b = 0; b < B2; ++b) dw2[a][b] = mfma16(o.h1[a], o.g2[b], dw2[a][b]);
+#pragma unroll
+                        for (int a = 0; a < B2; ++a) dw3[a] = mfma16(o.h2[a], o.g3, dw3[a]);
+#pragma unroll
+                        for (int b = 0; b < B1; ++b) ab1[b] += o.g1[b];
+#pragma unroll
+                        for (int b = 0; b < B2; ++b) ab2[b] += o.g2[b];
+                        ab3 += o.g3;
+                        if (q < 2) load_xq(u, q + 2);
+                    });
+            };
+            if constexpr (NCF_SPLIT_LATE) {
+                // unit it - 1 is contracted between barriers A(it) (the chain's layer 1 of unit it
+                // done) and B(it): beside the chain's sections that issue few MFMAs, not beside its
+                // layer 1
+                int64_t uprev = nunits;  // none
+                for (int64_t it = 0; it < nit; ++it, un += ustride) {
+                    const bool havep = uprev < nunits;
+                    if (havep) {  // in flight while the chain runs layer 1
+                        load_xq(uprev, 0);
+                        load_xq(uprev, 1);
+                    }
+                    if (!NCF_SPLIT_NOSYNC) __syncthreads();  // A(it)
+                    if (havep && !NCF_SPLIT_NODW) contract(uprev, (int)((it - 1) & 1));
+                    if (!NCF_SPLIT_NOSYNC) __syncthreads();  // B(it): unit it's buffers written
+                    uprev = un;
+                }
+                if (uprev < nunits && !NCF_SPLIT_NODW) {
+                    load_xq(uprev, 0);
+                    load_xq(uprev, 1);
+                    contract(uprev, (int)((nit - 1) & 1));
+                }
+            } else {
+                for (int64_t it = 0; it < nit; ++it, un += ustride) {
+                    const bool have = un < nunits;
+                    if (have) {  // in flight while the chain finishes the unit
+                        load_xq(un, 0);
+                        load_xq(un, 1);
+                    }
+                    if (!NCF_SPLIT_NOSYNC) __syncthreads();  // barrier it: chain wave pw wrote unit it's buffers
+                    if (have && !NCF_SPLIT_NODW) contract(un, (int)(it & 1));
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < B1; ++t) ab1[t] = group_allsum(ab1[t]);
+#pragma unroll
+            for (int t = 0; t < B2; ++t) ab2[t] = group_allsum(ab2[t]);
+            ab3 = group_allsum(ab3);
+            auto put_tiles = [&](int t0, int t1) {
+#pragma unroll
+                for (int a = 0; a < B0; ++a)
+#pragma unroll
+                    for (int b = 0; b < B1; ++b) {
+                        const int t = a * B1 + b;
+                        if (t >= t0 && t < t1) *reinterpret_cast<f32x4*>(R + (t - t0) * 256 + lane * 4) = dw1[a][b];
+                    }
+#pragma unroll
+                for (int a = 0; a < B1; ++a)
+#pragma unroll
+                    for (int b = 0; b < B2; ++b) {
+                        const int t = S::NT1 + a * B2 + b;
+                        if (t >= t0 && t < t1) *reinterpret_cast<f32x4*>(R + (t - t0) * 256 + lane * 4) = dw2[a][b];
+                    }
+#pragma unroll
+                for (int a = 0; a < B2; ++a) {
+                    const int t = S::NT1 + S::NT2 + a;
+                    if (t >= t0 && t < t1) *reinterpret_cast<f32x4*>(R + (t - t0) * 256 + lane * 4) = dw3[a];
+                }
+            };
+            __syncthreads();  // every wave is done with the weights and the buffers
+            if (g == 0) {
+#pragma unroll
+                for (int t = 0; t < B1; ++t) R[S::RB1 + 16 * t + li] = ab1[t];
+#pragma unroll
+                for (int t = 0; t < B2; ++t) R[S::RB2 + 16 * t + li] = ab2[t];
+                if (li < L3) R[S::RB3 + li] = ab3;
+            }
+            put_tiles(0, S::NTH);
+            __syncthreads();
+            reduce_tiles(0, S::NTH);
+            reduce_rest();
+            __syncthreads();  // the first round's rows are read before the second overwrites them
+            put_tiles(S::NTH, S::NT);
+            __syncthreads();
+            reduce_tiles(S::NTH, S::NT);
+            return;
+        }
+    }
 
     f32x4 dw1[B0][B1], dw2[B1][B2], dw3[B2];
 #pragma unroll
@@ -401,8 +658,22 @@ __global__ __launch_bounds__(256, 1) void k_fb_wave(const float* __restrict__ em
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), gs_rsrc, off, 0, 0);
     };
     NCF_WT(0, 8);
+#if NCF_SPLIT_PRIO
+    if constexpr (SPLIT) __builtin_amdgcn_s_setprio(1);  // the chain wave's serial sections first
+#endif
     int itw = -1;
-    for (; un < nunits; un += ustride) {
+    // split: one pass per barrier of the workgroup (a chain wave past its last unit only passes
+    // the barrier)
+    for (int64_t it = 0; SPLIT ? it < nit : un < nunits; ++it, un += ustride) {
+      if (SPLIT && un >= nunits) {
+        if (!NCF_SPLIT_NOSYNC) {
+            if (NCF_SPLIT_LATE) __syncthreads();
+            __syncthreads();
+        }
+        continue;
+      }
+      if constexpr (SPLIT) tb = tbuf((int)(it & 1));
+      {
         ++itw;
         NCF_WT(itw, 0);
         const int64_t s0 = un * 16, sg = s0 + li, un1 = un + ustride;
@@ -415,9 +686,11 @@ __global__ __launch_bounds__(256, 1) void k_fb_wave(const float* __restrict__ em
 
         // ---- X^T for dW1 (row li: features XQ lq + q), then layer 1: k-step q takes feature
         // XQ lq + q from lane group lq (A: W1 row XQ lq + q, all B1 output blocks in one read)
+        if constexpr (!SPLIT) {
 #pragma unroll
-        for (int q = 0; q < XQ; ++q)
-            tb[S::TX + li * T0 + (XQ / 16) * g + (q & 15) * B0 + (q >> 4)] = xr[q];
+            for (int q = 0; q < XQ; ++q)
+                tb[S::TX + li * T0 + (XQ / 16) * g + (q & 15) * B0 + (q >> 4)] = xr[q];
+        }
         f32x4 h1[B1];
 #pragma unroll
         for (int t = 0; t < B1; ++t) h1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -443,6 +716,8 @@ __global__ __launch_bounds__(256, 1) void k_fb_wave(const float* __restrict__ em
             stsv<B1>(tb + S::TH1 + li * T1 + (4 * g + r) * B1, v);
         }
 
+        // split, late contraction: barrier A (the weight-gradient wave starts on the previous unit)
+        if constexpr (SPLIT) if (NCF_SPLIT_LATE && !NCF_SPLIT_NOSYNC) __syncthreads();
         NCF_WT(itw, 1);
         // ---- layer 2: k-step (t, r) takes H1 feature 16 t + 4 lq + r (this lane's register)
         f32x4 h2[B2];
@@ -716,7 +991,7 @@ __global__ __launch_bounds__(256, 1) void k_fb_wave(const float* __restrict__ em
 
         // ---- weight gradients over the unit's 16 samples: k-step q takes sample 4 q + lq
         NCF_WT(itw, 6);
-        pipe<4, 2, DwOps<B0, B1, B2>>(
+        if constexpr (!SPLIT) pipe<4, 2, DwOps<B0, B1, B2>>(
             [&](int q, DwOps<B0, B1, B2>& o) {
                 const int srow = 4 * q + g;
                 ldsv<B0>(tb + S::TX + srow * T0 + li * B0, o.x);
@@ -750,18 +1025,25 @@ __global__ __launch_bounds__(256, 1) void k_fb_wave(const float* __restrict__ em
         cu = nu, cv = nv, cy = ny;
         nu = tu, nv = tv, ny = ty;
         NCF_WT(itw, 7);
+      }
+      if constexpr (SPLIT) if (!NCF_SPLIT_NOSYNC) __syncthreads();  // hand the unit to the weight-gradient wave
     }
+#if NCF_SPLIT_PRIO
+    if constexpr (SPLIT) __builtin_amdgcn_s_setprio(0);
+#endif
 
     // ---- epilogue: per-lane sums over the 16 sample lanes, then the four waves in LDS
     NCF_WS(11, __builtin_readcyclecounter());
 #pragma unroll
     for (int r = 0; r < 4; ++r) ah3[r] = row_sum(ah3[r]);
-    // bias sums: over the 4 lane groups (samples 4 q + lq)
+    if constexpr (!SPLIT) {
+        // bias sums: over the 4 lane groups (samples 4 q + lq)
 #pragma unroll
-    for (int t = 0; t < B1; ++t) ab1[t] = group_allsum(ab1[t]);
+        for (int t = 0; t < B1; ++t) ab1[t] = group_allsum(ab1[t]);
 #pragma unroll
-    for (int t = 0; t < B2; ++t) ab2[t] = group_allsum(ab2[t]);
-    ab3 = group_allsum(ab3);
+        for (int t = 0; t < B2; ++t) ab2[t] = group_allsum(ab2[t]);
+        ab3 = group_allsum(ab3);
+    }
 #pragma unroll
     for (int e = 0; e < GQ; ++e) agmf[e] = row_sum(agmf[e]);
     acc_dbo = group_allsum(row_sum(acc_dbo));
@@ -770,8 +1052,7 @@ __global__ __launch_bounds__(256, 1) void k_fb_wave(const float* __restrict__ em
     acc_dcg = group_allsum(row_sum(acc_dcg));
     __syncthreads();  // every wave is done with the weights and its buffers
     NCF_WS(14, __builtin_readcyclecounter());
-    float* R = lds + wv * S::PR;
-    // every dW tile of this wave with its tile number
+    // every dW tile of this wave with its tile number (one-wave form)
     auto for_tiles = [&](auto f) {
 #pragma unroll
         for (int a = 0; a < B0; ++a)
@@ -784,12 +1065,14 @@ __global__ __launch_bounds__(256, 1) void k_fb_wave(const float* __restrict__ em
 #pragma unroll
         for (int a = 0; a < B2; ++a) f(S::NT1 + S::NT2 + a, dw3[a]);
     };
-    if (g == 0) {
+    if constexpr (!SPLIT) {
+        if (g == 0) {
 #pragma unroll
-        for (int t = 0; t < B1; ++t) R[S::RB1 + 16 * t + li] = ab1[t];
+            for (int t = 0; t < B1; ++t) R[S::RB1 + 16 * t + li] = ab1[t];
 #pragma unroll
-        for (int t = 0; t < B2; ++t) R[S::RB2 + 16 * t + li] = ab2[t];
-        if (li < L3) R[S::RB3 + li] = ab3;
+            for (int t = 0; t < B2; ++t) R[S::RB2 + 16 * t + li] = ab2[t];
+            if (li < L3) R[S::RB3 + li] = ab3;
+        }
     }
     if (li == 0) {
 #pragma unroll
@@ -804,60 +1087,24 @@ __global__ __launch_bounds__(256, 1) void k_fb_wave(const float* __restrict__ em
         R[S::RX + 1] = acc_hit;
         R[S::RX + 2] = acc_dcg;
     }
-    // Two rounds of half the tiles: every wave puts its tiles in its own row (straight from the
-    // accumulators), then all 256 threads add the four rows in a fixed order,
-    // slab = (w0 + w2) + (w1 + w3), and write the flat slab; tile element (lane gq * 16 + c,
-    // register r) is row 16 a + 4 gq + r, column 16 b + c of its matrix
-    float* slab = slabs + (size_t)blockIdx.x * S::P;
-    const float* R0 = lds;
-    const float* R1 = lds + S::PR;
-    const float* R2 = lds + 2 * S::PR;
-    const float* R3 = lds + 3 * S::PR;
-    auto round = [&](int t0, int t1) {
-        for_tiles([&](int t, f32x4& v) {
-            if (t >= t0 && t < t1) *reinterpret_cast<f32x4*>(R + (t - t0) * 256 + lane * 4) = v;
-        });
-        __syncthreads();
-        for (int q = threadIdx.x; q < (t1 - t0) * 64; q += 256) {
-            auto at4 = [&](const float* row) { return *reinterpret_cast<const f32x4*>(row + 4 * q); };
-            const f32x4 x = (at4(R0) + at4(R2)) + (at4(R1) + at4(R3));
-            const int t = t0 + (q >> 6);  // uniform per wave
-            int base, ld;
-            bool keep = true;
-            if (t < S::NT1) {
-                base = S::OW1 + 16 * (t / B1) * L1 + 16 * (t % B1) + li, ld = L1;
-            } else if (t < S::NT1 + S::NT2) {
-                base = S::OW2 + 16 * ((t - S::NT1) / B2) * L2 + 16 * ((t - S::NT1) % B2) + li, ld = L2;
-            } else {
-                base = S::OW3 + 16 * (t - S::NT1 - S::NT2) * L3 + li, ld = L3;
-                keep = li < L3;
-            }
-            if (keep) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) slab[base + (4 * g + r) * ld] = x[r];
-            }
-        }
+    // Two rounds of half the tiles: every wave (split: every weight-gradient wave) puts its tiles
+    // in its own row straight from the accumulators, then all threads add the four rows in a fixed
+    // order, slab = (w0 + w2) + (w1 + w3), and write the flat slab
+    auto put_tiles = [&](int t0, int t1) {
+        if constexpr (!SPLIT)
+            for_tiles([&](int t, f32x4& v) {
+                if (t >= t0 && t < t1) *reinterpret_cast<f32x4*>(R + (t - t0) * 256 + lane * 4) = v;
+            });
     };
-    round(0, S::NTH);
-    // biases, output kernel, output bias: back to back in the rows (RB1 .. RBO), segment by
-    // segment in the flat layout
-    for (int e = threadIdx.x; e <= S::RBO - S::RB1; e += 256) {
-        const int d = e < L1 ? S::OB1 + e
-                      : e < L1 + L2 ? S::OB2 + (e - L1)
-                      : e < L1 + L2 + L3 ? S::OB3 + (e - L1 - L2)
-                                         : S::OWO + (e - L1 - L2 - L3);
-        slab[d] = (R0[S::RB1 + e] + R2[S::RB1 + e]) + (R1[S::RB1 + e] + R3[S::RB1 + e]);
-    }
-    if (threadIdx.x == 0) {
-        part_bce[blockIdx.x] = (R0[S::RX] + R2[S::RX]) + (R1[S::RX] + R3[S::RX]);
-        if constexpr (MET) {
-            part_hit[blockIdx.x] = (R0[S::RX + 1] + R2[S::RX + 1]) + (R1[S::RX + 1] + R3[S::RX + 1]);
-            part_dcg[blockIdx.x] = (R0[S::RX + 2] + R2[S::RX + 2]) + (R1[S::RX + 2] + R3[S::RX + 2]);
-        }
-    }
+    put_tiles(0, S::NTH);
+    __syncthreads();
+    reduce_tiles(0, S::NTH);
+    reduce_rest();
     NCF_WS(15, __builtin_readcyclecounter());
     __syncthreads();  // the first round's rows are read before the second overwrites them
-    round(S::NTH, S::NT);
+    put_tiles(S::NTH, S::NT);
+    __syncthreads();
+    reduce_tiles(S::NTH, S::NT);
     NCF_WT(0, 9);
     NCF_WS(12, __builtin_readcyclecounter());
     NCF_WS(13, __builtin_amdgcn_s_memrealtime());
@@ -874,18 +1121,28 @@ bool wmatches(const ncf_shape_t& s) {
            s.layers[3] == S::L3 && s.gmf_dim == S::G && s.row_width == S::W && s.gmf_stride == S::G;
 }
 
-template <class S>
-hipError_t launch_wave_one(const WsLayout& L, void* ws, const float* emb, const float* mlp, const int32_t* users,
-                           const int32_t* items, const float* labels, int64_t n, float inv_batch, IdSpace ids,
-                           int group, int topk, int* nslab, int* nbce, int* nmet, hipStream_t st, int fold,
-                           bool check_fold) {
-    static bool configured = false;  // one-time attribute set per shape (idempotent)
+// NCF_WAVE_SPLIT (environment, read once): 0 forces the one-wave form on shapes the split form fits
+static bool split_enabled() {
+    static const int on = [] {
+        const char* e = getenv("NCF_WAVE_SPLIT");
+        return e && *e ? atoi(e) : 1;
+    }();
+    return on != 0;
+}
+
+template <class S, bool SPLIT>
+hipError_t launch_wave_form(const WsLayout& L, void* ws, const float* emb, const float* mlp, const int32_t* users,
+                            const int32_t* items, const float* labels, int64_t n, float inv_batch, IdSpace ids,
+                            int group, int topk, int* nslab, int* nbce, int* nmet, hipStream_t st, int fold,
+                            bool check_fold) {
+    constexpr size_t lds = SPLIT ? S::LDS_BYTES2 : S::LDS_BYTES;
+    static bool configured = false;  // one-time attribute set per shape and form (idempotent)
     if (!configured) {
-        for (const void* k : {(const void*)k_fb_wave<S, 0, false>, (const void*)k_fb_wave<S, 2, false>,
-                              (const void*)k_fb_wave<S, 4, false>, (const void*)k_fb_wave<S, 8, false>,
-                              (const void*)k_fb_wave<S, 2, true>, (const void*)k_fb_wave<S, 4, true>,
-                              (const void*)k_fb_wave<S, 8, true>}) {
-            hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)S::LDS_BYTES);
+        for (const void* k : {(const void*)k_fb_wave<S, 0, false, SPLIT>, (const void*)k_fb_wave<S, 2, false, SPLIT>,
+                              (const void*)k_fb_wave<S, 4, false, SPLIT>, (const void*)k_fb_wave<S, 8, false, SPLIT>,
+                              (const void*)k_fb_wave<S, 2, true, SPLIT>, (const void*)k_fb_wave<S, 4, true, SPLIT>,
+                              (const void*)k_fb_wave<S, 8, true, SPLIT>}) {
+            hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (e != hipSuccess) return e;
         }
         configured = true;
@@ -898,25 +1155,39 @@ hipError_t launch_wave_one(const WsLayout& L, void* ws, const float* emb, const 
     // groups get the separate metrics launch
     const bool in_kernel = fold > 1 && group == fold;
     auto go = [&](auto kern) {
-        launch(kern, grid, 256, S::LDS_BYTES, st, emb, mlp, users, items, labels, n, ids, inv_batch,
+        launch(kern, grid, SPLIT ? 512 : 256, lds, st, emb, mlp, users, items, labels, n, ids, inv_batch,
                at<float>(ws, L.probs), at<float>(ws, L.gs), at<float>(ws, L.slabs), at<float>(ws, L.part_bce), group,
                topk, at<float>(ws, L.part_hit), at<float>(ws, L.part_dcg),
                check_fold ? at<const int32_t>(ws, L.ifold) : nullptr, at<int32_t>(ws, L.err));
     };
     switch (fold * 2 + (in_kernel ? 1 : 0)) {
-        case 0: go(k_fb_wave<S, 0, false>); break;
-        case 4: go(k_fb_wave<S, 2, false>); break;
-        case 8: go(k_fb_wave<S, 4, false>); break;
-        case 16: go(k_fb_wave<S, 8, false>); break;
-        case 5: go(k_fb_wave<S, 2, true>); break;
-        case 9: go(k_fb_wave<S, 4, true>); break;
-        case 17: go(k_fb_wave<S, 8, true>); break;
+        case 0: go(k_fb_wave<S, 0, false, SPLIT>); break;
+        case 4: go(k_fb_wave<S, 2, false, SPLIT>); break;
+        case 8: go(k_fb_wave<S, 4, false, SPLIT>); break;
+        case 16: go(k_fb_wave<S, 8, false, SPLIT>); break;
+        case 5: go(k_fb_wave<S, 2, true, SPLIT>); break;
+        case 9: go(k_fb_wave<S, 4, true, SPLIT>); break;
+        case 17: go(k_fb_wave<S, 8, true, SPLIT>); break;
         default: return hipErrorInvalidValue;
     }
     *nslab = grid;
     *nbce = grid;
     *nmet = in_kernel ? grid : 0;
     return hipGetLastError();
+}
+
+template <class S>
+hipError_t launch_wave_one(const WsLayout& L, void* ws, const float* emb, const float* mlp, const int32_t* users,
+                           const int32_t* items, const float* labels, int64_t n, float inv_batch, IdSpace ids,
+                           int group, int topk, int* nslab, int* nbce, int* nmet, hipStream_t st, int fold,
+                           bool check_fold, bool one_wave) {
+    if constexpr (S::SPLIT_OK) {
+        if (split_enabled() && !one_wave)
+            return launch_wave_form<S, true>(L, ws, emb, mlp, users, items, labels, n, inv_batch, ids, group, topk,
+                                             nslab, nbce, nmet, st, fold, check_fold);
+    }
+    return launch_wave_form<S, false>(L, ws, emb, mlp, users, items, labels, n, inv_batch, ids, group, topk, nslab,
+                                      nbce, nmet, st, fold, check_fold);
 }
 
 }  // namespace
@@ -939,10 +1210,11 @@ bool wave_supported(const ncf_shape_t& s) {
 hipError_t launch_fb_wave(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, const float* mlp,
                           const int32_t* users, const int32_t* items, const float* labels, int64_t n,
                           float inv_batch, IdSpace ids, int group, int topk, int* nslab, int* nbce, int* nmet,
-                          hipStream_t st, int fold, bool check_fold) {
+                          hipStream_t st, int fold, bool check_fold, bool one_wave) {
     if (fold != 0 && (fold < 2 || fold > 8 || (fold & (fold - 1)) != 0 || n % fold != 0)) return hipErrorInvalidValue;
 #define NCF_ARGS \
-    L, ws, emb, mlp, users, items, labels, n, inv_batch, ids, group, topk, nslab, nbce, nmet, st, fold, check_fold
+    L, ws, emb, mlp, users, items, labels, n, inv_batch, ids, group, topk, nslab, nbce, nmet, st, fold, check_fold, \
+        one_wave
     if (wmatches<WShapeC>(s)) return launch_wave_one<WShapeC>(NCF_ARGS);
     if (wmatches<WShapeB>(s)) return launch_wave_one<WShapeB>(NCF_ARGS);
     if (wmatches<WShapeR>(s)) return launch_wave_one<WShapeR>(NCF_ARGS);

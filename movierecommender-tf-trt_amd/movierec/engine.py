@@ -110,12 +110,12 @@ class NCFEngine(object):
         self.hyper.lazy_rows = self.lazy_rows or 0
         self._bind_optim()
         self.set_hyper(optimizer, lr, beta_1, beta_2, layers_l2reg or [0.0] * len(self.layers))
-        if fb_kernel not in (None, "tile", "unit", "wave"):
-            raise ValueError("fb_kernel must be None, 'tile', 'unit' or 'wave'")
+        if fb_kernel not in (None, "tile", "unit", "wave", "wave1"):
+            raise ValueError("fb_kernel must be None, 'tile', 'unit', 'wave' or 'wave1'")
         if precision not in ("fp32", "bf16"):
             raise ValueError("precision must be 'fp32' or 'bf16'")
         self.hyper.force_generic = (1 if force_generic else 2 if force_layered else
-                                    {None: 0, "tile": 3, "unit": 4, "wave": 5}[fb_kernel])
+                                    {None: 0, "tile": 3, "unit": 4, "wave": 5, "wave1": 6}[fb_kernel])
         # bf16 MLP operands (fp32 accumulation, master weights and Adam): BASELINE config B
         self.precision = precision
         self.hyper.mlp_bf16 = 1 if precision == "bf16" else 0

@@ -594,3 +594,28 @@ def test_group_metrics_wide_groups_match_oracle(group):
         np.testing.assert_array_equal(hit.cpu().numpy(), hits.astype(np.float32))
         ref_dcg = np.where(hits, np.log(2.0) / np.log(pos + 2.0), 0.0)
         np.testing.assert_allclose(dcg.cpu().numpy(), ref_dcg, rtol=1e-6, atol=0)
+
+
+@pytest.mark.parametrize("B,group", [(5000, 5), (3000, 3), (100, 5), (4095, 7)])
+def test_deferred_decay_step_metrics_in_update_launch(B, group):
+    """Deferred decay on one stream: a group the forward/backward kernel does not rank in-kernel
+    (not a fold width) has its hr/dcg partials computed by extra blocks of the touched-row update
+    launch (the batch summary follows it) — or, when the summary is written before that launch
+    (few slabs: the one-level tail), by the separate metrics launch.  Either way the step's stats
+    equal the oracle metric of the device probabilities, and the dense-sweep engine (metrics
+    always launched on their own) agrees bitwise on the stats."""
+    shape = O.NCFShape(*SHAPES[2])
+    w = _weights(shape, 70)
+    users, items, y = _batch(shape, B, group, 71 + B)
+    a = _engine(shape, w, lazy_adam=True, max_batch=B)
+    b = _engine(shape, w, lazy_adam=False, max_batch=B)
+    probs = torch.empty(B, dtype=torch.float32, device="cuda")
+    a.train_step(users, items, y, group=group, k=3, probs_out=probs)
+    b.train_step(users, items, y, group=group, k=3)
+    torch.cuda.synchronize()
+    hr, dcg = O.group_metrics(probs.cpu().numpy().astype(np.float64), y, group, 3)
+    r = NCFEngine.read_stats(a.stats)
+    assert r["hr"] == pytest.approx(hr, abs=1e-6) and r["dcg"] == pytest.approx(dcg, abs=1e-6)
+    rb = NCFEngine.read_stats(b.stats)
+    for key in ("hr", "dcg", "loss"):
+        assert r[key] == pytest.approx(rb[key], rel=1e-6, abs=1e-9), key

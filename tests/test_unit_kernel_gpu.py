@@ -1,6 +1,7 @@
 """The MFMA forward/backward kernels of the fused shapes — the sample-unit kernel (ncf_unit.hip,
-the default), the wave-chain kernel (ncf_wave.hip, hyper.force_generic 5) and the 128-sample
-tile kernel (ncf_fused.hip, hyper.force_generic 3) — each against the oracle (reference
+the default), the wave-chain kernel (ncf_wave.hip, hyper.force_generic 5: its split form with
+separate weight-gradient waves where the shape fits, "wave1" = force_generic 6: its one-wave form)
+and the 128-sample tile kernel (ncf_fused.hip, hyper.force_generic 3) — each against the oracle (reference
 movierec/model.py:154-214 restated) on the same batches, forced per engine (``fb_kernel=``) so
 every one runs at every size here.
 
@@ -51,14 +52,14 @@ def _engine(shape, w, kernel, max_batch=4096, **kw):
 
 
 @pytest.mark.parametrize("dims", FUSED_SHAPES, ids=IDS)
-@pytest.mark.parametrize("kernel", ["unit", "wave", "tile"])
+@pytest.mark.parametrize("kernel", ["unit", "wave", "wave1", "tile"])
 @pytest.mark.parametrize("B,group", [(32, 4), (100, 4), (1000, 5), (2050, 2), (4099, 1)])
 def test_grads_match_oracle(dims, kernel, B, group):
     shape = O.NCFShape(*dims)
     w = _weights(shape, 11)
     users, items, y = _batch(shape, B, group, 12 + B)
     eng = _engine(shape, w, kernel)
-    assert eng.kernel_for(B) == "fused-mfma-" + kernel
+    assert eng.kernel_for(B) == "fused-mfma-" + kernel.rstrip("1")
     grads = eng.alloc_grads()
     probs = torch.empty(B, dtype=torch.float32, device="cuda")
     eng.forward_backward(users, items, y, group=group, k=2, inv_batch=1.0 / B, grads=grads, probs_out=probs)
@@ -97,7 +98,7 @@ def test_unit_train_steps_match_oracle(dims, lazy, kernel):
 
 
 @pytest.mark.parametrize("B", [16384 + 100, 20000])
-@pytest.mark.parametrize("kernel", ["unit", "wave"])
+@pytest.mark.parametrize("kernel", ["unit", "wave", "wave1"])
 def test_two_group_schedule_matches_oracle(B, kernel):
     """Batches of >= 16384 run two unit groups per workgroup (two waves per SIMD); uneven rounds
     leave the last group of some workgroups on masked samples.  The wave kernel: several units
@@ -119,7 +120,7 @@ def test_two_group_schedule_matches_oracle(B, kernel):
     assert grads[2][0].item() == pytest.approx(O.bce_per_sample(pref, y).sum(), rel=1e-5)
 
 
-@pytest.mark.parametrize("kernel", ["unit", "wave"])
+@pytest.mark.parametrize("kernel", ["unit", "wave", "wave1"])
 def test_unit_masked_ids_and_metrics(kernel):
     """Ids outside the table: NaN probability, no gradient; in-kernel hr/dcg (group | 32, wave
     kernel group | 16) equal the metric of the device probabilities."""
@@ -168,6 +169,38 @@ def test_unit_deterministic_and_close_to_tile():
         assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
         assert torch.max(torch.abs(a[0] - t[0])).item() <= 1e-6
         assert torch.max(torch.abs(a[1] - t[1])).item() <= 1e-6
+
+
+@pytest.mark.parametrize("dims", FUSED_SHAPES, ids=IDS)
+@pytest.mark.parametrize("B,group", [(64, 4), (4096 + 48, 4), (16384 * 4 + 16, 4), (65536, 4), (20000, 8),
+                                     (12000, 2), (3000, 1), (131072 + 32, 4)])
+def test_wave_split_form_bitwise_one_wave(dims, B, group):
+    """The split form (chain waves + weight-gradient waves, one barrier per unit) issues the same
+    MFMAs on the same operands in the same order as the one-wave form: every output bitwise equal,
+    including workgroups whose waves run different unit counts (tails) and the fold / in-kernel
+    metric variants."""
+    shape = O.NCFShape(*dims)
+    w = _weights(shape, 61)
+    users, items, y = _batch(shape, B, group, 62 + B)
+    users[7] = shape.num_users + 1       # masked samples: row 0 read, zero gradient
+    items[B - 3] = -5
+    outs = []
+    for kernel in ("wave", "wave1"):
+        eng = _engine(shape, w, kernel, max_batch=B)
+        grads = eng.alloc_grads()
+        probs = torch.empty(B, dtype=torch.float32, device="cuda")
+        eng.forward_backward(users, items, y, group=group, k=2, inv_batch=1.0 / B, grads=grads, probs_out=probs)
+        eng2 = _engine(shape, w, kernel, max_batch=B)
+        users2 = users.copy()
+        users2[7] = 0
+        items2 = items.copy()
+        items2[B - 3] = 0
+        eng2.train_step(users2, items2, y, group=group, k=min(2, group))
+        torch.cuda.synchronize()
+        outs.append([grads[0].clone(), grads[1].clone(), grads[2].clone(), probs.clone(), eng2.emb.clone(),
+                     eng2.mlp.clone(), eng2.stats.clone()])
+    for a, b in zip(*outs):
+        assert torch.equal(a.nan_to_num(7.0), b.nan_to_num(7.0))
 
 
 def test_kernel_selection_by_batch():
