@@ -269,6 +269,7 @@ WsLayout make_layout(const ncf_shape_t& s, int64_t B, int world) {
     L.offs_local = take((size_t)(K + 1) * 4);
     L.offs = take((size_t)(K + 1) * 4);
     L.tot = take((size_t)L.nscan * 4);
+    L.pre = take((size_t)2 * L.nscan * 4);
     L.part_bce = take((size_t)kMaxSlabs * 4 + (size_t)L.nmetric * 4);
     // one partial per metrics block or per fused workgroup (up to kMaxSlabs)
     L.part_hit = take((size_t)(L.nmetric > kMaxSlabs ? L.nmetric : kMaxSlabs) * 4);

@@ -279,6 +279,155 @@ __global__ __launch_bounds__(kBlock) void k_fill(KeySrc ks, int64_t m, int32_t* 
     }
 }
 
+// Large key spaces (config D: 11 M rows, 5,371 scan blocks).  k_fill derives the exclusive prefix
+// of the scan-block totals in every workgroup (O(nscan) each), which caps its grid at 1,024
+// workgroups and leaves each thread a grid-stride chain of ~40 dependent row passes.  Here one
+// workgroup writes the prefixes to the workspace once (k_prefix) and the fill runs one workgroup
+// per scan block (8 rows per thread) — same outputs as k_fill.
+// One workgroup, one memory round trip: thread t loads the totals of its contiguous chunk of
+// ceil(nscan / 256) scan blocks all at once (at most kPrefixPer each), sums them, one block scan
+// of the chunk sums, then the chunk's prefixes are written.
+constexpr int kPrefixPer = 32;  // chunk length cap: nscan <= 8,192 scan blocks (16.7 M keys)
+__global__ __launch_bounds__(kBlock) void k_prefix(const int32_t* __restrict__ tot, const int32_t* __restrict__ utot,
+                                                   int nscan, int32_t* __restrict__ pre, int32_t* __restrict__ upre) {
+    __shared__ int sw[4];
+    const int per = (nscan + kBlock - 1) / kBlock;
+    const int i0 = (int)threadIdx.x * per;
+    int t[kPrefixPer], u[kPrefixPer];
+    int ts = 0, us = 0;
+#pragma unroll
+    for (int j = 0; j < kPrefixPer; ++j) {
+        const bool in = j < per && i0 + j < nscan;
+        t[j] = in ? tot[i0 + j] : 0;
+        u[j] = in && utot ? utot[i0 + j] : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < kPrefixPer; ++j) ts += t[j], us += u[j];
+    int total;
+    int run = block_exscan_256(ts, sw, &total);
+    int urun = utot ? block_exscan_256(us, sw, &total) : 0;
+#pragma unroll
+    for (int j = 0; j < kPrefixPer; ++j) {
+        if (j < per && i0 + j < nscan) {
+            pre[i0 + j] = run;
+            if (utot) upre[i0 + j] = urun;
+        }
+        run += t[j];
+        urun += u[j];
+    }
+}
+
+template <int MODE, bool UNIQ, bool LIST>
+__global__ __launch_bounds__(kBlock) void k_fill_big(KeySrc ks, int64_t m, int32_t* __restrict__ cnt,
+                                                     const int32_t* __restrict__ local, const int32_t* __restrict__ pre,
+                                                     const int32_t* __restrict__ upre, int nscan, int64_t r1,
+                                                     int32_t* __restrict__ offs_g, int32_t* __restrict__ list, PlanOut po,
+                                                     int32_t* __restrict__ err, int32_t* __restrict__ ifold) {
+    constexpr bool U2 = UNIQ || LIST;
+    const int64_t K = r1 - 1;
+    const int lane = threadIdx.x & 63;
+    const uint64_t par = (lane & 1) ? 0xAAAAAAAAAAAAAAAAull : 0x5555555555555555ull;
+    const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+    const int b = (int)blockIdx.x;
+    if (b == 0 && threadIdx.x == 0) *ifold = ks.fold;
+    if (b < nscan) {
+        // this scan block's keys, 8 per thread: their offsets (and, for a plan or the touched
+        // list, the compact numbering of the occupied keys)
+        const int pb = pre[b];
+        const int ub = U2 ? upre[b] : 0;
+        const int pn = b + 1 < nscan ? pre[b + 1] : 0;  // the next scan block's prefix (key r + 1)
+        const int64_t r0 = (int64_t)b * kScanBlock + threadIdx.x * 8;
+        int loc[9], ul[8];
+        const bool full = r0 + 9 <= r1;  // int4 pairs (256-byte aligned regions, r0 a multiple of 8)
+        if (full) {
+            const int4 a = *reinterpret_cast<const int4*>(local + r0), c = *reinterpret_cast<const int4*>(local + r0 + 4);
+            loc[0] = a.x, loc[1] = a.y, loc[2] = a.z, loc[3] = a.w, loc[4] = c.x, loc[5] = c.y, loc[6] = c.z, loc[7] = c.w;
+            loc[8] = U2 ? local[r0 + 8] : 0;
+            if constexpr (U2) {
+                const int4 x = *reinterpret_cast<const int4*>(po.uloc + r0), y = *reinterpret_cast<const int4*>(po.uloc + r0 + 4);
+                ul[0] = x.x, ul[1] = x.y, ul[2] = x.z, ul[3] = x.w, ul[4] = y.x, ul[5] = y.y, ul[6] = y.z, ul[7] = y.w;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 9; ++j) loc[j] = r0 + j < r1 && (j < 8 || U2) ? local[r0 + j] : 0;
+            if constexpr (U2) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) ul[j] = r0 + j < r1 ? po.uloc[r0 + j] : 0;
+            }
+        }
+        if (full) {
+            *reinterpret_cast<int4*>(offs_g + r0) = make_int4(loc[0] + pb, loc[1] + pb, loc[2] + pb, loc[3] + pb);
+            *reinterpret_cast<int4*>(offs_g + r0 + 4) = make_int4(loc[4] + pb, loc[5] + pb, loc[6] + pb, loc[7] + pb);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int64_t r = r0 + j;
+            if (r >= r1) break;
+            const int o = loc[j] + pb;
+            if (!full) offs_g[r] = o;
+            if constexpr (U2) {
+                if (r < K) {
+                    // key r + 1 opens the next scan block for the last thread's last key
+                    const int o1 = loc[j + 1] + ((r + 1) % kScanBlock == 0 ? pn : pb);
+                    if (o1 > o) {
+                        const int u = ul[j] + ub;
+                        if constexpr (UNIQ) {
+                            po.uniq_rows[u] = (int)(r % ks.S);
+                            po.uoffs[u] = o;
+                        } else {
+                            po.uniq_rows[u] = (int)r;
+                            po.uniq_oc[u] = make_int2(o, o1 - o);
+                        }
+                    }
+                }
+            }
+        }
+        if constexpr (LIST) {
+            if (K / kScanBlock == b && threadIdx.x == 0) *po.nuniq = po.uloc[K] + ub;
+        }
+    }
+    if constexpr (UNIQ) {
+        if (b == 0) {
+            auto uprefix = [&](int64_t x) { return po.uloc[x] + upre[x / kScanBlock]; };
+            for (int d = threadIdx.x; d < ks.world; d += kBlock)
+                po.send_counts[d] = uprefix((int64_t)(d + 1) * ks.S) - uprefix((int64_t)d * ks.S);
+            if (threadIdx.x == 0) {
+                const int nu = uprefix(K);
+                *po.nuniq = nu;
+                po.uoffs[nu] = local[K] + pre[K / kScanBlock];
+            }
+        }
+    }
+    // contributions a wave at a time (k_fill's scheme: a run's head takes its slots with one atomic)
+    const int64_t gstride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t cb = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); cb < m; cb += gstride) {
+        const int64_t c = cb + lane;
+        bool ok = false, own = true;
+        int key = 0;
+        if (c < m) {
+            key = contrib_key<MODE>(c, ks, &ok, &own);
+            if (!ok) atomicOr(err, kErrIdRange);
+            if constexpr (UNIQ) {
+                const int u = ok ? po.uloc[key] + upre[key / kScanBlock] : -1;
+                ((c & 1) ? po.cid_i : po.cid_u)[c >> 1] = u;
+            }
+            ok = ok && own;
+        }
+        const int kk = ok ? key : -2 - lane;
+        const int prev = __shfl_up(kk, 2, 64);
+        const uint64_t heads = ~__ballot(lane >= 2 && prev == kk) & par;
+        const int head = 63 - __clzll(heads & upto);
+        const uint64_t later = heads & ~upto;
+        const int next = later ? __ffsll((unsigned long long)later) - 1 : 64 + (lane & 1);
+        int top = 0;
+        if (ok && lane == head) top = atomicSub(&cnt[key], (next - head) >> 1);
+        top = __shfl(top, head, 64);
+        const int slot = top - 1 - ((lane - head) >> 1);
+        if (ok && slot >= 0) list[local[key] + pre[key / kScanBlock] + slot] = (int)c;
+        else if (ok) atomicOr(err, kErrStaleCount);
+    }
+}
+
 // Sort each key's contribution list ascending.  Keys of <= kSmallSeg entries: one thread,
 // odd-even network in registers.  Longer keys: queued in LDS and sorted by the whole
 // workgroup with a bitmap over the contribution ids (set bits, popcount scan, write back).
@@ -326,11 +475,19 @@ static hipError_t build(const WsLayout& L, void* ws, const KeySrc& ks, int64_t m
     if (!counted)
         launch(k_scan_local<U2>, nscan, kBlock, 0, st, cnt, r1, local, tot, U2 ? at<int32_t>(ws, L.uloc) : nullptr,
                                                    U2 ? at<int32_t>(ws, L.utot) : nullptr);
-    const size_t pre_bytes = (size_t)nscan * 4 * (U2 ? 2 : 1);
-    launch(k_fill<MODE, UNIQ, LIST>, grid_for(m > r1 ? m : r1, 1024), kBlock, pre_bytes, st, ks, m, cnt, local, tot,
-                                                                                         nscan, r1, offs, list, po,
-                                                                                         at<int32_t>(ws, L.err),
-                                                                                         at<int32_t>(ws, L.ifold));
+    if (nscan > kFillBigScan && nscan <= kBlock * kPrefixPer) {
+        int32_t* pre = at<int32_t>(ws, L.pre);
+        launch(k_prefix, 1, kBlock, 0, st, (const int32_t*)tot, U2 ? (const int32_t*)at<int32_t>(ws, L.utot) : nullptr,
+               nscan, pre, pre + nscan);
+        const int64_t gc = (m + kBlock - 1) / kBlock;
+        launch(k_fill_big<MODE, UNIQ, LIST>, (unsigned)(gc > nscan ? gc : nscan), kBlock, 0, st, ks, m, cnt,
+               (const int32_t*)local, (const int32_t*)pre, (const int32_t*)(pre + nscan), nscan, r1, offs, list, po,
+               at<int32_t>(ws, L.err), at<int32_t>(ws, L.ifold));
+    } else {
+        const size_t pre_bytes = (size_t)nscan * 4 * (U2 ? 2 : 1);
+        launch(k_fill<MODE, UNIQ, LIST>, grid_for(m > r1 ? m : r1, 1024), kBlock, pre_bytes, st, ks, m, cnt, local,
+               tot, nscan, r1, offs, list, po, at<int32_t>(ws, L.err), at<int32_t>(ws, L.ifold));
+    }
     if (skip_sort) return hipGetLastError();
     if (hipError_t e = set_sort_lds(nwords)) return e;
     launch(k_sort, (unsigned)((K + kBlock - 1) / kBlock), kBlock, (size_t)nwords * 4, st, offs, K, list, nwords, cnt,

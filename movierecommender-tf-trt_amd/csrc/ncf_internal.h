@@ -20,6 +20,7 @@ constexpr int kMaxSlabs = 1024;        // partial dense-gradient slabs (one per 
 constexpr int kSlabSplit = 16;         // first-level slab reduction fan-in groups
 constexpr int kUpdateGrid = 2048;      // grid of the embedding-table sweep (fixed: deterministic partials)
 constexpr int64_t kMaxBatch = 262144;  // heavy-segment bitmap must fit the LDS (2*B bits = 64 KB)
+constexpr int kFillBigScan = 256;      // scan blocks above which the index fill uses k_prefix + k_fill_big
 
 // Scalars every kernel of a step reads (device copy of hyper + derived).
 struct StepScalars {
@@ -39,6 +40,7 @@ struct WsLayout {
     size_t offs_local;// int32[R+1]  per-2048-row local exclusive scan
     size_t offs;      // int32[R+1]  row -> first list slot
     size_t tot;       // int32[nscan]
+    size_t pre;       // int32[2 * nscan]  exclusive prefixes of tot / utot (large key spaces: k_prefix)
     size_t part_bce;  // float[kMaxSlabs]
     size_t part_hit;  // float[nmetric]
     size_t part_dcg;  // float[nmetric]
@@ -102,20 +104,38 @@ __device__ inline void scan_local_body(const int32_t* __restrict__ cnt, int64_t 
                                        int32_t* __restrict__ utot, int blk) {
     __shared__ int sw[4];
     const int64_t base = (int64_t)blk * kScanBlock + threadIdx.x * 8;
+    // 8 keys per thread: two int4 loads / stores when all 8 are inside (the workspace regions
+    // are 256-byte aligned and base a multiple of 8), else key by key
+    const bool full = base + 8 <= r1;
     int v[8];
     int sum = 0, nz = 0;
+    if (full) {
+        const int4 a = *reinterpret_cast<const int4*>(cnt + base), b = *reinterpret_cast<const int4*>(cnt + base + 4);
+        v[0] = a.x, v[1] = a.y, v[2] = a.z, v[3] = a.w, v[4] = b.x, v[5] = b.y, v[6] = b.z, v[7] = b.w;
+    } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = (base + j < r1) ? cnt[base + j] : 0;
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        v[j] = (base + j < r1) ? cnt[base + j] : 0;
         sum += v[j];
         nz += v[j] > 0;
     }
     int total;
     int run = block_exscan_256(sum, sw, &total);
+    int o[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        if (base + j < r1) offs[base + j] = run;
+        o[j] = run;
         run += v[j];
+    }
+    if (full) {
+        *reinterpret_cast<int4*>(offs + base) = make_int4(o[0], o[1], o[2], o[3]);
+        *reinterpret_cast<int4*>(offs + base + 4) = make_int4(o[4], o[5], o[6], o[7]);
+    } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (base + j < r1) offs[base + j] = o[j];
     }
     if (threadIdx.x == 0) tot[blk] = total;
     if constexpr (UNIQ) {
@@ -123,8 +143,16 @@ __device__ inline void scan_local_body(const int32_t* __restrict__ cnt, int64_t 
         int urun = block_exscan_256(nz, sw, &utotal);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            if (base + j < r1) uloc[base + j] = urun;
+            o[j] = urun;
             urun += v[j] > 0;
+        }
+        if (full) {
+            *reinterpret_cast<int4*>(uloc + base) = make_int4(o[0], o[1], o[2], o[3]);
+            *reinterpret_cast<int4*>(uloc + base + 4) = make_int4(o[4], o[5], o[6], o[7]);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (base + j < r1) uloc[base + j] = o[j];
         }
         if (threadIdx.x == 0) utot[blk] = utotal;
     }

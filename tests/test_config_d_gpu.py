@@ -214,3 +214,45 @@ def test_config_d_full_size_matches_compacted_oracle():
         assert not bool((nz & cold).any()), "untouched rows got moments in [%d, %d)" % (r0, r1)
         assert bool((nz | ~touched[r0:r1]).all()), "a touched row kept zero moments in [%d, %d)" % (r0, r1)
     assert 0 < n_touched < eng.num_rows
+
+
+@pytest.mark.parametrize("lazy", [True, False], ids=["deferred", "dense"])
+def test_large_key_space_index_matches_compacted_table(lazy):
+    """Tables past 256 scan blocks (524,288 rows) build their index with k_prefix + k_fill_big
+    (one workgroup per scan block) instead of k_fill.  Training steps on a 600,000 x 500 table
+    equal, bit for bit, the same steps on the compacted table (the rows the batches read, ids
+    remapped: built by k_fill) — rows interact only through the batches, and with zero initial
+    moments an untouched row does not move under dense Adam either."""
+    Ub, Ib, layers, gmf = 600_000, 500, [64, 32, 16, 8], 8
+    B, steps = 4096, 3
+    rng = np.random.RandomState(7)
+    bt = []
+    for s in range(steps):
+        u = rng.randint(0, Ub, B // GROUP)
+        if s == 0:
+            u[:2] = [0, Ub - 1]
+        bt.append((u.repeat(GROUP).astype(np.int32), rng.randint(0, Ib, B).astype(np.int32),
+                   np.tile([0.0] * (GROUP - 1) + [1.0], B // GROUP).astype(np.float32)))
+    uu = np.unique(np.concatenate([b[0] for b in bt]))
+    ii = np.unique(np.concatenate([b[1] for b in bt]))
+    big = NCFEngine(Ub, Ib, layers, gmf, max_batch=B, lazy_adam=lazy)
+    assert big.num_rows + 1 > 256 * 2048   # more than 256 scan blocks of 2,048 keys
+    _device_tables(big, seed=8)
+    small = NCFEngine(len(uu), len(ii), layers, gmf, max_batch=B, lazy_adam=lazy)
+    small.emb[:len(uu)].copy_(big.emb[torch.from_numpy(uu.astype(np.int64)).cuda()])
+    small.emb[len(uu):].copy_(big.emb[torch.from_numpy(ii.astype(np.int64) + Ub).cuda()])
+    small.mlp.copy_(big.mlp)
+    dev_b = [tuple(torch.from_numpy(a).cuda() for a in b) for b in bt]
+    dev_s = [(torch.from_numpy(np.searchsorted(uu, b[0]).astype(np.int32)).cuda(),
+              torch.from_numpy(np.searchsorted(ii, b[1]).astype(np.int32)).cuda(), d[2]) for b, d in zip(bt, dev_b)]
+    for eng, dev in ((big, dev_b), (small, dev_s)):
+        for s, (u, it, y) in enumerate(dev):
+            nxt = (dev[s + 1][0], dev[s + 1][1]) if lazy and s + 1 < steps else None
+            eng.train_step(u, it, y, group=GROUP, k=2, next_batch=nxt)
+        eng.check_errors()
+        eng.flush() if lazy else None
+    torch.cuda.synchronize()
+    rows = torch.from_numpy(np.concatenate([uu, ii + Ub]).astype(np.int64)).cuda()
+    assert torch.equal(big.emb[rows], small.emb)
+    assert torch.equal(big.emb_m[rows], small.emb_m) and torch.equal(big.emb_v[rows], small.emb_v)
+    assert torch.equal(big.mlp, small.mlp) and torch.equal(big.stats, small.stats)
