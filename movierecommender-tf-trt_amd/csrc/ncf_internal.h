@@ -404,6 +404,16 @@ bool layered_supported(const ncf_shape_t& s);
 hipError_t launch_fb_layered(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, const float* mlp,
                              const int32_t* users, const int32_t* items, const float* labels, int64_t n,
                              float inv_batch, IdSpace ids, int* nslab, int* nbce, hipStream_t st);
+// layer 1 of the layered path on hand-written MFMA (ncf_layer1.hip, config D's widths):
+// forward = gather + X0 + GMF product + relu(W1^T x + b1); backward = dX = W1 G1 into the
+// gradient rows gs with their GMF part (the replaced gather / GEMM / bias / scatter kernels' outputs)
+bool layer1_supported(const ncf_shape_t& s);
+hipError_t launch_layer1_fwd(const ncf_shape_t& s, const float* emb, const float* mlp, const int32_t* users,
+                             const int32_t* items, int64_t n, IdSpace ids, float* x0, float* gmf, float* h1,
+                             hipStream_t st);
+hipError_t launch_layer1_bwd(const ncf_shape_t& s, const float* emb, const float* mlp, const int32_t* users,
+                             const int32_t* items, int64_t n, IdSpace ids, const float* dzo, const float* g1,
+                             float* gs, hipStream_t st);
 // its forward half alone (predict / evaluate): probs, and with labels the BCE partials
 hipError_t launch_predict_layered(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb,
                                   const float* mlp, const int32_t* users, const int32_t* items, const float* labels,

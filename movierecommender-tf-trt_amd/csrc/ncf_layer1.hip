@@ -1,0 +1,360 @@
+// First dense layer of the layer-by-layer path (config D: MLP [256,128,64,32] + GMF 128) on
+// hand-written fp32 MFMA (v_mfma_f32_16x16x4_f32), its gather and scatter fused in.
+//
+// rocBLAS ran this layer as a [n x 256] x [256 x 128] GEMM with the gather (X0, GMF product) and
+// bias + ReLU as separate HBM passes before it, and dX = G1 W1^T as a GEMM with the gradient-row
+// scatter after it (profiles/r03_c/tl_D_step.txt: 112 + 103 us per 65,536-sample step).  Here W1
+// (128 KB at config D) sits in LDS once per workgroup, in the operand layout of ncf_wave.hip
+// (column c of a row at position (c mod 16) B1 + c / 16, row stride 16 B1 + 4), and every wave
+// streams its own 16-sample units through it:
+//
+//   k_lay_l1f  rows -> registers (lane (sample li, lane group lq) holds MLP-input features
+//              XQ lq + q, q < XQ = L0 / 4), H1 = relu(W1^T x + b1) as B1 16 x 16 accumulator
+//              tiles [feature][sample] over L0 / 4 k-steps of B1 MFMAs, then X0, GMF product
+//              (u_g * i_g) and H1 written row-major for the GEMM layers behind it
+//              (model.py:159-181; masked samples: zero X0 and GMF, as k_lay_gather)
+//   k_lay_l1b  G1 rows -> registers (lane (li, lq): features 16 t + 4 lq + r), dX = W1 G1 as
+//              L0 / 16 tiles over 4 B1 k-steps each, written straight into the per-sample
+//              gradient rows gs[2i] / gs[2i + 1] together with their GMF part
+//              dz w_gmf * (the other side's GMF vector) (k_lay_scatter's rows, model.py:159-188)
+//
+// Two units in flight per wave (their loads alternate between two register sets, no copies).
+// Both kernels are HBM-bound more than MFMA-bound at config D: the forward reads the two rows
+// (1 KB of MLP input + 1 KB of GMF vectors per sample) and writes X0, the GMF product and H1 for the
+// GEMM layers (2 KB), the backward reads G1 and the GMF vectors and writes the two gradient rows.
+// Outputs are those of the replaced kernels, so the GEMM layers, the slab reduction and the
+// optimizer launches are unchanged.
+
+#include <cstdlib>
+
+#include "ncf_common.h"
+#include "ncf_internal.h"
+
+namespace ncf {
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+template <int L0_, int L1_, int G_>
+struct L1Shape {
+    static constexpr int L0 = L0_, L1 = L1_, G = G_, D0 = L0 / 2, W = G + D0;
+    static constexpr int B1 = L1 / 16, XQ = L0 / 4, GQ = G / 4, B0 = L0 / 16;
+    static constexpr int S1 = 16 * B1 + 4;            // LDS row stride of W1 (floats)
+    static constexpr int SB = L0 * S1;                // b1 after W1
+    static constexpr size_t LDS = (size_t)(SB + L1) * 4;
+    static_assert(L0 % 64 == 0 && L1 % 16 == 0 && B1 <= 8 && (B1 & (B1 - 1)) == 0 && G % 16 == 0, "layer-1 shape");
+    static_assert(LDS <= 163840, "W1 must fit the LDS");
+};
+
+// W1 [L0][L1] (flat Keras kernel at offset 0) and b1 into the LDS operand layout.  Every float4 a
+// thread moves is loaded in one batch before any LDS store (a load-store loop waits one memory
+// round trip per float4: 32 of them per thread at config D)
+template <class S, int NT>
+__device__ __forceinline__ void load_w1(float* wl, const float* __restrict__ mlp) {
+    constexpr int L0 = S::L0, L1 = S::L1, B1 = S::B1, NV = L0 * L1 / 4 / NT;
+    static_assert(L0 * L1 % (4 * NT) == 0, "W1 in whole float4 rounds");
+    const float4* w4 = reinterpret_cast<const float4*>(mlp);
+    float4 v[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) v[j] = w4[threadIdx.x + NT * j];
+    const float bv = threadIdx.x < L1 ? mlp[L0 * L1 + threadIdx.x] : 0.f;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        const int e = threadIdx.x + NT * j;
+        const int i = (4 * e) / L1, c0 = (4 * e) % L1;
+        float* row = wl + i * S::S1;
+        row[((c0 + 0) & 15) * B1 + ((c0 + 0) >> 4)] = v[j].x;
+        row[((c0 + 1) & 15) * B1 + ((c0 + 1) >> 4)] = v[j].y;
+        row[((c0 + 2) & 15) * B1 + ((c0 + 2) >> 4)] = v[j].z;
+        row[((c0 + 3) & 15) * B1 + ((c0 + 3) >> 4)] = v[j].w;
+    }
+    static_assert(L1 <= NT, "b1 by one pass");
+    if (threadIdx.x < L1) wl[S::SB + threadIdx.x] = bv;
+    __syncthreads();
+}
+
+template <int NB>
+__device__ __forceinline__ void ldsv(const float* p, float (&o)[NB]) {
+    if constexpr (NB == 8) {
+        const f32x4 x = *reinterpret_cast<const f32x4*>(p), y = *reinterpret_cast<const f32x4*>(p + 4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = x[i], o[4 + i] = y[i];
+    } else if constexpr (NB == 4) {
+        const f32x4 x = *reinterpret_cast<const f32x4*>(p);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = x[i];
+    } else if constexpr (NB == 2) {
+        o[0] = p[0], o[1] = p[1];
+    } else {
+        o[0] = p[0];
+    }
+}
+
+// NW waves per workgroup (8: two per SIMD, one unit's registers each; 4: one per SIMD with two
+// units' loads in flight)
+template <class S, int NW>
+__global__ __launch_bounds__(64 * NW, 1) void k_lay_l1f(const float* __restrict__ emb, const float* __restrict__ mlp,
+                                                    const int32_t* __restrict__ users,
+                                                    const int32_t* __restrict__ items, int64_t n, IdSpace ids,
+                                                    float* __restrict__ x0, float* __restrict__ gmf,
+                                                    float* __restrict__ h1) {
+    constexpr int L0 = S::L0, L1 = S::L1, G = S::G, W = S::W, B1 = S::B1, XQ = S::XQ, GQ = S::GQ;
+    extern __shared__ __attribute__((aligned(16))) float wl[];
+    load_w1<S, 64 * NW>(wl, mlp);
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
+    const int64_t nunits = (n + 15) / 16, ustride = (int64_t)gridDim.x * NW;
+    float bias[B1][4];
+#pragma unroll
+    for (int t = 0; t < B1; ++t) ldsv<4>(wl + S::SB + 16 * t + 4 * g, bias[t]);
+
+    struct Unit {
+        float x[XQ];
+        bool ok;
+        int urow, irow;
+    };
+    // the unit's ids and MLP-input rows (lane group lq < 2: the user half, else the item half)
+    auto load = [&](int64_t u, Unit& U) {
+        const int64_t s = u * 16 + li;
+        const bool in = s < n;
+        const int cu = in ? users[s] : 0, cv = in ? items[s] : 0;
+        U.ok = in && (unsigned)cu < (unsigned)ids.ubound && (unsigned)cv < (unsigned)ids.ibound;
+        U.urow = U.ok ? cu : 0;
+        U.irow = U.ok ? ids.ibase + cv : 0;
+        const float4* xs =
+            reinterpret_cast<const float4*>(emb + (size_t)(g < 2 ? U.urow : U.irow) * W + G + (g & 1) * XQ);
+#pragma unroll
+        for (int k = 0; k < XQ / 4; ++k) {
+            const float4 v = xs[k];
+            U.x[4 * k] = v.x, U.x[4 * k + 1] = v.y, U.x[4 * k + 2] = v.z, U.x[4 * k + 3] = v.w;
+        }
+    };
+    auto process = [&](int64_t u, Unit& U) {
+        const int64_t s = u * 16 + li;
+        const bool in = s < n;
+        // the GMF slices (dims GQ lq .. GQ lq + GQ - 1) go out now, under the MFMAs
+        float4 pu[GQ / 4], pi[GQ / 4];
+        {
+            const float4* gu = reinterpret_cast<const float4*>(emb + (size_t)U.urow * W + GQ * g);
+            const float4* gi = reinterpret_cast<const float4*>(emb + (size_t)U.irow * W + GQ * g);
+#pragma unroll
+            for (int k = 0; k < GQ / 4; ++k) pu[k] = gu[k], pi[k] = gi[k];
+        }
+#pragma unroll
+        for (int q = 0; q < XQ; ++q) U.x[q] = U.ok ? U.x[q] : 0.f;  // masked sample: zero input
+        f32x4 h[B1];
+#pragma unroll
+        for (int t = 0; t < B1; ++t) h[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        // k-step q: feature XQ lq + q from lane group lq (A: W1 row XQ lq + q, all B1 blocks in one read)
+        float a[2][B1];
+        ldsv<B1>(wl + (XQ * g) * S::S1 + li * B1, a[0]);
+#pragma unroll
+        for (int q = 0; q < XQ; ++q) {
+            if (q + 1 < XQ) ldsv<B1>(wl + (XQ * g + q + 1) * S::S1 + li * B1, a[(q + 1) & 1]);
+#pragma unroll
+            for (int t = 0; t < B1; ++t) h[t] = mfma16(a[q & 1][t], U.x[q], h[t]);
+        }
+        if (in) {
+            float* xo = x0 + s * L0 + XQ * g;
+#pragma unroll
+            for (int k = 0; k < XQ / 4; ++k)
+                *reinterpret_cast<float4*>(xo + 4 * k) = make_float4(U.x[4 * k], U.x[4 * k + 1], U.x[4 * k + 2], U.x[4 * k + 3]);
+            float* ho = h1 + s * L1 + 4 * g;
+#pragma unroll
+            for (int t = 0; t < B1; ++t)
+                *reinterpret_cast<float4*>(ho + 16 * t) =
+                    make_float4(fmaxf(h[t][0] + bias[t][0], 0.f), fmaxf(h[t][1] + bias[t][1], 0.f),
+                                fmaxf(h[t][2] + bias[t][2], 0.f), fmaxf(h[t][3] + bias[t][3], 0.f));
+            // GMF product of the two rows
+            float4* go = reinterpret_cast<float4*>(gmf + s * G + GQ * g);
+#pragma unroll
+            for (int k = 0; k < GQ / 4; ++k) {
+                const float4 p = pu[k], r = pi[k];
+                go[k] = U.ok ? make_float4(p.x * r.x, p.y * r.y, p.z * r.z, p.w * r.w) : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
+    };
+    const int64_t u0 = (int64_t)blockIdx.x * NW + wv;
+    if constexpr (NW == 8) {
+        Unit A;
+        for (int64_t u = u0; u < nunits; u += ustride) {
+            load(u, A);
+            process(u, A);
+        }
+    } else {
+        Unit A, B;
+        if (u0 < nunits) load(u0, A);
+        for (int64_t u = u0; u < nunits; u += 2 * ustride) {
+            const bool hb = u + ustride < nunits;
+            if (hb) load(u + ustride, B);
+            process(u, A);
+            if (u + 2 * ustride < nunits) load(u + 2 * ustride, A);
+            if (hb) process(u + ustride, B);
+        }
+    }
+}
+
+template <class S, int NW>
+__global__ __launch_bounds__(64 * NW, 1) void k_lay_l1b(const float* __restrict__ emb, const float* __restrict__ mlp,
+                                                    int wo_off, const int32_t* __restrict__ users,
+                                                    const int32_t* __restrict__ items, int64_t n, IdSpace ids,
+                                                    const float* __restrict__ dzo, const float* __restrict__ g1,
+                                                    float* __restrict__ gs) {
+    constexpr int L1 = S::L1, G = S::G, W = S::W, B1 = S::B1, GQ = S::GQ, B0 = S::B0, D0 = S::D0;
+    extern __shared__ __attribute__((aligned(16))) float wl[];
+    load_w1<S, 64 * NW>(wl, mlp);
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
+    const int64_t nunits = (n + 15) / 16, ustride = (int64_t)gridDim.x * NW;
+    const float* wg = mlp + wo_off;  // output kernel, GMF part first
+
+    struct Unit {
+        float gv[B1][4];  // G1 features 16 t + 4 lq + r of sample li
+    };
+    auto load = [&](int64_t u, Unit& U) {
+        const int64_t s = u * 16 + li;
+        const float* gr = g1 + (s < n ? s : 0) * L1 + 4 * g;
+#pragma unroll
+        for (int t = 0; t < B1; ++t) {
+            const float4 v = *reinterpret_cast<const float4*>(gr + 16 * t);
+            U.gv[t][0] = v.x, U.gv[t][1] = v.y, U.gv[t][2] = v.z, U.gv[t][3] = v.w;
+        }
+    };
+    auto process = [&](int64_t u, Unit& U) {
+        const int64_t s = u * 16 + li;
+        const bool in = s < n;
+        int cu = 0, cv = 0;
+        if (in) cu = users[s], cv = items[s];
+        const bool ok = in && (unsigned)cu < (unsigned)ids.ubound && (unsigned)cv < (unsigned)ids.ibound;
+        // the GMF part's operands go out now, under the dX MFMAs
+        float4 pu[GQ / 4], pi[GQ / 4], pw[GQ / 4];
+        float d = 0.f;
+        {
+            const float4* gu = reinterpret_cast<const float4*>(emb + (size_t)(ok ? cu : 0) * W + GQ * g);
+            const float4* gi = reinterpret_cast<const float4*>(emb + (size_t)(ok ? ids.ibase + cv : 0) * W + GQ * g);
+            const float4* w4 = reinterpret_cast<const float4*>(wg + GQ * g);
+#pragma unroll
+            for (int k = 0; k < GQ / 4; ++k) pu[k] = gu[k], pi[k] = gi[k], pw[k] = w4[k];
+            d = ok ? dzo[s] : 0.f;
+        }
+        float* ur = gs + (size_t)(2 * s) * W;      // user-row contribution c = 2s
+        float* ir = gs + (size_t)(2 * s + 1) * W;  // item-row contribution c = 2s + 1
+        // dX = W1 G1: block ti holds input features 16 ti + 4 lq + r of sample li; k-step (t, r)
+        // takes G1 feature 16 t + 4 lq + r (one LDS read gives the B1 steps of one r)
+        // (blocks two at a time: the whole block loop unrolled hoists every LDS read and spills)
+#pragma unroll 2
+        for (int ti = 0; ti < B0; ++ti) {
+            f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+            float a[2][B1];
+            ldsv<B1>(wl + (16 * ti + li) * S::S1 + (4 * g) * B1, a[0]);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                if (r + 1 < 4) ldsv<B1>(wl + (16 * ti + li) * S::S1 + (4 * g + r + 1) * B1, a[(r + 1) & 1]);
+#pragma unroll
+                for (int t = 0; t < B1; ++t) acc = mfma16(a[r & 1][t], U.gv[t][r], acc);
+            }
+            if (in) {
+                const int f0 = 16 * ti + 4 * g;
+                const bool user = 16 * ti < D0;
+                float* dst = (user ? ur : ir) + G + (user ? f0 : f0 - D0);
+                *reinterpret_cast<float4*>(dst) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+            }
+        }
+        if (in) {
+            // GMF part: dz w_gmf * the other side's GMF vector (zero rows for a masked sample)
+#pragma unroll
+            for (int k = 0; k < GQ / 4; ++k) {
+                const float4 p = pu[k], q = pi[k], w = pw[k];
+                const float4 zu = ok ? make_float4(d * w.x * q.x, d * w.y * q.y, d * w.z * q.z, d * w.w * q.w)
+                                     : make_float4(0.f, 0.f, 0.f, 0.f);
+                const float4 zi = ok ? make_float4(d * w.x * p.x, d * w.y * p.y, d * w.z * p.z, d * w.w * p.w)
+                                     : make_float4(0.f, 0.f, 0.f, 0.f);
+                reinterpret_cast<float4*>(ur + GQ * g)[k] = zu;
+                reinterpret_cast<float4*>(ir + GQ * g)[k] = zi;
+            }
+        }
+    };
+    const int64_t u0 = (int64_t)blockIdx.x * NW + wv;
+    Unit A, B;
+    if (u0 < nunits) load(u0, A);
+    for (int64_t u = u0; u < nunits; u += 2 * ustride) {
+        const bool hb = u + ustride < nunits;
+        if (hb) load(u + ustride, B);
+        process(u, A);
+        if (u + 2 * ustride < nunits) load(u + 2 * ustride, A);
+        if (hb) process(u + ustride, B);
+    }
+}
+
+// waves per workgroup (4 or 8), measured at config D (profiles/r03_d): the forward 87.8 us with 4
+// (two units' loads in flight per wave) vs 98.7 with 8; the backward 80.6 with 4 vs 70.4 with 8
+#ifndef NCF_L1F_WAVES
+#define NCF_L1F_WAVES 4
+#endif
+#ifndef NCF_L1B_WAVES
+#define NCF_L1B_WAVES 8
+#endif
+
+using L1ShapeD = L1Shape<256, 128, 128>;  // config D
+
+template <class S>
+bool l1matches(const ncf_shape_t& s) {
+    return s.num_layers >= 2 && s.layers[0] == S::L0 && s.layers[1] == S::L1 && s.gmf_dim == S::G &&
+           s.gmf_stride == S::G && s.du == S::D0 && s.di == S::D0 && s.row_width == S::W && s.layer_off[1] == 0;
+}
+
+template <class S, int NW>
+int grid_of(int64_t n) {
+    const int64_t wgs = ((n + 15) / 16 + NW - 1) / NW;
+    return (int)(wgs < 256 ? (wgs < 1 ? 1 : wgs) : 256);
+}
+
+template <class S>
+hipError_t configure(const void* k) {
+    return hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)S::LDS);
+}
+
+}  // namespace
+
+// NCF_LAYER1_MFMA=0 keeps the rocBLAS layer 1 (A/B)
+bool layer1_supported(const ncf_shape_t& s) {
+    static const int on = [] {
+        const char* e = getenv("NCF_LAYER1_MFMA");
+        return e && *e ? atoi(e) : 1;
+    }();
+    return on != 0 && l1matches<L1ShapeD>(s);
+}
+
+hipError_t launch_layer1_fwd(const ncf_shape_t& s, const float* emb, const float* mlp, const int32_t* users,
+                             const int32_t* items, int64_t n, IdSpace ids, float* x0, float* gmf, float* h1,
+                             hipStream_t st) {
+    using S = L1ShapeD;
+    if (!l1matches<S>(s)) return hipErrorInvalidValue;
+    static bool cfg = false;
+    if (!cfg) {
+        if (hipError_t e = configure<S>((const void*)k_lay_l1f<S, NCF_L1F_WAVES>)) return e;
+        cfg = true;
+    }
+    launch(k_lay_l1f<S, NCF_L1F_WAVES>, grid_of<S, NCF_L1F_WAVES>(n), 64 * NCF_L1F_WAVES, S::LDS, st, emb, mlp, users,
+           items, n, ids, x0, gmf, h1);
+    return hipGetLastError();
+}
+
+hipError_t launch_layer1_bwd(const ncf_shape_t& s, const float* emb, const float* mlp, const int32_t* users,
+                             const int32_t* items, int64_t n, IdSpace ids, const float* dzo, const float* g1,
+                             float* gs, hipStream_t st) {
+    using S = L1ShapeD;
+    if (!l1matches<S>(s)) return hipErrorInvalidValue;
+    static bool cfg = false;
+    if (!cfg) {
+        if (hipError_t e = configure<S>((const void*)k_lay_l1b<S, NCF_L1B_WAVES>)) return e;
+        cfg = true;
+    }
+    launch(k_lay_l1b<S, NCF_L1B_WAVES>, grid_of<S, NCF_L1B_WAVES>(n), 64 * NCF_L1B_WAVES, S::LDS, st, emb, mlp,
+           s.layer_off[0], users, items, n, ids, dzo, g1, gs);
+    return hipGetLastError();
+}
+
+}  // namespace ncf

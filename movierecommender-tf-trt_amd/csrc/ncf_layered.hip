@@ -282,13 +282,18 @@ hipError_t launch_predict_layered(const ncf_shape_t& s, const WsLayout& L, void*
     float* ones = at<float>(ws, L.ones);
     const float one = 1.0f, zero = 0.0f;
     const bool vec4 = du % 4 == 0 && di % 4 == 0 && G == G4 && W % 4 == 0;
-    if (vec4)
+    // layer 1 on hand-written MFMA with the gather fused (ncf_layer1.hip), where the shape has it
+    const bool l1 = layer1_supported(s);
+    if (l1)
+        e = launch_layer1_fwd(s, emb, mlp, users, items, n, ids, X[0], gmf, X[1], st);
+    else if (vec4)
         launch(k_lay_gather4, grid_for(n * (du + di + G) / 4), kBlock, 0, st, (const float4*)emb, users, items, n, ids,
                W / 4, G / 4, du / 4, di / 4, (float4*)X[0], (float4*)gmf);
     else
         launch(k_lay_gather, grid_for(n * (du + di + G)), kBlock, 0, st, emb, users, items, n, ids, W, G, G4, du, di,
                X[0], gmf);
-    for (int l = 1; l < nl; ++l) {
+    if (e != hipSuccess) return e;
+    for (int l = l1 ? 2 : 1; l < nl; ++l) {
         const int lin = s.layers[l - 1], lout = s.layers[l];
         const float* Wl = mlp + s.layer_off[l];
         e = blas_err(rocblas_sgemm(bh, rocblas_operation_none, rocblas_operation_none, lout, (int)n, lin, &one, Wl,
@@ -343,13 +348,19 @@ hipError_t launch_fb_layered(const ncf_shape_t& s, const WsLayout& L, void* ws, 
 
     // float4 paths when every part of the row is float4-aligned (config D); float otherwise
     const bool vec4 = du % 4 == 0 && di % 4 == 0 && G == G4 && W % 4 == 0;
-    if (vec4)
+    // layer 1 forward (with the gather) and its data gradient (with the gradient-row scatter) on
+    // hand-written MFMA (ncf_layer1.hip), where the shape has them
+    const bool l1 = layer1_supported(s);
+    if (l1)
+        e = launch_layer1_fwd(s, emb, mlp, users, items, n, ids, X[0], gmf, X[1], st);
+    else if (vec4)
         launch(k_lay_gather4, grid_for(n * (du + di + G) / 4), kBlock, 0, st, (const float4*)emb, users, items, n, ids,
                W / 4, G / 4, du / 4, di / 4, (float4*)X[0], (float4*)gmf);
     else
         launch(k_lay_gather, grid_for(n * (du + di + G)), kBlock, 0, st, emb, users, items, n, ids, W, G, G4, du, di,
                X[0], gmf);
-    for (int l = 1; l < nl; ++l) {
+    if (e != hipSuccess) return e;
+    for (int l = l1 ? 2 : 1; l < nl; ++l) {
         const int lin = s.layers[l - 1], lout = s.layers[l];
         const float* Wl = mlp + s.layer_off[l];
         // X_l^T (lout x n) = W_l^T (lout x lin) * X_{l-1}^T (lin x n), column-major views of row-major data
@@ -421,13 +432,18 @@ hipError_t launch_fb_layered(const ncf_shape_t& s, const WsLayout& L, void* ws, 
         e = gemv_parts(lout, Gd[l], ones, dWl + (int64_t)lin * lout);
         if (e != hipSuccess) return e;
         // G_{l-1}^T (lin x n) = W_l (lin x lout) * G_l^T (lout x n); layer 0: dX0 overwrites X0
+        // (hand-written layer 1: dX straight into the gradient rows, below)
+        if (l == 1 && l1) break;
         float* dst = l >= 2 ? Gd[l - 1] : X[0];
         e = blas_err(rocblas_sgemm(bh, rocblas_operation_transpose, rocblas_operation_none, lin, B, lout, &one, Wl,
                                    lout, Gd[l], lout, &zero, dst, lin));
         if (e != hipSuccess) return e;
         if (l >= 2) launch(k_relu_mask, grid_for(n * lin), kBlock, 0, st, Gd[l - 1], (const float*)X[l - 1], n * lin);
     }
-    if (vec4)
+    if (l1) {
+        e = launch_layer1_bwd(s, emb, mlp, users, items, n, ids, (const float*)dzo, (const float*)Gd[1], gs, st);
+        if (e != hipSuccess) return e;
+    } else if (vec4)
         launch(k_lay_scatter4, grid_for(n * 2 * W / 4), kBlock, 0, st, (const float4*)emb, mlp, wo_off, users, items, n,
                ids, W / 4, G / 4, du / 4, di / 4, (const float*)dzo, (const float4*)X[0], (float4*)gs);
     else

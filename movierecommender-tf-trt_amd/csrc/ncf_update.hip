@@ -233,6 +233,9 @@ constexpr int kRep = NCF_AHEAD_REP;
 #endif
 // occupancy floor of the touched-row update launch (its HBM-bound rows want many waves; the
 // catch-up-ahead blocks in the same launch must not raise its register count)
+#ifndef NCF_COUNT_BLOCKS_MAX
+#define NCF_COUNT_BLOCKS_MAX 4096  // count (+ catch-up ahead) blocks of the touched-row update launch
+#endif
 #ifndef NCF_TOUCHED_MIN_BLOCKS
 #define NCF_TOUCHED_MIN_BLOCKS 7
 #endif
@@ -1325,7 +1328,8 @@ hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, vo
         // count (+ catch-up ahead) blocks: 64 contributions per block and pass, 32 / 16 below 65,536
         // / 32,768 contributions (at least ~1,000 blocks of replay chains)
         const int per = mc >= 65536 ? NCF_COUNT_PER_MAX : mc >= 32768 ? 32 : 16;
-        const unsigned ncount = mc > 0 ? (unsigned)((mc + per - 1) / per < 4096 ? (mc + per - 1) / per : 4096) : 0u;
+        const int64_t npass = (mc + per - 1) / per;
+        const unsigned ncount = mc > 0 ? (unsigned)(npass < NCF_COUNT_BLOCKS_MAX ? npass : NCF_COUNT_BLOCKS_MAX) : 0u;
         CountAhead ca{(int)nupd, (int)ncount, next_users, next_items, mc, s.num_users, s.num_items,
                       at<int32_t>(ws, L.cnt), replay_ahead ? 1 : 0, next_fold, per, lazy_bound(s, h)};
         MlpTail mt{};
