@@ -15,7 +15,7 @@ ROOT = os.path.dirname(PKG)
 INCLUDE = os.path.join(ROOT, "include")
 OUT_DIR = os.path.join(PKG, "movierec", "_lib")
 LIB = os.path.join(OUT_DIR, "libmovierec_ncf.so")
-SOURCES = ["ncf_index.hip", "ncf_update.hip", "ncf_generic.hip", "ncf_fused.hip", "ncf_unit.hip", "ncf_wave.hip", "ncf_layered.hip", "ncf_layer1.hip", "ncf_score.hip", "ncf_sample.hip", "ncf_comm.hip", "ncf_capi.hip"]
+SOURCES = ["ncf_index.hip", "ncf_update.hip", "ncf_generic.hip", "ncf_fused.hip", "ncf_unit.hip", "ncf_wave.hip", "ncf_layered.hip", "ncf_layer1.hip", "ncf_laymid.hip", "ncf_score.hip", "ncf_sample.hip", "ncf_comm.hip", "ncf_capi.hip"]
 # per-source extra flags: the scorer keeps its MFMA accumulators in VGPRs (no v_accvgpr_read
 # before every epilogue op; its 226 registers fit the unified file at 2 waves/SIMD)
 EXTRA = {"ncf_score.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}

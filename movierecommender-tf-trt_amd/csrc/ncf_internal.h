@@ -414,6 +414,14 @@ hipError_t launch_layer1_fwd(const ncf_shape_t& s, const float* emb, const float
 hipError_t launch_layer1_bwd(const ncf_shape_t& s, const float* emb, const float* mlp, const int32_t* users,
                              const int32_t* items, int64_t n, IdSpace ids, const float* dzo, const float* g1,
                              float* gs, hipStream_t st);
+// layers 2.. of the layered path in one hand-written MFMA kernel (ncf_laymid.hip, config D's widths):
+// from H1 and the GMF product to probs, dz, G1 (row-major), the BCE partials and, per workgroup
+// (grid of them), one slab of every dense parameter after layer 1
+bool laymid_supported(const ncf_shape_t& s);
+hipError_t launch_laymid(const ncf_shape_t& s, const float* mlp, const float* h1, const float* gmf,
+                         const float* labels, const int32_t* users, const int32_t* items, int64_t n, IdSpace ids,
+                         float inv_batch, float* probs, float* dzo, float* g1, float* slabs, float* part_bce,
+                         int grid, hipStream_t st);
 // its forward half alone (predict / evaluate): probs, and with labels the BCE partials
 hipError_t launch_predict_layered(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb,
                                   const float* mlp, const int32_t* users, const int32_t* items, const float* labels,

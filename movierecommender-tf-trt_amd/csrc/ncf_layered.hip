@@ -360,6 +360,39 @@ hipError_t launch_fb_layered(const ncf_shape_t& s, const WsLayout& L, void* ws, 
         launch(k_lay_gather, grid_for(n * (du + di + G)), kBlock, 0, st, emb, users, items, n, ids, W, G, G4, du, di,
                X[0], gmf);
     if (e != hipSuccess) return e;
+    if (l1 && laymid_supported(s)) {
+        // layers 2.., output, BCE and the backward to G1 (+ db1) in one kernel (ncf_laymid.hip), one
+        // workgroup per batch chunk of the dW1 GEMM: slab c = that workgroup's parameters other than
+        // dW1 + chunk c's dW1
+        int64_t chunk = 256;
+        while ((n + chunk - 1) / chunk > 256) chunk *= 2;
+        const int nfull = (int)(n / chunk), rem = (int)(n - (int64_t)nfull * chunk);
+        const int nsl = nfull + (rem > 0 ? 1 : 0);
+        e = launch_laymid(s, mlp, X[1], gmf, labels, users, items, n, ids, inv_batch, probs, dzo, Gd[1], slab,
+                          at<float>(ws, L.part_bce), nsl, st);
+        if (e != hipSuccess) return e;
+        const int lin = s.layers[0], lout = s.layers[1];
+        const int64_t P = s.mlp_params;
+        float* dW1 = slab + s.layer_off[1];
+        if (nfull > 0) {
+            e = blas_err(rocblas_sgemm_strided_batched(
+                bh, rocblas_operation_none, rocblas_operation_transpose, lout, lin, (int)chunk, &one, Gd[1], lout,
+                (rocblas_stride)chunk * lout, X[0], lin, (rocblas_stride)chunk * lin, &zero, dW1, lout, (rocblas_stride)P,
+                nfull));
+            if (e != hipSuccess) return e;
+        }
+        if (rem > 0) {
+            e = blas_err(rocblas_sgemm(bh, rocblas_operation_none, rocblas_operation_transpose, lout, lin, rem, &one,
+                                       Gd[1] + (int64_t)nfull * chunk * lout, lout, X[0] + (int64_t)nfull * chunk * lin,
+                                       lin, &zero, dW1 + (int64_t)nfull * P, lout));
+            if (e != hipSuccess) return e;
+        }
+        e = launch_layer1_bwd(s, emb, mlp, users, items, n, ids, (const float*)dzo, (const float*)Gd[1], gs, st);
+        if (e != hipSuccess) return e;
+        *nbce = nsl;
+        *nslab = nsl;
+        return hipGetLastError();
+    }
     for (int l = l1 ? 2 : 1; l < nl; ++l) {
         const int lin = s.layers[l - 1], lout = s.layers[l];
         const float* Wl = mlp + s.layer_off[l];
