@@ -405,7 +405,7 @@ hipError_t launch_fb_layered(const ncf_shape_t& s, const WsLayout& L, void* ws, 
                              const int32_t* users, const int32_t* items, const float* labels, int64_t n,
                              float inv_batch, IdSpace ids, int* nslab, int* nbce, hipStream_t st);
 // layer 1 of the layered path on hand-written MFMA (ncf_layer1.hip, config D's widths):
-// forward = gather + X0 + GMF product + relu(W1^T x + b1); backward = dX = W1 G1 into the
+// forward = gather + X0 + (gmf != nullptr) GMF product + relu(W1^T x + b1); backward = dX = W1 G1 into the
 // gradient rows gs with their GMF part (the replaced gather / GEMM / bias / scatter kernels' outputs)
 bool layer1_supported(const ncf_shape_t& s);
 hipError_t launch_layer1_fwd(const ncf_shape_t& s, const float* emb, const float* mlp, const int32_t* users,
@@ -415,10 +415,10 @@ hipError_t launch_layer1_bwd(const ncf_shape_t& s, const float* emb, const float
                              const int32_t* items, int64_t n, IdSpace ids, const float* dzo, const float* g1,
                              float* gs, hipStream_t st);
 // layers 2.. of the layered path in one hand-written MFMA kernel (ncf_laymid.hip, config D's widths):
-// from H1 and the GMF product to probs, dz, G1 (row-major), the BCE partials and, per workgroup
+// from H1 and the rows' GMF vectors to probs, dz, G1 (row-major), the BCE partials and, per workgroup
 // (grid of them), one slab of every dense parameter after layer 1
 bool laymid_supported(const ncf_shape_t& s);
-hipError_t launch_laymid(const ncf_shape_t& s, const float* mlp, const float* h1, const float* gmf,
+hipError_t launch_laymid(const ncf_shape_t& s, const float* mlp, const float* h1, const float* emb,
                          const float* labels, const int32_t* users, const int32_t* items, int64_t n, IdSpace ids,
                          float inv_batch, float* probs, float* dzo, float* g1, float* slabs, float* part_bce,
                          int grid, hipStream_t st);

@@ -96,7 +96,9 @@ __device__ __forceinline__ void ldsv(const float* p, float (&o)[NB]) {
 
 // NW waves per workgroup (8: two per SIMD, one unit's registers each; 4: one per SIMD with two
 // units' loads in flight)
-template <class S, int NW>
+// GMF: also write the GMF product (the rocBLAS layers' output pass reads it; k_lay_mid forms it
+// from the rows itself)
+template <class S, int NW, bool GMF>
 __global__ __launch_bounds__(64 * NW, 1) void k_lay_l1f(const float* __restrict__ emb, const float* __restrict__ mlp,
                                                     const int32_t* __restrict__ users,
                                                     const int32_t* __restrict__ items, int64_t n, IdSpace ids,
@@ -137,7 +139,7 @@ __global__ __launch_bounds__(64 * NW, 1) void k_lay_l1f(const float* __restrict_
         const bool in = s < n;
         // the GMF slices (dims GQ lq .. GQ lq + GQ - 1) go out now, under the MFMAs
         float4 pu[GQ / 4], pi[GQ / 4];
-        {
+        if constexpr (GMF) {
             const float4* gu = reinterpret_cast<const float4*>(emb + (size_t)U.urow * W + GQ * g);
             const float4* gi = reinterpret_cast<const float4*>(emb + (size_t)U.irow * W + GQ * g);
 #pragma unroll
@@ -169,11 +171,13 @@ __global__ __launch_bounds__(64 * NW, 1) void k_lay_l1f(const float* __restrict_
                     make_float4(fmaxf(h[t][0] + bias[t][0], 0.f), fmaxf(h[t][1] + bias[t][1], 0.f),
                                 fmaxf(h[t][2] + bias[t][2], 0.f), fmaxf(h[t][3] + bias[t][3], 0.f));
             // GMF product of the two rows
-            float4* go = reinterpret_cast<float4*>(gmf + s * G + GQ * g);
+            if constexpr (GMF) {
+                float4* go = reinterpret_cast<float4*>(gmf + s * G + GQ * g);
 #pragma unroll
-            for (int k = 0; k < GQ / 4; ++k) {
-                const float4 p = pu[k], r = pi[k];
-                go[k] = U.ok ? make_float4(p.x * r.x, p.y * r.y, p.z * r.z, p.w * r.w) : make_float4(0.f, 0.f, 0.f, 0.f);
+                for (int k = 0; k < GQ / 4; ++k) {
+                    const float4 p = pu[k], r = pi[k];
+                    go[k] = U.ok ? make_float4(p.x * r.x, p.y * r.y, p.z * r.z, p.w * r.w) : make_float4(0.f, 0.f, 0.f, 0.f);
+                }
             }
         }
     };
@@ -334,11 +338,16 @@ hipError_t launch_layer1_fwd(const ncf_shape_t& s, const float* emb, const float
     if (!l1matches<S>(s)) return hipErrorInvalidValue;
     static bool cfg = false;
     if (!cfg) {
-        if (hipError_t e = configure<S>((const void*)k_lay_l1f<S, NCF_L1F_WAVES>)) return e;
+        if (hipError_t e = configure<S>((const void*)k_lay_l1f<S, NCF_L1F_WAVES, true>)) return e;
+        if (hipError_t e = configure<S>((const void*)k_lay_l1f<S, NCF_L1F_WAVES, false>)) return e;
         cfg = true;
     }
-    launch(k_lay_l1f<S, NCF_L1F_WAVES>, grid_of<S, NCF_L1F_WAVES>(n), 64 * NCF_L1F_WAVES, S::LDS, st, emb, mlp, users,
-           items, n, ids, x0, gmf, h1);
+    if (gmf)
+        launch(k_lay_l1f<S, NCF_L1F_WAVES, true>, grid_of<S, NCF_L1F_WAVES>(n), 64 * NCF_L1F_WAVES, S::LDS, st, emb, mlp,
+               users, items, n, ids, x0, gmf, h1);
+    else
+        launch(k_lay_l1f<S, NCF_L1F_WAVES, false>, grid_of<S, NCF_L1F_WAVES>(n), 64 * NCF_L1F_WAVES, S::LDS, st, emb,
+               mlp, users, items, n, ids, x0, gmf, h1);
     return hipGetLastError();
 }
 

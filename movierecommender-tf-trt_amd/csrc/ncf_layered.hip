@@ -351,8 +351,9 @@ hipError_t launch_fb_layered(const ncf_shape_t& s, const WsLayout& L, void* ws, 
     // layer 1 forward (with the gather) and its data gradient (with the gradient-row scatter) on
     // hand-written MFMA (ncf_layer1.hip), where the shape has them
     const bool l1 = layer1_supported(s);
+    const bool mid = l1 && laymid_supported(s);  // the middle kernel forms the GMF product itself
     if (l1)
-        e = launch_layer1_fwd(s, emb, mlp, users, items, n, ids, X[0], gmf, X[1], st);
+        e = launch_layer1_fwd(s, emb, mlp, users, items, n, ids, X[0], mid ? nullptr : gmf, X[1], st);
     else if (vec4)
         launch(k_lay_gather4, grid_for(n * (du + di + G) / 4), kBlock, 0, st, (const float4*)emb, users, items, n, ids,
                W / 4, G / 4, du / 4, di / 4, (float4*)X[0], (float4*)gmf);
@@ -360,7 +361,7 @@ hipError_t launch_fb_layered(const ncf_shape_t& s, const WsLayout& L, void* ws, 
         launch(k_lay_gather, grid_for(n * (du + di + G)), kBlock, 0, st, emb, users, items, n, ids, W, G, G4, du, di,
                X[0], gmf);
     if (e != hipSuccess) return e;
-    if (l1 && laymid_supported(s)) {
+    if (mid) {
         // layers 2.., output, BCE and the backward to G1 (+ db1) in one kernel (ncf_laymid.hip), one
         // workgroup per batch chunk of the dW1 GEMM: slab c = that workgroup's parameters other than
         // dW1 + chunk c's dW1
@@ -368,7 +369,7 @@ hipError_t launch_fb_layered(const ncf_shape_t& s, const WsLayout& L, void* ws, 
         while ((n + chunk - 1) / chunk > 256) chunk *= 2;
         const int nfull = (int)(n / chunk), rem = (int)(n - (int64_t)nfull * chunk);
         const int nsl = nfull + (rem > 0 ? 1 : 0);
-        e = launch_laymid(s, mlp, X[1], gmf, labels, users, items, n, ids, inv_batch, probs, dzo, Gd[1], slab,
+        e = launch_laymid(s, mlp, X[1], emb, labels, users, items, n, ids, inv_batch, probs, dzo, Gd[1], slab,
                           at<float>(ws, L.part_bce), nsl, st);
         if (e != hipSuccess) return e;
         const int lin = s.layers[0], lout = s.layers[1];

@@ -7,7 +7,7 @@
 // in LDS once per workgroup in the wave kernel's operand layout (ncf_wave.hip) and each wave runs
 // its own 16-sample units through the whole middle of the chain, the activations in registers:
 //
-//   in:   H1 = relu(W1^T x + b1) [n x 128] and the GMF product [n x 128] (k_lay_l1f's outputs)
+//   in:   H1 = relu(W1^T x + b1) [n x 128] (k_lay_l1f's output) and the two rows' GMF vectors
 //   fwd:  H2 = relu(W2^T H1 + b2), H3 = relu(W3^T H2 + b3) as 16 x 16 tiles [feature][sample]
 //         (a layer's output registers are the next layer's B operand), z = w_out . [GMF | H3] +
 //         b_out, Keras-clipped BCE, dz = (p - y) / B (model.py:175-188, 213-214)
@@ -108,7 +108,8 @@ struct MidArgs {
     int off2, off3, offo;  // flat offsets of the hidden_2 / hidden_3 / output kernels
     int b1off;             // flat offset of b1
     const float* h1;
-    const float* gmf;
+    const float* emb;  // the GMF vectors of the two rows (row width W)
+    int W;
     const float* labels;
     const int32_t* users;
     const int32_t* items;
@@ -232,16 +233,21 @@ __global__ __launch_bounds__(256, 1) void k_lay_mid(MidArgs a) {
                 const float4 v = *reinterpret_cast<const float4*>(hr + 16 * t);
                 h1[t][0] = v.x, h1[t][1] = v.y, h1[t][2] = v.z, h1[t][3] = v.w;
             }
-            const float4* gp = reinterpret_cast<const float4*>(a.gmf + sr * G + GQ * g);
-#pragma unroll
-            for (int k = 0; k < GQ / 4; ++k) {
-                const float4 v = gp[k];
-                gm[4 * k] = v.x, gm[4 * k + 1] = v.y, gm[4 * k + 2] = v.z, gm[4 * k + 3] = v.w;
-            }
         }
         const int cu = in ? a.users[s] : 0, cv = in ? a.items[s] : 0;
         const float y = in ? a.labels[s] : 0.f;
         const bool ok = in && (unsigned)cu < (unsigned)a.ids.ubound && (unsigned)cv < (unsigned)a.ids.ibound;
+        {
+            // the GMF product of the two rows (dims GQ lq .. GQ lq + GQ - 1; zero for a masked sample)
+            const float4* gu = reinterpret_cast<const float4*>(a.emb + (size_t)(ok ? cu : 0) * a.W + GQ * g);
+            const float4* gi = reinterpret_cast<const float4*>(a.emb + (size_t)(ok ? a.ids.ibase + cv : 0) * a.W + GQ * g);
+#pragma unroll
+            for (int k = 0; k < GQ / 4; ++k) {
+                const float4 p = gu[k], q = gi[k];
+                gm[4 * k] = ok ? p.x * q.x : 0.f, gm[4 * k + 1] = ok ? p.y * q.y : 0.f;
+                gm[4 * k + 2] = ok ? p.z * q.z : 0.f, gm[4 * k + 3] = ok ? p.w * q.w : 0.f;
+            }
+        }
         // H1^T for dW2
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -507,7 +513,7 @@ bool laymid_supported(const ncf_shape_t& s) {
            s.gmf_dim == S::G && s.gmf_stride == S::G && layer1_supported(s);
 }
 
-hipError_t launch_laymid(const ncf_shape_t& s, const float* mlp, const float* h1, const float* gmf,
+hipError_t launch_laymid(const ncf_shape_t& s, const float* mlp, const float* h1, const float* emb,
                          const float* labels, const int32_t* users, const int32_t* items, int64_t n, IdSpace ids,
                          float inv_batch, float* probs, float* dzo, float* g1, float* slabs, float* part_bce,
                          int grid, hipStream_t st) {
@@ -520,8 +526,8 @@ hipError_t launch_laymid(const ncf_shape_t& s, const float* mlp, const float* h1
             return e;
         cfg = true;
     }
-    MidArgs a{mlp, s.layer_off[2], s.layer_off[3], s.layer_off[0], s.layer_off[1] + s.layers[0] * s.layers[1], h1, gmf,
-              labels, users, items, n, ids, inv_batch, probs, dzo, g1, slabs, s.mlp_params, part_bce};
+    MidArgs a{mlp, s.layer_off[2], s.layer_off[3], s.layer_off[0], s.layer_off[1] + s.layers[0] * s.layers[1], h1, emb,
+              s.row_width, labels, users, items, n, ids, inv_batch, probs, dzo, g1, slabs, s.mlp_params, part_bce};
     launch(k_lay_mid<S>, grid, 256, S::LDS_BYTES, st, a);
     return hipGetLastError();
 }
