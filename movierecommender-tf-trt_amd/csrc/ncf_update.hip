@@ -270,6 +270,45 @@ struct RowLanes {
 // gap exceeds 64 steps often enough that the few such rows set the launch's tail
 constexpr int kLrLut = kBlock;
 
+#ifndef NCF_REPLAY_UNROLL
+#define NCF_REPLAY_UNROLL 4
+#endif
+// The zero-gradient steps (s, t] of one element pair, U steps at a time: the U steps' moment
+// chains first (two dependent operations per step), then their U step terms — independent of
+// each other, so their square roots and reciprocals overlap instead of each step waiting for the
+// previous one's — then p's U subtractions in step order.  Per step the operations and their
+// order are adam2_zero's: bitwise the one-step loop.  A row's replay is one such chain per element
+// pair, so its latency per step, not the VALU issue, set the replays' time.
+template <int U>
+__device__ __forceinline__ void replay2(f32x2& p, f32x2& m, f32x2& v, int s, int t, const float* lut, float lr,
+                                        float b1, float b2, float eps) {
+#pragma clang fp contract(off)
+    int st = s + 1;
+    for (; st <= t && t - st >= kLrLut; ++st) adam2_zero(p, m, v, adam_lr_t(lr, b1, b2, st), b1, b2, eps);
+    for (; st + U - 1 <= t; st += U) {
+        f32x2 mm[U], vv[U], r[U];
+        float lrt[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) lrt[u] = lut[t - st - u];
+        mm[0] = m * b1 + 0.0f;
+        vv[0] = v * b2 + 0.0f;
+#pragma unroll
+        for (int u = 1; u < U; ++u) {
+            mm[u] = mm[u - 1] * b1 + 0.0f;
+            vv[u] = vv[u - 1] * b2 + 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            r[u] = f32x2{__builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vv[u].x) + eps),
+                         __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vv[u].y) + eps)};
+#pragma unroll
+        for (int u = 0; u < U; ++u) p -= (mm[u] * lrt[u]) * r[u];
+        m = mm[U - 1];
+        v = vv[U - 1];
+    }
+    for (; st <= t; ++st) adam2_zero(p, m, v, lut[t - st], b1, b2, eps);
+}
+
 // replay the zero-gradient steps (s, t] of the touched rows list[0..*nlist) (ALL: every row,
 // ncf_lazy_flush)
 struct SortAhead {
@@ -405,7 +444,6 @@ __device__ __forceinline__ void catchup_body(float4* __restrict__ emb, float4* _
         for (int q = q0; q < W2; q += lanes_per_row) {  // element pair q: elements 2q, 2q + 1
             const f32x2 z2 = {0.f, 0.f};
             f32x2 p[kRep], m[kRep], v[kRep];
-            int smin = t;
 #pragma unroll
             for (int j = 0; j < kRep; ++j) {
                 const size_t e = (size_t)r[j] * W + 2 * q;
@@ -413,14 +451,21 @@ __device__ __forceinline__ void catchup_body(float4* __restrict__ emb, float4* _
                 p[j] = act ? *reinterpret_cast<const f32x2*>(embf + e) : z2;
                 m[j] = act ? *reinterpret_cast<const f32x2*>(mf + e) : z2;
                 v[j] = act ? *reinterpret_cast<const f32x2*>(vf + e) : z2;
-                smin = sr[j] < smin ? sr[j] : smin;
             }
+#if NCF_REPLAY_UNROLL > 1
+#pragma unroll
+            for (int j = 0; j < kRep; ++j) replay2<NCF_REPLAY_UNROLL>(p[j], m[j], v[j], sr[j], t, lut, lr, b1, b2, eps);
+#else
+            int smin = t;
+#pragma unroll
+            for (int j = 0; j < kRep; ++j) smin = sr[j] < smin ? sr[j] : smin;
             for (int st = smin + 1; st <= t; ++st) {
                 const float lrt = t - st < kLrLut ? lut[t - st] : adam_lr_t(lr, b1, b2, st);
 #pragma unroll
                 for (int j = 0; j < kRep; ++j)
                     if (st > sr[j]) adam2_zero(p[j], m[j], v[j], lrt, b1, b2, eps);
             }
+#endif
 #pragma unroll
             for (int j = 0; j < kRep; ++j) {
                 if (sr[j] < t) {
@@ -783,6 +828,11 @@ __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_tou
                     mm[j] = act[j] ? *reinterpret_cast<const f32x2*>(mf + e[j]) : z2;
                     vv[j] = act[j] ? *reinterpret_cast<const f32x2*>(vf + e[j]) : z2;
                 }
+#if NCF_REPLAY_UNROLL > 1
+#pragma unroll
+                for (int j = 0; j < kRepC; ++j)
+                    replay2<NCF_REPLAY_UNROLL>(p[j], mm[j], vv[j], sr[j], t, lut, lr, b1, b2, eps);
+#else
                 // the items' chains advance together (same per-element arithmetic, step by step)
                 int smin = t;
 #pragma unroll
@@ -793,6 +843,7 @@ __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_tou
                     for (int j = 0; j < kRepC; ++j)
                         if (st > sr[j]) adam2_zero(p[j], mm[j], vv[j], lrt, b1, b2, eps);
                 }
+#endif
 #pragma unroll
                 for (int j = 0; j < kRepC; ++j) {
                     if (act[j]) {
