@@ -626,19 +626,41 @@ def main():
     if not args.no_kernel_timing:
         N.profile_enable([N.K_EMB_UPDATE, N.K_FWD_BWD, N.K_INDEX, N.K_SAMPLE, N.K_CATCHUP], 2 * args.steps)
     t0 = time.perf_counter()
-    every = max(1, min(args.time_every, args.steps // 5))   # at least 5 timed steps
+    every = max(1, min(args.time_every, args.steps // 6))   # at least 6 sampled steps
+    # one launch group per sampled step (its events lengthen that step by ~9 us per group): the
+    # forward/backward and the embedding update (the two roofline kernels) alternate, the index and
+    # the catch-up (and the sampler) take every third turn
+    rota = [[N.K_FWD_BWD], [N.K_EMB_UPDATE]]
+    minor = [[N.K_INDEX], [N.K_CATCHUP]] + ([[N.K_SAMPLE]] if sampler is not None else [])
+    turns = []
+    for j in range(args.steps // every + 1):
+        turns.append(rota[j % 2] if j % 3 != 2 else minor[(j // 3) % len(minor)])
     for i in range(args.steps):
         if not args.no_kernel_timing and every > 1:
-            N.profile_pause(i % every != 0)
+            # mid-interval: the first timed step (after the pre-region flush and sync: clocks and
+            # caches cold) is not sampled
+            N.profile_pause(i % every != every // 2)
+            if i % every == every // 2:
+                N.profile_select(turns[i // every])
         step(args.warmup + i)
+    t_issue = time.perf_counter() - t0   # host time to issue the K steps (diagnostic, stderr)
     if not args.no_kernel_timing:
         N.profile_pause(True)    # the end-of-region flush is not a step's catch-up
     if hasattr(eng, "flush"):
         eng.flush()   # deferred decay settled inside the timed region: the table ends in the dense state
+    t_flush_issued = time.perf_counter() - t0
     barrier()
     if not args.no_kernel_timing:
         N.profile_pause(False)
     elapsed = time.perf_counter() - t0
+    print("host issue %.1f us for %d steps (%.1f us/step), flush issued at %.1f us, region %.1f us"
+          % (t_issue * 1e6, args.steps, t_issue * 1e6 / max(1, args.steps), t_flush_issued * 1e6, elapsed * 1e6),
+          file=sys.stderr)
+    # sampled steps per launch group (one group per sampled step when every > 1)
+    sampled = [turns[i // every] if every > 1 else None for i in range(every // 2 if every > 1 else 0, args.steps, every)]
+
+    def steps_of(k):
+        return max(1, sum(1 for t in sampled if t is None or k in t))
     ms_emb, nl = N.profile_read(N.K_EMB_UPDATE)
     ms_fb, nfb = N.profile_read(N.K_FWD_BWD)
     ms_idx, nidx = N.profile_read(N.K_INDEX)
@@ -780,8 +802,9 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "algorithmic_bytes_per_launch": nbytes, "avg_launch_ms": round(kern_ms, 5),
                 "gradient_rows_per_step": contribs, "replayed_rows_per_step": replay_rows,
-                "launches_per_step": round(nl / len(range(0, args.steps, every)), 2),
-                "timed_steps": "every %d-th step of the timed region (HIP events in the dispatch packets)" % every,
+                "launches_per_step": round(nl / steps_of(N.K_EMB_UPDATE), 2),
+                "timed_steps": "every %d-th step of the timed region, one launch group per sampled step "
+                               "(HIP events in the dispatch packets): %d launches timed" % (every, nl),
                 "traffic_source": "rocprofv3 --pmc FETCH_SIZE(x2 gfx950) + WRITE_SIZE, profiles/traffic/ "
                                   "(this config, batch and layout only; null if not measured)"}
     fb_achieved = fb_flops / (fb_ms * 1e-3) / 1e12
@@ -800,8 +823,8 @@ def main():
                "algorithmic_flops_per_launch": fb_flops, "avg_launch_ms": round(fb_ms, 5),
                "hbm_GBs": round(fb_bytes / (fb_ms * 1e-3) / 1e9, 1), "algorithmic_bytes_per_launch": fb_bytes}
     # `roofline` = the step's dominant kernel (longest average time per step)
-    fb_per_step = fb_ms * nfb / max(len(range(0, args.steps, every)), 1)
-    emb_per_step = kern_ms * nl / max(len(range(0, args.steps, every)), 1)
+    fb_per_step = fb_ms * nfb / steps_of(N.K_FWD_BWD)
+    emb_per_step = kern_ms * nl / steps_of(N.K_EMB_UPDATE)
     dominant_fb = not (emb_per_step > fb_per_step)
 
     if rank == 0:

@@ -487,6 +487,10 @@ int ncf_profile_read(int32_t kernel_id, double* total_ms, int64_t* launches);
  * timed region this way, because the events in the dispatch packets lengthen a
  * step (measured 16 us on the config-C step). */
 int ncf_profile_pause(int32_t paused);
+/* Of the enabled groups, only those in kernel_mask attach events from now on (all of them after
+ * ncf_profile_enable); slots already taken are kept.  bench.py times one group per sampled step,
+ * so a sampled step carries one pair of events instead of one per group. */
+int ncf_profile_select(int32_t kernel_mask);
 
 #ifdef __cplusplus
 }

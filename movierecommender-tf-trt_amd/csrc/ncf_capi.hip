@@ -76,6 +76,7 @@ struct ProfSlot {
 };
 struct Profiler {
     uint32_t mask = 0;  // bit k set: time launch group k
+    uint32_t select = ~0u;  // of those, the ones currently attaching events (ncf_profile_select)
     bool paused = false;
     ProfSlot slot[16];
 };
@@ -84,7 +85,7 @@ thread_local Profiler g_prof;
 // A profiled launch group's events ride on its kernels' dispatch packets (ncf::launch).
 void prof_begin(int k, hipStream_t) {
     ProfSlot& p = g_prof.slot[k & 15];
-    if (g_prof.paused || !(g_prof.mask >> k & 1u) || p.used >= p.start.size()) return;
+    if (g_prof.paused || !((g_prof.mask & g_prof.select) >> k & 1u) || p.used >= p.start.size()) return;
     ncf::LaunchEvents& ev = ncf::launch_events();
     ev.start = p.start[p.used];
     ev.stop = p.stop[p.used];
@@ -92,7 +93,7 @@ void prof_begin(int k, hipStream_t) {
 }
 void prof_end(int k, hipStream_t) {
     ProfSlot& p = g_prof.slot[k & 15];
-    if (g_prof.paused || !(g_prof.mask >> k & 1u) || p.used >= p.start.size()) return;
+    if (g_prof.paused || !((g_prof.mask & g_prof.select) >> k & 1u) || p.used >= p.start.size()) return;
     ncf::LaunchEvents& ev = ncf::launch_events();
     if (ev.launches > 0) ++p.used;
     ev = ncf::LaunchEvents{};
@@ -1226,6 +1227,7 @@ int ncf_score_topk(const ncf_shape_t* s, const ncf_model_t* model, const int32_t
 
 int ncf_profile_enable(int32_t kernel_mask, int32_t capacity) {
     g_prof.mask = kernel_mask < 0 ? 0u : (uint32_t)kernel_mask;
+    g_prof.select = ~0u;
     g_prof.paused = false;
     for (int k = 0; k < 16; ++k) {
         ProfSlot& p = g_prof.slot[k];
@@ -1245,6 +1247,11 @@ int ncf_profile_enable(int32_t kernel_mask, int32_t capacity) {
 
 int ncf_profile_pause(int32_t paused) {
     g_prof.paused = paused != 0;
+    return 0;
+}
+
+int ncf_profile_select(int32_t kernel_mask) {
+    g_prof.select = (uint32_t)kernel_mask;
     return 0;
 }
 

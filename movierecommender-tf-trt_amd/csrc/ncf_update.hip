@@ -129,13 +129,17 @@ __device__ __forceinline__ void adam1_zero(float& p, float& m, float& v, float l
 // v_pk_add_f32: IEEE per component, so bitwise adam1_zero per element), half the VALU issue of the
 // moment updates and the step term's products in the replays
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+// v's "+ 0" is dropped: v >= +0 always (never -0), so b2 * v + 0 rounds to b2 * v exactly; m keeps
+// it (b1 * m can be -0, which + 0 turns into the dense sweep's +0)
+__device__ __forceinline__ f32x2 rcp_sqrt_eps2(f32x2 v, float eps) {
+    const f32x2 q = f32x2{__builtin_amdgcn_sqrtf(v.x), __builtin_amdgcn_sqrtf(v.y)} + eps;
+    return f32x2{__builtin_amdgcn_rcpf(q.x), __builtin_amdgcn_rcpf(q.y)};
+}
 __device__ __forceinline__ void adam2_zero(f32x2& p, f32x2& m, f32x2& v, float lr_t, float b1, float b2, float eps) {
 #pragma clang fp contract(off)
     m = m * b1 + 0.0f;
-    v = v * b2 + 0.0f;
-    const f32x2 r = {__builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(v.x) + eps),
-                     __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(v.y) + eps)};
-    p -= (m * lr_t) * r;
+    v = v * b2;
+    p -= (m * lr_t) * rcp_sqrt_eps2(v, eps);
 }
 
 // adam4's moment updates with g = 0: b1*m + c1*0 and b2*v + c2*0 round like b1*m + 0, b2*v + 0
@@ -291,16 +295,14 @@ __device__ __forceinline__ void replay2(f32x2& p, f32x2& m, f32x2& v, int s, int
 #pragma unroll
         for (int u = 0; u < U; ++u) lrt[u] = lut[t - st - u];
         mm[0] = m * b1 + 0.0f;
-        vv[0] = v * b2 + 0.0f;
+        vv[0] = v * b2;
 #pragma unroll
         for (int u = 1; u < U; ++u) {
             mm[u] = mm[u - 1] * b1 + 0.0f;
-            vv[u] = vv[u - 1] * b2 + 0.0f;
+            vv[u] = vv[u - 1] * b2;
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-            r[u] = f32x2{__builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vv[u].x) + eps),
-                         __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vv[u].y) + eps)};
+        for (int u = 0; u < U; ++u) r[u] = rcp_sqrt_eps2(vv[u], eps);
 #pragma unroll
         for (int u = 0; u < U; ++u) p -= (mm[u] * lrt[u]) * r[u];
         m = mm[U - 1];

@@ -128,6 +128,7 @@ _SIGNATURES = {
     "ncf_profile_enable": (ctypes.c_int, [_i32, _i32]),
     "ncf_profile_read": (ctypes.c_int, [_i32, _P(ctypes.c_double), _P(_i64)]),
     "ncf_profile_pause": (ctypes.c_int, [_i32]),
+    "ncf_profile_select": (ctypes.c_int, [_i32]),
 }
 EXPORTED = sorted(_SIGNATURES)
 K_INDEX, K_FWD_BWD, K_EMB_UPDATE, K_MLP_UPDATE, K_METRICS, K_SCORE, K_SAMPLE, K_CATCHUP = 1, 2, 3, 4, 5, 6, 7, 8
@@ -145,6 +146,14 @@ def profile_enable(kernels, capacity):
 def profile_pause(paused):
     """Stop (True) / resume (False) attaching events to the enabled launch groups."""
     check(lib().ncf_profile_pause(1 if paused else 0))
+
+
+def profile_select(kernels):
+    """Of the enabled launch groups, attach events to these only (until the next call)."""
+    mask = 0
+    for k in kernels:
+        mask |= 1 << k
+    check(lib().ncf_profile_select(mask))
 
 
 def profile_read(kernel):
