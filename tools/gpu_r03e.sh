@@ -1,15 +1,16 @@
-# round 3: build-ahead native user step, layered forward for predict/evaluate, count-claimed
-# catch-up ahead — tests + benches
+# round 3: config E scorer counters (two PMC passes of their own: SQ instruction mix, then wait/busy states)
 export TMPDIR=/tmp
-R=$PWD
 O=gpurun_out/r03e; mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests/test_distributed.py tests/test_fit_dp_gpu.py tests/test_headline_parity_gpu.py tests/test_native_gpu.py -m gpu -v -s --timeout 300 --timeout-method thread > $O/gputest.log 2>&1 || { rc=$?; tail -3 $O/gputest.log; [ $rc -eq 1 ] || exit 1; }
-timeout -k 10 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline > $O/bench_C.json 2> $O/bench_C.err || exit 1
-for v in 65536 8192; do
-timeout -k 10 300 python bench.py --steps 30 --warmup 5 --dp user --emulate-world 8 --batch $v > $O/bench_user_emul8_b$v.json 2> $O/bench_user_emul8_b$v.err || { tail -5 $O/bench_user_emul8_b$v.err; exit 1; }
-done
-timeout -k 10 300 python bench.py --steps 30 --warmup 5 --dp user > $O/bench_user_w1.json 2> $O/bench_user_w1.err || exit 1
-timeout -k 10 300 python bench.py --config D --steps 40 --warmup 3 > $O/bench_D.json 2> $O/bench_D.err || exit 1
-cd /tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $R/$O/tl_user_65536 -o run -- python $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --dp user --emulate-world 8 > $R/$O/tl_user_65536.log 2>&1 || { tail -5 $R/$O/tl_user_65536.log; exit 1; }
+R=$GRAFT_REPO_ROOT
+p() { name=$1; shift; (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc "$@" --kernel-include-regex "k_score_topk" --output-format csv -d $R/$O/$name -o run -- python $R/bench.py --no-cpu-baseline --config E --steps 1 --warmup 1 > $R/$O/$name.log 2>&1) || { tail -5 $O/$name.log; exit 1; }
+  f=$(find $O/$name -name 'run_counter_collection.csv' | head -1); python - $f <<'PY'
+import csv, sys, collections
+acc = collections.defaultdict(float); n = collections.Counter()
+for r in csv.DictReader(open(sys.argv[1])):
+    acc[r["Counter_Name"]] += float(r["Counter_Value"]); n[r["Counter_Name"]] += 1
+for k in sorted(acc): print("%-32s %16.0f  (%d rows)" % (k, acc[k], n[k]))
+PY
+}
+p pa SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE
+p pb SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MFMA SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM SQ_WAVES GRBM_COUNT
 echo done
