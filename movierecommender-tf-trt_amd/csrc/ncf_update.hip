@@ -237,6 +237,9 @@ constexpr int kRep = NCF_AHEAD_REP;
 #endif
 // occupancy floor of the touched-row update launch (its HBM-bound rows want many waves; the
 // catch-up-ahead blocks in the same launch must not raise its register count)
+#ifndef NCF_COUNT_PER_SMALL
+#define NCF_COUNT_PER_SMALL 16  // contributions per count block and pass below 32,768 contributions
+#endif
 #ifndef NCF_COUNT_BLOCKS_MAX
 #define NCF_COUNT_BLOCKS_MAX 4096  // count (+ catch-up ahead) blocks of the touched-row update launch
 #endif
@@ -1380,7 +1383,7 @@ hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, vo
         const int64_t mc = next_users ? 2 * n_next : 0;
         // count (+ catch-up ahead) blocks: 64 contributions per block and pass, 32 / 16 below 65,536
         // / 32,768 contributions (at least ~1,000 blocks of replay chains)
-        const int per = mc >= 65536 ? NCF_COUNT_PER_MAX : mc >= 32768 ? 32 : 16;
+        const int per = mc >= 65536 ? NCF_COUNT_PER_MAX : mc >= 32768 ? 32 : NCF_COUNT_PER_SMALL;
         const int64_t npass = (mc + per - 1) / per;
         const unsigned ncount = mc > 0 ? (unsigned)(npass < NCF_COUNT_BLOCKS_MAX ? npass : NCF_COUNT_BLOCKS_MAX) : 0u;
         CountAhead ca{(int)nupd, (int)ncount, next_users, next_items, mc, s.num_users, s.num_items,
