@@ -280,6 +280,12 @@ constexpr int kLrLut = kBlock;
 #ifndef NCF_REPLAY_UNROLL
 #define NCF_REPLAY_UNROLL 4
 #endif
+#ifndef NCF_FLUSH_UNROLL
+#define NCF_FLUSH_UNROLL 1   // the flush (every row): the rows' joint one-step chains (79 VGPRs) beat replay2 (120) there
+#endif
+#ifndef NCF_FLUSH_WAVES
+#define NCF_FLUSH_WAVES 1    // launch-bound minimum waves per SIMD of k_emb_flush
+#endif
 // The zero-gradient steps (s, t] of one element pair, U steps at a time: the U steps' moment
 // chains first (two dependent operations per step), then their U step terms — independent of
 // each other, so their square roots and reciprocals overlap instead of each step waiting for the
@@ -457,20 +463,22 @@ __device__ __forceinline__ void catchup_body(float4* __restrict__ emb, float4* _
                 m[j] = act ? *reinterpret_cast<const f32x2*>(mf + e) : z2;
                 v[j] = act ? *reinterpret_cast<const f32x2*>(vf + e) : z2;
             }
-#if NCF_REPLAY_UNROLL > 1
-#pragma unroll
-            for (int j = 0; j < kRep; ++j) replay2<NCF_REPLAY_UNROLL>(p[j], m[j], v[j], sr[j], t, lut, lr, b1, b2, eps);
-#else
-            int smin = t;
-#pragma unroll
-            for (int j = 0; j < kRep; ++j) smin = sr[j] < smin ? sr[j] : smin;
-            for (int st = smin + 1; st <= t; ++st) {
-                const float lrt = t - st < kLrLut ? lut[t - st] : adam_lr_t(lr, b1, b2, st);
+            if constexpr ((ALL ? NCF_FLUSH_UNROLL : NCF_REPLAY_UNROLL) > 1) {
 #pragma unroll
                 for (int j = 0; j < kRep; ++j)
-                    if (st > sr[j]) adam2_zero(p[j], m[j], v[j], lrt, b1, b2, eps);
+                    replay2<(ALL ? NCF_FLUSH_UNROLL : NCF_REPLAY_UNROLL)>(p[j], m[j], v[j], sr[j], t, lut, lr, b1, b2, eps);
+            } else {
+                // the rows' chains advance together (same per-element arithmetic, step by step)
+                int smin = t;
+#pragma unroll
+                for (int j = 0; j < kRep; ++j) smin = sr[j] < smin ? sr[j] : smin;
+                for (int st = smin + 1; st <= t; ++st) {
+                    const float lrt = t - st < kLrLut ? lut[t - st] : adam_lr_t(lr, b1, b2, st);
+#pragma unroll
+                    for (int j = 0; j < kRep; ++j)
+                        if (st > sr[j]) adam2_zero(p[j], m[j], v[j], lrt, b1, b2, eps);
+                }
             }
-#endif
 #pragma unroll
             for (int j = 0; j < kRep; ++j) {
                 if (sr[j] < t) {
@@ -513,7 +521,7 @@ __device__ __forceinline__ void catchup_body(float4* __restrict__ emb, float4* _
 }
 
 // ncf_lazy_flush: every row
-__global__ __launch_bounds__(kBlock) void k_emb_flush(float4* __restrict__ emb, float4* __restrict__ m4,
+__global__ __launch_bounds__(kBlock, NCF_FLUSH_WAVES) void k_emb_flush(float4* __restrict__ emb, float4* __restrict__ m4,
                                                       float4* __restrict__ v4, uint32_t w4, int64_t R,
                                                       const int32_t* __restrict__ row_step,
                                                       const int32_t* __restrict__ step, float lr, float b1, float b2,
