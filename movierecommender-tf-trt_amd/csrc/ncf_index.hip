@@ -431,10 +431,11 @@ __global__ __launch_bounds__(kBlock) void k_fill_big(KeySrc ks, int64_t m, int32
 // Sort each key's contribution list ascending.  Keys of <= kSmallSeg entries: one thread,
 // odd-even network in registers.  Longer keys: queued in LDS and sorted by the whole
 // workgroup with a bitmap over the contribution ids (set bits, popcount scan, write back).
+template <int RPT>
 __global__ __launch_bounds__(kBlock) void k_sort(const int32_t* __restrict__ offs, int64_t R,
                                                  int32_t* __restrict__ list, int nwords, int32_t* __restrict__ cnt,
                                                  int32_t* __restrict__ err) {
-    sort_rows_body(offs, R, list, nwords, (int)blockIdx.x, cnt, err);
+    sort_rows_body<RPT>(offs, R, list, nwords, (int)blockIdx.x, cnt, err);
 }
 
 static int grid_for(int64_t work, int cap) {
@@ -447,9 +448,11 @@ static int grid_for(int64_t work, int cap) {
 static hipError_t set_sort_lds(int nwords) {
     static bool lds_cfg = false;
     if (!lds_cfg && (size_t)nwords * 4 > 65536) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_sort, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)((kMaxBatch * 2 / 32) * 4));
-        if (e != hipSuccess) return e;
+        for (const void* f : {(const void*)k_sort<1>, (const void*)k_sort<8>}) {
+            hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               (int)((kMaxBatch * 2 / 32) * 4));
+            if (e != hipSuccess) return e;
+        }
         lds_cfg = true;
     }
     return hipSuccess;
@@ -490,8 +493,12 @@ static hipError_t build(const WsLayout& L, void* ws, const KeySrc& ks, int64_t m
     }
     if (skip_sort) return hipGetLastError();
     if (hipError_t e = set_sort_lds(nwords)) return e;
-    launch(k_sort, (unsigned)((K + kBlock - 1) / kBlock), kBlock, (size_t)nwords * 4, st, offs, K, list, nwords, cnt,
-           at<int32_t>(ws, L.err));
+    const int rpt = sort_rpt(K);
+    const unsigned gs = (unsigned)((K + (int64_t)kBlock * rpt - 1) / ((int64_t)kBlock * rpt));
+    if (rpt == 8)
+        launch(k_sort<8>, gs, kBlock, (size_t)nwords * 4, st, offs, K, list, nwords, cnt, at<int32_t>(ws, L.err));
+    else
+        launch(k_sort<1>, gs, kBlock, (size_t)nwords * 4, st, offs, K, list, nwords, cnt, at<int32_t>(ws, L.err));
     return hipGetLastError();
 }
 

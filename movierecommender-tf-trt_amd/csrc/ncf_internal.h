@@ -182,25 +182,47 @@ constexpr int kErrFold = 8;        // an index built ahead folds user rows diffe
 // cnt/err (optional): every row's counter must be back at zero after k_fill; a residue means the
 // ids changed after they were counted ahead (ncf_train_step_ahead) — flagged, and the counter
 // cleared so that the next build starts from zero.
-template <int UNUSED = 0>
+// RPT rows per thread (8 for very large key spaces, config D's 11 M rows: int4 loads of the
+// offsets and counters, an eighth of the workgroups)
+constexpr int64_t kSortRpt8Rows = 1 << 20;
+__host__ __device__ inline int sort_rpt(int64_t R) { return R > kSortRpt8Rows ? 8 : 1; }
+template <int RPT = 1>
 __device__ inline void sort_rows_body(const int32_t* __restrict__ offs, int64_t R, int32_t* __restrict__ list,
                                       int nwords, int blk, int32_t* __restrict__ cnt = nullptr,
                                       int32_t* __restrict__ err = nullptr) {
     extern __shared__ __attribute__((aligned(16))) unsigned bm[];
-    __shared__ int hrows[kBlock];
-    __shared__ int mrows[kBlock];
+    __shared__ int hrows[kBlock * RPT];
+    __shared__ int mrows[kBlock * RPT];
     __shared__ int nh, nm;
     __shared__ int sw[4];
     if (threadIdx.x == 0) nh = nm = 0;
     __syncthreads();
-    const int64_t r = (int64_t)blk * kBlock + threadIdx.x;
-    if (cnt && r < R && cnt[r] != 0) {
+    const int64_t r0 = ((int64_t)blk * kBlock + threadIdx.x) * RPT;
+    int ov[RPT + 1], cv[RPT];
+    if (RPT > 1 && r0 + RPT < R) {
+        const int4 a = *reinterpret_cast<const int4*>(offs + r0), b = *reinterpret_cast<const int4*>(offs + r0 + 4);
+        ov[0] = a.x, ov[1] = a.y, ov[2] = a.z, ov[3] = a.w, ov[4] = b.x, ov[5] = b.y, ov[6] = b.z, ov[7] = b.w;
+        ov[RPT] = offs[r0 + RPT];
+        if (cnt) {
+            const int4 x = *reinterpret_cast<const int4*>(cnt + r0), y = *reinterpret_cast<const int4*>(cnt + r0 + 4);
+            cv[0] = x.x, cv[1] = x.y, cv[2] = x.z, cv[3] = x.w, cv[4] = y.x, cv[5] = y.y, cv[6] = y.z, cv[7] = y.w;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j <= RPT; ++j) ov[j] = r0 + j <= R ? offs[r0 + j] : 0;
+#pragma unroll
+        for (int j = 0; j < RPT; ++j) cv[j] = cnt && r0 + j < R ? cnt[r0 + j] : 0;
+    }
+#pragma unroll
+    for (int jr = 0; jr < RPT; ++jr) {
+    const int64_t r = r0 + jr;
+    if (cnt && r < R && cv[jr] != 0) {
         atomicOr(err, kErrStaleCount);
         cnt[r] = 0;
     }
     if (r < R) {
-        const int o = offs[r];
-        const int c = offs[r + 1] - o;
+        const int o = ov[jr];
+        const int c = ov[jr + 1] - o;
         if (c > 64) {
             hrows[atomicAdd(&nh, 1)] = (int)r;
         } else if (c > kSmallSeg) {
@@ -223,6 +245,7 @@ __device__ inline void sort_rows_body(const int32_t* __restrict__ offs, int64_t 
             for (int j = 0; j < kSmallSeg; ++j)
                 if (j < c) list[o + j] = v[j];
         }
+    }
     }
     __syncthreads();
     // rows of 17..64 entries (frequent when a rank's users are few — user-partitioned DP): one

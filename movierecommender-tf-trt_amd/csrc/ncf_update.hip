@@ -411,7 +411,10 @@ __device__ __forceinline__ void catchup_body(float4* __restrict__ emb, float4* _
     if (!ALL && (int)blockIdx.x >= so.ncatch) {
         // the contribution lists of this step's index, sorted while the rows replay (k_sort's work;
         // only the touched-row update after the forward pass reads them)
-        sort_rows_body(so.offs, so.keys, so.list, so.nwords, (int)blockIdx.x - so.ncatch, so.cnt, so.err);
+        if (sort_rpt(so.keys) == 8)
+            sort_rows_body<8>(so.offs, so.keys, so.list, so.nwords, (int)blockIdx.x - so.ncatch, so.cnt, so.err);
+        else
+            sort_rows_body<1>(so.offs, so.keys, so.list, so.nwords, (int)blockIdx.x - so.ncatch, so.cnt, so.err);
         return;
     }
     if (!ALL && sg.users) {
@@ -1317,7 +1320,7 @@ hipError_t launch_emb_catchup(const ncf_shape_t& s, const WsLayout& L, void* ws,
     if (sort_lists && !all_rows) {
         so = SortAhead{0, at<const int32_t>(ws, L.offs), R, at<int32_t>(ws, L.list), (int)((2 * n + 31) / 32),
                        at<int32_t>(ws, L.cnt), at<int32_t>(ws, L.err)};
-        nsort = (unsigned)((R + kBlock - 1) / kBlock);
+        nsort = (unsigned)((R + (int64_t)kBlock * sort_rpt(R) - 1) / ((int64_t)kBlock * sort_rpt(R)));
         lds = (size_t)so.nwords * 4;
         static bool lds_cfg = false;
         if (!lds_cfg && lds > 65536) {

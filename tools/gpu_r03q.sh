@@ -1,16 +1,13 @@
-# round 3: config D layer 1 on hand-written MFMA (gather + forward, dX + gradient rows) — tests and A/B
+# round 3: list sort 8 rows per thread (int4 loads) for key spaces > 1 M rows (config D)
 export TMPDIR=/tmp
 O=gpurun_out/r03q; mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests/test_native_gpu.py tests/test_config_d_gpu.py tests/test_distributed.py -m gpu -v --timeout 300 --timeout-method thread > $O/tests.log 2>&1; rc=$?
-tail -3 $O/tests.log
-[ $rc -eq 0 ] || { grep -E "FAILED|Error" $O/tests.log | head -30; exit 1; }
-b() { name=$1; shift; timeout -k 10 300 env "$@" > $O/$name.json 2> $O/$name.err || { tail -5 $O/$name.err; exit 1; }; python -c "
-import json; d=json.loads(open('$O/$name.json').read().strip().splitlines()[-1]); r=d['roofline']; print('%-16s %8.2f M/s %8.4f ms  fb %.4f ms frac %.3f eval %s' % ('$name', d['value']/1e6, d['ms_per_step'], r['avg_launch_ms'], r['frac'], d['hr_at_10']['eval_ms']))"; }
-for rep in 1 2; do
-b D_mfma.$rep python bench.py --no-cpu-baseline --config D --steps 30 --warmup 3
-b D_blas.$rep NCF_LAYER1_MFMA=0 python bench.py --no-cpu-baseline --config D --steps 30 --warmup 3
-done
-cd /tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/$O/tl_D -o run -- python $GRAFT_REPO_ROOT/bench.py --steps 6 --warmup 2 --no-cpu-baseline --config D > $GRAFT_REPO_ROOT/$O/tl_D.log 2>&1 || exit 1
-cd $GRAFT_REPO_ROOT && python tools/step_window.py $O/tl_D/run_kernel_trace.csv 3 k_lay_l1f | cut -c1-110
-echo done
+R=$GRAFT_REPO_ROOT
+timeout -k 10 700 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests -m gpu > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+b() { name=$1; shift; timeout -k 10 300 python bench.py --no-cpu-baseline "$@" > $O/$name.json 2> $O/$name.err || { tail -5 $O/$name.err; exit 1; }; python -c "
+import json; d=json.loads(open('$O/$name.json').read().strip().splitlines()[-1]); print('%-10s %8.2f M/s %8.4f ms idx %s cu %s' % ('$name', d['value']/1e6, d['ms_per_step'], d.get('index_build_ms'), d.get('catchup_ms')))"; }
+b D --config D --steps 50 --warmup 3
+b C --steps 50
+(cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $R/$O/tr -o run -- python $R/bench.py --no-cpu-baseline --config D --steps 10 --warmup 2 > $R/$O/tr.log 2>&1) || { tail -5 $O/tr.log; exit 1; }
+f=$(find $O/tr -name 'run_kernel_trace.csv' | head -1)
+python tools/step_window.py $f 6 k_lay_l1f > $O/tl_D.txt && rm -rf $O/tr && cat $O/tl_D.txt
