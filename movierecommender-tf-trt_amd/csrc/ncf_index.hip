@@ -420,7 +420,14 @@ __global__ __launch_bounds__(kBlock) void k_fill_big(KeySrc ks, int64_t m, int32
         const uint64_t later = heads & ~upto;
         const int next = later ? __ffsll((unsigned long long)later) - 1 : 64 + (lane & 1);
         int top = 0;
-        if (ok && lane == head) top = atomicSub(&cnt[key], (next - head) >> 1);
+        if (ok && lane == head) {
+            top = atomicSub(&cnt[key], (next - head) >> 1);
+            // what the run takes below zero (a key counted fewer times than it occurs) goes back:
+            // a counter ends at max(0, counted - placed), so a residue can only sit at a counted
+            // key (the list sort checks those only, sort_rows_body<..., LISTED>)
+            const int over = ((next - head) >> 1) - max(top, 0);
+            if (over > 0) atomicAdd(&cnt[key], over);
+        }
         top = __shfl(top, head, 64);
         const int slot = top - 1 - ((lane - head) >> 1);
         if (ok && slot >= 0) list[local[key] + pre[key / kScanBlock] + slot] = (int)c;

@@ -186,20 +186,37 @@ constexpr int kErrFold = 8;        // an index built ahead folds user rows diffe
 // offsets and counters, an eighth of the workgroups)
 constexpr int64_t kSortRpt8Rows = 1 << 20;
 __host__ __device__ inline int sort_rpt(int64_t R) { return R > kSortRpt8Rows ? 8 : 1; }
-template <int RPT = 1>
+// LISTED: the rows of the touched list (counted keys; (offset, count) from the list) instead of
+// every row: large key spaces, where k_fill_big adds back what it takes below zero, so a residue
+// can only sit at a counted key
+template <int RPT = 1, bool LISTED = false>
 __device__ inline void sort_rows_body(const int32_t* __restrict__ offs, int64_t R, int32_t* __restrict__ list,
                                       int nwords, int blk, int32_t* __restrict__ cnt = nullptr,
-                                      int32_t* __restrict__ err = nullptr) {
+                                      int32_t* __restrict__ err = nullptr, const int32_t* __restrict__ touched = nullptr,
+                                      const int2* __restrict__ toc = nullptr, const int32_t* __restrict__ nuniq = nullptr) {
     extern __shared__ __attribute__((aligned(16))) unsigned bm[];
-    __shared__ int hrows[kBlock * RPT];
-    __shared__ int mrows[kBlock * RPT];
+    __shared__ int2 hrows[kBlock * RPT];  // (offset, count) of the longer lists
+    __shared__ int2 mrows[kBlock * RPT];
     __shared__ int nh, nm;
     __shared__ int sw[4];
     if (threadIdx.x == 0) nh = nm = 0;
     __syncthreads();
     const int64_t r0 = ((int64_t)blk * kBlock + threadIdx.x) * RPT;
     int ov[RPT + 1], cv[RPT];
-    if (RPT > 1 && r0 + RPT < R) {
+    int64_t rl = -1;  // LISTED: this thread's row
+    if constexpr (LISTED) {
+        static_assert(RPT == 1, "listed rows: one per thread");
+        const int64_t i = (int64_t)blk * kBlock + threadIdx.x;
+        if (i < *nuniq) {
+            rl = touched[i];
+            const int2 oc = toc[i];
+            ov[0] = oc.x;
+            ov[1] = oc.x + oc.y;
+            cv[0] = cnt ? cnt[rl] : 0;
+        } else {
+            ov[0] = ov[1] = cv[0] = 0;
+        }
+    } else if (RPT > 1 && r0 + RPT < R) {
         const int4 a = *reinterpret_cast<const int4*>(offs + r0), b = *reinterpret_cast<const int4*>(offs + r0 + 4);
         ov[0] = a.x, ov[1] = a.y, ov[2] = a.z, ov[3] = a.w, ov[4] = b.x, ov[5] = b.y, ov[6] = b.z, ov[7] = b.w;
         ov[RPT] = offs[r0 + RPT];
@@ -215,18 +232,18 @@ __device__ inline void sort_rows_body(const int32_t* __restrict__ offs, int64_t 
     }
 #pragma unroll
     for (int jr = 0; jr < RPT; ++jr) {
-    const int64_t r = r0 + jr;
-    if (cnt && r < R && cv[jr] != 0) {
+    const int64_t r = LISTED ? rl : r0 + jr;
+    if (cnt && r >= 0 && r < R && cv[jr] != 0) {
         atomicOr(err, kErrStaleCount);
         cnt[r] = 0;
     }
-    if (r < R) {
+    if (r >= 0 && r < R) {
         const int o = ov[jr];
         const int c = ov[jr + 1] - o;
         if (c > 64) {
-            hrows[atomicAdd(&nh, 1)] = (int)r;
+            hrows[atomicAdd(&nh, 1)] = make_int2(o, c);
         } else if (c > kSmallSeg) {
-            mrows[atomicAdd(&nm, 1)] = (int)r;
+            mrows[atomicAdd(&nm, 1)] = make_int2(o, c);
         } else if (c >= 2) {
             int v[kSmallSeg];
 #pragma unroll
@@ -253,9 +270,8 @@ __device__ inline void sort_rows_body(const int32_t* __restrict__ offs, int64_t 
     {
         const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
         for (int hh = wv; hh < nm; hh += kBlock / 64) {
-            const int row = mrows[hh];
-            const int o = offs[row];
-            const int c = offs[row + 1] - o;
+            const int o = mrows[hh].x;
+            const int c = mrows[hh].y;
             int x = lane < c ? list[o + lane] : INT_MAX;
 #pragma unroll
             for (int k = 2; k <= 64; k <<= 1) {
@@ -273,9 +289,8 @@ __device__ inline void sort_rows_body(const int32_t* __restrict__ offs, int64_t 
     const int count = nh;
     const int per = (nwords + kBlock - 1) / kBlock;
     for (int hh = 0; hh < count; ++hh) {
-        const int row = hrows[hh];
-        const int o = offs[row];
-        const int c = offs[row + 1] - o;
+        const int o = hrows[hh].x;
+        const int c = hrows[hh].y;
         for (int w = threadIdx.x; w < nwords; w += kBlock) bm[w] = 0u;
         __syncthreads();
         for (int j = threadIdx.x; j < c; j += kBlock) {

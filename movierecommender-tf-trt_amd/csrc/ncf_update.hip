@@ -330,6 +330,9 @@ struct SortAhead {
     int nwords;
     int32_t* cnt;              // residue check of the counters (sort_rows_body)
     int32_t* err;
+    const int32_t* touched;    // large key spaces: sort the touched list's rows only
+    const int2* toc;
+    const int32_t* nuniq;
 };
 
 // A batch whose rows the previous step caught up ahead (counted ahead, index_ready == 2) needs no
@@ -411,7 +414,10 @@ __device__ __forceinline__ void catchup_body(float4* __restrict__ emb, float4* _
     if (!ALL && (int)blockIdx.x >= so.ncatch) {
         // the contribution lists of this step's index, sorted while the rows replay (k_sort's work;
         // only the touched-row update after the forward pass reads them)
-        if (sort_rpt(so.keys) == 8)
+        if (so.touched)
+            sort_rows_body<1, true>(so.offs, so.keys, so.list, so.nwords, (int)blockIdx.x - so.ncatch, so.cnt,
+                                    so.err, so.touched, so.toc, so.nuniq);
+        else if (sort_rpt(so.keys) == 8)
             sort_rows_body<8>(so.offs, so.keys, so.list, so.nwords, (int)blockIdx.x - so.ncatch, so.cnt, so.err);
         else
             sort_rows_body<1>(so.offs, so.keys, so.list, so.nwords, (int)blockIdx.x - so.ncatch, so.cnt, so.err);
@@ -529,7 +535,7 @@ __global__ __launch_bounds__(kBlock, NCF_FLUSH_WAVES) void k_emb_flush(float4* _
                                                       const int32_t* __restrict__ row_step,
                                                       const int32_t* __restrict__ step, float lr, float b1, float b2,
                                                       float eps) {
-    const SortAhead so{0, nullptr, 0, nullptr, 0, nullptr, nullptr};
+    const SortAhead so{0, nullptr, 0, nullptr, 0, nullptr, nullptr, nullptr, nullptr, nullptr};
     const StaleGate sg{nullptr, nullptr, 0, 0, 0, nullptr, 0};
     catchup_body<true>(emb, m4, v4, w4, nullptr, nullptr, R, row_step, step, lr, b1, b2, eps, so, sg);
 }
@@ -1312,15 +1318,24 @@ hipError_t launch_emb_catchup(const ncf_shape_t& s, const WsLayout& L, void* ws,
     const uint32_t w4 = (uint32_t)(s.row_width / 4);
     const int64_t R = s.num_rows;
     const int64_t nmax = R < 2 * L.max_batch ? R : 2 * L.max_batch;
-    SortAhead so{0, nullptr, 0, nullptr, 0, nullptr, at<int32_t>(ws, L.err)};
+    SortAhead so{0, nullptr, 0, nullptr, 0, nullptr, at<int32_t>(ws, L.err), nullptr, nullptr, nullptr};
     const StaleGate nogate{nullptr, nullptr, 0, 0, 0, nullptr, 0};
     const int64_t bound = lazy_bound(s, h);  // rows under deferred decay
     unsigned nsort = 0;
     size_t lds = 0;
     if (sort_lists && !all_rows) {
         so = SortAhead{0, at<const int32_t>(ws, L.offs), R, at<int32_t>(ws, L.list), (int)((2 * n + 31) / 32),
-                       at<int32_t>(ws, L.cnt), at<int32_t>(ws, L.err)};
-        nsort = (unsigned)((R + (int64_t)kBlock * sort_rpt(R) - 1) / ((int64_t)kBlock * sort_rpt(R)));
+                       at<int32_t>(ws, L.cnt), at<int32_t>(ws, L.err), nullptr, nullptr, nullptr};
+        if (sort_rpt(R) == 8) {
+            // large key spaces (k_fill_big): only the touched list's rows (at most 2n)
+            so.touched = at<const int32_t>(ws, L.touched);
+            so.toc = at<const int2>(ws, L.touched_oc);
+            so.nuniq = at<const int32_t>(ws, L.nuniq);
+            const int64_t nt = R < 2 * n ? R : 2 * n;
+            nsort = (unsigned)((nt + kBlock - 1) / kBlock);
+        } else {
+            nsort = (unsigned)((R + kBlock - 1) / kBlock);
+        }
         lds = (size_t)so.nwords * 4;
         static bool lds_cfg = false;
         if (!lds_cfg && lds > 65536) {
