@@ -1,0 +1,11 @@
+# round 3 close: every GPU test, smoke and the driver's bench command on the committed library
+export TMPDIR=/tmp
+O=gpurun_out/r03_close; mkdir -p $O
+timeout -k 10 700 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests -m gpu > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { cat $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
+timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || { tail -5 $O/bench.err; exit 1; }
+python -c "import json; d=json.loads(open('$O/bench.json').read().strip().splitlines()[-1]); print(d['value']/1e6, d['ms_per_step'], d['roofline']['frac'], d['cpu_baseline']['value'])"
+timeout -k 10 300 python bench.py --no-cpu-baseline --config D --steps 50 --warmup 3 > $O/bench_D.json 2> $O/bench_D.err || { tail -5 $O/bench_D.err; exit 1; }
+python -c "import json; d=json.loads(open('$O/bench_D.json').read().strip().splitlines()[-1]); print('D', d['value']/1e6, d['ms_per_step'])"
