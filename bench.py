@@ -121,6 +121,9 @@ def parse():
                     help="diagnostic: no HIP events on the profiled launches (the roofline fields are then null)")
     ap.add_argument("--dp", default="auto", choices=["auto", "user", "sharded", "replicated"],
                     help="multi-GPU layout (auto: single engine at N=1, user-partitioned at N>1)")
+    ap.add_argument("--item-optimizer", default="split", choices=["split", "replicated"],
+                    help="--dp user: the item rows' Adam split across the ranks (reduce-scatter + all-gather, "
+                         "ncf_user_dp_step_split) or replicated on every rank (one all-reduce, ncf_user_dp_step)")
     return ap.parse_args()
 
 
@@ -400,6 +403,35 @@ def device_glorot_init(eng, w_small, seed):
     torch.cuda.synchronize()
 
 
+def device_glorot_init_shard(eng, w_small, seed):
+    """device_glorot_init for one rank's shard of a row-sharded table (local row l = global row
+    l * world + rank): each row drawn with its table's (user / item) Keras glorot limits."""
+    from movierec.layout import Layout
+    lay = Layout(1, 1, eng.layers, eng.gmf_dim)
+    eng.mlp.copy_(torch.from_numpy(lay.to_device(w_small)[1]))
+    g = torch.Generator(device="cuda").manual_seed(seed + eng.rank)
+    U, I, G, G4 = eng.num_users, eng.num_items, eng.gmf_dim, eng.shape.gmf_stride
+    du, di = eng.shape.du, eng.shape.di
+    eng.emb.zero_()
+    chunk = 1 << 20
+    for r0 in range(0, eng.shard_rows, chunk):
+        r1 = min(eng.shard_rows, r0 + chunk)
+        gl = torch.arange(r0, r1, device="cuda", dtype=torch.int64) * eng.world + eng.rank
+        user = (gl < U).unsqueeze(1)
+        valid = (gl < U + I).unsqueeze(1)
+        for wu, wi, c0 in ((G, G, 0), (du, di, G4)):
+            width = max(wu, wi)
+            if not width:
+                continue
+            r = torch.rand(r1 - r0, width, generator=g, device="cuda") * 2 - 1
+            lim_u = (6.0 / (U + wu)) ** 0.5 if wu else 0.0
+            lim_i = (6.0 / (I + wi)) ** 0.5 if wi else 0.0
+            cols = torch.arange(width, device="cuda").unsqueeze(0)
+            lim = torch.where(user, torch.where(cols < wu, lim_u, 0.0), torch.where(cols < wi, lim_i, 0.0))
+            eng.emb[r0:r1, c0:c0 + width].copy_(r * lim * valid)
+    torch.cuda.synchronize()
+
+
 def pmc_traffic(kernel, config, batch, mode):
     """HBM bytes per launch of ``kernel`` measured by tools/gpu_profile.sh (separate FETCH_SIZE /
     WRITE_SIZE rocprofv3 passes) for exactly this config, per-GPU batch and layout; None when no
@@ -538,28 +570,36 @@ def main():
         raise SystemExit("bf16 MLP operands run on the single-table and user-partitioned layouts")
     assert B % g == 0, "batch must be divisible by negs+1"
     big = args.config == "D"   # 11 GB table: initialised on the device, not through host numpy
-    if big and mode != "single":
-        raise SystemExit("config D is benchmarked on one GPU (its row-sharded DP path is covered by tests)")
+    if big and mode not in ("single", "sharded"):
+        raise SystemExit("config D runs on one table or row-sharded (--dp sharded), as BASELINE names it")
+    ew = max(world, args.emulate_world)
+    if ew > world and (world > 1 or mode not in ("user", "sharded")):
+        raise SystemExit("--emulate-world: one process, --dp user or --dp sharded")
     w0 = initial_weights(1 if big else cfg["num_users"], 1 if big else cfg["num_items"], cfg["layers"],
                          cfg["gmf_dim"], seed=0)
     dp = None
     if mode == "sharded":
         from movierec.sharded import ShardedNCFEngine
         from movierec.distributed import RowShardedDataParallel
-        eng = ShardedNCFEngine(cfg["num_users"], cfg["num_items"], cfg["layers"], cfg["gmf_dim"], world=world,
-                               rank=rank, max_batch=B, force_generic=args.generic)
-        eng.set_keras_weights(w0)
-        dp = RowShardedDataParallel(eng)
+        # the shard's rows under deferred exact decay (its own rows, served when requested)
+        eng = ShardedNCFEngine(cfg["num_users"], cfg["num_items"], cfg["layers"], cfg["gmf_dim"], world=ew,
+                               rank=rank, max_batch=B, force_generic=args.generic, lazy_adam=not args.dense_sweep)
+        if big:
+            device_glorot_init_shard(eng, w0, seed=0)
+        else:
+            eng.set_keras_weights(w0)
+        dp = RowShardedDataParallel(eng, emulate=ew > world)
+        dp.broadcast_parameters()
     elif mode == "user":
         from movierec.distributed import UserPartitionedDataParallel, partition_keras_weights
-        ew = max(world, args.emulate_world)
         n_loc = (cfg["num_users"] - rank + ew - 1) // ew
         # the own users under deferred exact decay (the replicated item rows are swept every step)
         eng = NCFEngine(n_loc, cfg["num_items"], cfg["layers"], cfg["gmf_dim"], max_batch=B,
                         force_generic=args.generic, precision=prec, lazy_adam=not args.dense_sweep,
                         lazy_rows=n_loc)
         eng.set_keras_weights(partition_keras_weights(w0, ew, rank))
-        dp = UserPartitionedDataParallel(eng)
+        dp = UserPartitionedDataParallel(eng, split_items=args.item_optimizer == "split",
+                                         emulate_world=ew if ew > world else None)
         dp.broadcast_parameters()
     else:
         eng = NCFEngine(cfg["num_users"], cfg["num_items"], cfg["layers"], cfg["gmf_dim"], max_batch=B,
@@ -583,8 +623,20 @@ def main():
             raise SystemExit("--e2e supports the single-table and user-partitioned layouts")
     pool = []
     npool = args.pool if args.pool else max(8, min(1024, args.warmup + args.steps + 1))
+    own = mode == "sharded" and ew > world   # emulated rank: every row of its batches is its own
     for _ in range(npool):
         # user-partitioned data: this rank's users only, as local ids (u // world)
+        if own:
+            U, I = cfg["num_users"], cfg["num_items"]
+            u = torch.randint(0, (U - rank + ew - 1) // ew, (B // g,), generator=gen, device="cuda",
+                              dtype=torch.int32) * ew + rank
+            i0 = (rank - U) % ew   # the first item whose table row U + i0 is this rank's
+            it = torch.randint(0, (I - i0 + ew - 1) // ew, (B,), generator=gen, device="cuda",
+                               dtype=torch.int32) * ew + i0
+            u = u.repeat_interleave(g)
+            pool.append((u.contiguous(), it.contiguous(),
+                         torch.tensor([0.0] * (g - 1) + [1.0], device="cuda").repeat(B // g).contiguous()))
+            continue
         u = torch.randint(0, eng.num_users if mode == "user" else cfg["num_users"], (B // g,), generator=gen,
                           device="cuda", dtype=torch.int32)
         u = u.repeat_interleave(g)
@@ -604,7 +656,7 @@ def main():
             eng.train_step(u, it, y, group=g, k=k, inv_batch=inv, next_batch=(nu, ni))
         elif dp is None:
             eng.train_step(u, it, y, group=g, k=k, inv_batch=inv)
-        elif mode == "user" and sampler is None:
+        elif mode in ("user", "sharded") and sampler is None:
             nu, ni, _ = pool[(i + 1) % len(pool)]
             dp.train_step(u, it, y, group=g, k=k, next_batch=(nu, ni))
         else:
@@ -679,7 +731,12 @@ def main():
     replay_rows = 0.0
     fb_bytes = fwd_bwd_bytes(eng.shape, B, contribs)
     train_exchange = dp.last_exchange if mode == "sharded" else None
-    if mode == "sharded":
+    if mode == "sharded" and getattr(eng, "lazy", False):
+        # deferred decay: the m served rows (unique per source) read and written (p, m, v), their
+        # m received gradient rows, the owner index entries (list + (offset, count))
+        m_srv, W = train_exchange[1], eng.shape.row_width
+        nbytes = 24 * m_srv * W + m_srv * W * 4 + m_srv * 12
+    elif mode == "sharded":
         nbytes = emb_update_bytes(eng.shape, B, sparse_rows=(eng.shard_rows, train_exchange[1]))
     elif getattr(eng, "lazy", False) and mode == "single":
         touched = float(np.mean([torch.unique(u).numel() + torch.unique(it).numel() for u, it, _ in pool[:16]]))
@@ -712,7 +769,8 @@ def main():
             own += 24 * replay_rows * W
         else:
             own = 24 * Uloc * W + cu * W * 4 + cu * 4 + (Uloc + 1) * 4
-        nbytes = (own + 28 * (eng.num_rows - Uloc) * W) / 2.0
+        item_rows = (eng.num_rows - Uloc) if not dp.split else max(0, min(dp.Ic, eng.num_rows - Uloc))
+        nbytes = (own + 28 * item_rows * W) / 2.0
     else:
         nbytes = emb_update_bytes(eng.shape, B, dense_rows=(dp.row_count if mode == "replicated" else None),
                                   contribs=contribs)
@@ -726,6 +784,11 @@ def main():
     eval_ms = None
     ev_u = torch.randperm(ev_table, generator=gen, device="cuda")[:ev_users].to(torch.int32).repeat_interleave(100)
     ev_i = torch.randint(0, cfg["num_items"], (ev_users * 100,), generator=gen, device="cuda", dtype=torch.int32)
+    if own:   # the emulated rank evaluates on rows it owns
+        U, I = cfg["num_users"], cfg["num_items"]
+        i0 = (rank - U) % ew
+        ev_u = ((ev_u.long() % ((U - rank + ew - 1) // ew)) * ew + rank).to(torch.int32)
+        ev_i = ((ev_i.long() % ((I - i0 + ew - 1) // ew)) * ew + i0).to(torch.int32)
     ev_y = torch.tensor([0.0] * 99 + [1.0], device="cuda").repeat(ev_users)
     if mode == "sharded":
         probs = dp.predict(ev_u, ev_i)
@@ -746,16 +809,21 @@ def main():
         dist.all_reduce(hd)
     hr = {"hr": float(hd[0]) / (ev_users * world), "dcg": float(hd[1]) / (ev_users * world)}
 
-    emb_kernel = "k_emb_adam_touched" if getattr(eng, "lazy", False) and mode == "single" else "k_emb_update"
+    emb_kernel = "k_emb_adam_touched" if getattr(eng, "lazy", False) and mode in ("single", "sharded") else "k_emb_update"
     traffic = pmc_traffic(emb_kernel, args.config, B, mode)
     kpath = eng.kernel_for(B) if hasattr(eng, "kernel_for") else ("fused-mfma-tile" if eng.fast_path else "generic")
     fb_kernel = {"fused-mfma-tile": "k_fb_fused", "fused-mfma-unit": "k_fb_unit",
                  "fused-mfma-wave": "k_fb_wave"}.get(kpath)
     fb_traffic = pmc_traffic(fb_kernel, args.config, B, mode) if fb_kernel else None
     par = {"single": "dp1 (one table)",
-           "user": "dp%d user-partitioned data (rank r trains users u %% %d == r and alone holds their rows + "
-                   "Adam state); item table replicated; ONE all-reduce per step of [item-row grad | dense-layer "
-                   "grad | summary]" % (world, world),
+           "user": ("dp%d user-partitioned data (rank r trains users u %% %d == r and alone holds their rows + "
+                    "Adam state); item table replicated, its Adam split across the ranks (reduce-scatter of the "
+                    "item-row grad + all-reduce of the dense-layer grad in one RCCL group, Adam on 1/%d of the "
+                    "item rows, all-gather of the updated rows)" % (world, world, max(world, ew))
+                    if args.item_optimizer == "split" else
+                    "dp%d user-partitioned data (rank r trains users u %% %d == r and alone holds their rows + "
+                    "Adam state); item table replicated; ONE all-reduce per step of [item-row grad | dense-layer "
+                    "grad | summary]" % (world, world)),
            "sharded": "dp%d row-sharded tables (rank r owns rows g %% %d == r + their Adam state; all_to_all of "
                       "unique row ids / rows / row grads, all-reduce of the dense-layer grad)" % (world, world),
            "replicated": "dp%d replicated tables (reduce-scatter of the dense embedding grad, sharded Adam, "
@@ -778,8 +846,14 @@ def main():
                     "allreduce_ms_standalone": round(ar_ms, 4), "collectives_per_step": 1,
                     "local_users": eng.num_users}
     elif mode == "sharded":
+        W = eng.shape.row_width
         exchange = {"unique_rows_per_rank": train_exchange[0], "rows_served_per_rank": train_exchange[1],
-                    "shard_rows": eng.shard_rows}
+                    "shard_rows": eng.shard_rows,
+                    "all_to_all_bytes_per_step": {"row_ids": 4 * train_exchange[0],
+                                                  "row_values": 4 * W * train_exchange[0],
+                                                  "row_grads": 4 * W * train_exchange[0]},
+                    "allreduce_bytes_per_step": eng.dense_buf.numel() * 4,
+                    "counts": "planned a step ahead (pinned host copy, no per-step device sync)"}
     if exchange is not None:
         exchange.update(ranks=world, backend=dist.get_backend(),
                         transport="RCCL over xGMI" if dist.get_backend() == "nccl" else dist.get_backend())
@@ -797,6 +871,9 @@ def main():
                                            "embedding Adam, 2 launches per step (k_emb_update: own-user "
                                            "rows with their scatter-add; item rows with the all-reduced "
                                            "gradient)" if mode == "user" else
+                                           "row-sharded owner update: scatter-add of the received row gradients + Adam "
+                                           "on the served rows (k_emb_adam_touched; deferred exact decay)"
+                                           if mode == "sharded" and getattr(eng, "lazy", False) else
                                            "embedding scatter-add + Adam sweep (k_emb_update)"),
                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -867,7 +944,14 @@ def main():
         }
         if exchange is not None:
             line["exchange"] = exchange
-        if args.emulate_world > 1:
+        if args.emulate_world > 1 and mode == "sharded":
+            line["emulated_world"] = args.emulate_world
+            line["note"] = ("diagnostic: rank 0's per-rank compute of the %d-rank row-sharded step on one GPU (a "
+                            "1/%d shard of the table; batches drawn from its own rows so that its plan, serve, "
+                            "forward/backward and update see the work one rank of %d does; the all_to_all / "
+                            "all-reduce exchanges replaced by its own buffers); not a scaling result"
+                            % (args.emulate_world, args.emulate_world, args.emulate_world))
+        elif args.emulate_world > 1:
             line["emulated_world"] = args.emulate_world
             line["note"] = ("diagnostic: rank 0's per-rank compute of the %d-rank user-partitioned step on one GPU "
                             "(local table of 1/%d of the users, a one-rank communicator); not a scaling result"

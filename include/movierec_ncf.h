@@ -110,9 +110,16 @@ typedef struct ncf_optim {
      * their missed zero-gradient steps are replayed (same arithmetic, so the result is bitwise
      * the dense sweep's) before the forward pass, then the step is applied to them.  Needs
      * layers_l2reg[0] == 0.  Every other entry point reads the table as stored: call
-     * ncf_lazy_flush first. */
+     * ncf_lazy_flush first.
+     * row_step[r] == NCF_ROW_PRISTINE: row r's Adam moments are exactly +0 (a fresh table, or
+     * rows set_optimizer_state found at zero).  Such a row is a fixed point of the zero-gradient
+     * step (m = b1*0 + 0 = +0, v = +0, p -= (lr_t*0)/(sqrt(0)+eps) = p), so it is current at every
+     * step: no replay, no flush traffic, and its first update reads p only.  Initialise row_step
+     * to NCF_ROW_PRISTINE when the moments start at zero. */
     int32_t* row_step;
 } ncf_optim_t;
+
+#define NCF_ROW_PRISTINE 0x7fffffff
 
 typedef struct ncf_hyper {
     int32_t optimizer;                  /* NCF_OPT_ADAM / NCF_OPT_SGD (model.py:199-204) */
@@ -248,7 +255,8 @@ int ncf_evaluate(const ncf_shape_t* shape, const ncf_model_t* model, const ncf_h
                  double* stats, float* probs_out, void* ws, size_t ws_bytes, void* stream);
 
 /* Deferred exact decay: bring every row up to optim->step (replay its missed zero-gradient
- * Adam steps) and set row_step[r] = step.  After it the table equals the dense-sweep state. */
+ * Adam steps) and set row_step[r] = step (pristine rows stay NCF_ROW_PRISTINE: their state is
+ * already the dense sweep's).  After it the table equals the dense-sweep state. */
 int ncf_lazy_flush(const ncf_shape_t* shape, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* hyper,
                    void* ws, size_t ws_bytes, void* stream);
 
@@ -363,6 +371,23 @@ int ncf_user_dp_step(const ncf_shape_t* shape, ncf_model_t* model, ncf_optim_t* 
                      const int32_t* users, const int32_t* items, const float* labels, int64_t n,
                      const int32_t* next_users, const int32_t* next_items, int64_t n_next, float* shared,
                      int32_t include_dense_reg, void* comm, double* stats, void* ws, size_t ws_bytes, void* stream);
+/* ncf_user_dp_step with the item rows' Adam split across the ranks (item_world = the
+ * communicator's ranks, item_rank = this rank; Ic = ceil(items / item_world)): shared = [item-row
+ * gradient, item_world * Ic rows (rows past the items zero) | dense-layer gradient | summary];
+ * model->emb holds lazy_rows + item_world * Ic rows (zero padding past num_rows).  On the side
+ * stream one RCCL group reduce-scatters the item-row gradient (this rank's Ic rows into
+ * slice_grad, Ic x row_width floats) and all-reduces [dense-layer gradient | summary] while the
+ * compute stream runs the own-user update and the next index; then Adam on this rank's item
+ * rows [lazy_rows + item_rank * Ic, + Ic) and the dense layers, stats, step++; then an in-place
+ * all-gather of the item rows before the call returns control of the stream.  Same bytes on the
+ * links as the all-reduce; the item Adam per rank is 1/item_world of the table.  A one-rank
+ * communicator with item_world > 1 runs rank item_rank's compute of that step without the
+ * exchange (slice_grad unused).  item_world == 1: bitwise ncf_user_dp_step. */
+int ncf_user_dp_step_split(const ncf_shape_t* shape, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* hyper,
+                           const int32_t* users, const int32_t* items, const float* labels, int64_t n,
+                           const int32_t* next_users, const int32_t* next_items, int64_t n_next, float* shared,
+                           float* slice_grad, int32_t item_world, int32_t item_rank, int32_t include_dense_reg,
+                           void* comm, double* stats, void* ws, size_t ws_bytes, void* stream);
 
 /* Row-sharded data parallelism (no reference counterpart — the
  * reference trains on one CPU).  Rank r of `world` (1..16) owns the table rows g
@@ -374,6 +399,7 @@ int ncf_user_dp_step(const ncf_shape_t* shape, ncf_model_t* model, ncf_optim_t* 
  *                             send_counts[world]); compact ids kept in ws
  *   all_to_all (host, RCCL)   row ids to their owners
  *   ncf_gather_rows           owner: rows requested by every rank
+ *                             (ncf_shard_serve_rows under deferred decay)
  *   all_to_all                row values back, in uniq_rows order
  *   ncf_shard_forward_backward  fused forward/backward on the unique rows:
  *                             per-unique-row gradient uniq_grad, dense-layer
@@ -407,9 +433,26 @@ int ncf_shard_forward_backward(const ncf_shape_t* shape, const ncf_model_t* mode
                                int32_t world, const float* labels, int64_t n, float* uniq_grad, float* mlp_grad,
                                float* summary, float* probs_out, const float* reg_table, int64_t reg_rows,
                                int32_t include_dense_reg, void* ws, size_t ws_bytes, void* stream);
+/* Deferred exact decay of the shard (optim->row_step: int32[shard_rows], NCF_ROW_PRISTINE for
+ * fresh rows; Adam; embedding L2 off).  The owner serves the m rows requested by every rank
+ * (rows[m] = local row ids, concatenated in source-rank order; a source lists a row once): it
+ * builds the owner index of those entries (its own workspace regions: the plan's index
+ * survives), replays the served rows' missed zero-gradient steps (p; m, v follow in the update),
+ * and gathers out[j] = shard row rows[j].  The ncf_shard_apply_update of the same step then
+ * updates exactly those rows through that index (recv_grad in the order of rows[]) — bitwise
+ * the dense shard sweep's result, moving only the served rows.  Replaces ncf_gather_rows on the
+ * owner side of the step. */
+int ncf_shard_serve_rows(const ncf_shape_t* shape, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* hyper,
+                         int32_t world, const int32_t* rows, int64_t m, float* out, void* ws, size_t ws_bytes,
+                         void* stream);
+/* Deferred decay: bring every shard row up to optim->step (ncf_lazy_flush of the shard). */
+int ncf_shard_flush(const ncf_shape_t* shape, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* hyper,
+                    int32_t world, void* ws, size_t ws_bytes, void* stream);
 /* model->emb / optim->emb_m / emb_v = this rank's shard; recv_rows[m] /
  * recv_grad[m x row_width] = the rows requested by (and gradients from) every
- * rank, concatenated in source-rank order; mlp_grad and summary summed over ranks. */
+ * rank, concatenated in source-rank order; mlp_grad and summary summed over ranks.
+ * With optim->row_step (deferred decay) only the rows of the step's ncf_shard_serve_rows are
+ * updated (recv_rows is not read again); else every shard row is swept. */
 int ncf_shard_apply_update(const ncf_shape_t* shape, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* hyper,
                            int32_t world, const int32_t* recv_rows, const float* recv_grad, int64_t m,
                            const float* mlp_grad, const float* summary, double* stats, void* ws, size_t ws_bytes,

@@ -254,7 +254,27 @@ WsLayout make_layout(const ncf_shape_t& s, int64_t B, int world) {
     L.heavy_n = take(4);
     L.err = take(4);
     L.ifold = take(4);
+    const int64_t S = L.shard_rows;
+    if (world > 0) {
+        L.ocnt = take((size_t)(S + 1) * 4);
+        L.oheavy = take(4);
+        L.oifold = take(4);
+    }
     L.persistent_end = off;
+    if (world > 0) {
+        // the owner index: sized by the shard only, ahead of every per-batch region
+        L.onscan = (int)((S + 1 + kScanBlock - 1) / kScanBlock);
+        L.ooffs_local = take((size_t)(S + 1) * 4);
+        L.ooffs = take((size_t)(S + 1) * 4);
+        L.ouloc = take((size_t)(S + 1) * 4);
+        L.otot = take((size_t)L.onscan * 4);
+        L.outot = take((size_t)L.onscan * 4);
+        L.opre = take((size_t)2 * L.onscan * 4);
+        L.olist = take((size_t)world * S * 4);
+        L.otouched = take((size_t)S * 4);
+        L.otoc = take((size_t)S * 8);
+        L.onuniq = take(4);
+    }
     L.nscan = (int)((K + 1 + kScanBlock - 1) / kScanBlock);
     L.nmetric = (int)((B + kBlock - 1) / kBlock);
     int A = 0;
@@ -298,6 +318,29 @@ WsLayout make_layout(const ncf_shape_t& s, int64_t B, int world) {
     return L;
 }
 
+WsLayout owner_view(const WsLayout& L, int64_t m) {
+    WsLayout o = L;
+    o.cnt = L.ocnt;
+    o.heavy_n = L.oheavy;
+    o.ifold = L.oifold;
+    o.offs_local = L.ooffs_local;
+    o.offs = L.ooffs;
+    o.uloc = L.ouloc;
+    o.tot = L.otot;
+    o.utot = L.outot;
+    o.pre = L.opre;
+    o.list = L.olist;
+    o.touched = L.otouched;
+    o.touched_oc = L.otoc;
+    o.nuniq = L.onuniq;
+    o.nscan = L.onscan;
+    o.keys = L.shard_rows;
+    o.list_cap = (int64_t)L.world * L.shard_rows;
+    o.max_batch = m > 1 ? (m + 1) / 2 : 1;
+    o.world = 0;
+    return o;
+}
+
 int set_error(int code, const char* fmt, ...) {
     char buf[512];
     va_list ap;
@@ -329,8 +372,9 @@ int build_next_index(const ncf_shape_t& s, const ncf_hyper_t& h, ncf_model_t* mo
     prof_end(NCF_K_INDEX, st);
     if (e != hipSuccess) return hip_check(e, "next index");
     prof_begin(NCF_K_CATCHUP, st);
+    // enqueued before ncf_apply_update bumps the step: a stale-count gate replays to *step + 1
     e = launch_emb_catchup(s, L, ws, model->emb, optim->emb_m, optim->emb_v, optim->row_step, optim->step, h, false, st,
-                           true, n, true, next_users, next_items);
+                           true, n, true, next_users, next_items, 1);
     prof_end(NCF_K_CATCHUP, st);
     return hip_check(e, "next index sort");
 }
@@ -1021,6 +1065,73 @@ int ncf_gather_rows(const ncf_shape_t* s, const float* table, int64_t table_rows
                      "gather rows");
 }
 
+// The shard as a table of its own: S rows, every one under deferred decay (lazy_rows 0)
+static ncf_shape_t shard_shape(const ncf_shape_t& s, int world) {
+    ncf_shape_t o = s;
+    o.num_rows = ncf::shard_rows_of(s.num_rows, world);
+    return o;
+}
+
+static int check_shard_lazy(const ncf_shape_t* s, const ncf_model_t* model, const ncf_optim_t* optim,
+                            const ncf_hyper_t* h, int world) {
+    if (int r = check_shape(s)) return r;
+    if (int r = check_hyper(h)) return r;
+    if (int r = check_world(world)) return r;
+    if (!model || !model->emb) return fail(NCF_EINVAL, "NULL device pointer");
+    if (!optim || !optim->step || !optim->row_step || (h->optimizer == NCF_OPT_ADAM && (!optim->emb_m || !optim->emb_v)))
+        return fail(NCF_EINVAL, "deferred decay needs the optimizer state and row_step");
+    if (h->l2[0] != 0.0f)
+        return fail(NCF_EINVAL, "deferred decay (row_step) needs the embedding L2 off: the loss sums the whole table");
+    return 0;
+}
+
+int ncf_shard_serve_rows(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* h,
+                         int32_t world, const int32_t* rows, int64_t m, float* out, void* ws, size_t ws_bytes,
+                         void* stream) {
+    if (int r = check_shard_lazy(s, model, optim, h, world)) return r;
+    const int64_t S = ncf::shard_rows_of(s->num_rows, world);
+    if (m < 0 || m > (int64_t)world * S)
+        return fail(NCF_EINVAL, "served row count %lld outside [0, world * shard_rows]", (long long)m);
+    if (m > 0 && (!rows || !out)) return fail(NCF_EINVAL, "NULL device pointer");
+    ncf::WsLayout L;
+    if (int r = check_ws(*s, 1, ws, ws_bytes, &L, world)) return r;
+    hipStream_t st = (hipStream_t)stream;
+    const ncf::WsLayout O = ncf::owner_view(L, m);
+    const ncf_shape_t ss = shard_shape(*s, world);
+    ncf_hyper_t hs = *h;
+    hs.lazy_rows = 0;
+    // the owner index of the served rows (ascending entry = ascending source rank): the served
+    // rows' list for the catch-up now, the per-row entry lists for ncf_shard_apply_update later
+    prof_begin(NCF_K_INDEX, st);
+    hipError_t e = ncf::launch_owner_touched_index(L, ws, rows, m, st);
+    prof_end(NCF_K_INDEX, st);
+    if (e != hipSuccess) return hip_check(e, "owner index");
+    if (h->optimizer == NCF_OPT_ADAM) {
+        // the served rows' missed zero-gradient steps (p only: the update re-derives m, v)
+        prof_begin(NCF_K_CATCHUP, st);
+        e = ncf::launch_emb_catchup(ss, O, ws, model->emb, optim->emb_m, optim->emb_v, optim->row_step, optim->step,
+                                    hs, false, st);
+        prof_end(NCF_K_CATCHUP, st);
+        if (e != hipSuccess) return hip_check(e, "served-row catch-up");
+    }
+    return hip_check(ncf::launch_gather_rows(*s, model->emb, S, rows, m, out, st), "gather rows");
+}
+
+int ncf_shard_flush(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* h,
+                    int32_t world, void* ws, size_t ws_bytes, void* stream) {
+    if (int r = check_shard_lazy(s, model, optim, h, world)) return r;
+    ncf::WsLayout L;
+    if (int r = check_ws(*s, 1, ws, ws_bytes, &L, world)) return r;
+    hipStream_t st = (hipStream_t)stream;
+    const ncf_shape_t ss = shard_shape(*s, world);
+    ncf_hyper_t hs = *h;
+    hs.lazy_rows = 0;
+    hipError_t e = ncf::launch_emb_catchup(ss, ncf::owner_view(L, 1), ws, model->emb, optim->emb_m, optim->emb_v,
+                                           optim->row_step, optim->step, hs, true, st);
+    if (e != hipSuccess) return hip_check(e, "shard flush");
+    return hip_check(ncf::launch_row_step_fill(optim->row_step, ss.num_rows, optim->step, st), "row-step fill");
+}
+
 int ncf_shard_forward_backward(const ncf_shape_t* s, const ncf_model_t* model, const ncf_hyper_t* h, int32_t world,
                                const float* labels, int64_t n, float* uniq_grad, float* mlp_grad, float* summary,
                                float* probs_out, const float* reg_table, int64_t reg_rows,
@@ -1073,6 +1184,34 @@ int ncf_shard_apply_update(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t
     const int64_t S = ncf::shard_rows_of(s->num_rows, world);
     if (m < 0 || m > (int64_t)world * S)
         return fail(NCF_EINVAL, "received row count %lld outside [0, world * shard_rows]", (long long)m);
+    if (optim->row_step) {
+        // deferred decay: the served rows only, through the owner index ncf_shard_serve_rows built
+        // for these m entries (their gradients arrive in the same order as their ids did)
+        if (int r = check_shard_lazy(s, model, optim, h, world)) return r;
+        ncf::WsLayout L;
+        if (int r = check_ws(*s, 1, ws, ws_bytes, &L, world)) return r;
+        hipStream_t st = (hipStream_t)stream;
+        const ncf::WsLayout O = ncf::owner_view(L, m);
+        const ncf_shape_t ss = shard_shape(*s, world);
+        ncf_hyper_t hs = *h;
+        hs.lazy_rows = 0;
+        int nreg_mlp = 0;
+        prof_begin(NCF_K_MLP_UPDATE, st);
+        hipError_t e = ncf::launch_mlp_update(*s, L, ws, model->mlp, optim->mlp_m, optim->mlp_v, optim->step, *h, 0,
+                                              mlp_grad, nullptr, true, &nreg_mlp, st);
+        prof_end(NCF_K_MLP_UPDATE, st);
+        if (e != hipSuccess) return hip_check(e, "dense update");
+        if (m > 0) {
+            prof_begin(NCF_K_EMB_UPDATE, st);
+            e = ncf::launch_emb_update_touched(ss, O, ws, model->emb, optim->emb_m, optim->emb_v, optim->row_step,
+                                               optim->step, hs, st, nullptr, nullptr, 0, nullptr, 0, nullptr,
+                                               recv_grad);
+            prof_end(NCF_K_EMB_UPDATE, st);
+            if (e != hipSuccess) return hip_check(e, "served-row update");
+        }
+        e = ncf::launch_stats(L, ws, summary, 0, 0, h->inv_batch, stats, optim->step, true, st);
+        return hip_check(e, "stats");
+    }
     // smallest batch whose layout holds m received rows (the workspace was sized for a larger one)
     int64_t nb = (m + 2 * world - 1) / (2 * world);
     if (nb < 1) nb = 1;

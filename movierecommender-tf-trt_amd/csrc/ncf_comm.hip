@@ -64,6 +64,9 @@ int ncf_comm_init(int32_t world, int32_t rank, const void* id, size_t bytes, voi
     if (!r) r = hip_ok(hipEventCreateWithFlags(&c->join, hipEventDisableTiming), "hipEventCreate");
     if (r) {
         if (c->nccl) ncclCommDestroy(c->nccl);
+        if (c->fork) hipEventDestroy(c->fork);
+        if (c->join) hipEventDestroy(c->join);
+        if (c->side) hipStreamDestroy(c->side);
         delete c;
         return r;
     }
@@ -145,6 +148,91 @@ int ncf_user_dp_step(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* opti
                                  stream))
         return r;
     return 0;
+}
+
+// The user-partitioned step with the item rows' optimizer split across the ranks (the item table
+// stays replicated for the forward pass, but each rank applies Adam to 1/item_world of it):
+//   forward/backward (as ncf_user_dp_step) -> shared = [item-row gradient, item_world x Ic rows |
+//   dense-layer gradient | summary]
+//   comm stream: reduce-scatter of the item-row gradient (rank r receives rows [r Ic, r Ic + Ic) in
+//   slice_grad) + all-reduce of [dense-layer gradient | summary], one RCCL group ...
+//   ... beside the own-user update and the next batch's index on the compute stream
+//   join; Adam on this rank's item slice (table rows U + r Ic ..), the dense layers, stats
+//   comm stream: all-gather of the updated item rows (in place: the table holds item_world x Ic
+//   item rows, the rows past num_rows are zero padding); the compute stream waits for it
+// The same bytes cross the links as the all-reduce of ncf_user_dp_step; each rank's item Adam and
+// item-moment traffic shrink to 1/item_world.  item_world == 1 (or a one-rank communicator with
+// item_world > 1: the per-rank compute of that layout, no exchange) is bitwise ncf_user_dp_step.
+int ncf_user_dp_step_split(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* h,
+                           const int32_t* users, const int32_t* items, const float* labels, int64_t n,
+                           const int32_t* next_users, const int32_t* next_items, int64_t n_next, float* shared,
+                           float* slice_grad, int32_t item_world, int32_t item_rank, int32_t include_dense_reg,
+                           void* comm, double* stats, void* ws, size_t ws_bytes, void* stream) {
+    Comm* c = static_cast<Comm*>(comm);
+    if (!s || !model || !optim || !h || !shared || !c)
+        return comm_fail(NCF_EINVAL, "ncf_user_dp_step_split", "NULL argument");
+    if (h->lazy_rows <= 0 || h->lazy_rows > s->num_rows)
+        return comm_fail(NCF_EINVAL, "ncf_user_dp_step_split", "hyper->lazy_rows must be the rank's user count");
+    if (item_world < 1 || item_rank < 0 || item_rank >= item_world || (c->world != item_world && c->world != 1) ||
+        (c->world == item_world && c->rank != item_rank))
+        return comm_fail(NCF_EINVAL, "ncf_user_dp_step_split", "item_world/item_rank do not match the communicator");
+    const int64_t U = h->lazy_rows, R = s->num_rows, W = s->row_width, P = s->mlp_params;
+    const int64_t I = R - U, Ic = (I + item_world - 1) / item_world;
+    const bool exchange = c->world > 1;
+    if (exchange && !slice_grad) return comm_fail(NCF_EINVAL, "ncf_user_dp_step_split", "NULL slice_grad");
+    float* item_grad = shared;
+    float* mlp_grad = shared + item_world * Ic * W;
+    float* summary = mlp_grad + P;
+    hipStream_t st = (hipStream_t)stream;
+    if (int r = ncf_forward_backward_part_lazy(s, model, optim, h, users, items, labels, n, item_grad, mlp_grad, summary,
+                                               nullptr, include_dense_reg, ws, ws_bytes, stream))
+        return r;
+    hipStream_t side = c->side;
+    if (int r = hip_ok(hipEventRecord(c->fork, st), "fork")) return r;
+    if (int r = hip_ok(hipStreamWaitEvent(side, c->fork, 0), "fork wait")) return r;
+    if (exchange) {
+        if (int r = nccl_check(ncclGroupStart(), "ncclGroupStart")) return r;
+        if (int r = nccl_check(ncclReduceScatter(item_grad, slice_grad, (size_t)(Ic * W), ncclFloat32, ncclSum,
+                                                 c->nccl, side), "ncclReduceScatter"))
+            return r;
+        if (int r = nccl_check(ncclAllReduce(mlp_grad, mlp_grad, (size_t)(P + NCF_NUM_SUMMARY), ncclFloat32, ncclSum,
+                                             c->nccl, side), "ncclAllReduce"))
+            return r;
+        if (int r = nccl_check(ncclGroupEnd(), "ncclGroupEnd")) return r;
+    } else {
+        // one rank: its slice of the (local) item gradient is the reduced one
+        slice_grad = item_grad + item_rank * Ic * W;
+        if (int r = nccl_check(ncclAllReduce(mlp_grad, mlp_grad, (size_t)(P + NCF_NUM_SUMMARY), ncclFloat32, ncclSum,
+                                             c->nccl, side), "ncclAllReduce"))
+            return r;
+    }
+    if (int r = hip_ok(hipEventRecord(c->join, side), "join")) return r;
+    if (int r = ncf_update_rows_lazy(s, model, optim, h, n, next_users, next_items, n_next, ws, ws_bytes, stream))
+        return r;
+    if (next_users)
+        if (int r = ncf::build_next_index(*s, *h, model, optim, next_users, next_items, n_next, ws, ws_bytes, st))
+            return r;
+    if (int r = hip_ok(hipStreamWaitEvent(st, c->join, 0), "join wait")) return r;
+    // this rank's item slice (its moments indexed by table row) and the dense layers
+    const int64_t r0 = item_rank * Ic;
+    const int64_t cnt = r0 >= I ? 0 : (I - r0 < Ic ? I - r0 : Ic);
+    ncf_optim_t items_opt = *optim;
+    if (items_opt.emb_m) items_opt.emb_m += (U + r0) * W;
+    if (items_opt.emb_v) items_opt.emb_v += (U + r0) * W;
+    items_opt.row_step = nullptr;
+    if (int r = ncf_apply_update(s, model, &items_opt, h, U + (cnt ? r0 : I), cnt, slice_grad, mlp_grad, summary, stats,
+                                 ws, ws_bytes, stream))
+        return r;
+    if (!exchange) return 0;
+    // the updated slices to every rank (in place), before the next forward pass reads an item row
+    if (int r = hip_ok(hipEventRecord(c->fork, st), "fork")) return r;
+    if (int r = hip_ok(hipStreamWaitEvent(side, c->fork, 0), "fork wait")) return r;
+    float* items0 = model->emb + U * W;
+    if (int r = nccl_check(ncclAllGather(items0 + r0 * W, items0, (size_t)(Ic * W), ncclFloat32, c->nccl, side),
+                           "ncclAllGather"))
+        return r;
+    if (int r = hip_ok(hipEventRecord(c->join, side), "join")) return r;
+    return hip_ok(hipStreamWaitEvent(st, c->join, 0), "join wait");
 }
 
 }  // extern "C"

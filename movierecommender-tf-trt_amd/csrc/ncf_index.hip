@@ -552,4 +552,17 @@ hipError_t launch_owner_index(const WsLayout& L, void* ws, const int32_t* keys, 
     return build<kKeyList, false>(L, ws, ks, m, L.shard_rows, PlanOut{}, nwords, st);
 }
 
+hipError_t launch_owner_touched_index(const WsLayout& L, void* ws, const int32_t* keys, int64_t m, hipStream_t st) {
+    const WsLayout O = owner_view(L, m);
+    KeySrc ks{nullptr, nullptr, keys, 0, 0, L.world, (int32_t)L.shard_rows, 0};
+    PlanOut po{};
+    po.uloc = at<int32_t>(ws, O.uloc);
+    po.utot = at<int32_t>(ws, O.utot);
+    po.uniq_rows = at<int32_t>(ws, O.touched);
+    po.nuniq = at<int32_t>(ws, O.nuniq);
+    po.uniq_oc = at<int2>(ws, O.touched_oc);
+    // a row gets at most one entry per source rank: <= world <= kSmallSeg entries, no bitmap sort
+    return build<kKeyList, false, true>(O, ws, ks, m, L.shard_rows, po, 0, st);
+}
+
 }  // namespace ncf

@@ -62,6 +62,20 @@ struct WsLayout {
     size_t act;       // float[B * A] generic kernel activations
     size_t dz;        // float[B * D] generic kernel pre-activation grad
     size_t ones;      // float[B] layered path: all-ones vector (column sums as GEMV)ients
+    // row-sharded owner index (world > 0 only): the rows this rank serves, keyed by local shard row;
+    // every region sized by the shard alone (placed before the per-batch regions, so serving rows
+    // and updating them use the same offsets whatever the requesters' batch size)
+    size_t ocnt;      // int32[S+1]  persistent, all-zero between calls
+    size_t oheavy;    // int32       persistent
+    size_t oifold;    // int32       persistent (written by the index build, never read)
+    size_t ooffs_local, ooffs, ouloc;  // int32[S+1]
+    size_t otot, outot;                // int32[onscan]
+    size_t opre;                       // int32[2 * onscan]
+    size_t olist;     // int32[world * S] received entries grouped by local row (ascending entry)
+    size_t otouched;  // int32[S] the served rows, ascending
+    size_t otoc;      // int2[S] their (list offset, entry count)
+    size_t onuniq;    // int32
+    int onscan;
     size_t total;
     int64_t max_batch;
     int nscan;        // blocks of the offset scan
@@ -391,6 +405,12 @@ hipError_t launch_shard_plan(const ncf_shape_t& s, const WsLayout& L, void* ws, 
                              hipStream_t st, int fold = 0);
 // owner index: m received local row ids keys[j] grouped by row (ascending j), S = L.shard_rows keys
 hipError_t launch_owner_index(const WsLayout& L, void* ws, const int32_t* keys, int64_t m, hipStream_t st);
+// The owner index of the deferred-decay shard (world > 0): its own regions (WsLayout o*), so the
+// plan's index of the same workspace survives it; also the ascending list of the served rows.
+// owner_view: the layout with the index regions pointed at the owner's, keys = S, max_batch
+// sized for m entries (grid sizing of the catch-up and update launches over them)
+WsLayout owner_view(const WsLayout& L, int64_t m);
+hipError_t launch_owner_touched_index(const WsLayout& L, void* ws, const int32_t* keys, int64_t m, hipStream_t st);
 // compact gradient: out[u] = sum over the plan's contributions of unique row u (ascending c)
 hipError_t launch_uniq_grad(const ncf_shape_t& s, const WsLayout& L, void* ws, int64_t n, float* out,
                             hipStream_t st);
@@ -492,7 +512,9 @@ hipError_t launch_emb_update(const ncf_shape_t& s, const WsLayout& L, void* ws, 
 hipError_t launch_emb_catchup(const ncf_shape_t& s, const WsLayout& L, void* ws, float* emb, float* m, float* v,
                               int32_t* row_step, const int32_t* step, const ncf_hyper_t& h, bool all_rows,
                               hipStream_t st, bool sort_lists = false, int64_t n = 0, bool rows_current = false,
-                              const int32_t* users = nullptr, const int32_t* items = nullptr);
+                              const int32_t* users = nullptr, const int32_t* items = nullptr, int gate_ahead = 0);
+// (gate_ahead 1: enqueued before the step counter's bump — ncf_user_dp_step's next index — so the
+// gate replays to *step + 1, the step the next forward pass reads)
 hipError_t launch_row_step_fill(int32_t* row_step, int64_t R, const int32_t* step, hipStream_t st);
 // next_users/next_items (optional, n_next samples): extra blocks of the same launch count the NEXT
 // batch's contributions into the index counters (the next build skips its k_count) and replay the
@@ -520,7 +542,8 @@ hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, vo
                                      hipStream_t st, const int32_t* next_users = nullptr,
                                      const int32_t* next_items = nullptr, int64_t n_next = 0,
                                      const MlpDeferred* mlp = nullptr, int next_fold = 0,
-                                     const MetricsDeferred* met = nullptr);
+                                     const MetricsDeferred* met = nullptr, const float* grad_rows = nullptr);
+// (grad_rows: the contribution rows the list indexes; default the workspace's per-sample rows gs)
 // dense gradient of rows [row_begin, num_rows) into out (indexed from row_begin)
 hipError_t launch_emb_grad_dense(const ncf_shape_t& s, const WsLayout& L, void* ws, float* out, hipStream_t st,
                                   int64_t row_begin = 0);

@@ -350,6 +350,7 @@ struct StaleGate {
     int32_t U, I;
     int32_t* row_step;
     int64_t lazy_rows;         // rows [0, lazy_rows) are under deferred decay
+    int ahead;                 // the replay target is *step + ahead (1: enqueued before the step's bump)
 };
 
 __device__ __forceinline__ void stale_replay_body(float* __restrict__ embf, float* __restrict__ mf,
@@ -425,7 +426,7 @@ __device__ __forceinline__ void catchup_body(float4* __restrict__ emb, float4* _
     }
     if (!ALL && sg.users) {
         stale_replay_body(reinterpret_cast<float*>(emb), reinterpret_cast<float*>(m4), reinterpret_cast<float*>(v4),
-                          4 * (int)w4, sg, *step, lr, b1, b2, eps, so.err, (int)blockIdx.x, so.ncatch);
+                          4 * (int)w4, sg, *step + sg.ahead, lr, b1, b2, eps, so.err, (int)blockIdx.x, so.ncatch);
         return;
     }
     __shared__ float lut[kLrLut];
@@ -458,8 +459,11 @@ __device__ __forceinline__ void catchup_body(float4* __restrict__ emb, float4* _
         for (int j = 0; j < kRep; ++j) {
             const int64_t i = i0 + j * pstride;
             r[j] = i < n ? (ALL ? i : list[i]) : 0;
-            // R: rows [0, R) are under deferred decay (touched rows past it are swept densely)
-            sr[j] = i < n && (ALL || r[j] < R) ? row_step[r[j]] : t;
+            // R: rows [0, R) are under deferred decay (touched rows past it are swept densely); a
+            // pristine row (NCF_ROW_PRISTINE, past every t) is current: clamped to t, so no step loop
+            // ever starts from its mark (s + 1 would overflow)
+            const int rs = i < n && (ALL || r[j] < R) ? row_step[r[j]] : t;
+            sr[j] = rs < t ? rs : t;
         }
         for (int q = q0; q < W2; q += lanes_per_row) {  // element pair q: elements 2q, 2q + 1
             const f32x2 z2 = {0.f, 0.f};
@@ -536,7 +540,7 @@ __global__ __launch_bounds__(kBlock, NCF_FLUSH_WAVES) void k_emb_flush(float4* _
                                                       const int32_t* __restrict__ step, float lr, float b1, float b2,
                                                       float eps) {
     const SortAhead so{0, nullptr, 0, nullptr, 0, nullptr, nullptr, nullptr, nullptr, nullptr};
-    const StaleGate sg{nullptr, nullptr, 0, 0, 0, nullptr, 0};
+    const StaleGate sg{nullptr, nullptr, 0, 0, 0, nullptr, 0, 0};
     catchup_body<true>(emb, m4, v4, w4, nullptr, nullptr, R, row_step, step, lr, b1, b2, eps, so, sg);
 }
 
@@ -552,12 +556,13 @@ __global__ __launch_bounds__(kBlock, 8) void k_emb_catchup(float4* __restrict__ 
     catchup_body<false>(emb, m4, v4, w4, list, nlist, R, row_step, step, lr, b1, b2, eps, so, sg);
 }
 
-// row_step[r] = *step for every row (after a flush: the replay kernel above only reads row_step)
+// row_step[r] = *step for every row that is not pristine (after a flush: the replay kernel above
+// only reads row_step; a pristine row is current at every step and keeps its mark)
 __global__ __launch_bounds__(kBlock) void k_row_step_fill(int32_t* __restrict__ row_step, int64_t R,
                                                           const int32_t* __restrict__ step) {
     const int t = *step;
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < R; r += (int64_t)gridDim.x * blockDim.x)
-        row_step[r] = t;
+        if (row_step[r] != NCF_ROW_PRISTINE) row_step[r] = t;
 }
 
 // Adam step t = *step + 1 on the touched rows, which were brought up to step t-1 before the
@@ -899,11 +904,15 @@ __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_tou
             const int c = oc.y;
             // rows past lazy_rows (the list is ascending: its tail) are the caller's dense sweep's
             const bool mine = r < ca.lazy_rows;
-            const int k = NCF_CATCHUP_P_ONLY && mine ? t - 1 - row_step[r] : 0;  // m/v decay steps still owed
+            const int rs = mine ? row_step[r] : 0;
+            // a pristine row's moments are +0 (NCF_ROW_PRISTINE): only p is read
+            const bool fresh = rs == NCF_ROW_PRISTINE;
+            const int k = NCF_CATCHUP_P_ONLY && mine && !fresh ? t - 1 - rs : 0;  // m/v decay steps still owed
             for (uint32_t q = rl.q; mine && q < w4; q += rl.qstep) {
                 const size_t e = (size_t)r * w4 + q;
                 // the row's state does not depend on the gradient chain: its loads go out first
-                float4 p = emb[e], m = m4[e], v = v4[e];
+                const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+                float4 p = emb[e], m = fresh ? z : m4[e], v = fresh ? z : v4[e];
                 // k_emb_catchup brought p up to step t-1 and left m, v at row_step: the same
                 // per-step decay adam4 applies with g = 0 (b1*m + 0, b2*v + 0), bitwise
                 for (int j = 0; j < k; ++j) decay4(m, v, b1, b2);
@@ -1314,12 +1323,12 @@ static unsigned row_grid(int64_t rows, uint32_t w4, int64_t cap) {
 hipError_t launch_emb_catchup(const ncf_shape_t& s, const WsLayout& L, void* ws, float* emb, float* m, float* v,
                               int32_t* row_step, const int32_t* step, const ncf_hyper_t& h, bool all_rows,
                               hipStream_t st, bool sort_lists, int64_t n, bool rows_current, const int32_t* users,
-                              const int32_t* items) {
+                              const int32_t* items, int gate_ahead) {
     const uint32_t w4 = (uint32_t)(s.row_width / 4);
     const int64_t R = s.num_rows;
     const int64_t nmax = R < 2 * L.max_batch ? R : 2 * L.max_batch;
     SortAhead so{0, nullptr, 0, nullptr, 0, nullptr, at<int32_t>(ws, L.err), nullptr, nullptr, nullptr};
-    const StaleGate nogate{nullptr, nullptr, 0, 0, 0, nullptr, 0};
+    const StaleGate nogate{nullptr, nullptr, 0, 0, 0, nullptr, 0, 0};
     const int64_t bound = lazy_bound(s, h);  // rows under deferred decay
     unsigned nsort = 0;
     size_t lds = 0;
@@ -1353,7 +1362,7 @@ hipError_t launch_emb_catchup(const ncf_shape_t& s, const WsLayout& L, void* ws,
         StaleGate sg = nogate;
         unsigned ngate = 0;
         if (h.optimizer == NCF_OPT_ADAM && users && items && n > 0) {
-            sg = StaleGate{users, items, 2 * n, s.num_users, s.num_items, row_step, bound};
+            sg = StaleGate{users, items, 2 * n, s.num_users, s.num_items, row_step, bound, gate_ahead};
             ngate = 64;
         }
         if (nsort + ngate) {
@@ -1396,13 +1405,14 @@ hipError_t launch_row_step_fill(int32_t* row_step, int64_t R, const int32_t* ste
 hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, void* ws, float* emb, float* m,
                                      float* v, int32_t* row_step, int32_t* step, const ncf_hyper_t& h,
                                      hipStream_t st, const int32_t* next_users, const int32_t* next_items,
-                                     int64_t n_next, const MlpDeferred* mlp, int next_fold, const MetricsDeferred* met) {
+                                     int64_t n_next, const MlpDeferred* mlp, int next_fold, const MetricsDeferred* met,
+                                     const float* grad_rows) {
     const bool replay_ahead = next_users != nullptr && NCF_CATCHUP_AHEAD;
     const uint32_t w4 = (uint32_t)(s.row_width / 4);
     const uint32_t n4 = (uint32_t)(lazy_bound(s, h) * w4);  // SGD: the rows under deferred decay
     const int32_t* offs = at<int32_t>(ws, L.offs);
     const int32_t* list = at<int32_t>(ws, L.list);
-    const float4* gs = at<const float4>(ws, L.gs);
+    const float4* gs = grad_rows ? reinterpret_cast<const float4*>(grad_rows) : at<const float4>(ws, L.gs);
     const int64_t R = s.num_rows;
     if (h.optimizer == NCF_OPT_ADAM) {
         const unsigned nupd = row_grid(R < 2 * L.max_batch ? R : 2 * L.max_batch, w4, NCF_TOUCHED_GRID_MAX);

@@ -23,6 +23,7 @@ NCF_OPT_SGD = 1
 NCF_NUM_STATS = 8
 NCF_NUM_SUMMARY = 8
 NCF_WSERR_ID_RANGE, NCF_WSERR_STALE_COUNT, NCF_WSERR_FOLD = 1, 4, 8
+NCF_ROW_PRISTINE = 0x7fffffff   # row_step mark of a row whose Adam moments are exactly +0
 FB_KERNELS = {0: "generic", 1: "layered-rocblas", 2: "fused-mfma-tile", 3: "fused-mfma-unit", 4: "fused-mfma-wave"}
 SUM_BCE, SUM_HIT, SUM_DCG, SUM_GROUPS, SUM_REG = range(5)
 STAT_LOSS_SUM, STAT_HR_SUM, STAT_DCG_SUM, STAT_STEPS, STAT_LAST_LOSS, STAT_LAST_HR, STAT_LAST_DCG, STAT_BCE_SUM = \
@@ -104,6 +105,9 @@ _SIGNATURES = {
     "ncf_comm_allreduce": (ctypes.c_int, [_vp, _vp, _i64, _vp]),
     "ncf_user_dp_step": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _vp, _vp, _vp, _i64,
                                         _vp, _vp, _i64, _vp, _i32, _vp, _vp, _vp, ctypes.c_size_t, _vp]),
+    "ncf_user_dp_step_split": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _vp, _vp, _vp,
+                                              _i64, _vp, _vp, _i64, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp,
+                                              ctypes.c_size_t, _vp]),
     "ncf_lazy_flush": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _vp, ctypes.c_size_t,
                                       _vp]),
     "ncf_apply_update": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _i64, _i64, _vp, _vp,
@@ -118,6 +122,10 @@ _SIGNATURES = {
                                                   _vp, _vp, _vp, _vp, _i64, _i32, _vp, ctypes.c_size_t, _vp]),
     "ncf_shard_apply_update": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _i32, _vp,
                                               _vp, _i64, _vp, _vp, _vp, _vp, ctypes.c_size_t, _vp]),
+    "ncf_shard_serve_rows": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _i32, _vp,
+                                            _i64, _vp, _vp, ctypes.c_size_t, _vp]),
+    "ncf_shard_flush": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _i32, _vp,
+                                       ctypes.c_size_t, _vp]),
     "ncf_shard_predict": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _i32, _i64, _vp, _vp, ctypes.c_size_t, _vp]),
     "ncf_sample_batch": (ctypes.c_int, [_P(NcfSamplerData), _vp, _i64, _i32, _i32, ctypes.c_uint64, ctypes.c_uint64,
                                         _vp, _vp, _vp, _vp, _vp]),

@@ -148,27 +148,49 @@ class RowShardedDataParallel(object):
     """Drives one rank's ``ShardedNCFEngine`` (or a look-alike) through the row-sharded step:
 
       1. plan: unique rows of the local batch, grouped by owner (device)
-      2. all_to_all of the per-owner counts; one host read of the counts (split sizes)
-      3. all_to_all of the row ids to their owners; owners gather the rows; all_to_all back
+      2. all_to_all of the per-owner counts; their host copy gives the split sizes
+      3. all_to_all of the row ids to their owners; owners serve the rows (deferred decay: caught
+         up first and indexed for step 6); all_to_all back
       4. forward/backward on the fetched unique rows (per-unique-row gradients)
       5. all_to_all of the gradients to their owners; all_reduce of dense grad + summary
-      6. owner: per-row sum of the received gradients (ascending source rank), dense Adam over
-         the shard; Adam on the replicated dense layers
+      6. owner: per-row sum of the received gradients (ascending source rank), Adam on the served
+         rows (deferred decay) or a dense sweep of the shard; Adam on the replicated dense layers
+
+    ``train_step(..., next_batch=(users, items))`` plans the next batch right after this step's
+    forward/backward and exchanges its counts there, copying them to pinned host memory
+    asynchronously: the next step reads them with its event long done, so no step waits for
+    the device (the host stays up to a step ahead).  Pass exactly those tensors next step.
+
+    ``emulate=True`` (one process, engine built as rank ``engine.rank`` of ``engine.world``):
+    every row of the batches must be owned by this rank (the bench draws them so); the exchanges
+    become this rank's own buffers, so the step is the per-rank compute of the ``world``-rank step
+    without its collectives (a diagnostic of one rank's work, not a scaling result).
     """
 
-    def __init__(self, engine, group=None):
+    def __init__(self, engine, group=None, emulate=False):
         self.eng = engine
         self.group = group
-        self.world = dist.get_world_size(group)
-        self.rank = dist.get_rank(group)
+        self.emulate = bool(emulate)
+        if self.emulate:
+            self.world, self.rank = engine.world, engine.rank
+        else:
+            self.world = dist.get_world_size(group)
+            self.rank = dist.get_rank(group)
         if (engine.world, engine.rank) != (self.world, self.rank):
             raise ValueError("engine built for rank %d of %d, process group has rank %d of %d"
                              % (engine.rank, engine.world, self.rank, self.world))
         self.recv_counts = torch.zeros_like(engine.send_counts)
         self.last_exchange = None
+        self._ahead = None       # (users, items, n, versions, group) planned ahead, counts in flight
+        dev = engine.send_counts.device
+        pin = dev.type == "cuda"
+        self._counts_host = torch.zeros(2 * self.world, dtype=torch.int32, pin_memory=pin)
+        self._counts_event = torch.cuda.Event() if pin else None
 
     def broadcast_parameters(self, src=0):
         """Make every rank's dense layers equal to rank ``src``'s (shards are per rank)."""
+        if self.emulate:
+            return
         if self.eng.mlp.is_cuda and dist.get_backend(self.group) == "gloo":
             h = self.eng.mlp.cpu()
             dist.broadcast(h, src, group=self.group)
@@ -176,38 +198,94 @@ class RowShardedDataParallel(object):
         else:
             dist.broadcast(self.eng.mlp, src, group=self.group)
 
+    def _plan_and_count(self, users, items, group, ahead):
+        """Plan a batch and exchange its per-owner counts; ``ahead``: the counts' host copy is
+        left in flight (read by _counts() of the next step), else read now."""
+        eng = self.eng
+        eng.plan(users, items, group)
+        cat = self._counts_dev = getattr(self, "_counts_dev", None)
+        if cat is None or cat.device != eng.send_counts.device:
+            cat = self._counts_dev = torch.zeros(2 * self.world, dtype=torch.int32, device=eng.send_counts.device)
+        if self.emulate:
+            cat[:self.world].copy_(eng.send_counts)
+            cat[self.world:].copy_(eng.send_counts)   # the only source is this rank
+        else:
+            _all_to_all(self.recv_counts, eng.send_counts, None, None, self.group)
+            cat[:self.world].copy_(eng.send_counts)
+            cat[self.world:].copy_(self.recv_counts)
+        if self._counts_event is not None:
+            self._counts_host.copy_(cat, non_blocking=True)
+            self._counts_event.record()
+        else:
+            self._counts_host.copy_(cat)
+        if not ahead and self._counts_event is not None:
+            self._counts_event.synchronize()
+
+    def _counts(self):
+        if self._counts_event is not None:
+            self._counts_event.synchronize()   # recorded a step ago when planned ahead
+        c = self._counts_host.tolist()
+        return c[:self.world], c[self.world:]
+
     def _fetch_rows(self, users, items, group=None):
         eng = self.eng
-        uniq, send_counts = eng.plan(users, items, group)
-        _all_to_all(self.recv_counts, send_counts, None, None, self.group)
-        counts = torch.cat([send_counts, self.recv_counts]).cpu().tolist()
-        send, recv = counts[:self.world], counts[self.world:]
+        held = self._ahead
+        self._ahead = None
+        u, i = eng._ids(users), eng._ids(items)
+        ready = (held is not None and group is not None and held[0].data_ptr() == u.data_ptr() and
+                 held[1].data_ptr() == i.data_ptr() and held[2] == u.numel() and
+                 (held[0]._version, held[1]._version) == held[3] and held[4] == int(group))
+        if not ready:
+            self._plan_and_count(u, i, group, ahead=False)
+        else:
+            eng._n = u.numel()   # the plan ahead's batch (the engine planned it last)
+        send, recv = self._counts()
         nu, m = sum(send), sum(recv)
-        _all_to_all(eng.recv_rows[:m], uniq[:nu], recv, send, self.group)
-        vals = eng.gather_rows(eng.recv_rows, m)
-        _all_to_all(eng.uniq_vals[:nu], vals, send, recv, self.group)
+        if self.emulate:
+            # every row is this rank's own: its unique rows are the served rows (the id copy stands
+            # for the id exchange: the next batch's plan reuses uniq before this step's update)
+            eng.recv_rows[:nu].copy_(eng.uniq[:nu])
+            vals = eng.gather_rows(eng.recv_rows, nu, out=eng.uniq_vals)
+            self._rows_in, self._grad_in = eng.recv_rows, eng.uniq_grad
+        else:
+            _all_to_all(eng.recv_rows[:m], eng.uniq[:nu], recv, send, self.group)
+            vals = eng.gather_rows(eng.recv_rows, m)
+            _all_to_all(eng.uniq_vals[:nu], vals, send, recv, self.group)
+            self._rows_in, self._grad_in = eng.recv_rows, eng.recv_grad
         self.last_exchange = (nu, m)
         return send, recv, nu, m
 
-    def train_step(self, users, items, labels, group, k, global_batch=None):
+    def train_step(self, users, items, labels, group, k, global_batch=None, next_batch=None):
         n = len(users)
         gb = n * self.world if global_batch is None else int(global_batch)
         inv = 1.0 / gb
         eng = self.eng
         send, recv, nu, m = self._fetch_rows(users, items, group)
         eng.forward_backward(labels, group=group, k=k, inv_batch=inv, include_dense_reg=self.rank == 0)
-        _all_to_all(eng.recv_grad[:m], eng.uniq_grad[:nu], recv, send, self.group)
-        _all_reduce(eng.dense_buf, self.group)
-        eng.apply_update(eng.recv_rows, eng.recv_grad, m, inv)
+        if next_batch is not None:
+            # the forward/backward and its compact gradient were the last readers of this step's plan
+            nu_, ni_ = eng._ids(next_batch[0]), eng._ids(next_batch[1])
+            if nu_.data_ptr() == next_batch[0].data_ptr() and ni_.data_ptr() == next_batch[1].data_ptr():
+                self._plan_and_count(nu_, ni_, group, ahead=True)
+                self._ahead = (nu_, ni_, nu_.numel(), (nu_._version, ni_._version), int(group))
+        if not self.emulate:
+            _all_to_all(eng.recv_grad[:m], eng.uniq_grad[:nu], recv, send, self.group)
+            _all_reduce(eng.dense_buf, self.group)
+        eng.apply_update(self._rows_in, self._grad_in, m, inv)
 
     def predict(self, users, items):
         """Predictions for this rank's (users, items); every rank must call it (exchanges)."""
+        self.eng.flush()
         self._fetch_rows(users, items)
         return self.eng.predict_planned()
+
+    def flush(self):
+        self.eng.flush()
 
     def full_table(self):
         """The whole embedding table [num_rows x row_width] assembled from every shard."""
         eng = self.eng
+        eng.flush()
         parts = [torch.empty_like(eng.emb) for _ in range(self.world)]
         if eng.emb.is_cuda and dist.get_backend(self.group) == "gloo":
             hp = [p.cpu() for p in parts]
@@ -334,12 +412,22 @@ class UserPartitionedDataParallel(object):
     device stepping on the concatenated global batch, up to fp32 order of the cross-rank sum.
     """
 
-    def __init__(self, engine, group=None, native=None):
+    def __init__(self, engine, group=None, native=None, split_items=False, emulate_world=None):
         """``native``: drive the step through ``ncf_user_dp_step`` with the library's own RCCL
         communicator (one host call per step, the all-reduce on its side stream); default: when the
         process group is RCCL (``nccl``) and the engine defers its users' decay.  Otherwise the
-        step's calls and the torch.distributed all-reduce are issued one by one (gloo: ranks that
-        share one GPU in the tests)."""
+        step's calls and the torch.distributed collectives are issued one by one (gloo: ranks that
+        share one GPU in the tests).
+
+        ``split_items``: the item rows' Adam split across the ranks (``ncf_user_dp_step_split``):
+        a reduce-scatter of the item-row gradient (rank r gets item rows [r Ic, r Ic + Ic), Ic =
+        ceil(items / world)) with the all-reduce of [dense-layer gradient | summary], Adam on the
+        rank's item slice, an all-gather of the updated item rows.  The same bytes on the links
+        as the all-reduce; the item Adam and its moment traffic per rank are 1/world.  The table
+        is padded to world * Ic item rows for the in-place all-gather.
+
+        ``emulate_world`` (one-rank process group): rank 0's compute of a step of that many ranks
+        (its item slice only, no exchange) — the bench's per-rank diagnostic."""
         self.eng = engine
         self.group = group
         self.world = dist.get_world_size(group)
@@ -353,13 +441,32 @@ class UserPartitionedDataParallel(object):
             native = (dist.get_backend(group) == "nccl" and getattr(engine, "row_step", None) is not None and
                       hasattr(engine, "user_dp_step"))
         self.comm = _native_comm(self.rank, self.world, group) if native else None
+        iw = self.world
+        if emulate_world is not None and int(emulate_world) > 1:
+            if self.world != 1:
+                raise ValueError("emulate_world needs a one-rank process group")
+            iw = int(emulate_world)
+        self.split = bool(split_items)
+        self.item_world, self.item_rank = (iw, self.rank) if self.split else (1, 0)
+        I = R - U
+        self.Ic = -(-I // self.item_world)
+        rows_g = self.item_world * self.Ic if self.split else I
+        if self.split and U + rows_g > engine.emb.shape[0]:
+            # zero padding rows past the items: the in-place all-gather writes item_world * Ic rows
+            emb = torch.zeros(U + rows_g, W, dtype=engine.emb.dtype, device=engine.emb.device)
+            emb[:R].copy_(engine.emb[:R])
+            engine.emb = emb
+            from . import _native as N
+            engine.model_s = N.NcfModel(engine.emb.data_ptr(), engine.mlp.data_ptr())
         _, mg0, sm0 = engine.alloc_grads(rows=0)
         P, S = mg0.numel(), sm0.numel()
         dev = engine.emb.device
-        self.flat = torch.zeros((R - U) * W + P + S, dtype=engine.emb.dtype, device=dev)
-        self.grads = (self.flat[:(R - U) * W].view(R - U, W), self.flat[(R - U) * W:(R - U) * W + P],
-                      self.flat[(R - U) * W + P:])
+        self.flat = torch.zeros(rows_g * W + P + S, dtype=engine.emb.dtype, device=dev)
+        self.grads = (self.flat[:rows_g * W].view(rows_g, W), self.flat[rows_g * W:rows_g * W + P],
+                      self.flat[rows_g * W + P:])
         self.shared = self.flat                  # item rows | dense-layer grad | summary
+        self.slice_grad = (torch.zeros(self.Ic, W, dtype=engine.emb.dtype, device=dev)
+                           if self.split else None)
         self.num_local_users = U
         # the L2 loss of the replicated item rows is reported by rank 0 only
         self.reg_rows = (0, R) if self.rank == 0 else (0, U)
@@ -384,10 +491,13 @@ class UserPartitionedDataParallel(object):
         U, R = self.num_local_users, int(eng.num_rows)
         if self.comm is not None and eng.row_step is not None:
             eng.user_dp_step(users, items, labels, group=group, k=k, inv_batch=inv, shared=self.shared,
-                             comm=self.comm.handle, next_batch=next_batch, include_dense_reg=self.rank == 0)
+                             comm=self.comm.handle, next_batch=next_batch, include_dense_reg=self.rank == 0,
+                             split=(self.item_world, self.item_rank, self.slice_grad) if self.split else None)
             return
         eng.forward_backward_part(users, items, labels, group=group, k=k, inv_batch=inv, shared_row_begin=U,
                                   grads=self.grads, reg_rows=self.reg_rows, include_dense_reg=self.rank == 0)
+        if self.split:
+            return self._split_tail(U, R, inv, group, next_batch)
         work = _all_reduce_async(self.shared, self.group)
         if getattr(eng, "lazy_rows", None) == U and eng.row_step is not None:
             # deferred decay of the own users: the touched ones' update, and the next batch's index
@@ -400,6 +510,36 @@ class UserPartitionedDataParallel(object):
         if work is not None:
             work.wait()
         eng.apply_update(self.grads, inv, rows=(U, R - U), moments_by_row=True)
+
+    def _split_tail(self, U, R, inv, group, next_batch):
+        """The split-items step after the forward/backward, call by call (ncf_user_dp_step_split's
+        sequence): reduce-scatter of the item gradient + all-reduce of the dense part, the own
+        users' update and the next index meanwhile, the item slice's Adam, the all-gather."""
+        eng = self.eng
+        eg, mg, sm = self.grads
+        r0 = self.item_rank * self.Ic
+        cnt = max(0, min(self.Ic, (R - U) - r0))
+        dense = self.flat[eg.numel():]
+        exchange = self.world > 1
+        if exchange:
+            _reduce_scatter(self.slice_grad, eg, self.group)
+            work = _all_reduce_async(dense, self.group)
+            slice_grad = self.slice_grad
+        else:
+            work = None
+            slice_grad = eg[r0:r0 + self.Ic]
+        if getattr(eng, "lazy_rows", None) == U and eng.row_step is not None:
+            eng.update_rows(0, U, inv, next_batch=next_batch)
+        else:
+            eng.update_rows(0, U, inv)
+            if next_batch is not None and hasattr(eng, "build_index"):
+                eng.build_index(*next_batch, group)
+        if work is not None:
+            work.wait()
+        eng.apply_update((slice_grad, mg, sm), inv, rows=(U + (r0 if cnt else R - U), cnt), moments_by_row=True)
+        if exchange:
+            items = eng.emb[U:U + self.item_world * self.Ic]
+            _all_gather_inplace(items, self.Ic, self.group)
 
     def keras_weights(self):
         """Full Keras-layout weights (collective: every rank must call it): user rows gathered

@@ -51,6 +51,17 @@ def raise_ws_flags(f):
         raise ValueError("an id outside the embedding table reached the device (those samples were masked)")
 
 
+def pristine_marks(m, v, rows, step):
+    """row_step of rows [0, rows) whose Adam state was just set: NCF_ROW_PRISTINE where a row's
+    moments are all bitwise +0 (the zero-gradient step's fixed point), else ``step``."""
+    mi = m[:rows].view(torch.int32)
+    vi = v[:rows].view(torch.int32)
+    zero = ((mi == 0) & (vi == 0)).all(dim=1)
+    out = torch.full((rows,), int(step), dtype=torch.int32, device=m.device)
+    out[zero] = N.NCF_ROW_PRISTINE
+    return out
+
+
 class NCFEngine(object):
     """Model + optimizer state of one replica on one device."""
 
@@ -96,7 +107,10 @@ class NCFEngine(object):
             if self.lazy_rows is not None and not 0 < self.lazy_rows <= s.num_rows:
                 raise ValueError("lazy_rows must be in [1, %d]" % s.num_rows)
             nlazy = s.num_rows if self.lazy_rows is None else self.lazy_rows
-            self.row_step = torch.zeros(nlazy, dtype=torch.int32, device=dev) if lazy_adam else None
+            # fresh moments are +0: every row starts pristine (a fixed point of the zero-gradient
+            # step, so it owes no replay until its first gradient)
+            self.row_step = (torch.full((nlazy,), N.NCF_ROW_PRISTINE, dtype=torch.int32, device=dev)
+                             if lazy_adam else None)
             self._dirty = False
             self.stats = torch.zeros(N.NCF_NUM_STATS, dtype=torch.float64, device=dev)
             self.val_stats = torch.zeros(N.NCF_NUM_STATS, dtype=torch.float64, device=dev)
@@ -229,7 +243,7 @@ class NCFEngine(object):
         self.mlp.copy_(saved[1])
         self.step.fill_(int(step))
         if self.row_step is not None:
-            self.row_step.fill_(int(step))
+            self.row_step.copy_(pristine_marks(self.emb_m, self.emb_v, self.row_step.numel(), int(step)))
 
     # ------------------------------------------------------------- hot path
     def _ids(self, x):
@@ -483,7 +497,7 @@ class NCFEngine(object):
         self._dirty = True
 
     def user_dp_step(self, users, items, labels, group, k, inv_batch, shared, comm, next_batch=None,
-                     include_dense_reg=True):
+                     include_dense_reg=True, split=None):
         """The whole user-partitioned step with deferred decay in one library call
         (ncf_user_dp_step): forward/backward, the RCCL all-reduce of ``shared`` = [item-row grad |
         dense-layer grad | summary] on the native communicator ``comm`` beside the own-user update
@@ -508,11 +522,21 @@ class NCFEngine(object):
                 nu = ni = None
         h.index_ready = 3 if ready else 0
         try:
-            N.check(N.lib().ncf_user_dp_step(
-                ctypes.byref(self.shape), ctypes.byref(self.model_s), ctypes.byref(self.optim_s), ctypes.byref(h),
-                N.ptr(u), N.ptr(i), N.ptr(y), n, N.ptr(nu), N.ptr(ni), n if nu is not None else 0, N.ptr(shared),
-                1 if include_dense_reg else 0, comm, N.ptr(self.stats), N.ptr(self.ws), self.ws_bytes,
-                N.stream_handle(self.device)))
+            if split is not None:
+                # (item_world, item_rank, slice_grad): the item rows' Adam split across the ranks
+                iw, ir, sg = split
+                N.check(N.lib().ncf_user_dp_step_split(
+                    ctypes.byref(self.shape), ctypes.byref(self.model_s), ctypes.byref(self.optim_s),
+                    ctypes.byref(h), N.ptr(u), N.ptr(i), N.ptr(y), n, N.ptr(nu), N.ptr(ni),
+                    n if nu is not None else 0, N.ptr(shared), N.ptr(sg), int(iw), int(ir),
+                    1 if include_dense_reg else 0, comm, N.ptr(self.stats), N.ptr(self.ws), self.ws_bytes,
+                    N.stream_handle(self.device)))
+            else:
+                N.check(N.lib().ncf_user_dp_step(
+                    ctypes.byref(self.shape), ctypes.byref(self.model_s), ctypes.byref(self.optim_s),
+                    ctypes.byref(h), N.ptr(u), N.ptr(i), N.ptr(y), n, N.ptr(nu), N.ptr(ni),
+                    n if nu is not None else 0, N.ptr(shared), 1 if include_dense_reg else 0, comm,
+                    N.ptr(self.stats), N.ptr(self.ws), self.ws_bytes, N.stream_handle(self.device)))
         finally:
             h.index_ready = 0
         if nu is not None:

@@ -27,7 +27,10 @@ class ShardedNCFEngine(object):
 
     def __init__(self, num_users, num_items, layers_sizes, gmf_dim=0, world=1, rank=0, max_batch=65536,
                  device=None, optimizer="adam", lr=0.001, beta_1=0.9, beta_2=0.999, layers_l2reg=None,
-                 force_generic=False, force_layered=False):
+                 force_generic=False, force_layered=False, lazy_adam=False):
+        """``lazy_adam``: deferred exact decay of the shard (``row_step``, as ``NCFEngine``): the owner
+        replays a served row's missed zero-gradient steps when a rank requests it and updates only
+        the served rows; bitwise the dense shard sweep.  Needs layers_l2reg[0] == 0."""
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device())
         self.device = torch.device(device)
@@ -65,11 +68,19 @@ class ShardedNCFEngine(object):
             self.mlp_grad = self.dense_buf[:self.mlp_params]
             self.summary = self.dense_buf[self.mlp_params:]
             self.send_counts = torch.zeros(self.world, dtype=torch.int32, device=dev)
+            l2 = layers_l2reg or [0.0]
+            if lazy_adam and float(l2[0]) != 0.0:
+                raise ValueError("lazy_adam needs layers_l2reg[0] == 0 (the L2 loss sums the whole table)")
+            # fresh moments are +0: every shard row starts pristine (include/movierec_ncf.h)
+            self.row_step = (torch.full((self.shard_rows,), N.NCF_ROW_PRISTINE, dtype=torch.int32, device=dev)
+                             if lazy_adam else None)
+        self._dirty = False
         self.max_batch = 0
         self._ensure_ws(int(max_batch))
         self.model_s = N.NcfModel(self.emb.data_ptr(), self.mlp.data_ptr())
         self.optim_s = N.NcfOptim(self.emb_m.data_ptr(), self.emb_v.data_ptr(), self.mlp_m.data_ptr(),
-                                  self.mlp_v.data_ptr(), self.step.data_ptr())
+                                  self.mlp_v.data_ptr(), self.step.data_ptr(),
+                                  self.row_step.data_ptr() if self.row_step is not None else None)
         self.hyper = N.NcfHyper()
         self.set_hyper(optimizer, lr, beta_1, beta_2, layers_l2reg or [0.0] * len(self.layers))
         self.hyper.force_generic = 1 if force_generic else (2 if force_layered else 0)
@@ -134,8 +145,21 @@ class ShardedNCFEngine(object):
         g[g >= self.num_rows] = -1
         return g
 
+    @property
+    def lazy(self):
+        return self.row_step is not None
+
+    def flush(self):
+        """Deferred decay: bring every shard row up to the current step (no-op in dense mode)."""
+        if self.row_step is not None and self._dirty:
+            N.check(N.lib().ncf_shard_flush(ctypes.byref(self.shape), ctypes.byref(self.model_s),
+                                            ctypes.byref(self.optim_s), ctypes.byref(self.hyper), self.world,
+                                            N.ptr(self.ws), self.ws_bytes, N.stream_handle(self.device)))
+        self._dirty = False
+
     def set_keras_weights(self, w):
         """Load this rank's rows (and the dense layers) from a full Keras-layout dict."""
+        self.flush()
         emb, flat = self.layout.to_device(w)
         g = self.owned_rows()
         shard = np.zeros((self.shard_rows, self.row_width), dtype=np.float32)
@@ -176,11 +200,22 @@ class ShardedNCFEngine(object):
                                        N.ptr(self.ws), self.ws_bytes, N.stream_handle(self.device)))
         return self.uniq, self.send_counts
 
-    def gather_rows(self, rows, m):
-        """Owner side: this shard's rows ``rows[:m]`` (local ids) into ``recv_vals[:m]``."""
-        N.check(N.lib().ncf_gather_rows(ctypes.byref(self.shape), N.ptr(self.emb), self.shard_rows, N.ptr(rows),
-                                        int(m), N.ptr(self.recv_vals), N.stream_handle(self.device)))
-        return self.recv_vals[:m]
+    def gather_rows(self, rows, m, out=None):
+        """Owner side: this shard's rows ``rows[:m]`` (local ids, each source's rows once, sources
+        in rank order) into ``out`` (default ``recv_vals``).  Under deferred decay the rows are
+        served (ncf_shard_serve_rows): caught up first, and indexed for this step's
+        ``apply_update``, which must follow with their gradients in the same order."""
+        out = self.recv_vals if out is None else out
+        if self.row_step is not None:
+            self._dirty = True
+            N.check(N.lib().ncf_shard_serve_rows(ctypes.byref(self.shape), ctypes.byref(self.model_s),
+                                                 ctypes.byref(self.optim_s), ctypes.byref(self.hyper), self.world,
+                                                 N.ptr(rows), int(m), N.ptr(out), N.ptr(self.ws), self.ws_bytes,
+                                                 N.stream_handle(self.device)))
+        else:
+            N.check(N.lib().ncf_gather_rows(ctypes.byref(self.shape), N.ptr(self.emb), self.shard_rows, N.ptr(rows),
+                                            int(m), N.ptr(out), N.stream_handle(self.device)))
+        return out[:m]
 
     def forward_backward(self, labels, group, k, inv_batch, include_dense_reg=True, probs_out=None):
         """Forward/backward of the planned batch on ``uniq_vals`` (the fetched unique rows):
@@ -201,9 +236,11 @@ class ShardedNCFEngine(object):
             N.stream_handle(self.device)))
 
     def apply_update(self, recv_rows, recv_grad, m, inv_batch):
-        """Owner side: optimizer step of the whole shard from ``m`` received row gradients, and of
-        the dense layers from the (already reduced) ``mlp_grad`` / ``summary``."""
+        """Owner side: optimizer step of the whole shard (deferred decay: of the rows served this
+        step) from ``m`` received row gradients, and of the dense layers from the (already
+        reduced) ``mlp_grad`` / ``summary``."""
         self.hyper.inv_batch = float(inv_batch)
+        self._dirty = self._dirty or self.row_step is not None
         N.check(N.lib().ncf_shard_apply_update(
             ctypes.byref(self.shape), ctypes.byref(self.model_s), ctypes.byref(self.optim_s), ctypes.byref(self.hyper),
             self.world, N.ptr(recv_rows), N.ptr(recv_grad), int(m), N.ptr(self.mlp_grad), N.ptr(self.summary),

@@ -5,7 +5,7 @@ split, train generator (no extra data, shuffled) and validation generator
 (train as extra, not shuffled), table sizes from the dataset constants, build,
 ``fit_generator``, ``save``.  The CLI keeps ``-m -n -d -o -l``
 (``trainer.py:83-102``) and adds ``--gmf-dim``, ``--epochs``, ``--seed``,
-``--sampler``, ``--batch-size``, ``--negs``, ``--precision``.
+``--sampler``, ``--batch-size``, ``--batch-size-eval``, ``--negs``, ``--precision``.
 
 New params keys (optional):
   * ``sampler``: ``"host"`` (default: ``MovieLensDataGenerator``, the reference's numpy RNG
@@ -14,8 +14,9 @@ New params keys (optional):
   * ``world_size``: data parallelism over that many GPUs, one process each (``python -m
     torch.distributed.run --nproc-per-node N -m movierec.trainer ...``; the CLI takes it from
     WORLD_SIZE).  The ratings are partitioned by user — rank r trains the users u % N == r as
-    local ids u // N (``UserPartitionedDataParallel``) — and ``batch_size`` /
-    ``batch_size_eval`` stay the GLOBAL batch of one step, split evenly over the ranks.
+    local ids u // N (``UserPartitionedDataParallel``) — and ``batch_size`` stays the GLOBAL batch
+    of one step, split evenly over the ranks; ``batch_size_eval`` is split into whole groups per
+    rank (``eval_batch_per_rank``).
 """
 
 import copy
@@ -62,6 +63,17 @@ def _per_rank(batch, negs, world, what):
     return batch // world
 
 
+def eval_batch_per_rank(batch_eval, negs_eval, world):
+    """Validation batch of one rank: the global ``batch_size_eval`` split over the ranks, rounded
+    down to whole (negs + 1)-groups (at least one group).  Validation metrics are means over
+    groups, so the split does not change what a group contributes; it only sizes the batches
+    (the reference's default 200 with 99 negatives is 2 groups: one per rank at world 2, one
+    group per rank at any larger world)."""
+    g = negs_eval + 1
+    per = (batch_eval // world) // g * g
+    return max(per, g)
+
+
 def train(model_name, dataset_name, data_dir, output_dir, params=DEFAULT_PARAMS, verbose=1):
     train_df, validation_df, _test_df = data_pipeline.load_ratings_train_test_sets(dataset_name, data_dir)
     world = int(params.get("world_size", 1))
@@ -73,7 +85,7 @@ def train(model_name, dataset_name, data_dir, output_dir, params=DEFAULT_PARAMS,
         train_df = user_partition(train_df, world, rank)
         validation_df = user_partition(validation_df, world, rank)
         bs = _per_rank(bs, params["num_negs_per_pos"], world, "batch_size")
-        bs_eval = _per_rank(bs_eval, params["num_negs_per_pos_eval"], world, "batch_size_eval")
+        bs_eval = eval_batch_per_rank(bs_eval, params["num_negs_per_pos_eval"], world)
     if params.get("sampler", "host") == "device":
         from .sampler import DeviceMovieLensDataGenerator
 
@@ -121,16 +133,23 @@ def main(argv=None):
     parser.add_argument("--sampler", choices=["host", "device"], default="host",
                         help="host: the reference's numpy negative sampling; device: sampled on the GPU.")
     parser.add_argument("--batch-size", type=int, default=None, help="Training batch (global, all ranks).")
+    parser.add_argument("--batch-size-eval", type=int, default=None,
+                        help="Validation batch (global; each rank takes its share in whole groups).")
     parser.add_argument("--negs", type=int, default=None, help="Negatives per positive in training.")
     parser.add_argument("--precision", choices=["fp32", "bf16"], default=None,
                         help="MLP operand precision (bf16: BASELINE config B).")
+    parser.add_argument("--dist-backend", choices=["nccl", "gloo"], default=None,
+                        help="Process-group backend under torch.distributed.run (default: nccl = RCCL over xGMI).")
     args = parser.parse_args(argv)
     logging.getLogger().setLevel(logging.getLevelName(args.log_level))
     params = copy.deepcopy(DEFAULT_PARAMS)
     params["gmf_dim"] = args.gmf_dim
     params["sampler"] = args.sampler
     params["world_size"] = int(os.environ.get("WORLD_SIZE", "1"))   # under torch.distributed.run
+    if args.dist_backend:
+        params["dist_backend"] = args.dist_backend
     for key, val in (("epochs", args.epochs), ("seed", args.seed), ("batch_size", args.batch_size),
+                     ("batch_size_eval", args.batch_size_eval),
                      ("num_negs_per_pos", args.negs), ("precision", args.precision)):
         if val is not None:
             params[key] = val

@@ -41,7 +41,7 @@ class OracleEngine(object):
         self.mlp_lam = torch.from_numpy(lam)
 
     def weights(self):
-        return self.layout.from_device(self.emb.numpy(), self.mlp.numpy())
+        return self.layout.from_device(self.emb[:self.num_rows].numpy(), self.mlp.numpy())
 
     def alloc_grads(self, rows=None):
         rows = self.num_rows if rows is None else rows
@@ -89,7 +89,8 @@ class OracleEngine(object):
         self.forward_backward(users, items, labels, group, k, inv_batch, full, reg_rows=reg_rows,
                               include_dense_reg=include_dense_reg)
         self._local_grad = full[0]
-        grads[0][:] = full[0][shared_row_begin:self.num_rows]
+        grads[0].zero_()   # padding rows past the items (split item optimizer) stay zero
+        grads[0][:self.num_rows - shared_row_begin] = full[0][shared_row_begin:self.num_rows]
         grads[1][:] = full[1]
         grads[2][:] = full[2]
 
@@ -164,18 +165,30 @@ class OracleShardedEngine(object):
         self.send_counts = torch.from_numpy(np.bincount(ukeys // self.shard_rows, minlength=self.world)
                                             .astype(np.int32))
         n2 = rows.size
-        cap = self.world * min(n2, self.shard_rows)
-        self.uniq = torch.from_numpy((ukeys % self.shard_rows).astype(np.int32))
-        self.uniq_vals = torch.zeros(ukeys.size, self.row_width, dtype=torch.float64)
-        self.uniq_grad = torch.zeros(ukeys.size, self.row_width, dtype=torch.float64)
-        self.recv_rows = torch.zeros(cap, dtype=torch.int32)
-        self.recv_vals = torch.zeros(cap, self.row_width, dtype=torch.float64)
-        self.recv_grad = torch.zeros(cap, self.row_width, dtype=torch.float64)
+        if getattr(self, "_cap", 0) < n2:
+            # fixed-capacity buffers, as the device engine's: a plan made ahead (the next batch's)
+            # must not move the current step's unique-row gradients
+            self._cap = n2
+            cap = self.world * min(n2, self.shard_rows)
+            self.uniq = torch.zeros(n2, dtype=torch.int32)
+            self.uniq_vals = torch.zeros(n2, self.row_width, dtype=torch.float64)
+            self.uniq_grad = torch.zeros(n2, self.row_width, dtype=torch.float64)
+            self.recv_rows = torch.zeros(cap, dtype=torch.int32)
+            self.recv_vals = torch.zeros(cap, self.row_width, dtype=torch.float64)
+            self.recv_grad = torch.zeros(cap, self.row_width, dtype=torch.float64)
+        self.uniq[:ukeys.size] = torch.from_numpy((ukeys % self.shard_rows).astype(np.int32))
         return self.uniq, self.send_counts
 
-    def gather_rows(self, rows, m):
-        self.recv_vals[:m] = self.emb[rows[:m].long()]
-        return self.recv_vals[:m]
+    def _ids(self, x):
+        return x if torch.is_tensor(x) else torch.from_numpy(np.ascontiguousarray(np.asarray(x).reshape(-1)))
+
+    def flush(self):
+        pass
+
+    def gather_rows(self, rows, m, out=None):
+        out = self.recv_vals if out is None else out
+        out[:m] = self.emb[rows[:m].long()]
+        return out[:m]
 
     def _global_of_uniq(self):
         owner = self._ukeys // self.shard_rows
@@ -185,13 +198,13 @@ class OracleShardedEngine(object):
     def forward_backward(self, labels, group, k, inv_batch, include_dense_reg=True, probs_out=None):
         g = self._global_of_uniq()
         full = np.zeros((self.num_rows, self.row_width))
-        full[g] = self.uniq_vals.numpy()
+        full[g] = self.uniq_vals[:len(g)].numpy()
         w = self.layout.from_device(full, self.mlp.numpy())
         zero_l2 = [0.0] * len(self.shape.layers)
         _, grads, p = O.loss_and_grads(self.shape, w, self._users, self._items, labels, zero_l2,
                                        batch_norm=1.0 / inv_batch)
         eg, mg = self.layout.to_device(grads, dtype=np.float64)
-        self.uniq_grad[:] = torch.from_numpy(eg[g])
+        self.uniq_grad[:len(g)] = torch.from_numpy(eg[g])
         self.mlp_grad[:] = torch.from_numpy(mg)
         y = np.asarray(labels, dtype=np.float64)
         ng = len(y) // group

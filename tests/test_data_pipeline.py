@@ -299,3 +299,18 @@ def test_movie_titles_decoded_latin1(tmp_path):
     (d / "u.item").write_bytes("1|Très Bien (1996)|01-Jan-1996||http://x|0|1\n".encode("latin-1"))
     m = ml.load_movies_data(str(tmp_path), "ml-100k", download=False)
     assert m["movieTitle"][0] == "Très Bien (1996)"
+
+
+def test_eval_batch_per_rank_whole_groups():
+    """trainer.eval_batch_per_rank: the global validation batch split over the ranks in whole
+    (negs + 1)-groups, at least one group per rank (the reference defaults: 200 with 99 negatives)."""
+    from movierec.trainer import eval_batch_per_rank, _per_rank
+    assert eval_batch_per_rank(200, 99, 1) == 200
+    assert eval_batch_per_rank(200, 99, 2) == 100
+    assert eval_batch_per_rank(200, 99, 4) == 100
+    assert eval_batch_per_rank(200, 99, 8) == 100
+    assert eval_batch_per_rank(1000, 99, 4) == 200
+    assert eval_batch_per_rank(400, 3, 3) == 132
+    assert _per_rank(120, 9, 4, "batch_size") == 30
+    with pytest.raises(ValueError):
+        _per_rank(100, 9, 4, "batch_size")

@@ -121,7 +121,7 @@ def test_replicated_dp_matches_single_process_cpu():
             np.testing.assert_allclose(a[:5], b[:5], rtol=1e-6, atol=1e-9)
 
 
-def _cpu_sharded_worker(rank, world, port, q):
+def _cpu_sharded_worker(rank, world, port, q, ahead=False):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path[:0] = [here, os.path.dirname(here), os.path.join(os.path.dirname(here), "movierecommender-tf-trt_amd")]
@@ -133,9 +133,12 @@ def _cpu_sharded_worker(rank, world, port, q):
     dp = RowShardedDataParallel(eng)
     summaries, probs = [], []
     per = B // world
-    for users, items, y in _batches():
-        sl = slice(rank * per, (rank + 1) * per)
-        dp.train_step(users[sl], items[sl], y[sl], group=GROUP, k=2, global_batch=B)
+    sl = slice(rank * per, (rank + 1) * per)
+    mine = [tuple(torch.from_numpy(np.ascontiguousarray(a[sl])) for a in b) for b in _batches()]
+    for s, (users, items, y) in enumerate(mine):
+        # ahead: the next batch planned (and its counts exchanged) inside this step
+        nxt = mine[s + 1][:2] if ahead and s + 1 < len(mine) else None
+        dp.train_step(users, items, y.numpy(), group=GROUP, k=2, global_batch=B, next_batch=nxt)
         summaries.append(eng.summary.clone().numpy())
     full = dp.full_table().numpy().copy()
     q.put((rank, full, eng.mlp.numpy().copy(), summaries))
@@ -143,11 +146,11 @@ def _cpu_sharded_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def _run_cpu(worker, world):
+def _run_cpu(worker, world, *extra):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=worker, args=(r, world, port, q) + extra) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
@@ -160,15 +163,16 @@ def _run_cpu(worker, world):
     return res
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_row_sharded_dp_matches_single_process_cpu(world):
+@pytest.mark.parametrize("world,ahead", [(2, False), (3, False), (2, True)])
+def test_row_sharded_dp_matches_single_process_cpu(world, ahead):
     """Row-sharded exchanges (plan, all_to_all of ids/rows/grads, owner update) reproduce the
-    single-process step; world 3 leaves padding rows in the last shard (40 rows)."""
+    single-process step; world 3 leaves padding rows in the last shard (40 rows); ahead: each step
+    plans the next batch and exchanges its counts (the next step reads them, no replan)."""
     import sys
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from oracle_engine import OracleEngine
     assert B % (world * GROUP) == 0
-    res = _run_cpu(_cpu_sharded_worker, world)
+    res = _run_cpu(_cpu_sharded_worker, world, ahead)
     shape, w = _weights()
     ref = OracleEngine(shape, w, layers_l2reg=L2)
     grads = ref.alloc_grads()
@@ -204,7 +208,7 @@ def _user_part_batches(world):
     return out
 
 
-def _cpu_user_part_worker(rank, world, port, q):
+def _cpu_user_part_worker(rank, world, port, q, split=False):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path[:0] = [here, os.path.dirname(here), os.path.join(os.path.dirname(here), "movierecommender-tf-trt_amd")]
@@ -215,7 +219,7 @@ def _cpu_user_part_worker(rank, world, port, q):
     n_loc = (shape.num_users - rank + world - 1) // world
     local = O.NCFShape(n_loc, shape.num_items, shape.layers, shape.gmf_dim)
     eng = OracleEngine(local, partition_keras_weights(w, world, rank), layers_l2reg=L2)
-    dp = UserPartitionedDataParallel(eng)
+    dp = UserPartitionedDataParallel(eng, split_items=split)
     dp.broadcast_parameters()
     summaries = []
     for parts in _user_part_batches(world):
@@ -227,14 +231,16 @@ def _cpu_user_part_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_user_partitioned_dp_matches_single_process_cpu(world):
-    """User-partitioned data + replicated items (one all-reduce per step) reproduce the
-    single-process step on the concatenated global batch; world 3 gives unequal user shards."""
+@pytest.mark.parametrize("world,split", [(2, False), (3, False), (2, True), (3, True)])
+def test_user_partitioned_dp_matches_single_process_cpu(world, split):
+    """User-partitioned data + replicated items reproduce the single-process step on the
+    concatenated global batch, with the item rows' Adam on every rank (one all-reduce per step) or
+    split across the ranks (reduce-scatter, Adam on the rank's item slice, all-gather); world 3
+    gives unequal user shards and, split, a short last item slice (17 items = 6 + 6 + 5)."""
     import sys
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from oracle_engine import OracleEngine
-    res = _run_cpu(_cpu_user_part_worker, world)
+    res = _run_cpu(_cpu_user_part_worker, world, split)
     shape, w = _weights()
     ref = OracleEngine(shape, w, layers_l2reg=L2)
     grads = ref.alloc_grads()
@@ -582,11 +588,11 @@ def test_user_partitioned_deferred_decay_bitwise_dense_gpu(world):
     assert gpu_available()
 
 
-def _gpu_user_full_worker(rank, world, port, q):
-    _reporting(_gpu_user_full_worker_body, rank, world, port, q)
+def _gpu_user_full_worker(rank, world, port, q, per=65536, split=False):
+    _reporting(lambda *a: _gpu_user_full_worker_body(*a, per=per, split=split), rank, world, port, q)
 
 
-def _gpu_user_full_worker_body(rank, world, port, q):
+def _gpu_user_full_worker_body(rank, world, port, q, per=65536, split=False):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path[:0] = [here, os.path.dirname(here), os.path.join(os.path.dirname(here), "movierecommender-tf-trt_amd")]
@@ -596,12 +602,11 @@ def _gpu_user_full_worker_body(rank, world, port, q):
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
     U, I, layers, gmf = 138493, 27278, [128, 64, 32, 16], 64
-    per = 65536
     n_loc = (U - rank + world - 1) // world
     w = initial_weights(U, I, layers, gmf, seed=3)
     eng = NCFEngine(n_loc, I, layers, gmf, max_batch=per, lazy_adam=True, lazy_rows=n_loc)
     eng.set_keras_weights(partition_keras_weights(w, world, rank))
-    dp = UserPartitionedDataParallel(eng)
+    dp = UserPartitionedDataParallel(eng, split_items=split)
     batches = _user_part_device_batches((U, I, layers, gmf), world, per, 3, 31)
     dev = [tuple(torch.from_numpy(x).cuda() for x in (p[rank][0] // world, p[rank][1], p[rank][2]))
            for p in batches]
@@ -615,10 +620,14 @@ def _gpu_user_full_worker_body(rank, world, port, q):
 
 
 @pytest.mark.gpu
-def test_user_partitioned_full_config_c_tables_gpu():
-    """The user layout at config C's full tables (138,493 x 27,278), 65,536 samples per rank at
-    world 2, deferred decay with counting ahead, 3 steps, against ncf_train_step on the
-    concatenated 131,072-sample batches.  The step is the same arithmetic up to fp32 summation
+@pytest.mark.parametrize("per,split", [(65536, False), (8192, True)], ids=["65536-replicated-items",
+                                                                          "8192-split-items"])
+def test_user_partitioned_full_config_c_tables_gpu(per, split):
+    """The user layout at config C's full tables (138,493 x 27,278) at world 2, deferred decay with
+    counting ahead, 3 steps, against ncf_train_step on the concatenated 2 x per batches: 65,536
+    samples per rank with the item rows' Adam replicated (one all-reduce), and 8,192 per rank
+    (config C's BASELINE global batch over 8 GPUs, the strong-scaling shape) with it split across
+    the ranks (reduce-scatter + all-gather).  The step is the same arithmetic up to fp32 summation
     order of the item-row and dense-layer gradients; from step 2 on that order can move a sample
     across a ReLU kink (a pre-activation within ~1e-9 of 0), which changes its rows by up to two
     Adam steps.  So: dense layers within 1e-5; embedding rows beyond 1e-5 fewer than 0.1 % of the
@@ -630,7 +639,7 @@ def test_user_partitioned_full_config_c_tables_gpu():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_gpu_user_full_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_gpu_user_full_worker, args=(r, world, port, q, per, split)) for r in range(world)]
     for p in procs:
         p.start()
     res = _get(q, world)
@@ -638,9 +647,9 @@ def test_user_partitioned_full_config_c_tables_gpu():
         p.join(timeout=120)
         assert p.exitcode == 0
     U, I, layers, gmf = 138493, 27278, [128, 64, 32, 16], 64
-    ref = NCFEngine(U, I, layers, gmf, max_batch=2 * 65536, lazy_adam=True)
+    ref = NCFEngine(U, I, layers, gmf, max_batch=2 * per, lazy_adam=True)
     ref.set_keras_weights(initial_weights(U, I, layers, gmf, seed=3))
-    batches = _user_part_device_batches((U, I, layers, gmf), world, 65536, 3, 31)
+    batches = _user_part_device_batches((U, I, layers, gmf), world, per, 3, 31)
     dev = [tuple(torch.from_numpy(np.concatenate(x)).cuda() for x in zip(*parts)) for parts in batches]
     for s, (u, it, y) in enumerate(dev):
         nxt = (dev[s + 1][0], dev[s + 1][1]) if s + 1 < len(dev) else None
@@ -679,11 +688,11 @@ def _gpu_native_comm_worker_body(rank, world, port, q):
     shape, w = _weights(SHAPE_C)
     per = 256
     out = []
-    for native in (True, False):
+    for native, split in ((True, False), (False, False), (True, True), (False, True)):
         eng = NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=per, lazy_adam=True,
                         lazy_rows=shape.num_users)
         eng.set_keras_weights(partition_keras_weights(w, world, rank))
-        dp = UserPartitionedDataParallel(eng, native=native)
+        dp = UserPartitionedDataParallel(eng, native=native, split_items=split)
         assert (dp.comm is not None) == native
         batches = _user_part_device_batches(SHAPE_C, world, per, 10, 41)
         dev = [tuple(torch.from_numpy(x).cuda() for x in p[rank]) for p in batches]
@@ -697,7 +706,22 @@ def _gpu_native_comm_worker_body(rank, world, port, q):
         out.append((eng.keras_weights(), m, v, t, NCFEngine.read_stats(eng.stats)))
         if dp.comm is not None:
             dp.comm.close()
-    q.put((rank, out))
+    # an emulated rank 0 of 8 with the split item optimizer (its item slice only, no exchange): one
+    # step, natively and call by call, against the replicated-item step of the same local table
+    emu = []
+    for native, split in ((True, True), (False, True), (True, False)):
+        eng = NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=per, lazy_adam=True,
+                        lazy_rows=shape.num_users)
+        eng.set_keras_weights(partition_keras_weights(w, world, rank))
+        dp = UserPartitionedDataParallel(eng, native=native, split_items=split, emulate_world=8)
+        u, it, y = (torch.from_numpy(x).cuda() for x in _user_part_device_batches(SHAPE_C, world, per, 1, 43)[0][rank])
+        dp.train_step(u, it, y, group=GROUP, k=2, global_batch=8 * per)
+        eng.flush()
+        torch.cuda.synchronize()
+        emu.append((eng.emb[:eng.num_rows].cpu().numpy(), eng.mlp.cpu().numpy(), dp.Ic))
+        if dp.comm is not None:
+            dp.comm.close()
+    q.put((rank, out, emu, eng.num_users, partition_keras_weights(w, world, rank)))
     dist.destroy_process_group()
 
 
@@ -712,13 +736,27 @@ def test_user_partitioned_native_comm_step_bitwise_gpu():
     port = _free_port()
     p = ctx.Process(target=_gpu_native_comm_worker, args=(0, 1, port, q))
     p.start()
-    out = _get(q, 1)[0]
+    out, emu, U, w0 = _get(q, 1)[0]
     p.join(timeout=120)
     assert p.exitcode == 0
-    (wa, ma, va, ta, sa), (wb, mb, vb, tb, sb) = out
-    for name in wa:
-        np.testing.assert_array_equal(wa[name], wb[name], err_msg=name)
-        np.testing.assert_array_equal(ma[name], mb[name], err_msg="m " + name)
-        np.testing.assert_array_equal(va[name], vb[name], err_msg="v " + name)
-    assert ta == tb == 10 and sa == sb
+    (wa, ma, va, ta, sa) = out[0]
+    # native / call by call, replicated / split item optimizer: all bitwise at one rank
+    for (wb, mb, vb, tb, sb) in out[1:]:
+        for name in wa:
+            np.testing.assert_array_equal(wa[name], wb[name], err_msg=name)
+            np.testing.assert_array_equal(ma[name], mb[name], err_msg="m " + name)
+            np.testing.assert_array_equal(va[name], vb[name], err_msg="v " + name)
+        assert ta == tb == 10 and sa == sb
+    # emulated rank 0 of 8, split: its user rows, its item slice and the dense layers are those of
+    # the replicated step; the other item rows keep their values (no all-gather)
+    (es, ms, ic), (ep, mp_, _), (er, mr, _) = emu
+    np.testing.assert_array_equal(es, ep)
+    np.testing.assert_array_equal(ms, mp_)
+    np.testing.assert_array_equal(ms, mr)
+    np.testing.assert_array_equal(es[:U + ic], er[:U + ic])
+    assert not np.array_equal(es[U + ic:], er[U + ic:])
+    from movierec.layout import Layout
+    shape, _ = _weights(SHAPE_C)
+    e0, _ = Layout(U, shape.num_items, shape.layers, shape.gmf_dim).to_device(w0)
+    np.testing.assert_array_equal(es[U + ic:], e0[U + ic:])
     assert gpu_available()

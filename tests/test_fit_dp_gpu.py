@@ -219,3 +219,50 @@ def test_trainer_world2_device_sampler(tmp_path):
     loaded = MovierecModel.load_from_dir(out_dir, "dp2", verbose=0)
     assert loaded.model.get_weights()["user_embedding"].shape[0] == 943
     assert gpu_available()
+
+
+def _trainer_main_worker(rank, world, port, data_dir, out_dir, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [here, os.path.dirname(here), os.path.join(os.path.dirname(here), "movierecommender-tf-trt_amd")]
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    try:
+        from movierec import trainer
+        np.random.seed(rank)
+        random.seed(5)
+        # the reference's DEFAULT_PARAMS (batch_size_eval 200 with 99 negatives: 2 groups) at 4 ranks;
+        # only the training batch is given (100 does not split into 4 ranks of whole 10-groups)
+        trainer.main(["-m", "w4", "-n", "ml-100k", "-d", data_dir, "-o", out_dir, "--epochs", "1", "--batch-size",
+                      "120", "--sampler", "device", "--dist-backend", "gloo", "-l", "WARNING"])
+        q.put((rank, "ok"))
+    except BaseException as e:
+        import traceback
+        q.put((rank, "worker failed:\n" + traceback.format_exc()))
+        raise
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_trainer_main_world4_default_params(tmp_path):
+    """The CLI (trainer.main) under a four-rank launch with the reference's default params: the
+    validation batch (200 samples = 2 groups of 100) is split per rank in whole groups
+    (trainer.eval_batch_per_rank) instead of raising."""
+    from movierec.model import MovierecModel
+    data_dir, out_dir = str(tmp_path / "data"), str(tmp_path / "models")
+    _write_ml100k(data_dir, seed=3)
+    world = 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_trainer_main_worker, args=(r, world, port, data_dir, out_dir, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for _ in range(world):
+        r, msg = q.get(timeout=300)
+        assert msg == "ok", msg
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert os.path.exists(MovierecModel.get_model_weights_path(out_dir, "w4"))

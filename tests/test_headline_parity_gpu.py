@@ -39,6 +39,7 @@ pytestmark = pytest.mark.gpu
 
 if gpu_available():
     import torch
+    from movierec import _native as N
     from movierec.engine import NCFEngine
 
 U, I, LAYERS, GMF = 138493, 27278, [128, 64, 32, 16], 64
@@ -271,6 +272,13 @@ def test_deferred_decay_long_gaps_bitwise():
         assert torch.equal(dense.emb, e.emb)
         assert torch.equal(dense.emb_m, e.emb_m) and torch.equal(dense.emb_v, e.emb_v)
         assert torch.equal(dense.mlp, e.mlp) and torch.equal(dense.mlp_m, e.mlp_m)
-        assert int(e.row_step.min()) == int(e.row_step.max()) == steps == int(e.step.item())
+        rs = e.row_step[e.row_step != N.NCF_ROW_PRISTINE]
+        assert int(rs.min()) == int(rs.max()) == steps == int(e.step.item())
+        # rows no batch touched kept the pristine mark through the flush (never replayed): the
+        # dense sweep left them bitwise where they started, with +0 moments
+        fresh = (e.row_step == N.NCF_ROW_PRISTINE).nonzero().flatten()
+        assert fresh.numel() > 100
+        assert int(e.emb_m[fresh].view(torch.int32).abs().max()) == 0
+        assert int(e.emb_v[fresh].view(torch.int32).abs().max()) == 0
     assert NCFEngine.read_stats(dense.stats) == NCFEngine.read_stats(lazy.stats)
     assert gpu_available()

@@ -20,7 +20,8 @@ pytestmark = pytest.mark.gpu
 
 if gpu_available():
     import torch
-    from movierec.engine import NCFEngine
+    from movierec import _native as N
+    from movierec.engine import NCFEngine, pristine_marks
 
 
 SHAPES = [
@@ -294,7 +295,11 @@ def test_lazy_decay_bitwise_equals_dense_sweep(dims, opt):
             assert torch.equal(dense.emb, lazy.emb) and torch.equal(dense.mlp, lazy.mlp)
             if opt == "adam":
                 assert torch.equal(dense.emb_m, lazy.emb_m) and torch.equal(dense.emb_v, lazy.emb_v)
-            assert int(lazy.row_step.min()) == int(lazy.step.item()) == s + 1
+            rs = lazy.row_step[lazy.row_step != N.NCF_ROW_PRISTINE]
+            if opt == "adam":
+                assert int(rs.min()) == int(lazy.step.item()) == s + 1
+            else:   # SGD leaves no moments: every row stays pristine (current at any step)
+                assert rs.numel() == 0 and int(lazy.step.item()) == s + 1
     # reads flush implicitly
     users, items, y = _batch(shape, 40, 4, 99)
     dense.train_step(users, items, y, group=4, k=2)
@@ -303,6 +308,53 @@ def test_lazy_decay_bitwise_equals_dense_sweep(dims, opt):
     assert torch.equal(dense.emb, lazy.emb)
     np.testing.assert_array_equal(dense.keras_weights()["item_embedding"], lazy.keras_weights()["item_embedding"])
     assert NCFEngine.read_stats(dense.stats) == NCFEngine.read_stats(lazy.stats)
+
+
+@pytest.mark.parametrize("dims", [SHAPES[3], SHAPES[5]], ids=["configC", "configD"])
+def test_pristine_rows_after_set_optimizer_state_bitwise(dims):
+    """Pristine rows (row_step == NCF_ROW_PRISTINE: Adam moments exactly +0) skip every replay
+    and the flush; set_optimizer_state marks exactly the rows whose moments are all +0 (a -0
+    moment is not +0: the zero-gradient step would flip a -0 weight's sign).  The run continues
+    bitwise the dense sweep, with and without counting ahead."""
+    shape = O.NCFShape(*dims)
+    w = _weights(shape, 21)
+    dense = _engine(shape, w)
+    lazy = _engine(shape, w, lazy_adam=True)
+    ahead = _engine(shape, w, lazy_adam=True)
+    R = int(dense.num_rows)
+    assert int((lazy.row_step == N.NCF_ROW_PRISTINE).sum()) == R   # fresh moments: every row pristine
+    # a saved optimizer state: moments on the even rows (one of them only a -0 entry), +0 elsewhere
+    rng = np.random.RandomState(5)
+    m, v, _ = dense.optimizer_state()
+    for name in m:
+        if name.endswith("embedding"):
+            mm = np.zeros_like(m[name])
+            vv = np.zeros_like(v[name])
+            mm[::2] = rng.uniform(-1e-3, 1e-3, size=mm[::2].shape)
+            vv[::2] = rng.uniform(0, 1e-6, size=vv[::2].shape)
+            m[name], v[name] = mm, vv
+        else:
+            m[name] = rng.uniform(-1e-3, 1e-3, size=m[name].shape)
+            v[name] = rng.uniform(0, 1e-6, size=v[name].shape)
+    for e in (dense, lazy, ahead):
+        e.set_optimizer_state(m, v, 9)
+    for e in (lazy, ahead):
+        e.emb_m[1, 0] = -0.0
+        e.row_step.copy_(pristine_marks(e.emb_m, e.emb_v, R, 9))
+    dense.emb_m[1, 0] = -0.0
+    marks = lazy.row_step.cpu().numpy()
+    assert marks[1] == 9 and (marks[3::2] == N.NCF_ROW_PRISTINE).all() and (marks[0::2] == 9).all()
+    batches = [tuple(torch.from_numpy(a).cuda() for a in _batch(shape, 24, 4, 70 + s)) for s in range(6)]
+    for s, (u, it, y) in enumerate(batches):
+        dense.train_step(u, it, y, group=4, k=2)
+        lazy.train_step(u, it, y, group=4, k=2)
+        nxt = (batches[s + 1][0], batches[s + 1][1]) if s + 1 < len(batches) else None
+        ahead.train_step(u, it, y, group=4, k=2, next_batch=nxt)
+    for e in (lazy, ahead):
+        e.flush()
+        assert torch.equal(dense.emb, e.emb) and torch.equal(dense.mlp, e.mlp)
+        assert torch.equal(dense.emb_m, e.emb_m) and torch.equal(dense.emb_v, e.emb_v)
+        assert (e.row_step == N.NCF_ROW_PRISTINE).any()
 
 
 @pytest.mark.parametrize("dims", [SHAPES[3], SHAPES[1], SHAPES[5]], ids=["configC", "small", "configD"])

@@ -1,7 +1,7 @@
-# round 3 close: every GPU test, smoke and the driver's bench command on the committed library
+# GPU box: every GPU test, smoke, the driver's bench command and config D. Usage: bash tools/gpu_check.sh OUT
 export TMPDIR=/tmp
-O=gpurun_out/r03_close; mkdir -p $O
-timeout -k 10 700 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests -m gpu > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
+O=${1:-gpurun_out/check}; mkdir -p $O
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests -m gpu > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
 tail -1 $O/tests.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { cat $O/smoke.log; exit 1; }
 tail -1 $O/smoke.log
