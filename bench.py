@@ -65,7 +65,7 @@ CONFIGS = {
                        "bf16 MLP operands (fp32 accumulation, master weights and Adam)",
               num_users=6040, num_items=3952, layers=[64, 32, 16, 8], gmf_dim=8, negs=4, batch=4095, precision="bf16"),
     "D": dict(workload="synthetic 10M users x 1M items (config D): gmf 128 + MLP [256,128,64,32], 3 neg/pos, "
-                       "Adam dense semantics via deferred exact decay, one GPU (layered rocBLAS GEMM path)",
+                       "Adam dense semantics via deferred exact decay (layer-by-layer hand-written MFMA path)",
               num_users=10000000, num_items=1000000, layers=[256, 128, 64, 32], gmf_dim=128, negs=3, batch=65536),
     "E": dict(workload="ml-20m all-item scoring + top-10 (config E): every one of 138493 users x all 27278 items, "
                        "NeuMF gmf 64 + MLP [128,64,32,16] (config C's model), fp16 MFMA / fp32 accumulate",
@@ -155,6 +155,29 @@ def emb_update_bytes(cfg_shape, batch, dense_rows=None, sparse_rows=None, touche
         S, m = sparse_rows
         return 24 * S * W + m * W * 4 + m * 4 + (S + 1) * 4
     return 24 * R * W + c * W * 4 + c * 4 + (R + 1) * 4
+
+
+def replayed_rows(pool, warmup, steps, U, rows, items=True):
+    """Rows the catch-up-ahead blocks of a timed step's update launch replay, averaged over the
+    timed steps: those of the next batch that this step does not touch and that some earlier step
+    did (a row no step has touched yet is pristine: its zero moments make the zero-gradient steps
+    a fixed point, nothing to replay).  ``items``: item rows are under deferred decay too (one
+    table; the user layout sweeps its replicated item rows)."""
+    seq = [pool[i % len(pool)] for i in range(warmup + steps + 1)]
+
+    def rows_of(b):
+        r = torch.unique(b[0].long())
+        return torch.cat([r, U + torch.unique(b[1].long())]) if items else r
+    seen = torch.zeros(rows, dtype=torch.bool, device=seq[0][0].device)
+    out = []
+    cur = rows_of(seq[0])
+    for t in range(len(seq) - 1):
+        nxt = rows_of(seq[t + 1])
+        if t >= warmup:
+            out.append(int((~torch.isin(nxt, cur) & seen[nxt]).sum()))
+        seen[cur] = True
+        cur = nxt
+    return float(np.mean(out)) if out else 0.0
 
 
 def fwd_bwd_flops(cfg):
@@ -432,6 +455,50 @@ def device_glorot_init_shard(eng, w_small, seed):
     torch.cuda.synchronize()
 
 
+def native_step_check(cfg, world, rank, split, steps=5, per=2048):
+    """At N > 1 over RCCL, before the measured run: the library's one-call user-partitioned step
+    (ncf_user_dp_step / _split: its own communicator, the collective on a side stream beside the
+    own-user update and the next batch's index) against the same step issued call by call with
+    torch.distributed's collectives, from identical state, on config C's model with small tables.
+    Every rank compares its weights, Adam moments and stats; the max difference over the ranks is
+    the result.  The measured run uses the native step only when the two agree (to fp32 order of
+    the cross-rank sums; bitwise when RCCL picks the same reduction order for both)."""
+    from movierec.engine import NCFEngine
+    from movierec.distributed import UserPartitionedDataParallel, partition_keras_weights
+    from movierec.model import initial_weights
+    U, I, g = 4000, 3000, cfg["negs"] + 1
+    w = initial_weights(U, I, cfg["layers"], cfg["gmf_dim"], seed=7)
+    n_loc = (U - rank + world - 1) // world
+    gen = torch.Generator(device="cuda").manual_seed(99 + rank)
+    batches = []
+    for _ in range(steps):
+        u = torch.randint(0, n_loc, (per // g,), generator=gen, device="cuda", dtype=torch.int32).repeat_interleave(g)
+        it = torch.randint(0, I, (per,), generator=gen, device="cuda", dtype=torch.int32)
+        y = torch.tensor([0.0] * (g - 1) + [1.0], device="cuda").repeat(per // g)
+        batches.append((u.contiguous(), it, y))
+    states = []
+    for native in (True, False):
+        eng = NCFEngine(n_loc, I, cfg["layers"], cfg["gmf_dim"], max_batch=per, lazy_adam=True, lazy_rows=n_loc)
+        eng.set_keras_weights(partition_keras_weights(w, world, rank))
+        dp = UserPartitionedDataParallel(eng, native=native, split_items=split)
+        for s_, (u, it, y) in enumerate(batches):
+            nxt = batches[s_ + 1][:2] if s_ + 1 < steps else None
+            dp.train_step(u, it, y, group=g, k=min(10, g - 1), next_batch=nxt)
+        eng.flush()
+        R = eng.num_rows
+        states.append(torch.cat([eng.emb[:R].flatten(), eng.emb_m[:R].flatten(), eng.emb_v[:R].flatten(), eng.mlp,
+                                 eng.mlp_m, eng.mlp_v, eng.stats.float()]))
+        if dp.comm is not None:
+            dp.comm.close()
+    d = (states[0] - states[1]).abs().max().double().reshape(1)
+    same = torch.tensor([0.0 if torch.equal(states[0], states[1]) else 1.0], dtype=torch.float64, device="cuda")
+    t = torch.cat([d, same])
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    torch.cuda.synchronize()
+    return {"max_abs_diff": float(t[0]), "bitwise": bool(t[1] == 0), "steps": steps, "per_rank_batch": per,
+            "tables": "%d x %d" % (U, I), "ok": float(t[0]) <= 1e-5}
+
+
 def pmc_traffic(kernel, config, batch, mode):
     """HBM bytes per launch of ``kernel`` measured by tools/gpu_profile.sh (separate FETCH_SIZE /
     WRITE_SIZE rocprofv3 passes) for exactly this config, per-GPU batch and layout; None when no
@@ -578,6 +645,7 @@ def main():
     w0 = initial_weights(1 if big else cfg["num_users"], 1 if big else cfg["num_items"], cfg["layers"],
                          cfg["gmf_dim"], seed=0)
     dp = None
+    native_check = None
     if mode == "sharded":
         from movierec.sharded import ShardedNCFEngine
         from movierec.distributed import RowShardedDataParallel
@@ -598,7 +666,11 @@ def main():
                         force_generic=args.generic, precision=prec, lazy_adam=not args.dense_sweep,
                         lazy_rows=n_loc)
         eng.set_keras_weights(partition_keras_weights(w0, ew, rank))
-        dp = UserPartitionedDataParallel(eng, split_items=args.item_optimizer == "split",
+        native = None
+        if world > 1 and dist.get_backend() == "nccl" and not args.dense_sweep:
+            native_check = native_step_check(cfg, world, rank, args.item_optimizer == "split")
+            native = native_check["ok"]
+        dp = UserPartitionedDataParallel(eng, native=native, split_items=args.item_optimizer == "split",
                                          emulate_world=ew if ew > world else None)
         dp.broadcast_parameters()
     else:
@@ -745,13 +817,12 @@ def main():
             nbytes += 2 * B * (4 + 8)   # the launch also counts the next batch: id reads + counter atomics
             # ... and catches the next batch's stale rows up (the rows it touches that this step
             # did not): their p, m, v read and written once more before the next forward pass
-            stale = []
-            for (u0, i0, _), (u1, i1, _) in zip(pool[:16], pool[1:17]):
-                r0 = torch.cat([torch.unique(u0.long()), eng.num_users + torch.unique(i0.long())])
-                r1 = torch.cat([torch.unique(u1.long()), eng.num_users + torch.unique(i1.long())])
-                stale.append(int((~torch.isin(r1, r0)).sum()))
-            replay_rows = float(np.mean(stale)) if stale else 0.0
+            replay_rows = replayed_rows(pool, args.warmup, args.steps, eng.num_users, eng.num_rows, items=True)
             nbytes += 24 * replay_rows * eng.shape.row_width
+        if eng.kernel_for(B) == "fused-mfma-wave" and B >= 16384:
+            # the launch's dense-layer blocks reduce the wave kernel's 256 dense-gradient slabs (both
+            # levels) and step the dense layers: slab reads + p, m, v of every dense parameter
+            nbytes += 256 * eng.mlp_params * 4 + 24 * eng.mlp_params
     elif mode == "user":
         # two launches per step: the own users' scatter-add + Adam over the B user contributions
         # (ncf_update_rows), then Adam over the item rows with the all-reduced dense gradient
@@ -763,9 +834,7 @@ def main():
             # batch's id reads + counter atomics and the replay of its own rows this step missed
             tu = float(np.mean([torch.unique(u).numel() for u, _, _ in pool[:16]]))
             own = 24 * tu * W + cu * W * 4 + cu * 4 + 2 * B * (4 + 8)
-            stale = [int((~torch.isin(torch.unique(u1.long()), torch.unique(u0.long()))).sum())
-                     for (u0, _, _), (u1, _, _) in zip(pool[:16], pool[1:17])]
-            replay_rows = float(np.mean(stale)) if stale else 0.0
+            replay_rows = replayed_rows(pool, args.warmup, args.steps, eng.num_users, Uloc, items=False)
             own += 24 * replay_rows * W
         else:
             own = 24 * Uloc * W + cu * W * 4 + cu * 4 + (Uloc + 1) * 4
@@ -810,7 +879,10 @@ def main():
     hr = {"hr": float(hd[0]) / (ev_users * world), "dcg": float(hd[1]) / (ev_users * world)}
 
     emb_kernel = "k_emb_adam_touched" if getattr(eng, "lazy", False) and mode in ("single", "sharded") else "k_emb_update"
-    traffic = pmc_traffic(emb_kernel, args.config, B, mode)
+    # the update launch's traffic depends on whether it also counts (and catches up) the next batch:
+    # the files are keyed on it (layout "single-ahead" / "single")
+    ahead = getattr(eng, "lazy", False) and sampler is None and mode in ("single", "user", "sharded")
+    traffic = pmc_traffic(emb_kernel, args.config, B, mode + ("-ahead" if ahead else ""))
     kpath = eng.kernel_for(B) if hasattr(eng, "kernel_for") else ("fused-mfma-tile" if eng.fast_path else "generic")
     fb_kernel = {"fused-mfma-tile": "k_fb_fused", "fused-mfma-unit": "k_fb_unit",
                  "fused-mfma-wave": "k_fb_wave"}.get(kpath)
@@ -834,16 +906,33 @@ def main():
         # the step's one collective, timed alone after the timed region (same buffer size, same
         # communicator): how long the all-reduce the step overlaps with its own-user update takes
         buf = dp.shared.clone()
+
+        def collectives():
+            if dp.split and world > 1:
+                # reduce-scatter of the item-row grad, all-reduce of the dense part, all-gather of the rows
+                ig = buf[:dp.grads[0].numel()]
+                part = torch.empty(ig.numel() // world, dtype=buf.dtype, device=buf.device)
+                dist.reduce_scatter_tensor(part, ig)
+                dist.all_reduce(buf[dp.grads[0].numel():])
+                dist.all_gather_into_tensor(ig, part)
+            else:
+                dist.all_reduce(buf)
         for _ in range(3):
-            dist.all_reduce(buf)
+            collectives()
         torch.cuda.synchronize()
         t_ar = time.perf_counter()
         for _ in range(10):
-            dist.all_reduce(buf)
+            collectives()
         torch.cuda.synchronize()
         ar_ms = (time.perf_counter() - t_ar) / 10 * 1e3
         exchange = {"allreduce_bytes_per_step": dp.shared.numel() * dp.shared.element_size(),
-                    "allreduce_ms_standalone": round(ar_ms, 4), "collectives_per_step": 1,
+                    "allreduce_ms_standalone": round(ar_ms, 4),   # the step's collectives, timed alone
+                    "collectives_per_step": 3 if dp.split else 1,
+                    "item_optimizer": ("split: reduce-scatter of the item-row grad + all-reduce of [dense-layer "
+                                       "grad | summary] (one RCCL group), all-gather of the updated item rows"
+                                       if dp.split else "replicated: one all-reduce"),
+                    "native_step": dp.comm is not None,
+                    "native_step_check": native_check,
                     "local_users": eng.num_users}
     elif mode == "sharded":
         W = eng.shape.row_width
@@ -883,7 +972,8 @@ def main():
                 "timed_steps": "every %d-th step of the timed region, one launch group per sampled step "
                                "(HIP events in the dispatch packets): %d launches timed" % (every, nl),
                 "traffic_source": "rocprofv3 --pmc FETCH_SIZE(x2 gfx950) + WRITE_SIZE, profiles/traffic/ "
-                                  "(this config, batch and layout only; null if not measured)"}
+                                  "(this config, batch, layout and counted-ahead form only; null if not "
+                                  "measured)"}
     fb_achieved = fb_flops / (fb_ms * 1e-3) / 1e12
     fb_roof = {"bound": "mfma", "kernel": {
                    "fused-mfma-tile": "fused NeuMF forward+backward, 128-sample tiles (k_fb_fused, fp32 MFMA "
@@ -892,6 +982,9 @@ def main():
                                       "over a workgroup's waves (k_fb_unit, fp32 MFMA 16x16x4)",
                    "fused-mfma-wave": "fused NeuMF forward+backward, 16-sample units, the whole chain in one "
                                       "wave (k_fb_wave, fp32 MFMA 16x16x4)",
+                   "layered-mfma": "layer-by-layer forward+backward, every layer on hand-written fp32 MFMA "
+                                   "(k_lay_l1f gather + layer 1, k_lay_mid layers 2.. + loss + backward to G1, "
+                                   "k_lay_dw1, k_lay_l1b dX + gradient rows)",
                    "layered-rocblas": "layer-by-layer forward+backward (rocBLAS fp32 GEMMs + glue kernels, "
                                       "ncf_layered.hip)"}.get(kpath, "generic forward+backward"),
                "achieved": round(fb_achieved, 2), "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",

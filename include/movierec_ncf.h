@@ -164,6 +164,7 @@ int ncf_abi_version(void);
 #define NCF_FB_TILE 2
 #define NCF_FB_UNIT 3
 #define NCF_FB_WAVE 4
+#define NCF_FB_LAYERED_MFMA 5   /* the layer-by-layer path with every layer on hand-written MFMA (config D) */
 int ncf_fb_kernel(const ncf_shape_t* shape, const ncf_hyper_t* hyper, int64_t n);
 const char* ncf_last_error(void);
 

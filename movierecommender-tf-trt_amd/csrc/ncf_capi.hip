@@ -388,7 +388,8 @@ int ncf_abi_version(void) { return NCF_ABI_VERSION; }
 int ncf_fb_kernel(const ncf_shape_t* s, const ncf_hyper_t* h, int64_t n) {
     if (int r = check_shape(s)) return r;
     if (use_fused(*s, h)) return fb_variant(*s, h, n);
-    return use_layered(*s, h) ? NCF_FB_LAYERED : NCF_FB_GENERIC;
+    if (!use_layered(*s, h)) return NCF_FB_GENERIC;
+    return ncf::layered_all_mfma(*s) ? NCF_FB_LAYERED_MFMA : NCF_FB_LAYERED;
 }
 
 const char* ncf_last_error(void) { return g_err.c_str(); }

@@ -459,6 +459,9 @@ hipError_t launch_fwd_fused(const ncf_shape_t& s, const WsLayout& L, void* ws, c
 // layer-by-layer path (ncf_layered.hip): rocBLAS fp32 GEMMs + HBM-bound glue kernels, same
 // outputs as launch_fb_generic (probs, gs, part_bce, one slab)
 bool layered_supported(const ncf_shape_t& s);
+// every layer of the layered path on hand-written MFMA (k_lay_l1f, k_lay_mid, k_lay_dw1, k_lay_l1b):
+// no vendor GEMM on the step
+bool layered_all_mfma(const ncf_shape_t& s);
 hipError_t launch_fb_layered(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, const float* mlp,
                              const int32_t* users, const int32_t* items, const float* labels, int64_t n,
                              float inv_batch, IdSpace ids, int* nslab, int* nbce, hipStream_t st);
@@ -469,6 +472,9 @@ bool layer1_supported(const ncf_shape_t& s);
 hipError_t launch_layer1_fwd(const ncf_shape_t& s, const float* emb, const float* mlp, const int32_t* users,
                              const int32_t* items, int64_t n, IdSpace ids, float* x0, float* gmf, float* h1,
                              hipStream_t st);
+// dW1 = X0^T G1 per batch chunk of `chunk` samples into slab c (hidden_1 kernel at offset 0), c < nchunks
+hipError_t launch_layer1_dw(const ncf_shape_t& s, const float* x0, const float* g1, int64_t n, int64_t chunk,
+                            int nchunks, float* slabs, hipStream_t st);
 hipError_t launch_layer1_bwd(const ncf_shape_t& s, const float* emb, const float* mlp, const int32_t* users,
                              const int32_t* items, int64_t n, IdSpace ids, const float* dzo, const float* g1,
                              float* gs, hipStream_t st);

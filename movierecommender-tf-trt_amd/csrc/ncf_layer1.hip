@@ -301,6 +301,120 @@ __global__ __launch_bounds__(64 * NW, 1) void k_lay_l1b(const float* __restrict_
 #define NCF_L1B_WAVES 8
 #endif
 
+// dW1 = X0^T G1 over one batch chunk per workgroup (the slab of the k_lay_mid workgroup of the same
+// chunk: slab c already holds its other parameters), on fp32 MFMA: it replaces the strided-batched
+// rocBLAS GEMM (profiles/r03_q2/tl_D.txt: 53.6 us of the 276 us forward/backward).  The L0 x L1
+// result is (L0 / 16) x (L1 / 16) 16 x 16 tiles; wave w owns the X0-feature tiles XT w .. XT w +
+// XT - 1 against every G1-feature tile, accumulated over the chunk's samples in order.  A 16-sample
+// unit of X0 and G1 rows is staged in LDS (rows padded by 4 floats: the four lane groups' rows fall
+// on different banks), double-buffered: the workgroup's float4 loads of unit u + 1 are in flight
+// while unit u's MFMAs run, one barrier per unit.  k-step j of a unit gives lane group lq sample
+// 4 j + lq and lane li feature li of a tile (A = X0[s][16 x + li], B = G1[s][16 y + li]).  Tile
+// element (lane 16 lq + c, register r) is dW1 row 16 x + 4 lq + r (input feature), column 16 y + c
+// (output feature): Keras' [in][out] kernel.
+constexpr int kDw1Waves = 8;
+constexpr int kDw1Split = 2;    // workgroups per chunk (each takes 1 / kDw1Split of the G1 features)
+constexpr int kDw1Depth = 3;    // LDS unit buffers: units u + 1, u + 2 in flight while u computes
+template <int L0, int L1>
+constexpr size_t dw1_lds() {
+    return (size_t)kDw1Depth * (16 * (L0 + 16) + 16 * (L1 / kDw1Split + 16)) * 4;
+}
+template <int L0, int L1>
+__global__ __launch_bounds__(64 * kDw1Waves, 2) void k_lay_dw1(const float* __restrict__ x0,
+                                                             const float* __restrict__ g1, int64_t n, int chunk,
+                                                             float* __restrict__ slabs, int64_t P) {
+    constexpr int LY = L1 / kDw1Split;                      // G1 features of this workgroup
+    constexpr int XT = L0 / 16 / kDw1Waves, YT = LY / 16;
+    constexpr int NT = 64 * kDw1Waves;
+    // LDS row strides (floats): 16 banks apart, so the four lane groups' ds_read_b32 (16
+    // consecutive floats each, rows 4 k + lq) fall on disjoint banks
+    constexpr int SX = L0 + 16, SG = LY + 16;
+    constexpr int BUF = 16 * SX + 16 * SG;                  // one unit's X0 and G1 rows
+    constexpr int QX = 16 * L0 / 4, QG = 16 * LY / 4;       // float4s per unit
+    constexpr int NQ = (QX + QG + NT - 1) / NT;             // float4s per thread per unit
+    static_assert(L0 % (16 * kDw1Waves) == 0 && LY % 16 == 0, "dW1 tiles per wave");
+    extern __shared__ __attribute__((aligned(16))) float lds[];   // [kDw1Depth * BUF]
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, lq = lane >> 4;
+    const int chunk_id = (int)blockIdx.x / kDw1Split, ysplit = (int)blockIdx.x % kDw1Split;
+    const int64_t s0 = (int64_t)chunk_id * chunk;
+    const int64_t s1 = s0 + chunk < n ? s0 + chunk : n;
+    const int nu = (int)((s1 - s0 + 15) / 16);
+    const float* g1y = g1 + LY * ysplit;
+    f32x4 acc[XT][YT];
+#pragma unroll
+    for (int x = 0; x < XT; ++x)
+#pragma unroll
+        for (int y = 0; y < YT; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // thread's float4 q of a unit: q < QX: X0 row q / (L0 / 4), column 4 (q % (L0 / 4)); else G1
+    // the thread's float4s of a unit (q = tid + NT j): X0 row q / (L0 / 4) for q < QX, else G1;
+    // ext-vector registers, filled and drained by macros (no arrays behind references: they would
+    // live in scratch)
+    f32x4 v0[NQ], v1[NQ];
+#define NCF_DW1_FETCH(U, VV)                                                                           \
+    _Pragma("unroll") for (int j = 0; j < NQ; ++j) {                                                   \
+        const int q = (int)threadIdx.x + NT * j;                                                       \
+        const bool isx = q < QX;                                                                       \
+        const int r = isx ? q / (L0 / 4) : (q - QX) / (LY / 4);                                        \
+        const int c = isx ? q % (L0 / 4) : (q - QX) % (LY / 4);                                        \
+        const int64_t s = s0 + 16 * (int64_t)(U) + r;                                                  \
+        const bool ok = (U) < nu && s < s1 && q < QX + QG;                                             \
+        const f32x4* src = isx ? reinterpret_cast<const f32x4*>(x0 + s * L0) + c                       \
+                               : reinterpret_cast<const f32x4*>(g1y + s * L1) + c;                     \
+        VV[j] = ok ? *src : f32x4{0.f, 0.f, 0.f, 0.f};                                                 \
+    }
+#define NCF_DW1_STASH(VV, B)                                                                           \
+    _Pragma("unroll") for (int j = 0; j < NQ; ++j) {                                                   \
+        const int q = (int)threadIdx.x + NT * j;                                                       \
+        const bool isx = q < QX;                                                                       \
+        const int r = isx ? q / (L0 / 4) : (q - QX) / (LY / 4);                                        \
+        const int c = isx ? q % (L0 / 4) : (q - QX) % (LY / 4);                                        \
+        float* dst = isx ? (B) + r * SX + 4 * c : (B) + 16 * SX + r * SG + 4 * c;                      \
+        if (q < QX + QG) *reinterpret_cast<f32x4*>(dst) = VV[j];                                       \
+    }
+    // prologue: units 0 and 1 staged, unit 2 in registers
+    NCF_DW1_FETCH(0, v0);
+    NCF_DW1_FETCH(1, v1);
+    NCF_DW1_STASH(v0, lds);
+    NCF_DW1_STASH(v1, lds + BUF);
+    NCF_DW1_FETCH(2, v0);
+    // one unit (a macro, not a lambda: the accumulators must stay in registers): unit u + 3's loads
+    // go out into NXT (in flight under units u and u + 1), unit u's MFMAs, then unit u + 2 (held in
+    // CUR since the previous unit) into the buffer unit u - 1 used
+#define NCF_DW1_UNIT(U, CUR, NXT)                                                                      \
+    {                                                                                                  \
+        const int u_ = (U);                                                                            \
+        NCF_DW1_FETCH(u_ + 3, NXT);                                                                    \
+        __syncthreads();                                                                               \
+        const float* base = lds + (u_ % kDw1Depth) * BUF;                                              \
+        const float* bx = base + 16 * XT * wv + li;                                                    \
+        const float* bg = base + 16 * SX + li;                                                         \
+        _Pragma("unroll") for (int k = 0; k < 4; ++k) {                                                \
+            const int row = 4 * k + lq;                                                                \
+            float a[XT], b[YT];                                                                        \
+            _Pragma("unroll") for (int x = 0; x < XT; ++x) a[x] = bx[row * SX + 16 * x];               \
+            _Pragma("unroll") for (int y = 0; y < YT; ++y) b[y] = bg[row * SG + 16 * y];               \
+            _Pragma("unroll") for (int x = 0; x < XT; ++x)                                             \
+            _Pragma("unroll") for (int y = 0; y < YT; ++y) acc[x][y] = mfma16(a[x], b[y], acc[x][y]);  \
+        }                                                                                              \
+        if (u_ + 2 < nu) { NCF_DW1_STASH(CUR, lds + ((u_ + 2) % kDw1Depth) * BUF); }                  \
+    }
+    for (int u = 0; u < nu; u += 2) {   // two units per trip: the register sets alternate statically
+        NCF_DW1_UNIT(u, v0, v1);
+        if (u + 1 < nu) NCF_DW1_UNIT(u + 1, v1, v0);
+    }
+#undef NCF_DW1_UNIT
+#undef NCF_DW1_FETCH
+#undef NCF_DW1_STASH
+    float* slab = slabs + (int64_t)chunk_id * P + LY * ysplit;
+#pragma unroll
+    for (int x = 0; x < XT; ++x)
+#pragma unroll
+        for (int y = 0; y < YT; ++y)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                slab[(int64_t)(16 * (XT * wv + x) + 4 * lq + r) * L1 + 16 * y + li] = acc[x][y][r];
+}
+
 using L1ShapeD = L1Shape<256, 128, 128>;  // config D
 
 template <class S>
@@ -348,6 +462,22 @@ hipError_t launch_layer1_fwd(const ncf_shape_t& s, const float* emb, const float
     else
         launch(k_lay_l1f<S, NCF_L1F_WAVES, false>, grid_of<S, NCF_L1F_WAVES>(n), 64 * NCF_L1F_WAVES, S::LDS, st, emb,
                mlp, users, items, n, ids, x0, gmf, h1);
+    return hipGetLastError();
+}
+
+hipError_t launch_layer1_dw(const ncf_shape_t& s, const float* x0, const float* g1, int64_t n, int64_t chunk,
+                            int nchunks, float* slabs, hipStream_t st) {
+    using S = L1ShapeD;
+    if (!l1matches<S>(s) || chunk <= 0 || nchunks <= 0) return hipErrorInvalidValue;
+    static bool cfg = false;
+    if (!cfg) {
+        if (hipError_t e = hipFuncSetAttribute((const void*)k_lay_dw1<S::L0, S::L1>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)dw1_lds<S::L0, S::L1>()))
+            return e;
+        cfg = true;
+    }
+    launch(k_lay_dw1<S::L0, S::L1>, nchunks * kDw1Split, 64 * kDw1Waves, dw1_lds<S::L0, S::L1>(), st, x0, g1, n,
+           (int)chunk, slabs, (int64_t)s.mlp_params);
     return hipGetLastError();
 }
 

@@ -21,6 +21,7 @@
 // [batch x width] matrix per layer.
 
 #include <cmath>
+#include <cstdlib>
 
 #include <rocblas/rocblas.h>
 
@@ -315,6 +316,19 @@ hipError_t launch_predict_layered(const ncf_shape_t& s, const WsLayout& L, void*
 
 constexpr int kLayeredSlabs = 64;  // batch chunks of the weight-gradient GEMMs (<= kMaxSlabs)
 
+// NCF_DW1_MFMA=0 keeps the rocBLAS dW1 GEMM of the middle-kernel path (A/B)
+bool dw1_mfma() {
+    static const int on = [] {
+        const char* e = getenv("NCF_DW1_MFMA");
+        return e && *e ? atoi(e) : 1;
+    }();
+    return on != 0;
+}
+
+bool layered_all_mfma(const ncf_shape_t& s) {
+    return layer1_supported(s) && laymid_supported(s) && dw1_mfma();
+}
+
 
 hipError_t launch_fb_layered(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, const float* mlp,
                              const int32_t* users, const int32_t* items, const float* labels, int64_t n,
@@ -375,14 +389,18 @@ hipError_t launch_fb_layered(const ncf_shape_t& s, const WsLayout& L, void* ws, 
         const int lin = s.layers[0], lout = s.layers[1];
         const int64_t P = s.mlp_params;
         float* dW1 = slab + s.layer_off[1];
-        if (nfull > 0) {
+        if (dw1_mfma()) {
+            // dW1 on hand-written MFMA (ncf_layer1.hip), one workgroup per chunk
+            e = launch_layer1_dw(s, X[0], Gd[1], n, chunk, nsl, slab, st);
+            if (e != hipSuccess) return e;
+        } else if (nfull > 0) {
             e = blas_err(rocblas_sgemm_strided_batched(
                 bh, rocblas_operation_none, rocblas_operation_transpose, lout, lin, (int)chunk, &one, Gd[1], lout,
                 (rocblas_stride)chunk * lout, X[0], lin, (rocblas_stride)chunk * lin, &zero, dW1, lout, (rocblas_stride)P,
                 nfull));
             if (e != hipSuccess) return e;
         }
-        if (rem > 0) {
+        if (rem > 0 && !dw1_mfma()) {
             e = blas_err(rocblas_sgemm(bh, rocblas_operation_none, rocblas_operation_transpose, lout, lin, rem, &one,
                                        Gd[1] + (int64_t)nfull * chunk * lout, lout, X[0] + (int64_t)nfull * chunk * lin,
                                        lin, &zero, dW1 + (int64_t)nfull * P, lout));

@@ -266,6 +266,15 @@ __device__ unsigned long long g_wave_s[256 * 4 * 16];
 #ifndef NCF_SPLIT_LATE
 #define NCF_SPLIT_LATE 0
 #endif
+// 1: the split form's weight-gradient wave also computes dX = W1 G1 and writes the gradient rows'
+// MLP parts (from the transposed G1 the chain wave hands over anyway), taking 128 MFMAs per unit
+// off the chain; 0 (the default): the chain wave computes dX.  Measured at config C (round 4,
+// profiles/r04_i/ab, same session): 58.6 us with 1 against 54.4-54.9 us with 0 — the two waves of a
+// SIMD share its issue (MI355X_MICROARCH.md "Two waves per SIMD"), and the partner wave then needs
+// more than the 256 registers two waves per SIMD leave it (a few spills)
+#ifndef NCF_SPLIT_DX
+#define NCF_SPLIT_DX 0
+#endif
 template <class S, int FOLD, bool MET, bool SPLIT = false>
 __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* __restrict__ emb, const float* __restrict__ mlp,
                                                      const int32_t* __restrict__ users,
@@ -474,6 +483,57 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
         }
     };
 
+    const int fm = FOLD > 1 ? FOLD - 1 : 0;
+    // stores through buffer resources: a lane whose sample is past n (or whose user row is folded
+    // into its group head) gets an offset past the buffer (kDrop) and the hardware drops the
+    // store, so the unit body has no branches and the scheduler sees it as one block
+    const __amdgpu_buffer_rsrc_t gs_rsrc =
+        __builtin_amdgcn_make_buffer_rsrc(gs, (short)0, (int)(uint32_t)(2 * n * W * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t pr_rsrc = __builtin_amdgcn_make_buffer_rsrc(probs, (short)0, (int)(uint32_t)(n * 4), 0x00020000);
+    auto st4 = [&](uint32_t off, float a, float b, float c, float d) {
+        const f32x4 v = {a, b, c, d};
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), gs_rsrc, off, 0, 0);
+    };
+    // dX = W1 G1 of one 16-sample unit into the gradient rows' MLP parts: block ti holds input
+    // features 16 ti + 4 lq .. + 3 of sample li (user half folded into the group head like the
+    // GMF part); two blocks' chains interleaved, k-step (t, r) takes G1 feature 16 t + 4 lq + r
+    auto dx_rows = [&](const float (&g1)[B1][4], uint32_t urow_off, uint32_t irow_off, bool fmatch, bool fhead) {
+#pragma unroll
+        for (int tp = 0; tp < B0 / 2; ++tp) {
+            f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+            pipe<4, 2, Ops2<2, B1>>(
+                [&](int r, Ops2<2, B1>& o) {
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        ldsv<B1>(wl + S::SW1 + (16 * (2 * tp + j) + li) * S::S1 + (4 * g + r) * B1, o.v[j]);
+                },
+                [&](int r, const Ops2<2, B1>& o) {
+#pragma unroll
+                    for (int t = 0; t < B1; ++t)
+#pragma unroll
+                        for (int j = 0; j < 2; ++j) acc[j] = mfma16(o.v[j][t], g1[t][r], acc[j]);
+                });
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int ti = 2 * tp + j;
+                const int f0 = 16 * ti + 4 * g;
+                const bool user = 16 * ti < D0;  // compile time: D0 is a multiple of 16
+                f32x4 d = acc[j];
+                if constexpr (FOLD > 1) {
+                    if (user) {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const float sm = fold_sum<FOLD>(fmatch ? d[r] : 0.f);
+                            d[r] = fhead ? sm : d[r];
+                        }
+                    }
+                }
+                const uint32_t base = user ? urow_off : irow_off;
+                st4(base == kDrop ? kDrop : base + (G + (user ? f0 : f0 - D0)) * 4, d[0], d[1], d[2], d[3]);
+            }
+        }
+    };
+
     if constexpr (SPLIT) {
         if (dwave) {
             // ---- the weight-gradient wave of pair pw
@@ -568,12 +628,74 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
             } else {
                 for (int64_t it = 0; it < nit; ++it, un += ustride) {
                     const bool have = un < nunits;
+                    int xu = 0;
                     if (have) {  // in flight while the chain finishes the unit
                         load_xq(un, 0);
                         load_xq(un, 1);
+                        if constexpr (NCF_SPLIT_DX) {
+                            // sample li's user id: the dX rows' offsets and folding
+                            const int64_t si = un * 16 + li;
+                            xu = (int)__builtin_amdgcn_raw_buffer_load_b32(us_rsrc, si < n ? (uint32_t)si * 4u : kDrop,
+                                                                          0, 0);
+                        }
                     }
                     if (!NCF_SPLIT_NOSYNC) __syncthreads();  // barrier it: chain wave pw wrote unit it's buffers
-                    if (have && !NCF_SPLIT_NODW) contract(un, (int)(it & 1));
+                    if (have && !NCF_SPLIT_NODW) {
+                        // the contraction first: its X operands (loaded before the barrier) are dead
+                        // once it is done, which leaves dX the registers its chains need
+                        contract(un, (int)(it & 1));
+                        if constexpr (NCF_SPLIT_DX) {
+                            // the chain's G1 (transposed buffer row li: feature 16 t + 4 lq + r at
+                            // position (4 lq + r) B1 + t), read with each k-step's W1 operands (the
+                            // 168 accumulators leave no room to hold all of it), and the row offsets
+                            // the chain uses
+                            const float* tq = tbuf((int)(it & 1));
+                            const int64_t sg = un * 16 + li;
+                            const bool inb = sg < n;
+                            const int su = inb ? xu : -1;
+                            const bool fmatch = FOLD > 1 && inb && su == grp_bcast<(FOLD > 1 ? FOLD : 2)>(su, 0, lane);
+                            const bool fhead = (li & fm) == 0;
+                            const uint32_t urow_off = inb && (fhead || !fmatch) ? (uint32_t)(2 * sg * W) * 4u : kDrop;
+                            const uint32_t irow_off = inb ? (uint32_t)((2 * sg + 1) * W) * 4u : kDrop;
+#pragma unroll
+                            for (int tp = 0; tp < B0 / 2; ++tp) {
+                                f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+                                pipe<4, 2, Ops2<3, B1>>(
+                                    [&](int r, Ops2<3, B1>& o) {
+#pragma unroll
+                                        for (int j = 0; j < 2; ++j)
+                                            ldsv<B1>(wl + S::SW1 + (16 * (2 * tp + j) + li) * S::S1 + (4 * g + r) * B1,
+                                                     o.v[j]);
+                                        ldsv<B1>(tq + S::TG1 + li * T1 + (4 * g + r) * B1, o.v[2]);
+                                    },
+                                    [&](int r, const Ops2<3, B1>& o) {
+#pragma unroll
+                                        for (int t = 0; t < B1; ++t)
+#pragma unroll
+                                            for (int j = 0; j < 2; ++j) acc[j] = mfma16(o.v[j][t], o.v[2][t], acc[j]);
+                                    });
+#pragma unroll
+                                for (int j = 0; j < 2; ++j) {
+                                    const int ti = 2 * tp + j;
+                                    const int f0 = 16 * ti + 4 * g;
+                                    const bool user = 16 * ti < D0;
+                                    f32x4 d = acc[j];
+                                    if constexpr (FOLD > 1) {
+                                        if (user) {
+#pragma unroll
+                                            for (int r = 0; r < 4; ++r) {
+                                                const float sm = fold_sum<FOLD>(fmatch ? d[r] : 0.f);
+                                                d[r] = fhead ? sm : d[r];
+                                            }
+                                        }
+                                    }
+                                    const uint32_t base = user ? urow_off : irow_off;
+                                    st4(base == kDrop ? kDrop : base + (G + (user ? f0 : f0 - D0)) * 4, d[0], d[1], d[2],
+                                        d[3]);
+                                }
+                            }
+                        }
+                    }
                 }
             }
 #pragma unroll
@@ -646,17 +768,6 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
     for (int e = 0; e < GQA; ++e) agmf[e] = 0.f;
     float acc_bce = 0.f, acc_dbo = 0.f, acc_hit = 0.f, acc_dcg = 0.f;
 
-    const int fm = FOLD > 1 ? FOLD - 1 : 0;
-    // stores through buffer resources: a lane whose sample is past n (or whose user row is folded
-    // into its group head) gets an offset past the buffer (kDrop) and the hardware drops the
-    // store, so the unit body has no branches and the scheduler sees it as one block
-    const __amdgpu_buffer_rsrc_t gs_rsrc =
-        __builtin_amdgcn_make_buffer_rsrc(gs, (short)0, (int)(uint32_t)(2 * n * W * 4), 0x00020000);
-    const __amdgpu_buffer_rsrc_t pr_rsrc = __builtin_amdgcn_make_buffer_rsrc(probs, (short)0, (int)(uint32_t)(n * 4), 0x00020000);
-    auto st4 = [&](uint32_t off, float a, float b, float c, float d) {
-        const f32x4 v = {a, b, c, d};
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), gs_rsrc, off, 0, 0);
-    };
     NCF_WT(0, 8);
 #if NCF_SPLIT_PRIO
     if constexpr (SPLIT) __builtin_amdgcn_s_setprio(1);  // the chain wave's serial sections first
@@ -951,43 +1062,8 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
         }
 
         NCF_WT(itw, 5);
-        // ---- dX = W1 G1 -> the per-sample gradient rows: block ti holds input features
-        // 16 ti + 4 lq .. + 3 of sample li (user half folded like the GMF part); two blocks'
-        // chains interleaved, k-step (t, r) takes G1 feature 16 t + 4 lq + r
-#pragma unroll
-        for (int tp = 0; tp < B0 / 2; ++tp) {
-            f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-            pipe<4, 2, Ops2<2, B1>>(
-                [&](int r, Ops2<2, B1>& o) {
-#pragma unroll
-                    for (int j = 0; j < 2; ++j)
-                        ldsv<B1>(wl + S::SW1 + (16 * (2 * tp + j) + li) * S::S1 + (4 * g + r) * B1, o.v[j]);
-                },
-                [&](int r, const Ops2<2, B1>& o) {
-#pragma unroll
-                    for (int t = 0; t < B1; ++t)
-#pragma unroll
-                        for (int j = 0; j < 2; ++j) acc[j] = mfma16(o.v[j][t], g1[t][r], acc[j]);
-                });
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int ti = 2 * tp + j;
-                const int f0 = 16 * ti + 4 * g;
-                const bool user = 16 * ti < D0;  // compile time: D0 is a multiple of 16
-                f32x4 d = acc[j];
-                if constexpr (FOLD > 1) {
-                    if (user) {
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            const float sm = fold_sum<FOLD>(fmatch ? d[r] : 0.f);
-                            d[r] = fhead ? sm : d[r];
-                        }
-                    }
-                }
-                const uint32_t base = user ? urow_off : irow_off;
-                st4(base == kDrop ? kDrop : base + (G + (user ? f0 : f0 - D0)) * 4, d[0], d[1], d[2], d[3]);
-            }
-        }
+        // ---- dX = W1 G1 -> the per-sample gradient rows (split form: the weight-gradient wave's)
+        if constexpr (!SPLIT || !NCF_SPLIT_DX || NCF_SPLIT_LATE) dx_rows(g1, urow_off, irow_off, fmatch, fhead);
 
         // ---- weight gradients over the unit's 16 samples: k-step q takes sample 4 q + lq
         NCF_WT(itw, 6);

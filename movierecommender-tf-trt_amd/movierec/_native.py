@@ -24,7 +24,8 @@ NCF_NUM_STATS = 8
 NCF_NUM_SUMMARY = 8
 NCF_WSERR_ID_RANGE, NCF_WSERR_STALE_COUNT, NCF_WSERR_FOLD = 1, 4, 8
 NCF_ROW_PRISTINE = 0x7fffffff   # row_step mark of a row whose Adam moments are exactly +0
-FB_KERNELS = {0: "generic", 1: "layered-rocblas", 2: "fused-mfma-tile", 3: "fused-mfma-unit", 4: "fused-mfma-wave"}
+FB_KERNELS = {0: "generic", 1: "layered-rocblas", 2: "fused-mfma-tile", 3: "fused-mfma-unit", 4: "fused-mfma-wave",
+              5: "layered-mfma"}
 SUM_BCE, SUM_HIT, SUM_DCG, SUM_GROUPS, SUM_REG = range(5)
 STAT_LOSS_SUM, STAT_HR_SUM, STAT_DCG_SUM, STAT_STEPS, STAT_LAST_LOSS, STAT_LAST_HR, STAT_LAST_DCG, STAT_BCE_SUM = \
     range(8)

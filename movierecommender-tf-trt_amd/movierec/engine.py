@@ -143,7 +143,8 @@ class NCFEngine(object):
 
     def kernel_for(self, n):
         """Forward/backward kernel a training call with n samples runs (ncf_fb_kernel):
-        "fused-mfma-unit", "fused-mfma-wave", "fused-mfma-tile", "layered-rocblas" or "generic"."""
+        "fused-mfma-unit", "fused-mfma-wave", "fused-mfma-tile", "layered-mfma" (every layer hand-written MFMA),
+        "layered-rocblas" (some layers on rocBLAS) or "generic"."""
         k = N.check_value(N.lib().ncf_fb_kernel(ctypes.byref(self.shape), ctypes.byref(self.hyper), int(n)))
         return N.FB_KERNELS[k]
 

@@ -44,4 +44,7 @@ def run(ahead, B=65536, steps=30):
 
 
 if __name__ == "__main__":
-    print(json.dumps({"ahead": run(True), "not_ahead": run(False)}))
+    # argv[1] (optional): "ahead" / "not_ahead" runs one mode only (a PMC pass per mode:
+    # tools/pmc_update_roles.sh)
+    modes = sys.argv[1:] or ["ahead", "not_ahead"]
+    print(json.dumps({m: run(m == "ahead") for m in modes}))
