@@ -975,6 +975,8 @@ def main():
                                   "(this config, batch, layout and counted-ahead form only; null if not "
                                   "measured)"}
     fb_achieved = fb_flops / (fb_ms * 1e-3) / 1e12
+    # the MLP tower's matrix products run on bf16 MFMA in the bf16 mode (config B): its dense peak
+    fb_peak = FP16_MFMA_PEAK_TFS if prec == "bf16" else FP32_MFMA_PEAK_TFS
     fb_roof = {"bound": "mfma", "kernel": {
                    "fused-mfma-tile": "fused NeuMF forward+backward, 128-sample tiles (k_fb_fused, fp32 MFMA "
                                       "32x32x2)",
@@ -987,8 +989,10 @@ def main():
                                    "k_lay_dw1, k_lay_l1b dX + gradient rows)",
                    "layered-rocblas": "layer-by-layer forward+backward (rocBLAS fp32 GEMMs + glue kernels, "
                                       "ncf_layered.hip)"}.get(kpath, "generic forward+backward"),
-               "achieved": round(fb_achieved, 2), "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
-               "frac": round(fb_achieved / FP32_MFMA_PEAK_TFS, 4), "traffic": fb_traffic,
+               "achieved": round(fb_achieved, 2), "peak": fb_peak, "unit": "TFLOP/s",
+               "frac": round(fb_achieved / fb_peak, 4), "traffic": fb_traffic,
+               "peak_of": "bf16 dense MFMA (the MLP products; GMF, loss and Adam stay fp32)" if prec == "bf16"
+                          else "fp32 dense MFMA",
                "traffic_unit": "HBM bytes per launch",
                "algorithmic_flops_per_launch": fb_flops, "avg_launch_ms": round(fb_ms, 5),
                "hbm_GBs": round(fb_bytes / (fb_ms * 1e-3) / 1e9, 1), "algorithmic_bytes_per_launch": fb_bytes}
