@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define NCF_ABI_VERSION 7
+#define NCF_ABI_VERSION 8
 #define NCF_MAX_LAYERS 8
 #define NCF_EINVAL (-1)
 #define NCF_EHIP (-2)
