@@ -193,6 +193,19 @@ def fwd_bwd_flops(cfg):
     return 2 * (fwd + bwd_data + dw)
 
 
+def fwd_bwd_executed_flops(cfg, batch, group, kpath):
+    """MFMA-issued flops per launch when they differ from the algorithmic count: the wave kernel's
+    group-user form (split form with user-row folding) runs the user half of layer 1,
+    of dX and of dW1 once per group of F = group samples, i.e. 3 x 2 x (L0 / 2) x L1 flops per
+    sample fewer by a factor F.  None when the kernel does the per-sample work."""
+    L = cfg["layers"]
+    if (kpath != "fused-mfma-wave" or group not in (2, 4, 8) or os.environ.get("NCF_WAVE_SPLIT", "1") == "0"
+            or os.environ.get("NCF_FOLD_USERS", "1") == "0"):
+        return None
+    user_half = 3 * 2 * (L[0] // 2) * L[1]
+    return fwd_bwd_flops(cfg) * batch - user_half * batch * (group - 1) // group
+
+
 def fwd_bwd_bytes(shape, batch, contribs=None):
     """Algorithmic HBM bytes of the fused kernel: ids+label (12 B), both gathered rows
     (2W floats), the per-sample gradient rows written (``contribs`` rows of W floats, default
@@ -975,6 +988,7 @@ def main():
                                   "(this config, batch, layout and counted-ahead form only; null if not "
                                   "measured)"}
     fb_achieved = fb_flops / (fb_ms * 1e-3) / 1e12
+    fb_exec = fwd_bwd_executed_flops(cfg, B, g, kpath)
     # the MLP tower's matrix products run on bf16 MFMA in the bf16 mode (config B): its dense peak
     fb_peak = FP16_MFMA_PEAK_TFS if prec == "bf16" else FP32_MFMA_PEAK_TFS
     fb_roof = {"bound": "mfma", "kernel": {
@@ -995,6 +1009,8 @@ def main():
                           else "fp32 dense MFMA",
                "traffic_unit": "HBM bytes per launch",
                "algorithmic_flops_per_launch": fb_flops, "avg_launch_ms": round(fb_ms, 5),
+               "executed_flops_per_launch": fb_exec,
+               "executed_TFLOPs": round(fb_exec / (fb_ms * 1e-3) / 1e12, 2) if fb_exec else None,
                "hbm_GBs": round(fb_bytes / (fb_ms * 1e-3) / 1e9, 1), "algorithmic_bytes_per_launch": fb_bytes}
     # `roofline` = the step's dominant kernel (longest average time per step)
     fb_per_step = fb_ms * nfb / steps_of(N.K_FWD_BWD)

@@ -34,6 +34,7 @@
 
 #include <cmath>
 #include <cstdlib>
+#include <type_traits>
 
 #include "ncf_common.h"
 #include "ncf_internal.h"
@@ -275,6 +276,22 @@ __device__ unsigned long long g_wave_s[256 * 4 * 16];
 #ifndef NCF_SPLIT_DX
 #define NCF_SPLIT_DX 0
 #endif
+// timing diagnostic (wrong results): 1 = the chain runs layer 1 and dX over half of the MLP input
+// (the MFMAs a per-group user half would leave per unit)
+// 1 (the default): with user-row folding (FOLD 2, 4, 8) the split form's chain computes the user
+// half of layer 1 and of dX once per group instead of once per sample (see k_fb_wave)
+#ifndef NCF_GROUP_USER
+#define NCF_GROUP_USER 1
+#endif
+#if NCF_GROUP_USER && NCF_SPLIT_LATE
+#error "the late contraction is not written for the group-user form: build it with NCF_GROUP_USER=0"
+#endif
+#if NCF_GROUP_USER && NCF_SPLIT_DX
+#error "NCF_SPLIT_DX computes dX per sample on the weight-gradient wave: build it with NCF_GROUP_USER=0"
+#endif
+#ifndef NCF_DIAG_HALFL1
+#define NCF_DIAG_HALFL1 0
+#endif
 template <class S, int FOLD, bool MET, bool SPLIT = false>
 __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* __restrict__ emb, const float* __restrict__ mlp,
                                                      const int32_t* __restrict__ users,
@@ -284,9 +301,26 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
                                                      float* __restrict__ gs, float* __restrict__ slabs,
                                                      float* __restrict__ part_bce, int group, int topk,
                                                      float* __restrict__ part_hit, float* __restrict__ part_dcg,
-                                                     const int32_t* __restrict__ ifold, int32_t* __restrict__ ferr) {
+                                                     const int32_t* __restrict__ ifold, int32_t* __restrict__ ferr,
+                                                     float* __restrict__ gpart) {
     constexpr int L0 = S::L0, L1 = S::L1, L2 = S::L2, L3 = S::L3, G = S::G, D0 = S::D0, W = S::W;
     constexpr int B0 = S::B0, B1 = S::B1, B2 = S::B2, XQ = S::XQ, GQ = S::GQ, GQA = GQ > 0 ? GQ : 1;
+    // Group-user form (GU: split form, FOLD > 1).  The reference's batches are groups of FOLD
+    // samples sharing one user (data_pipeline.py:141), and layer 1 is linear in the user half of
+    // its input: W1^T [x_u; x_i] = W1_u^T x_u + W1_i^T x_i, and the folded user row's dX is
+    // sum_s W1_u g1_s = W1_u (sum_s g1_s).  So the chain computes P_u = W1_u^T x_u once per group
+    // (16 groups, one MFMA tile, per FOLD units: phase 0) into gpart, starts each sample's layer-1
+    // accumulators from its group's P_u and runs only the item half per unit, writes each group's
+    // sum of G1 over the samples that share the head's user to gpart, and after its units computes
+    // W1_u (sum g1) for 16 groups per tile (phase N) into the head samples' user rows.  Per 16-sample
+    // unit that is 2 x 64 MFMAs less on the chain at config C, for 2 x 64 per FOLD units.  A sample
+    // whose user differs from its group head's (any batch is accepted) takes its own user half in a
+    // per-unit branch that only such units enter.  Same sums, reassociated: within fp32 rounding of
+    // the per-sample form, checked against the oracle like it.
+    constexpr bool GU = SPLIT && FOLD > 1 && NCF_GROUP_USER;
+    constexpr int XH = XQ / 2;                // per lane: D0 / 4 features of one half of the input
+    constexpr int XN = GU ? XH : XQ;          // MLP-input floats per lane in the unit loop
+    constexpr int NGU = FOLD > 1 ? 16 / FOLD : 16;  // groups per unit
     constexpr int T0 = S::ts(B0), T1 = S::ts(B1), T2 = S::ts(B2);
     NCF_WS(0, __builtin_amdgcn_s_memrealtime());
     NCF_WS(1, __builtin_readcyclecounter());
@@ -332,15 +366,44 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
         urow = okr ? cu : 0;
         irow = okr ? ids.ibase + cv : 0;
     };
-    float xr[XQ], gu[GQA], gi[GQA];
+    constexpr uint32_t kDrop = 0x80000000u;
+    constexpr unsigned kVmcnt0 = 0x0F70;  // s_waitcnt vmcnt(0), expcnt / lgkmcnt unconstrained
+    float xr[XN], gu[GQA], gi[GQA];
+    // GU: gpart = P_u [n / FOLD][L1] (rows 16 t + 4 lq .. + 3 of a group at 16 t + 4 lq), then the
+    // groups' G1 sums [n / FOLD][L1] at gpart + (n / 2) L1
+    const int64_t ngrp = FOLD > 1 ? n / (FOLD > 1 ? FOLD : 1) : 0;
+    const __amdgpu_buffer_rsrc_t pu_rsrc =
+        __builtin_amdgcn_make_buffer_rsrc(gpart, (short)0, (int)(uint32_t)(ngrp * L1 * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t sgr_rsrc =
+        __builtin_amdgcn_make_buffer_rsrc(gpart + (n / 2) * L1, (short)0, (int)(uint32_t)(ngrp * L1 * 4), 0x00020000);
+    f32x4 pun[B1];  // GU: the unit's layer-1 accumulators as its groups' P_u left them
+    auto load_pu = [&](int64_t u) {
+        if constexpr (GU) {
+            const int64_t si = u * 16 + li;
+            const uint32_t off = si < n ? (uint32_t)(((si / FOLD) * L1 + 4 * g) * 4) : kDrop;
+#pragma unroll
+            for (int t = 0; t < B1; ++t)
+                pun[t] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(pu_rsrc, off + 64u * t, 0, 0));
+        }
+    };
     auto load_x = [&](int64_t u, int cu, int cv) {
         int urow, irow;
         rows_of(u, cu, cv, urow, irow);
-        const float4* xs = reinterpret_cast<const float4*>(emb + (size_t)(g < 2 ? urow : irow) * W + G + (g & 1) * XQ);
+        if constexpr (GU) {
+            // the item half only: lane group lq holds item features XH lq .. + XH - 1
+            const float4* xs = reinterpret_cast<const float4*>(emb + (size_t)irow * W + G + g * XH);
 #pragma unroll
-        for (int k = 0; k < XQ / 4; ++k) {
-            const float4 v = xs[k];
-            xr[4 * k] = v.x, xr[4 * k + 1] = v.y, xr[4 * k + 2] = v.z, xr[4 * k + 3] = v.w;
+            for (int k = 0; k < XH / 4; ++k) {
+                const float4 v = xs[k];
+                xr[4 * k] = v.x, xr[4 * k + 1] = v.y, xr[4 * k + 2] = v.z, xr[4 * k + 3] = v.w;
+            }
+        } else {
+            const float4* xs = reinterpret_cast<const float4*>(emb + (size_t)(g < 2 ? urow : irow) * W + G + (g & 1) * XQ);
+#pragma unroll
+            for (int k = 0; k < XQ / 4; ++k) {
+                const float4 v = xs[k];
+                xr[4 * k] = v.x, xr[4 * k + 1] = v.y, xr[4 * k + 2] = v.z, xr[4 * k + 3] = v.w;
+            }
         }
     };
     auto load_g = [&](int64_t u, int cu, int cv) {
@@ -365,7 +428,6 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
     };
     int cu, cv, nu, nv;
     float cy, ny;
-    constexpr uint32_t kDrop = 0x80000000u;
 
     // Prologue.  The first unit's ids, then every dense parameter (one b128 buffer load per 4
     // floats, all issued before any is used), are in flight while the operand layout's padding is
@@ -377,8 +439,33 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
         __builtin_amdgcn_make_buffer_rsrc((void*)mlp, (short)0, (int)(S::P * 4), 0x00020000);
     f32x4 pv[NVT];
     float pbo = 0.f;
+    // GU: phase-0 tile tau's column li is group li % NGU of the wave's unit tau FOLD + li / NGU
+    const int64_t un0 = un;
+    const int64_t nown = un0 < nunits ? (nunits - un0 + ustride - 1) / ustride : 0;
+    auto tile_head = [&](int64_t tau, int64_t& hs) {
+        const int64_t k = tau * FOLD + li / NGU;
+        hs = (un0 + k * ustride) * 16 + (li % NGU) * FOLD;
+        return k < nown && hs < n;
+    };
+    float xu[GU ? XH : 1];
+    auto load_xu = [&](int hu, bool hv) {  // the head's user half: features XH lq .. + XH - 1
+        const int row = hv && (unsigned)hu < (unsigned)ids.ubound ? hu : 0;
+        const float4* xs = reinterpret_cast<const float4*>(emb + (size_t)row * W + G + g * XH);
+#pragma unroll
+        for (int k = 0; k < (GU ? XH / 4 : 0); ++k) {
+            const float4 v = xs[k];
+            xu[4 * k] = v.x, xu[4 * k + 1] = v.y, xu[4 * k + 2] = v.z, xu[4 * k + 3] = v.w;
+        }
+    };
+    int64_t hs0 = 0;
+    bool hv0 = false;
+    int hu0 = 0;
     if (!dwave) {
         load_ids(un, cu, cv, cy);
+        if constexpr (GU) {
+            hv0 = tile_head(0, hs0);
+            hu0 = (int)__builtin_amdgcn_raw_buffer_load_b32(us_rsrc, hv0 ? (uint32_t)hs0 * 4u : kDrop, 0, 0);
+        }
 #pragma unroll
         for (int j = 0; j < NVT; ++j) {
             const int q = (int)threadIdx.x + 256 * j;
@@ -390,6 +477,7 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
     __syncthreads();
     if (!dwave) {
         load_x(un, cu, cv);
+        if constexpr (GU) load_xu(hu0, hv0);
         load_ids(un + ustride, nu, nv, ny);
     }
     // float4 group at flat offset e0 -> its LDS operand-layout positions
@@ -425,6 +513,39 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
     }
     __syncthreads();
     NCF_WS(2, __builtin_readcyclecounter());
+    // GU phase 0: P_u = W1_u^T x_u of every group of this chain wave's units, one 16-group tile per
+    // FOLD units (k-step q takes user feature XH lq + q), into gpart
+    if constexpr (GU) {
+        if (!dwave) {
+            const int64_t ntile = (nown + FOLD - 1) / FOLD;
+            for (int64_t tau = 0; tau < ntile; ++tau) {
+                int64_t hs = hs0;
+                bool hv = hv0;
+                if (tau > 0) {
+                    hv = tile_head(tau, hs);
+                    load_xu((int)__builtin_amdgcn_raw_buffer_load_b32(us_rsrc, hv ? (uint32_t)hs * 4u : kDrop, 0, 0), hv);
+                }
+                f32x4 acc[B1];
+#pragma unroll
+                for (int t = 0; t < B1; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+                pipe<XH, 4, Ops<B1>>(
+                    [&](int q, Ops<B1>& o) { ldsv<B1>(wl + S::SW1 + (XH * g + q) * S::S1 + li * B1, o.v); },
+                    [&](int q, const Ops<B1>& o) {
+#pragma unroll
+                        for (int t = 0; t < B1; ++t) acc[t] = mfma16(o.v[t], xu[q], acc[t]);
+                    });
+                const uint32_t off = hv ? (uint32_t)(((hs / FOLD) * L1 + 4 * g) * 4) : kDrop;
+#pragma unroll
+                for (int t = 0; t < B1; ++t)
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[t]), pu_rsrc,
+                                                           off == kDrop ? kDrop : off + 64u * t, 0, 0);
+            }
+            // the P_u rows are read back by other lanes of this wave: wait for the stores (a
+            // workgroup-scope fence emits no vmcnt wait on gfx950, nor does __syncthreads)
+            __builtin_amdgcn_s_waitcnt(kVmcnt0);
+            load_pu(un);
+        }
+    }
 
     // ---- epilogue pieces shared by both forms: row w (one per chain / pair) holds half of the dW
     // tiles at a time in the accumulator layout ([tile][lane][4]) followed by the bias /
@@ -447,7 +568,12 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
             int base, ld, rs = 1;
             bool keep = true;
             if (t < S::NT1) {
-                if constexpr (SPLIT) {
+                if constexpr (GU) {
+                    // tile a < B0 / 2: user feature (B0 / 2) row + a; else item feature D0 + (B0 / 2) row + a - B0 / 2
+                    const int a = t / B1;
+                    base = S::OW1 + ((a < B0 / 2 ? 0 : D0) + a % (B0 / 2)) * L1 + 16 * (t % B1) + li, ld = L1,
+                    rs = B0 / 2;
+                } else if constexpr (SPLIT) {
                     base = S::OW1 + (t / B1) * L1 + 16 * (t % B1) + li, ld = L1, rs = B0;
                 } else {
                     base = S::OW1 + 16 * (t / B1) * L1 + 16 * (t % B1) + li, ld = L1;
@@ -497,9 +623,13 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
     // dX = W1 G1 of one 16-sample unit into the gradient rows' MLP parts: block ti holds input
     // features 16 ti + 4 lq .. + 3 of sample li (user half folded into the group head like the
     // GMF part); two blocks' chains interleaved, k-step (t, r) takes G1 feature 16 t + 4 lq + r
-    auto dx_rows = [&](const float (&g1)[B1][4], uint32_t urow_off, uint32_t irow_off, bool fmatch, bool fhead) {
+    // (tile pairs [TP0, TP1): B0 / 4 pairs of user tiles, then the item ones; FU: fold the user rows)
+    auto dx_rows = [&](const float (&g1)[B1][4], uint32_t urow_off, uint32_t irow_off, bool fmatch, bool fhead,
+                       auto tp0c, auto tp1c, auto fuc) {
+        constexpr int TP0 = decltype(tp0c)::value, TP1 = decltype(tp1c)::value;
+        constexpr bool FU = decltype(fuc)::value;
 #pragma unroll
-        for (int tp = 0; tp < B0 / 2; ++tp) {
+        for (int tp = NCF_DIAG_HALFL1 ? B0 / 4 : TP0; tp < TP1; ++tp) {
             f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
             pipe<4, 2, Ops2<2, B1>>(
                 [&](int r, Ops2<2, B1>& o) {
@@ -519,7 +649,7 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
                 const int f0 = 16 * ti + 4 * g;
                 const bool user = 16 * ti < D0;  // compile time: D0 is a multiple of 16
                 f32x4 d = acc[j];
-                if constexpr (FOLD > 1) {
+                if constexpr (FOLD > 1 && FU) {
                     if (user) {
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
@@ -533,6 +663,9 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
             }
         }
     };
+    using ic0 = std::integral_constant<int, 0>;
+    using icU = std::integral_constant<int, B0 / 4>;
+    using icA = std::integral_constant<int, B0 / 2>;
 
     if constexpr (SPLIT) {
         if (dwave) {
@@ -557,20 +690,74 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
             // li < 8 the user half, else the item half) in slot q & 1: steps 0 and 1 are loaded
             // before the unit's barrier, steps 2 and 3 once the MFMAs of steps 0 and 1 have read
             // their slot.  A masked sample reads the chain's row 0 (its G rows are zero).
-            float xq[2][B0];
+            // GU: the unit contracts the item half only (lane li: item features HB li .. + HB - 1, dW1
+            // tiles HB + a); the user half is contracted per group after the units (phase N)
+            constexpr int HB = B0 / 2;
+            constexpr int XW = GU ? HB : B0;
+            float xq[2][XW];
+            // XW floats of table row `row` from MLP-input float f0 of the row's MLP half into the local
+            // array dst (a macro: an array handed to a lambda by reference would live in scratch)
+#define NCF_LD_HALF(dst, row, f0)                                                                      \
+    do {                                                                                               \
+        const float* xs_ = emb + (size_t)(row) * W + G + (f0);                                         \
+        if constexpr (XW % 4 == 0) {                                                                   \
+            _Pragma("unroll") for (int k_ = 0; k_ < XW / 4; ++k_) {                                     \
+                const float4 v_ = reinterpret_cast<const float4*>(xs_)[k_];                            \
+                dst[4 * k_] = v_.x, dst[4 * k_ + 1] = v_.y, dst[4 * k_ + 2] = v_.z, dst[4 * k_ + 3] = v_.w; \
+            }                                                                                          \
+        } else {                                                                                       \
+            _Pragma("unroll") for (int k_ = 0; k_ < XW / 2; ++k_) {                                     \
+                const float2 v_ = reinterpret_cast<const float2*>(xs_)[k_];                            \
+                dst[2 * k_] = v_.x, dst[2 * k_ + 1] = v_.y;                                            \
+            }                                                                                          \
+        }                                                                                              \
+    } while (0)
             auto load_xq = [&](int64_t u, int q) {
                 const int64_t si = u * 16 + 4 * q + g;
                 const uint32_t off = si < n ? (uint32_t)si * 4u : kDrop;
                 const int xu = (int)__builtin_amdgcn_raw_buffer_load_b32(us_rsrc, off, 0, 0);
                 const int xv = (int)__builtin_amdgcn_raw_buffer_load_b32(it_rsrc, off, 0, 0);
                 const bool okr = si < n && (unsigned)xu < (unsigned)ids.ubound && (unsigned)xv < (unsigned)ids.ibound;
-                const int row = okr ? (li < 8 ? xu : ids.ibase + xv) : 0;
-                const float4* xs = reinterpret_cast<const float4*>(emb + (size_t)row * W + G + (li & 7) * B0);
+                const int row = GU ? (okr ? ids.ibase + xv : 0) : (okr ? (li < 8 ? xu : ids.ibase + xv) : 0);
+                const float* xs = emb + (size_t)row * W + G + (GU ? li * HB : (li & 7) * B0);
+                if constexpr (XW % 4 == 0) {
 #pragma unroll
-                for (int k = 0; k < B0 / 4; ++k) {
-                    const float4 v = xs[k];
-                    xq[q & 1][4 * k] = v.x, xq[q & 1][4 * k + 1] = v.y, xq[q & 1][4 * k + 2] = v.z,
-                                 xq[q & 1][4 * k + 3] = v.w;
+                    for (int k = 0; k < XW / 4; ++k) {
+                        const float4 v = reinterpret_cast<const float4*>(xs)[k];
+                        xq[q & 1][4 * k] = v.x, xq[q & 1][4 * k + 1] = v.y, xq[q & 1][4 * k + 2] = v.z,
+                                     xq[q & 1][4 * k + 3] = v.w;
+                    }
+                } else {
+#pragma unroll
+                    for (int k = 0; k < XW / 2; ++k) {
+                        const float2 v = reinterpret_cast<const float2*>(xs)[k];
+                        xq[q & 1][2 * k] = v.x, xq[q & 1][2 * k + 1] = v.y;
+                    }
+                }
+            };
+            // GU, a unit with samples whose user is not their group head's: their user half per sample
+            // (k-step q: sample 4 q + lq, G1 zero for the other samples, whose user half is the group's)
+            auto contract_mixed = [&](int64_t u, int par) {
+                const float* tq = tbuf(par);
+#pragma unroll 1
+                for (int q = 0; q < 4; ++q) {
+                    const int64_t si = u * 16 + 4 * q + g;
+                    const uint32_t off = si < n ? (uint32_t)si * 4u : kDrop;
+                    const int xu = (int)__builtin_amdgcn_raw_buffer_load_b32(us_rsrc, off, 0, 0);
+                    const int xv = (int)__builtin_amdgcn_raw_buffer_load_b32(it_rsrc, off, 0, 0);
+                    const int hu = (int)__builtin_amdgcn_raw_buffer_load_b32(
+                        us_rsrc, si < n ? (uint32_t)(si & ~(int64_t)(FOLD - 1)) * 4u : kDrop, 0, 0);
+                    const bool okr = si < n && (unsigned)xu < (unsigned)ids.ubound && (unsigned)xv < (unsigned)ids.ibound;
+                    const bool mism = si < n && xu != hu;
+                    float g1v[B1], xo[XW];
+                    NCF_LD_HALF(xo, okr ? xu : 0, li * HB);
+                    ldsv<B1>(tq + S::TG1 + (4 * q + g) * T1 + li * B1, g1v);
+#pragma unroll
+                    for (int b = 0; b < B1; ++b) g1v[b] = mism ? g1v[b] : 0.f;
+#pragma unroll
+                    for (int a = 0; a < HB; ++a)
+#pragma unroll
+                        for (int b = 0; b < B1; ++b) dw1[a][b] = mfma16(xo[a], g1v[b], dw1[a][b]);
                 }
             };
             // unit u's contraction from chain buffer `par`
@@ -587,9 +774,10 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
                     },
                     [&](int q, const DwOps<1, B1, B2>& o) {
 #pragma unroll
-                        for (int a = 0; a < B0; ++a)
+                        for (int a = 0; a < XW; ++a)
 #pragma unroll
-                            for (int b = 0; b < B1; ++b) dw1[a][b] = mfma16(xq[q & 1][a], o.g1[b], dw1[a][b]);
+                            for (int b = 0; b < B1; ++b)
+                                dw1[GU ? HB + a : a][b] = mfma16(xq[q & 1][a], o.g1[b], dw1[GU ? HB + a : a][b]);
 #pragma unroll
                         for (int a = 0; a < B1; ++a)
 #pragma unroll
@@ -629,9 +817,18 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
                 for (int64_t it = 0; it < nit; ++it, un += ustride) {
                     const bool have = un < nunits;
                     int xu = 0;
+                    bool mixed = false;
                     if (have) {  // in flight while the chain finishes the unit
                         load_xq(un, 0);
                         load_xq(un, 1);
+                        if constexpr (GU) {
+                            // sample li's user against its group head's
+                            const int64_t si = un * 16 + li;
+                            const int su = (int)__builtin_amdgcn_raw_buffer_load_b32(us_rsrc, si < n ? (uint32_t)si * 4u : kDrop, 0, 0);
+                            const int hu = (int)__builtin_amdgcn_raw_buffer_load_b32(
+                                us_rsrc, si < n ? (uint32_t)(si & ~(int64_t)(FOLD - 1)) * 4u : kDrop, 0, 0);
+                            mixed = __ballot(si < n && su != hu) != 0;
+                        }
                         if constexpr (NCF_SPLIT_DX) {
                             // sample li's user id: the dX rows' offsets and folding
                             const int64_t si = un * 16 + li;
@@ -644,6 +841,9 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
                         // the contraction first: its X operands (loaded before the barrier) are dead
                         // once it is done, which leaves dX the registers its chains need
                         contract(un, (int)(it & 1));
+                        if constexpr (GU) {
+                            if (mixed) contract_mixed(un, (int)(it & 1));
+                        }
                         if constexpr (NCF_SPLIT_DX) {
                             // the chain's G1 (transposed buffer row li: feature 16 t + 4 lq + r at
                             // position (4 lq + r) B1 + t), read with each k-step's W1 operands (the
@@ -725,6 +925,33 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
                 }
             };
             __syncthreads();  // every wave is done with the weights and the buffers
+            if constexpr (GU) {
+                // phase N: dW1's user half, sum over groups of x_u (sum g1)^T, 16 groups per tile
+                // (k-step q: column 4 q + lq of chain wave pw's phase-0 tile); the chain wave waited
+                // for its group-sum stores before the barrier above
+                const int64_t ntile = (nown + FOLD - 1) / FOLD;
+                for (int64_t tau = 0; tau < ntile; ++tau) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int c = 4 * q + g;
+                        const int64_t k = tau * FOLD + c / NGU;
+                        const int64_t hs = (un0 + k * ustride) * 16 + (c % NGU) * FOLD;
+                        const bool hv = k < nown && hs < n;
+                        const int hu = (int)__builtin_amdgcn_raw_buffer_load_b32(us_rsrc, hv ? (uint32_t)hs * 4u : kDrop, 0, 0);
+                        float s1[B1], xo[XW];
+                        NCF_LD_HALF(xo, hv && (unsigned)hu < (unsigned)ids.ubound ? hu : 0, li * HB);
+                        const uint32_t off = hv ? (uint32_t)(((hs / FOLD) * L1 + li) * 4) : kDrop;
+#pragma unroll
+                        for (int b = 0; b < B1; ++b)
+                            s1[b] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(sgr_rsrc, off == kDrop ? kDrop : off + 64u * b, 0, 0));
+#pragma unroll
+                        for (int a = 0; a < HB; ++a)
+#pragma unroll
+                            for (int b = 0; b < B1; ++b) dw1[a][b] = mfma16(xo[a], s1[b], dw1[a][b]);
+                    }
+                }
+            }
+#undef NCF_LD_HALF
             if (g == 0) {
 #pragma unroll
                 for (int t = 0; t < B1; ++t) R[S::RB1 + 16 * t + li] = ab1[t];
@@ -794,6 +1021,13 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
         load_g(un, cu, cv);                    // this unit's GMF slices, first used by the output
         const bool inb = sg < n;
         const bool ok = inb && (unsigned)cu < (unsigned)ids.ubound && (unsigned)cv < (unsigned)ids.ibound;
+        // user rows of a fold group summed into its head sample (fmatch: this sample's user is the head's)
+        const int su = inb ? cu : -1;
+        const bool fmatch = FOLD > 1 && inb && su == grp_bcast<(FOLD > 1 ? FOLD : 2)>(su, 0, lane);
+        const bool fhead = (li & fm) == 0;
+        // byte offsets of this sample's user / item gradient rows (or dropped)
+        const uint32_t urow_off = inb && (fhead || !fmatch) ? (uint32_t)(2 * sg * W) * 4u : kDrop;
+        const uint32_t irow_off = inb ? (uint32_t)((2 * sg + 1) * W) * 4u : kDrop;
 
         // ---- X^T for dW1 (row li: features XQ lq + q), then layer 1: k-step q takes feature
         // XQ lq + q from lane group lq (A: W1 row XQ lq + q, all B1 output blocks in one read)
@@ -803,14 +1037,51 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
                 tb[S::TX + li * T0 + (XQ / 16) * g + (q & 15) * B0 + (q >> 4)] = xr[q];
         }
         f32x4 h1[B1];
+        if constexpr (GU) {
+            // the group's P_u, then the item half (k-step q: item feature XH lq + q)
 #pragma unroll
-        for (int t = 0; t < B1; ++t) h1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-        pipe<XQ, 4, Ops<B1>>(
-            [&](int q, Ops<B1>& o) { ldsv<B1>(wl + S::SW1 + (XQ * g + q) * S::S1 + li * B1, o.v); },
-            [&](int q, const Ops<B1>& o) {
+            for (int t = 0; t < B1; ++t) h1[t] = pun[t];
+            if (__ballot(inb && !fmatch)) {
+                // a sample whose user is not its head's: its own user half (units of such batches only)
+                int urow, irow;
+                rows_of(un, cu, cv, urow, irow);
+                const float4* xs = reinterpret_cast<const float4*>(emb + (size_t)urow * W + G + g * XH);
+                float xo[XH];
 #pragma unroll
-                for (int t = 0; t < B1; ++t) h1[t] = mfma16(o.v[t], xr[q], h1[t]);
-            });
+                for (int k = 0; k < XH / 4; ++k) {
+                    const float4 v = xs[k];
+                    xo[4 * k] = v.x, xo[4 * k + 1] = v.y, xo[4 * k + 2] = v.z, xo[4 * k + 3] = v.w;
+                }
+                f32x4 a2[B1];
+#pragma unroll
+                for (int t = 0; t < B1; ++t) a2[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+                pipe<XH, 4, Ops<B1>>(
+                    [&](int q, Ops<B1>& o) { ldsv<B1>(wl + S::SW1 + (XH * g + q) * S::S1 + li * B1, o.v); },
+                    [&](int q, const Ops<B1>& o) {
+#pragma unroll
+                        for (int t = 0; t < B1; ++t) a2[t] = mfma16(o.v[t], xo[q], a2[t]);
+                    });
+                if (inb && !fmatch) {
+#pragma unroll
+                    for (int t = 0; t < B1; ++t) h1[t] = a2[t];
+                }
+            }
+            pipe<XH, 4, Ops<B1>>(
+                [&](int q, Ops<B1>& o) { ldsv<B1>(wl + S::SW1 + (D0 + XH * g + q) * S::S1 + li * B1, o.v); },
+                [&](int q, const Ops<B1>& o) {
+#pragma unroll
+                    for (int t = 0; t < B1; ++t) h1[t] = mfma16(o.v[t], xr[q], h1[t]);
+                });
+        } else {
+#pragma unroll
+            for (int t = 0; t < B1; ++t) h1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+            pipe<NCF_DIAG_HALFL1 ? XQ / 2 : XQ, 4, Ops<B1>>(
+                [&](int q, Ops<B1>& o) { ldsv<B1>(wl + S::SW1 + (XQ * g + q) * S::S1 + li * B1, o.v); },
+                [&](int q, const Ops<B1>& o) {
+#pragma unroll
+                    for (int t = 0; t < B1; ++t) h1[t] = mfma16(o.v[t], xr[q], h1[t]);
+                });
+        }
 
 #pragma unroll
         for (int t = 0; t < B1; ++t) {
@@ -881,7 +1152,10 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
         }
         // the next unit's MLP input into the registers layer 1 has consumed (issued after the
         // fence above, whose wait covers every load before it)
-        if (un1 < nunits) load_x(un1, nu, nv);
+        if (un1 < nunits) {
+            load_x(un1, nu, nv);
+            load_pu(un1);
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) zp += wo3[r] * h3[r];
         if constexpr (G > 0) {
@@ -954,12 +1228,6 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
         stsv<4>(tb + S::TG3 + li * 16 + 4 * g, g3);
 
         // ---- GMF backward; user rows of a fold group summed into its head sample
-        const int su = inb ? cu : -1;
-        const bool fmatch = FOLD > 1 && inb && su == grp_bcast<(FOLD > 1 ? FOLD : 2)>(su, 0, lane);
-        const bool fhead = (li & fm) == 0;
-        // byte offsets of this sample's user / item gradient rows (or dropped)
-        const uint32_t urow_off = inb && (fhead || !fmatch) ? (uint32_t)(2 * sg * W) * 4u : kDrop;
-        const uint32_t irow_off = inb ? (uint32_t)((2 * sg + 1) * W) * 4u : kDrop;
         if constexpr (G > 0) {
             float gug[GQ], gig[GQ];
 #pragma unroll
@@ -1063,7 +1331,27 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
 
         NCF_WT(itw, 5);
         // ---- dX = W1 G1 -> the per-sample gradient rows (split form: the weight-gradient wave's)
-        if constexpr (!SPLIT || !NCF_SPLIT_DX || NCF_SPLIT_LATE) dx_rows(g1, urow_off, irow_off, fmatch, fhead);
+        if constexpr (GU) {
+            // the group's G1 summed over the samples that share the head's user, for phase N; the
+            // item half here; a sample whose user is not its head's: its own user row here too
+            {
+                const uint32_t off = inb && fhead ? (uint32_t)(((sg / FOLD) * L1 + 4 * g) * 4) : kDrop;
+#pragma unroll
+                for (int t = 0; t < B1; ++t) {
+                    f32x4 v;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = fold_sum<FOLD>(fmatch ? g1[t][r] : 0.f);
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), sgr_rsrc,
+                                                           off == kDrop ? kDrop : off + 64u * t, 0, 0);
+                }
+            }
+            dx_rows(g1, kDrop, irow_off, fmatch, fhead, icU{}, icA{}, std::false_type{});
+            if (__ballot(inb && !fmatch))
+                dx_rows(g1, inb && !fmatch ? (uint32_t)(2 * sg * W) * 4u : kDrop, kDrop, fmatch, fhead, ic0{}, icU{},
+                        std::false_type{});
+        } else if constexpr (!SPLIT || !NCF_SPLIT_DX || NCF_SPLIT_LATE) {
+            dx_rows(g1, urow_off, irow_off, fmatch, fhead, ic0{}, icA{}, std::true_type{});
+        }
 
         // ---- weight gradients over the unit's 16 samples: k-step q takes sample 4 q + lq
         NCF_WT(itw, 6);
@@ -1108,6 +1396,27 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
     if constexpr (SPLIT) __builtin_amdgcn_s_setprio(0);
 #endif
 
+    // ---- GU phase N: the folded user rows' MLP part, W1_u (sum g1), 16 groups per tile
+    if constexpr (GU) {
+        // the group sums were stored by this wave's lanes; the weight-gradient wave reads them after
+        // the epilogue's first barrier
+        __builtin_amdgcn_s_waitcnt(kVmcnt0);
+        const int64_t ntile = (nown + FOLD - 1) / FOLD;
+        for (int64_t tau = 0; tau < ntile; ++tau) {
+            int64_t hs;
+            const bool hv = tile_head(tau, hs);
+            const uint32_t off = hv ? (uint32_t)(((hs / FOLD) * L1 + 4 * g) * 4) : kDrop;
+            float s1[B1][4];
+#pragma unroll
+            for (int t = 0; t < B1; ++t) {
+                const f32x4 v = __builtin_bit_cast(
+                    f32x4, __builtin_amdgcn_raw_buffer_load_b128(sgr_rsrc, off == kDrop ? kDrop : off + 64u * t, 0, 0));
+#pragma unroll
+                for (int r = 0; r < 4; ++r) s1[t][r] = v[r];
+            }
+            dx_rows(s1, hv ? (uint32_t)(2 * hs * W) * 4u : kDrop, kDrop, true, true, ic0{}, icU{}, std::false_type{});
+        }
+    }
     // ---- epilogue: per-lane sums over the 16 sample lanes, then the four waves in LDS
     NCF_WS(11, __builtin_readcyclecounter());
 #pragma unroll
@@ -1234,7 +1543,7 @@ hipError_t launch_wave_form(const WsLayout& L, void* ws, const float* emb, const
         launch(kern, grid, SPLIT ? 512 : 256, lds, st, emb, mlp, users, items, labels, n, ids, inv_batch,
                at<float>(ws, L.probs), at<float>(ws, L.gs), at<float>(ws, L.slabs), at<float>(ws, L.part_bce), group,
                topk, at<float>(ws, L.part_hit), at<float>(ws, L.part_dcg),
-               check_fold ? at<const int32_t>(ws, L.ifold) : nullptr, at<int32_t>(ws, L.err));
+               check_fold ? at<const int32_t>(ws, L.ifold) : nullptr, at<int32_t>(ws, L.err), at<float>(ws, L.act));
     };
     switch (fold * 2 + (in_kernel ? 1 : 0)) {
         case 0: go(k_fb_wave<S, 0, false, SPLIT>); break;

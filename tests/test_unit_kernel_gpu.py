@@ -177,8 +177,11 @@ def test_unit_deterministic_and_close_to_tile():
 def test_wave_split_form_bitwise_one_wave(dims, B, group):
     """The split form (chain waves + weight-gradient waves, one barrier per unit) issues the same
     MFMAs on the same operands in the same order as the one-wave form: every output bitwise equal,
-    including workgroups whose waves run different unit counts (tails) and the fold / in-kernel
-    metric variants."""
+    including workgroups whose waves run different unit counts (tails) and the in-kernel metric
+    variants.  With user-row folding (group 2, 4, 8) the split form computes the user half of
+    layer 1 and of dX once per group (group-user form): the same sums reassociated, so there the
+    two forms agree within fp32 rounding — sample 7 (an out-of-range user, not its group head's)
+    takes the group-user form's per-sample branch."""
     shape = O.NCFShape(*dims)
     w = _weights(shape, 61)
     users, items, y = _batch(shape, B, group, 62 + B)
@@ -199,8 +202,21 @@ def test_wave_split_form_bitwise_one_wave(dims, B, group):
         torch.cuda.synchronize()
         outs.append([grads[0].clone(), grads[1].clone(), grads[2].clone(), probs.clone(), eng2.emb.clone(),
                      eng2.mlp.clone(), eng2.stats.clone()])
-    for a, b in zip(*outs):
-        assert torch.equal(a.nan_to_num(7.0), b.nan_to_num(7.0))
+    if group == 1:
+        for a, b in zip(*outs):
+            assert torch.equal(a.nan_to_num(7.0), b.nan_to_num(7.0))
+        return
+    (ge, gm, gsum, p, emb, mlp, st), (re_, rm, rsum, rp, remb, rmlp, rst) = outs
+    assert torch.equal(torch.isnan(p), torch.isnan(rp))
+    assert torch.max(torch.abs(p.nan_to_num(0.0) - rp.nan_to_num(0.0))).item() <= 2e-6
+    for a, b in ((ge, re_), (gm, rm)):
+        assert torch.max(torch.abs(a - b)).item() <= 1e-5 * max(torch.max(torch.abs(b)).item(), 1e-30)
+    assert torch.max(torch.abs(emb - remb)).item() <= 1e-6 and torch.max(torch.abs(mlp - rmlp)).item() <= 1e-6
+    # summary / stats: the loss and the counts; hit / dcg rank probabilities that may tie (or
+    # saturate at 1) within rounding, so they are compared through the oracle in other tests
+    ia, ib = NCFEngine.read_stats(st), NCFEngine.read_stats(rst)
+    assert ia["loss"] == pytest.approx(ib["loss"], rel=1e-5)
+    assert gsum[0].item() == pytest.approx(rsum[0].item(), rel=1e-5)
 
 
 def test_kernel_selection_by_batch():

@@ -32,10 +32,12 @@ def _weights(shape, seed):
     return w(shape, seed)
 
 
-def _mixed_batch(shape, B, group, seed):
+def _mixed_batch(shape, B, group, seed, w=None):
     """Groups of `group` samples sharing a user, then: ~25% of the non-head samples get another
     user, ~10% of the heads get another user (the rest of that group still shares one), and one
-    group whose samples all differ."""
+    group whose samples all differ.  With the weights ``w``: samples on a ReLU kink (a hidden
+    pre-activation within rounding of 0, where fp32 and fp64 may take different sides, and two fp32
+    summation orders too) draw another item until none is left."""
     rng = np.random.RandomState(seed)
     users = rng.randint(0, shape.num_users, B // group).repeat(group)
     items = rng.randint(0, shape.num_items, B)
@@ -46,6 +48,13 @@ def _mixed_batch(shape, B, group, seed):
     heads = (pos == 0) & (rng.rand(B) < 0.10)
     users[heads] = rng.randint(0, shape.num_users, int(heads.sum()))
     users[group:2 * group] = rng.permutation(shape.num_users)[:group]
+    if w is not None:
+        from test_headline_parity_gpu import kink_samples
+        for _ in range(50):
+            k = kink_samples(shape, w, users, items)
+            if not k.any():
+                break
+            items[k] = rng.randint(0, shape.num_items, int(k.sum()))
     return users.astype(np.int32), items.astype(np.int32), y
 
 
@@ -55,7 +64,7 @@ def test_mixed_groups_grads_match_oracle(group, kernel):
     shape = O.NCFShape(*CONFIG_C)
     w = _weights(shape, 60 + group)
     B = 1024
-    users, items, y = _mixed_batch(shape, B, group, 61 + group)
+    users, items, y = _mixed_batch(shape, B, group, 61 + group, w)
     eng = NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=B, fb_kernel=kernel)
     eng.set_keras_weights(w)
     grads = eng.alloc_grads()
@@ -81,7 +90,7 @@ def test_mixed_groups_train_steps_match_oracle(lazy, kernel):
     eng.set_keras_weights(w)
     ref = {k: v.copy() for k, v in w.items()}
     st = O.new_opt_state(ref)
-    batches = [_mixed_batch(shape, 512, 4, 71 + s) for s in range(3)]
+    batches = [_mixed_batch(shape, 512, 4, 71 + s, w) for s in range(3)]
     dev = [tuple(torch.from_numpy(x).cuda() for x in b) for b in batches]
     for s, (u, it, yy) in enumerate(dev):
         nxt = (dev[s + 1][0], dev[s + 1][1]) if lazy and s + 1 < len(dev) else None
