@@ -289,6 +289,14 @@ __device__ unsigned long long g_wave_s[256 * 4 * 16];
 #if NCF_GROUP_USER && NCF_SPLIT_DX
 #error "NCF_SPLIT_DX computes dX per sample on the weight-gradient wave: build it with NCF_GROUP_USER=0"
 #endif
+// timing diagnostics (wrong results): NCF_DIAG_NOP0 1 skips the group-user form's phase 0 (its
+// loads of P_u stay), NCF_DIAG_NOPN 1 skips phase N on both waves
+#ifndef NCF_DIAG_NOP0
+#define NCF_DIAG_NOP0 0
+#endif
+#ifndef NCF_DIAG_NOPN
+#define NCF_DIAG_NOPN 0
+#endif
 #ifndef NCF_DIAG_HALFL1
 #define NCF_DIAG_HALFL1 0
 #endif
@@ -517,7 +525,7 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
     // FOLD units (k-step q takes user feature XH lq + q), into gpart
     if constexpr (GU) {
         if (!dwave) {
-            const int64_t ntile = (nown + FOLD - 1) / FOLD;
+            const int64_t ntile = NCF_DIAG_NOP0 ? 0 : (nown + FOLD - 1) / FOLD;
             for (int64_t tau = 0; tau < ntile; ++tau) {
                 int64_t hs = hs0;
                 bool hv = hv0;
@@ -898,6 +906,33 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
                     }
                 }
             }
+            if constexpr (GU) {
+                // phase N: dW1's user half, sum over groups of x_u (sum g1)^T, 16 groups per tile
+                // (k-step q: column 4 q + lq of chain wave pw's phase-0 tile); the chain wave waited
+                // for its group-sum stores before the last unit barrier, so this runs beside the
+                // chain wave's own phase N
+                const int64_t ntile = NCF_DIAG_NOPN ? 0 : (nown + FOLD - 1) / FOLD;
+                for (int64_t tau = 0; tau < ntile; ++tau) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int c = 4 * q + g;
+                        const int64_t k = tau * FOLD + c / NGU;
+                        const int64_t hs = (un0 + k * ustride) * 16 + (c % NGU) * FOLD;
+                        const bool hv = k < nown && hs < n;
+                        const int hu = (int)__builtin_amdgcn_raw_buffer_load_b32(us_rsrc, hv ? (uint32_t)hs * 4u : kDrop, 0, 0);
+                        float s1[B1], xo[XW];
+                        NCF_LD_HALF(xo, hv && (unsigned)hu < (unsigned)ids.ubound ? hu : 0, li * HB);
+                        const uint32_t off = hv ? (uint32_t)(((hs / FOLD) * L1 + li) * 4) : kDrop;
+#pragma unroll
+                        for (int b = 0; b < B1; ++b)
+                            s1[b] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(sgr_rsrc, off == kDrop ? kDrop : off + 64u * b, 0, 0));
+#pragma unroll
+                        for (int a = 0; a < HB; ++a)
+#pragma unroll
+                            for (int b = 0; b < B1; ++b) dw1[a][b] = mfma16(xo[a], s1[b], dw1[a][b]);
+                    }
+                }
+            }
 #pragma unroll
             for (int t = 0; t < B1; ++t) ab1[t] = group_allsum(ab1[t]);
 #pragma unroll
@@ -925,32 +960,6 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
                 }
             };
             __syncthreads();  // every wave is done with the weights and the buffers
-            if constexpr (GU) {
-                // phase N: dW1's user half, sum over groups of x_u (sum g1)^T, 16 groups per tile
-                // (k-step q: column 4 q + lq of chain wave pw's phase-0 tile); the chain wave waited
-                // for its group-sum stores before the barrier above
-                const int64_t ntile = (nown + FOLD - 1) / FOLD;
-                for (int64_t tau = 0; tau < ntile; ++tau) {
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const int c = 4 * q + g;
-                        const int64_t k = tau * FOLD + c / NGU;
-                        const int64_t hs = (un0 + k * ustride) * 16 + (c % NGU) * FOLD;
-                        const bool hv = k < nown && hs < n;
-                        const int hu = (int)__builtin_amdgcn_raw_buffer_load_b32(us_rsrc, hv ? (uint32_t)hs * 4u : kDrop, 0, 0);
-                        float s1[B1], xo[XW];
-                        NCF_LD_HALF(xo, hv && (unsigned)hu < (unsigned)ids.ubound ? hu : 0, li * HB);
-                        const uint32_t off = hv ? (uint32_t)(((hs / FOLD) * L1 + li) * 4) : kDrop;
-#pragma unroll
-                        for (int b = 0; b < B1; ++b)
-                            s1[b] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(sgr_rsrc, off == kDrop ? kDrop : off + 64u * b, 0, 0));
-#pragma unroll
-                        for (int a = 0; a < HB; ++a)
-#pragma unroll
-                            for (int b = 0; b < B1; ++b) dw1[a][b] = mfma16(xo[a], s1[b], dw1[a][b]);
-                    }
-                }
-            }
 #undef NCF_LD_HALF
             if (g == 0) {
 #pragma unroll
@@ -1004,6 +1013,9 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
     // the barrier)
     for (int64_t it = 0; SPLIT ? it < nit : un < nunits; ++it, un += ustride) {
       if (SPLIT && un >= nunits) {
+        // GU: this wave's group sums have landed before the last barrier (its partner reads them
+        // right after the loop)
+        if constexpr (GU) if (it + 1 == nit) __builtin_amdgcn_s_waitcnt(kVmcnt0);
         if (!NCF_SPLIT_NOSYNC) {
             if (NCF_SPLIT_LATE) __syncthreads();
             __syncthreads();
@@ -1390,6 +1402,7 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
         nu = tu, nv = tv, ny = ty;
         NCF_WT(itw, 7);
       }
+      if constexpr (GU) if (it + 1 == nit) __builtin_amdgcn_s_waitcnt(kVmcnt0);  // as above
       if constexpr (SPLIT) if (!NCF_SPLIT_NOSYNC) __syncthreads();  // hand the unit to the weight-gradient wave
     }
 #if NCF_SPLIT_PRIO
@@ -1398,10 +1411,8 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
 
     // ---- GU phase N: the folded user rows' MLP part, W1_u (sum g1), 16 groups per tile
     if constexpr (GU) {
-        // the group sums were stored by this wave's lanes; the weight-gradient wave reads them after
-        // the epilogue's first barrier
-        __builtin_amdgcn_s_waitcnt(kVmcnt0);
-        const int64_t ntile = (nown + FOLD - 1) / FOLD;
+        // the group sums were stored by this wave's lanes and waited for before the last barrier
+        const int64_t ntile = NCF_DIAG_NOPN ? 0 : (nown + FOLD - 1) / FOLD;
         for (int64_t tau = 0; tau < ntile; ++tau) {
             int64_t hs;
             const bool hv = tile_head(tau, hs);
