@@ -1041,6 +1041,14 @@ def main():
                        "kernel_path": kpath},
             "roofline": fb_roof if dominant_fb else emb_roof,
             "roofline_emb_update" if dominant_fb else "roofline_fwd_bwd": emb_roof if dominant_fb else fb_roof,
+            # the north star's gather + scatter bandwidth over both kernels together: the
+            # forward/backward's rows in and gradient rows out plus the update's bytes, over the two
+            # launches' summed average durations
+            "gather_scatter_hbm": {
+                "bytes_per_step": int(fb_bytes + nbytes), "ms_per_step": round(fb_ms + kern_ms, 5),
+                "achieved": round((fb_bytes + nbytes) / ((fb_ms + kern_ms) * 1e-3) / 1e9, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round((fb_bytes + nbytes) / ((fb_ms + kern_ms) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
             "index_build_ms": round(ms_idx / max(nidx, 1), 5),
             "sampler_ms": round(ms_smp / nsmp, 5) if nsmp else None,
             "catchup_ms": round(ms_cu / ncu, 5) if ncu else None,
