@@ -831,7 +831,8 @@ def main():
             # ... and catches the next batch's stale rows up (the rows it touches that this step
             # did not): their p, m, v read and written once more before the next forward pass
             replay_rows = replayed_rows(pool, args.warmup, args.steps, eng.num_users, eng.num_rows, items=True)
-            nbytes += 24 * replay_rows * eng.shape.row_width
+            # a replayed row: p, m, v read, p written (the next update re-derives m and v: P-ahead rows)
+            nbytes += 16 * replay_rows * eng.shape.row_width
         if eng.kernel_for(B) == "fused-mfma-wave" and B >= 16384:
             # the launch's dense-layer blocks reduce the wave kernel's 256 dense-gradient slabs (both
             # levels) and step the dense layers: slab reads + p, m, v of every dense parameter
@@ -848,7 +849,7 @@ def main():
             tu = float(np.mean([torch.unique(u).numel() for u, _, _ in pool[:16]]))
             own = 24 * tu * W + cu * W * 4 + cu * 4 + 2 * B * (4 + 8)
             replay_rows = replayed_rows(pool, args.warmup, args.steps, eng.num_users, Uloc, items=False)
-            own += 24 * replay_rows * W
+            own += 16 * replay_rows * W   # P-ahead replays: p, m, v read, p written
         else:
             own = 24 * Uloc * W + cu * W * 4 + cu * 4 + (Uloc + 1) * 4
         item_rows = (eng.num_rows - Uloc) if not dp.split else max(0, min(dp.Ic, eng.num_rows - Uloc))

@@ -27,6 +27,12 @@
 
 #include <cstdlib>
 
+// timing diagnostic (wrong results): 1 = layer 1's user half skipped in all three kernels (the
+// work a per-group user half would leave)
+#ifndef NCF_DIAG_DHALF
+#define NCF_DIAG_DHALF 0
+#endif
+
 #include "ncf_common.h"
 #include "ncf_internal.h"
 
@@ -127,9 +133,9 @@ __global__ __launch_bounds__(64 * NW, 1) void k_lay_l1f(const float* __restrict_
         U.urow = U.ok ? cu : 0;
         U.irow = U.ok ? ids.ibase + cv : 0;
         const float4* xs =
-            reinterpret_cast<const float4*>(emb + (size_t)(g < 2 ? U.urow : U.irow) * W + G + (g & 1) * XQ);
+            reinterpret_cast<const float4*>(emb + (size_t)(g < 2 && !NCF_DIAG_DHALF ? U.urow : U.irow) * W + G + (g & 1) * XQ);
 #pragma unroll
-        for (int k = 0; k < XQ / 4; ++k) {
+        for (int k = 0; k < (NCF_DIAG_DHALF ? XQ / 8 : XQ / 4); ++k) {
             const float4 v = xs[k];
             U.x[4 * k] = v.x, U.x[4 * k + 1] = v.y, U.x[4 * k + 2] = v.z, U.x[4 * k + 3] = v.w;
         }
@@ -154,7 +160,7 @@ __global__ __launch_bounds__(64 * NW, 1) void k_lay_l1f(const float* __restrict_
         float a[2][B1];
         ldsv<B1>(wl + (XQ * g) * S::S1 + li * B1, a[0]);
 #pragma unroll
-        for (int q = 0; q < XQ; ++q) {
+        for (int q = 0; q < (NCF_DIAG_DHALF ? XQ / 2 : XQ); ++q) {
             if (q + 1 < XQ) ldsv<B1>(wl + (XQ * g + q + 1) * S::S1 + li * B1, a[(q + 1) & 1]);
 #pragma unroll
             for (int t = 0; t < B1; ++t) h[t] = mfma16(a[q & 1][t], U.x[q], h[t]);
@@ -249,7 +255,7 @@ __global__ __launch_bounds__(64 * NW, 1) void k_lay_l1b(const float* __restrict_
         // takes G1 feature 16 t + 4 lq + r (one LDS read gives the B1 steps of one r)
         // (blocks two at a time: the whole block loop unrolled hoists every LDS read and spills)
 #pragma unroll 2
-        for (int ti = 0; ti < B0; ++ti) {
+        for (int ti = NCF_DIAG_DHALF ? B0 / 2 : 0; ti < B0; ++ti) {
             f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
             float a[2][B1];
             ldsv<B1>(wl + (16 * ti + li) * S::S1 + (4 * g) * B1, a[0]);
@@ -389,6 +395,7 @@ __global__ __launch_bounds__(64 * kDw1Waves, 2) void k_lay_dw1(const float* __re
         const float* bx = base + 16 * XT * wv + li;                                                    \
         const float* bg = base + 16 * SX + li;                                                         \
         _Pragma("unroll") for (int k = 0; k < 4; ++k) {                                                \
+            if (NCF_DIAG_DHALF && wv < kDw1Waves / 2) break;                                           \
             const int row = 4 * k + lq;                                                                \
             float a[XT], b[YT];                                                                        \
             _Pragma("unroll") for (int x = 0; x < XT; ++x) a[x] = bx[row * SX + 16 * x];               \

@@ -149,6 +149,27 @@ __device__ __forceinline__ void decay4(float4& m, float4& v, float b1, float b2)
     v.x = b2 * v.x + 0.0f; v.y = b2 * v.y + 0.0f; v.z = b2 * v.z + 0.0f; v.w = b2 * v.w + 0.0f;
 }
 
+// decay4 on an element pair (adam2_zero's moment updates: bitwise)
+__device__ __forceinline__ void decay2(f32x2& m, f32x2& v, float b1, float b2) {
+#pragma clang fp contract(off)
+    m = m * b1 + 0.0f;
+    v = v * b2;
+}
+
+// P-ahead rows.  The catch-up ahead (the next batch's stale rows, replayed in the touched-row
+// update launch) writes p only: the next step's update reads m and v anyway and re-derives their
+// missed zero-gradient decays (the moments do not depend on p), as it does after the per-step
+// catch-up.  Such a row's row_step holds -(s0 + 2), s0 = the step its m and v are at; its p is at
+// the step of the launch that caught it up, which every consumer knows: the next update's t - 1,
+// the flush's and the stale-count gate's target (nothing else runs in between: the engine flushes
+// before it discards a counted-ahead batch).  Pristine rows are never caught up, so s0 >= 0 and
+// the mark is negative.
+#ifndef NCF_AHEAD_P_ONLY
+#define NCF_AHEAD_P_ONLY 1
+#endif
+__device__ __forceinline__ int pahead_mark(int s0) { return -(s0 + 2); }
+__device__ __forceinline__ int pahead_s0(int rs) { return -rs - 2; }
+
 // blocks blk of nblk stride over the table's float4 elements
 template <int OPT, int SRC, bool L2>
 __device__ __forceinline__ void emb_update_body(float4* __restrict__ emb, float4* __restrict__ m4,
@@ -220,6 +241,9 @@ __global__ __launch_bounds__(kBlock) void k_emb_update(float4* __restrict__ emb,
 
 #ifndef NCF_CATCHUP_P_ONLY
 #define NCF_CATCHUP_P_ONLY 1
+#endif
+#if NCF_AHEAD_P_ONLY && !NCF_CATCHUP_P_ONLY
+#error "P-ahead rows need the update's m / v re-derivation (NCF_CATCHUP_P_ONLY)"
 #endif
 #ifndef NCF_CATCHUP_SCALAR
 #define NCF_CATCHUP_SCALAR 1
@@ -361,6 +385,29 @@ __device__ __forceinline__ void stale_replay_body(float* __restrict__ embf, floa
     const int lane = threadIdx.x & 63;
     const int64_t wave = (int64_t)blk * (kBlock / 64) + (threadIdx.x >> 6);
     const int64_t nw = (int64_t)nblk * (kBlock / 64);
+    // P-ahead rows of the counted batch (their p was caught up to t by the previous step's launch)
+    // may now stay out of this step's batch: give every such row its m, v decays here, so that
+    // row_step again tells the step of all three (the claim loop below leaves them alone)
+    for (int64_t r0 = wave * 64; r0 < sg.lazy_rows; r0 += nw * 64) {
+        const int64_t rr = r0 + lane;
+        const int rs = rr < sg.lazy_rows ? sg.row_step[rr] : 0;
+        uint64_t pm = __ballot(rs < 0);
+        while (pm) {
+            const int src = __ffsll((unsigned long long)pm) - 1;
+            pm &= pm - 1;
+            const int64_t r = r0 + src;
+            const int s0 = pahead_s0(__shfl(rs, src, 64));
+            for (int q = lane; 2 * q < W; q += 64) {
+                const size_t e = (size_t)r * W + 2 * q;
+                f32x2 m = *reinterpret_cast<const f32x2*>(mf + e);
+                f32x2 v = *reinterpret_cast<const f32x2*>(vf + e);
+                for (int st = s0 + 1; st <= t; ++st) decay2(m, v, b1, b2);
+                *reinterpret_cast<f32x2*>(mf + e) = m;
+                *reinterpret_cast<f32x2*>(vf + e) = v;
+            }
+            if (lane == 0) sg.row_step[r] = t;
+        }
+    }
     for (int64_t c0 = wave * 64; c0 < sg.m; c0 += nw * 64) {
         const int64_t c = c0 + lane;
         int key = -1;
@@ -374,7 +421,7 @@ __device__ __forceinline__ void stale_replay_body(float* __restrict__ embf, floa
         int s0 = t;
         if (key >= 0) {
             int sv = sg.row_step[key];
-            while (sv < t) {
+            while (sv >= 0 && sv < t) {  // (a P-ahead mark is the loop above's)
                 const int prev = atomicCAS(&sg.row_step[key], sv, t);
                 if (prev == sv) {
                     claim = true;
@@ -455,15 +502,18 @@ __device__ __forceinline__ void catchup_body(float4* __restrict__ emb, float4* _
     for (int64_t i0 = (int64_t)blockIdx.x * rpb + sub; i0 < n; i0 += pstride * kRep) {
         int64_t r[kRep];
         int sr[kRep];
+        bool pa[kRep];
 #pragma unroll
         for (int j = 0; j < kRep; ++j) {
             const int64_t i = i0 + j * pstride;
             r[j] = i < n ? (ALL ? i : list[i]) : 0;
             // R: rows [0, R) are under deferred decay (touched rows past it are swept densely); a
             // pristine row (NCF_ROW_PRISTINE, past every t) is current: clamped to t, so no step loop
-            // ever starts from its mark (s + 1 would overflow)
+            // ever starts from its mark (s + 1 would overflow).  A P-ahead row's p is current (at t):
+            // the flush decays its m and v from s0; the per-step catch-up leaves them to the update
             const int rs = i < n && (ALL || r[j] < R) ? row_step[r[j]] : t;
-            sr[j] = rs < t ? rs : t;
+            pa[j] = ALL && rs < 0;
+            sr[j] = rs < 0 ? (ALL ? pahead_s0(rs) : t) : (rs < t ? rs : t);
         }
         for (int q = q0; q < W2; q += lanes_per_row) {  // element pair q: elements 2q, 2q + 1
             const f32x2 z2 = {0.f, 0.f};
@@ -478,8 +528,14 @@ __device__ __forceinline__ void catchup_body(float4* __restrict__ emb, float4* _
             }
             if constexpr ((ALL ? NCF_FLUSH_UNROLL : NCF_REPLAY_UNROLL) > 1) {
 #pragma unroll
-                for (int j = 0; j < kRep; ++j)
-                    replay2<(ALL ? NCF_FLUSH_UNROLL : NCF_REPLAY_UNROLL)>(p[j], m[j], v[j], sr[j], t, lut, lr, b1, b2, eps);
+                for (int j = 0; j < kRep; ++j) {
+                    if (pa[j]) {  // wave-uniform: a row spans whole waves
+                        for (int st = sr[j] + 1; st <= t; ++st) decay2(m[j], v[j], b1, b2);
+                    } else {
+                        replay2<(ALL ? NCF_FLUSH_UNROLL : NCF_REPLAY_UNROLL)>(p[j], m[j], v[j], sr[j], t, lut, lr, b1, b2,
+                                                                              eps);
+                    }
+                }
             } else {
                 // the rows' chains advance together (same per-element arithmetic, step by step)
                 int smin = t;
@@ -488,15 +544,17 @@ __device__ __forceinline__ void catchup_body(float4* __restrict__ emb, float4* _
                 for (int st = smin + 1; st <= t; ++st) {
                     const float lrt = t - st < kLrLut ? lut[t - st] : adam_lr_t(lr, b1, b2, st);
 #pragma unroll
-                    for (int j = 0; j < kRep; ++j)
-                        if (st > sr[j]) adam2_zero(p[j], m[j], v[j], lrt, b1, b2, eps);
+                    for (int j = 0; j < kRep; ++j) {
+                        if (st > sr[j] && pa[j]) decay2(m[j], v[j], b1, b2);
+                        else if (st > sr[j]) adam2_zero(p[j], m[j], v[j], lrt, b1, b2, eps);
+                    }
                 }
             }
 #pragma unroll
             for (int j = 0; j < kRep; ++j) {
                 if (sr[j] < t) {
                     const size_t e = (size_t)r[j] * W + 2 * q;
-                    *reinterpret_cast<f32x2*>(embf + e) = p[j];
+                    if (!pa[j]) *reinterpret_cast<f32x2*>(embf + e) = p[j];
                     if (ALL || !NCF_CATCHUP_P_ONLY) {
                         *reinterpret_cast<f32x2*>(mf + e) = m[j];
                         *reinterpret_cast<f32x2*>(vf + e) = v[j];
@@ -514,14 +572,19 @@ __device__ __forceinline__ void catchup_body(float4* __restrict__ emb, float4* _
     for (int64_t i = wave * rl.rpw + rl.sub; i < n; i += waves * rl.rpw) {
         const int64_t r = ALL ? i : list[i];
         if (!ALL && r >= R) continue;
-        const int s = row_step[r];
+        int s = row_step[r];
+        const bool pah = s < 0;  // P-ahead: p current; the flush decays m, v, the catch-up skips it
+        if (pah && !ALL) continue;
+        if (pah) s = pahead_s0(s);
         if (s >= t) continue;
         for (uint32_t q = rl.q; q < w4; q += rl.qstep) {
             const size_t e = (size_t)r * w4 + q;
             float4 p = emb[e], m = m4[e], v = v4[e];
-            for (int j = s + 1; j <= t; ++j)
-                adam4(p, m, v, zero, t - j < kLrLut ? lut[t - j] : adam_lr_t(lr, b1, b2, j), b1, b2, eps);
-            st_stream(&emb[e], p);
+            for (int j = s + 1; j <= t; ++j) {
+                if (pah) decay4(m, v, b1, b2);
+                else adam4(p, m, v, zero, t - j < kLrLut ? lut[t - j] : adam_lr_t(lr, b1, b2, j), b1, b2, eps);
+            }
+            if (!pah) st_stream(&emb[e], p);
             if (ALL || !NCF_CATCHUP_P_ONLY) {  // the flush leaves the dense state; with P_ONLY the
                         // per-step replay writes only p (the forward pass reads p) and
                         // k_emb_adam_touched re-derives m and v from row_step
@@ -820,9 +883,10 @@ __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_tou
                 }
                 const bool first = wave_run_count<true>(ca.cnt, key, ok);
                 // not in this step's batch (this launch's update blocks do not touch it) and behind
-                const bool claim = ca.replay && first && key < ca.lazy_rows && o1 == o0 && sv < t;
+                // (a P-ahead mark, negative, never occurs here: the previous step's update consumed it)
+                const bool claim = ca.replay && first && key < ca.lazy_rows && o1 == o0 && (unsigned)sv < (unsigned)t;
                 const int s0 = sv;
-                if (claim) row_step[key] = t;
+                if (claim) row_step[key] = NCF_AHEAD_P_ONLY ? pahead_mark(s0) : t;
                 const uint64_t cm = __ballot(claim);
                 if (claim) {
                     const int slot = __popcll(cm & ((1ull << lane) - 1));
@@ -875,8 +939,10 @@ __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_tou
                 for (int j = 0; j < kRepC; ++j) {
                     if (act[j]) {
                         *reinterpret_cast<f32x2*>(embf + e[j]) = p[j];
-                        *reinterpret_cast<f32x2*>(mf + e[j]) = mm[j];
-                        *reinterpret_cast<f32x2*>(vf + e[j]) = vv[j];
+                        if (!NCF_AHEAD_P_ONLY) {  // P-ahead: the next update re-derives m and v
+                            *reinterpret_cast<f32x2*>(mf + e[j]) = mm[j];
+                            *reinterpret_cast<f32x2*>(vf + e[j]) = vv[j];
+                        }
                     }
                 }
             }
@@ -904,9 +970,11 @@ __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_tou
             const int c = oc.y;
             // rows past lazy_rows (the list is ascending: its tail) are the caller's dense sweep's
             const bool mine = r < ca.lazy_rows;
-            const int rs = mine ? row_step[r] : 0;
+            int rs = mine ? row_step[r] : 0;
             // a pristine row's moments are +0 (NCF_ROW_PRISTINE): only p is read
             const bool fresh = rs == NCF_ROW_PRISTINE;
+            // a P-ahead row (caught up ahead by the previous step's launch): p at t - 1, m / v at s0
+            if (rs < 0) rs = pahead_s0(rs);
             const int k = NCF_CATCHUP_P_ONLY && mine && !fresh ? t - 1 - rs : 0;  // m/v decay steps still owed
             for (uint32_t q = rl.q; mine && q < w4; q += rl.qstep) {
                 const size_t e = (size_t)r * w4 + q;

@@ -800,6 +800,18 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
                         if (q < 2) load_xq(u, q + 2);
                     });
             };
+            // GU: the user ids of phase N's first tile, loaded now (one memory round trip less
+            // at the kernel's tail)
+            int phu[4] = {0, 0, 0, 0};
+            if constexpr (GU) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int c = 4 * q + g;
+                    const int64_t hs = (un0 + (int64_t)(c / NGU) * ustride) * 16 + (c % NGU) * FOLD;
+                    const bool hv = c / NGU < nown && hs < n;
+                    phu[q] = (int)__builtin_amdgcn_raw_buffer_load_b32(us_rsrc, hv ? (uint32_t)hs * 4u : kDrop, 0, 0);
+                }
+            }
             if constexpr (NCF_SPLIT_LATE) {
                 // unit it - 1 is contracted between barriers A(it) (the chain's layer 1 of unit it
                 // done) and B(it): beside the chain's sections that issue few MFMAs, not beside its
@@ -919,7 +931,8 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
                         const int64_t k = tau * FOLD + c / NGU;
                         const int64_t hs = (un0 + k * ustride) * 16 + (c % NGU) * FOLD;
                         const bool hv = k < nown && hs < n;
-                        const int hu = (int)__builtin_amdgcn_raw_buffer_load_b32(us_rsrc, hv ? (uint32_t)hs * 4u : kDrop, 0, 0);
+                        const int hu = tau == 0 ? phu[q]
+                                                : (int)__builtin_amdgcn_raw_buffer_load_b32(us_rsrc, hv ? (uint32_t)hs * 4u : kDrop, 0, 0);
                         float s1[B1], xo[XW];
                         NCF_LD_HALF(xo, hv && (unsigned)hu < (unsigned)ids.ubound ? hu : 0, li * HB);
                         const uint32_t off = hv ? (uint32_t)(((hs / FOLD) * L1 + li) * 4) : kDrop;

@@ -200,6 +200,7 @@ class NCFEngine(object):
     def _ensure_ws(self, n):
         if n <= self.max_batch:
             return
+        self._discard_counted()  # (a new workspace starts with zero counters)
         L = N.lib()
         nbytes = ctypes.c_size_t()
         N.check(L.ncf_workspace_size(ctypes.byref(self.shape), int(n), ctypes.byref(nbytes)))
@@ -334,6 +335,9 @@ class NCFEngine(object):
         """Clear the index counters holding a next batch's counts (ncf_train_step_ahead) before any
         other index build uses them."""
         if self._counted is not None:
+            # the counted batch's stale rows were caught up ahead with p only (P-ahead rows,
+            # ncf_update.hip): settle them before the batch is given up
+            self.flush()
             # counters only: the sticky error flags stay for check_errors
             N.check(N.lib().ncf_workspace_discard_counts(ctypes.byref(self.shape), self.max_batch, N.ptr(self.ws),
                                                          self.ws_bytes, N.stream_handle(self.device)))
