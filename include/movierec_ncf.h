@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define NCF_ABI_VERSION 8
+#define NCF_ABI_VERSION 9
 #define NCF_MAX_LAYERS 8
 #define NCF_EINVAL (-1)
 #define NCF_EHIP (-2)
@@ -115,7 +115,11 @@ typedef struct ncf_optim {
      * rows set_optimizer_state found at zero).  Such a row is a fixed point of the zero-gradient
      * step (m = b1*0 + 0 = +0, v = +0, p -= (lr_t*0)/(sqrt(0)+eps) = p), so it is current at every
      * step: no replay, no flush traffic, and its first update reads p only.  Initialise row_step
-     * to NCF_ROW_PRISTINE when the moments start at zero. */
+     * to NCF_ROW_PRISTINE when the moments start at zero.
+     * row_step[r] < 0 (set only by ncf_train_step_ahead's catch-up ahead, consumed by the next
+     * step, ncf_lazy_flush or the stale-count gate): row r's p is current, its m and v are at step
+     * -row_step[r] - 2 (the next update re-derives them).  Call ncf_lazy_flush before giving up a
+     * counted-ahead batch (ncf_workspace_discard_counts). */
     int32_t* row_step;
 } ncf_optim_t;
 
@@ -209,7 +213,8 @@ int ncf_shard_workspace_flags(const ncf_shape_t* shape, int64_t max_batch, int32
                               int32_t* flags, void* stream);
 /* Drop the next batch's index counts that ncf_train_step_ahead took (the batch will not be
  * passed after all): clears the index counters only — the sticky error flags and the fold of the
- * last index build stay (ncf_workspace_init would clear them too). */
+ * last index build stay (ncf_workspace_init would clear them too).  Under deferred decay call
+ * ncf_lazy_flush first: the counted batch's rows were caught up ahead with p only (row_step). */
 int ncf_workspace_discard_counts(const ncf_shape_t* shape, int64_t max_batch, void* ws, size_t ws_bytes,
                                  void* stream);
 

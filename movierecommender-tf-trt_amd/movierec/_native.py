@@ -172,7 +172,7 @@ def profile_read(kernel):
     return ms.value, n.value
 
 _lib = None
-ABI_VERSION = 8   # include/movierec_ncf.h ncf_abi_version()
+ABI_VERSION = 9   # include/movierec_ncf.h ncf_abi_version()
 
 
 def lib():
