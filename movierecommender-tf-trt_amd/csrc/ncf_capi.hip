@@ -364,7 +364,7 @@ namespace ncf {
 // the next step starts at its forward/backward (index_ready = 3)
 int build_next_index(const ncf_shape_t& s, const ncf_hyper_t& h, ncf_model_t* model, ncf_optim_t* optim,
                      const int32_t* next_users, const int32_t* next_items, int64_t n, void* ws, size_t ws_bytes,
-                     hipStream_t st) {
+                     hipStream_t st, int gate_ahead) {
     WsLayout L;
     if (int r = check_ws(s, n, ws, ws_bytes, &L)) return r;
     prof_begin(NCF_K_INDEX, st);
@@ -372,9 +372,10 @@ int build_next_index(const ncf_shape_t& s, const ncf_hyper_t& h, ncf_model_t* mo
     prof_end(NCF_K_INDEX, st);
     if (e != hipSuccess) return hip_check(e, "next index");
     prof_begin(NCF_K_CATCHUP, st);
-    // enqueued before ncf_apply_update bumps the step: a stale-count gate replays to *step + 1
+    // gate_ahead 1: enqueued before ncf_apply_update bumps the step, a stale-count gate replays to
+    // *step + 1; 0: after it
     e = launch_emb_catchup(s, L, ws, model->emb, optim->emb_m, optim->emb_v, optim->row_step, optim->step, h, false, st,
-                           true, n, true, next_users, next_items, 1);
+                           true, n, true, next_users, next_items, gate_ahead);
     prof_end(NCF_K_CATCHUP, st);
     return hip_check(e, "next index sort");
 }

@@ -209,9 +209,8 @@ int ncf_user_dp_step_split(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t
     if (int r = hip_ok(hipEventRecord(c->join, side), "join")) return r;
     if (int r = ncf_update_rows_lazy(s, model, optim, h, n, next_users, next_items, n_next, ws, ws_bytes, stream))
         return r;
-    if (next_users)
-        if (int r = ncf::build_next_index(*s, *h, model, optim, next_users, next_items, n_next, ws, ws_bytes, st))
-            return r;
+    // (the next batch's index is built after the item rows' Adam, beside the all-gather below: this
+    // window already holds the own-user update; the all-gather's holds nothing else)
     if (int r = hip_ok(hipStreamWaitEvent(st, c->join, 0), "join wait")) return r;
     // this rank's item slice (its moments indexed by table row) and the dense layers
     const int64_t r0 = item_rank * Ic;
@@ -223,8 +222,15 @@ int ncf_user_dp_step_split(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t
     if (int r = ncf_apply_update(s, model, &items_opt, h, U + (cnt ? r0 : I), cnt, slice_grad, mlp_grad, summary, stats,
                                  ws, ws_bytes, stream))
         return r;
-    if (!exchange) return 0;
-    // the updated slices to every rank (in place), before the next forward pass reads an item row
+    if (!exchange) {
+        if (next_users)  // (after the step's bump)
+            if (int r = ncf::build_next_index(*s, *h, model, optim, next_users, next_items, n_next, ws, ws_bytes, st, 0))
+                return r;
+        return 0;
+    }
+    // the updated slices to every rank (in place) on the side stream, while the compute stream
+    // builds the next batch's index (it reads ids and the own rows' steps, never an item row); the
+    // compute stream waits for the gather before the next forward pass can read an item row
     if (int r = hip_ok(hipEventRecord(c->fork, st), "fork")) return r;
     if (int r = hip_ok(hipStreamWaitEvent(side, c->fork, 0), "fork wait")) return r;
     float* items0 = model->emb + U * W;
@@ -232,6 +238,9 @@ int ncf_user_dp_step_split(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t
                            "ncclAllGather"))
         return r;
     if (int r = hip_ok(hipEventRecord(c->join, side), "join")) return r;
+    if (next_users)  // (after the step's bump)
+        if (int r = ncf::build_next_index(*s, *h, model, optim, next_users, next_items, n_next, ws, ws_bytes, st, 0))
+            return r;
     return hip_ok(hipStreamWaitEvent(st, c->join, 0), "join wait");
 }
 

@@ -333,7 +333,7 @@ __device__ inline void sort_rows_body(const int32_t* __restrict__ offs, int64_t 
 // ncf_user_dp_step's helpers (ncf_capi.hip)
 int build_next_index(const ncf_shape_t& s, const ncf_hyper_t& h, ncf_model_t* model, ncf_optim_t* optim,
                      const int32_t* next_users, const int32_t* next_items, int64_t n, void* ws, size_t ws_bytes,
-                     hipStream_t st);
+                     hipStream_t st, int gate_ahead = 1);
 
 // the thread's ncf_last_error() text (printf format); returns code
 int set_error(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
