@@ -468,48 +468,13 @@ def device_glorot_init_shard(eng, w_small, seed):
     torch.cuda.synchronize()
 
 
-def native_step_check(cfg, world, rank, split, steps=5, per=2048):
-    """At N > 1 over RCCL, before the measured run: the library's one-call user-partitioned step
-    (ncf_user_dp_step / _split: its own communicator, the collective on a side stream beside the
-    own-user update and the next batch's index) against the same step issued call by call with
-    torch.distributed's collectives, from identical state, on config C's model with small tables.
-    Every rank compares its weights, Adam moments and stats; the max difference over the ranks is
-    the result.  The measured run uses the native step only when the two agree (to fp32 order of
-    the cross-rank sums; bitwise when RCCL picks the same reduction order for both)."""
-    from movierec.engine import NCFEngine
-    from movierec.distributed import UserPartitionedDataParallel, partition_keras_weights
-    from movierec.model import initial_weights
-    U, I, g = 4000, 3000, cfg["negs"] + 1
-    w = initial_weights(U, I, cfg["layers"], cfg["gmf_dim"], seed=7)
-    n_loc = (U - rank + world - 1) // world
-    gen = torch.Generator(device="cuda").manual_seed(99 + rank)
-    batches = []
-    for _ in range(steps):
-        u = torch.randint(0, n_loc, (per // g,), generator=gen, device="cuda", dtype=torch.int32).repeat_interleave(g)
-        it = torch.randint(0, I, (per,), generator=gen, device="cuda", dtype=torch.int32)
-        y = torch.tensor([0.0] * (g - 1) + [1.0], device="cuda").repeat(per // g)
-        batches.append((u.contiguous(), it, y))
-    states = []
-    for native in (True, False):
-        eng = NCFEngine(n_loc, I, cfg["layers"], cfg["gmf_dim"], max_batch=per, lazy_adam=True, lazy_rows=n_loc)
-        eng.set_keras_weights(partition_keras_weights(w, world, rank))
-        dp = UserPartitionedDataParallel(eng, native=native, split_items=split)
-        for s_, (u, it, y) in enumerate(batches):
-            nxt = batches[s_ + 1][:2] if s_ + 1 < steps else None
-            dp.train_step(u, it, y, group=g, k=min(10, g - 1), next_batch=nxt)
-        eng.flush()
-        R = eng.num_rows
-        states.append(torch.cat([eng.emb[:R].flatten(), eng.emb_m[:R].flatten(), eng.emb_v[:R].flatten(), eng.mlp,
-                                 eng.mlp_m, eng.mlp_v, eng.stats.float()]))
-        if dp.comm is not None:
-            dp.comm.close()
-    d = (states[0] - states[1]).abs().max().double().reshape(1)
-    same = torch.tensor([0.0 if torch.equal(states[0], states[1]) else 1.0], dtype=torch.float64, device="cuda")
-    t = torch.cat([d, same])
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    torch.cuda.synchronize()
-    return {"max_abs_diff": float(t[0]), "bitwise": bool(t[1] == 0), "steps": steps, "per_rank_batch": per,
-            "tables": "%d x %d" % (U, I), "ok": float(t[0]) <= 1e-5}
+def native_step_check(cfg, world, rank, split):
+    """At N > 1 over RCCL, before the measured run: movierec.distributed.native_step_check — the
+    library's one-call user-partitioned step against the same step issued call by call with
+    torch.distributed's collectives, from identical state, on this config's model with small
+    tables; the measured run uses the native step only when the two agree."""
+    from movierec.distributed import native_step_check as check
+    return check(cfg["layers"], cfg["gmf_dim"], cfg["negs"] + 1, split)
 
 
 def pmc_traffic(kernel, config, batch, mode):

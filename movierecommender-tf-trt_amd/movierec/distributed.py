@@ -386,6 +386,55 @@ def partition_keras_weights(w, world, rank):
     return out
 
 
+_NATIVE_CHECKS = {}
+
+
+def native_step_check(layers, gmf_dim, group_size, split, group=None, steps=5, per=2048):
+    """The library's one-call user-partitioned step (``ncf_user_dp_step`` / ``_split``: its own RCCL
+    communicator, the collectives on a side stream beside the own-user update and the next
+    batch's index) against the same step issued call by call with torch.distributed's
+    collectives, from identical state, on a model of these shapes with small tables (4,000 users x
+    3,000 items), ``steps`` steps of ``per`` samples per rank.  Every rank compares its weights,
+    Adam moments and stats; returns the max difference over the ranks and whether it is within
+    fp32 order of the cross-rank sums (``ok``: <= 1e-5).  A collective: every rank of ``group``
+    calls it."""
+    from .engine import NCFEngine
+    from .model import initial_weights
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    U, I, g = 4000, 3000, int(group_size)
+    per = per // g * g
+    w = initial_weights(U, I, list(layers), int(gmf_dim), seed=7)
+    n_loc = (U - rank + world - 1) // world
+    gen = torch.Generator(device="cuda").manual_seed(99 + rank)
+    batches = []
+    for _ in range(steps):
+        u = torch.randint(0, n_loc, (per // g,), generator=gen, device="cuda", dtype=torch.int32).repeat_interleave(g)
+        it = torch.randint(0, I, (per,), generator=gen, device="cuda", dtype=torch.int32)
+        y = torch.tensor([0.0] * (g - 1) + [1.0], device="cuda").repeat(per // g)
+        batches.append((u.contiguous(), it, y))
+    states = []
+    for native in (True, False):
+        eng = NCFEngine(n_loc, I, list(layers), int(gmf_dim), max_batch=per, lazy_adam=True, lazy_rows=n_loc)
+        eng.set_keras_weights(partition_keras_weights(w, world, rank))
+        dp = UserPartitionedDataParallel(eng, group=group, native=native, split_items=split)
+        for s_, (u, it, y) in enumerate(batches):
+            nxt = batches[s_ + 1][:2] if s_ + 1 < steps else None
+            dp.train_step(u, it, y, group=g, k=min(10, g - 1), next_batch=nxt)
+        eng.flush()
+        R = eng.num_rows
+        states.append(torch.cat([eng.emb[:R].flatten(), eng.emb_m[:R].flatten(), eng.emb_v[:R].flatten(), eng.mlp,
+                                 eng.mlp_m, eng.mlp_v, eng.stats.float()]))
+        if dp.comm is not None:
+            dp.comm.close()
+    d = (states[0] - states[1]).abs().max().double().reshape(1)
+    same = torch.tensor([0.0 if torch.equal(states[0], states[1]) else 1.0], dtype=torch.float64, device="cuda")
+    t = torch.cat([d, same])
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    torch.cuda.synchronize()
+    return {"max_abs_diff": float(t[0]), "bitwise": bool(t[1] == 0), "steps": steps, "per_rank_batch": per,
+            "tables": "%d x %d" % (U, I), "ok": float(t[0]) <= 1e-5}
+
+
 class UserPartitionedDataParallel(object):
     """Data parallelism with the training data partitioned by user.
 
@@ -437,9 +486,18 @@ class UserPartitionedDataParallel(object):
         if getattr(engine, "row_step", None) is not None and lazy != U:
             raise ValueError("a deferred-decay engine for user-partitioned training needs lazy_rows = its %d users "
                              "(the replicated item rows are swept every step)" % U)
+        self.native_check = None
         if native is None:
             native = (dist.get_backend(group) == "nccl" and getattr(engine, "row_step", None) is not None and
                       hasattr(engine, "user_dp_step"))
+            if native and self.world > 1:
+                # a world > 1 run uses the one-call step only after it matched the call-by-call step
+                # on this process group (once per model shape)
+                key = (tuple(engine.layers), int(engine.gmf_dim), bool(split_items), id(group))
+                if key not in _NATIVE_CHECKS:
+                    _NATIVE_CHECKS[key] = native_step_check(engine.layers, engine.gmf_dim, 4, bool(split_items), group)
+                self.native_check = _NATIVE_CHECKS[key]
+                native = self.native_check["ok"]
         self.comm = _native_comm(self.rank, self.world, group) if native else None
         iw = self.world
         if emulate_world is not None and int(emulate_world) > 1:
