@@ -35,6 +35,10 @@
 #include "ncf_common.h"
 #include "ncf_internal.h"
 
+#ifndef NCF_DIAG_SCORE
+#define NCF_DIAG_SCORE 0
+#endif
+
 namespace ncf {
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
@@ -49,20 +53,11 @@ __device__ __forceinline__ sf32x16 mfma16(f16x8 a, f16x8 b, sf32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
 
-// elementwise max of packed halves (v_pk_max_f16, no IEEE canonicalisation of the inputs)
-__device__ __forceinline__ f16x8 pkmax(f16x8 a, f16x8 b) {
-    su32x4 x = __builtin_bit_cast(su32x4, a), y = __builtin_bit_cast(su32x4, b), r;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) asm("v_pk_max_f16 %0, %1, %2" : "=v"(r[i]) : "v"(x[i]), "v"(y[i]));
-    return __builtin_bit_cast(f16x8, r);
-}
+// elementwise max of packed halves: v_pk_maximum3_f16 (a, b, b), no canonicalisation of the
+// inputs, and visible to the compiler's MFMA hazard checks (no inline asm)
+__device__ __forceinline__ f16x8 pkmax(f16x8 a, f16x8 b) { return __builtin_elementwise_maximum(a, b); }
 
-__device__ __forceinline__ f16x8 relu_f16(f16x8 a) {
-    su32x4 x = __builtin_bit_cast(su32x4, a), r;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) asm("v_pk_max_f16 %0, %1, 0" : "=v"(r[i]) : "v"(x[i]));
-    return __builtin_bit_cast(f16x8, r);
-}
+__device__ __forceinline__ f16x8 relu_f16(f16x8 a) { return __builtin_elementwise_maximum(a, f16x8{}); }
 
 // ----------------------------------------------------------------------------- preparation
 
@@ -209,17 +204,6 @@ __device__ __forceinline__ float unkey(int k) { return __int_as_float(k >= 0 ? k
 // admission bound from another range's k-th best g: admit z >= g (ties resolve in the merge)
 __device__ __forceinline__ float below(float g) { return g - fmaxf(fabsf(g) * 1e-6f, 1e-30f); }
 
-typedef _Float16 h2v __attribute__((ext_vector_type(2)));
-
-// relu of two packed halves (v_pk_max_f16 with 0).  Its input must come from a VALU op (here
-// v_cvt_pk_f16_f32), never straight from an MFMA: the compiler's MFMA->VALU hazard padding does
-// not see through inline-asm operands.
-__device__ __forceinline__ h2v relu_h2(h2v a) {
-    uint32_t r;
-    asm("v_pk_max_f16 %0, %1, 0" : "=v"(r) : "v"(__builtin_bit_cast(uint32_t, a)));
-    return __builtin_bit_cast(h2v, r);
-}
-
 template <int KS2, int KS3, int NR3, int KSG>
 __global__ __launch_bounds__(kBlock, 2) void k_score_topk(ScoreArgs a) {
     constexpr int L1P = 16 * KS2;
@@ -255,13 +239,19 @@ __global__ __launch_bounds__(kBlock, 2) void k_score_topk(ScoreArgs a) {
     for (int s = 0; s < KS2; ++s) A2[s] = a.a2[s * 64 + lane];
 #pragma unroll
     for (int s = 0; s < KS3; ++s) A3[s] = a.a3[s * 64 + lane];
-    const f16x8* ag = a.ug + (int64_t)ub * KSG * 64 + lane;  // GMF A fragments, re-read per tile (L1)
+    // GMF A fragments of the wave's 32 users, in registers for the whole sweep
+    f16x8 AG[KSG > 0 ? KSG : 1];
+#pragma unroll
+    for (int s = 0; s < KSG; ++s) AG[s] = a.ug[((int64_t)ub * KSG + s) * 64 + lane];
     sf32x16 init3;
 #pragma unroll
     for (int r = 0; r < 16; ++r) init3[r] = a.init3[h * 16 + r];
-    h2v wh[NR3 / 2];
+    // output layer as one MFMA (K = 16, the layer-3 D rows of lane half h as B): rows 0 and 4
+    // of its A operand hold w_out, so register 0 of EVERY lane ends up with its item's dot
+    f16x8 AO;
 #pragma unroll
-    for (int r = 0; r < NR3 / 2; ++r) wh[r] = h2v{(_Float16)a.wh[h * 16 + 2 * r], (_Float16)a.wh[h * 16 + 2 * r + 1]};
+    for (int e = 0; e < 8; ++e)
+        AO[e] = ((j == 0 || j == 4) && e < NR3) ? (_Float16)a.wh[h * 16 + e] : (_Float16)0.0f;
     const float bo = a.bo[0];
     // lane q (< 32): user q0+q's own k-th best so far (thr) and admission bound (adm >= thr is
     // raised further by the k-th best any other range of the user has published: an item
@@ -277,10 +267,14 @@ __global__ __launch_bounds__(kBlock, 2) void k_score_topk(ScoreArgs a) {
 #pragma unroll
     for (int s = 0; s < KSG; ++s) BG[s] = a.ig[((int64_t)t0 * KSG + s) * 64 + lane];
 
+    // the other ranges' published k-th best, read one tile ahead of its use (a bound: a late
+    // value only admits more candidates, which the exact insertion test then rejects)
+    int gk = fkey(-INFINITY);
+    if (a.splits > 1 && lane < 32) gk = __hip_atomic_load(gth, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (int t = t0; t < t1; ++t) {
         if (a.splits > 1 && lane < 32) {
-            const int gk = __hip_atomic_load(gth, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (gk > pub) adm = fmaxf(adm, below(unkey(gk)));
+            gk = __hip_atomic_load(gth, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         // GMF + output bias of the 32 users x 32 items, parked in LDS ([user][item]) for the
         // user loop; a user's slot is then reused for its flagged logits
@@ -289,42 +283,54 @@ __global__ __launch_bounds__(kBlock, 2) void k_score_topk(ScoreArgs a) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) accg[r] = bo;
 #pragma unroll
-            for (int s = 0; s < KSG; ++s) accg = mfma16(ag[s * 64], BG[s], accg);
+            for (int s = 0; s < KSG; ++s) accg = mfma16(AG[s], BG[s], accg);
 #pragma unroll
             for (int r = 0; r < 16; ++r) s_z[w][drow_s(r, h)][j] = accg[r];
+        }
+        // the next tile's GMF operands: a whole tile in flight
+        if (t + 1 < t1) {
+#pragma unroll
+            for (int s = 0; s < KSG; ++s) BG[s] = a.ig[((int64_t)(t + 1) * KSG + s) * 64 + lane];
         }
 
         const bool item_ok = h == 0 && 32 * t + j < a.num_items;
         uint32_t flagged = 0;
         // per-user operands from LDS, fetched one user ahead of their use
-        float4 ui[4];
-        f16x8 un[KS2];
-        float ug = s_z[w][0][j];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) ui[c] = s_init2[w][0][h * 4 + c];
-#pragma unroll
-        for (int s = 0; s < KS2; ++s) un[s] = *reinterpret_cast<const f16x8*>(&s_nega[w][0][16 * s + 8 * h]);
+        // software pipeline over the 32 users: iteration q runs layer 3 + output of user q beside
+        // layer 2 of user q+1, whose operands were read from LDS one iteration earlier (the reads
+        // for user q+2 are in flight meanwhile); a scheduling barrier closes each iteration, so
+        // the register footprint stays that of one
+        float4 ui[4], vi[4];
+        f16x8 un[KS2], vn[KS2];
+        float ug = s_z[w][0][j], ugn = s_z[w][1][j];
+#define NCF_SCORE_USER_OPS(UI, UN, Q)                                                           \
+    {                                                                                           \
+        if (NCF_DIAG_SCORE != 5)                                                                \
+            _Pragma("unroll") for (int c = 0; c < 4; ++c) UI[c] = s_init2[w][Q][h * 4 + c];     \
+        _Pragma("unroll") for (int s = 0; s < KS2; ++s)                                         \
+            UN[s] = *reinterpret_cast<const f16x8*>(&s_nega[w][Q][16 * s + 8 * h]);             \
+    }
+#define NCF_SCORE_LAYER2(ACC)                                                                   \
+    {                                                                                           \
+        _Pragma("unroll") for (int c = 0; c < 4; ++c) {                                         \
+            ACC[4 * c + 0] = ui[c].x; ACC[4 * c + 1] = ui[c].y;                                 \
+            ACC[4 * c + 2] = ui[c].z; ACC[4 * c + 3] = ui[c].w;                                 \
+        }                                                                                       \
+        _Pragma("unroll") for (int s = 0; s < KS2; ++s) ACC = mfma16(A2[s], pkmax(BC[s], un[s]), ACC); \
+    }
+        NCF_SCORE_USER_OPS(ui, un, 0)
+        sf32x16 acc2;
+        NCF_SCORE_LAYER2(acc2)
+        NCF_SCORE_USER_OPS(ui, un, 1)
 #pragma unroll
         for (int q = 0; q < 32; ++q) {
-            float4 vi[4];
-            f16x8 vn[KS2];
-            float vg = 0.0f;
-            if (q + 1 < 32) {
-                vg = s_z[w][q + 1][j];
-#pragma unroll
-                for (int c = 0; c < 4; ++c) vi[c] = s_init2[w][q + 1][h * 4 + c];
-#pragma unroll
-                for (int s = 0; s < KS2; ++s)
-                    vn[s] = *reinterpret_cast<const f16x8*>(&s_nega[w][q + 1][16 * s + 8 * h]);
+            float ugnn = 0.0f;
+            if (q + 2 < 32) {
+                ugnn = s_z[w][q + 2][j];
+#if NCF_DIAG_SCORE != 1  // diagnostic builds only (wrong results)
+                NCF_SCORE_USER_OPS(vi, vn, q + 2)
+#endif
             }
-            sf32x16 acc2;
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                acc2[4 * c + 0] = ui[c].x; acc2[4 * c + 1] = ui[c].y;
-                acc2[4 * c + 2] = ui[c].z; acc2[4 * c + 3] = ui[c].w;
-            }
-#pragma unroll
-            for (int s = 0; s < KS2; ++s) acc2 = mfma16(A2[s], pkmax(BC[s], un[s]), acc2);
             sf32x16 acc3 = init3;
 #pragma unroll
             for (int s = 0; s < KS3; ++s) {
@@ -333,37 +339,41 @@ __global__ __launch_bounds__(kBlock, 2) void k_score_topk(ScoreArgs a) {
                 for (int e = 0; e < 8; ++e) x[e] = (_Float16)acc2[8 * s + e];
                 acc3 = mfma16(A3[s], relu_f16(x), acc3);
             }
-            // output layer: relu(h3) . w_out in packed halves (cvt_pk, pk_max, dot2: 1.5 ops/feature)
-            float z = 0.0f;
+            if (q + 1 < 32) NCF_SCORE_LAYER2(acc2)
+            // output layer: one MFMA over relu(h3) (zero accumulator), then the GMF term + bias
+            f16x8 x3;
 #pragma unroll
-            for (int r = 0; r < NR3 / 2; ++r) {
-                const h2v hv = relu_h2(h2v{(_Float16)acc3[2 * r], (_Float16)acc3[2 * r + 1]});
-                z = __builtin_amdgcn_fdot2(hv, wh[r], z, false);
-            }
-            z += h == 0 ? ug : 0.0f;
-            // v_permlane32_swap(vdst = z, src = z): the new src holds the upper half's z in lanes
-            // 0-31, so lanes 0-31 (the only ones read below) get the full sum
-            const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(z), __float_as_uint(z), false, false);
-            z += __uint_as_float(sw[1]);
+            for (int e = 0; e < 8; ++e) x3[e] = e < NR3 ? (_Float16)acc3[e] : (_Float16)0.0f;
+            const sf32x16 acc4 = mfma16(AO, relu_f16(x3), sf32x16{});
+            const float z = acc4[0] + ug;
+            // branch-free: both lane halves hold the same z (rows 0 and 4) and store it to the
+            // user's slot (its GMF value was read two users ahead); the flag is a scalar select
+            s_z[w][q][j] = z;
             const float tq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(adm), q));
-            if (__ballot(item_ok && z > tq)) {
-                if (h == 0) s_z[w][q][j] = z;
-                flagged |= 1u << q;
-            }
-            if (q + 1 < 32) {
-                ug = vg;
+            flagged |= __ballot(item_ok && z > tq) ? (1u << q) : 0u;
+            ug = ugn;
+            ugn = ugnn;
+            if (q + 2 < 32) {
 #pragma unroll
                 for (int c = 0; c < 4; ++c) ui[c] = vi[c];
 #pragma unroll
                 for (int s = 0; s < KS2; ++s) un[s] = vn[s];
             }
+            __builtin_amdgcn_sched_barrier(0);
         }
+#undef NCF_SCORE_LAYER2
+#undef NCF_SCORE_USER_OPS
         // the next tile's item operands: loads in flight over the insertions below
+#if NCF_DIAG_SCORE == 2
+        flagged = 0;
+#endif
+#if NCF_DIAG_SCORE == 4
+        if (false) {
+#else
         if (t + 1 < t1) {
+#endif
 #pragma unroll
             for (int s = 0; s < KS2; ++s) BC[s] = a.ic[((int64_t)(t + 1) * KS2 + s) * 64 + lane];
-#pragma unroll
-            for (int s = 0; s < KSG; ++s) BG[s] = a.ig[((int64_t)(t + 1) * KSG + s) * 64 + lane];
         }
         // insertions (rare once the lists fill): ascending item order, ties keep the earlier item
         while (flagged) {

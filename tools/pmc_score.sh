@@ -1,15 +1,7 @@
-cd /tmp && export TMPDIR=/tmp
-R=$GRAFT_REPO_ROOT
-mkdir -p $R/gpurun_out/scpmc
-SU=20000 timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MFMA SQ_INSTS_VALU --kernel-include-regex k_score_topk --output-format csv -d $R/gpurun_out/scpmc/p1 -o run -- python3 $R/tools/score_timing.py > $R/gpurun_out/scpmc/p1.log 2>&1
-SU=20000 timeout -s KILL 90 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_WAVES SQ_INST_CYCLES_VMEM SQ_LDS_BANK_CONFLICT --kernel-include-regex k_score_topk --output-format csv -d $R/gpurun_out/scpmc/p2 -o run -- python3 $R/tools/score_timing.py > $R/gpurun_out/scpmc/p2.log 2>&1
-cd $R && python3 - <<'PY'
-import csv,glob
-for p in ["p1","p2"]:
-    for f in glob.glob("gpurun_out/scpmc/%s/*counter_collection.csv"%p):
-        rows=list(csv.DictReader(open(f)))
-        agg={}
-        for r in rows:
-            agg.setdefault(r["Counter_Name"],[]).append(float(r["Counter_Value"]))
-        for k,v in agg.items(): print(p,k,len(v),v[-1])
-PY
+# GPU box: two PMC passes over the config E scorer (bench.py --config E, 2 steps).  Usage: bash tools/pmc_score.sh OUT
+O=${1:-gpurun_out/pmc_score}; mkdir -p $O
+cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+A="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE"
+B="SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU SQ_ACTIVE_INST_LDS SQ_WAVES GRBM_GUI_ACTIVE"
+timeout -s KILL 240 rocprofv3 --pmc $A -d $O/a -o pmc --output-format csv -- python bench.py --config E --steps 2 --warmup 1 --no-cpu-baseline > $O/a.log 2>&1 &&
+timeout -s KILL 240 rocprofv3 --pmc $B -d $O/b -o pmc --output-format csv -- python bench.py --config E --steps 2 --warmup 1 --no-cpu-baseline > $O/b.log 2>&1
