@@ -294,6 +294,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_score_topk(ScoreArgs a) {
         }
 
         const bool item_ok = h == 0 && 32 * t + j < a.num_items;
+        const uint64_t okm = __builtin_amdgcn_ballot_w64(item_ok);
         uint32_t flagged = 0;
         // per-user operands from LDS, fetched one user ahead of their use
         // software pipeline over the 32 users: iteration q runs layer 3 + output of user q beside
@@ -316,7 +317,8 @@ __global__ __launch_bounds__(kBlock, 2) void k_score_topk(ScoreArgs a) {
             ACC[4 * c + 0] = ui[c].x; ACC[4 * c + 1] = ui[c].y;                                 \
             ACC[4 * c + 2] = ui[c].z; ACC[4 * c + 3] = ui[c].w;                                 \
         }                                                                                       \
-        _Pragma("unroll") for (int s = 0; s < KS2; ++s) ACC = mfma16(A2[s], pkmax(BC[s], un[s]), ACC); \
+        _Pragma("unroll") for (int s = 0; s < KS2; ++s)                                         \
+            ACC = mfma16(A2[s], NCF_DIAG_SCORE == 6 ? BC[s] : pkmax(BC[s], un[s]), ACC);        \
     }
         NCF_SCORE_USER_OPS(ui, un, 0)
         sf32x16 acc2;
@@ -331,6 +333,9 @@ __global__ __launch_bounds__(kBlock, 2) void k_score_topk(ScoreArgs a) {
                 NCF_SCORE_USER_OPS(vi, vn, q + 2)
 #endif
             }
+            // keep those reads at the top of the iteration (the scheduler would sink them to the
+            // end, next to their use, and expose the LDS latency)
+            __builtin_amdgcn_sched_barrier(0);
             sf32x16 acc3 = init3;
 #pragma unroll
             for (int s = 0; s < KS3; ++s) {
@@ -344,13 +349,17 @@ __global__ __launch_bounds__(kBlock, 2) void k_score_topk(ScoreArgs a) {
             f16x8 x3;
 #pragma unroll
             for (int e = 0; e < 8; ++e) x3[e] = e < NR3 ? (_Float16)acc3[e] : (_Float16)0.0f;
+#if NCF_DIAG_SCORE == 7
+            const float z = acc3[0] + ug;
+#else
             const sf32x16 acc4 = mfma16(AO, relu_f16(x3), sf32x16{});
             const float z = acc4[0] + ug;
+#endif
             // branch-free: both lane halves hold the same z (rows 0 and 4) and store it to the
             // user's slot (its GMF value was read two users ahead); the flag is a scalar select
             s_z[w][q][j] = z;
             const float tq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(adm), q));
-            flagged |= __ballot(item_ok && z > tq) ? (1u << q) : 0u;
+            flagged |= (__builtin_amdgcn_ballot_w64(z > tq) & okm) ? (1u << q) : 0u;
             ug = ugn;
             ugn = ugnn;
             if (q + 2 < 32) {
@@ -390,7 +399,11 @@ __global__ __launch_bounds__(kBlock, 2) void k_score_topk(ScoreArgs a) {
                 const float zc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(zl), c));
                 if (!(zc > tq)) continue;
                 const int p = __popcll(__ballot(lane < K && ent.x >= zc));
-                const float px = __shfl_up(ent.x, 1, 64), py = __shfl_up(ent.y, 1, 64);
+                // lane i <- lane i-1 (DPP wave_shr:1; lane 0 keeps its own, and never takes it)
+                const float px = __int_as_float(__builtin_amdgcn_update_dpp(
+                    __float_as_int(ent.x), __float_as_int(ent.x), 0x138, 0xf, 0xf, false));
+                const float py = __int_as_float(__builtin_amdgcn_update_dpp(
+                    __float_as_int(ent.y), __float_as_int(ent.y), 0x138, 0xf, 0xf, false));
                 if (lane == p) ent = make_float2(zc, __int_as_float(32 * t + c));
                 else if (lane > p) ent = make_float2(px, py);
                 tk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ent.x), K - 1));
