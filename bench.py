@@ -335,7 +335,9 @@ def score_main(args, cfg, world, rank):
                        "parallelism": "users split across %d ranks" % world},
             "roofline": {"bound": "mfma", "kernel": "k_score_topk (+ k_score_merge)", "achieved": round(achieved, 1),
                          "peak": FP16_MFMA_PEAK_TFS, "unit": "TFLOP/s", "frac": round(achieved / FP16_MFMA_PEAK_TFS, 4),
-                         "traffic": None, "algorithmic_flops_per_pair": fl, "naive_flops_per_pair": fl_naive,
+                         "traffic": pmc_traffic("k_score_topk", "E", U, "all-items") if world == 1 else None,
+                         "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/traffic/)",
+                         "algorithmic_flops_per_pair": fl, "naive_flops_per_pair": fl_naive,
                          "avg_launch_ms": round(kern_ms, 4)},
             "cpu_baseline": cpu}))
     if dist.is_initialized():
