@@ -214,8 +214,22 @@ def check(rc):
 
 
 def ptr(t):
-    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+    """A tensor's device address for a ``c_void_p`` parameter (every entry point has its argtypes
+    set, so the int converts in C); None passes NULL."""
+    return t.data_ptr() if t is not None else None
+
+
+# the current stream as a raw handle without building a torch Stream object (host issue cost of
+# the small-batch step); torch.cuda.current_stream where the private call is absent
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
 
 
 def stream_handle(device=None):
-    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+    """The current HIP stream of ``device`` (None, an index or a torch.device) as an int address."""
+    if _RAW_STREAM is not None:
+        if isinstance(device, int):
+            return _RAW_STREAM(device)
+        if device is None or torch.device(device).index is None:
+            return _RAW_STREAM(torch.cuda.current_device())
+        return _RAW_STREAM(torch.device(device).index)
+    return torch.cuda.current_stream(device).cuda_stream

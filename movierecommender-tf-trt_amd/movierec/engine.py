@@ -80,6 +80,9 @@ class NCFEngine(object):
         self.device = torch.device(device)
         if self.device.type != "cuda":
             raise RuntimeError("NCFEngine needs a HIP device (got %s); there is no CPU path" % self.device)
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        self._dev_idx = self.device.index
         L = N.lib()
         self.layers = [int(x) for x in layers_sizes]
         self.gmf_dim = int(gmf_dim)
@@ -249,6 +252,10 @@ class NCFEngine(object):
 
     # ------------------------------------------------------------- hot path
     def _ids(self, x):
+        # fast path (the step's host issue cost): a 1-D contiguous int32 tensor on this device as is
+        if (type(x) is torch.Tensor and x.dtype is torch.int32 and x.is_cuda and x.dim() == 1 and
+                x.is_contiguous() and x.get_device() == self._dev_idx):
+            return x
         if not torch.is_tensor(x):
             x = torch.from_numpy(np.ascontiguousarray(np.asarray(x).reshape(-1), dtype=np.int32))
         if x.dtype != torch.int32:
@@ -256,6 +263,9 @@ class NCFEngine(object):
         return x.reshape(-1).to(self.device, non_blocking=True).contiguous()
 
     def _labels(self, y):
+        if (type(y) is torch.Tensor and y.dtype is torch.float32 and y.is_cuda and y.dim() == 1 and
+                y.is_contiguous() and y.get_device() == self._dev_idx):
+            return y
         if not torch.is_tensor(y):
             y = torch.from_numpy(np.ascontiguousarray(np.asarray(y).reshape(-1), dtype=np.float32))
         return y.reshape(-1).to(device=self.device, dtype=torch.float32, non_blocking=True).contiguous()
@@ -305,7 +315,7 @@ class NCFEngine(object):
                 N.check(N.lib().ncf_train_step_ahead(
                     ctypes.byref(self.shape), ctypes.byref(self.model_s), ctypes.byref(self.optim_s), ctypes.byref(h),
                     N.ptr(u), N.ptr(i), N.ptr(y), n, N.ptr(nu), N.ptr(ni), nu.numel(), N.ptr(self.stats),
-                    N.ptr(probs_out), N.ptr(self.ws), self.ws_bytes, N.stream_handle(self.device)))
+                    N.ptr(probs_out), N.ptr(self.ws), self.ws_bytes, N.stream_handle(self._dev_idx)))
                 # holds the tensors (their memory stays theirs) and their versions: an in-place
                 # refill through torch (copy_, fill_, index assignment) bumps _version and the next
                 # call rebuilds the index; writes that bypass torch's version counter are caught on
@@ -315,7 +325,7 @@ class NCFEngine(object):
                 N.check(N.lib().ncf_train_step(ctypes.byref(self.shape), ctypes.byref(self.model_s),
                                                ctypes.byref(self.optim_s), ctypes.byref(h), N.ptr(u), N.ptr(i),
                                                N.ptr(y), n, N.ptr(self.stats), N.ptr(probs_out), N.ptr(self.ws),
-                                               self.ws_bytes, N.stream_handle(self.device)))
+                                               self.ws_bytes, N.stream_handle(self._dev_idx)))
         finally:
             h.index_ready = 0
         self._dirty = self.row_step is not None
