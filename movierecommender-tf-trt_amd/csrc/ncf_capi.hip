@@ -251,6 +251,7 @@ WsLayout make_layout(const ncf_shape_t& s, int64_t B, int world) {
         if ((int64_t)world * per > L.list_cap) L.list_cap = (int64_t)world * per;
     }
     L.cnt = take((size_t)(K + 1) * 4);
+    L.cnt_ahead = take((size_t)(K + 1) * 4);  // right behind cnt: one memset clears both
     L.heavy_n = take(4);
     L.err = take(4);
     L.ifold = take(4);
@@ -310,6 +311,8 @@ WsLayout make_layout(const ncf_shape_t& s, int64_t B, int world) {
     } else {
         L.touched = take((size_t)(R < 2 * B ? R : 2 * B) * 4);
         L.touched_oc = take((size_t)(R < 2 * B ? R : 2 * B) * 8);
+        L.heavy = take((size_t)(2 * B / kHeavyMin + 1) * 4);
+        L.slist = take((size_t)2 * B * 4);
     }
     L.act = take((size_t)B * A * 4);
     L.dz = take((size_t)B * D * 4);
@@ -321,6 +324,7 @@ WsLayout make_layout(const ncf_shape_t& s, int64_t B, int world) {
 WsLayout owner_view(const WsLayout& L, int64_t m) {
     WsLayout o = L;
     o.cnt = L.ocnt;
+    o.cnt_ahead = L.ocnt;  // (the owner index never counts ahead)
     o.heavy_n = L.oheavy;
     o.ifold = L.oifold;
     o.offs_local = L.ooffs_local;
@@ -486,8 +490,10 @@ int ncf_workspace_discard_counts(const ncf_shape_t* s, int64_t max_batch, void* 
     if (int r = check_shape(s)) return r;
     ncf::WsLayout L = ncf::make_layout(*s, max_batch);
     if (!ws || ws_bytes < L.total) return fail(NCF_EINVAL, "workspace too small");
-    // the index counters only: the sticky error flags and the last build's fold stay
-    return hip_check(hipMemsetAsync(ncf::at<int32_t>(ws, L.cnt), 0, (size_t)(L.keys + 1) * 4, (hipStream_t)stream),
+    // the index counters only (cursors and counts taken ahead, adjacent): the sticky error flags and
+    // the last build's fold stay
+    return hip_check(hipMemsetAsync(ncf::at<int32_t>(ws, L.cnt), 0, L.cnt_ahead - L.cnt + (size_t)(L.keys + 1) * 4,
+                                    (hipStream_t)stream),
                      "counter clear");
 }
 
@@ -564,17 +570,21 @@ static int index_join(hipStream_t st, FbOut& fb) {
 // index build + forward/backward (+ group metrics): shared by train_step and forward_backward
 // sharded: ids are the compact ids of the last ncf_shard_plan (model->emb = its unique rows)
 // after_index(ctx) (optional) runs once the index is enqueued, before the forward/backward
+// fill (optional): the wave kernel's weight-gradient waves build the index (a batch counted and
+// scanned ahead; fill_in_kernel): no index launch, no catch-up / sort launch
 static int run_fb(const ncf_shape_t& s, const ncf::WsLayout& L, const ncf_model_t* model, const ncf_hyper_t* h,
                   const int32_t* users, const int32_t* items, const float* labels, int64_t n, void* ws,
                   float* probs_out, FbOut* out, hipStream_t st, bool sharded = false,
-                  int (*after_index)(void*) = nullptr, void* ctx = nullptr) {
+                  int (*after_index)(void*) = nullptr, void* ctx = nullptr, const ncf::FillArgs* fill = nullptr) {
     hipError_t e = hipSuccess;
     ncf::IdSpace ids = ncf::table_ids(s);
     const int fold = index_fold(s, h);
     const int variant = use_fused(s, h) ? fb_variant(s, h, n) : -1;
     const bool unit = variant == NCF_FB_UNIT || variant == NCF_FB_WAVE;
     bool check_fold = false;  // the unit / wave kernels check an earlier call's index fold themselves
-    if (sharded || (h->index_ready == 1 && !after_index) || h->index_ready == 3) {
+    if (fill) {
+        if (variant != NCF_FB_WAVE || sharded) return fail(NCF_EINVAL, "in-kernel index fill: wave kernel only");
+    } else if (sharded || (h->index_ready == 1 && !after_index) || h->index_ready == 3) {
         // the index was built by an earlier call — ncf_shard_plan (compact ids), ncf_build_index
         // (the deferred-decay step needs the touched-row list too and builds its own), or the
         // previous ncf_user_dp_step (index_ready 3: list, touched rows and catch-up all done): it
@@ -615,7 +625,7 @@ static int run_fb(const ncf_shape_t& s, const ncf::WsLayout& L, const ncf_model_
     if (variant == NCF_FB_WAVE)
         e = ncf::launch_fb_wave(s, L, ws, model->emb, model->mlp, users, items, labels, n, h->inv_batch, ids,
                                 h->group, h->k, &out->nslab, &out->nbce, &out->nmet, st, fold, check_fold,
-                                h->force_generic == 6);
+                                h->force_generic == 6, fill);
     else if (unit)
         e = ncf::launch_fb_unit(s, L, ws, model->emb, model->mlp, users, items, labels, n, h->inv_batch, ids,
                                 h->group, h->k, &out->nslab, &out->nbce, &out->nmet, st, fold, h->mlp_bf16 != 0,
@@ -666,6 +676,34 @@ static int check_train_args(const ncf_shape_t* s, const ncf_model_t* model, cons
     return 0;
 }
 
+#ifndef NCF_FILL_IN_KERNEL
+#define NCF_FILL_IN_KERNEL 1  // 0: the fill and list-sort launches of round 4 (timing comparisons)
+#endif
+// The step's index from the wave kernel's weight-gradient waves (FillArgs): a batch counted and
+// scanned ahead by the previous step (index_ready 2, deferred-decay Adam), the split wave kernel,
+// a key space the fill's prefix table holds, one stream.  The lists stay unsorted (the touched-row
+// update orders them), and the counted rows were caught up by the previous step's update launch.
+// (A batch whose ids changed after they were counted is flagged as before, NCF_WSERR_STALE_COUNT;
+// the rows the counted set missed are then read by this forward pass at their last step — there
+// is no launch before it to replay them — and settled when next touched or flushed.)
+static bool fill_in_kernel(const ncf_shape_t& s, const ncf::WsLayout& L, const ncf_hyper_t* h, int64_t n) {
+    return NCF_FILL_IN_KERNEL && h->index_ready == 2 && h->optimizer == NCF_OPT_ADAM && side_stream_mode() == 0 &&
+           use_fused(s, h) && fb_variant(s, h, n) == NCF_FB_WAVE && h->force_generic != 6 &&
+           ncf::wave_fill_supported(s) && L.world == 0 && L.nscan <= ncf::kMaxFillScan &&
+           ncf::unsorted_heavy_c(s) >= ncf::kHeavyMin;
+}
+
+static ncf::FillArgs fill_args(const ncf_shape_t& s, const ncf::WsLayout& L, void* ws) {
+    using ncf::at;
+    return ncf::FillArgs{at<int32_t>(ws, L.cnt), at<const int32_t>(ws, L.offs_local), at<const int32_t>(ws, L.tot),
+                         at<const int32_t>(ws, L.uloc), at<const int32_t>(ws, L.utot), L.nscan, L.keys + 1,
+                         at<int32_t>(ws, L.offs), at<int32_t>(ws, L.list), at<int32_t>(ws, L.touched),
+                         at<int2>(ws, L.touched_oc), at<int32_t>(ws, L.nuniq), at<int32_t>(ws, L.heavy),
+                         at<int32_t>(ws, L.heavy_n), ncf::unsorted_heavy_c(s), at<int32_t>(ws, L.err),
+                         at<int32_t>(ws, L.ifold), s.num_users, s.num_items, L.list_cap,
+                         L.keys < 2 * L.max_batch ? L.keys : 2 * L.max_batch, 2 * L.max_batch / ncf::kHeavyMin + 1};
+}
+
 static int train_step_impl(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* h,
                            const int32_t* users, const int32_t* items, const float* labels, int64_t n,
                            const int32_t* next_users, const int32_t* next_items, int64_t n_next, double* stats,
@@ -690,8 +728,10 @@ static int train_step_impl(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t
     // deferred decay on one stream: the group metrics (groups <= 8 the kernel does not compute)
     // ride in the touched-row update launch
     fb.defer_metrics = lazy && side_stream_mode() == 0;
+    const bool kfill = lazy && fill_in_kernel(*s, L, h, n);
+    const ncf::FillArgs fa = kfill ? fill_args(*s, L, ws) : ncf::FillArgs{};
     if (int r = run_fb(*s, L, model, h, users, items, labels, n, ws, probs_out, &fb, st, false,
-                       lazy ? catchup_touched : nullptr, &cc))
+                       lazy && !kfill ? catchup_touched : nullptr, &cc, kfill ? &fa : nullptr))
         return r;
     // the index (side stream) must be complete before the side stream takes the dense tail
     if (int r = index_join(st, fb)) return r;
@@ -737,7 +777,7 @@ static int train_step_impl(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t
         e = ncf::launch_emb_update_touched(*s, L, ws, model->emb, optim->emb_m, optim->emb_v, optim->row_step,
                                            optim->step, *h, st, next_users, next_items, n_next,
                                            mlp_def.p ? &mlp_def : nullptr, index_fold(*s, h),
-                                           fb.met.nblocks > 0 ? &fb.met : nullptr);
+                                           fb.met.nblocks > 0 ? &fb.met : nullptr, nullptr, kfill);
     else
         e = ncf::launch_emb_update(*s, L, ws, model->emb, optim->emb_m, optim->emb_v, optim->step, *h, nullptr,
                                    s->num_rows, st);

@@ -21,6 +21,12 @@ constexpr int kSlabSplit = 16;         // first-level slab reduction fan-in grou
 constexpr int kUpdateGrid = 2048;      // grid of the embedding-table sweep (fixed: deterministic partials)
 constexpr int64_t kMaxBatch = 262144;  // heavy-segment bitmap must fit the LDS (2*B bits = 64 KB)
 constexpr int kFillBigScan = 256;      // scan blocks above which the index fill uses k_prefix + k_fill_big
+constexpr int kMaxFillScan = 128;      // scan blocks (262,144 keys) the in-kernel index fill holds (FillArgs)
+constexpr int kHeavyMin = 8;           // smallest list length the touched-row update leaves to its heavy blocks
+
+#ifndef NCF_DEBUG_BOUNDS
+#define NCF_DEBUG_BOUNDS 0   // 1: printf + skip on out-of-range index-path accesses (diagnostic builds)
+#endif
 
 // Scalars every kernel of a step reads (device copy of hyper + derived).
 struct StepScalars {
@@ -30,7 +36,10 @@ struct StepScalars {
 
 // Byte offsets of the workspace regions (host-computed, passed by value).
 struct WsLayout {
-    size_t cnt;       // int32[R+1]  persistent, all-zero between calls
+    size_t cnt;       // int32[R+1]  persistent, all-zero between calls: the index fill's per-key cursors
+    size_t cnt_ahead; // int32[R+1]  persistent, all-zero between calls: the NEXT batch's counts, taken by
+                      // the touched-row update; the scan ahead copies them into cnt and zeroes them, so
+                      // the fill of one batch and the count of the next never share a counter
     size_t heavy_n;   // int32       persistent
     size_t err;       // int32       persistent (sticky id-out-of-range flag)
     size_t persistent_end;
@@ -59,6 +68,9 @@ struct WsLayout {
     size_t nuniq;     // int32       number of unique rows (single table: of touched rows)
     size_t touched;   // int32[min(R, 2B)] single table, deferred decay: the touched rows, ascending
     size_t touched_oc;  // int2[min(R, 2B)] their (list offset, contribution count): the update needs no offs
+    size_t heavy;     // int32[2B / kHeavyMin + 1] single table: touched-list positions of the rows whose
+                      // lists the touched-row update sorts block-wide (FillArgs); count in heavy_n
+    size_t slist;     // int32[2B] single table: the heavy rows' sorted lists (indexed like list)
     size_t act;       // float[B * A] generic kernel activations
     size_t dz;        // float[B * D] generic kernel pre-activation grad
     size_t ones;      // float[B] layered path: all-ones vector (column sums as GEMV)ients
@@ -112,10 +124,14 @@ __device__ __forceinline__ bool wave_run_count(int32_t* __restrict__ cnt, int ke
     return false;
 }
 
+// move_to (optional): the counts were taken ahead (ws cnt_ahead); they also move to the fill's
+// cursors move_to (ws cnt) and cnt is zeroed for the next batch's count
 template <bool UNIQ>
-__device__ inline void scan_local_body(const int32_t* __restrict__ cnt, int64_t r1, int32_t* __restrict__ offs,
+// (cnt is written through when moving: not a const __restrict__ pointer, whose memory the compiler
+// may assume nothing writes)
+__device__ inline void scan_local_body(const int32_t* cnt, int64_t r1, int32_t* __restrict__ offs,
                                        int32_t* __restrict__ tot, int32_t* __restrict__ uloc,
-                                       int32_t* __restrict__ utot, int blk) {
+                                       int32_t* __restrict__ utot, int blk, int32_t* __restrict__ move_to = nullptr) {
     __shared__ int sw[4];
     const int64_t base = (int64_t)blk * kScanBlock + threadIdx.x * 8;
     // 8 keys per thread: two int4 loads / stores when all 8 are inside (the workspace regions
@@ -129,6 +145,19 @@ __device__ inline void scan_local_body(const int32_t* __restrict__ cnt, int64_t 
     } else {
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = (base + j < r1) ? cnt[base + j] : 0;
+    }
+    if (move_to) {
+        int32_t* zc = const_cast<int32_t*>(cnt);
+        if (full) {
+            *reinterpret_cast<int4*>(move_to + base) = make_int4(v[0], v[1], v[2], v[3]);
+            *reinterpret_cast<int4*>(move_to + base + 4) = make_int4(v[4], v[5], v[6], v[7]);
+            *reinterpret_cast<int4*>(zc + base) = make_int4(0, 0, 0, 0);
+            *reinterpret_cast<int4*>(zc + base + 4) = make_int4(0, 0, 0, 0);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (base + j < r1) move_to[base + j] = v[j], zc[base + j] = 0;
+        }
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -170,6 +199,9 @@ __device__ inline void scan_local_body(const int32_t* __restrict__ cnt, int64_t 
         }
         if (threadIdx.x == 0) utot[blk] = utotal;
     }
+#if NCF_DEBUG_BOUNDS
+    if (move_to && threadIdx.x == 0 && blk < 4) printf("scan ahead blk %d: tot %d utot %d\n", blk, total, 0);
+#endif
 }
 
 // User-row folding (the north star's duplicate-index reduction, done where the gradients are
@@ -330,6 +362,186 @@ __device__ inline void sort_rows_body(const int32_t* __restrict__ offs, int64_t 
     }
 }
 
+// In-kernel index fill (a batch counted and scanned ahead; single-table keys, touched list):
+// k_fill's outputs, computed by the waves of another launch that would otherwise wait (the wave
+// kernel's weight-gradient waves before their first unit), so the step has no fill launch.  The
+// lists are left UNSORTED: the touched-row update orders each row's list itself (rows of up to hc
+// entries across the lanes of their row group, longer ones — listed in `heavy` — block-wide).  A
+// run that takes a counter below zero gives the excess back (k_fill_big's rule): a residue can
+// only sit at a counted key, i.e. in the touched list, where the update checks it.
+struct FillArgs {
+    int32_t* cnt;             // per-key cursors: the counts the scan ahead copied (ws cnt)
+    const int32_t* local;     // per-scan-block exclusive offsets (ws offs_local)
+    const int32_t* tot;       // scan-block totals
+    const int32_t* uloc;      // occupied-key numbering, per scan block
+    const int32_t* utot;
+    int nscan;                // <= kMaxFillScan
+    int64_t r1;               // keys + 1
+    int32_t* offs;            // key -> first list slot
+    int32_t* list;
+    int32_t* touched;         // touched rows, ascending
+    int2* toc;                // their (list offset, count)
+    int32_t* nuniq;
+    int32_t* heavy;           // touched-list positions of the rows with more than hc entries
+    int32_t* heavy_n;         // zeroed by the scan ahead
+    int hc;
+    int32_t* err;
+    int32_t* ifold;
+    int32_t U, I;             // user u -> key u, item v -> key U + v
+    int64_t list_cap, touched_cap, heavy_cap;  // region sizes (debug bound checks)
+};
+#if NCF_DEBUG_BOUNDS
+#define NCF_BOUND(cond, ...)          \
+    if (!(cond)) {                    \
+        printf(__VA_ARGS__);          \
+    } else
+#else
+#define NCF_BOUND(cond, ...)
+#endif
+
+// Wave gw of nw: its share of the fill of batch (users, items, n) folded by `fold`.  The
+// exclusive prefixes of the scan-block totals stay in registers (lane l: blocks l and l + 64) and
+// are read with lane shuffles, so every loop below is wave-uniform.
+__device__ inline void fill_wave(const FillArgs& f, const int32_t* __restrict__ users,
+                                 const int32_t* __restrict__ items, int64_t n, int fold, int gw, int nw) {
+    const int lane = threadIdx.x & 63;
+    int p0, p1, q0, q1;  // pre[lane], pre[lane + 64], upre[lane], upre[lane + 64]
+    {
+        const int t0 = lane < f.nscan ? f.tot[lane] : 0, t1 = lane + 64 < f.nscan ? f.tot[lane + 64] : 0;
+        const int u0 = lane < f.nscan ? f.utot[lane] : 0, u1 = lane + 64 < f.nscan ? f.utot[lane + 64] : 0;
+        int a0 = t0, a1 = t1, b0 = u0, b1 = u1;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int x0 = __shfl_up(a0, d, 64), x1 = __shfl_up(a1, d, 64);
+            const int y0 = __shfl_up(b0, d, 64), y1 = __shfl_up(b1, d, 64);
+            if (lane >= d) a0 += x0, a1 += x1, b0 += y0, b1 += y1;
+        }
+        const int ca = __shfl(a0, 63, 64), cb = __shfl(b0, 63, 64);
+        p0 = a0 - t0;
+        p1 = ca + a1 - t1;
+        q0 = b0 - u0;
+        q1 = cb + b1 - u1;
+#if NCF_DEBUG_BOUNDS
+        if (gw == 0 && lane < 4 && lane < f.nscan)
+            printf("fill lane %d: tot %d utot %d pre %d upre %d nscan %d\n", lane, t0, u0, p0, q0, f.nscan);
+#endif
+    }
+    // prefix of scan block b (b < kMaxFillScan), every lane its own b
+    auto pre = [&](int64_t key) {
+        const int b = (int)(key / kScanBlock);
+        const int x = __shfl(p0, b & 63, 64), y = __shfl(p1, b & 63, 64);
+        return b < 64 ? x : y;
+    };
+    auto upre = [&](int64_t key) {
+        const int b = (int)(key / kScanBlock);
+        const int x = __shfl(q0, b & 63, 64), y = __shfl(q1, b & 63, 64);
+        return b < 64 ? x : y;
+    };
+    const int64_t K = f.r1 - 1;
+    const int64_t rstep = (int64_t)nw * 64;
+    // rows: offsets, the touched list with (offset, count), the heavy rows (RU rows per lane and
+    // pass, their loads issued together)
+    constexpr int RU = 4;
+    for (int64_t rw = (int64_t)gw * 64; rw < f.r1; rw += RU * rstep) {
+        int lo[RU], lo1[RU], ul[RU];
+#pragma unroll
+        for (int j = 0; j < RU; ++j) {
+            const int64_t r = rw + j * rstep + lane;
+            lo[j] = r < f.r1 ? f.local[r] : 0;
+            lo1[j] = r < K ? f.local[r + 1] : 0;
+            ul[j] = r < K ? f.uloc[r] : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < RU; ++j) {
+            const int64_t r = rw + j * rstep + lane;
+            const int64_t rc = r < f.r1 ? r : K;  // (shuffles: every lane)
+            const int o = lo[j] + pre(rc);
+            const int o1 = lo1[j] + pre(rc < K ? rc + 1 : K);
+            const int u = ul[j] + upre(rc);
+            if (r < f.r1) f.offs[r] = o;
+            if (r < K && o1 > o) {
+                NCF_BOUND(u >= 0 && u < f.touched_cap && o >= 0 && o1 <= f.list_cap,
+                          "fill row %lld: u %d (cap %lld) o %d o1 %d (list cap %lld)\n", (long long)r, u,
+                          (long long)f.touched_cap, o, o1, (long long)f.list_cap) {
+                f.touched[u] = (int)r;
+                f.toc[u] = make_int2(o, o1 - o);
+                if (o1 - o > f.hc) {
+                    const int hx = atomicAdd(f.heavy_n, 1);
+                    NCF_BOUND(hx < f.heavy_cap, "fill heavy %d cap %lld\n", hx, (long long)f.heavy_cap)
+                    f.heavy[hx] = u;
+                }
+                }
+            }
+        }
+    }
+    {
+        const int nu = f.uloc[K] + upre(K);
+        if (gw == 0 && lane == 0) {
+            *f.nuniq = nu;
+            *f.ifold = fold;
+        }
+    }
+    // contributions c = 2i + side, a wave at a time (k_fill's runs: equal keys two lanes apart share
+    // one atomic; slot order inside a key is free, the update sorts)
+    const int64_t m = 2 * n;
+    const uint64_t par = (lane & 1) ? 0xAAAAAAAAAAAAAAAAull : 0x5555555555555555ull;
+    const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+    constexpr int CU = 2;
+    for (int64_t cb = (int64_t)gw * 64; cb < m; cb += CU * rstep) {
+        int id[CU], hid[CU];
+#pragma unroll
+        for (int j = 0; j < CU; ++j) {
+            const int64_t c = cb + j * rstep + lane;
+            const int64_t i = c >> 1;
+            id[j] = c < m ? ((c & 1) ? items[i] : users[i]) : 0;
+            hid[j] = c < m && !(c & 1) && fold > 1 ? users[i - i % fold] : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < CU; ++j) {
+            const int64_t c0 = cb + j * rstep;
+            if (c0 >= m) break;
+            const int64_t c = c0 + lane;
+            const int64_t i = c >> 1;
+            bool ok = false;
+            int key = 0;
+            if (c < m) {
+                if (c & 1) {
+                    ok = (unsigned)id[j] < (unsigned)f.I;
+                    key = f.U + id[j];
+                } else {
+                    ok = (unsigned)id[j] < (unsigned)f.U;
+                    key = id[j];
+                }
+                if (!ok) atomicOr(f.err, kErrIdRange);
+                // a user contribution folded into its group head's has no slot
+                if (!(c & 1) && fold > 1 && i % fold != 0 && hid[j] == id[j]) ok = false;
+            }
+            const int kp = pre(ok ? key : 0);
+            const int kk = ok ? key : -2 - lane;  // inactive lanes: unique keys
+            const int prev = __shfl_up(kk, 2, 64);
+            const uint64_t heads = ~__ballot(lane >= 2 && prev == kk) & par;
+            const int head = 63 - __clzll(heads & upto);
+            const uint64_t later = heads & ~upto;
+            const int next = later ? __ffsll((unsigned long long)later) - 1 : 64 + (lane & 1);
+            int top = 0, loc = 0;
+            if (ok) loc = f.local[key];
+            if (ok && lane == head) {
+                top = atomicSub(&f.cnt[key], (next - head) >> 1);
+                const int over = ((next - head) >> 1) - max(top, 0);
+                if (over > 0) atomicAdd(&f.cnt[key], over);
+            }
+            top = __shfl(top, head, 64);
+            const int slot = top - 1 - ((lane - head) >> 1);
+            if (ok && slot >= 0) {
+                const int64_t li = (int64_t)loc + kp + slot;
+                NCF_BOUND(li >= 0 && li < f.list_cap && key < f.r1 - 1, "fill c %lld key %d list %lld cap %lld\n",
+                          (long long)c, key, (long long)li, (long long)f.list_cap)
+                f.list[li] = (int)c;
+            } else if (ok) atomicOr(f.err, kErrStaleCount);
+        }
+    }
+}
+
 // ncf_user_dp_step's helpers (ncf_capi.hip)
 int build_next_index(const ncf_shape_t& s, const ncf_hyper_t& h, ncf_model_t* model, ncf_optim_t* optim,
                      const int32_t* next_users, const int32_t* next_items, int64_t n, void* ws, size_t ws_bytes,
@@ -446,7 +658,10 @@ bool wave_supported(const ncf_shape_t& s);
 hipError_t launch_fb_wave(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, const float* mlp,
                           const int32_t* users, const int32_t* items, const float* labels, int64_t n,
                           float inv_batch, IdSpace ids, int group, int topk, int* nslab, int* nbce, int* nmet,
-                          hipStream_t st, int fold, bool check_fold, bool one_wave = false);
+                          hipStream_t st, int fold, bool check_fold, bool one_wave = false,
+                          const FillArgs* fill = nullptr);
+// the split form runs for this shape (its weight-gradient waves can build the index: FillArgs)
+bool wave_fill_supported(const ncf_shape_t& s);
 hipError_t launch_fb_unit(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, const float* mlp,
                           const int32_t* users, const int32_t* items, const float* labels, int64_t n,
                           float inv_batch, IdSpace ids, int group, int topk, int* nslab, int* nbce, int* nmet,
@@ -548,8 +763,13 @@ hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, vo
                                      hipStream_t st, const int32_t* next_users = nullptr,
                                      const int32_t* next_items = nullptr, int64_t n_next = 0,
                                      const MlpDeferred* mlp = nullptr, int next_fold = 0,
-                                     const MetricsDeferred* met = nullptr, const float* grad_rows = nullptr);
+                                     const MetricsDeferred* met = nullptr, const float* grad_rows = nullptr,
+                                     bool unsorted_lists = false);
 // (grad_rows: the contribution rows the list indexes; default the workspace's per-sample rows gs)
+// (unsorted_lists: the index came from the in-kernel fill (FillArgs): the launch orders each row's
+// list itself and checks the touched rows' counters for a stale count)
+// heavy-row threshold of the touched-row update over unsorted lists (FillArgs::hc)
+inline int unsorted_heavy_c(const ncf_shape_t& s) { return s.row_width / 4 < 64 ? s.row_width / 4 : 64; }
 // dense gradient of rows [row_begin, num_rows) into out (indexed from row_begin)
 hipError_t launch_emb_grad_dense(const ncf_shape_t& s, const WsLayout& L, void* ws, float* out, hipStream_t st,
                                   int64_t row_begin = 0);

@@ -796,6 +796,63 @@ __device__ __forceinline__ void mlp_slabs_adam(const MlpTail& mt, int blk) {
     }
 }
 
+// Lists left unsorted by the in-kernel fill (FillArgs, ncf_internal.h): the touched-row update
+// orders each row's contributions itself.  A row of c <= hc entries: lane q of its row group holds
+// entry q, its rank (how many of the row's entries are smaller; the entries are distinct
+// contribution ids) comes from c shuffles and one ds_permute puts it at lane rank, so the sum
+// reads the ids in ascending order from the lanes — the order of a sorted list, so the same sum
+// bitwise.  Longer rows (heavy: listed by the fill) go to the launch's first blocks, which sort
+// block-wide by rank through LDS into slist and update the row.  A counter left at a touched row
+// (a batch counted ahead whose ids changed since) is flagged and cleared here, as k_sort does.
+struct SortRows {
+    int on;                    // 0: the lists are sorted (a fill + sort launch built the index)
+    int hc;                    // rows of more entries are heavy
+    int nheavy;                // heavy blocks (the first blocks of the launch)
+    const int32_t* heavy;      // touched-list positions of the heavy rows
+    const int32_t* heavy_n;
+    int32_t* cursor;           // ws cnt
+    int32_t* err;
+    int32_t* slist;            // heavy rows' lists, sorted (indexed like the list)
+    int mcap;                  // contribution ids are below this (2 * max batch): a stale list slot is clamped
+};
+constexpr int kHeavyChunk = 1024;  // heavy-row list entries staged in LDS per round
+
+// Row r's Adam step t from its c contributions, ids id(j) ascending; lanes q, q + qstep, ... of
+// its w4 float4 elements.  k: the m / v decays it still owes (P-ahead / caught-up rows), fresh:
+// pristine (m = v = 0, only p read).  The element expressions of every touched-row path.
+template <class ID>
+__device__ __forceinline__ void row_adam(float4* __restrict__ emb, float4* __restrict__ m4, float4* __restrict__ v4,
+                                         const float4* __restrict__ gs, uint32_t w4, int64_t r, int c, uint32_t q0,
+                                         uint32_t qstep, int k, bool fresh, float lr_t, float b1, float b2, float eps,
+                                         ID id) {
+    for (uint32_t q = q0; q < w4; q += qstep) {
+        const size_t e = (size_t)r * w4 + q;
+        float4 p = emb[e], m = make_float4(0.f, 0.f, 0.f, 0.f), v = m;
+        if (!fresh) {
+            m = m4[e];
+            v = v4[e];
+        }
+        for (int j = 0; j < k; ++j) decay4(m, v, b1, b2);
+        float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+        int j = 0;
+        for (; j + 4 <= c; j += 4) {
+            const int c0 = id(j), c1 = id(j + 1), c2 = id(j + 2), c3 = id(j + 3);
+            const float4 g0 = gs[(size_t)c0 * w4 + q], g1 = gs[(size_t)c1 * w4 + q];
+            const float4 g2 = gs[(size_t)c2 * w4 + q], g3 = gs[(size_t)c3 * w4 + q];
+            g = f4add(g, g0);
+            g = f4add(g, g1);
+            g = f4add(g, g2);
+            g = f4add(g, g3);
+        }
+        for (; j < c; ++j) g = f4add(g, gs[(size_t)id(j) * w4 + q]);
+        adam4(p, m, v, g, lr_t, b1, b2, eps);
+        st_stream(&emb[e], p);
+        st_stream(&m4[e], m);
+        st_stream(&v4[e], v);
+    }
+}
+
+template <bool UNSORTED>
 __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_touched(float4* __restrict__ emb, float4* __restrict__ m4,
                                                              float4* __restrict__ v4, uint32_t w4,
                                                              const int32_t* __restrict__ list,
@@ -806,7 +863,8 @@ __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_tou
                                                              const float4* __restrict__ gs,
                                                              int32_t* __restrict__ row_step, const int32_t* step,
                                                              float lr, float b1, float b2, float eps,
-                                                             CountAhead ca, MlpTail mt, MetricsTail mm) {
+                                                             CountAhead ca, MlpTail mt, MetricsTail mm,
+                                                             SortRows so) {
     // block order: [count (+ catch-up ahead)] [touched-row update] [dense-layer Adam]: the
     // latency-bound replay blocks are dispatched first, so they run under the HBM-bound update
     // (interleaving them one in every (nupd + ncount) / ncount blocks was measured slower: 60.2
@@ -814,6 +872,68 @@ __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_tou
     // (two_level: the dense-layer blocks come first — each waits one round of slab loads, under
     // everything else)
     int b = (int)blockIdx.x;
+    if (UNSORTED && b < so.nheavy) {
+        // heavy rows (lists longer than so.hc, unsorted): one per block and pass
+        __shared__ int chunk[kHeavyChunk];
+        const int t = *step + 1;
+        const float lr_t = adam_lr_t(lr, b1, b2, t);
+        const int nh = *so.heavy_n;
+        for (int hi = b; hi < nh; hi += so.nheavy) {
+            const int u = so.heavy[hi];
+            const int64_t r = list[u];
+            const int2 oc = toc[u];
+            const int o = oc.x, c = oc.y;
+#if NCF_DEBUG_BOUNDS
+            if (u < 0 || u >= so.mcap || r < 0 || r >= ca.lazy_rows || o < 0 || c < 0 || o + c > so.mcap) {
+                if (threadIdx.x == 0) printf("heavy %d: u %d nlist %d r %lld o %d c %d (skipped)\n", hi, u, *nlist, (long long)r, o, c);
+                continue;
+            }
+#endif
+            // rank of each entry among the row's: the list staged through LDS a chunk at a time
+            int e[4], rk[4];
+            for (int j0 = 0; j0 < c; j0 += 4 * kBlock) {
+#pragma unroll
+                for (int a = 0; a < 4; ++a) {
+                    const int j = j0 + a * kBlock + (int)threadIdx.x;
+                    e[a] = j < c ? (int)min((unsigned)clist[o + j], (unsigned)(so.mcap - 1)) : INT_MAX;
+                    rk[a] = 0;
+                }
+                for (int i0 = 0; i0 < c; i0 += kHeavyChunk) {
+                    const int ni = min(kHeavyChunk, c - i0);
+                    __syncthreads();
+                    for (int i = threadIdx.x; i < ni; i += kBlock)
+                        chunk[i] = (int)min((unsigned)clist[o + i0 + i], (unsigned)(so.mcap - 1));
+                    __syncthreads();
+                    for (int i = 0; i < ni; ++i) {
+                        const int x = chunk[i];
+#pragma unroll
+                        for (int a = 0; a < 4; ++a) rk[a] += x < e[a];
+                    }
+                }
+#pragma unroll
+                for (int a = 0; a < 4; ++a)
+                    if (j0 + a * kBlock + (int)threadIdx.x < c) so.slist[o + rk[a]] = e[a];
+            }
+            __syncthreads();  // the sorted list is the workgroup's own stores
+            const bool mine = r < ca.lazy_rows;
+            int rs = mine ? row_step[r] : 0;
+            const bool fresh = rs == NCF_ROW_PRISTINE;
+            if (rs < 0) rs = pahead_s0(rs);
+            const int k = NCF_CATCHUP_P_ONLY && mine && !fresh ? t - 1 - rs : 0;
+            if (mine)
+                row_adam(emb, m4, v4, gs, w4, r, c, threadIdx.x, kBlock, k, fresh, lr_t, b1, b2, eps,
+                         [&](int j) { return so.slist[o + j]; });
+            if (threadIdx.x == 0) {
+                if (mine) row_step[r] = t;
+                if (so.cursor[r] != 0) {
+                    atomicOr(so.err, kErrStaleCount);
+                    so.cursor[r] = 0;
+                }
+            }
+        }
+        return;
+    }
+    b -= so.nheavy;
     // the step's hr/dcg partials (k_group_metrics' work, groups <= 8) in the first blocks: the
     // probabilities are final once the forward/backward launch before this one is done
     if (b < mm.nblocks) {
@@ -952,6 +1072,103 @@ __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_tou
     const int ublk = b - ca.ncount;   // this block's index among the update blocks
     const RowLanes rl(w4);
     const int t = *step + 1;
+    if constexpr (UNSORTED) {
+        // unsorted lists (in-kernel fill): every lane runs the row loop (its shuffles), a lane outside
+        // a row group (w4 not dividing 64) or past the list with c = 0
+        const float lr_t = adam_lr_t(lr, b1, b2, t);
+        const int64_t n = *nlist;
+        const int lane = threadIdx.x & 63;
+        const int gsz = w4 <= 64 ? (int)w4 : 64;            // lanes of a row group
+        const int base = w4 <= 64 ? rl.sub * (int)w4 : 0;   // its first lane
+        const int ql = lane - base;                          // this lane's entry slot
+        const int64_t wave = ((int64_t)ublk * kBlock + threadIdx.x) >> 6;
+        const int64_t wstride = ((int64_t)ca.nupd * kBlock) >> 6;
+        for (int64_t i0 = wave * rl.rpw; i0 < n; i0 += wstride * rl.rpw) {  // wave-uniform
+            const int64_t i = i0 + rl.sub;
+            bool has = rl.on && i < n;
+            int r = has ? list[i] : 0;
+            int2 oc = has ? toc[i] : make_int2(0, 0);
+#if NCF_DEBUG_BOUNDS
+            if (has && (i >= so.mcap || r < 0 || r >= ca.lazy_rows || oc.x < 0 || oc.y < 0 || oc.x + oc.y > so.mcap)) {
+                if (ql == 0) printf("row %lld of %lld: r %d o %d c %d (skipped)\n", (long long)i, (long long)n, r, oc.x, oc.y);
+                has = false;
+                r = 0;
+                oc = make_int2(0, 0);
+            }
+#endif
+            const bool heavy = oc.y > so.hc;
+            const int c = heavy ? 0 : oc.y;
+            const bool mine = has && !heavy && r < ca.lazy_rows;
+            int rs = mine ? row_step[r] : 0;
+            const int res = has && !heavy && ql == 0 ? so.cursor[r] : 0;
+            int e = ql < c ? (int)min((unsigned)clist[oc.x + ql], (unsigned)(so.mcap - 1)) : INT_MAX;
+            // the wave's longest light list (its row groups' counts, read lane by lane)
+            int cmax = 0;
+            for (int g = 0; g < rl.rpw; ++g) cmax = max(cmax, __builtin_amdgcn_readlane(c, g * (int)w4));
+            int rank = 0;
+            for (int j = 0; j < cmax; ++j) {
+                const int x = __shfl(e, base + j, 64);
+                rank += j < c && x < e;
+            }
+            // entry ql goes to lane base + rank (a permutation of the group's first c lanes; the
+            // other lanes keep their own value)
+            const int to = ql < c ? base + rank : lane;
+            const int srt = __builtin_amdgcn_ds_permute(to * 4, e);
+            if (res != 0) {
+                atomicOr(so.err, kErrStaleCount);
+                so.cursor[r] = 0;
+            }
+            const bool fresh = rs == NCF_ROW_PRISTINE;
+            if (rs < 0) rs = pahead_s0(rs);
+            const int k = NCF_CATCHUP_P_ONLY && mine && !fresh ? t - 1 - rs : 0;
+            // the sum's ids from the lanes: a wave-uniform loop over the longest list, masked per row
+            for (uint32_t q = w4 <= 64 ? (uint32_t)ql : (uint32_t)lane; ; q += 64) {
+                const bool act = mine && q < w4 && ql < gsz;
+                const size_t ee = (size_t)r * w4 + (act ? q : 0);
+                // (explicit branches, no `c ? a[i] : local` lvalue selects: those compile to a flat load
+                // through a selected pointer, the local's being a scratch address)
+                float4 p = make_float4(0.f, 0.f, 0.f, 0.f), m = p, v = p;
+                if (act) {
+                    p = emb[ee];
+                    if (!fresh) {
+                        m = m4[ee];
+                        v = v4[ee];
+                    }
+                }
+                for (int j = 0; j < k; ++j) decay4(m, v, b1, b2);
+                float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+                for (int j = 0; j < cmax; j += 4) {
+                    const int c0 = __shfl(srt, base + j, 64), c1 = __shfl(srt, base + min(j + 1, gsz - 1), 64);
+                    const int c2 = __shfl(srt, base + min(j + 2, gsz - 1), 64);
+                    const int c3 = __shfl(srt, base + min(j + 3, gsz - 1), 64);
+                    const bool v0 = act && j < c, v1 = act && j + 1 < c, v2 = act && j + 2 < c, v3 = act && j + 3 < c;
+#if NCF_DEBUG_BOUNDS
+                    if ((v0 && (unsigned)c0 >= (unsigned)so.mcap) || (v1 && (unsigned)c1 >= (unsigned)so.mcap) ||
+                        (v2 && (unsigned)c2 >= (unsigned)so.mcap) || (v3 && (unsigned)c3 >= (unsigned)so.mcap))
+                        printf("sum r %d j %d c %d ids %d %d %d %d\n", r, j, c, c0, c1, c2, c3);
+#endif
+                    float4 g0, g1, g2, g3;
+                    if (v0) g0 = gs[(size_t)c0 * w4 + q];
+                    if (v1) g1 = gs[(size_t)c1 * w4 + q];
+                    if (v2) g2 = gs[(size_t)c2 * w4 + q];
+                    if (v3) g3 = gs[(size_t)c3 * w4 + q];
+                    if (v0) g = f4add(g, g0);
+                    if (v1) g = f4add(g, g1);
+                    if (v2) g = f4add(g, g2);
+                    if (v3) g = f4add(g, g3);
+                }
+                if (act) {
+                    adam4(p, m, v, g, lr_t, b1, b2, eps);
+                    st_stream(&emb[ee], p);
+                    st_stream(&m4[ee], m);
+                    st_stream(&v4[ee], v);
+                }
+                if (w4 <= 64 || q + 64 >= w4) break;
+            }
+            if (ql == 0 && mine) row_step[r] = t;
+        }
+        return;
+    }
     if (rl.on) {
         const float lr_t = adam_lr_t(lr, b1, b2, t);
         const int64_t n = *nlist;
@@ -1293,9 +1510,11 @@ __global__ __launch_bounds__(kBlock) void k_stats(float* __restrict__ summary,
 // Block 0: k_stats; blocks 1..: the next batch's per-block key scan (k_scan_local<true>) over the
 // counts the touched update took ahead — one launch instead of two.
 struct ScanAhead {
-    const int32_t* cnt;
+    const int32_t* cnt;        // the counts taken ahead (ws cnt_ahead): moved to cursor, then zeroed
     int64_t r1;
     int32_t *offs, *tot, *uloc, *utot;
+    int32_t* cursor;           // ws cnt
+    int32_t* heavy_n;          // the in-kernel fill's heavy-row count (FillArgs), zeroed here
 };
 __global__ __launch_bounds__(kBlock) void k_stats_scan(float* __restrict__ summary,
                                                        const float* __restrict__ reg_emb, int nreg_emb,
@@ -1311,21 +1530,23 @@ __global__ __launch_bounds__(kBlock) void k_stats_scan(float* __restrict__ summa
         }
         stats_body(summary, reg_emb, nreg_emb, reg_mlp, nreg_mlp, inv_batch, stats, step, bump, red);
     } else {
-        scan_local_body<true>(sc.cnt, sc.r1, sc.offs, sc.tot, sc.uloc, sc.utot, (int)blockIdx.x - 1);
+        if (blockIdx.x == 1 && threadIdx.x == 0) *sc.heavy_n = 0;
+        scan_local_body<true>(sc.cnt, sc.r1, sc.offs, sc.tot, sc.uloc, sc.utot, (int)blockIdx.x - 1, sc.cursor);
     }
 }
 
 // The next batch's per-block key scan alone (k_stats_scan's blocks >= 1), for a counting-ahead
 // update that has no stats launch of its own behind it (user-partitioned data parallelism).
 __global__ __launch_bounds__(kBlock) void k_scan_ahead(ScanAhead sc) {
-    scan_local_body<true>(sc.cnt, sc.r1, sc.offs, sc.tot, sc.uloc, sc.utot, (int)blockIdx.x);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *sc.heavy_n = 0;
+    scan_local_body<true>(sc.cnt, sc.r1, sc.offs, sc.tot, sc.uloc, sc.utot, (int)blockIdx.x, sc.cursor);
 }
 
 hipError_t launch_scan_ahead(const WsLayout& L, void* ws, int64_t keys, hipStream_t st) {
     const int64_t r1 = keys + 1;
     const int nscan = (int)((r1 + kScanBlock - 1) / kScanBlock);
-    ScanAhead sc{at<const int32_t>(ws, L.cnt), r1, at<int32_t>(ws, L.offs_local), at<int32_t>(ws, L.tot),
-                 at<int32_t>(ws, L.uloc), at<int32_t>(ws, L.utot)};
+    ScanAhead sc{at<const int32_t>(ws, L.cnt_ahead), r1, at<int32_t>(ws, L.offs_local), at<int32_t>(ws, L.tot),
+                 at<int32_t>(ws, L.uloc), at<int32_t>(ws, L.utot), at<int32_t>(ws, L.cnt), at<int32_t>(ws, L.heavy_n)};
     launch(k_scan_ahead, nscan, kBlock, 0, st, sc);
     return hipGetLastError();
 }
@@ -1474,7 +1695,7 @@ hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, vo
                                      float* v, int32_t* row_step, int32_t* step, const ncf_hyper_t& h,
                                      hipStream_t st, const int32_t* next_users, const int32_t* next_items,
                                      int64_t n_next, const MlpDeferred* mlp, int next_fold, const MetricsDeferred* met,
-                                     const float* grad_rows) {
+                                     const float* grad_rows, bool unsorted_lists) {
     const bool replay_ahead = next_users != nullptr && NCF_CATCHUP_AHEAD;
     const uint32_t w4 = (uint32_t)(s.row_width / 4);
     const uint32_t n4 = (uint32_t)(lazy_bound(s, h) * w4);  // SGD: the rows under deferred decay
@@ -1491,7 +1712,7 @@ hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, vo
         const int64_t npass = (mc + per - 1) / per;
         const unsigned ncount = mc > 0 ? (unsigned)(npass < NCF_COUNT_BLOCKS_MAX ? npass : NCF_COUNT_BLOCKS_MAX) : 0u;
         CountAhead ca{(int)nupd, (int)ncount, next_users, next_items, mc, s.num_users, s.num_items,
-                      at<int32_t>(ws, L.cnt), replay_ahead ? 1 : 0, next_fold, per, lazy_bound(s, h)};
+                      at<int32_t>(ws, L.cnt_ahead), replay_ahead ? 1 : 0, next_fold, per, lazy_bound(s, h)};
         MlpTail mt{};
         if (mlp) {
             mt = MlpTail{mlp->two_level ? (s.mlp_params + 15) / 16 : (s.mlp_params + kBlock - 1) / kBlock, mlp->p,
@@ -1501,10 +1722,18 @@ hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, vo
         MetricsTail mm{};
         if (met) mm = MetricsTail{met->nblocks, met->probs, met->labels, met->ng, met->group, met->k,
                                   at<float>(ws, L.part_hit), at<float>(ws, L.part_dcg)};
-        launch(k_emb_adam_touched, nupd + ncount + (unsigned)mt.nblocks + (unsigned)mm.nblocks, kBlock, 0, st,
-               (float4*)emb, (float4*)m, (float4*)v, w4, at<const int32_t>(ws, L.touched),
-               at<const int2>(ws, L.touched_oc), at<const int32_t>(ws, L.nuniq), offs, list, gs, row_step, (const int32_t*)step, h.lr, h.beta_1, h.beta_2,
-               h.epsilon, ca, mt, mm);
+        SortRows so{};
+        if (unsorted_lists) {
+            if (L.world != 0 || unsorted_heavy_c(s) < kHeavyMin) return hipErrorInvalidValue;
+            // heavy rows are rare (lists longer than a row group's lanes): a few blocks stride over them
+            so = SortRows{1, unsorted_heavy_c(s), 32, at<const int32_t>(ws, L.heavy), at<const int32_t>(ws, L.heavy_n),
+                          at<int32_t>(ws, L.cnt), at<int32_t>(ws, L.err), at<int32_t>(ws, L.slist),
+                          (int)(2 * L.max_batch)};
+        }
+        launch(unsorted_lists ? k_emb_adam_touched<true> : k_emb_adam_touched<false>, (unsigned)so.nheavy + nupd + ncount + (unsigned)mt.nblocks + (unsigned)mm.nblocks,
+               kBlock, 0, st, (float4*)emb, (float4*)m, (float4*)v, w4, at<const int32_t>(ws, L.touched),
+               at<const int2>(ws, L.touched_oc), at<const int32_t>(ws, L.nuniq), offs, list, gs, row_step,
+               (const int32_t*)step, h.lr, h.beta_1, h.beta_2, h.epsilon, ca, mt, mm, so);
     } else
         launch(k_emb_sgd_hot, kUpdateGrid, kBlock, 0, st, (float4*)emb, n4, w4, offs, list, gs, h.lr);
     return hipGetLastError();
@@ -1746,8 +1975,8 @@ hipError_t launch_stats(const WsLayout& L, void* ws, const float* summary_in, in
     if (scan_ahead) {
         const int64_t r1 = scan_keys + 1;
         const int nscan = (int)((r1 + kScanBlock - 1) / kScanBlock);
-        ScanAhead sc{at<const int32_t>(ws, L.cnt), r1, at<int32_t>(ws, L.offs_local), at<int32_t>(ws, L.tot),
-                     at<int32_t>(ws, L.uloc), at<int32_t>(ws, L.utot)};
+        ScanAhead sc{at<const int32_t>(ws, L.cnt_ahead), r1, at<int32_t>(ws, L.offs_local), at<int32_t>(ws, L.tot),
+                     at<int32_t>(ws, L.uloc), at<int32_t>(ws, L.utot), at<int32_t>(ws, L.cnt), at<int32_t>(ws, L.heavy_n)};
         launch(k_stats_scan, 1 + nscan, kBlock, 0, st, summary, reg, nreg_emb, reg + kUpdateGrid, nreg_mlp, inv_batch,
                stats, step, bump_step ? 1 : 0, sc, sa);
         return hipGetLastError();

@@ -310,7 +310,7 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
                                                      float* __restrict__ part_bce, int group, int topk,
                                                      float* __restrict__ part_hit, float* __restrict__ part_dcg,
                                                      const int32_t* __restrict__ ifold, int32_t* __restrict__ ferr,
-                                                     float* __restrict__ gpart) {
+                                                     float* __restrict__ gpart, FillArgs fa) {
     constexpr int L0 = S::L0, L1 = S::L1, L2 = S::L2, L3 = S::L3, G = S::G, D0 = S::D0, W = S::W;
     constexpr int B0 = S::B0, B1 = S::B1, B2 = S::B2, XQ = S::XQ, GQ = S::GQ, GQA = GQ > 0 ? GQ : 1;
     // Group-user form (GU: split form, FOLD > 1).  The reference's batches are groups of FOLD
@@ -521,6 +521,14 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
     }
     __syncthreads();
     NCF_WS(2, __builtin_readcyclecounter());
+    // split, a batch counted and scanned ahead (fa.cnt): the weight-gradient waves, idle until the
+    // chain hands over its first unit, build this batch's index (the fill; the lists unsorted, the
+    // touched-row update after this launch orders them) — the step's fill launch and list sort
+    // launch disappear.
+    if constexpr (SPLIT) {
+        if (dwave && fa.cnt)
+            fill_wave(fa, users, items, n, FOLD, (int)blockIdx.x * 4 + pw, (int)gridDim.x * 4);
+    }
     // GU phase 0: P_u = W1_u^T x_u of every group of this chain wave's units, one 16-group tile per
     // FOLD units (k-step q takes user feature XH lq + q), into gpart
     if constexpr (GU) {
@@ -1543,8 +1551,10 @@ template <class S, bool SPLIT>
 hipError_t launch_wave_form(const WsLayout& L, void* ws, const float* emb, const float* mlp, const int32_t* users,
                             const int32_t* items, const float* labels, int64_t n, float inv_batch, IdSpace ids,
                             int group, int topk, int* nslab, int* nbce, int* nmet, hipStream_t st, int fold,
-                            bool check_fold) {
+                            bool check_fold, const FillArgs* fill) {
     constexpr size_t lds = SPLIT ? S::LDS_BYTES2 : S::LDS_BYTES;
+    if (fill && !SPLIT) return hipErrorInvalidValue;
+    const FillArgs fa = fill ? *fill : FillArgs{};
     static bool configured = false;  // one-time attribute set per shape and form (idempotent)
     if (!configured) {
         for (const void* k : {(const void*)k_fb_wave<S, 0, false, SPLIT>, (const void*)k_fb_wave<S, 2, false, SPLIT>,
@@ -1567,7 +1577,7 @@ hipError_t launch_wave_form(const WsLayout& L, void* ws, const float* emb, const
         launch(kern, grid, SPLIT ? 512 : 256, lds, st, emb, mlp, users, items, labels, n, ids, inv_batch,
                at<float>(ws, L.probs), at<float>(ws, L.gs), at<float>(ws, L.slabs), at<float>(ws, L.part_bce), group,
                topk, at<float>(ws, L.part_hit), at<float>(ws, L.part_dcg),
-               check_fold ? at<const int32_t>(ws, L.ifold) : nullptr, at<int32_t>(ws, L.err), at<float>(ws, L.act));
+               check_fold ? at<const int32_t>(ws, L.ifold) : nullptr, at<int32_t>(ws, L.err), at<float>(ws, L.act), fa);
     };
     switch (fold * 2 + (in_kernel ? 1 : 0)) {
         case 0: go(k_fb_wave<S, 0, false, SPLIT>); break;
@@ -1589,14 +1599,15 @@ template <class S>
 hipError_t launch_wave_one(const WsLayout& L, void* ws, const float* emb, const float* mlp, const int32_t* users,
                            const int32_t* items, const float* labels, int64_t n, float inv_batch, IdSpace ids,
                            int group, int topk, int* nslab, int* nbce, int* nmet, hipStream_t st, int fold,
-                           bool check_fold, bool one_wave) {
+                           bool check_fold, bool one_wave, const FillArgs* fill) {
     if constexpr (S::SPLIT_OK) {
         if (split_enabled() && !one_wave)
             return launch_wave_form<S, true>(L, ws, emb, mlp, users, items, labels, n, inv_batch, ids, group, topk,
-                                             nslab, nbce, nmet, st, fold, check_fold);
+                                             nslab, nbce, nmet, st, fold, check_fold, fill);
     }
+    if (fill) return hipErrorInvalidValue;  // the fill needs the split form's weight-gradient waves
     return launch_wave_form<S, false>(L, ws, emb, mlp, users, items, labels, n, inv_batch, ids, group, topk, nslab,
-                                      nbce, nmet, st, fold, check_fold);
+                                      nbce, nmet, st, fold, check_fold, nullptr);
 }
 
 }  // namespace
@@ -1616,14 +1627,21 @@ bool wave_supported(const ncf_shape_t& s) {
     return wmatches<WShapeC>(s) || wmatches<WShapeB>(s) || wmatches<WShapeR>(s) || wmatches<WShapeC0>(s);
 }
 
+bool wave_fill_supported(const ncf_shape_t& s) {
+    auto ok = [](bool split_ok) { return split_ok && split_enabled(); };
+    return (wmatches<WShapeC>(s) && ok(WShapeC::SPLIT_OK)) || (wmatches<WShapeB>(s) && ok(WShapeB::SPLIT_OK)) ||
+           (wmatches<WShapeR>(s) && ok(WShapeR::SPLIT_OK)) || (wmatches<WShapeC0>(s) && ok(WShapeC0::SPLIT_OK));
+}
+
 hipError_t launch_fb_wave(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, const float* mlp,
                           const int32_t* users, const int32_t* items, const float* labels, int64_t n,
                           float inv_batch, IdSpace ids, int group, int topk, int* nslab, int* nbce, int* nmet,
-                          hipStream_t st, int fold, bool check_fold, bool one_wave) {
+                          hipStream_t st, int fold, bool check_fold, bool one_wave, const FillArgs* fill) {
     if (fold != 0 && (fold < 2 || fold > 8 || (fold & (fold - 1)) != 0 || n % fold != 0)) return hipErrorInvalidValue;
+    if (fill && (fill->nscan > kMaxFillScan || fill->nscan < 1)) return hipErrorInvalidValue;
 #define NCF_ARGS \
     L, ws, emb, mlp, users, items, labels, n, inv_batch, ids, group, topk, nslab, nbce, nmet, st, fold, check_fold, \
-        one_wave
+        one_wave, fill
     if (wmatches<WShapeC>(s)) return launch_wave_one<WShapeC>(NCF_ARGS);
     if (wmatches<WShapeB>(s)) return launch_wave_one<WShapeB>(NCF_ARGS);
     if (wmatches<WShapeR>(s)) return launch_wave_one<WShapeR>(NCF_ARGS);

@@ -235,6 +235,12 @@ class RowShardedDataParallel(object):
         ready = (held is not None and group is not None and held[0].data_ptr() == u.data_ptr() and
                  held[1].data_ptr() == i.data_ptr() and held[2] == u.numel() and
                  (held[0]._version, held[1]._version) == held[3] and held[4] == int(group))
+        if held is not None and group is not None and not ready:
+            # re-planning here would issue a counts exchange the ranks whose held plan matches do
+            # not issue: the collectives would no longer pair up.  Every rank holds a plan for the
+            # batch it announced, so a different batch (or ids refilled in place) is an error
+            raise RuntimeError("train_step got another batch than the next_batch= announced in the previous "
+                               "step (or its ids changed since): pass exactly those tensors, unmodified")
         if not ready:
             self._plan_and_count(u, i, group, ahead=False)
         else:
@@ -262,7 +268,12 @@ class RowShardedDataParallel(object):
         eng = self.eng
         send, recv, nu, m = self._fetch_rows(users, items, group)
         eng.forward_backward(labels, group=group, k=k, inv_batch=inv, include_dense_reg=self.rank == 0)
-        if next_batch is not None:
+        # The next batch is planned here only under deferred decay: the dense shard update
+        # (ncf_shard_apply_update without row_step) builds its owner index in per-batch workspace
+        # regions that a plan of the next batch would overwrite, and a next batch larger than the
+        # workspace would reallocate it under this step's pending update.  (Every rank decides
+        # alike: the engines share the layout and the batches their size.)
+        if next_batch is not None and eng.lazy and len(next_batch[0]) <= eng.max_batch:
             # the forward/backward and its compact gradient were the last readers of this step's plan
             nu_, ni_ = eng._ids(next_batch[0]), eng._ids(next_batch[1])
             if nu_.data_ptr() == next_batch[0].data_ptr() and ni_.data_ptr() == next_batch[1].data_ptr():

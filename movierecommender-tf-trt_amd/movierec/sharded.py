@@ -96,6 +96,11 @@ class ShardedNCFEngine(object):
         return N.FB_KERNELS[k]
 
     def set_hyper(self, optimizer, lr, beta_1=0.9, beta_2=0.999, layers_l2reg=None):
+        if getattr(self, "row_step", None) is not None:
+            # pending zero-gradient steps are owed under the previous hyper-parameters
+            self.flush()
+            if layers_l2reg is not None and len(layers_l2reg) and float(layers_l2reg[0]) != 0.0:
+                raise ValueError("lazy_adam needs layers_l2reg[0] == 0 (the L2 loss sums the whole table)")
         h = self.hyper
         opt = {"adam": N.NCF_OPT_ADAM, "sgd": N.NCF_OPT_SGD}.get(optimizer)
         if opt is None:

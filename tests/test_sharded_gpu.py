@@ -303,3 +303,84 @@ def test_config_d_row_sharded_world2_matches_compacted_oracle():
         d = np.abs(g - ref[name])
         assert float(d.max()) <= tol, "%s: max err %g > %g (%d rows beyond)" % (
             name, float(d.max()), tol, int((d > tol).any(axis=1).sum()))
+
+
+# ------------------------------- dense shard, next batch announced, K >> batch, world 2 (gloo)
+
+def _dense_world2_worker(rank, world, port, q, dims, w, batches):
+    import traceback
+    try:
+        import torch.distributed as dist
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+        eng = ShardedNCFEngine(*dims, world=world, rank=rank, max_batch=len(batches[0][0]))
+        eng.set_keras_weights(w)
+        dp = RowShardedDataParallel(eng)
+        dev = [tuple(torch.from_numpy(a).cuda() for a in b) for b in batches]
+        for s, (u, it, y) in enumerate(dev):
+            nxt = (dev[s + 1][0], dev[s + 1][1]) if s + 1 < len(dev) else None
+            dp.train_step(u, it, y, group=GROUP, k=2, global_batch=world * len(u), next_batch=nxt)
+        eng.check_errors()
+        full = dp.full_table().cpu().numpy()
+        q.put((rank, full, eng.mlp.cpu().numpy(), NCFEngine.read_stats(eng.stats)))
+        dist.barrier()
+        dist.destroy_process_group()
+    except BaseException:
+        q.put((rank, "worker failed:\n" + traceback.format_exc()))
+        raise
+
+
+def test_dense_shard_next_batch_large_table_world2():
+    """a DENSE shard (no deferred decay) with next_batch passed, a key space far
+    larger than the batch (400,000 x 300,000 rows, 256 samples per rank) — the layout where the
+    dense update's owner index would overlap a plan of the next batch.  The row-sharded step does
+    not plan ahead for a dense shard; two gloo ranks sharing the GPU must equal one table stepping
+    the concatenated batches (fp32 order of the cross-rank sums)."""
+    import socket
+    import torch.multiprocessing as mp
+    dims = (400_000, 300_000, [128, 64, 32, 16], 64)
+    shape = O.NCFShape(*dims)
+    world, per, steps = 2, 256, 4
+    rng = np.random.RandomState(7)
+    w = O.init_weights(shape, seed=8)
+    w = {k: v.astype(np.float32).astype(np.float64) for k, v in w.items()}
+    rank_batches = [[] for _ in range(world)]
+    glob = []
+    for s in range(steps):
+        u = rng.randint(0, dims[0], world * per // GROUP).repeat(GROUP).astype(np.int32)
+        it = rng.randint(0, dims[1], world * per).astype(np.int32)
+        y = np.tile([0.0] * (GROUP - 1) + [1.0], world * per // GROUP).astype(np.float32)
+        glob.append((u, it, y))
+        for r in range(world):
+            sl = slice(r * per, (r + 1) * per)
+            rank_batches[r].append((u[sl], it[sl], y[sl]))
+    single = NCFEngine(*dims, max_batch=world * per)
+    single.set_keras_weights(w)
+    for u, it, y in glob:
+        single.train_step(u, it, y, group=GROUP, k=2)
+    want_emb = single.emb.cpu().numpy()
+    want_mlp = single.mlp.cpu().numpy()
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dense_world2_worker, args=(r, world, port, q, dims, w, rank_batches[r]))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        item = q.get(timeout=600)
+        if isinstance(item[1], str):
+            pytest.fail(item[1])
+        res[item[0]] = item[1:]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for r in range(world):
+        full, mlp, stats = res[r]
+        assert stats["steps"] == steps
+        assert float(np.max(np.abs(full - want_emb))) <= 1e-6
+        assert float(np.max(np.abs(mlp - want_mlp))) <= 1e-6
