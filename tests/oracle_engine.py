@@ -138,6 +138,11 @@ class OracleShardedEngine(object):
         self.mlp_grad = self.dense_buf[:P]
         self.summary = self.dense_buf[P:]
         self.send_counts = torch.zeros(self.world, dtype=torch.int32)
+        # RowShardedDataParallel plans the next batch ahead only for a deferred-decay shard whose
+        # workspace holds it (the device's dense owner index shares the plan's regions); this
+        # look-alike's buffers grow as needed and its update reads no index: it takes that path
+        self.lazy = True
+        self.max_batch = 1 << 30
         self.t = 0
         self.lr, self.b1, self.b2 = lr, beta_1, beta_2
         self.l2 = list(layers_l2reg or [0.0] * len(shape.layers))
