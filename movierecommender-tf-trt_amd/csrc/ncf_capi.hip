@@ -486,6 +486,21 @@ int ncf_shard_workspace_flags(const ncf_shape_t* s, int64_t max_batch, int32_t w
     return hip_check(hipMemsetAsync(ncf::at<int32_t>(ws, L.err), 0, 4, st), "flags clear");
 }
 
+// Diagnostics (tools/, not in the ABI header): byte offsets of the single-table index regions
+// cnt, cnt_ahead, heavy_n, err, offs_local, offs, tot, uloc, utot, nuniq, touched, touched_oc,
+// heavy, list, slist, then nscan and list_cap
+extern "C" int ncf_debug_index_regions(const ncf_shape_t* s, int64_t max_batch, int64_t* out17) {
+    if (int r = check_shape(s)) return r;
+    if (!out17) return fail(NCF_EINVAL, "out is NULL");
+    const ncf::WsLayout L = ncf::make_layout(*s, max_batch);
+    const size_t v[] = {L.cnt, L.cnt_ahead, L.heavy_n, L.err, L.offs_local, L.offs, L.tot, L.uloc, L.utot,
+                        L.nuniq, L.touched, L.touched_oc, L.heavy, L.list, L.slist};
+    for (int j = 0; j < 15; ++j) out17[j] = (int64_t)v[j];
+    out17[15] = L.nscan;
+    out17[16] = L.list_cap;
+    return 0;
+}
+
 int ncf_workspace_discard_counts(const ncf_shape_t* s, int64_t max_batch, void* ws, size_t ws_bytes, void* stream) {
     if (int r = check_shape(s)) return r;
     ncf::WsLayout L = ncf::make_layout(*s, max_batch);
@@ -575,7 +590,8 @@ static int index_join(hipStream_t st, FbOut& fb) {
 static int run_fb(const ncf_shape_t& s, const ncf::WsLayout& L, const ncf_model_t* model, const ncf_hyper_t* h,
                   const int32_t* users, const int32_t* items, const float* labels, int64_t n, void* ws,
                   float* probs_out, FbOut* out, hipStream_t st, bool sharded = false,
-                  int (*after_index)(void*) = nullptr, void* ctx = nullptr, const ncf::FillArgs* fill = nullptr) {
+                  int (*after_index)(void*) = nullptr, void* ctx = nullptr, const ncf::FillArgs* fill = nullptr,
+                  bool index_filled = false) {
     hipError_t e = hipSuccess;
     ncf::IdSpace ids = ncf::table_ids(s);
     const int fold = index_fold(s, h);
@@ -584,6 +600,8 @@ static int run_fb(const ncf_shape_t& s, const ncf::WsLayout& L, const ncf_model_
     bool check_fold = false;  // the unit / wave kernels check an earlier call's index fold themselves
     if (fill) {
         if (variant != NCF_FB_WAVE || sharded) return fail(NCF_EINVAL, "in-kernel index fill: wave kernel only");
+    } else if (index_filled) {
+        // k_fill_ahead has just filled this step's index (its fold is the kernel's)
     } else if (sharded || (h->index_ready == 1 && !after_index) || h->index_ready == 3) {
         // the index was built by an earlier call — ncf_shard_plan (compact ids), ncf_build_index
         // (the deferred-decay step needs the touched-row list too and builds its own), or the
@@ -677,7 +695,10 @@ static int check_train_args(const ncf_shape_t* s, const ncf_model_t* model, cons
 }
 
 #ifndef NCF_FILL_IN_KERNEL
-#define NCF_FILL_IN_KERNEL 1  // 0: the fill and list-sort launches of round 4 (timing comparisons)
+// 1: the wave kernel's weight-gradient waves fill the index; 2: a fill launch of its own
+// (k_fill_ahead) before the forward/backward; either way the touched-row update orders the lists.
+// 0: round 4's fill and list-sort launches (timing comparisons)
+#define NCF_FILL_IN_KERNEL 2
 #endif
 // The step's index from the wave kernel's weight-gradient waves (FillArgs): a batch counted and
 // scanned ahead by the previous step (index_ready 2, deferred-decay Adam), the split wave kernel,
@@ -686,11 +707,15 @@ static int check_train_args(const ncf_shape_t* s, const ncf_model_t* model, cons
 // (A batch whose ids changed after they were counted is flagged as before, NCF_WSERR_STALE_COUNT;
 // the rows the counted set missed are then read by this forward pass at their last step — there
 // is no launch before it to replay them — and settled when next touched or flushed.)
-static bool fill_in_kernel(const ncf_shape_t& s, const ncf::WsLayout& L, const ncf_hyper_t* h, int64_t n) {
-    return NCF_FILL_IN_KERNEL && h->index_ready == 2 && h->optimizer == NCF_OPT_ADAM && side_stream_mode() == 0 &&
-           use_fused(s, h) && fb_variant(s, h, n) == NCF_FB_WAVE && h->force_generic != 6 &&
-           ncf::wave_fill_supported(s) && L.world == 0 && L.nscan <= ncf::kMaxFillScan &&
-           ncf::unsorted_heavy_c(s) >= ncf::kHeavyMin;
+// 0: the index launches; 1: the wave kernel fills; 2: k_fill_ahead fills
+static int fill_in_kernel(const ncf_shape_t& s, const ncf::WsLayout& L, const ncf_hyper_t* h, int64_t n) {
+    if (!NCF_FILL_IN_KERNEL || h->index_ready != 2 || h->optimizer != NCF_OPT_ADAM || side_stream_mode() != 0 ||
+        L.world != 0 || L.nscan > ncf::kMaxFillScan || ncf::unsorted_heavy_c(s) < ncf::kHeavyMin)
+        return 0;
+    if (NCF_FILL_IN_KERNEL == 1 && use_fused(s, h) && fb_variant(s, h, n) == NCF_FB_WAVE && h->force_generic != 6 &&
+        ncf::wave_fill_supported(s))
+        return 1;
+    return 2;
 }
 
 static ncf::FillArgs fill_args(const ncf_shape_t& s, const ncf::WsLayout& L, void* ws) {
@@ -728,10 +753,18 @@ static int train_step_impl(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t
     // deferred decay on one stream: the group metrics (groups <= 8 the kernel does not compute)
     // ride in the touched-row update launch
     fb.defer_metrics = lazy && side_stream_mode() == 0;
-    const bool kfill = lazy && fill_in_kernel(*s, L, h, n);
+    const int fmode = lazy ? fill_in_kernel(*s, L, h, n) : 0;
+    const bool kfill = fmode != 0;
     const ncf::FillArgs fa = kfill ? fill_args(*s, L, ws) : ncf::FillArgs{};
+    if (fmode == 2) {
+        prof_begin(NCF_K_INDEX, st);
+        hipError_t e = ncf::launch_fill_ahead(fa, users, items, n, index_fold(*s, h), st);
+        prof_end(NCF_K_INDEX, st);
+        if (e != hipSuccess) return hip_check(e, "index fill");
+    }
     if (int r = run_fb(*s, L, model, h, users, items, labels, n, ws, probs_out, &fb, st, false,
-                       lazy && !kfill ? catchup_touched : nullptr, &cc, kfill ? &fa : nullptr))
+                       lazy && !kfill ? catchup_touched : nullptr, &cc, fmode == 1 ? &fa : nullptr,
+                       fmode == 2))
         return r;
     // the index (side stream) must be complete before the side stream takes the dense tail
     if (int r = index_join(st, fb)) return r;

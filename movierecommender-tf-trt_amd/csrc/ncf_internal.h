@@ -131,7 +131,8 @@ template <bool UNIQ>
 // may assume nothing writes)
 __device__ inline void scan_local_body(const int32_t* cnt, int64_t r1, int32_t* __restrict__ offs,
                                        int32_t* __restrict__ tot, int32_t* __restrict__ uloc,
-                                       int32_t* __restrict__ utot, int blk, int32_t* __restrict__ move_to = nullptr) {
+                                       int32_t* __restrict__ utot, int blk, int32_t* __restrict__ move_to = nullptr,
+                                       int32_t* __restrict__ zero_at_end = nullptr) {
     __shared__ int sw[4];
     const int64_t base = (int64_t)blk * kScanBlock + threadIdx.x * 8;
     // 8 keys per thread: two int4 loads / stores when all 8 are inside (the workspace regions
@@ -199,9 +200,12 @@ __device__ inline void scan_local_body(const int32_t* cnt, int64_t r1, int32_t* 
         }
         if (threadIdx.x == 0) utot[blk] = utotal;
     }
-#if NCF_DEBUG_BOUNDS
+#if NCF_DEBUG_BOUNDS == 1
     if (move_to && threadIdx.x == 0 && blk < 4) printf("scan ahead blk %d: tot %d utot %d\n", blk, total, 0);
 #endif
+    // last, after every use of threadIdx.x: a `blockIdx.x == 1 && threadIdx.x == 0` store ahead of
+    // the body made hipcc (ROCm 7.2) feed the later blocks an undefined thread id
+    if (zero_at_end && blk == 0 && threadIdx.x == 0) *zero_at_end = 0;
 }
 
 // User-row folding (the north star's duplicate-index reduction, done where the gradients are
@@ -390,10 +394,16 @@ struct FillArgs {
     int32_t U, I;             // user u -> key u, item v -> key U + v
     int64_t list_cap, touched_cap, heavy_cap;  // region sizes (debug bound checks)
 };
-#if NCF_DEBUG_BOUNDS
+#if NCF_DEBUG_BOUNDS == 1
 #define NCF_BOUND(cond, ...)          \
     if (!(cond)) {                    \
         printf(__VA_ARGS__);          \
+    } else
+#elif NCF_DEBUG_BOUNDS == 2
+// no printf (the kernel's code stays close to the release build): flag bit 0x100 and skip
+#define NCF_BOUND(cond, ...)          \
+    if (!(cond)) {                    \
+        atomicOr(f.err, 0x100);       \
     } else
 #else
 #define NCF_BOUND(cond, ...)
@@ -421,7 +431,7 @@ __device__ inline void fill_wave(const FillArgs& f, const int32_t* __restrict__ 
         p1 = ca + a1 - t1;
         q0 = b0 - u0;
         q1 = cb + b1 - u1;
-#if NCF_DEBUG_BOUNDS
+#if NCF_DEBUG_BOUNDS == 1
         if (gw == 0 && lane < 4 && lane < f.nscan)
             printf("fill lane %d: tot %d utot %d pre %d upre %d nscan %d\n", lane, t0, u0, p0, q0, f.nscan);
 #endif
@@ -662,6 +672,9 @@ hipError_t launch_fb_wave(const ncf_shape_t& s, const WsLayout& L, void* ws, con
                           const FillArgs* fill = nullptr);
 // the split form runs for this shape (its weight-gradient waves can build the index: FillArgs)
 bool wave_fill_supported(const ncf_shape_t& s);
+// the in-kernel fill as a launch of its own (ncf_index.hip)
+hipError_t launch_fill_ahead(const FillArgs& f, const int32_t* users, const int32_t* items, int64_t n, int fold,
+                             hipStream_t st);
 hipError_t launch_fb_unit(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, const float* mlp,
                           const int32_t* users, const int32_t* items, const float* labels, int64_t n,
                           float inv_batch, IdSpace ids, int group, int topk, int* nslab, int* nbce, int* nmet,

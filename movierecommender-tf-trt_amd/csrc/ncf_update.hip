@@ -883,7 +883,7 @@ __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_tou
             const int64_t r = list[u];
             const int2 oc = toc[u];
             const int o = oc.x, c = oc.y;
-#if NCF_DEBUG_BOUNDS
+#if NCF_DEBUG_BOUNDS == 1
             if (u < 0 || u >= so.mcap || r < 0 || r >= ca.lazy_rows || o < 0 || c < 0 || o + c > so.mcap) {
                 if (threadIdx.x == 0) printf("heavy %d: u %d nlist %d r %lld o %d c %d (skipped)\n", hi, u, *nlist, (long long)r, o, c);
                 continue;
@@ -1088,7 +1088,7 @@ __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_tou
             bool has = rl.on && i < n;
             int r = has ? list[i] : 0;
             int2 oc = has ? toc[i] : make_int2(0, 0);
-#if NCF_DEBUG_BOUNDS
+#if NCF_DEBUG_BOUNDS == 1
             if (has && (i >= so.mcap || r < 0 || r >= ca.lazy_rows || oc.x < 0 || oc.y < 0 || oc.x + oc.y > so.mcap)) {
                 if (ql == 0) printf("row %lld of %lld: r %d o %d c %d (skipped)\n", (long long)i, (long long)n, r, oc.x, oc.y);
                 has = false;
@@ -1142,7 +1142,7 @@ __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_tou
                     const int c2 = __shfl(srt, base + min(j + 2, gsz - 1), 64);
                     const int c3 = __shfl(srt, base + min(j + 3, gsz - 1), 64);
                     const bool v0 = act && j < c, v1 = act && j + 1 < c, v2 = act && j + 2 < c, v3 = act && j + 3 < c;
-#if NCF_DEBUG_BOUNDS
+#if NCF_DEBUG_BOUNDS == 1
                     if ((v0 && (unsigned)c0 >= (unsigned)so.mcap) || (v1 && (unsigned)c1 >= (unsigned)so.mcap) ||
                         (v2 && (unsigned)c2 >= (unsigned)so.mcap) || (v3 && (unsigned)c3 >= (unsigned)so.mcap))
                         printf("sum r %d j %d c %d ids %d %d %d %d\n", r, j, c, c0, c1, c2, c3);
@@ -1530,16 +1530,15 @@ __global__ __launch_bounds__(kBlock) void k_stats_scan(float* __restrict__ summa
         }
         stats_body(summary, reg_emb, nreg_emb, reg_mlp, nreg_mlp, inv_batch, stats, step, bump, red);
     } else {
-        if (blockIdx.x == 1 && threadIdx.x == 0) *sc.heavy_n = 0;
-        scan_local_body<true>(sc.cnt, sc.r1, sc.offs, sc.tot, sc.uloc, sc.utot, (int)blockIdx.x - 1, sc.cursor);
+        scan_local_body<true>(sc.cnt, sc.r1, sc.offs, sc.tot, sc.uloc, sc.utot, (int)blockIdx.x - 1, sc.cursor,
+                              sc.heavy_n);
     }
 }
 
 // The next batch's per-block key scan alone (k_stats_scan's blocks >= 1), for a counting-ahead
 // update that has no stats launch of its own behind it (user-partitioned data parallelism).
 __global__ __launch_bounds__(kBlock) void k_scan_ahead(ScanAhead sc) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) *sc.heavy_n = 0;
-    scan_local_body<true>(sc.cnt, sc.r1, sc.offs, sc.tot, sc.uloc, sc.utot, (int)blockIdx.x, sc.cursor);
+    scan_local_body<true>(sc.cnt, sc.r1, sc.offs, sc.tot, sc.uloc, sc.utot, (int)blockIdx.x, sc.cursor, sc.heavy_n);
 }
 
 hipError_t launch_scan_ahead(const WsLayout& L, void* ws, int64_t keys, hipStream_t st) {
