@@ -122,7 +122,7 @@ struct SideStream {
 
 int side_stream_mode() {
     static const int mode = [] {
-        const char* e = getenv("NCF_SIDE_STREAM");
+        const char* e = ncf::experiment_env("NCF_SIDE_STREAM");
         return e ? atoi(e) : 0;
     }();
     return mode;
@@ -196,7 +196,7 @@ hipError_t launch_predict(const ncf_shape_t& s, const ncf_hyper_t* h, const ncf:
 // per call (6: the wave kernel's one-wave form).  bf16 operands run on the unit kernel only.
 int fb_variant(const ncf_shape_t& s, const ncf_hyper_t* h, int64_t n) {
     static const int mode = [] {
-        const char* e = getenv("NCF_FB_KERNEL");
+        const char* e = ncf::experiment_env("NCF_FB_KERNEL");
         if (!e) return 0;
         return strcmp(e, "tile") == 0 ? NCF_FB_TILE : strcmp(e, "unit") == 0 ? NCF_FB_UNIT
                                                     : strcmp(e, "wave") == 0 ? NCF_FB_WAVE : 0;
@@ -219,7 +219,7 @@ int fb_variant(const ncf_shape_t& s, const ncf_hyper_t* h, int64_t n) {
 // NCF_FOLD_USERS=0 turns it off (A/B measurements)
 int index_fold(const ncf_shape_t& s, const ncf_hyper_t* h) {
     static const bool on = [] {
-        const char* e = getenv("NCF_FOLD_USERS");
+        const char* e = ncf::experiment_env("NCF_FOLD_USERS");
         return !e || atoi(e) != 0;
     }();
     return h && on ? ncf::fold_of(h->group, use_fused(s, h)) : 0;
@@ -718,15 +718,19 @@ static int fill_in_kernel(const ncf_shape_t& s, const ncf::WsLayout& L, const nc
     return 2;
 }
 
-static ncf::FillArgs fill_args(const ncf_shape_t& s, const ncf::WsLayout& L, void* ws) {
+static ncf::FillArgs fill_args(const ncf_shape_t& s, const ncf::WsLayout& L, void* ws, ncf_model_t* model,
+                               ncf_optim_t* optim, const ncf_hyper_t* h) {
     using ncf::at;
+    const ncf::FillReplay rp{model->emb, optim->emb_m, optim->emb_v, s.row_width, optim->row_step, optim->step,
+                             h->lr, h->beta_1, h->beta_2, h->epsilon, ncf::lazy_bound(s, *h)};
     return ncf::FillArgs{at<int32_t>(ws, L.cnt), at<const int32_t>(ws, L.offs_local), at<const int32_t>(ws, L.tot),
                          at<const int32_t>(ws, L.uloc), at<const int32_t>(ws, L.utot), L.nscan, L.keys + 1,
                          at<int32_t>(ws, L.offs), at<int32_t>(ws, L.list), at<int32_t>(ws, L.touched),
                          at<int2>(ws, L.touched_oc), at<int32_t>(ws, L.nuniq), at<int32_t>(ws, L.heavy),
                          at<int32_t>(ws, L.heavy_n), ncf::unsorted_heavy_c(s), at<int32_t>(ws, L.err),
                          at<int32_t>(ws, L.ifold), s.num_users, s.num_items, L.list_cap,
-                         L.keys < 2 * L.max_batch ? L.keys : 2 * L.max_batch, 2 * L.max_batch / ncf::kHeavyMin + 1};
+                         L.keys < 2 * L.max_batch ? L.keys : 2 * L.max_batch, 2 * L.max_batch / ncf::kHeavyMin + 1,
+                         rp};
 }
 
 static int train_step_impl(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* h,
@@ -755,7 +759,7 @@ static int train_step_impl(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t
     fb.defer_metrics = lazy && side_stream_mode() == 0;
     const int fmode = lazy ? fill_in_kernel(*s, L, h, n) : 0;
     const bool kfill = fmode != 0;
-    const ncf::FillArgs fa = kfill ? fill_args(*s, L, ws) : ncf::FillArgs{};
+    const ncf::FillArgs fa = kfill ? fill_args(*s, L, ws, model, optim, h) : ncf::FillArgs{};
     if (fmode == 2) {
         prof_begin(NCF_K_INDEX, st);
         hipError_t e = ncf::launch_fill_ahead(fa, users, items, n, index_fold(*s, h), st);

@@ -535,22 +535,6 @@ hipError_t launch_shard_plan(const ncf_shape_t& s, const WsLayout& L, void* ws, 
     return build<kKeyPairPerm, true>(L, ws, ks, 2 * n, L.keys, po, (int)((2 * n + 31) / 32), st);
 }
 
-// The in-kernel fill's body (FillArgs) as a launch of its own: one wave per 64 keys / contributions
-// of the larger of the two, before the forward/backward (forward/backward kernels without idle waves)
-__global__ __launch_bounds__(kBlock) void k_fill_ahead(FillArgs f, const int32_t* __restrict__ users,
-                                                       const int32_t* __restrict__ items, int64_t n, int fold) {
-    fill_wave(f, users, items, n, fold, (int)blockIdx.x * (kBlock / 64) + (int)(threadIdx.x >> 6),
-              (int)gridDim.x * (kBlock / 64));
-}
-
-hipError_t launch_fill_ahead(const FillArgs& f, const int32_t* users, const int32_t* items, int64_t n, int fold,
-                             hipStream_t st) {
-    if (f.nscan < 1 || f.nscan > kMaxFillScan) return hipErrorInvalidValue;
-    const int64_t work = f.r1 > 2 * n ? f.r1 : 2 * n;
-    launch(k_fill_ahead, grid_for(work, 2048), kBlock, 0, st, f, users, items, n, fold);
-    return hipGetLastError();
-}
-
 __global__ void k_fold_check(const int32_t* __restrict__ ifold, int fold, int32_t* __restrict__ err) {
     if (threadIdx.x == 0 && *ifold != fold) atomicOr(err, kErrFold);
 }

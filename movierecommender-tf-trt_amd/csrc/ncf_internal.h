@@ -3,6 +3,7 @@
 #pragma once
 
 #include <climits>
+#include <cstdlib>
 
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
@@ -27,6 +28,14 @@ constexpr int kHeavyMin = 8;           // smallest list length the touched-row u
 #ifndef NCF_DEBUG_BOUNDS
 #define NCF_DEBUG_BOUNDS 0   // 1: printf + skip on out-of-range index-path accesses (diagnostic builds)
 #endif
+
+// Kernel-selection switches for A/B experiments (NCF_FB_KERNEL, NCF_WAVE_SPLIT, NCF_FOLD_USERS,
+// NCF_UNIT_SCHED, NCF_SIDE_STREAM): read from the environment only by a library built with
+// -DNCF_EXPERIMENT_ENV=1 (tools/ variants); the product library ignores them
+#ifndef NCF_EXPERIMENT_ENV
+#define NCF_EXPERIMENT_ENV 0
+#endif
+inline const char* experiment_env(const char* name) { return NCF_EXPERIMENT_ENV ? getenv(name) : nullptr; }
 
 // Scalars every kernel of a step reads (device copy of hyper + derived).
 struct StepScalars {
@@ -373,6 +382,16 @@ __device__ inline void sort_rows_body(const int32_t* __restrict__ offs, int64_t 
 // entries across the lanes of their row group, longer ones — listed in `heavy` — block-wide).  A
 // run that takes a counter below zero gives the excess back (k_fill_big's rule): a residue can
 // only sit at a counted key, i.e. in the touched list, where the update checks it.
+// The rows the in-kernel fill replays when the counted set turns out stale (ncf_adam.h
+// fill_stale_replay): the table's state and the Adam hyper-parameters (row_step nullptr: none)
+struct FillReplay {
+    float *emb, *m, *v;
+    int W;
+    int32_t* row_step;
+    const int32_t* step;
+    float lr, b1, b2, eps;
+    int64_t lazy_rows;
+};
 struct FillArgs {
     int32_t* cnt;             // per-key cursors: the counts the scan ahead copied (ws cnt)
     const int32_t* local;     // per-scan-block exclusive offsets (ws offs_local)
@@ -393,6 +412,7 @@ struct FillArgs {
     int32_t* ifold;
     int32_t U, I;             // user u -> key u, item v -> key U + v
     int64_t list_cap, touched_cap, heavy_cap;  // region sizes (debug bound checks)
+    FillReplay rp;
 };
 #if NCF_DEBUG_BOUNDS == 1
 #define NCF_BOUND(cond, ...)          \
@@ -409,11 +429,24 @@ struct FillArgs {
 #define NCF_BOUND(cond, ...)
 #endif
 
+constexpr int kFillRowsPerLane = 4;     // fill_wave's RU: keys per lane and pass of the rows part
+constexpr int kFillContribPerLane = 2;  // its CU: contributions per lane and pass
+
+// the count key had in the counted set (0: the counted set missed it — not in the touched list)
+__device__ inline int fill_count0(const FillArgs& f, int key) {
+    const int nx = (key + 1) % kScanBlock != 0 ? f.local[key + 1] : f.tot[key / kScanBlock];
+    return nx - f.local[key];
+}
+
 // Wave gw of nw: its share of the fill of batch (users, items, n) folded by `fold`.  The
 // exclusive prefixes of the scan-block totals stay in registers (lane l: blocks l and l + 64) and
-// are read with lane shuffles, so every loop below is wave-uniform.
+// are read with lane shuffles, so every loop below is wave-uniform.  on_stale(stale, key): called by
+// the whole wave after each pass of contributions, stale = this lane's contribution found no slot
+// (the counted set differs from the ids passed).  PART: 1 the rows, 2 the contributions, 3 both
+template <int PART = 3, class OnStale>
 __device__ inline void fill_wave(const FillArgs& f, const int32_t* __restrict__ users,
-                                 const int32_t* __restrict__ items, int64_t n, int fold, int gw, int nw) {
+                                 const int32_t* __restrict__ items, int64_t n, int fold, int gw, int nw,
+                                 OnStale on_stale) {
     const int lane = threadIdx.x & 63;
     int p0, p1, q0, q1;  // pre[lane], pre[lane + 64], upre[lane], upre[lane + 64]
     {
@@ -451,8 +484,8 @@ __device__ inline void fill_wave(const FillArgs& f, const int32_t* __restrict__ 
     const int64_t rstep = (int64_t)nw * 64;
     // rows: offsets, the touched list with (offset, count), the heavy rows (RU rows per lane and
     // pass, their loads issued together)
-    constexpr int RU = 4;
-    for (int64_t rw = (int64_t)gw * 64; rw < f.r1; rw += RU * rstep) {
+    constexpr int RU = kFillRowsPerLane;
+    for (int64_t rw = (int64_t)gw * 64; (PART & 1) && rw < f.r1; rw += RU * rstep) {
         int lo[RU], lo1[RU], ul[RU];
 #pragma unroll
         for (int j = 0; j < RU; ++j) {
@@ -484,7 +517,7 @@ __device__ inline void fill_wave(const FillArgs& f, const int32_t* __restrict__ 
             }
         }
     }
-    {
+    if constexpr ((PART & 1) != 0) {
         const int nu = f.uloc[K] + upre(K);
         if (gw == 0 && lane == 0) {
             *f.nuniq = nu;
@@ -496,8 +529,8 @@ __device__ inline void fill_wave(const FillArgs& f, const int32_t* __restrict__ 
     const int64_t m = 2 * n;
     const uint64_t par = (lane & 1) ? 0xAAAAAAAAAAAAAAAAull : 0x5555555555555555ull;
     const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
-    constexpr int CU = 2;
-    for (int64_t cb = (int64_t)gw * 64; cb < m; cb += CU * rstep) {
+    constexpr int CU = kFillContribPerLane;
+    for (int64_t cb = (int64_t)gw * 64; (PART & 2) && cb < m; cb += CU * rstep) {
         int id[CU], hid[CU];
 #pragma unroll
         for (int j = 0; j < CU; ++j) {
@@ -547,7 +580,10 @@ __device__ inline void fill_wave(const FillArgs& f, const int32_t* __restrict__ 
                 NCF_BOUND(li >= 0 && li < f.list_cap && key < f.r1 - 1, "fill c %lld key %d list %lld cap %lld\n",
                           (long long)c, key, (long long)li, (long long)f.list_cap)
                 f.list[li] = (int)c;
-            } else if (ok) atomicOr(f.err, kErrStaleCount);
+            }
+            const bool stale = ok && slot < 0;
+            if (stale) atomicOr(f.err, kErrStaleCount);
+            on_stale(stale, key);
         }
     }
 }
@@ -673,6 +709,8 @@ hipError_t launch_fb_wave(const ncf_shape_t& s, const WsLayout& L, void* ws, con
 // the split form runs for this shape (its weight-gradient waves can build the index: FillArgs)
 bool wave_fill_supported(const ncf_shape_t& s);
 // the in-kernel fill as a launch of its own (ncf_index.hip)
+// (ncf_update.hip) the fill, and — the counted set stale — the replay of the rows it missed to
+// *step (the stale-count gate's rule, before the forward pass reads them; f.rp)
 hipError_t launch_fill_ahead(const FillArgs& f, const int32_t* users, const int32_t* items, int64_t n, int fold,
                              hipStream_t st);
 hipError_t launch_fb_unit(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, const float* mlp,
@@ -714,7 +752,7 @@ hipError_t launch_laymid(const ncf_shape_t& s, const float* mlp, const float* h1
                          const float* labels, const int32_t* users, const int32_t* items, int64_t n, IdSpace ids,
                          float inv_batch, float* probs, float* dzo, float* g1, float* slabs, float* part_bce,
                          int grid, hipStream_t st);
-// its forward half alone (predict / evaluate): probs, and with labels the BCE partials
+// (dzo nullptr: the forward half alone — probs, and with labels the BCE partials; predict / evaluate)
 hipError_t launch_predict_layered(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb,
                                   const float* mlp, const int32_t* users, const int32_t* items, const float* labels,
                                   int64_t n, float* probs, IdSpace ids, int* nbce, hipStream_t st);

@@ -443,14 +443,7 @@ hipError_t configure(const void* k) {
 
 }  // namespace
 
-// NCF_LAYER1_MFMA=0 keeps the rocBLAS layer 1 (A/B)
-bool layer1_supported(const ncf_shape_t& s) {
-    static const int on = [] {
-        const char* e = getenv("NCF_LAYER1_MFMA");
-        return e && *e ? atoi(e) : 1;
-    }();
-    return on != 0 && l1matches<L1ShapeD>(s);
-}
+bool layer1_supported(const ncf_shape_t& s) { return l1matches<L1ShapeD>(s); }
 
 hipError_t launch_layer1_fwd(const ncf_shape_t& s, const float* emb, const float* mlp, const int32_t* users,
                              const int32_t* items, int64_t n, IdSpace ids, float* x0, float* gmf, float* h1,

@@ -269,9 +269,9 @@ hipError_t launch_predict_layered(const ncf_shape_t& s, const WsLayout& L, void*
                                   const float* mlp, const int32_t* users, const int32_t* items, const float* labels,
                                   int64_t n, float* probs, IdSpace ids, int* nbce, hipStream_t st) {
     if (!layered_supported(s) || n > L.max_batch) return hipErrorInvalidValue;
-    rocblas_handle bh;
-    hipError_t e = blas(st, &bh);
-    if (e != hipSuccess) return e;
+    // (the rocBLAS handle only on the general-shape path below: none on config D's)
+    rocblas_handle bh = nullptr;
+    hipError_t e = hipSuccess;
     const int nl = s.num_layers, G = s.gmf_dim, G4 = s.gmf_stride, W = s.row_width;
     const int du = s.du, di = s.di, Ll = s.layers[nl - 1];
     float* act = at<float>(ws, L.act);
@@ -285,6 +285,18 @@ hipError_t launch_predict_layered(const ncf_shape_t& s, const WsLayout& L, void*
     const bool vec4 = du % 4 == 0 && di % 4 == 0 && G == G4 && W % 4 == 0;
     // layer 1 on hand-written MFMA with the gather fused (ncf_layer1.hip), where the shape has it
     const bool l1 = layer1_supported(s);
+    if (l1 && laymid_supported(s)) {
+        // config D: layers 2.., the output and the BCE partials in the middle kernel's forward-only
+        // form (ncf_laymid.hip) — no vendor GEMM on the evaluation path either
+        e = launch_layer1_fwd(s, emb, mlp, users, items, n, ids, X[0], nullptr, X[1], st);
+        if (e != hipSuccess) return e;
+        const int64_t units = (n + 15) / 16;
+        const int grid = (int)(units >= 8 * 512 ? 512 : (units + 7) / 8);
+        e = launch_laymid(s, mlp, X[1], emb, labels, users, items, n, ids, 1.0f, probs, nullptr, nullptr, nullptr,
+                          at<float>(ws, L.part_bce), grid, st);
+        *nbce = labels ? grid : 0;
+        return e;
+    }
     if (l1)
         e = launch_layer1_fwd(s, emb, mlp, users, items, n, ids, X[0], gmf, X[1], st);
     else if (vec4)
@@ -293,6 +305,8 @@ hipError_t launch_predict_layered(const ncf_shape_t& s, const WsLayout& L, void*
     else
         launch(k_lay_gather, grid_for(n * (du + di + G)), kBlock, 0, st, emb, users, items, n, ids, W, G, G4, du, di,
                X[0], gmf);
+    if (e != hipSuccess) return e;
+    e = blas(st, &bh);
     if (e != hipSuccess) return e;
     for (int l = l1 ? 2 : 1; l < nl; ++l) {
         const int lin = s.layers[l - 1], lout = s.layers[l];
@@ -316,27 +330,16 @@ hipError_t launch_predict_layered(const ncf_shape_t& s, const WsLayout& L, void*
 
 constexpr int kLayeredSlabs = 64;  // batch chunks of the weight-gradient GEMMs (<= kMaxSlabs)
 
-// NCF_DW1_MFMA=0 keeps the rocBLAS dW1 GEMM of the middle-kernel path (A/B)
-bool dw1_mfma() {
-    static const int on = [] {
-        const char* e = getenv("NCF_DW1_MFMA");
-        return e && *e ? atoi(e) : 1;
-    }();
-    return on != 0;
-}
-
-bool layered_all_mfma(const ncf_shape_t& s) {
-    return layer1_supported(s) && laymid_supported(s) && dw1_mfma();
-}
+bool layered_all_mfma(const ncf_shape_t& s) { return layer1_supported(s) && laymid_supported(s); }
 
 
 hipError_t launch_fb_layered(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, const float* mlp,
                              const int32_t* users, const int32_t* items, const float* labels, int64_t n,
                              float inv_batch, IdSpace ids, int* nslab, int* nbce, hipStream_t st) {
     if (!layered_supported(s) || n > L.max_batch) return hipErrorInvalidValue;
-    rocblas_handle bh;
-    hipError_t e = blas(st, &bh);
-    if (e != hipSuccess) return e;
+    // (the rocBLAS handle only on the general-shape path below: none on config D's)
+    rocblas_handle bh = nullptr;
+    hipError_t e = hipSuccess;
     const int nl = s.num_layers, G = s.gmf_dim, G4 = s.gmf_stride, W = s.row_width;
     const int du = s.du, di = s.di, Ll = s.layers[nl - 1];
     const int wo_off = s.layer_off[0];
@@ -386,32 +389,17 @@ hipError_t launch_fb_layered(const ncf_shape_t& s, const WsLayout& L, void* ws, 
         e = launch_laymid(s, mlp, X[1], emb, labels, users, items, n, ids, inv_batch, probs, dzo, Gd[1], slab,
                           at<float>(ws, L.part_bce), nsl, st);
         if (e != hipSuccess) return e;
-        const int lin = s.layers[0], lout = s.layers[1];
-        const int64_t P = s.mlp_params;
-        float* dW1 = slab + s.layer_off[1];
-        if (dw1_mfma()) {
-            // dW1 on hand-written MFMA (ncf_layer1.hip), one workgroup per chunk
-            e = launch_layer1_dw(s, X[0], Gd[1], n, chunk, nsl, slab, st);
-            if (e != hipSuccess) return e;
-        } else if (nfull > 0) {
-            e = blas_err(rocblas_sgemm_strided_batched(
-                bh, rocblas_operation_none, rocblas_operation_transpose, lout, lin, (int)chunk, &one, Gd[1], lout,
-                (rocblas_stride)chunk * lout, X[0], lin, (rocblas_stride)chunk * lin, &zero, dW1, lout, (rocblas_stride)P,
-                nfull));
-            if (e != hipSuccess) return e;
-        }
-        if (rem > 0 && !dw1_mfma()) {
-            e = blas_err(rocblas_sgemm(bh, rocblas_operation_none, rocblas_operation_transpose, lout, lin, rem, &one,
-                                       Gd[1] + (int64_t)nfull * chunk * lout, lout, X[0] + (int64_t)nfull * chunk * lin,
-                                       lin, &zero, dW1 + (int64_t)nfull * P, lout));
-            if (e != hipSuccess) return e;
-        }
+        // dW1 on hand-written MFMA (ncf_layer1.hip), one workgroup per chunk
+        e = launch_layer1_dw(s, X[0], Gd[1], n, chunk, nsl, slab, st);
+        if (e != hipSuccess) return e;
         e = launch_layer1_bwd(s, emb, mlp, users, items, n, ids, (const float*)dzo, (const float*)Gd[1], gs, st);
         if (e != hipSuccess) return e;
         *nbce = nsl;
         *nslab = nsl;
         return hipGetLastError();
     }
+    e = blas(st, &bh);
+    if (e != hipSuccess) return e;
     for (int l = l1 ? 2 : 1; l < nl; ++l) {
         const int lin = s.layers[l - 1], lout = s.layers[l];
         const float* Wl = mlp + s.layer_off[l];

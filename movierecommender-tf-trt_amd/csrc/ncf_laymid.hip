@@ -124,7 +124,9 @@ struct MidArgs {
     float* part_bce;
 };
 
-template <class S>
+// FWD: forward only (ncf_predict / ncf_evaluate): probabilities and, labels given, the BCE partial
+// of the workgroup; no gradients
+template <class S, bool FWD>
 __global__ __launch_bounds__(256, 1) void k_lay_mid(MidArgs a) {
     constexpr int L1 = S::L1, L2 = S::L2, L3 = S::L3, G = S::G, B1 = S::B1, B2 = S::B2, B3 = S::B3, GQ = S::GQ;
     extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -235,7 +237,7 @@ __global__ __launch_bounds__(256, 1) void k_lay_mid(MidArgs a) {
             }
         }
         const int cu = in ? a.users[s] : 0, cv = in ? a.items[s] : 0;
-        const float y = in ? a.labels[s] : 0.f;
+        const float y = in && a.labels ? a.labels[s] : 0.f;
         const bool ok = in && (unsigned)cu < (unsigned)a.ids.ubound && (unsigned)cv < (unsigned)a.ids.ibound;
         {
             // the GMF product of the two rows (dims GQ lq .. GQ lq + GQ - 1; zero for a masked sample)
@@ -250,7 +252,7 @@ __global__ __launch_bounds__(256, 1) void k_lay_mid(MidArgs a) {
         }
         // H1^T for dW2
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
+        for (int r = 0; r < 4 && !FWD; ++r) {
             float v[B1];
 #pragma unroll
             for (int t = 0; t < B1; ++t) v[t] = h1[t][r];
@@ -272,7 +274,7 @@ __global__ __launch_bounds__(256, 1) void k_lay_mid(MidArgs a) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) h2[t][r] = fmaxf(h2[t][r] + b2r[t][r], 0.f);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
+        for (int r = 0; r < 4 && !FWD; ++r) {
             float v[B2];
 #pragma unroll
             for (int t = 0; t < B2; ++t) v[t] = h2[t][r];
@@ -306,7 +308,7 @@ __global__ __launch_bounds__(256, 1) void k_lay_mid(MidArgs a) {
         const float dz = ok && p >= eps && p <= hi_clip ? (p - y) * a.inv_batch : 0.0f;
         if (g == 0 && in) {
             a.probs[s] = ok ? p : __int_as_float(0x7fc00000);
-            a.dzo[s] = dz;
+            if constexpr (!FWD) a.dzo[s] = dz;
         }
         {
             const float pc = fminf(fmaxf(p, eps), hi_clip);
@@ -315,6 +317,7 @@ __global__ __launch_bounds__(256, 1) void k_lay_mid(MidArgs a) {
             acc_bce += g == 0 && ok ? bce : 0.f;
             acc_dbo += g == 0 ? dz : 0.f;
         }
+        if constexpr (FWD) continue;
 #pragma unroll
         for (int e = 0; e < GQ; ++e) agmf[e] += dz * gm[e];
         // ---- G3 (registers) and its transposed copy
@@ -400,6 +403,15 @@ __global__ __launch_bounds__(256, 1) void k_lay_mid(MidArgs a) {
         }
     }
 
+    if constexpr (FWD) {
+        // the workgroup's BCE partial, the four waves summed as the training epilogue sums them
+        acc_bce = group_allsum(row_sum(acc_bce));
+        __syncthreads();
+        if (lane == 0) lds[wv] = acc_bce;
+        __syncthreads();
+        if (threadIdx.x == 0 && a.labels) a.part_bce[blockIdx.x] = (lds[0] + lds[2]) + (lds[1] + lds[3]);
+        return;
+    }
     // ---- epilogue: per-lane sums, then the four waves' contributions in LDS, one slab per workgroup
 #pragma unroll
     for (int t = 0; t < B2; ++t) ab2[t] = group_allsum(ab2[t]);
@@ -502,14 +514,9 @@ using MShapeD = MShape<128, 64, 32, 128>;  // config D after layer 1
 
 }  // namespace
 
-// NCF_LAYMID_MFMA=0 keeps the rocBLAS layers 2.. (A/B)
 bool laymid_supported(const ncf_shape_t& s) {
-    static const int on = [] {
-        const char* e = getenv("NCF_LAYMID_MFMA");
-        return e && *e ? atoi(e) : 1;
-    }();
     using S = MShapeD;
-    return on != 0 && s.num_layers == 4 && s.layers[1] == S::L1 && s.layers[2] == S::L2 && s.layers[3] == S::L3 &&
+    return s.num_layers == 4 && s.layers[1] == S::L1 && s.layers[2] == S::L2 && s.layers[3] == S::L3 &&
            s.gmf_dim == S::G && s.gmf_stride == S::G && layer1_supported(s);
 }
 
@@ -518,17 +525,19 @@ hipError_t launch_laymid(const ncf_shape_t& s, const float* mlp, const float* h1
                          float inv_batch, float* probs, float* dzo, float* g1, float* slabs, float* part_bce,
                          int grid, hipStream_t st) {
     using S = MShapeD;
-    if (!laymid_supported(s) || grid < 1) return hipErrorInvalidValue;
+    const bool fwd = dzo == nullptr;
+    if (!laymid_supported(s) || grid < 1 || grid > kMaxSlabs || (!fwd && (!labels || !g1 || !slabs)))
+        return hipErrorInvalidValue;
     static bool cfg = false;
     if (!cfg) {
-        if (hipError_t e = hipFuncSetAttribute((const void*)k_lay_mid<S>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               (int)S::LDS_BYTES))
-            return e;
+        for (const void* k : {(const void*)k_lay_mid<S, false>, (const void*)k_lay_mid<S, true>})
+            if (hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)S::LDS_BYTES))
+                return e;
         cfg = true;
     }
     MidArgs a{mlp, s.layer_off[2], s.layer_off[3], s.layer_off[0], s.layer_off[1] + s.layers[0] * s.layers[1], h1, emb,
               s.row_width, labels, users, items, n, ids, inv_batch, probs, dzo, g1, slabs, s.mlp_params, part_bce};
-    launch(k_lay_mid<S>, grid, 256, S::LDS_BYTES, st, a);
+    launch(fwd ? k_lay_mid<S, true> : k_lay_mid<S, false>, grid, 256, S::LDS_BYTES, st, a);
     return hipGetLastError();
 }
 

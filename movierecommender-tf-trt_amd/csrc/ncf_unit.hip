@@ -865,7 +865,7 @@ hipError_t launch_unit_one(const WsLayout& L, void* ws, const float* emb, const 
 // NCF_UNIT_SCHED=1|2|64 forces one (64: one group of 64-sample units)
 int unit_sched(int64_t n) {
     static const int forced = [] {
-        const char* e = getenv("NCF_UNIT_SCHED");
+        const char* e = ncf::experiment_env("NCF_UNIT_SCHED");
         return e ? atoi(e) : 0;
     }();
     if (forced == 1 || forced == 2 || forced == 64) return forced;

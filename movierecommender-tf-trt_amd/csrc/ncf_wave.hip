@@ -36,6 +36,7 @@
 #include <cstdlib>
 #include <type_traits>
 
+#include "ncf_adam.h"
 #include "ncf_common.h"
 #include "ncf_internal.h"
 
@@ -43,7 +44,6 @@ namespace ncf {
 namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -527,7 +527,8 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
     // launch disappear.
     if constexpr (SPLIT) {
         if (dwave && fa.cnt)
-            fill_wave(fa, users, items, n, FOLD, (int)blockIdx.x * 4 + pw, (int)gridDim.x * 4);
+            fill_wave(fa, users, items, n, FOLD, (int)blockIdx.x * 4 + pw, (int)gridDim.x * 4,
+                          [&](bool stale, int key) { fill_stale_replay(fa, stale, key); });
     }
     // GU phase 0: P_u = W1_u^T x_u of every group of this chain wave's units, one 16-group tile per
     // FOLD units (k-step q takes user feature XH lq + q), into gpart
@@ -1541,7 +1542,7 @@ bool wmatches(const ncf_shape_t& s) {
 // NCF_WAVE_SPLIT (environment, read once): 0 forces the one-wave form on shapes the split form fits
 static bool split_enabled() {
     static const int on = [] {
-        const char* e = getenv("NCF_WAVE_SPLIT");
+        const char* e = ncf::experiment_env("NCF_WAVE_SPLIT");
         return e && *e ? atoi(e) : 1;
     }();
     return on != 0;

@@ -37,3 +37,19 @@ def test_integration_example_runs(tmp_path):
     assert len(h["loss"]) == 2 and np.isfinite(h["loss"]).all()
     assert np.isfinite(h["val_output_hr"]).all()
     assert gpu_available()
+
+
+def test_integration_ctypes_stub_runs():
+    """INTEGRATION.md §2's ctypes stub, as written (the library path aside): one training step
+    through the bare C ABI, Keras `iterations` bumped, a finite BCE near log(2) for near-zero
+    initial weights."""
+    import torch
+    from movierec import _native as N
+    from test_integration_doc import stub_code
+    code = stub_code().replace('ctypes.CDLL("libmovierec_ncf.so")', "ctypes.CDLL(%r)" % N.LIB_PATH)
+    ns = {}
+    exec(compile(code, "INTEGRATION.md", "exec"), ns)
+    torch.cuda.synchronize()
+    assert int(ns["state"][4].item()) == 1
+    assert np.isfinite(ns["loss"]) and 0.3 < ns["loss"] < 1.0, ns["loss"]
+    assert torch.isfinite(ns["emb"]).all()
