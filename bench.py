@@ -127,12 +127,18 @@ def parse():
     return ap.parse_args()
 
 
+def experiment_env(name, default):
+    """A kernel-selection switch of the library: only a -DNCF_EXPERIMENT_ENV=1 build reads it
+    (csrc/ncf_internal.h experiment_env); the product library runs its default."""
+    return os.environ.get(name, default) if os.environ.get("NCF_EXPERIMENT_ENV") == "1" else default
+
+
 def grad_rows(eng, batch, group):
     """Per-sample gradient rows one batch produces: B item rows plus the user rows — one per
     group when the fused kernel folds a group's user rows (include/movierec_ncf.h "User-row
     folding"; the synthetic batches share the user within a group), else B."""
     fused = bool(eng.fast_path)
-    fold = group if (fused and group in (2, 4, 8) and os.environ.get("NCF_FOLD_USERS", "1") != "0") else 1
+    fold = group if (fused and group in (2, 4, 8) and experiment_env("NCF_FOLD_USERS", "1") != "0") else 1
     return batch + batch // fold
 
 
@@ -199,8 +205,8 @@ def fwd_bwd_executed_flops(cfg, batch, group, kpath):
     of dX and of dW1 once per group of F = group samples, i.e. 3 x 2 x (L0 / 2) x L1 flops per
     sample fewer by a factor F.  None when the kernel does the per-sample work."""
     L = cfg["layers"]
-    if (kpath != "fused-mfma-wave" or group not in (2, 4, 8) or os.environ.get("NCF_WAVE_SPLIT", "1") == "0"
-            or os.environ.get("NCF_FOLD_USERS", "1") == "0"):
+    if (kpath != "fused-mfma-wave" or group not in (2, 4, 8) or experiment_env("NCF_WAVE_SPLIT", "1") == "0"
+            or experiment_env("NCF_FOLD_USERS", "1") == "0"):
         return None
     user_half = 3 * 2 * (L[0] // 2) * L[1]
     return fwd_bwd_flops(cfg) * batch - user_half * batch * (group - 1) // group
@@ -650,6 +656,17 @@ def main():
         if world > 1 and dist.get_backend() == "nccl" and not args.dense_sweep:
             native_check = native_step_check(cfg, world, rank, args.item_optimizer == "split")
             native = native_check["ok"]
+            if not native:
+                # the one-call RCCL step disagrees with the call-by-call step: no silent fallback
+                # (every rank holds the same all-reduced verdict, so every rank exits)
+                msg = json.dumps({"error": "native_step_check failed: the one-call RCCL step (ncf_user_dp_step%s) "
+                                           "does not match the call-by-call step" %
+                                           ("_split" if args.item_optimizer == "split" else ""),
+                                  "native_step_check": native_check, "n_gpus": world})
+                print(msg, file=sys.stderr)
+                if rank == 0:
+                    emit(msg)
+                sys.exit(3)
         dp = UserPartitionedDataParallel(eng, native=native, split_items=args.item_optimizer == "split",
                                          emulate_world=ew if ew > world else None)
         dp.broadcast_parameters()
@@ -729,8 +746,12 @@ def main():
     # (hipExtLaunchKernel): per-kernel durations with no marker packets added to the stream.
     if not args.no_kernel_timing:
         N.profile_enable([N.K_EMB_UPDATE, N.K_FWD_BWD, N.K_INDEX, N.K_SAMPLE, N.K_CATCHUP], 2 * args.steps)
-    t0 = time.perf_counter()
     every = max(1, min(args.time_every, args.steps // 6))   # at least 6 sampled steps
+    if mode == "user":
+        # the collectives as they run inside the step: side-stream spans and the compute stream's
+        # waits, on the same sampled steps' schedule (read after the region)
+        dp.exchange_timing(every)
+    t0 = time.perf_counter()
     # one launch group per sampled step (its events lengthen that step by ~9 us per group): the
     # forward/backward and the embedding update (the two roofline kernels) alternate, the index and
     # the catch-up (and the sampler) take every third turn
@@ -765,6 +786,24 @@ def main():
 
     def steps_of(k):
         return max(1, sum(1 for t in sampled if t is None or k in t))
+    in_step = None
+    if mode == "user":
+        xt = dp.read_exchange_timing()
+        dp.exchange_timing(0)
+        keys = ("rs_ar_ms", "ag_ms", "rs_ar_exposed_ms", "ag_exposed_ms")
+        mine = torch.tensor([xt[k_] if xt[k_] is not None else float("nan") for k_ in keys], dtype=torch.float64,
+                            device="cuda")
+        allr = [torch.zeros_like(mine) for _ in range(world)] if dist.is_initialized() else [mine]
+        if dist.is_initialized():
+            dist.all_gather(allr, mine)
+        allr = torch.stack(allr).cpu().numpy()
+        in_step = {"path": xt["path"], "sampled_steps_per_rank": xt["steps"],
+                   "note": "ms per sampled step; *_ms: the collective on the communicator's side stream, "
+                           "*_exposed_ms: the compute stream's wait for it (max/min over the ranks)"}
+        for j, k_ in enumerate(keys):
+            col = allr[:, j]
+            in_step[k_] = (None if np.isnan(col).all() else
+                           {"max": round(float(np.nanmax(col)), 4), "min": round(float(np.nanmin(col)), 4)})
     ms_emb, nl = N.profile_read(N.K_EMB_UPDATE)
     ms_fb, nfb = N.profile_read(N.K_FWD_BWD)
     ms_idx, nidx = N.profile_read(N.K_INDEX)
@@ -914,6 +953,7 @@ def main():
                                        if dp.split else "replicated: one all-reduce"),
                     "native_step": dp.comm is not None,
                     "native_step_check": native_check,
+                    "in_step": in_step,
                     "local_users": eng.num_users}
     elif mode == "sharded":
         W = eng.shape.row_width

@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define NCF_ABI_VERSION 9
+#define NCF_ABI_VERSION 10
 #define NCF_MAX_LAYERS 8
 #define NCF_EINVAL (-1)
 #define NCF_EHIP (-2)
@@ -394,6 +394,16 @@ int ncf_user_dp_step_split(const ncf_shape_t* shape, ncf_model_t* model, ncf_opt
                            const int32_t* next_users, const int32_t* next_items, int64_t n_next, float* shared,
                            float* slice_grad, int32_t item_world, int32_t item_rank, int32_t include_dense_reg,
                            void* comm, double* stats, void* ws, size_t ws_bytes, void* stream);
+/* Exchange timing of the one-call steps (ABI 10; the bench's multi-GPU diagnostic).  every > 0:
+ * from the next call on, every every-th ncf_user_dp_step[_split] records timing events — on the
+ * side stream around its reduce-scatter + all-reduce group (or its all-reduce) and around its
+ * all-gather, on the compute stream around its two join waits; every = 0 stops.
+ * ncf_comm_timing_read waits for the recorded events and returns, summed over the sampled steps
+ * since the last read, out[0] = ms of the reduce-scatter + all-reduce on the side stream, out[1]
+ * = ms of the all-gather, out[2] = ms the compute stream waited for the former (exposed), out[3] =
+ * ms it waited for the all-gather; *steps = the sampled steps (then cleared). */
+int ncf_comm_timing(void* comm, int32_t every);
+int ncf_comm_timing_read(void* comm, double* out4, int64_t* steps);
 
 /* Row-sharded data parallelism (no reference counterpart — the
  * reference trains on one CPU).  Rank r of `world` (1..16) owns the table rows g

@@ -13,18 +13,53 @@
 #include <rccl/rccl.h>
 
 #include <cstring>
+#include <vector>
 
 #include "movierec_ncf.h"
 #include "ncf_internal.h"
 
 namespace {
 
+// timing events of one sampled step: side stream c0..c1 (reduce-scatter + all-reduce), a0..a1
+// (all-gather); compute stream j0..j1 (its wait for the former), g0..g1 (for the all-gather)
+struct StepEvents {
+    hipEvent_t e[8] = {};
+    bool gather = false;
+};
+enum { kC0, kC1, kA0, kA1, kJ0, kJ1, kG0, kG1 };
+
 struct Comm {
     ncclComm_t nccl = nullptr;
     hipStream_t side = nullptr;   // the collective's stream
     hipEvent_t fork = nullptr, join = nullptr;
     int world = 0, rank = 0, device = 0;
+    int every = 0;                // ncf_comm_timing
+    int64_t calls = 0;
+    std::vector<StepEvents> sets; // recorded since the last read (events kept for reuse)
+    size_t used = 0;
+    StepEvents* cur = nullptr;    // the current call's, when sampled
 };
+
+int hip_ok(hipError_t e, const char* what);
+
+// the current call's event set (nullptr: not sampled)
+StepEvents* timing_begin(Comm* c) {
+    c->cur = nullptr;
+    if (c->every <= 0 || (c->calls++ % c->every) != 0 || c->used >= 4096) return nullptr;
+    if (c->used == c->sets.size()) {
+        StepEvents se;
+        for (hipEvent_t& e : se.e)
+            if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        c->sets.push_back(se);
+    }
+    c->cur = &c->sets[c->used++];
+    c->cur->gather = false;
+    return c->cur;
+}
+
+inline int mark(Comm* c, int which, hipStream_t st) {
+    return c->cur ? hip_ok(hipEventRecord(c->cur->e[which], st), "timing event") : 0;
+}
 
 int comm_fail(int code, const char* what, const char* detail) { return ncf::set_error(code, "%s: %s", what, detail); }
 
@@ -81,9 +116,46 @@ int ncf_comm_destroy(void* comm) {
     int r = c->nccl ? nccl_check(ncclCommDestroy(c->nccl), "ncclCommDestroy") : 0;
     if (c->fork) hipEventDestroy(c->fork);
     if (c->join) hipEventDestroy(c->join);
+    for (StepEvents& se : c->sets)
+        for (hipEvent_t e : se.e)
+            if (e) hipEventDestroy(e);
     if (c->side) hipStreamDestroy(c->side);
     delete c;
     return r;
+}
+
+int ncf_comm_timing(void* comm, int32_t every) {
+    Comm* c = static_cast<Comm*>(comm);
+    if (!c || every < 0) return comm_fail(NCF_EINVAL, "ncf_comm_timing", "NULL communicator or every < 0");
+    c->every = every;
+    c->calls = 0;
+    return 0;
+}
+
+int ncf_comm_timing_read(void* comm, double* out4, int64_t* steps) {
+    Comm* c = static_cast<Comm*>(comm);
+    if (!c || !out4 || !steps) return comm_fail(NCF_EINVAL, "ncf_comm_timing_read", "NULL argument");
+    double acc[4] = {0, 0, 0, 0};
+    auto span = [&](const StepEvents& se, int a, int b, double* into) -> int {
+        float ms = 0.f;
+        if (int r = hip_ok(hipEventSynchronize(se.e[b]), "timing sync")) return r;
+        if (int r = hip_ok(hipEventElapsedTime(&ms, se.e[a], se.e[b]), "timing read")) return r;
+        *into += ms;
+        return 0;
+    };
+    for (size_t i = 0; i < c->used; ++i) {
+        const StepEvents& se = c->sets[i];
+        if (int r = span(se, kC0, kC1, &acc[0])) return r;
+        if (int r = span(se, kJ0, kJ1, &acc[2])) return r;
+        if (se.gather) {
+            if (int r = span(se, kA0, kA1, &acc[1])) return r;
+            if (int r = span(se, kG0, kG1, &acc[3])) return r;
+        }
+    }
+    for (int j = 0; j < 4; ++j) out4[j] = acc[j];
+    *steps = (int64_t)c->used;
+    c->used = 0;
+    return 0;
 }
 
 // in-place sum over the ranks on the communicator's stream, ordered after everything enqueued on
@@ -124,11 +196,14 @@ int ncf_user_dp_step(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* opti
         return r;   // the message is set
     const int64_t count = (R - U) * W + P + NCF_NUM_SUMMARY;
     hipStream_t side = c->side;
+    timing_begin(c);
     if (int r = hip_ok(hipEventRecord(c->fork, st), "fork")) return r;
     if (int r = hip_ok(hipStreamWaitEvent(side, c->fork, 0), "fork wait")) return r;
+    if (int r = mark(c, kC0, side)) return r;
     if (int r = nccl_check(ncclAllReduce(shared, shared, (size_t)count, ncclFloat32, ncclSum, c->nccl, side),
                            "ncclAllReduce"))
         return r;
+    if (int r = mark(c, kC1, side)) return r;
     if (int r = hip_ok(hipEventRecord(c->join, side), "join")) return r;
     // meanwhile on the compute stream: the own users' update (+ the next batch counted and its own
     // rows caught up ahead), then the next batch's index finished — none of it reads an item row,
@@ -138,7 +213,9 @@ int ncf_user_dp_step(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* opti
     if (next_users)
         if (int r = ncf::build_next_index(*s, *h, model, optim, next_users, next_items, n_next, ws, ws_bytes, st))
             return r;
+    if (int r = mark(c, kJ0, st)) return r;
     if (int r = hip_ok(hipStreamWaitEvent(st, c->join, 0), "join wait")) return r;
+    if (int r = mark(c, kJ1, st)) return r;
     // the replicated item rows (their moments indexed by table row) and the dense layers
     ncf_optim_t items_opt = *optim;
     if (items_opt.emb_m) items_opt.emb_m += U * W;
@@ -188,8 +265,10 @@ int ncf_user_dp_step_split(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t
                                                nullptr, include_dense_reg, ws, ws_bytes, stream))
         return r;
     hipStream_t side = c->side;
+    timing_begin(c);
     if (int r = hip_ok(hipEventRecord(c->fork, st), "fork")) return r;
     if (int r = hip_ok(hipStreamWaitEvent(side, c->fork, 0), "fork wait")) return r;
+    if (int r = mark(c, kC0, side)) return r;
     if (exchange) {
         if (int r = nccl_check(ncclGroupStart(), "ncclGroupStart")) return r;
         if (int r = nccl_check(ncclReduceScatter(item_grad, slice_grad, (size_t)(Ic * W), ncclFloat32, ncclSum,
@@ -206,12 +285,15 @@ int ncf_user_dp_step_split(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t
                                              c->nccl, side), "ncclAllReduce"))
             return r;
     }
+    if (int r = mark(c, kC1, side)) return r;
     if (int r = hip_ok(hipEventRecord(c->join, side), "join")) return r;
     if (int r = ncf_update_rows_lazy(s, model, optim, h, n, next_users, next_items, n_next, ws, ws_bytes, stream))
         return r;
     // (the next batch's index is built after the item rows' Adam, beside the all-gather below: this
     // window already holds the own-user update; the all-gather's holds nothing else)
+    if (int r = mark(c, kJ0, st)) return r;
     if (int r = hip_ok(hipStreamWaitEvent(st, c->join, 0), "join wait")) return r;
+    if (int r = mark(c, kJ1, st)) return r;
     // this rank's item slice (its moments indexed by table row) and the dense layers
     const int64_t r0 = item_rank * Ic;
     const int64_t cnt = r0 >= I ? 0 : (I - r0 < Ic ? I - r0 : Ic);
@@ -233,15 +315,20 @@ int ncf_user_dp_step_split(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t
     // compute stream waits for the gather before the next forward pass can read an item row
     if (int r = hip_ok(hipEventRecord(c->fork, st), "fork")) return r;
     if (int r = hip_ok(hipStreamWaitEvent(side, c->fork, 0), "fork wait")) return r;
+    if (c->cur) c->cur->gather = true;
+    if (int r = mark(c, kA0, side)) return r;
     float* items0 = model->emb + U * W;
     if (int r = nccl_check(ncclAllGather(items0 + r0 * W, items0, (size_t)(Ic * W), ncclFloat32, c->nccl, side),
                            "ncclAllGather"))
         return r;
+    if (int r = mark(c, kA1, side)) return r;
     if (int r = hip_ok(hipEventRecord(c->join, side), "join")) return r;
     if (next_users)  // (after the step's bump)
         if (int r = ncf::build_next_index(*s, *h, model, optim, next_users, next_items, n_next, ws, ws_bytes, st, 0))
             return r;
-    return hip_ok(hipStreamWaitEvent(st, c->join, 0), "join wait");
+    if (int r = mark(c, kG0, st)) return r;
+    if (int r = hip_ok(hipStreamWaitEvent(st, c->join, 0), "join wait")) return r;
+    return mark(c, kG1, st);
 }
 
 }  // extern "C"

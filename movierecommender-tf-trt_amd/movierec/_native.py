@@ -104,6 +104,8 @@ _SIGNATURES = {
     "ncf_comm_init": (ctypes.c_int, [_i32, _i32, _vp, ctypes.c_size_t, _P(_vp)]),
     "ncf_comm_destroy": (ctypes.c_int, [_vp]),
     "ncf_comm_allreduce": (ctypes.c_int, [_vp, _vp, _i64, _vp]),
+    "ncf_comm_timing": (ctypes.c_int, [_vp, _i32]),
+    "ncf_comm_timing_read": (ctypes.c_int, [_vp, _vp, _P(_i64)]),
     "ncf_user_dp_step": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _vp, _vp, _vp, _i64,
                                         _vp, _vp, _i64, _vp, _i32, _vp, _vp, _vp, ctypes.c_size_t, _vp]),
     "ncf_user_dp_step_split": (ctypes.c_int, [_P(NcfShape), _P(NcfModel), _P(NcfOptim), _P(NcfHyper), _vp, _vp, _vp,
@@ -172,7 +174,7 @@ def profile_read(kernel):
     return ms.value, n.value
 
 _lib = None
-ABI_VERSION = 9   # include/movierec_ncf.h ncf_abi_version()
+ABI_VERSION = 10  # include/movierec_ncf.h ncf_abi_version()
 
 
 def lib():

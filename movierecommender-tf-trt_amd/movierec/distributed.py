@@ -539,6 +539,72 @@ class UserPartitionedDataParallel(object):
         self.num_local_users = U
         # the L2 loss of the replicated item rows is reported by rank 0 only
         self.reg_rows = (0, R) if self.rank == 0 else (0, U)
+        self._t_every, self._t_calls, self._t_sets = 0, 0, []
+
+    # ---- exchange timing (bench.py's in-step diagnostic at N > 1) ----
+    def exchange_timing(self, every):
+        """Every ``every``-th step from now on (0: none) records how long its collectives run and
+        how long the compute stream waits for them: HIP events on the library communicator's side
+        stream and around its join waits (one-call step, ``ncf_comm_timing``), or CUDA events on the
+        compute stream around the collective calls and waits (call-by-call step)."""
+        self._t_every, self._t_calls, self._t_sets = int(every), 0, []
+        if self.comm is not None:
+            from . import _native as N
+            N.check(N.lib().ncf_comm_timing(self.comm.handle, int(every)))
+
+    def read_exchange_timing(self):
+        """Mean ms per sampled step since ``exchange_timing``: ``rs_ar_ms`` / ``ag_ms`` (the
+        reduce-scatter + all-reduce group, or the all-reduce, and the all-gather on the
+        communicator's stream; None when not observable — torch's collectives run on streams of
+        their own), ``rs_ar_exposed_ms`` / ``ag_exposed_ms`` (the compute stream's waits), the
+        sampled ``steps`` and the ``path``."""
+        if self.comm is not None:
+            import ctypes
+            from . import _native as N
+            out = (ctypes.c_double * 4)()
+            k = ctypes.c_int64()
+            N.check(N.lib().ncf_comm_timing_read(self.comm.handle, out, ctypes.byref(k)))
+            k = int(k.value)
+            mean = [v / k if k else None for v in out]
+            return {"steps": k, "rs_ar_ms": mean[0], "ag_ms": mean[1] if self.split and self.world > 1 else None,
+                    "rs_ar_exposed_ms": mean[2], "ag_exposed_ms": mean[3] if self.split and self.world > 1 else None,
+                    "path": "one-call step (ncf_user_dp_step%s, library RCCL communicator)" % ("_split" if self.split else "")}
+        torch.cuda.synchronize()
+        k = len(self._t_sets)
+        acc = [0.0, 0.0]
+        for ev in self._t_sets:
+            for j, pair in enumerate(ev):
+                for a, b in pair:
+                    acc[j] += a.elapsed_time(b)
+        self._t_sets = []
+        gather = self.split and self.world > 1
+        return {"steps": k, "rs_ar_ms": None, "ag_ms": None,
+                "rs_ar_exposed_ms": acc[0] / k if k else None, "ag_exposed_ms": acc[1] / k if k and gather else None,
+                "path": "call by call (torch.distributed %s collectives)" % dist.get_backend(self.group)}
+
+    def _t_begin(self):
+        """The call-by-call step's event lists ([waits for the reduce-scatter/all-reduce], [for the
+        all-gather]) when this step is sampled, else None."""
+        if self._t_every <= 0:
+            return None
+        self._t_calls += 1
+        if (self._t_calls - 1) % self._t_every:
+            return None
+        ev = ([], [])
+        self._t_sets.append(ev)
+        return ev
+
+    @staticmethod
+    def _t_span(ev, j, fn):
+        """fn() bracketed by CUDA events on the current stream when ev is set."""
+        if ev is None:
+            return fn()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        r = fn()
+        b.record()
+        ev[j].append((a, b))
+        return r
 
     def broadcast_parameters(self, src=0):
         """Make the replicated part (item rows, dense layers) equal to rank ``src``'s."""
@@ -565,8 +631,9 @@ class UserPartitionedDataParallel(object):
             return
         eng.forward_backward_part(users, items, labels, group=group, k=k, inv_batch=inv, shared_row_begin=U,
                                   grads=self.grads, reg_rows=self.reg_rows, include_dense_reg=self.rank == 0)
+        ev = self._t_begin()
         if self.split:
-            return self._split_tail(U, R, inv, group, next_batch)
+            return self._split_tail(U, R, inv, group, next_batch, ev)
         work = _all_reduce_async(self.shared, self.group)
         if getattr(eng, "lazy_rows", None) == U and eng.row_step is not None:
             # deferred decay of the own users: the touched ones' update, and the next batch's index
@@ -577,10 +644,10 @@ class UserPartitionedDataParallel(object):
             if next_batch is not None and hasattr(eng, "build_index"):
                 eng.build_index(*next_batch, group)  # so does the next step's index
         if work is not None:
-            work.wait()
+            self._t_span(ev, 0, work.wait)
         eng.apply_update(self.grads, inv, rows=(U, R - U), moments_by_row=True)
 
-    def _split_tail(self, U, R, inv, group, next_batch):
+    def _split_tail(self, U, R, inv, group, next_batch, ev=None):
         """The split-items step after the forward/backward, call by call (ncf_user_dp_step_split's
         sequence): reduce-scatter of the item gradient + all-reduce of the dense part, the own
         users' update and the next index meanwhile, the item slice's Adam, the all-gather."""
@@ -591,7 +658,7 @@ class UserPartitionedDataParallel(object):
         dense = self.flat[eg.numel():]
         exchange = self.world > 1
         if exchange:
-            _reduce_scatter(self.slice_grad, eg, self.group)
+            self._t_span(ev, 0, lambda: _reduce_scatter(self.slice_grad, eg, self.group))
             work = _all_reduce_async(dense, self.group)
             slice_grad = self.slice_grad
         else:
@@ -604,11 +671,11 @@ class UserPartitionedDataParallel(object):
             if next_batch is not None and hasattr(eng, "build_index"):
                 eng.build_index(*next_batch, group)
         if work is not None:
-            work.wait()
+            self._t_span(ev, 0, work.wait)
         eng.apply_update((slice_grad, mg, sm), inv, rows=(U + (r0 if cnt else R - U), cnt), moments_by_row=True)
         if exchange:
             items = eng.emb[U:U + self.item_world * self.Ic]
-            _all_gather_inplace(items, self.Ic, self.group)
+            self._t_span(ev, 1, lambda: _all_gather_inplace(items, self.Ic, self.group))
 
     def keras_weights(self):
         """Full Keras-layout weights (collective: every rank must call it): user rows gathered

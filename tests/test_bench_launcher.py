@@ -7,6 +7,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -39,3 +41,23 @@ def test_single_rank_selftest():
     r = _run(["--selftest-launch", "--steps", "2"])
     assert r.returncode == 0, r.stderr[-2000:]
     assert json.loads(r.stdout.strip())["n_gpus"] == 1
+
+
+@pytest.mark.gpu
+def test_gloo_two_ranks_report_in_step_exchange():
+    """`bench.py --gpus 2 --dist-backend gloo` (two ranks on one GPU, the multi-rank logic's
+    rehearsal): the line carries the exchange fields as the step ran them — the compute stream's
+    waits for the reduce-scatter/all-reduce and for the all-gather, max and min over the ranks —
+    and names the path (call by call under gloo)."""
+    r = _run(["--gpus", "2", "--dist-backend", "gloo", "--dp", "user", "--batch", "8192", "--steps", "12",
+              "--warmup", "2", "--no-cpu-baseline"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.strip()][-1])
+    assert d["n_gpus"] == 2
+    x = d["exchange"]
+    assert x["ranks"] == 2 and x["backend"] == "gloo" and x["native_step"] is False
+    s = x["in_step"]
+    assert s["path"].startswith("call by call") and s["sampled_steps_per_rank"] >= 2
+    for k in ("rs_ar_exposed_ms", "ag_exposed_ms"):
+        assert s[k]["max"] >= s[k]["min"] >= 0.0, (k, s[k])
+    assert s["rs_ar_ms"] is None and s["ag_ms"] is None   # torch's collectives: not observable

@@ -26,7 +26,7 @@ def test_library_exports_every_symbol():
     L = N.lib()
     for name in _declared():
         assert hasattr(L, name), name
-    assert L.ncf_abi_version() == N.ABI_VERSION == 9
+    assert L.ncf_abi_version() == N.ABI_VERSION == 10
 
 
 def _shape(nu, ni, layers, g):
