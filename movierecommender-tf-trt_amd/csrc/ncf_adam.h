@@ -1,6 +1,5 @@
 // Keras-v1 Adam arithmetic shared by every embedding-table path (ncf_update.hip's sweeps, updates,
-// replays and flush; the stale-row replay of the in-kernel index fill in ncf_update.hip and
-// ncf_wave.hip): one definition, so every path rounds identically.
+// replays and flush): one definition, so every path rounds identically.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -135,16 +134,5 @@ __device__ inline void claim_replay(float* __restrict__ embf, float* __restrict_
     }
 }
 
-
-// the whole wave, after a pass of the fill's contributions (fill_wave's on_stale): the rows whose
-// contributions found no slot because the counted set missed them altogether (a key it counted
-// is in the touched list: the update takes it) are replayed to *step, before the forward pass
-// reads them
-__device__ inline void fill_stale_replay(const FillArgs& f, bool stale, int key) {
-    const FillReplay& rp = f.rp;
-    if (!rp.row_step || !__ballot(stale)) return;
-    const int k = stale && key < rp.lazy_rows && fill_count0(f, key) == 0 ? key : -1;
-    claim_replay(rp.emb, rp.m, rp.v, rp.W, rp.row_step, k, *rp.step, rp.lr, rp.b1, rp.b2, rp.eps);
-}
 
 }  // namespace ncf

@@ -255,6 +255,7 @@ WsLayout make_layout(const ncf_shape_t& s, int64_t B, int world) {
     L.heavy_n = take(4);
     L.err = take(4);
     L.ifold = take(4);
+    L.stale_step = take(4);
     const int64_t S = L.shard_rows;
     if (world > 0) {
         L.ocnt = take((size_t)(S + 1) * 4);
@@ -698,16 +699,19 @@ static int check_train_args(const ncf_shape_t* s, const ncf_model_t* model, cons
 // 1: the wave kernel's weight-gradient waves fill the index; 2: a fill launch of its own
 // (k_fill_ahead) before the forward/backward; either way the touched-row update orders the lists.
 // 0: round 4's fill and list-sort launches (timing comparisons)
-#define NCF_FILL_IN_KERNEL 2
+#define NCF_FILL_IN_KERNEL 1
 #endif
-// The step's index from the wave kernel's weight-gradient waves (FillArgs): a batch counted and
-// scanned ahead by the previous step (index_ready 2, deferred-decay Adam), the split wave kernel,
-// a key space the fill's prefix table holds, one stream.  The lists stay unsorted (the touched-row
-// update orders them), and the counted rows were caught up by the previous step's update launch.
-// (A batch whose ids changed after they were counted is flagged as before, NCF_WSERR_STALE_COUNT;
-// the rows the counted set missed are then read by this forward pass at their last step — there
-// is no launch before it to replay them — and settled when next touched or flushed.)
-// 0: the index launches; 1: the wave kernel fills; 2: k_fill_ahead fills
+// The step's index built inside a launch that runs anyway (FillArgs): a batch counted and scanned
+// ahead by the previous step (index_ready 2, deferred-decay Adam), a key space the fill's prefix
+// table holds, one stream — by the split wave kernel's weight-gradient waves where that kernel
+// runs (1), else by a fill launch ahead of the forward/backward (2).  The lists stay unsorted (the
+// touched-row update orders them), and the counted rows were caught up by the previous step's
+// update launch.  A batch whose ids changed after they were counted (a write that bypassed torch's
+// version counter: NCF_WSERR_STALE_COUNT) is DROPPED: the forward pass may have read rows the
+// counted set missed at their deferred step, so the update and stats launches apply nothing of
+// the step (ws stale_step, fill_wave) — table, moments, dense layers, stats and step counter stay
+// as they were, a consistent deferred-decay state — and check_errors raises.
+// Returns 0: the index launches; 1: the wave kernel fills; 2: k_fill_ahead fills
 static int fill_in_kernel(const ncf_shape_t& s, const ncf::WsLayout& L, const ncf_hyper_t* h, int64_t n) {
     if (!NCF_FILL_IN_KERNEL || h->index_ready != 2 || h->optimizer != NCF_OPT_ADAM || side_stream_mode() != 0 ||
         L.world != 0 || L.nscan > ncf::kMaxFillScan || ncf::unsorted_heavy_c(s) < ncf::kHeavyMin)
@@ -718,11 +722,8 @@ static int fill_in_kernel(const ncf_shape_t& s, const ncf::WsLayout& L, const nc
     return 2;
 }
 
-static ncf::FillArgs fill_args(const ncf_shape_t& s, const ncf::WsLayout& L, void* ws, ncf_model_t* model,
-                               ncf_optim_t* optim, const ncf_hyper_t* h) {
+static ncf::FillArgs fill_args(const ncf_shape_t& s, const ncf::WsLayout& L, void* ws) {
     using ncf::at;
-    const ncf::FillReplay rp{model->emb, optim->emb_m, optim->emb_v, s.row_width, optim->row_step, optim->step,
-                             h->lr, h->beta_1, h->beta_2, h->epsilon, ncf::lazy_bound(s, *h)};
     return ncf::FillArgs{at<int32_t>(ws, L.cnt), at<const int32_t>(ws, L.offs_local), at<const int32_t>(ws, L.tot),
                          at<const int32_t>(ws, L.uloc), at<const int32_t>(ws, L.utot), L.nscan, L.keys + 1,
                          at<int32_t>(ws, L.offs), at<int32_t>(ws, L.list), at<int32_t>(ws, L.touched),
@@ -730,7 +731,7 @@ static ncf::FillArgs fill_args(const ncf_shape_t& s, const ncf::WsLayout& L, voi
                          at<int32_t>(ws, L.heavy_n), ncf::unsorted_heavy_c(s), at<int32_t>(ws, L.err),
                          at<int32_t>(ws, L.ifold), s.num_users, s.num_items, L.list_cap,
                          L.keys < 2 * L.max_batch ? L.keys : 2 * L.max_batch, 2 * L.max_batch / ncf::kHeavyMin + 1,
-                         rp};
+                         at<int32_t>(ws, L.stale_step)};
 }
 
 static int train_step_impl(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* h,
@@ -759,7 +760,7 @@ static int train_step_impl(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t
     fb.defer_metrics = lazy && side_stream_mode() == 0;
     const int fmode = lazy ? fill_in_kernel(*s, L, h, n) : 0;
     const bool kfill = fmode != 0;
-    const ncf::FillArgs fa = kfill ? fill_args(*s, L, ws, model, optim, h) : ncf::FillArgs{};
+    const ncf::FillArgs fa = kfill ? fill_args(*s, L, ws) : ncf::FillArgs{};
     if (fmode == 2) {
         prof_begin(NCF_K_INDEX, st);
         hipError_t e = ncf::launch_fill_ahead(fa, users, items, n, index_fold(*s, h), st);
@@ -824,9 +825,12 @@ static int train_step_impl(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t
     if (e != hipSuccess) return hip_check(e, "side-stream join");
     const int nreg_emb = h->l2[0] != 0.0f ? ncf::kUpdateGrid : 0;
     // counting ahead: the stats launch also scans the next batch's counts
+    // (an in-kernel fill's step may have been dropped: the stats launch then adds nothing, bumps
+    // nothing and clears the word)
     e = ncf::launch_stats(L, ws, summary, nreg_emb, nreg_mlp, h->inv_batch, stats, optim->step, true, st,
                           lazy && next_users != nullptr, s->num_rows,
-                          two_level ? ncf::SummaryFirst{fb.nbce, fb.nmet, fb.n_groups} : ncf::SummaryFirst{-1, 0, 0.f});
+                          two_level ? ncf::SummaryFirst{fb.nbce, fb.nmet, fb.n_groups} : ncf::SummaryFirst{-1, 0, 0.f},
+                          kfill ? ncf::at<int32_t>(ws, L.stale_step) : nullptr);
     return hip_check(e, "stats");
 }
 

@@ -71,6 +71,7 @@ struct WsLayout {
     size_t uloc;      // int32[K+1]  per-2048-key local exclusive scan of (cnt > 0)
     size_t utot;      // int32[nscan]
     size_t ifold;     // int32       user-row folding of the last index build (persistent)
+    size_t stale_step;// int32      persistent: nonzero while the current step is dropped (fill_wave)
     size_t cid_u;     // int32[B]    compact (unique-row) id of each sample's user row
     size_t cid_i;     // int32[B]    compact id of each sample's item row
     size_t uoffs;     // int32[2B+1] compact row -> first list slot
@@ -382,16 +383,6 @@ __device__ inline void sort_rows_body(const int32_t* __restrict__ offs, int64_t 
 // entries across the lanes of their row group, longer ones — listed in `heavy` — block-wide).  A
 // run that takes a counter below zero gives the excess back (k_fill_big's rule): a residue can
 // only sit at a counted key, i.e. in the touched list, where the update checks it.
-// The rows the in-kernel fill replays when the counted set turns out stale (ncf_adam.h
-// fill_stale_replay): the table's state and the Adam hyper-parameters (row_step nullptr: none)
-struct FillReplay {
-    float *emb, *m, *v;
-    int W;
-    int32_t* row_step;
-    const int32_t* step;
-    float lr, b1, b2, eps;
-    int64_t lazy_rows;
-};
 struct FillArgs {
     int32_t* cnt;             // per-key cursors: the counts the scan ahead copied (ws cnt)
     const int32_t* local;     // per-scan-block exclusive offsets (ws offs_local)
@@ -412,7 +403,7 @@ struct FillArgs {
     int32_t* ifold;
     int32_t U, I;             // user u -> key u, item v -> key U + v
     int64_t list_cap, touched_cap, heavy_cap;  // region sizes (debug bound checks)
-    FillReplay rp;
+    int32_t* stale_step;      // set when a contribution finds no slot: the step is dropped (below)
 };
 #if NCF_DEBUG_BOUNDS == 1
 #define NCF_BOUND(cond, ...)          \
@@ -432,21 +423,19 @@ struct FillArgs {
 constexpr int kFillRowsPerLane = 4;     // fill_wave's RU: keys per lane and pass of the rows part
 constexpr int kFillContribPerLane = 2;  // its CU: contributions per lane and pass
 
-// the count key had in the counted set (0: the counted set missed it — not in the touched list)
-__device__ inline int fill_count0(const FillArgs& f, int key) {
-    const int nx = (key + 1) % kScanBlock != 0 ? f.local[key + 1] : f.tot[key / kScanBlock];
-    return nx - f.local[key];
-}
-
 // Wave gw of nw: its share of the fill of batch (users, items, n) folded by `fold`.  The
 // exclusive prefixes of the scan-block totals stay in registers (lane l: blocks l and l + 64) and
-// are read with lane shuffles, so every loop below is wave-uniform.  on_stale(stale, key): called by
-// the whole wave after each pass of contributions, stale = this lane's contribution found no slot
-// (the counted set differs from the ids passed).  PART: 1 the rows, 2 the contributions, 3 both
-template <int PART = 3, class OnStale>
+// are read with lane shuffles, so every loop below is wave-uniform.  PART: 1 the rows, 2 the
+// contributions, 3 both.
+// A contribution that finds no slot means the ids changed after they were counted (a write that
+// bypassed torch's version counter): the forward pass of this very launch or the next may have
+// read rows the counted set missed, at their deferred step.  Such a step is DROPPED — f.stale_step
+// tells the touched-row update and the stats launch to apply nothing of it (the table, moments,
+// dense layers, stats and step counter stay as they were: a consistent deferred-decay state) —
+// and reported (NCF_WSERR_STALE_COUNT, RuntimeError from check_errors).
+template <int PART = 3>
 __device__ inline void fill_wave(const FillArgs& f, const int32_t* __restrict__ users,
-                                 const int32_t* __restrict__ items, int64_t n, int fold, int gw, int nw,
-                                 OnStale on_stale) {
+                                 const int32_t* __restrict__ items, int64_t n, int fold, int gw, int nw) {
     const int lane = threadIdx.x & 63;
     int p0, p1, q0, q1;  // pre[lane], pre[lane + 64], upre[lane], upre[lane + 64]
     {
@@ -581,9 +570,10 @@ __device__ inline void fill_wave(const FillArgs& f, const int32_t* __restrict__ 
                           (long long)c, key, (long long)li, (long long)f.list_cap)
                 f.list[li] = (int)c;
             }
-            const bool stale = ok && slot < 0;
-            if (stale) atomicOr(f.err, kErrStaleCount);
-            on_stale(stale, key);
+            if (ok && slot < 0) {
+                atomicOr(f.err, kErrStaleCount);
+                atomicOr(f.stale_step, 1);
+            }
         }
     }
 }
@@ -709,8 +699,7 @@ hipError_t launch_fb_wave(const ncf_shape_t& s, const WsLayout& L, void* ws, con
 // the split form runs for this shape (its weight-gradient waves can build the index: FillArgs)
 bool wave_fill_supported(const ncf_shape_t& s);
 // the in-kernel fill as a launch of its own (ncf_index.hip)
-// (ncf_update.hip) the fill, and — the counted set stale — the replay of the rows it missed to
-// *step (the stale-count gate's rule, before the forward pass reads them; f.rp)
+// (ncf_update.hip) the fill as a launch of its own
 hipError_t launch_fill_ahead(const FillArgs& f, const int32_t* users, const int32_t* items, int64_t n, int fold,
                              hipStream_t st);
 hipError_t launch_fb_unit(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, const float* mlp,
@@ -856,9 +845,12 @@ struct SummaryFirst {
     int nbce, nmet;
     float n_groups;
 };
+// drop (in-kernel fill steps: ws stale_step): nonzero — the step is dropped: no stats, no bump; the
+// launch clears it
 hipError_t launch_stats(const WsLayout& L, void* ws, const float* summary, int nreg_emb, int nreg_mlp,
                         float inv_batch, double* stats, int32_t* step, bool bump_step, hipStream_t st,
-                        bool scan_ahead = false, int64_t scan_keys = 0, SummaryFirst sf = SummaryFirst{-1, 0, 0.f});
+                        bool scan_ahead = false, int64_t scan_keys = 0, SummaryFirst sf = SummaryFirst{-1, 0, 0.f},
+                        int32_t* drop = nullptr);
 
 // on-device negative sampling (ncf_sample.hip)
 hipError_t launch_sample_batch(const int32_t* pos_users, const int32_t* pos_items, const int32_t* excl_ptr,

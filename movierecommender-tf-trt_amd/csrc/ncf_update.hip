@@ -186,6 +186,9 @@ constexpr int kRep = NCF_AHEAD_REP;
 #ifndef NCF_TOUCHED_MIN_BLOCKS
 #define NCF_TOUCHED_MIN_BLOCKS 7
 #endif
+#ifndef NCF_TOUCHED_MIN_BLOCKS_UNSORTED
+#define NCF_TOUCHED_MIN_BLOCKS_UNSORTED NCF_TOUCHED_MIN_BLOCKS   // the unsorted-list variant (experiments)
+#endif
 
 // Deferred exact decay ("lazy" dense Adam, L2 off).  Keras' dense Adam (F5) moves EVERY row
 // every step; a row no sample touches gets g = 0, so its update is a pure function of
@@ -700,6 +703,8 @@ struct SortRows {
     int32_t* err;
     int32_t* slist;            // heavy rows' lists, sorted (indexed like the list)
     int mcap;                  // contribution ids are below this (2 * max batch): a stale list slot is clamped
+    const int32_t* drop;       // ws stale_step: nonzero — the step is dropped (fill_wave): only the next
+                               // batch's count and catch-up ahead run, the latter to *step
 };
 constexpr int kHeavyChunk = 1024;  // heavy-row list entries staged in LDS per round
 
@@ -739,7 +744,7 @@ __device__ __forceinline__ void row_adam(float4* __restrict__ emb, float4* __res
 }
 
 template <bool UNSORTED>
-__global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_touched(float4* __restrict__ emb, float4* __restrict__ m4,
+__global__ __launch_bounds__(kBlock, UNSORTED ? NCF_TOUCHED_MIN_BLOCKS_UNSORTED : NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_touched(float4* __restrict__ emb, float4* __restrict__ m4,
                                                              float4* __restrict__ v4, uint32_t w4,
                                                              const int32_t* __restrict__ list,
                                                              const int2* __restrict__ toc,
@@ -758,7 +763,10 @@ __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_tou
     // (two_level: the dense-layer blocks come first — each waits one round of slab loads, under
     // everything else)
     int b = (int)blockIdx.x;
+    // a dropped step (stale counted set, unsorted lists only): nothing of it is applied
+    const bool dropped = UNSORTED && so.drop && *so.drop != 0;
     if (UNSORTED && b < so.nheavy) {
+        if (dropped) return;
         // heavy rows (lists longer than so.hc, unsorted): one per block and pass
         __shared__ int chunk[kHeavyChunk];
         const int t = *step + 1;
@@ -823,17 +831,19 @@ __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_tou
     // the step's hr/dcg partials (k_group_metrics' work, groups <= 8) in the first blocks: the
     // probabilities are final once the forward/backward launch before this one is done
     if (b < mm.nblocks) {
+        if (dropped) return;
         group_metrics_body(mm.probs, mm.labels, mm.ng, mm.group, mm.k, nullptr, nullptr, mm.part_hit, mm.part_dcg, b);
         return;
     }
     b -= mm.nblocks;
     if (mt.two_level) {
         if (b < mt.nblocks) {
-            mlp_slabs_adam(mt, b);
+            if (!dropped) mlp_slabs_adam(mt, b);
             return;
         }
         b -= mt.nblocks;
     } else if (b >= ca.nupd + ca.ncount) {
+        if (dropped) return;
         mlp_update_body<NCF_OPT_ADAM>(mt.p, mt.m, mt.v, mt.P, mt.slabs, mt.nslab, nullptr, nullptr, 1, 0, mt.step,
                                       mt.lr, mt.b1, mt.b2, mt.eps, mt.l2t, mt.part_reg,
                                       b - ca.nupd - ca.ncount);
@@ -849,8 +859,9 @@ __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_tou
         // arithmetic: bitwise) under the touched-row update, instead of in a launch of its own
         // before the next forward pass.  One lane claims a row (CAS on row_step: a user's
         // repeated contributions replay it once) and leaves p, m, v and row_step at step t.
+        // (A dropped step applies nothing: the next batch's rows are caught up to *step instead.)
         __shared__ float lut[kLrLut];
-        const int t = *step + 1;
+        const int t = *step + (dropped ? 0 : 1);
         if (ca.replay && threadIdx.x < kLrLut)
             lut[threadIdx.x] = t - (int)threadIdx.x >= 1 ? adam_lr_t(lr, b1, b2, t - threadIdx.x) : 0.f;
         const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -955,6 +966,16 @@ __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_tou
         }
         return;
     }
+    if (dropped) {
+        // nothing of the step is applied; the fill's leftover cursors (entries counted but absent:
+        // every counted key is a touched row) go back to zero for the next index
+        const int64_t nt = *nlist;
+        for (int64_t i = (int64_t)(b - ca.ncount) * kBlock + threadIdx.x; i < nt; i += (int64_t)ca.nupd * kBlock) {
+            const int r = list[i];
+            if (so.cursor[r] != 0) so.cursor[r] = 0;
+        }
+        return;
+    }
     const int ublk = b - ca.ncount;   // this block's index among the update blocks
     const RowLanes rl(w4);
     const int t = *step + 1;
@@ -969,11 +990,23 @@ __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_tou
         const int ql = lane - base;                          // this lane's entry slot
         const int64_t wave = ((int64_t)ublk * kBlock + threadIdx.x) >> 6;
         const int64_t wstride = ((int64_t)ca.nupd * kBlock) >> 6;
-        for (int64_t i0 = wave * rl.rpw; i0 < n; i0 += wstride * rl.rpw) {  // wave-uniform
+        const int64_t istep = wstride * rl.rpw;
+        // software pipeline: the next row's (row, list offset, count) load while this row runs
+        int r = 0;
+        int2 oc = make_int2(0, 0);
+        if (rl.on && wave * rl.rpw + rl.sub < n) {
+            r = list[wave * rl.rpw + rl.sub];
+            oc = toc[wave * rl.rpw + rl.sub];
+        }
+        for (int64_t i0 = wave * rl.rpw; i0 < n; i0 += istep) {  // wave-uniform
             const int64_t i = i0 + rl.sub;
             bool has = rl.on && i < n;
-            int r = has ? list[i] : 0;
-            int2 oc = has ? toc[i] : make_int2(0, 0);
+            int rn = 0;
+            int2 ocn = make_int2(0, 0);
+            if (rl.on && i + istep < n) {
+                rn = list[i + istep];
+                ocn = toc[i + istep];
+            }
 #if NCF_DEBUG_BOUNDS == 1
             if (has && (i >= so.mcap || r < 0 || r >= ca.lazy_rows || oc.x < 0 || oc.y < 0 || oc.x + oc.y > so.mcap)) {
                 if (ql == 0) printf("row %lld of %lld: r %d o %d c %d (skipped)\n", (long long)i, (long long)n, r, oc.x, oc.y);
@@ -1052,6 +1085,8 @@ __global__ __launch_bounds__(kBlock, NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_tou
                 if (w4 <= 64 || q + 64 >= w4) break;
             }
             if (ql == 0 && mine) row_step[r] = t;
+            r = rn;
+            oc = ocn;
         }
         return;
     }
@@ -1238,7 +1273,18 @@ struct SummaryArgs {
     const float* part_dcg;
     int nbce, nmet;
     float n_groups;
+    int32_t* drop;             // (stats launches) nonzero: the step was dropped — no summary, stats or
+                               // bump; cleared here
 };
+
+// whole block 0 of a stats launch: true when the step was dropped (and the word is cleared)
+__device__ inline bool stats_dropped(int32_t* drop) {
+    if (!drop) return false;
+    const int d = *drop;
+    __syncthreads();
+    if (d && threadIdx.x == 0) *drop = 0;
+    return d != 0;
+}
 
 __global__ __launch_bounds__(kBlock) void k_slab_partial(const float* __restrict__ slabs, int P, int nslab, int per,
                                                          float* __restrict__ part, SummaryArgs sa) {
@@ -1385,6 +1431,7 @@ __global__ __launch_bounds__(kBlock) void k_stats(float* __restrict__ summary,
                                                   const float* __restrict__ reg_mlp, int nreg_mlp, float inv_batch,
                                                   double* __restrict__ stats, int32_t* step, int bump, SummaryArgs sa) {
     __shared__ float red[4];
+    if (stats_dropped(sa.drop)) return;
     if (sa.summary) {
         summary_body(sa.part_bce, sa.nbce, sa.part_hit, sa.part_dcg, sa.nmet, sa.n_groups, nullptr, 0, nullptr, 0,
                      summary, red);
@@ -1393,22 +1440,16 @@ __global__ __launch_bounds__(kBlock) void k_stats(float* __restrict__ summary,
     stats_body(summary, reg_emb, nreg_emb, reg_mlp, nreg_mlp, inv_batch, stats, step, bump, red);
 }
 
-// The in-kernel fill's body (FillArgs) as a launch of its own, before the forward/backward: one
-// wave per 64 keys / contributions of the larger of the two.  A stale counted set (ids changed
-// after they were counted, NCF_WSERR_STALE_COUNT): the rows of the ids passed that it missed are
-// not in the touched list, yet the forward pass reads them — the waves that meet them replay them
-// fully to *step here (the stale-count gate's rule, stale_replay_body: the table stays the dense
-// sweep's state; that step's gradient is still wrong, as the flag reports)
-// The rows part and the contributions part run in waves of their own (the first nr waves, the
+// The in-kernel fill's body (FillArgs) as a launch of its own, before the forward/backward (a stale
+// counted set drops the step: fill_wave).  The rows part and the contributions part run in waves of their own (the first nr waves, the
 // rest), so the launch waits on the longer of the two dependency chains instead of their sum.
 __global__ __launch_bounds__(kBlock) void k_fill_ahead(FillArgs f, const int32_t* __restrict__ users,
                                                        const int32_t* __restrict__ items, int64_t n, int fold, int nr) {
     const int gw = (int)blockIdx.x * (kBlock / 64) + (int)(threadIdx.x >> 6);
-    auto replay = [&](bool stale, int key) { fill_stale_replay(f, stale, key); };
     if (gw < nr)
-        fill_wave<1>(f, users, items, n, fold, gw, nr, replay);
+        fill_wave<1>(f, users, items, n, fold, gw, nr);
     else
-        fill_wave<2>(f, users, items, n, fold, gw - nr, (int)gridDim.x * (kBlock / 64) - nr, replay);
+        fill_wave<2>(f, users, items, n, fold, gw - nr, (int)gridDim.x * (kBlock / 64) - nr);
 }
 
 hipError_t launch_fill_ahead(const FillArgs& f, const int32_t* users, const int32_t* items, int64_t n, int fold,
@@ -1442,6 +1483,7 @@ __global__ __launch_bounds__(kBlock) void k_stats_scan(float* __restrict__ summa
                                                        int bump, ScanAhead sc, SummaryArgs sa) {
     if (blockIdx.x == 0) {
         __shared__ float red[4];
+        if (stats_dropped(sa.drop)) return;
         if (sa.summary) {   // the batch summary first (launch_summary's work), then the stats
             summary_body(sa.part_bce, sa.nbce, sa.part_hit, sa.part_dcg, sa.nmet, sa.n_groups, nullptr, 0, nullptr, 0,
                          summary, red);
@@ -1646,7 +1688,7 @@ hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, vo
             // heavy rows are rare (lists longer than a row group's lanes): a few blocks stride over them
             so = SortRows{1, unsorted_heavy_c(s), 32, at<const int32_t>(ws, L.heavy), at<const int32_t>(ws, L.heavy_n),
                           at<int32_t>(ws, L.cnt), at<int32_t>(ws, L.err), at<int32_t>(ws, L.slist),
-                          (int)(2 * L.max_batch)};
+                          (int)(2 * L.max_batch), at<const int32_t>(ws, L.stale_step)};
         }
         launch(unsorted_lists ? k_emb_adam_touched<true> : k_emb_adam_touched<false>, (unsigned)so.nheavy + nupd + ncount + (unsigned)mt.nblocks + (unsigned)mm.nblocks,
                kBlock, 0, st, (float4*)emb, (float4*)m, (float4*)v, w4, at<const int32_t>(ws, L.touched),
@@ -1882,14 +1924,14 @@ hipError_t launch_summary(const WsLayout& L, void* ws, int nbce, int nmet, float
 
 hipError_t launch_stats(const WsLayout& L, void* ws, const float* summary_in, int nreg_emb, int nreg_mlp,
                         float inv_batch, double* stats, int32_t* step, bool bump_step, hipStream_t st,
-                        bool scan_ahead, int64_t scan_keys, SummaryFirst sf) {
+                        bool scan_ahead, int64_t scan_keys, SummaryFirst sf, int32_t* drop) {
     const float* reg = at<float>(ws, L.part_reg);
     // written only by the summary_first block (the workspace's summary); read-only otherwise
     float* summary = const_cast<float*>(summary_in);
-    SummaryArgs sa{nullptr, nullptr, nullptr, nullptr, 0, 0, 0.f};
+    SummaryArgs sa{nullptr, nullptr, nullptr, nullptr, 0, 0, 0.f, drop};
     if (sf.nbce >= 0)
         sa = SummaryArgs{summary, at<float>(ws, L.part_bce), at<float>(ws, L.part_hit), at<float>(ws, L.part_dcg),
-                         sf.nbce, sf.nmet, sf.n_groups};
+                         sf.nbce, sf.nmet, sf.n_groups, drop};
     if (scan_ahead) {
         const int64_t r1 = scan_keys + 1;
         const int nscan = (int)((r1 + kScanBlock - 1) / kScanBlock);

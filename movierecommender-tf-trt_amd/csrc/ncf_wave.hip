@@ -527,8 +527,7 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
     // launch disappear.
     if constexpr (SPLIT) {
         if (dwave && fa.cnt)
-            fill_wave(fa, users, items, n, FOLD, (int)blockIdx.x * 4 + pw, (int)gridDim.x * 4,
-                          [&](bool stale, int key) { fill_stale_replay(fa, stale, key); });
+            fill_wave(fa, users, items, n, FOLD, (int)blockIdx.x * 4 + pw, (int)gridDim.x * 4);
     }
     // GU phase 0: P_u = W1_u^T x_u of every group of this chain wave's units, one 16-group tile per
     // FOLD units (k-step q takes user feature XH lq + q), into gpart

@@ -154,3 +154,43 @@ def test_in_kernel_index_flags_stale_and_range():
     assert torch.equal(eng.mlp, twin.mlp)
     assert torch.isfinite(eng.emb).all()
     assert N.NCF_ROW_PRISTINE > 0
+
+
+@pytest.mark.parametrize("B", [16384, 1024])
+def test_stale_counted_step_is_dropped(B):
+    """A counted batch whose ids change behind torch's back is dropped by the in-kernel fill
+    (the wave kernel's at 16,384 samples, the fill launch's at 1,024): nothing of the step is
+    applied — bitwise the engine that never ran it (same counted-ahead history, final flush) —
+    the error is raised, and the next counted steps train normally."""
+    U, I = 3000, 2000
+    shape = O.NCFShape(U, I, LAYERS, GMF)
+    w = _weights(shape, 13)
+    bt = [_batch(U, I, B, 90 + s) for s in range(5)]
+    engines = []
+    for stale in (True, False):
+        e = NCFEngine(U, I, LAYERS, GMF, max_batch=B, lazy_adam=True)
+        e.set_keras_weights(w)
+        e.train_step(*bt[0], group=GROUP, k=2)
+        stage = (bt[1][0].clone(), bt[1][1].clone())
+        e.train_step(*bt[0], group=GROUP, k=2, next_batch=stage)
+        if stale:
+            stage[1].data.copy_(bt[2][1])                 # behind torch's back
+            e.train_step(stage[0], stage[1], bt[1][2], group=GROUP, k=2)
+            with pytest.raises(RuntimeError):
+                e.check_errors()
+        e.flush()
+        engines.append(e)
+    a, d = engines
+    torch.cuda.synchronize()
+    assert torch.equal(a.emb, d.emb) and torch.equal(a.emb_m, d.emb_m) and torch.equal(a.emb_v, d.emb_v)
+    assert torch.equal(a.mlp, d.mlp) and torch.equal(a.mlp_m, d.mlp_m) and torch.equal(a.mlp_v, d.mlp_v)
+    assert NCFEngine.read_stats(a.stats) == NCFEngine.read_stats(d.stats)
+    assert int(a.step.item()) == int(d.step.item())
+    # afterwards both train the same counted steps to the same bits
+    for s in (3, 4):
+        for e in engines:
+            e.train_step(*bt[s], group=GROUP, k=2, next_batch=(bt[4][0], bt[4][1]) if s == 3 else None)
+    for e in engines:
+        e.check_errors()
+        e.flush()
+    assert torch.equal(a.emb, d.emb) and torch.equal(a.mlp, d.mlp)

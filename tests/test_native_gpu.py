@@ -520,10 +520,11 @@ def test_counted_ahead_ids_changed_in_place():
 
 def test_stale_count_step_keeps_the_dense_decay_state():
     """A counted-ahead batch whose item ids change behind torch's back (NCF_WSERR_STALE_COUNT):
-    the rows it reads that the counted set missed owe their deferred decay — the step replays them
-    before the forward pass, so the table stays in the dense-sweep state.  Pinned against an engine
-    that flushes (every row current) right before the same stale step: with the replay the two are
-    bitwise equal; without it the missed rows' p would be stale and differ."""
+    the rows it reads that the counted set missed owe their deferred decay.  The step must leave
+    the table in a consistent deferred-decay state either way — the in-kernel fill drops the step
+    (nothing of it applied), the index launches replay the missed rows before the forward pass —
+    so an engine that flushes (every row current) right before the same stale step ends bitwise
+    equal after the final flush; a stale p read and then applied would differ."""
     shape = O.NCFShape(*SHAPES[3])
     w = _weights(shape, 70)
     bt = []
