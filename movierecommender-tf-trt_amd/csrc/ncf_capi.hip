@@ -600,7 +600,8 @@ static int run_fb(const ncf_shape_t& s, const ncf::WsLayout& L, const ncf_model_
     const bool unit = variant == NCF_FB_UNIT || variant == NCF_FB_WAVE;
     bool check_fold = false;  // the unit / wave kernels check an earlier call's index fold themselves
     if (fill) {
-        if (variant != NCF_FB_WAVE || sharded) return fail(NCF_EINVAL, "in-kernel index fill: wave kernel only");
+        if ((variant != NCF_FB_WAVE && variant != NCF_FB_UNIT) || sharded)
+            return fail(NCF_EINVAL, "in-kernel index fill: wave or unit kernel only");
     } else if (index_filled) {
         // k_fill_ahead has just filled this step's index (its fold is the kernel's)
     } else if (sharded || (h->index_ready == 1 && !after_index) || h->index_ready == 3) {
@@ -648,7 +649,7 @@ static int run_fb(const ncf_shape_t& s, const ncf::WsLayout& L, const ncf_model_
     else if (unit)
         e = ncf::launch_fb_unit(s, L, ws, model->emb, model->mlp, users, items, labels, n, h->inv_batch, ids,
                                 h->group, h->k, &out->nslab, &out->nbce, &out->nmet, st, fold, h->mlp_bf16 != 0,
-                                check_fold);
+                                check_fold, fill);
     else if (use_fused(s, h))
         e = ncf::launch_fb_fused(s, L, ws, model->emb, model->mlp, users, items, labels, n, h->inv_batch, ids,
                                  h->group, h->k, &out->nslab, &out->nbce, &out->nmet, st, fold);
@@ -711,13 +712,18 @@ static int check_train_args(const ncf_shape_t* s, const ncf_model_t* model, cons
 // counted set missed at their deferred step, so the update and stats launches apply nothing of
 // the step (ws stale_step, fill_wave) — table, moments, dense layers, stats and step counter stay
 // as they were, a consistent deferred-decay state — and check_errors raises.
-// Returns 0: the index launches; 1: the wave kernel fills; 2: k_fill_ahead fills
+// Returns 0: the index launches; 1: the forward/backward launch fills (the wave kernel's weight-gradient
+// waves, or spare workgroups of a unit launch that leaves CUs idle); 2: k_fill_ahead fills
 static int fill_in_kernel(const ncf_shape_t& s, const ncf::WsLayout& L, const ncf_hyper_t* h, int64_t n) {
     if (!NCF_FILL_IN_KERNEL || h->index_ready != 2 || h->optimizer != NCF_OPT_ADAM || side_stream_mode() != 0 ||
         L.world != 0 || L.nscan > ncf::kMaxFillScan || ncf::unsorted_heavy_c(s) < ncf::kHeavyMin)
         return 0;
     if (NCF_FILL_IN_KERNEL == 1 && use_fused(s, h) && fb_variant(s, h, n) == NCF_FB_WAVE && h->force_generic != 6 &&
         ncf::wave_fill_supported(s))
+        return 1;
+    // the unit kernel's grid leaves CUs idle (small batches, e.g. config B): fill workgroups there
+    if (NCF_FILL_IN_KERNEL == 1 && use_fused(s, h) && fb_variant(s, h, n) == NCF_FB_UNIT &&
+        ncf::unit_fill_fits(s, n, h->mlp_bf16 != 0, L.keys + 1))
         return 1;
     return 2;
 }

@@ -698,14 +698,16 @@ hipError_t launch_fb_wave(const ncf_shape_t& s, const WsLayout& L, void* ws, con
                           const FillArgs* fill = nullptr);
 // the split form runs for this shape (its weight-gradient waves can build the index: FillArgs)
 bool wave_fill_supported(const ncf_shape_t& s);
-// the in-kernel fill as a launch of its own (ncf_index.hip)
-// (ncf_update.hip) the fill as a launch of its own
+// the in-kernel fill as a launch of its own (ncf_update.hip)
 hipError_t launch_fill_ahead(const FillArgs& f, const int32_t* users, const int32_t* items, int64_t n, int fold,
                              hipStream_t st);
+// fill (optional): the batch's index filled by extra workgroups of the unit launch, on the CUs its
+// unit grid leaves idle (unit_fill_fits)
 hipError_t launch_fb_unit(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, const float* mlp,
                           const int32_t* users, const int32_t* items, const float* labels, int64_t n,
                           float inv_batch, IdSpace ids, int group, int topk, int* nslab, int* nbce, int* nmet,
-                          hipStream_t st, int fold, bool bf16, bool check_fold = false);
+                          hipStream_t st, int fold, bool bf16, bool check_fold = false, const FillArgs* fill = nullptr);
+bool unit_fill_fits(const ncf_shape_t& s, int64_t n, bool bf16, int64_t r1);
 // fused MFMA forward only (shapes with s.fast_path): probs; with labels also one BCE partial per
 // workgroup in ws part_bce (*nbce of them)
 hipError_t launch_fwd_fused(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, const float* mlp,

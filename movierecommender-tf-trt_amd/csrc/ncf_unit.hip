@@ -332,8 +332,17 @@ __global__ __launch_bounds__(S::NT, 1) void k_fb_unit(const float* __restrict__ 
                                                        float* __restrict__ gs, float* __restrict__ slabs,
                                                        float* __restrict__ part_bce, int group, int topk,
                                                        float* __restrict__ part_hit, float* __restrict__ part_dcg,
-                                                       const int32_t* __restrict__ ifold, int32_t* __restrict__ ferr) {
+                                                       const int32_t* __restrict__ ifold, int32_t* __restrict__ ferr,
+                                                       FillArgs fa, int nunit_blocks) {
     constexpr int L0 = S::L0, L1 = S::L1, L2 = S::L2, L3 = S::L3, G = S::G, D0 = S::D0, W = S::W, U = S::U;
+    // a batch counted and scanned ahead (fa.cnt) and a unit grid that leaves CUs idle: the
+    // workgroups past the unit grid fill this batch's index there (fill_wave) — no fill launch
+    if ((int)blockIdx.x >= nunit_blocks) {
+        if (fa.cnt)
+            fill_wave(fa, users, items, n, FOLD, ((int)blockIdx.x - nunit_blocks) * (S::NT / 64) + (int)(threadIdx.x >> 6),
+                      ((int)gridDim.x - nunit_blocks) * (S::NT / 64));
+        return;
+    }
     // an index built by an earlier call (ncf_build_index / ncf_shard_plan) must fold as this kernel does
     if (ifold && blockIdx.x == 0 && threadIdx.x == 0 && *ifold != FOLD) atomicOr(ferr, kErrFold);
     constexpr int XP = S::XP, GP = S::GP, GPA = GP > 0 ? GP : 1, NQ = S::NQ;
@@ -822,11 +831,18 @@ bool umatches(const ncf_shape_t& s) {
            s.layers[3] == S::L3 && s.gmf_dim == S::G && s.row_width == S::W && s.gmf_stride == S::G;
 }
 
+// fill workgroups of NT threads for one pass per wave (fill_wave: 256 keys, 128 contributions)
+int unit_fill_blocks(int64_t r1, int64_t n, int nt) {
+    const int64_t rows = (r1 + 255) / 256, contribs = (2 * n + 127) / 128;
+    const int64_t waves = rows > contribs ? rows : contribs;
+    return (int)((waves + nt / 64 - 1) / (nt / 64));
+}
+
 template <class S, bool BF>
 hipError_t launch_unit_one(const WsLayout& L, void* ws, const float* emb, const float* mlp, const int32_t* users,
                            const int32_t* items, const float* labels, int64_t n, float inv_batch, IdSpace ids,
                            int group, int topk, int* nslab, int* nbce, int* nmet, hipStream_t st, int fold,
-                           bool check_fold) {
+                           bool check_fold, const FillArgs* fill) {
     static bool configured = false;  // one-time attribute set per shape (idempotent)
     if (!configured) {
         for (const void* k : {(const void*)k_fb_unit<S, 0, BF>, (const void*)k_fb_unit<S, 2, BF>,
@@ -841,11 +857,14 @@ hipError_t launch_unit_one(const WsLayout& L, void* ws, const float* emb, const 
     int grid = (int)(wgs < 256 ? wgs : 256);
     if (grid < 1) grid = 1;
     const bool in_kernel = group > 0 && group <= 32 && 32 % group == 0;
+    const int nfill = fill ? unit_fill_blocks(fill->r1, n, S::NT) : 0;
+    if (fill && (check_fold || fill->nscan < 1 || fill->nscan > kMaxFillScan)) return hipErrorInvalidValue;
+    const FillArgs fa = fill ? *fill : FillArgs{};
     auto go = [&](auto kern) {
-        launch(kern, grid, S::NT, S::LDS_BYTES, st, emb, mlp, users, items, labels, n, ids, inv_batch,
+        launch(kern, grid + nfill, S::NT, S::LDS_BYTES, st, emb, mlp, users, items, labels, n, ids, inv_batch,
                at<float>(ws, L.probs), at<float>(ws, L.gs), at<float>(ws, L.slabs), at<float>(ws, L.part_bce), group,
                topk, in_kernel ? at<float>(ws, L.part_hit) : nullptr, in_kernel ? at<float>(ws, L.part_dcg) : nullptr,
-               check_fold ? at<const int32_t>(ws, L.ifold) : nullptr, at<int32_t>(ws, L.err));
+               check_fold ? at<const int32_t>(ws, L.ifold) : nullptr, at<int32_t>(ws, L.err), fa, grid);
     };
     switch (fold) {
         case 0: go(k_fb_unit<S, 0, BF>); break;
@@ -886,15 +905,25 @@ bool unit_supported(const ncf_shape_t& s) {
            umatches<UShapeC0<32, 1>>(s);
 }
 
+// the unit launch's grid leaves room for the fill workgroups on CUs it does not use (in-kernel fill)
+bool unit_fill_fits(const ncf_shape_t& s, int64_t n, bool bf16, int64_t r1) {
+    if (!unit_supported(s)) return false;
+    const int sched = bf16 ? 1 : unit_sched(n);
+    const int ng = sched == 2 ? 2 : 1, nt = 256 * ng;
+    const int64_t units = (n + (sched == 64 ? 63 : 31)) / (sched == 64 ? 64 : 32);
+    const int64_t wgs = (units + ng - 1) / ng;
+    return wgs + unit_fill_blocks(r1, n, nt) <= 256;
+}
+
 hipError_t launch_fb_unit(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, const float* mlp,
                           const int32_t* users, const int32_t* items, const float* labels, int64_t n,
                           float inv_batch, IdSpace ids, int group, int topk, int* nslab, int* nbce, int* nmet,
-                          hipStream_t st, int fold, bool bf16, bool check_fold) {
+                          hipStream_t st, int fold, bool bf16, bool check_fold, const FillArgs* fill) {
     if (fold != 0 && (fold < 2 || fold > 8 || (fold & (fold - 1)) != 0 || n % fold != 0)) return hipErrorInvalidValue;
     const int sched = unit_sched(n);
     // bf16 operands: one 32-sample unit group per workgroup at every size (config B's path)
 #define NCF_ARGS \
-    L, ws, emb, mlp, users, items, labels, n, inv_batch, ids, group, topk, nslab, nbce, nmet, st, fold, check_fold
+    L, ws, emb, mlp, users, items, labels, n, inv_batch, ids, group, topk, nslab, nbce, nmet, st, fold, check_fold, fill
 #define NCF_TRY(SH)                                                                                           \
     if (umatches<SH<32, 1>>(s))                                                                               \
         return bf16 ? launch_unit_one<SH<32, 1>, true>(NCF_ARGS)                                              \

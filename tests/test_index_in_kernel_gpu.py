@@ -1,11 +1,12 @@
 """The step's index built inside the forward/backward launch (ncf_capi.hip fill_in_kernel).
 
-From 16,384 samples a deferred-decay step whose batch was counted ahead by the previous step
-(``train_step(..., next_batch=)``, as bench.py and fit_generator run it) skips the index fill and
-list-sort launches: the wave kernel's weight-gradient waves fill the index while their chain
-waves run the first unit (``fill_wave``, ncf_internal.h), and the touched-row update orders each
-row's contribution list itself — across the lanes of the row's group, or block-wide for rows
-longer than a row group (heavy rows).  The embedding update must still sum every row's
+A deferred-decay step whose batch was counted ahead by the previous step (``train_step(...,
+next_batch=)``, as bench.py and fit_generator run it) skips the index fill and list-sort
+launches: from 16,384 samples the wave kernel's weight-gradient waves fill the index while their
+chain waves run the first unit (``fill_wave``, ncf_internal.h); below, spare workgroups of the
+unit kernel's launch do, where its grid leaves CUs idle (else a fill launch of its own).  The
+touched-row update orders each row's contribution list itself — across the lanes of the row's
+group, or block-wide for rows longer than a row group (heavy rows).  The embedding update must still sum every row's
 contributions in ascending order, so these tests hold that path BITWISE against the dense Keras
 sweep (every row, sorted lists) and against deferred decay with the fill and sort launches
 (reference semantics: movierec/model.py:199-202, Keras v1 Adam over the densified IndexedSlices).
@@ -56,7 +57,7 @@ def _batch(U, I, B, seed, hot_items=3, hot_frac=0.05, mixed_frac=0.1):
             (users.astype(np.int32), items.astype(np.int32), y.astype(np.float32))]
 
 
-@pytest.mark.parametrize("B", [16384, 20480])
+@pytest.mark.parametrize("B", [16384, 20480, 4096])
 def test_in_kernel_index_bitwise_dense_sweep(B):
     U, I = 3000, 2000
     shape = O.NCFShape(U, I, LAYERS, GMF)
@@ -66,7 +67,9 @@ def test_in_kernel_index_bitwise_dense_sweep(B):
         e = NCFEngine(U, I, LAYERS, GMF, max_batch=B, **kw)
         e.set_keras_weights(w)
         engines[name] = e
-    assert engines["ahead"].kernel_for(B) == "fused-mfma-wave"
+    # 16,384 and up: the wave kernel's weight-gradient waves fill; 4,096: the unit kernel's grid leaves
+    # CUs idle and spare workgroups of its launch fill
+    assert engines["ahead"].kernel_for(B) == ("fused-mfma-wave" if B >= 16384 else "fused-mfma-unit")
     batches = [_batch(U, I, B, 40 + s) for s in range(6)]
     for s, (u, it, y) in enumerate(batches):
         nxt = (batches[s + 1][0], batches[s + 1][1]) if s + 1 < len(batches) else None
