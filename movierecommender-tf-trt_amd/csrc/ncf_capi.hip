@@ -313,6 +313,8 @@ WsLayout make_layout(const ncf_shape_t& s, int64_t B, int world) {
         L.touched = take((size_t)(R < 2 * B ? R : 2 * B) * 4);
         L.touched_oc = take((size_t)(R < 2 * B ? R : 2 * B) * 8);
         L.heavy = take((size_t)(2 * B / kHeavyMin + 1) * 4);
+        L.tl = take((size_t)L.nscan * kScanBlock * 4);
+        L.tocl = take((size_t)L.nscan * kScanBlock * 8);
         L.slist = take((size_t)2 * B * 4);
     }
     L.act = take((size_t)B * A * 4);
@@ -731,8 +733,8 @@ static int fill_in_kernel(const ncf_shape_t& s, const ncf::WsLayout& L, const nc
 static ncf::FillArgs fill_args(const ncf_shape_t& s, const ncf::WsLayout& L, void* ws) {
     using ncf::at;
     return ncf::FillArgs{at<int32_t>(ws, L.cnt), at<const int32_t>(ws, L.offs_local), at<const int32_t>(ws, L.tot),
-                         at<const int32_t>(ws, L.uloc), at<const int32_t>(ws, L.utot), L.nscan, L.keys + 1,
-                         at<int32_t>(ws, L.offs), at<int32_t>(ws, L.list), at<int32_t>(ws, L.touched),
+                         at<const int32_t>(ws, L.utot), at<const int32_t>(ws, L.tl), at<const int2>(ws, L.tocl),
+                         L.nscan, L.keys + 1, at<int32_t>(ws, L.list), at<int32_t>(ws, L.touched),
                          at<int2>(ws, L.touched_oc), at<int32_t>(ws, L.nuniq), at<int32_t>(ws, L.heavy),
                          at<int32_t>(ws, L.heavy_n), ncf::unsorted_heavy_c(s), at<int32_t>(ws, L.err),
                          at<int32_t>(ws, L.ifold), s.num_users, s.num_items, L.list_cap,

@@ -80,6 +80,8 @@ struct WsLayout {
     size_t touched_oc;  // int2[min(R, 2B)] their (list offset, contribution count): the update needs no offs
     size_t heavy;     // int32[2B / kHeavyMin + 1] single table: touched-list positions of the rows whose
                       // lists the touched-row update sorts block-wide (FillArgs); count in heavy_n
+    size_t tl;        // int32[nscan * kScanBlock] single table: the scan ahead's touched rows per scan block
+    size_t tocl;      // int2[nscan * kScanBlock]  their (offset inside the block's list part, count)
     size_t slist;     // int32[2B] single table: the heavy rows' sorted lists (indexed like list)
     size_t act;       // float[B * A] generic kernel activations
     size_t dz;        // float[B * D] generic kernel pre-activation grad
@@ -134,6 +136,15 @@ __device__ __forceinline__ bool wave_run_count(int32_t* __restrict__ cnt, int ke
     return false;
 }
 
+// The scan ahead's share of the next index's row side: scan block b's touched rows, in key order,
+// at [b * kScanBlock, + utot[b]) of tl, with their (offset inside the block's part of the list,
+// count) in tocl — the fill compacts them into the touched list (fill_wave), touching occupied
+// keys only instead of every key of the table
+struct TouchedOut {
+    int32_t* tl;
+    int2* tocl;
+};
+
 // move_to (optional): the counts were taken ahead (ws cnt_ahead); they also move to the fill's
 // cursors move_to (ws cnt) and cnt is zeroed for the next batch's count
 template <bool UNIQ>
@@ -142,7 +153,7 @@ template <bool UNIQ>
 __device__ inline void scan_local_body(const int32_t* cnt, int64_t r1, int32_t* __restrict__ offs,
                                        int32_t* __restrict__ tot, int32_t* __restrict__ uloc,
                                        int32_t* __restrict__ utot, int blk, int32_t* __restrict__ move_to = nullptr,
-                                       int32_t* __restrict__ zero_at_end = nullptr) {
+                                       int32_t* __restrict__ zero_at_end = nullptr, TouchedOut to = TouchedOut{}) {
     __shared__ int sw[4];
     const int64_t base = (int64_t)blk * kScanBlock + threadIdx.x * 8;
     // 8 keys per thread: two int4 loads / stores when all 8 are inside (the workspace regions
@@ -209,6 +220,18 @@ __device__ inline void scan_local_body(const int32_t* cnt, int64_t r1, int32_t* 
                 if (base + j < r1) uloc[base + j] = o[j];
         }
         if (threadIdx.x == 0) utot[blk] = utotal;
+        if (to.tl) {
+            int ro = run - sum;  // this thread's first list offset inside the block (o[] is the numbering now)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                if (v[j] > 0) {
+                    const int64_t e = (int64_t)blk * kScanBlock + o[j];
+                    to.tl[e] = (int)(base + j);
+                    to.tocl[e] = make_int2(ro, v[j]);
+                }
+                ro += v[j];
+            }
+        }
     }
 #if NCF_DEBUG_BOUNDS == 1
     if (move_to && threadIdx.x == 0 && blk < 4) printf("scan ahead blk %d: tot %d utot %d\n", blk, total, 0);
@@ -387,11 +410,11 @@ struct FillArgs {
     int32_t* cnt;             // per-key cursors: the counts the scan ahead copied (ws cnt)
     const int32_t* local;     // per-scan-block exclusive offsets (ws offs_local)
     const int32_t* tot;       // scan-block totals
-    const int32_t* uloc;      // occupied-key numbering, per scan block
-    const int32_t* utot;
+    const int32_t* utot;      // occupied keys per scan block
+    const int32_t* tl;        // the scan ahead's touched rows per block (TouchedOut)
+    const int2* tocl;
     int nscan;                // <= kMaxFillScan
     int64_t r1;               // keys + 1
-    int32_t* offs;            // key -> first list slot
     int32_t* list;
     int32_t* touched;         // touched rows, ascending
     int2* toc;                // their (list offset, count)
@@ -420,7 +443,6 @@ struct FillArgs {
 #define NCF_BOUND(cond, ...)
 #endif
 
-constexpr int kFillRowsPerLane = 4;     // fill_wave's RU: keys per lane and pass of the rows part
 constexpr int kFillContribPerLane = 2;  // its CU: contributions per lane and pass
 
 // Wave gw of nw: its share of the fill of batch (users, items, n) folded by `fold`.  The
@@ -438,9 +460,11 @@ __device__ inline void fill_wave(const FillArgs& f, const int32_t* __restrict__ 
                                  const int32_t* __restrict__ items, int64_t n, int fold, int gw, int nw) {
     const int lane = threadIdx.x & 63;
     int p0, p1, q0, q1;  // pre[lane], pre[lane + 64], upre[lane], upre[lane + 64]
+    int u0, u1, ntouched;  // utot[lane], utot[lane + 64], their sum
     {
         const int t0 = lane < f.nscan ? f.tot[lane] : 0, t1 = lane + 64 < f.nscan ? f.tot[lane + 64] : 0;
-        const int u0 = lane < f.nscan ? f.utot[lane] : 0, u1 = lane + 64 < f.nscan ? f.utot[lane + 64] : 0;
+        u0 = lane < f.nscan ? f.utot[lane] : 0;
+        u1 = lane + 64 < f.nscan ? f.utot[lane + 64] : 0;
         int a0 = t0, a1 = t1, b0 = u0, b1 = u1;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
@@ -453,6 +477,7 @@ __device__ inline void fill_wave(const FillArgs& f, const int32_t* __restrict__ 
         p1 = ca + a1 - t1;
         q0 = b0 - u0;
         q1 = cb + b1 - u1;
+        ntouched = cb + __shfl(b1, 63, 64);
 #if NCF_DEBUG_BOUNDS == 1
         if (gw == 0 && lane < 4 && lane < f.nscan)
             printf("fill lane %d: tot %d utot %d pre %d upre %d nscan %d\n", lane, t0, u0, p0, q0, f.nscan);
@@ -464,52 +489,44 @@ __device__ inline void fill_wave(const FillArgs& f, const int32_t* __restrict__ 
         const int x = __shfl(p0, b & 63, 64), y = __shfl(p1, b & 63, 64);
         return b < 64 ? x : y;
     };
-    auto upre = [&](int64_t key) {
-        const int b = (int)(key / kScanBlock);
-        const int x = __shfl(q0, b & 63, 64), y = __shfl(q1, b & 63, 64);
-        return b < 64 ? x : y;
-    };
-    const int64_t K = f.r1 - 1;
     const int64_t rstep = (int64_t)nw * 64;
-    // rows: offsets, the touched list with (offset, count), the heavy rows (RU rows per lane and
-    // pass, their loads issued together)
-    constexpr int RU = kFillRowsPerLane;
-    for (int64_t rw = (int64_t)gw * 64; (PART & 1) && rw < f.r1; rw += RU * rstep) {
-        int lo[RU], lo1[RU], ul[RU];
-#pragma unroll
-        for (int j = 0; j < RU; ++j) {
-            const int64_t r = rw + j * rstep + lane;
-            lo[j] = r < f.r1 ? f.local[r] : 0;
-            lo1[j] = r < K ? f.local[r + 1] : 0;
-            ul[j] = r < K ? f.uloc[r] : 0;
-        }
-#pragma unroll
-        for (int j = 0; j < RU; ++j) {
-            const int64_t r = rw + j * rstep + lane;
-            const int64_t rc = r < f.r1 ? r : K;  // (shuffles: every lane)
-            const int o = lo[j] + pre(rc);
-            const int o1 = lo1[j] + pre(rc < K ? rc + 1 : K);
-            const int u = ul[j] + upre(rc);
-            if (r < f.r1) f.offs[r] = o;
-            if (r < K && o1 > o) {
-                NCF_BOUND(u >= 0 && u < f.touched_cap && o >= 0 && o1 <= f.list_cap,
-                          "fill row %lld: u %d (cap %lld) o %d o1 %d (list cap %lld)\n", (long long)r, u,
-                          (long long)f.touched_cap, o, o1, (long long)f.list_cap) {
-                f.touched[u] = (int)r;
-                f.toc[u] = make_int2(o, o1 - o);
-                if (o1 - o > f.hc) {
-                    const int hx = atomicAdd(f.heavy_n, 1);
-                    NCF_BOUND(hx < f.heavy_cap, "fill heavy %d cap %lld\n", hx, (long long)f.heavy_cap)
-                    f.heavy[hx] = u;
-                }
-                }
+    // rows: the scan ahead's per-block touched rows compacted into the touched list with (list
+    // offset, count), and the heavy rows — one 64-slot chunk of a block's row slots per wave and
+    // pass; a chunk past the block's occupied keys costs a compare (its count from a register)
+    const int64_t nchunk = (int64_t)f.nscan * (kScanBlock / 64);
+    for (int64_t ch = gw; (PART & 1) && ch < nchunk; ch += nw) {
+        const int b = (int)(ch / (kScanBlock / 64));
+        const int j = (int)(ch % (kScanBlock / 64)) * 64 + lane;
+        // the block's count and prefixes, read while every lane is active: v_readlane takes the
+        // named lane's register whatever the exec mask, and inside the branch below that lane may
+        // be inactive — its copy of the register then holds whatever the allocator put there (a
+        // first version read them there and wrote a row at another block's position)
+        const int ub = __builtin_amdgcn_readlane(b < 64 ? u0 : u1, b & 63);     // utot[b]
+        const int ubase = __builtin_amdgcn_readlane(b < 64 ? q0 : q1, b & 63);  // upre(b)
+        const int obase = __builtin_amdgcn_readlane(b < 64 ? p0 : p1, b & 63);  // pre(b)
+        if ((int)(ch % (kScanBlock / 64)) * 64 >= ub) continue;                 // wave-uniform
+        if (j < ub) {
+            const int64_t e = (int64_t)b * kScanBlock + j;
+            const int key = f.tl[e];
+            const int2 lc = f.tocl[e];
+            const int u = ubase + j;
+            const int o = obase + lc.x;
+            NCF_BOUND(u >= 0 && u < f.touched_cap && o >= 0 && o + lc.y <= f.list_cap,
+                      "fill row %d: u %d (cap %lld) o %d c %d (list cap %lld)\n", key, u,
+                      (long long)f.touched_cap, o, lc.y, (long long)f.list_cap) {
+            f.touched[u] = key;
+            f.toc[u] = make_int2(o, lc.y);
+            if (lc.y > f.hc) {
+                const int hx = atomicAdd(f.heavy_n, 1);
+                NCF_BOUND(hx < f.heavy_cap, "fill heavy %d cap %lld\n", hx, (long long)f.heavy_cap)
+                f.heavy[hx] = u;
+            }
             }
         }
     }
     if constexpr ((PART & 1) != 0) {
-        const int nu = f.uloc[K] + upre(K);
         if (gw == 0 && lane == 0) {
-            *f.nuniq = nu;
+            *f.nuniq = ntouched;
             *f.ifold = fold;
         }
     }

@@ -705,6 +705,8 @@ struct SortRows {
     int mcap;                  // contribution ids are below this (2 * max batch): a stale list slot is clamped
     const int32_t* drop;       // ws stale_step: nonzero — the step is dropped (fill_wave): only the next
                                // batch's count and catch-up ahead run, the latter to *step
+    const int32_t* local;      // this step's per-block key offsets and block totals (a key's count:
+    const int32_t* tot;        // the next key's offset minus its own; the fill writes no offs array)
 };
 constexpr int kHeavyChunk = 1024;  // heavy-row list entries staged in LDS per round
 
@@ -894,8 +896,13 @@ __global__ __launch_bounds__(kBlock, UNSORTED ? NCF_TOUCHED_MIN_BLOCKS_UNSORTED 
                 // (its count was 0) owns the row's replay — no claim atomic of its own
                 int o0 = 0, o1 = 0, sv = t;
                 if (ca.replay && ok && key < ca.lazy_rows) {
-                    o0 = offs[key];
-                    o1 = offs[key + 1];
+                    if (UNSORTED) {   // (the in-kernel fill writes no offs array: the key's count instead)
+                        o0 = so.local[key];
+                        o1 = (key + 1) % kScanBlock != 0 ? so.local[key + 1] : so.tot[key / kScanBlock];
+                    } else {
+                        o0 = offs[key];
+                        o1 = offs[key + 1];
+                    }
                     sv = row_step[key];
                 }
                 const bool first = wave_run_count<true>(ca.cnt, key, ok);
@@ -1457,7 +1464,7 @@ hipError_t launch_fill_ahead(const FillArgs& f, const int32_t* users, const int3
     if (f.nscan < 1 || f.nscan > kMaxFillScan || n < 1) return hipErrorInvalidValue;
     // one pass per wave where the grid allows (4 waves per block)
     auto waves = [](int64_t work, int per) { return (work + 64 * per - 1) / (64 * per); };
-    int64_t nr = waves(f.r1, kFillRowsPerLane), nc = waves(2 * n, kFillContribPerLane);
+    int64_t nr = (int64_t)f.nscan * (kScanBlock / 64), nc = waves(2 * n, kFillContribPerLane);
     const int64_t cap = 2048 * (kBlock / 64) / 2;  // at most 2048 blocks, half for each part
     nr = nr > cap ? cap : nr;
     nc = nc > cap ? cap : nc;
@@ -1475,6 +1482,7 @@ struct ScanAhead {
     int32_t *offs, *tot, *uloc, *utot;
     int32_t* cursor;           // ws cnt
     int32_t* heavy_n;          // the in-kernel fill's heavy-row count (FillArgs), zeroed here
+    TouchedOut to;             // the next index's per-block touched rows (single-table workspaces)
 };
 __global__ __launch_bounds__(kBlock) void k_stats_scan(float* __restrict__ summary,
                                                        const float* __restrict__ reg_emb, int nreg_emb,
@@ -1492,21 +1500,27 @@ __global__ __launch_bounds__(kBlock) void k_stats_scan(float* __restrict__ summa
         stats_body(summary, reg_emb, nreg_emb, reg_mlp, nreg_mlp, inv_batch, stats, step, bump, red);
     } else {
         scan_local_body<true>(sc.cnt, sc.r1, sc.offs, sc.tot, sc.uloc, sc.utot, (int)blockIdx.x - 1, sc.cursor,
-                              sc.heavy_n);
+                              sc.heavy_n, sc.to);
     }
 }
 
 // The next batch's per-block key scan alone (k_stats_scan's blocks >= 1), for a counting-ahead
 // update that has no stats launch of its own behind it (user-partitioned data parallelism).
 __global__ __launch_bounds__(kBlock) void k_scan_ahead(ScanAhead sc) {
-    scan_local_body<true>(sc.cnt, sc.r1, sc.offs, sc.tot, sc.uloc, sc.utot, (int)blockIdx.x, sc.cursor, sc.heavy_n);
+    scan_local_body<true>(sc.cnt, sc.r1, sc.offs, sc.tot, sc.uloc, sc.utot, (int)blockIdx.x, sc.cursor, sc.heavy_n,
+                          sc.to);
+}
+
+static TouchedOut touched_out(const WsLayout& L, void* ws) {
+    return L.world == 0 ? TouchedOut{at<int32_t>(ws, L.tl), at<int2>(ws, L.tocl)} : TouchedOut{};
 }
 
 hipError_t launch_scan_ahead(const WsLayout& L, void* ws, int64_t keys, hipStream_t st) {
     const int64_t r1 = keys + 1;
     const int nscan = (int)((r1 + kScanBlock - 1) / kScanBlock);
     ScanAhead sc{at<const int32_t>(ws, L.cnt_ahead), r1, at<int32_t>(ws, L.offs_local), at<int32_t>(ws, L.tot),
-                 at<int32_t>(ws, L.uloc), at<int32_t>(ws, L.utot), at<int32_t>(ws, L.cnt), at<int32_t>(ws, L.heavy_n)};
+                 at<int32_t>(ws, L.uloc), at<int32_t>(ws, L.utot), at<int32_t>(ws, L.cnt), at<int32_t>(ws, L.heavy_n),
+                 touched_out(L, ws)};
     launch(k_scan_ahead, nscan, kBlock, 0, st, sc);
     return hipGetLastError();
 }
@@ -1688,7 +1702,8 @@ hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, vo
             // heavy rows are rare (lists longer than a row group's lanes): a few blocks stride over them
             so = SortRows{1, unsorted_heavy_c(s), 32, at<const int32_t>(ws, L.heavy), at<const int32_t>(ws, L.heavy_n),
                           at<int32_t>(ws, L.cnt), at<int32_t>(ws, L.err), at<int32_t>(ws, L.slist),
-                          (int)(2 * L.max_batch), at<const int32_t>(ws, L.stale_step)};
+                          (int)(2 * L.max_batch), at<const int32_t>(ws, L.stale_step),
+                          at<const int32_t>(ws, L.offs_local), at<const int32_t>(ws, L.tot)};
         }
         launch(unsorted_lists ? k_emb_adam_touched<true> : k_emb_adam_touched<false>, (unsigned)so.nheavy + nupd + ncount + (unsigned)mt.nblocks + (unsigned)mm.nblocks,
                kBlock, 0, st, (float4*)emb, (float4*)m, (float4*)v, w4, at<const int32_t>(ws, L.touched),
@@ -1936,7 +1951,8 @@ hipError_t launch_stats(const WsLayout& L, void* ws, const float* summary_in, in
         const int64_t r1 = scan_keys + 1;
         const int nscan = (int)((r1 + kScanBlock - 1) / kScanBlock);
         ScanAhead sc{at<const int32_t>(ws, L.cnt_ahead), r1, at<int32_t>(ws, L.offs_local), at<int32_t>(ws, L.tot),
-                     at<int32_t>(ws, L.uloc), at<int32_t>(ws, L.utot), at<int32_t>(ws, L.cnt), at<int32_t>(ws, L.heavy_n)};
+                     at<int32_t>(ws, L.uloc), at<int32_t>(ws, L.utot), at<int32_t>(ws, L.cnt), at<int32_t>(ws, L.heavy_n),
+                     touched_out(L, ws)};
         launch(k_stats_scan, 1 + nscan, kBlock, 0, st, summary, reg, nreg_emb, reg + kUpdateGrid, nreg_mlp, inv_batch,
                stats, step, bump_step ? 1 : 0, sc, sa);
         return hipGetLastError();
