@@ -905,6 +905,9 @@ bool unit_supported(const ncf_shape_t& s) {
            umatches<UShapeC0<32, 1>>(s);
 }
 
+#ifndef NCF_UNIT_FILL_MAX_BLOCKS
+#define NCF_UNIT_FILL_MAX_BLOCKS 1024  // unit + fill workgroups (a fill workgroup shares a CU with a unit one when the units take them all: C at 8,192 53.3 vs 56.3 us with a fill launch)
+#endif
 // the unit launch's grid leaves room for the fill workgroups on CUs it does not use (in-kernel fill)
 bool unit_fill_fits(const ncf_shape_t& s, int64_t n, bool bf16, int64_t r1) {
     if (!unit_supported(s)) return false;
@@ -912,7 +915,7 @@ bool unit_fill_fits(const ncf_shape_t& s, int64_t n, bool bf16, int64_t r1) {
     const int ng = sched == 2 ? 2 : 1, nt = 256 * ng;
     const int64_t units = (n + (sched == 64 ? 63 : 31)) / (sched == 64 ? 64 : 32);
     const int64_t wgs = (units + ng - 1) / ng;
-    return wgs + unit_fill_blocks(r1, n, nt) <= 256;
+    return wgs + unit_fill_blocks(r1, n, nt) <= NCF_UNIT_FILL_MAX_BLOCKS;
 }
 
 hipError_t launch_fb_unit(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, const float* mlp,
