@@ -485,6 +485,17 @@ def native_step_check(cfg, world, rank, split):
     return check(cfg["layers"], cfg["gmf_dim"], cfg["negs"] + 1, split)
 
 
+def pmc_mfma_busy(kernel, config, batch):
+    """The MFMA-busy fraction of a forward/backward kernel from its committed rocprofv3 PMC pass
+    (profiles/mfma/<config>_b<batch>_<kernel>.json, tools/pmc_mfma.sh), or None."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "mfma",
+                        "%s_b%d_%s.json" % (config, batch, kernel))
+    if not os.path.exists(path):
+        return None
+    d = json.load(open(path))
+    return {"mfma_busy_frac": round(float(d["mfma_busy_frac"]), 3), "source": os.path.relpath(path, os.path.dirname(path) + "/../..")}
+
+
 def pmc_traffic(kernel, config, batch, mode):
     """HBM bytes per launch of ``kernel`` measured by tools/gpu_profile.sh (separate FETCH_SIZE /
     WRITE_SIZE rocprofv3 passes) for exactly this config, per-GPU batch and layout; None when no
@@ -821,6 +832,7 @@ def main():
     contribs = grad_rows(eng, B, g) if mode != "sharded" else 2 * B
     replay_rows = 0.0
     fb_bytes = fwd_bwd_bytes(eng.shape, B, contribs)
+    fill_bytes = 0
     train_exchange = dp.last_exchange if mode == "sharded" else None
     if mode == "sharded" and getattr(eng, "lazy", False):
         # deferred decay: the m served rows (unique per source) read and written (p, m, v), their
@@ -832,6 +844,11 @@ def main():
     elif getattr(eng, "lazy", False) and mode == "single":
         touched = float(np.mean([torch.unique(u).numel() + torch.unique(it).numel() for u, it, _ in pool[:16]]))
         nbytes = emb_update_bytes(eng.shape, B, touched_rows=touched, contribs=contribs)
+        if sampler is None and eng.kernel_for(B) in ("fused-mfma-wave", "fused-mfma-unit"):
+            # the counted batch's index is filled inside the forward/backward launch: per contribution
+            # its key's block offset read, cursor atomic and list slot written (the ids are already
+            # counted), per touched row its scan-ahead entry read and touched-list entry written
+            fill_bytes = contribs * 12 + touched * 24
         if sampler is None:
             nbytes += 2 * B * (4 + 8)   # the launch also counts the next batch: id reads + counter atomics
             # ... and catches the next batch's stale rows up (the rows it touches that this step
@@ -995,6 +1012,7 @@ def main():
                 "traffic_source": "rocprofv3 --pmc FETCH_SIZE(x2 gfx950) + WRITE_SIZE, profiles/traffic/ "
                                   "(this config, batch, layout and counted-ahead form only; null if not "
                                   "measured)"}
+    fb_bytes += fill_bytes
     fb_achieved = fb_flops / (fb_ms * 1e-3) / 1e12
     fb_exec = fwd_bwd_executed_flops(cfg, B, g, kpath)
     # the MLP tower's matrix products run on bf16 MFMA in the bf16 mode (config B): its dense peak
@@ -1019,7 +1037,17 @@ def main():
                "algorithmic_flops_per_launch": fb_flops, "avg_launch_ms": round(fb_ms, 5),
                "executed_flops_per_launch": fb_exec,
                "executed_TFLOPs": round(fb_exec / (fb_ms * 1e-3) / 1e12, 2) if fb_exec else None,
-               "hbm_GBs": round(fb_bytes / (fb_ms * 1e-3) / 1e9, 1), "algorithmic_bytes_per_launch": fb_bytes}
+               "frac_executed": round(fb_exec / (fb_ms * 1e-3) / 1e12 / fb_peak, 4) if fb_exec else None,
+               "hbm_GBs": round(fb_bytes / (fb_ms * 1e-3) / 1e9, 1), "algorithmic_bytes_per_launch": fb_bytes,
+               "index_fill_bytes_in_launch": fill_bytes or None}
+    busy = pmc_mfma_busy(fb_kernel, args.config, B) if fb_kernel else None
+    if busy is not None:
+        # what the counters say limits it: "bound" names the roofline it is priced against
+        hbm_frac = fb_roof["hbm_GBs"] / HBM_PEAK_GBS
+        fb_roof["mfma_busy_frac"] = busy["mfma_busy_frac"]
+        fb_roof["limiter"] = ("mfma" if busy["mfma_busy_frac"] >= 0.6 else "hbm" if hbm_frac >= 0.6 else
+                              "issue/latency: MFMA pipe busy %.2f of the kernel's cycles, HBM %.2f of peak "
+                              "(%s)" % (busy["mfma_busy_frac"], hbm_frac, busy["source"]))
     # `roofline` = the step's dominant kernel (longest average time per step)
     fb_per_step = fb_ms * nfb / steps_of(N.K_FWD_BWD)
     emb_per_step = kern_ms * nl / steps_of(N.K_EMB_UPDATE)

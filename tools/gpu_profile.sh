@@ -10,9 +10,8 @@ mkdir -p $OUT/traffic
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$OUT/trace -o run -- python $R/bench.py --steps 20 --warmup 3 --no-cpu-baseline > $R/$OUT/trace.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_emb_update|k_emb_adam_touched|k_emb_catchup|k_fb_fused|k_fb_unit|k_fb_wave" --output-format csv -d $R/$OUT/fetch -o run -- python $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline > $R/$OUT/fetch.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_emb_update|k_emb_adam_touched|k_emb_catchup|k_fb_fused|k_fb_unit|k_fb_wave" --output-format csv -d $R/$OUT/write -o run -- python $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline > $R/$OUT/write.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_emb_update|k_emb_adam_touched|k_fb_fused|k_fb_unit|k_fb_wave" --output-format csv -d $R/$OUT/fetch -o run -- python $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline > $R/$OUT/fetch.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_emb_update|k_emb_adam_touched|k_fb_fused|k_fb_unit|k_fb_wave" --output-format csv -d $R/$OUT/write -o run -- python $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline > $R/$OUT/write.log 2>&1
 cd $R
 python tools/pmc_traffic.py $OUT/fetch/run_counter_collection.csv $OUT/write/run_counter_collection.csv k_emb_adam_touched $OUT/traffic/C_b65536_single-ahead_k_emb_adam_touched.json C 65536 single-ahead
-python tools/pmc_traffic.py $OUT/fetch/run_counter_collection.csv $OUT/write/run_counter_collection.csv k_emb_catchup $OUT/traffic/C_b65536_single_k_emb_catchup.json
 python tools/pmc_traffic.py $OUT/fetch/run_counter_collection.csv $OUT/write/run_counter_collection.csv k_fb_wave $OUT/traffic/C_b65536_single_k_fb_wave.json
