@@ -47,31 +47,6 @@ __device__ inline void summary_body(const float* __restrict__ part_bce, int nbce
     }
 }
 
-// fold the summary into stats[] (loss, hr, dcg running sums) and bump the step (whole block)
-__device__ inline void stats_body(const float* __restrict__ summary, const float* __restrict__ reg_emb, int nreg_emb,
-                                  const float* __restrict__ reg_mlp, int nreg_mlp, float inv_batch,
-                                  double* __restrict__ stats, int32_t* step, int bump, float* red) {
-    const float re = block_sum_array(reg_emb, nreg_emb, red);
-    const float rm = block_sum_array(reg_mlp, nreg_mlp, red);
-    if (threadIdx.x == 0) {
-        const float loss = summary[NCF_SUM_BCE] * inv_batch + summary[NCF_SUM_REG] + (re + rm);
-        const float ng = summary[NCF_SUM_GROUPS];
-        const float hr = ng > 0.f ? summary[NCF_SUM_HIT] / ng : 0.f;
-        const float dc = ng > 0.f ? summary[NCF_SUM_DCG] / ng : 0.f;
-        if (stats) {
-            stats[NCF_STAT_LOSS_SUM] += (double)loss;
-            stats[NCF_STAT_HR_SUM] += (double)hr;
-            stats[NCF_STAT_DCG_SUM] += (double)dc;
-            stats[NCF_STAT_STEPS] += 1.0;
-            stats[NCF_STAT_LAST_LOSS] = loss;
-            stats[NCF_STAT_LAST_HR] = hr;
-            stats[NCF_STAT_LAST_DCG] = dc;
-            stats[NCF_STAT_BCE_SUM] += (double)(summary[NCF_SUM_BCE] * inv_batch);
-        }
-        if (bump) *step += 1;
-    }
-}
-
 // P-ahead rows.  The catch-up ahead (the next batch's stale rows, replayed in the touched-row
 // update launch) writes p only: the next step's update reads m and v anyway and re-derives their
 // missed zero-gradient decays (the moments do not depend on p), as it does after the per-step
@@ -182,6 +157,9 @@ constexpr int kRep = NCF_AHEAD_REP;
 #endif
 #ifndef NCF_COUNT_BLOCKS_MAX
 #define NCF_COUNT_BLOCKS_MAX 4096  // count (+ catch-up ahead) blocks of the touched-row update launch
+#endif
+#ifndef NCF_DIAG_UPD
+#define NCF_DIAG_UPD 0
 #endif
 #ifndef NCF_TOUCHED_MIN_BLOCKS
 #define NCF_TOUCHED_MIN_BLOCKS 7
@@ -983,6 +961,9 @@ __global__ __launch_bounds__(kBlock, UNSORTED ? NCF_TOUCHED_MIN_BLOCKS_UNSORTED 
         }
         return;
     }
+#if NCF_DIAG_UPD == 2  // diagnostic timing builds only (wrong numerics): no touched-row update
+    return;
+#endif
     const int ublk = b - ca.ncount;   // this block's index among the update blocks
     const RowLanes rl(w4);
     const int t = *step + 1;
@@ -1284,15 +1265,6 @@ struct SummaryArgs {
                                // bump; cleared here
 };
 
-// whole block 0 of a stats launch: true when the step was dropped (and the word is cleared)
-__device__ inline bool stats_dropped(int32_t* drop) {
-    if (!drop) return false;
-    const int d = *drop;
-    __syncthreads();
-    if (d && threadIdx.x == 0) *drop = 0;
-    return d != 0;
-}
-
 __global__ __launch_bounds__(kBlock) void k_slab_partial(const float* __restrict__ slabs, int P, int nslab, int per,
                                                          float* __restrict__ part, SummaryArgs sa) {
     if (sa.summary && blockIdx.x == gridDim.x - 1) {  // the extra column: the batch summary
@@ -1433,18 +1405,84 @@ __global__ __launch_bounds__(kBlock) void k_summary(const float* __restrict__ pa
                  red);
 }
 
+// Block 0 of a stats launch in one round trip: k_stats' work (the drop word, the batch summary when
+// sa.summary, the stats fold and the step bump) with every load issued before the first barrier and
+// the five block sums reduced together — the same per-thread orders and the same tree as
+// block_sum_256 per value, so the results are bitwise the earlier per-value block sums.  (Those chained a
+// load round trip and two barriers per value; this block was the stats launch's critical path.)
+__device__ inline void summary_stats_block(const SummaryArgs& sa, float* __restrict__ summary,
+                                           const float* __restrict__ reg_emb, int nreg_emb,
+                                           const float* __restrict__ reg_mlp, int nreg_mlp, float inv_batch,
+                                           double* __restrict__ stats, int32_t* step, int bump) {
+    __shared__ float red[5][4];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int dropped = sa.drop ? *sa.drop : 0;
+    float x[5] = {0.f, 0.f, 0.f, 0.f, 0.f};  // bce, hit, dcg, reg_emb, reg_mlp
+    if (sa.summary) {
+        for (int j = tid; j < sa.nbce; j += kBlock) x[0] += sa.part_bce[j];
+        for (int j = tid; j < sa.nmet; j += kBlock) x[1] += sa.part_hit[j];
+        for (int j = tid; j < sa.nmet; j += kBlock) x[2] += sa.part_dcg[j];
+    }
+    for (int j = tid; j < nreg_emb; j += kBlock) x[3] += reg_emb[j];
+    for (int j = tid; j < nreg_mlp; j += kBlock) x[4] += reg_mlp[j];
+    // thread 0's operands of the fold, in flight with the sums
+    double s[NCF_NUM_STATS];
+    float sb = 0.f, sh = 0.f, sd = 0.f, sg = sa.n_groups, sreg = 0.f;
+    if (tid == 0) {
+        if (stats)
+#pragma unroll
+            for (int k = 0; k < NCF_NUM_STATS; ++k) s[k] = stats[k];
+        if (!sa.summary) {
+            sb = summary[NCF_SUM_BCE], sh = summary[NCF_SUM_HIT], sd = summary[NCF_SUM_DCG];
+            sg = summary[NCF_SUM_GROUPS], sreg = summary[NCF_SUM_REG];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 5; ++k) x[k] = wave_sum(x[k]);
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < 5; ++k) red[k][w] = x[k];
+    __syncthreads();
+    if (tid != 0) return;
+    float r[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) r[k] = (red[k][0] + red[k][1]) + (red[k][2] + red[k][3]);
+    if (dropped) {  // the step was dropped (fill_wave): no summary, stats or bump; clear the word
+        *sa.drop = 0;
+        return;
+    }
+    if (sa.summary) {
+        sb = r[0], sh = r[1], sd = r[2];
+        sreg = 0.f + 0.f;  // summary_body's reg terms: empty sums
+        summary[NCF_SUM_BCE] = sb;
+        summary[NCF_SUM_HIT] = sh;
+        summary[NCF_SUM_DCG] = sd;
+        summary[NCF_SUM_GROUPS] = sg;
+        summary[NCF_SUM_REG] = sreg;
+#pragma unroll
+        for (int k = NCF_SUM_REG + 1; k < NCF_NUM_SUMMARY; ++k) summary[k] = 0.f;
+    }
+    const float loss = sb * inv_batch + sreg + (r[3] + r[4]);
+    const float hr = sg > 0.f ? sh / sg : 0.f;
+    const float dc = sg > 0.f ? sd / sg : 0.f;
+    if (stats) {
+        stats[NCF_STAT_LOSS_SUM] = s[NCF_STAT_LOSS_SUM] + (double)loss;
+        stats[NCF_STAT_HR_SUM] = s[NCF_STAT_HR_SUM] + (double)hr;
+        stats[NCF_STAT_DCG_SUM] = s[NCF_STAT_DCG_SUM] + (double)dc;
+        stats[NCF_STAT_STEPS] = s[NCF_STAT_STEPS] + 1.0;
+        stats[NCF_STAT_LAST_LOSS] = loss;
+        stats[NCF_STAT_LAST_HR] = hr;
+        stats[NCF_STAT_LAST_DCG] = dc;
+        stats[NCF_STAT_BCE_SUM] = s[NCF_STAT_BCE_SUM] + (double)(sb * inv_batch);
+    }
+    if (bump) *step += 1;
+}
+
 __global__ __launch_bounds__(kBlock) void k_stats(float* __restrict__ summary,
                                                   const float* __restrict__ reg_emb, int nreg_emb,
                                                   const float* __restrict__ reg_mlp, int nreg_mlp, float inv_batch,
                                                   double* __restrict__ stats, int32_t* step, int bump, SummaryArgs sa) {
-    __shared__ float red[4];
-    if (stats_dropped(sa.drop)) return;
-    if (sa.summary) {
-        summary_body(sa.part_bce, sa.nbce, sa.part_hit, sa.part_dcg, sa.nmet, sa.n_groups, nullptr, 0, nullptr, 0,
-                     summary, red);
-        __syncthreads();
-    }
-    stats_body(summary, reg_emb, nreg_emb, reg_mlp, nreg_mlp, inv_batch, stats, step, bump, red);
+    summary_stats_block(sa, summary, reg_emb, nreg_emb, reg_mlp, nreg_mlp, inv_batch, stats, step, bump);
 }
 
 // The in-kernel fill's body (FillArgs) as a launch of its own, before the forward/backward (a stale
@@ -1459,7 +1497,7 @@ __global__ __launch_bounds__(kBlock) void k_fill_ahead(FillArgs f, const int32_t
         fill_wave<2>(f, users, items, n, fold, gw - nr, (int)gridDim.x * (kBlock / 64) - nr);
 }
 
-hipError_t launch_fill_ahead(const FillArgs& f, const int32_t* users, const int32_t* items, int64_t n, int fold,
+hipError_t launch_fill_ahead(const FillArgs& f,const int32_t* users, const int32_t* items, int64_t n, int fold,
                              hipStream_t st) {
     if (f.nscan < 1 || f.nscan > kMaxFillScan || n < 1) return hipErrorInvalidValue;
     // one pass per wave where the grid allows (4 waves per block)
@@ -1490,14 +1528,7 @@ __global__ __launch_bounds__(kBlock) void k_stats_scan(float* __restrict__ summa
                                                        float inv_batch, double* __restrict__ stats, int32_t* step,
                                                        int bump, ScanAhead sc, SummaryArgs sa) {
     if (blockIdx.x == 0) {
-        __shared__ float red[4];
-        if (stats_dropped(sa.drop)) return;
-        if (sa.summary) {   // the batch summary first (launch_summary's work), then the stats
-            summary_body(sa.part_bce, sa.nbce, sa.part_hit, sa.part_dcg, sa.nmet, sa.n_groups, nullptr, 0, nullptr, 0,
-                         summary, red);
-            __syncthreads();
-        }
-        stats_body(summary, reg_emb, nreg_emb, reg_mlp, nreg_mlp, inv_batch, stats, step, bump, red);
+        summary_stats_block(sa, summary, reg_emb, nreg_emb, reg_mlp, nreg_mlp, inv_batch, stats, step, bump);
     } else {
         scan_local_body<true>(sc.cnt, sc.r1, sc.offs, sc.tot, sc.uloc, sc.utot, (int)blockIdx.x - 1, sc.cursor,
                               sc.heavy_n, sc.to);
@@ -1670,7 +1701,11 @@ hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, vo
                                      hipStream_t st, const int32_t* next_users, const int32_t* next_items,
                                      int64_t n_next, const MlpDeferred* mlp, int next_fold, const MetricsDeferred* met,
                                      const float* grad_rows, bool unsorted_lists) {
+#if NCF_DIAG_UPD == 1  // diagnostic timing builds only (wrong numerics): no catch-up ahead
+    const bool replay_ahead = false;
+#else
     const bool replay_ahead = next_users != nullptr && NCF_CATCHUP_AHEAD;
+#endif
     const uint32_t w4 = (uint32_t)(s.row_width / 4);
     const uint32_t n4 = (uint32_t)(lazy_bound(s, h) * w4);  // SGD: the rows under deferred decay
     const int32_t* offs = at<int32_t>(ws, L.offs);
