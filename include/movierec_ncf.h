@@ -190,9 +190,9 @@ int ncf_workspace_init(const ncf_shape_t* shape, int64_t max_batch, void* ws, si
  *   NCF_WSERR_STALE_COUNT  a batch passed with hyper->index_ready = 2 differed from the ids
  *                          ncf_train_step_ahead counted (their contents changed in between): the
  *                          index build wrote no slot outside its keys' ranges and cleared the
- *                          counters, and the step replayed the deferred decay of the rows it read
- *                          that the counted set missed (the table stays in the dense-sweep state),
- *                          but that step's embedding gradient is wrong.
+ *                          counters; with the in-kernel index (the single-table default) the step
+ *                          was dropped — nothing of it applied, the state a consistent deferred-
+ *                          decay state — otherwise that step's embedding gradient is wrong.
  *   NCF_WSERR_FOLD         an index built by an earlier call (ncf_build_index, ncf_shard_plan)
  *                          folds user rows differently than the step that used it (their hypers'
  *                          group / force_generic differ): that step's embedding gradient is wrong.
