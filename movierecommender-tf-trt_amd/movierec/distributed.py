@@ -39,6 +39,7 @@ The result equals a single-device step on the concatenated global batch (up
 to fp32 summation order of the cross-rank gradient sum).
 """
 
+import warnings
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -487,7 +488,13 @@ class UserPartitionedDataParallel(object):
         is padded to world * Ic item rows for the in-place all-gather.
 
         ``emulate_world`` (one-rank process group): rank 0's compute of a step of that many ranks
-        (its item slice only, no exchange) — the bench's per-rank diagnostic."""
+        (its item slice only, no exchange) — the bench's per-rank diagnostic.
+
+        Construction is a COLLECTIVE over ``group`` when the one-call step is considered at world
+        > 1: every rank must construct its instance together (the first construction per model
+        shape runs ``native_step_check``, 2 x 5 training steps with their collectives, and the
+        library communicator's rendezvous).  A failed check logs a warning and falls back to the
+        call-by-call step (``self.native_check`` holds its numbers)."""
         self.eng = engine
         self.group = group
         self.world = dist.get_world_size(group)
@@ -509,6 +516,10 @@ class UserPartitionedDataParallel(object):
                     _NATIVE_CHECKS[key] = native_step_check(engine.layers, engine.gmf_dim, 4, bool(split_items), group)
                 self.native_check = _NATIVE_CHECKS[key]
                 native = self.native_check["ok"]
+                if not native:
+                    warnings.warn("the one-call RCCL user step differs from the call-by-call step on this process "
+                                  "group (%r): falling back to the call-by-call step" % (self.native_check,),
+                                  RuntimeWarning, stacklevel=2)
         self.comm = _native_comm(self.rank, self.world, group) if native else None
         iw = self.world
         if emulate_world is not None and int(emulate_world) > 1:
