@@ -109,6 +109,10 @@ def parse():
                          "sampler (trainer params sampler='device'; world_size = --gpus); samples/s of the epochs")
     ap.add_argument("--dense-sweep", action="store_true",
                     help="sweep every embedding row every step instead of the deferred exact decay (same result)")
+    ap.add_argument("--id-span", type=float, default=1.0,
+                    help="diagnostic (single table): draw user ids from the first FRACTION of the user "
+                         "range only (row locality of the gather and the update, e.g. the TLB question "
+                         "on config D's 11 GB table); the line's config names it")
     ap.add_argument("--emulate-world", type=int, default=1,
                     help="--dp user at N=1 only: size the local table as rank 0 of this many ranks would "
                          "(per-rank compute of the N-GPU step without its all-reduce; a diagnostic, not a result)")
@@ -717,8 +721,10 @@ def main():
             pool.append((u.contiguous(), it.contiguous(),
                          torch.tensor([0.0] * (g - 1) + [1.0], device="cuda").repeat(B // g).contiguous()))
             continue
-        u = torch.randint(0, eng.num_users if mode == "user" else cfg["num_users"], (B // g,), generator=gen,
-                          device="cuda", dtype=torch.int32)
+        u_hi = eng.num_users if mode == "user" else cfg["num_users"]
+        if mode == "single" and args.id_span < 1.0:
+            u_hi = max(1, int(round(u_hi * args.id_span)))
+        u = torch.randint(0, u_hi, (B // g,), generator=gen, device="cuda", dtype=torch.int32)
         u = u.repeat_interleave(g)
         it = torch.randint(0, cfg["num_items"], (B,), generator=gen, device="cuda", dtype=torch.int32)
         y = torch.tensor([0.0] * (g - 1) + [1.0], device="cuda").repeat(B // g)
@@ -1074,7 +1080,7 @@ def main():
                      "synthetic (uniform ids, seeded; %d distinct batches cycled; random-init weights)" % len(pool)),
             "config": {"workload": cfg["workload"], "global_batch": B * world, "per_gpu_batch": B,
                        "negatives_per_positive": cfg["negs"], "parallelism": par,
-                       "kernel_path": kpath},
+                       "kernel_path": kpath, **({"id_span": args.id_span} if args.id_span < 1.0 else {})},
             "roofline": fb_roof if dominant_fb else emb_roof,
             "roofline_emb_update" if dominant_fb else "roofline_fwd_bwd": emb_roof if dominant_fb else fb_roof,
             # the north star's gather + scatter bandwidth over both kernels together: the
