@@ -35,6 +35,9 @@
 #include "ncf_common.h"
 #include "ncf_internal.h"
 
+#ifndef NCF_SCORE_OUT_DEFER
+#define NCF_SCORE_OUT_DEFER 1
+#endif
 #ifndef NCF_DIAG_SCORE
 #define NCF_DIAG_SCORE 0
 #endif
@@ -324,6 +327,12 @@ __global__ __launch_bounds__(kBlock, 2) void k_score_topk(ScoreArgs a) {
         sf32x16 acc2;
         NCF_SCORE_LAYER2(acc2)
         NCF_SCORE_USER_OPS(ui, un, 1)
+#if NCF_SCORE_OUT_DEFER
+        // the output MFMA of user q is consumed in iteration q + 1 (its latency hidden behind that
+        // iteration's work instead of an s_nop before the logit's add)
+        sf32x16 acc4p;
+        float ugp = 0.0f;
+#endif
 #pragma unroll
         for (int q = 0; q < 32; ++q) {
             float ugnn = 0.0f;
@@ -349,6 +358,16 @@ __global__ __launch_bounds__(kBlock, 2) void k_score_topk(ScoreArgs a) {
             f16x8 x3;
 #pragma unroll
             for (int e = 0; e < 8; ++e) x3[e] = e < NR3 ? (_Float16)acc3[e] : (_Float16)0.0f;
+#if NCF_SCORE_OUT_DEFER
+            if (q > 0) {
+                const float z = acc4p[0] + ugp;
+                s_z[w][q - 1][j] = z;
+                const float tq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(adm), q - 1));
+                flagged |= (__builtin_amdgcn_ballot_w64(z > tq) & okm) ? (1u << (q - 1)) : 0u;
+            }
+            acc4p = mfma16(AO, relu_f16(x3), sf32x16{});
+            ugp = ug;
+#else
 #if NCF_DIAG_SCORE == 7
             const float z = acc3[0] + ug;
 #else
@@ -360,6 +379,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_score_topk(ScoreArgs a) {
             s_z[w][q][j] = z;
             const float tq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(adm), q));
             flagged |= (__builtin_amdgcn_ballot_w64(z > tq) & okm) ? (1u << q) : 0u;
+#endif
             ug = ugn;
             ugn = ugnn;
             if (q + 2 < 32) {
@@ -370,6 +390,14 @@ __global__ __launch_bounds__(kBlock, 2) void k_score_topk(ScoreArgs a) {
             }
             __builtin_amdgcn_sched_barrier(0);
         }
+#if NCF_SCORE_OUT_DEFER
+        {   // the last user's logit
+            const float z = acc4p[0] + ugp;
+            s_z[w][31][j] = z;
+            const float tq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(adm), 31));
+            flagged |= (__builtin_amdgcn_ballot_w64(z > tq) & okm) ? (1u << 31) : 0u;
+        }
+#endif
 #undef NCF_SCORE_LAYER2
 #undef NCF_SCORE_USER_OPS
         // the next tile's item operands: loads in flight over the insertions below
