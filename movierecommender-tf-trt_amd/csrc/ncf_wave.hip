@@ -247,6 +247,9 @@ __device__ unsigned long long g_wave_s[256 * 4 * 16];
 // contraction, so barrier k + 1 also frees unit k's buffers for unit k + 2.  The chain's phases
 // that issue no MFMA now have the weight-gradient wave's 168 MFMAs per unit beside them on the
 // same SIMD.  Same MFMAs on the same operands in the same order as the one-wave form: bitwise.
+#ifndef NCF_PRIO_P0
+#define NCF_PRIO_P0 1
+#endif
 #ifndef NCF_SPLIT_PRIO
 #define NCF_SPLIT_PRIO 1
 #endif
@@ -528,6 +531,10 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
     if constexpr (SPLIT) {
         if (dwave && fa.cnt)
             fill_wave(fa, users, items, n, FOLD, (int)blockIdx.x * 4 + pw, (int)gridDim.x * 4);
+#if NCF_SPLIT_PRIO && NCF_PRIO_P0
+        // the chain waves' phase 0 and first unit ahead of their partners' fill in the SIMD's issue
+        if (!dwave) __builtin_amdgcn_s_setprio(1);
+#endif
     }
     // GU phase 0: P_u = W1_u^T x_u of every group of this chain wave's units, one 16-group tile per
     // FOLD units (k-step q takes user feature XH lq + q), into gpart
