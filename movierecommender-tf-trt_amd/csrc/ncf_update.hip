@@ -153,7 +153,8 @@ constexpr int kRep = NCF_AHEAD_REP;
 // occupancy floor of the touched-row update launch (its HBM-bound rows want many waves; the
 // catch-up-ahead blocks in the same launch must not raise its register count)
 #ifndef NCF_COUNT_PER_SMALL
-#define NCF_COUNT_PER_SMALL 16  // contributions per count block and pass below 32,768 contributions
+#define NCF_COUNT_PER_SMALL 32  // contributions per count block and pass below 32,768 contributions
+                                // (16 until round 5: 32 is 0.6-0.9 % faster at 8,192 and 4,095 samples, profiles/r05_cps)
 #endif
 #ifndef NCF_COUNT_BLOCKS_MAX
 #define NCF_COUNT_BLOCKS_MAX 4096  // count (+ catch-up ahead) blocks of the touched-row update launch
@@ -1715,8 +1716,8 @@ hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, vo
     if (h.optimizer == NCF_OPT_ADAM) {
         const unsigned nupd = row_grid(R < 2 * L.max_batch ? R : 2 * L.max_batch, w4, NCF_TOUCHED_GRID_MAX);
         const int64_t mc = next_users ? 2 * n_next : 0;
-        // count (+ catch-up ahead) blocks: 64 contributions per block and pass, 32 / 16 below 65,536
-        // / 32,768 contributions (at least ~1,000 blocks of replay chains)
+        // count (+ catch-up ahead) blocks: 64 contributions per block and pass, 32 below 65,536
+        // contributions (NCF_COUNT_PER_SMALL below 32,768)
         const int per = mc >= 65536 ? NCF_COUNT_PER_MAX : mc >= 32768 ? 32 : NCF_COUNT_PER_SMALL;
         const int64_t npass = (mc + per - 1) / per;
         const unsigned ncount = mc > 0 ? (unsigned)(npass < NCF_COUNT_BLOCKS_MAX ? npass : NCF_COUNT_BLOCKS_MAX) : 0u;
