@@ -585,6 +585,22 @@ def selftest_main(args, world, rank):
         dist.destroy_process_group()
 
 
+def _native_build_info():
+    from movierec import _native as N
+    info = N.build_info()
+    try:
+        import importlib.util
+        spec = importlib.util.spec_from_file_location(
+            "ncf_build", os.path.join(os.path.dirname(os.path.abspath(__file__)), "movierecommender-tf-trt_amd",
+                                      "csrc", "build.py"))
+        b = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(b)
+        info["matches_tree"] = info["src_sha256"] == b.source_hash()
+    except Exception as exc:  # the sources are always shipped with the tree; report rather than fail
+        info["matches_tree"] = "unknown (%s)" % exc
+    return info
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "RANK" not in os.environ:
@@ -1032,9 +1048,7 @@ def main():
                                       "wave (k_fb_wave, fp32 MFMA 16x16x4)",
                    "layered-mfma": "layer-by-layer forward+backward, every layer on hand-written fp32 MFMA "
                                    "(k_lay_l1f gather + layer 1, k_lay_mid layers 2.. + loss + backward to G1, "
-                                   "k_lay_dw1, k_lay_l1b dX + gradient rows)",
-                   "layered-rocblas": "layer-by-layer forward+backward (rocBLAS fp32 GEMMs + glue kernels, "
-                                      "ncf_layered.hip)"}.get(kpath, "generic forward+backward"),
+                                   "k_lay_dw1, k_lay_l1b dX + gradient rows)"}.get(kpath, "generic forward+backward"),
                "achieved": round(fb_achieved, 2), "peak": fb_peak, "unit": "TFLOP/s",
                "frac": round(fb_achieved / fb_peak, 4), "traffic": fb_traffic,
                "peak_of": "bf16 dense MFMA (the MLP products; GMF, loss and Adam stay fp32)" if prec == "bf16"
@@ -1107,6 +1121,9 @@ def main():
         }
         if exchange is not None:
             line["exchange"] = exchange
+        # provenance of the benched binary: the source hash compiled into it and its -D defines
+        # (empty for the product build; csrc/build.py rebuilds whenever the tree's hash differs)
+        line["build_info"] = _native_build_info()
         if args.emulate_world > 1 and mode == "sharded":
             line["emulated_world"] = args.emulate_world
             line["note"] = ("diagnostic: rank 0's per-rank compute of the %d-rank row-sharded step on one GPU (a "

@@ -23,9 +23,9 @@
  *    attributes (set on first launch of each kernel variant), the NCF_* tuning knobs read from
  *    the environment on first use (NCF_SIDE_STREAM, NCF_FB_KERNEL, NCF_FOLD_USERS,
  *    NCF_UNIT_SCHED; experiments only), and the side streams of NCF_SIDE_STREAM (one per
- *    device, mutex-guarded).  Thread-local: the error text, the profiling events, the
- *    layered path's rocBLAS handle.  Calls on different workspaces may run concurrently from
- *    different threads.
+ *    device, mutex-guarded).  Thread-local: the error text, the profiling events.  Calls on
+ *    different workspaces may run concurrently from different threads.
+ *  - Every kernel is hand-written HIP for gfx950; the library links no vendor BLAS.
  *
  * Device data layout (DESIGN.md §Data layout)
  *  - One combined embedding table `emb`: rows [0, num_users) are users, rows
@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define NCF_ABI_VERSION 10
+#define NCF_ABI_VERSION 11
 #define NCF_MAX_LAYERS 8
 #define NCF_EINVAL (-1)
 #define NCF_EHIP (-2)
@@ -133,9 +133,9 @@ typedef struct ncf_hyper {
     int32_t k;                          /* top-k of the hr/dcg metrics */
     float inv_batch;                    /* 1 / (global batch) for the BCE mean */
     int32_t force_generic;              /* 1: the generic per-sample kernel even if fast_path;
-                                           2: the layer-by-layer GEMM path (default for shapes the
-                                           fused kernel does not hold whose dense weights exceed
-                                           12288 floats, e.g. config D);
+                                           2: the layer-by-layer MFMA path where the shape has it
+                                           (config D's widths; the default there), else the
+                                           generic kernel;
                                            3 / 4 / 5: (fast_path shapes) the 128-sample tile
                                            kernel / the sample-unit kernel (the default) / the
                                            wave-chain kernel (fp32 operands; else the unit one);
@@ -164,13 +164,19 @@ int ncf_abi_version(void);
 
 /* The forward/backward kernel a training call with n samples runs (for reporting). */
 #define NCF_FB_GENERIC 0
-#define NCF_FB_LAYERED 1
+#define NCF_FB_LAYERED 1        /* retired in ABI 11 (the rocBLAS layered path): never returned */
 #define NCF_FB_TILE 2
 #define NCF_FB_UNIT 3
 #define NCF_FB_WAVE 4
 #define NCF_FB_LAYERED_MFMA 5   /* the layer-by-layer path with every layer on hand-written MFMA (config D) */
 int ncf_fb_kernel(const ncf_shape_t* shape, const ncf_hyper_t* hyper, int64_t n);
 const char* ncf_last_error(void);
+
+/* Provenance of the loaded library (ABI 11): a JSON object with the SHA-256 of the sources it was
+ * compiled from (every .hip and .h source of csrc/ and this header, in name order, plus the
+ * compiler flags), the -D defines of the build ("" for the product build), the offload arch and the ABI
+ * version.  build.py recompiles whenever the hash of the tree differs from the one embedded. */
+const char* ncf_build_info(void);
 
 /* Validate the model dimensions and fill the derived fields.
  * Replaces the shape checks of MovierecModel.__init__ (model.py:73-80).  num_layers == 0 with
@@ -191,8 +197,10 @@ int ncf_workspace_init(const ncf_shape_t* shape, int64_t max_batch, void* ws, si
  *                          ncf_train_step_ahead counted (their contents changed in between): the
  *                          index build wrote no slot outside its keys' ranges and cleared the
  *                          counters; with the in-kernel index (the single-table default) the step
- *                          was dropped — nothing of it applied, the state a consistent deferred-
- *                          decay state — otherwise that step's embedding gradient is wrong.
+ *                          was dropped — whether a changed id overflowed a counted row or left one
+ *                          short (the fill compares the contributions it placed with the counted
+ *                          total) — nothing of it applied, the state a consistent deferred-decay
+ *                          state; otherwise that step's embedding gradient is wrong.
  *   NCF_WSERR_FOLD         an index built by an earlier call (ncf_build_index, ncf_shard_plan)
  *                          folds user rows differently than the step that used it (their hypers'
  *                          group / force_generic differ): that step's embedding gradient is wrong.

@@ -5,6 +5,7 @@ to the GPU box.  Usage: ``python csrc/build.py [--force]``.
 """
 
 import concurrent.futures as cf
+import hashlib
 import os
 import subprocess
 import sys
@@ -25,18 +26,53 @@ CFLAGS = ["--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17", "-I" + INCLUDE
           "-Wno-unused-result"]
 
 
-def _deps_mtime():
-    files = [os.path.join(HERE, f) for f in os.listdir(HERE) if f.endswith((".hip", ".h"))]
-    files.append(os.path.join(INCLUDE, "movierec_ncf.h"))
-    return max(os.path.getmtime(f) for f in files)
+HASH_MARK = b"NCF_SRC_SHA256="
+
+
+def source_hash(defines=()):
+    """SHA-256 of what the library is compiled from: every csrc .hip/.h source and the ABI header
+    (name order, name + content), the compiler flags and the -D defines.  Embedded in the binary
+    (ncf_build_info) so a library can be matched to the tree it came from."""
+    files = sorted(f for f in os.listdir(HERE) if f.endswith((".hip", ".h")))
+    h = hashlib.sha256()
+    for f in files:
+        h.update(f.encode() + b"\0")
+        with open(os.path.join(HERE, f), "rb") as fh:
+            h.update(fh.read())
+    with open(os.path.join(INCLUDE, "movierec_ncf.h"), "rb") as fh:
+        h.update(b"movierec_ncf.h\0" + fh.read())
+    h.update(repr(([f for f in CFLAGS if not f.startswith("-I")], sorted(EXTRA.items()), list(defines), _env_extras())).encode())
+    return h.hexdigest()
+
+
+def _env_extras():
+    """NCF_EXTRA_<SOURCE STEM> compiler flags in the environment (experiment variants)."""
+    return sorted((k, v) for k, v in os.environ.items() if k.startswith("NCF_EXTRA_") and v.strip())
+
+
+def embedded_hash(lib_path):
+    """The source hash a built library carries (None if absent or unreadable)."""
+    try:
+        with open(lib_path, "rb") as fh:
+            data = fh.read()
+    except OSError:
+        return None
+    i = data.find(HASH_MARK)
+    if i < 0:
+        return None
+    return data[i + len(HASH_MARK):i + len(HASH_MARK) + 64].decode("ascii", "replace")
 
 
 def build(force=False, verbose=False, defines=(), out=None):
-    """Compile and link; ``defines``/``out`` build an experiment variant elsewhere."""
+    """Compile and link; ``defines``/``out`` build an experiment variant elsewhere.  An existing
+    library is reused only when its embedded source hash equals the tree's (no mtime trust)."""
     lib_path = out or LIB
     os.makedirs(os.path.dirname(lib_path), exist_ok=True)
-    if not force and os.path.exists(lib_path) and os.path.getmtime(lib_path) >= _deps_mtime():
+    want = source_hash(defines)
+    if not force and embedded_hash(lib_path) == want:
         return lib_path
+    variant = " ".join(["-D" + d for d in defines] + ["%s=%s" % kv for kv in _env_extras()])
+    info = ["-DNCF_BUILD_HASH=\"%s\"" % want, "-DNCF_BUILD_DEFINES=\"%s\"" % variant.replace('"', "'")]
     obj_dir = os.path.join(os.path.dirname(lib_path), "obj" + ("_" + os.path.basename(lib_path) if out else ""))
     os.makedirs(obj_dir, exist_ok=True)
 
@@ -45,7 +81,7 @@ def build(force=False, verbose=False, defines=(), out=None):
         # NCF_EXTRA_<SOURCE STEM>: extra compiler flags of one source (experiment variants)
         env_extra = os.environ.get("NCF_EXTRA_" + src.replace(".hip", "").upper(), "").split()
         cmd = ([HIPCC] + CFLAGS + EXTRA.get(src, []) + env_extra + ["-D" + d for d in defines] +
-               ["-c", os.path.join(HERE, src), "-o", obj])
+               (info if src == "ncf_capi.hip" else []) + ["-c", os.path.join(HERE, src), "-o", obj])
         if verbose:
             print(" ".join(cmd))
         r = subprocess.run(cmd, capture_output=True, text=True)
@@ -56,10 +92,9 @@ def build(force=False, verbose=False, defines=(), out=None):
     with cf.ThreadPoolExecutor(max_workers=min(8, len(SOURCES))) as ex:
         objs = list(ex.map(compile_one, SOURCES))
     tmp = lib_path + ".tmp"
-    # rocBLAS (plain fp32 GEMMs of the layered path): same soname as the copy torch loads, so one
-    # rocBLAS serves the process
-    # RCCL (the data-parallel step's all-reduce, ncf_comm.hip): librccl.so.1, the soname torch loads too
-    cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-o", tmp] + objs + ["-L/opt/rocm/lib", "-lrocblas", "-lrccl"]
+    # RCCL (the data-parallel step's collectives, ncf_comm.hip): librccl.so.1, the soname torch loads
+    # too.  No vendor BLAS: every matrix product is a hand-written MFMA kernel.
+    cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-o", tmp] + objs + ["-L/opt/rocm/lib", "-lrccl"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError("link failed:\n%s\n%s" % (r.stdout, r.stderr))

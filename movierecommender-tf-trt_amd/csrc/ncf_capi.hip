@@ -170,6 +170,9 @@ bool use_fused(const ncf_shape_t& s, const ncf_hyper_t* h) {
     return s.fast_path && !(h && (h->force_generic == 1 || h->force_generic == 2)) && ncf::fused_supported(s);
 }
 
+// the layered kernels hold config D's widths only (ncf_layered.hip); any other shape whose weights
+// outgrow the fused kernels — or asked for the layered path (force_generic == 2) — runs the
+// generic per-sample kernel: no vendor-GEMM path exists
 bool use_layered(const ncf_shape_t& s, const ncf_hyper_t* h) {
     if (!ncf::layered_supported(s)) return false;
     if (h && h->force_generic == 2) return true;
@@ -255,7 +258,7 @@ WsLayout make_layout(const ncf_shape_t& s, int64_t B, int world) {
     L.heavy_n = take(4);
     L.err = take(4);
     L.ifold = take(4);
-    L.stale_step = take(4);
+    L.stale_step = take(8);  // int32[2] (FillArgs::stale_step)
     const int64_t S = L.shard_rows;
     if (world > 0) {
         L.ocnt = take((size_t)(S + 1) * 4);
@@ -393,11 +396,26 @@ extern "C" {
 
 int ncf_abi_version(void) { return NCF_ABI_VERSION; }
 
+// Provenance (csrc/build.py passes the tree's source hash and the build's -D defines; a build by
+// other means reports "unknown").  The marker string lets build.py read the hash from the file.
+#ifndef NCF_BUILD_HASH
+#define NCF_BUILD_HASH "unknown"
+#endif
+#ifndef NCF_BUILD_DEFINES
+#define NCF_BUILD_DEFINES ""
+#endif
+#define NCF_STR2(x) #x
+#define NCF_STR(x) NCF_STR2(x)
+__attribute__((used)) static const char kNcfHashMark[] = "NCF_SRC_SHA256=" NCF_BUILD_HASH;
+static const char kNcfBuildInfo[] = "{\"src_sha256\": \"" NCF_BUILD_HASH "\", \"defines\": \"" NCF_BUILD_DEFINES
+                                    "\", \"arch\": \"gfx950\", \"abi\": " NCF_STR(NCF_ABI_VERSION) "}";
+
+const char* ncf_build_info(void) { return kNcfBuildInfo + 0 * sizeof(kNcfHashMark); }
+
 int ncf_fb_kernel(const ncf_shape_t* s, const ncf_hyper_t* h, int64_t n) {
     if (int r = check_shape(s)) return r;
     if (use_fused(*s, h)) return fb_variant(*s, h, n);
-    if (!use_layered(*s, h)) return NCF_FB_GENERIC;
-    return ncf::layered_all_mfma(*s) ? NCF_FB_LAYERED_MFMA : NCF_FB_LAYERED;
+    return use_layered(*s, h) ? NCF_FB_LAYERED_MFMA : NCF_FB_GENERIC;
 }
 
 const char* ncf_last_error(void) { return g_err.c_str(); }

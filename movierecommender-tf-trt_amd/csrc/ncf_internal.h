@@ -71,7 +71,7 @@ struct WsLayout {
     size_t uloc;      // int32[K+1]  per-2048-key local exclusive scan of (cnt > 0)
     size_t utot;      // int32[nscan]
     size_t ifold;     // int32       user-row folding of the last index build (persistent)
-    size_t stale_step;// int32      persistent: nonzero while the current step is dropped (fill_wave)
+    size_t stale_step;// int32[2]   persistent: nonzero while the current step is dropped (fill_wave)
     size_t cid_u;     // int32[B]    compact (unique-row) id of each sample's user row
     size_t cid_i;     // int32[B]    compact id of each sample's item row
     size_t uoffs;     // int32[2B+1] compact row -> first list slot
@@ -426,7 +426,8 @@ struct FillArgs {
     int32_t* ifold;
     int32_t U, I;             // user u -> key u, item v -> key U + v
     int64_t list_cap, touched_cap, heavy_cap;  // region sizes (debug bound checks)
-    int32_t* stale_step;      // set when a contribution finds no slot: the step is dropped (below)
+    int32_t* stale_step;      // int32[2]: [0] set when a contribution finds no slot, [1] contributions
+                              // placed minus contributions counted; either nonzero drops the step (below)
 };
 #if NCF_DEBUG_BOUNDS == 1
 #define NCF_BOUND(cond, ...)          \
@@ -454,13 +455,21 @@ constexpr int kFillContribPerLane = 2;  // its CU: contributions per lane and pa
 // read rows the counted set missed, at their deferred step.  Such a step is DROPPED — f.stale_step
 // tells the touched-row update and the stats launch to apply nothing of it (the table, moments,
 // dense layers, stats and step counter stay as they were: a consistent deferred-decay state) —
-// and reported (NCF_WSERR_STALE_COUNT, RuntimeError from check_errors).
+// and reported (NCF_WSERR_STALE_COUNT, RuntimeError from check_errors).  Changed ids need not
+// overflow a slot: fewer valid, unfolded contributions than were counted leave list slots
+// unfilled (residues at counted keys) with nothing overflowing.  So every wave also adds the
+// contributions it placed to stale_step[1] (one atomic per wave) and the rows part's wave 0
+// subtracts the scanned total: the word is 0 exactly when every counted slot was filled.
 template <int PART = 3>
+__device__ inline void fill_wave(const FillArgs& f, const int32_t* __restrict__ users,
+                                 const int32_t* __restrict__ items, int64_t n, int fold, int gw, int nw);
+template <int PART>
 __device__ inline void fill_wave(const FillArgs& f, const int32_t* __restrict__ users,
                                  const int32_t* __restrict__ items, int64_t n, int fold, int gw, int nw) {
     const int lane = threadIdx.x & 63;
     int p0, p1, q0, q1;  // pre[lane], pre[lane + 64], upre[lane], upre[lane + 64]
     int u0, u1, ntouched;  // utot[lane], utot[lane + 64], their sum
+    int counted;           // the scan blocks' total: the contributions counted ahead
     {
         const int t0 = lane < f.nscan ? f.tot[lane] : 0, t1 = lane + 64 < f.nscan ? f.tot[lane + 64] : 0;
         u0 = lane < f.nscan ? f.utot[lane] : 0;
@@ -478,6 +487,7 @@ __device__ inline void fill_wave(const FillArgs& f, const int32_t* __restrict__ 
         q0 = b0 - u0;
         q1 = cb + b1 - u1;
         ntouched = cb + __shfl(b1, 63, 64);
+        counted = ca + __shfl(a1, 63, 64);
 #if NCF_DEBUG_BOUNDS == 1
         if (gw == 0 && lane < 4 && lane < f.nscan)
             printf("fill lane %d: tot %d utot %d pre %d upre %d nscan %d\n", lane, t0, u0, p0, q0, f.nscan);
@@ -528,8 +538,10 @@ __device__ inline void fill_wave(const FillArgs& f, const int32_t* __restrict__ 
         if (gw == 0 && lane == 0) {
             *f.nuniq = ntouched;
             *f.ifold = fold;
+            if (counted != 0) atomicSub(&f.stale_step[1], counted);
         }
     }
+    int placed = 0;  // this wave's placed contributions (lane 0's count)
     // contributions c = 2i + side, a wave at a time (k_fill's runs: equal keys two lanes apart share
     // one atomic; slot order inside a key is free, the update sorts)
     const int64_t m = 2 * n;
@@ -587,12 +599,14 @@ __device__ inline void fill_wave(const FillArgs& f, const int32_t* __restrict__ 
                           (long long)c, key, (long long)li, (long long)f.list_cap)
                 f.list[li] = (int)c;
             }
+            placed += __popcll(__ballot(ok && slot >= 0));
             if (ok && slot < 0) {
                 atomicOr(f.err, kErrStaleCount);
-                atomicOr(f.stale_step, 1);
+                atomicOr(&f.stale_step[0], 1);
             }
         }
     }
+    if ((PART & 2) && lane == 0 && placed != 0) atomicAdd(&f.stale_step[1], placed);
 }
 
 // ncf_user_dp_step's helpers (ncf_capi.hip)
@@ -730,12 +744,11 @@ bool unit_fill_fits(const ncf_shape_t& s, int64_t n, bool bf16, int64_t r1);
 hipError_t launch_fwd_fused(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, const float* mlp,
                             const int32_t* users, const int32_t* items, const float* labels, int64_t n,
                             float* probs, IdSpace ids, int* nbce, hipStream_t st);
-// layer-by-layer path (ncf_layered.hip): rocBLAS fp32 GEMMs + HBM-bound glue kernels, same
-// outputs as launch_fb_generic (probs, gs, part_bce, one slab)
+// layer-by-layer path (ncf_layered.hip): hand-written fp32 MFMA kernels (k_lay_l1f, k_lay_mid,
+// k_lay_dw1, k_lay_l1b) for the shapes they hold (config D's widths); same outputs as
+// launch_fb_generic (probs, gs, part_bce, slabs).  Other shapes run the generic kernel.
 bool layered_supported(const ncf_shape_t& s);
-// every layer of the layered path on hand-written MFMA (k_lay_l1f, k_lay_mid, k_lay_dw1, k_lay_l1b):
-// no vendor GEMM on the step
-bool layered_all_mfma(const ncf_shape_t& s);
+bool layered_all_mfma(const ncf_shape_t& s);  // == layered_supported (no vendor-GEMM variant remains)
 hipError_t launch_fb_layered(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, const float* mlp,
                              const int32_t* users, const int32_t* items, const float* labels, int64_t n,
                              float inv_batch, IdSpace ids, int* nslab, int* nbce, hipStream_t st);

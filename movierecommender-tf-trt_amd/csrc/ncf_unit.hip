@@ -443,8 +443,10 @@ __global__ __launch_bounds__(S::NT, 1) void k_fb_unit(const float* __restrict__ 
         }
     };
     // units of group gq: u0 + r * ustride; every group runs the workgroup's round count (the
-    // barriers are shared), a group past the end works on masked samples and adds nothing
-    const int64_t u0 = (int64_t)blockIdx.x * S::NG + gq, ustride = (int64_t)gridDim.x * S::NG;
+    // barriers are shared), a group past the end works on masked samples and adds nothing.  The
+    // stride is the UNIT grid's (nunit_blocks), not gridDim.x: the fill workgroups appended past
+    // it take no units, and counting them would skip units [grid, grid + nfill) of every round.
+    const int64_t u0 = (int64_t)blockIdx.x * S::NG + gq, ustride = (int64_t)nunit_blocks * S::NG;
     const int64_t first = (int64_t)blockIdx.x * S::NG;
     const int64_t rounds = nunits > first ? (nunits - first + ustride - 1) / ustride : 0;
     // Prologue.  The first unit's ids, then every dense parameter (one b128 buffer load per 4

@@ -745,7 +745,7 @@ __global__ __launch_bounds__(kBlock, UNSORTED ? NCF_TOUCHED_MIN_BLOCKS_UNSORTED 
     // everything else)
     int b = (int)blockIdx.x;
     // a dropped step (stale counted set, unsorted lists only): nothing of it is applied
-    const bool dropped = UNSORTED && so.drop && *so.drop != 0;
+    const bool dropped = UNSORTED && so.drop && (so.drop[0] | so.drop[1]) != 0;
     if (UNSORTED && b < so.nheavy) {
         if (dropped) return;
         // heavy rows (lists longer than so.hc, unsorted): one per block and pass
@@ -953,12 +953,49 @@ __global__ __launch_bounds__(kBlock, UNSORTED ? NCF_TOUCHED_MIN_BLOCKS_UNSORTED 
         return;
     }
     if (dropped) {
-        // nothing of the step is applied; the fill's leftover cursors (entries counted but absent:
-        // every counted key is a touched row) go back to zero for the next index
+        // Nothing of the step is applied; the fill's leftover cursors (entries counted but absent:
+        // every counted key is a touched row) go back to zero for the next index.  The counted rows
+        // the previous launch caught up ahead are P-ahead (p at *step, m and v owed from s0): with
+        // the step gone, a row that the next batch does not touch would keep that mark past the
+        // next bump, its p a step behind what the mark promises.  Settle them here — m and v
+        // decayed to *step (the per-step decay's arithmetic, as the stale gate does), row_step =
+        // *step — so that row_step again tells the step of all three.  (This launch's count blocks
+        // never claim a negative or current mark, so nothing else writes these rows.)
         const int64_t nt = *nlist;
-        for (int64_t i = (int64_t)(b - ca.ncount) * kBlock + threadIdx.x; i < nt; i += (int64_t)ca.nupd * kBlock) {
-            const int r = list[i];
-            if (so.cursor[r] != 0) so.cursor[r] = 0;
+        const int tdrop = *step;
+        const int lane = threadIdx.x & 63;
+        const int W = 4 * (int)w4;
+        float* mf = reinterpret_cast<float*>(m4);
+        float* vf = reinterpret_cast<float*>(v4);
+        const int64_t wave = ((int64_t)(b - ca.ncount) * kBlock + threadIdx.x) >> 6;
+        const int64_t nw = ((int64_t)ca.nupd * kBlock) >> 6;
+        for (int64_t i0 = wave * 64; i0 < nt; i0 += nw * 64) {  // wave-uniform
+            const int64_t i = i0 + lane;
+            const int r = i < nt ? list[i] : -1;
+            int rs = 0;
+            if (r >= 0) {
+                if (so.cursor[r] != 0) {
+                    atomicOr(so.err, kErrStaleCount);
+                    so.cursor[r] = 0;
+                }
+                if (r < ca.lazy_rows) rs = row_step[r];
+            }
+            uint64_t pm = __ballot(rs < 0);
+            while (pm) {
+                const int src = __ffsll((unsigned long long)pm) - 1;
+                pm &= pm - 1;
+                const int64_t rr = __shfl(r, src, 64);
+                const int s0 = pahead_s0(__shfl(rs, src, 64));
+                for (int q = lane; 2 * q < W; q += 64) {
+                    const size_t e = (size_t)rr * W + 2 * q;
+                    f32x2 m = *reinterpret_cast<const f32x2*>(mf + e);
+                    f32x2 v = *reinterpret_cast<const f32x2*>(vf + e);
+                    for (int st = s0 + 1; st <= tdrop; ++st) decay2(m, v, b1, b2);
+                    *reinterpret_cast<f32x2*>(mf + e) = m;
+                    *reinterpret_cast<f32x2*>(vf + e) = v;
+                }
+                if (lane == 0) row_step[rr] = tdrop;
+            }
         }
         return;
     }
@@ -1417,7 +1454,7 @@ __device__ inline void summary_stats_block(const SummaryArgs& sa, float* __restr
                                            double* __restrict__ stats, int32_t* step, int bump) {
     __shared__ float red[5][4];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int dropped = sa.drop ? *sa.drop : 0;
+    const int dropped = sa.drop ? (sa.drop[0] | sa.drop[1]) : 0;
     float x[5] = {0.f, 0.f, 0.f, 0.f, 0.f};  // bce, hit, dcg, reg_emb, reg_mlp
     if (sa.summary) {
         for (int j = tid; j < sa.nbce; j += kBlock) x[0] += sa.part_bce[j];
@@ -1448,8 +1485,9 @@ __device__ inline void summary_stats_block(const SummaryArgs& sa, float* __restr
     float r[5];
 #pragma unroll
     for (int k = 0; k < 5; ++k) r[k] = (red[k][0] + red[k][1]) + (red[k][2] + red[k][3]);
-    if (dropped) {  // the step was dropped (fill_wave): no summary, stats or bump; clear the word
-        *sa.drop = 0;
+    if (dropped) {  // the step was dropped (fill_wave): no summary, stats or bump; clear the words
+        sa.drop[0] = 0;
+        sa.drop[1] = 0;
         return;
     }
     if (sa.summary) {

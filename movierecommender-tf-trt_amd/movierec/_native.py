@@ -24,7 +24,7 @@ NCF_NUM_STATS = 8
 NCF_NUM_SUMMARY = 8
 NCF_WSERR_ID_RANGE, NCF_WSERR_STALE_COUNT, NCF_WSERR_FOLD = 1, 4, 8
 NCF_ROW_PRISTINE = 0x7fffffff   # row_step mark of a row whose Adam moments are exactly +0
-FB_KERNELS = {0: "generic", 1: "layered-rocblas", 2: "fused-mfma-tile", 3: "fused-mfma-unit", 4: "fused-mfma-wave",
+FB_KERNELS = {0: "generic", 2: "fused-mfma-tile", 3: "fused-mfma-unit", 4: "fused-mfma-wave",
               5: "layered-mfma"}
 SUM_BCE, SUM_HIT, SUM_DCG, SUM_GROUPS, SUM_REG = range(5)
 STAT_LOSS_SUM, STAT_HR_SUM, STAT_DCG_SUM, STAT_STEPS, STAT_LAST_LOSS, STAT_LAST_HR, STAT_LAST_DCG, STAT_BCE_SUM = \
@@ -71,6 +71,7 @@ _P = ctypes.POINTER
 _SIGNATURES = {
     "ncf_abi_version": (ctypes.c_int, []),
     "ncf_last_error": (ctypes.c_char_p, []),
+    "ncf_build_info": (ctypes.c_char_p, []),
     "ncf_shape_init": (ctypes.c_int, [_P(NcfShape), _i32, _i32, _P(_i32), _i32, _i32]),
     "ncf_workspace_size": (ctypes.c_int, [_P(NcfShape), _i64, _P(ctypes.c_size_t)]),
     "ncf_workspace_init": (ctypes.c_int, [_P(NcfShape), _i64, _vp, ctypes.c_size_t, _vp]),
@@ -174,7 +175,7 @@ def profile_read(kernel):
     return ms.value, n.value
 
 _lib = None
-ABI_VERSION = 10  # include/movierec_ncf.h ncf_abi_version()
+ABI_VERSION = 11  # include/movierec_ncf.h ncf_abi_version()
 
 
 def lib():
@@ -195,6 +196,12 @@ def lib():
                                "(__graft_entry__.build())" % (LIB_PATH, got, ABI_VERSION))
         _lib = handle
     return _lib
+
+
+def build_info():
+    """The loaded library's provenance (ncf_build_info): source SHA-256, -D defines, arch, ABI."""
+    import json
+    return json.loads(lib().ncf_build_info().decode("utf-8", "replace"))
 
 
 def check_value(rc):

@@ -57,19 +57,25 @@ def _batch(U, I, B, seed, hot_items=3, hot_frac=0.05, mixed_frac=0.1):
             (users.astype(np.int32), items.astype(np.int32), y.astype(np.float32))]
 
 
-@pytest.mark.parametrize("B", [16384, 20480, 4096])
-def test_in_kernel_index_bitwise_dense_sweep(B):
+@pytest.mark.parametrize("B,prec", [(16384, "fp32"), (20480, "fp32"), (4096, "fp32"), (12288, "fp32"),
+                                    (12288, "bf16"), (4096, "bf16")])
+def test_in_kernel_index_bitwise_dense_sweep(B, prec):
+    """12,288 samples: the unit kernel (fp32 below 16,384, bf16 at every size) needs 384 unit
+    workgroups, so its grid is clamped to 256 and every workgroup runs two rounds while fill
+    workgroups sit past the unit grid — the units' stride must be the unit grid's, not gridDim's
+    (units [256, 256 + nfill) of each round were skipped)."""
     U, I = 3000, 2000
     shape = O.NCFShape(U, I, LAYERS, GMF)
     w = _weights(shape, 5)
     engines = {}
     for name, kw in (("dense", {}), ("lazy", dict(lazy_adam=True)), ("ahead", dict(lazy_adam=True))):
-        e = NCFEngine(U, I, LAYERS, GMF, max_batch=B, **kw)
+        e = NCFEngine(U, I, LAYERS, GMF, max_batch=B, precision=prec, **kw)
         e.set_keras_weights(w)
         engines[name] = e
-    # 16,384 and up: the wave kernel's weight-gradient waves fill; 4,096: the unit kernel's grid leaves
-    # CUs idle and spare workgroups of its launch fill
-    assert engines["ahead"].kernel_for(B) == ("fused-mfma-wave" if B >= 16384 else "fused-mfma-unit")
+    # 16,384 and up: the wave kernel's weight-gradient waves fill; below (and bf16): the unit kernel's
+    # grid leaves CUs idle and spare workgroups of its launch fill
+    assert engines["ahead"].kernel_for(B) == ("fused-mfma-wave" if B >= 16384 and prec == "fp32"
+                                              else "fused-mfma-unit")
     batches = [_batch(U, I, B, 40 + s) for s in range(6)]
     for s, (u, it, y) in enumerate(batches):
         nxt = (batches[s + 1][0], batches[s + 1][1]) if s + 1 < len(batches) else None
@@ -159,16 +165,33 @@ def test_in_kernel_index_flags_stale_and_range():
     assert N.NCF_ROW_PRISTINE > 0
 
 
-@pytest.mark.parametrize("B", [16384, 1024])
-def test_stale_counted_step_is_dropped(B):
+def _short_count(users):
+    """Ids changed so that fewer contributions are valid than were counted, with no counted row
+    overflowing: the mixed groups' users set to their group head's, so those samples' user rows fold
+    into the head's (no contribution of their own) while no key gains one — counted slots are left
+    unfilled and nothing overflows (such a step was applied, not dropped)."""
+    u = users.cpu().numpy().reshape(-1, GROUP).copy()
+    mixed = (u != u[:, :1]).any(axis=1)
+    assert mixed.any()
+    u[mixed] = u[mixed, :1]
+    return torch.from_numpy(u.reshape(-1)).cuda()
+
+
+@pytest.mark.parametrize("B,mode", [(16384, "moved"), (1024, "moved"), (16384, "short"), (4096, "short")])
+def test_stale_counted_step_is_dropped(B, mode):
     """A counted batch whose ids change behind torch's back is dropped by the in-kernel fill
-    (the wave kernel's at 16,384 samples, the fill launch's at 1,024): nothing of the step is
-    applied — bitwise the engine that never ran it (same counted-ahead history, final flush) —
-    the error is raised, and the next counted steps train normally."""
+    (the wave kernel's at 16,384 samples, the unit launch's fill workgroups at 4,096, the fill
+    launch's at 1,024) — whether the change overflows a counted row ("moved") or only leaves counted
+    slots unfilled ("short"): nothing of the step is applied — bitwise the engine that never ran it
+    (same counted-ahead history, final flush) — the error is raised, and the next counted steps train
+    normally.  The dropped step counts the next batch ahead itself, and two counted steps run before
+    any flush: the counted rows the previous step caught up ahead (P-ahead: p current, m and v owed)
+    must be settled by the dropped launch, or a row absent from the next batch keeps its mark past
+    the next bump."""
     U, I = 3000, 2000
     shape = O.NCFShape(U, I, LAYERS, GMF)
     w = _weights(shape, 13)
-    bt = [_batch(U, I, B, 90 + s) for s in range(5)]
+    bt = [_batch(U, I, B, 90 + s) for s in range(6)]
     engines = []
     for stale in (True, False):
         e = NCFEngine(U, I, LAYERS, GMF, max_batch=B, lazy_adam=True)
@@ -177,10 +200,17 @@ def test_stale_counted_step_is_dropped(B):
         stage = (bt[1][0].clone(), bt[1][1].clone())
         e.train_step(*bt[0], group=GROUP, k=2, next_batch=stage)
         if stale:
-            stage[1].data.copy_(bt[2][1])                 # behind torch's back
-            e.train_step(stage[0], stage[1], bt[1][2], group=GROUP, k=2)
+            if mode == "moved":
+                stage[1].data.copy_(bt[2][1])             # behind torch's back
+            else:
+                stage[0].data.copy_(_short_count(stage[0]))
+            e.train_step(stage[0], stage[1], bt[1][2], group=GROUP, k=2, next_batch=(bt[3][0], bt[3][1]))
             with pytest.raises(RuntimeError):
                 e.check_errors()
+        # two counted steps before any flush (the twin gives up its counted batch here: flushed)
+        e.train_step(*bt[3], group=GROUP, k=2, next_batch=(bt[4][0], bt[4][1]))
+        e.train_step(*bt[4], group=GROUP, k=2)
+        e.check_errors()
         e.flush()
         engines.append(e)
     a, d = engines
@@ -190,9 +220,9 @@ def test_stale_counted_step_is_dropped(B):
     assert NCFEngine.read_stats(a.stats) == NCFEngine.read_stats(d.stats)
     assert int(a.step.item()) == int(d.step.item())
     # afterwards both train the same counted steps to the same bits
-    for s in (3, 4):
+    for s in (5, 0):
         for e in engines:
-            e.train_step(*bt[s], group=GROUP, k=2, next_batch=(bt[4][0], bt[4][1]) if s == 3 else None)
+            e.train_step(*bt[s], group=GROUP, k=2, next_batch=(bt[0][0], bt[0][1]) if s == 5 else None)
     for e in engines:
         e.check_errors()
         e.flush()

@@ -26,7 +26,34 @@ def test_library_exports_every_symbol():
     L = N.lib()
     for name in _declared():
         assert hasattr(L, name), name
-    assert L.ncf_abi_version() == N.ABI_VERSION == 10
+    assert L.ncf_abi_version() == N.ABI_VERSION == 11
+
+
+def test_library_links_no_vendor_blas():
+    """Every matrix product is a hand-written MFMA kernel: the library neither needs a BLAS
+    library nor references one of its symbols (the rocBLAS layered path is gone)."""
+    import subprocess
+    needed = subprocess.run(["readelf", "-d", N.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    assert "blas" not in needed.lower(), needed
+    syms = subprocess.run(["nm", "-D", N.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    assert "rocblas" not in syms.lower() and "hipblas" not in syms.lower()
+
+
+def test_build_info_matches_the_tree():
+    """The loaded library carries the SHA-256 of the sources it was built from (ncf_build_info);
+    for the product library it equals the tree's hash and lists no experiment defines, so the
+    benched binary is provably the committed code."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "ncf_build", os.path.join(ROOT, "movierecommender-tf-trt_amd", "csrc", "build.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    info = N.build_info()
+    assert info["arch"] == "gfx950" and info["abi"] == N.ABI_VERSION
+    assert info["src_sha256"] == b.embedded_hash(N.LIB_PATH)
+    if not os.environ.get("NCF_LIB"):
+        assert info["defines"] == ""
+        assert info["src_sha256"] == b.source_hash(), "the library is stale: run __graft_entry__.build()"
 
 
 def _shape(nu, ni, layers, g):
