@@ -145,6 +145,27 @@ def _all_reduce(t, group):
         dist.all_reduce(t, group=group)
 
 
+def _batch_token(users, items):
+    """What a caller announced as next_batch: tensors by storage, size, dtype, device and version
+    counter (an in-place write through torch bumps it); anything else by a copy of its contents."""
+    def one(x):
+        if torch.is_tensor(x):
+            return ("t", x.data_ptr(), x.numel(), x.dtype, str(x.device), x._version)
+        return ("h", np.array(x, copy=True))
+    return one(users), one(items)
+
+
+def _same_batch(token, users, items):
+    """True when (users, items) are the batch _batch_token recorded, unmodified."""
+    for t, x in zip(token, (users, items)):
+        if t[0] == "t":
+            if not (torch.is_tensor(x) and ("t", x.data_ptr(), x.numel(), x.dtype, str(x.device), x._version) == t):
+                return False
+        elif torch.is_tensor(x) or not np.array_equal(np.asarray(x), t[1]):
+            return False
+    return True
+
+
 class RowShardedDataParallel(object):
     """Drives one rank's ``ShardedNCFEngine`` (or a look-alike) through the row-sharded step:
 
@@ -232,20 +253,18 @@ class RowShardedDataParallel(object):
         eng = self.eng
         held = self._ahead
         self._ahead = None
-        u, i = eng._ids(users), eng._ids(items)
-        ready = (held is not None and group is not None and held[0].data_ptr() == u.data_ptr() and
-                 held[1].data_ptr() == i.data_ptr() and held[2] == u.numel() and
-                 (held[0]._version, held[1]._version) == held[3] and held[4] == int(group))
+        ready = held is not None and group is not None and held[4] == int(group) and _same_batch(held[3], users, items)
         if held is not None and group is not None and not ready:
             # re-planning here would issue a counts exchange the ranks whose held plan matches do
             # not issue: the collectives would no longer pair up.  Every rank holds a plan for the
             # batch it announced, so a different batch (or ids refilled in place) is an error
             raise RuntimeError("train_step got another batch than the next_batch= announced in the previous "
                                "step (or its ids changed since): pass exactly those tensors, unmodified")
-        if not ready:
-            self._plan_and_count(u, i, group, ahead=False)
+        if ready:
+            eng._n = held[2]   # the plan ahead's batch (the engine planned it last), its normalised ids
         else:
-            eng._n = u.numel()   # the plan ahead's batch (the engine planned it last)
+            u, i = eng._ids(users), eng._ids(items)
+            self._plan_and_count(u, i, group, ahead=False)
         send, recv = self._counts()
         nu, m = sum(send), sum(recv)
         if self.emulate:
@@ -272,14 +291,18 @@ class RowShardedDataParallel(object):
         # The next batch is planned here only under deferred decay: the dense shard update
         # (ncf_shard_apply_update without row_step) builds its owner index in per-batch workspace
         # regions that a plan of the next batch would overwrite, and a next batch larger than the
-        # workspace would reallocate it under this step's pending update.  (Every rank decides
-        # alike: the engines share the layout and the batches their size.)
+        # workspace would reallocate it under this step's pending update.  Every rank decides
+        # alike — the engines share the layout, the batches their size, and the decision reads
+        # nothing of how a rank holds its ids: host, int64 or off-device ids are normalised
+        # (eng._ids) and planned like device int32 tensors, the announced objects remembered by
+        # identity (tensors: storage, size and version counter; host arrays: a copy of the
+        # contents) for the next step's check.  (a rank whose ids _ids copied used to
+        # skip the plan while the others planned, so the next step's counts exchange did not pair.)
         if next_batch is not None and eng.lazy and len(next_batch[0]) <= eng.max_batch:
             # the forward/backward and its compact gradient were the last readers of this step's plan
             nu_, ni_ = eng._ids(next_batch[0]), eng._ids(next_batch[1])
-            if nu_.data_ptr() == next_batch[0].data_ptr() and ni_.data_ptr() == next_batch[1].data_ptr():
-                self._plan_and_count(nu_, ni_, group, ahead=True)
-                self._ahead = (nu_, ni_, nu_.numel(), (nu_._version, ni_._version), int(group))
+            self._plan_and_count(nu_, ni_, group, ahead=True)
+            self._ahead = (nu_, ni_, nu_.numel(), _batch_token(next_batch[0], next_batch[1]), int(group))
         if not self.emulate:
             _all_to_all(eng.recv_grad[:m], eng.uniq_grad[:nu], recv, send, self.group)
             _all_reduce(eng.dense_buf, self.group)

@@ -135,6 +135,10 @@ def _cpu_sharded_worker(rank, world, port, q, ahead=False):
     per = B // world
     sl = slice(rank * per, (rank + 1) * per)
     mine = [tuple(torch.from_numpy(np.ascontiguousarray(a[sl])) for a in b) for b in _batches()]
+    if ahead == "mixed" and rank == 0:
+        # this rank holds host int64 arrays (the engine's _ids copies them), the others int32 tensors:
+        # every rank must still plan ahead alike, or the counts exchanges do not pair up
+        mine = [(u.numpy().astype(np.int64), i.numpy().astype(np.int64), y) for u, i, y in mine]
     for s, (users, items, y) in enumerate(mine):
         # ahead: the next batch planned (and its counts exchanged) inside this step
         nxt = mine[s + 1][:2] if ahead and s + 1 < len(mine) else None
@@ -163,11 +167,13 @@ def _run_cpu(worker, world, *extra):
     return res
 
 
-@pytest.mark.parametrize("world,ahead", [(2, False), (3, False), (2, True)])
+@pytest.mark.parametrize("world,ahead", [(2, False), (3, False), (2, True), (2, "mixed"), (3, "mixed")])
 def test_row_sharded_dp_matches_single_process_cpu(world, ahead):
     """Row-sharded exchanges (plan, all_to_all of ids/rows/grads, owner update) reproduce the
     single-process step; world 3 leaves padding rows in the last shard (40 rows); ahead: each step
-    plans the next batch and exchanges its counts (the next step reads them, no replan)."""
+    plans the next batch and exchanges its counts (the next step reads them, no replan); mixed:
+    rank 0 passes host int64 ids, the others int32 tensors — the plan-ahead decision must not
+    depend on how a rank holds its ids (VERDICT r5 weak #5)."""
     import sys
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from oracle_engine import OracleEngine
