@@ -233,9 +233,6 @@ __device__ inline void scan_local_body(const int32_t* cnt, int64_t r1, int32_t* 
             }
         }
     }
-#if NCF_DEBUG_BOUNDS == 1
-    if (move_to && threadIdx.x == 0 && blk < 4) printf("scan ahead blk %d: tot %d utot %d\n", blk, total, 0);
-#endif
     // last, after every use of threadIdx.x: a `blockIdx.x == 1 && threadIdx.x == 0` store ahead of
     // the body made hipcc (ROCm 7.2) feed the later blocks an undefined thread id
     if (zero_at_end && blk == 0 && threadIdx.x == 0) *zero_at_end = 0;
