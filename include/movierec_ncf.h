@@ -196,11 +196,12 @@ int ncf_workspace_init(const ncf_shape_t* shape, int64_t max_batch, void* ws, si
  *   NCF_WSERR_STALE_COUNT  a batch passed with hyper->index_ready = 2 differed from the ids
  *                          ncf_train_step_ahead counted (their contents changed in between): the
  *                          index build wrote no slot outside its keys' ranges and cleared the
- *                          counters; with the in-kernel index (the single-table default) the step
- *                          was dropped — whether a changed id overflowed a counted row or left one
- *                          short (the fill compares the contributions it placed with the counted
- *                          total) — nothing of it applied, the state a consistent deferred-decay
- *                          state; otherwise that step's embedding gradient is wrong.
+ *                          counters; with the in-kernel index (the single-table default) a step
+ *                          whose changed ids reached a row that was not counted was dropped —
+ *                          nothing of it applied, the state a consistent deferred-decay state —
+ *                          and one whose changed ids only left counted rows short was applied
+ *                          exactly on the ids passed (the unfilled list slots skipped); on the
+ *                          other index paths that step's embedding gradient is wrong.
  *   NCF_WSERR_FOLD         an index built by an earlier call (ncf_build_index, ncf_shard_plan)
  *                          folds user rows differently than the step that used it (their hypers'
  *                          group / force_generic differ): that step's embedding gradient is wrong.

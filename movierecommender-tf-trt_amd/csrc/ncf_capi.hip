@@ -258,7 +258,7 @@ WsLayout make_layout(const ncf_shape_t& s, int64_t B, int world) {
     L.heavy_n = take(4);
     L.err = take(4);
     L.ifold = take(4);
-    L.stale_step = take(8);  // int32[2] (FillArgs::stale_step)
+    L.stale_step = take(4);
     const int64_t S = L.shard_rows;
     if (world > 0) {
         L.ocnt = take((size_t)(S + 1) * 4);

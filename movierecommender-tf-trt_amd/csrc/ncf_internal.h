@@ -71,7 +71,7 @@ struct WsLayout {
     size_t uloc;      // int32[K+1]  per-2048-key local exclusive scan of (cnt > 0)
     size_t utot;      // int32[nscan]
     size_t ifold;     // int32       user-row folding of the last index build (persistent)
-    size_t stale_step;// int32[2]   persistent: nonzero while the current step is dropped (fill_wave)
+    size_t stale_step;// int32      persistent: nonzero while the current step is dropped (fill_wave)
     size_t cid_u;     // int32[B]    compact (unique-row) id of each sample's user row
     size_t cid_i;     // int32[B]    compact id of each sample's item row
     size_t uoffs;     // int32[2B+1] compact row -> first list slot
@@ -423,8 +423,7 @@ struct FillArgs {
     int32_t* ifold;
     int32_t U, I;             // user u -> key u, item v -> key U + v
     int64_t list_cap, touched_cap, heavy_cap;  // region sizes (debug bound checks)
-    int32_t* stale_step;      // int32[2]: [0] set when a contribution finds no slot, [1] contributions
-                              // placed minus contributions counted; either nonzero drops the step (below)
+    int32_t* stale_step;      // set when a contribution finds no slot: the step is dropped (below)
 };
 #if NCF_DEBUG_BOUNDS == 1
 #define NCF_BOUND(cond, ...)          \
@@ -452,11 +451,15 @@ constexpr int kFillContribPerLane = 2;  // its CU: contributions per lane and pa
 // read rows the counted set missed, at their deferred step.  Such a step is DROPPED — f.stale_step
 // tells the touched-row update and the stats launch to apply nothing of it (the table, moments,
 // dense layers, stats and step counter stay as they were: a consistent deferred-decay state) —
-// and reported (NCF_WSERR_STALE_COUNT, RuntimeError from check_errors).  Changed ids need not
-// overflow a slot: fewer valid, unfolded contributions than were counted leave list slots
-// unfilled (residues at counted keys) with nothing overflowing.  So every wave also adds the
-// contributions it placed to stale_step[1] (one atomic per wave) and the rows part's wave 0
-// subtracts the scanned total: the word is 0 exactly when every counted slot was filled.
+// and reported (NCF_WSERR_STALE_COUNT, RuntimeError from check_errors).
+// Changed ids that overflow no counted row — fewer valid, unfolded contributions at some keys than
+// were counted (ids moved out of the table, users that now fold into their group head), none more
+// anywhere — read no row outside the counted set.  Such a step is exact as it stands: a key's
+// run takes slots from the top of its range down, so its unfilled slots are the lowest `residue`
+// ones (the cursor a key keeps after the fill); the touched-row update sums only the slots above
+// them (a counted row left with no contribution takes the zero-gradient step, as in the dense
+// sweep) and clears the residue, and the error is still reported.  (the update used to
+// read those stale slots as contributions.)
 template <int PART = 3>
 __device__ inline void fill_wave(const FillArgs& f, const int32_t* __restrict__ users,
                                  const int32_t* __restrict__ items, int64_t n, int fold, int gw, int nw);
@@ -466,7 +469,6 @@ __device__ inline void fill_wave(const FillArgs& f, const int32_t* __restrict__ 
     const int lane = threadIdx.x & 63;
     int p0, p1, q0, q1;  // pre[lane], pre[lane + 64], upre[lane], upre[lane + 64]
     int u0, u1, ntouched;  // utot[lane], utot[lane + 64], their sum
-    int counted;           // the scan blocks' total: the contributions counted ahead
     {
         const int t0 = lane < f.nscan ? f.tot[lane] : 0, t1 = lane + 64 < f.nscan ? f.tot[lane + 64] : 0;
         u0 = lane < f.nscan ? f.utot[lane] : 0;
@@ -484,7 +486,6 @@ __device__ inline void fill_wave(const FillArgs& f, const int32_t* __restrict__ 
         q0 = b0 - u0;
         q1 = cb + b1 - u1;
         ntouched = cb + __shfl(b1, 63, 64);
-        counted = ca + __shfl(a1, 63, 64);
 #if NCF_DEBUG_BOUNDS == 1
         if (gw == 0 && lane < 4 && lane < f.nscan)
             printf("fill lane %d: tot %d utot %d pre %d upre %d nscan %d\n", lane, t0, u0, p0, q0, f.nscan);
@@ -535,10 +536,8 @@ __device__ inline void fill_wave(const FillArgs& f, const int32_t* __restrict__ 
         if (gw == 0 && lane == 0) {
             *f.nuniq = ntouched;
             *f.ifold = fold;
-            if (counted != 0) atomicSub(&f.stale_step[1], counted);
         }
     }
-    int placed = 0;  // this wave's placed contributions (lane 0's count)
     // contributions c = 2i + side, a wave at a time (k_fill's runs: equal keys two lanes apart share
     // one atomic; slot order inside a key is free, the update sorts)
     const int64_t m = 2 * n;
@@ -596,14 +595,12 @@ __device__ inline void fill_wave(const FillArgs& f, const int32_t* __restrict__ 
                           (long long)c, key, (long long)li, (long long)f.list_cap)
                 f.list[li] = (int)c;
             }
-            placed += __popcll(__ballot(ok && slot >= 0));
             if (ok && slot < 0) {
                 atomicOr(f.err, kErrStaleCount);
-                atomicOr(&f.stale_step[0], 1);
+                atomicOr(f.stale_step, 1);
             }
         }
     }
-    if ((PART & 2) && lane == 0 && placed != 0) atomicAdd(&f.stale_step[1], placed);
 }
 
 // ncf_user_dp_step's helpers (ncf_capi.hip)

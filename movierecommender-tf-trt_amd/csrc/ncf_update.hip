@@ -745,7 +745,7 @@ __global__ __launch_bounds__(kBlock, UNSORTED ? NCF_TOUCHED_MIN_BLOCKS_UNSORTED 
     // everything else)
     int b = (int)blockIdx.x;
     // a dropped step (stale counted set, unsorted lists only): nothing of it is applied
-    const bool dropped = UNSORTED && so.drop && (so.drop[0] | so.drop[1]) != 0;
+    const bool dropped = UNSORTED && so.drop && *so.drop != 0;
     if (UNSORTED && b < so.nheavy) {
         if (dropped) return;
         // heavy rows (lists longer than so.hc, unsorted): one per block and pass
@@ -764,20 +764,22 @@ __global__ __launch_bounds__(kBlock, UNSORTED ? NCF_TOUCHED_MIN_BLOCKS_UNSORTED 
                 continue;
             }
 #endif
+            // the key's residue: slots [0, res) were never filled (fill_wave; the light rows' rule)
+            const int res = min(max(so.cursor[r], 0), c);
             // rank of each entry among the row's: the list staged through LDS a chunk at a time
             int e[4], rk[4];
             for (int j0 = 0; j0 < c; j0 += 4 * kBlock) {
 #pragma unroll
                 for (int a = 0; a < 4; ++a) {
                     const int j = j0 + a * kBlock + (int)threadIdx.x;
-                    e[a] = j < c ? (int)min((unsigned)clist[o + j], (unsigned)(so.mcap - 1)) : INT_MAX;
+                    e[a] = j >= res && j < c ? (int)min((unsigned)clist[o + j], (unsigned)(so.mcap - 1)) : INT_MAX;
                     rk[a] = 0;
                 }
                 for (int i0 = 0; i0 < c; i0 += kHeavyChunk) {
                     const int ni = min(kHeavyChunk, c - i0);
                     __syncthreads();
                     for (int i = threadIdx.x; i < ni; i += kBlock)
-                        chunk[i] = (int)min((unsigned)clist[o + i0 + i], (unsigned)(so.mcap - 1));
+                        chunk[i] = i0 + i >= res ? (int)min((unsigned)clist[o + i0 + i], (unsigned)(so.mcap - 1)) : INT_MAX;
                     __syncthreads();
                     for (int i = 0; i < ni; ++i) {
                         const int x = chunk[i];
@@ -786,8 +788,10 @@ __global__ __launch_bounds__(kBlock, UNSORTED ? NCF_TOUCHED_MIN_BLOCKS_UNSORTED 
                     }
                 }
 #pragma unroll
-                for (int a = 0; a < 4; ++a)
-                    if (j0 + a * kBlock + (int)threadIdx.x < c) so.slist[o + rk[a]] = e[a];
+                for (int a = 0; a < 4; ++a) {
+                    const int j = j0 + a * kBlock + (int)threadIdx.x;
+                    if (j >= res && j < c) so.slist[o + rk[a]] = e[a];
+                }
             }
             __syncthreads();  // the sorted list is the workgroup's own stores
             const bool mine = r < ca.lazy_rows;
@@ -796,7 +800,7 @@ __global__ __launch_bounds__(kBlock, UNSORTED ? NCF_TOUCHED_MIN_BLOCKS_UNSORTED 
             if (rs < 0) rs = pahead_s0(rs);
             const int k = NCF_CATCHUP_P_ONLY && mine && !fresh ? t - 1 - rs : 0;
             if (mine)
-                row_adam(emb, m4, v4, gs, w4, r, c, threadIdx.x, kBlock, k, fresh, lr_t, b1, b2, eps,
+                row_adam(emb, m4, v4, gs, w4, r, c - res, threadIdx.x, kBlock, k, fresh, lr_t, b1, b2, eps,
                          [&](int j) { return so.slist[o + j]; });
             if (threadIdx.x == 0) {
                 if (mine) row_step[r] = t;
@@ -1045,8 +1049,12 @@ __global__ __launch_bounds__(kBlock, UNSORTED ? NCF_TOUCHED_MIN_BLOCKS_UNSORTED 
             const int c = heavy ? 0 : oc.y;
             const bool mine = has && !heavy && r < ca.lazy_rows;
             int rs = mine ? row_step[r] : 0;
-            const int res = has && !heavy && ql == 0 ? so.cursor[r] : 0;
-            int e = ql < c ? (int)min((unsigned)clist[oc.x + ql], (unsigned)(so.mcap - 1)) : INT_MAX;
+            // the key's residue (normally 0): its lowest `res` slots were never filled — ids changed
+            // after they were counted, with fewer contributions here and no overflow anywhere (else
+            // the step is dropped) — so the row sums the slots [res, c) only (fill_wave)
+            const int res = has && !heavy ? min(max(so.cursor[r], 0), c) : 0;
+            const bool valid = ql >= res && ql < c;
+            int e = valid ? (int)min((unsigned)clist[oc.x + ql], (unsigned)(so.mcap - 1)) : INT_MAX;
             // the wave's longest light list (its row groups' counts, read lane by lane)
             int cmax = 0;
             for (int g = 0; g < rl.rpw; ++g) cmax = max(cmax, __builtin_amdgcn_readlane(c, g * (int)w4));
@@ -1055,11 +1063,12 @@ __global__ __launch_bounds__(kBlock, UNSORTED ? NCF_TOUCHED_MIN_BLOCKS_UNSORTED 
                 const int x = __shfl(e, base + j, 64);
                 rank += j < c && x < e;
             }
-            // entry ql goes to lane base + rank (a permutation of the group's first c lanes; the
-            // other lanes keep their own value)
-            const int to = ql < c ? base + rank : lane;
+            // entry ql goes to lane base + rank (a permutation of the group's first c lanes: the
+            // unfilled slots' lanes to [c - res, c); the other lanes keep their own value)
+            const int cv = c - res;
+            const int to = valid ? base + rank : ql < res ? base + cv + ql : lane;
             const int srt = __builtin_amdgcn_ds_permute(to * 4, e);
-            if (res != 0) {
+            if (res != 0 && ql == 0) {
                 atomicOr(so.err, kErrStaleCount);
                 so.cursor[r] = 0;
             }
@@ -1086,7 +1095,7 @@ __global__ __launch_bounds__(kBlock, UNSORTED ? NCF_TOUCHED_MIN_BLOCKS_UNSORTED 
                     const int c0 = __shfl(srt, base + j, 64), c1 = __shfl(srt, base + min(j + 1, gsz - 1), 64);
                     const int c2 = __shfl(srt, base + min(j + 2, gsz - 1), 64);
                     const int c3 = __shfl(srt, base + min(j + 3, gsz - 1), 64);
-                    const bool v0 = act && j < c, v1 = act && j + 1 < c, v2 = act && j + 2 < c, v3 = act && j + 3 < c;
+                    const bool v0 = act && j < cv, v1 = act && j + 1 < cv, v2 = act && j + 2 < cv, v3 = act && j + 3 < cv;
 #if NCF_DEBUG_BOUNDS == 1
                     if ((v0 && (unsigned)c0 >= (unsigned)so.mcap) || (v1 && (unsigned)c1 >= (unsigned)so.mcap) ||
                         (v2 && (unsigned)c2 >= (unsigned)so.mcap) || (v3 && (unsigned)c3 >= (unsigned)so.mcap))
@@ -1454,7 +1463,7 @@ __device__ inline void summary_stats_block(const SummaryArgs& sa, float* __restr
                                            double* __restrict__ stats, int32_t* step, int bump) {
     __shared__ float red[5][4];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int dropped = sa.drop ? (sa.drop[0] | sa.drop[1]) : 0;
+    const int dropped = sa.drop ? *sa.drop : 0;
     float x[5] = {0.f, 0.f, 0.f, 0.f, 0.f};  // bce, hit, dcg, reg_emb, reg_mlp
     if (sa.summary) {
         for (int j = tid; j < sa.nbce; j += kBlock) x[0] += sa.part_bce[j];
@@ -1485,9 +1494,8 @@ __device__ inline void summary_stats_block(const SummaryArgs& sa, float* __restr
     float r[5];
 #pragma unroll
     for (int k = 0; k < 5; ++k) r[k] = (red[k][0] + red[k][1]) + (red[k][2] + red[k][3]);
-    if (dropped) {  // the step was dropped (fill_wave): no summary, stats or bump; clear the words
-        sa.drop[0] = 0;
-        sa.drop[1] = 0;
+    if (dropped) {  // the step was dropped (fill_wave): no summary, stats or bump; clear the word
+        *sa.drop = 0;
         return;
     }
     if (sa.summary) {

@@ -247,6 +247,11 @@ __device__ unsigned long long g_wave_s[256 * 4 * 16];
 // contraction, so barrier k + 1 also frees unit k's buffers for unit k + 2.  The chain's phases
 // that issue no MFMA now have the weight-gradient wave's 168 MFMAs per unit beside them on the
 // same SIMD.  Same MFMAs on the same operands in the same order as the one-wave form: bitwise.
+// 1 (the default): the epilogue's tile rows transposed in LDS and the slab written 16 bytes per lane
+// (reduce_tiles); 0: the round-2 epilogue (4-byte slab stores), for A/B
+#ifndef NCF_EPI_WIDE
+#define NCF_EPI_WIDE 1
+#endif
 #ifndef NCF_PRIO_P0
 #define NCF_PRIO_P0 1
 #endif
@@ -583,6 +588,48 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
     static_assert((size_t)4 * S::PR * 4 <= (SPLIT ? S::LDS_BYTES2 : S::LDS_BYTES), "epilogue rows");
     // tile element (lane gq * 16 + c, register r) is row 16 a + 4 gq + r (split dW1: row
     // B0 (4 gq + r) + a), column 16 b + c of its matrix
+#if NCF_EPI_WIDE
+    // Wide form: a tile sits in its row as [4 gq + r][c] (put_tile: four ds_write_b32 per lane, 2-way
+    // at most), so thread q of a reduction round reads 4 consecutive columns of tile row (q & 63) / 4
+    // (b128, the wave's 256 contiguous floats: conflict-free) and writes them with ONE 16-byte store
+    // (buffer store: a slab starts at blockIdx.x * P floats, 4-byte aligned) — a quarter of the
+    // end-of-kernel store instructions, which set that tail (MI355X_MICROARCH.md, epilogue store tail)
+    const __amdgpu_buffer_rsrc_t slab_rsrc = __builtin_amdgcn_make_buffer_rsrc(slab, (short)0, (int)(S::P * 4), 0x00020000);
+    auto put_tile = [&](float* Rt, const f32x4& v) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Rt[(4 * g + r) * 16 + li] = v[r];
+    };
+    auto reduce_tiles = [&](int t0, int t1) {
+        for (int q = threadIdx.x; q < (t1 - t0) * 64; q += NTHR) {
+            const int tl = q >> 6, tr = (q & 63) >> 2, cq = q & 3;
+            auto at4 = [&](const float* row) { return *reinterpret_cast<const f32x4*>(row + tl * 256 + 4 * (q & 63)); };
+            const f32x4 x = (at4(R0) + at4(R2)) + (at4(R1) + at4(R3));
+            const int t = t0 + tl;  // uniform per wave
+            int off;
+            bool keep = true;
+            if (t < S::NT1) {
+                int row;
+                if constexpr (GU) {
+                    const int a = t / B1;
+                    row = (a < B0 / 2 ? 0 : D0) + a % (B0 / 2) + tr * (B0 / 2);
+                } else if constexpr (SPLIT) {
+                    row = t / B1 + tr * B0;
+                } else {
+                    row = 16 * (t / B1) + tr;
+                }
+                off = S::OW1 + row * L1 + 16 * (t % B1) + 4 * cq;
+            } else if (t < S::NT1 + S::NT2) {
+                off = S::OW2 + (16 * ((t - S::NT1) / B2) + tr) * L2 + 16 * ((t - S::NT1) % B2) + 4 * cq;
+            } else {
+                off = S::OW3 + (16 * (t - S::NT1 - S::NT2) + tr) * L3 + 4 * cq;
+                keep = 4 * cq < L3;
+            }
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, x), slab_rsrc,
+                                                   keep ? (uint32_t)off * 4u : kDrop, 0, 0);
+        }
+    };
+#else
+    auto put_tile = [&](float* Rt, const f32x4& v) { *reinterpret_cast<f32x4*>(Rt + lane * 4) = v; };
     auto reduce_tiles = [&](int t0, int t1) {
         for (int q = threadIdx.x; q < (t1 - t0) * 64; q += NTHR) {
             auto at4 = [&](const float* row) { return *reinterpret_cast<const f32x4*>(row + 4 * q); };
@@ -613,6 +660,7 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
             }
         }
     };
+#endif
     // biases, output kernel, output bias: back to back in the rows (RB1 .. RBO), segment by
     // segment in the flat layout; the loss / hit / dcg partials
     auto reduce_rest = [&]() {
@@ -972,19 +1020,19 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
 #pragma unroll
                     for (int b = 0; b < B1; ++b) {
                         const int t = a * B1 + b;
-                        if (t >= t0 && t < t1) *reinterpret_cast<f32x4*>(R + (t - t0) * 256 + lane * 4) = dw1[a][b];
+                        if (t >= t0 && t < t1) put_tile(R + (t - t0) * 256, dw1[a][b]);
                     }
 #pragma unroll
                 for (int a = 0; a < B1; ++a)
 #pragma unroll
                     for (int b = 0; b < B2; ++b) {
                         const int t = S::NT1 + a * B2 + b;
-                        if (t >= t0 && t < t1) *reinterpret_cast<f32x4*>(R + (t - t0) * 256 + lane * 4) = dw2[a][b];
+                        if (t >= t0 && t < t1) put_tile(R + (t - t0) * 256, dw2[a][b]);
                     }
 #pragma unroll
                 for (int a = 0; a < B2; ++a) {
                     const int t = S::NT1 + S::NT2 + a;
-                    if (t >= t0 && t < t1) *reinterpret_cast<f32x4*>(R + (t - t0) * 256 + lane * 4) = dw3[a];
+                    if (t >= t0 && t < t1) put_tile(R + (t - t0) * 256, dw3[a]);
                 }
             };
             __syncthreads();  // every wave is done with the weights and the buffers
@@ -1517,7 +1565,7 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256, 1) void k_fb_wave(const float* _
     auto put_tiles = [&](int t0, int t1) {
         if constexpr (!SPLIT)
             for_tiles([&](int t, f32x4& v) {
-                if (t >= t0 && t < t1) *reinterpret_cast<f32x4*>(R + (t - t0) * 256 + lane * 4) = v;
+                if (t >= t0 && t < t1) put_tile(R + (t - t0) * 256, v);
             });
     };
     put_tiles(0, S::NTH);

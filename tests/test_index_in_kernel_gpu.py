@@ -177,21 +177,26 @@ def _short_count(users):
     return torch.from_numpy(u.reshape(-1)).cuda()
 
 
-@pytest.mark.parametrize("B,mode", [(16384, "moved"), (1024, "moved"), (16384, "short"), (4096, "short")])
+@pytest.mark.parametrize("B,mode", [(16384, "moved"), (1024, "moved"), (16384, "short"), (4096, "short"),
+                                    (1024, "short")])
 def test_stale_counted_step_is_dropped(B, mode):
-    """A counted batch whose ids change behind torch's back is dropped by the in-kernel fill
-    (the wave kernel's at 16,384 samples, the unit launch's fill workgroups at 4,096, the fill
-    launch's at 1,024) — whether the change overflows a counted row ("moved") or only leaves counted
-    slots unfilled ("short"): nothing of the step is applied — bitwise the engine that never ran it
-    (same counted-ahead history, final flush) — the error is raised, and the next counted steps train
-    normally.  The dropped step counts the next batch ahead itself, and two counted steps run before
-    any flush: the counted rows the previous step caught up ahead (P-ahead: p current, m and v owed)
-    must be settled by the dropped launch, or a row absent from the next batch keeps its mark past
-    the next bump."""
+    """A counted batch whose ids change behind torch's back (the in-kernel fill: the wave kernel's
+    at 16,384 samples, the unit launch's fill workgroups at 4,096, the fill launch's at 1,024).
+    "moved": a changed id reaches a row that was not counted (the forward pass may have read it at
+    its deferred step): the step is dropped — nothing applied, bitwise the engine that never ran it.
+    "short": the changes only leave counted rows with fewer contributions (mixed groups' users set to
+    their head's: they now fold) — no row outside the counted set is read, so the step is applied
+    exactly: the unfilled list slots are skipped, bitwise the engine that runs the same ids without
+    counting ahead (those slots were summed as contributions).  Either way the error is
+    raised.  The stale step counts the next batch ahead itself, and two counted steps run before any
+    flush: the counted rows the previous step caught up ahead (P-ahead: p current, m and v owed) must
+    be settled by a dropped launch, or a row absent from the next batch keeps its mark past the next
+    bump."""
     U, I = 3000, 2000
     shape = O.NCFShape(U, I, LAYERS, GMF)
     w = _weights(shape, 13)
     bt = [_batch(U, I, B, 90 + s) for s in range(6)]
+    short_users = _short_count(bt[1][0])
     engines = []
     for stale in (True, False):
         e = NCFEngine(U, I, LAYERS, GMF, max_batch=B, lazy_adam=True)
@@ -203,11 +208,15 @@ def test_stale_counted_step_is_dropped(B, mode):
             if mode == "moved":
                 stage[1].data.copy_(bt[2][1])             # behind torch's back
             else:
-                stage[0].data.copy_(_short_count(stage[0]))
+                stage[0].data.copy_(short_users)
             e.train_step(stage[0], stage[1], bt[1][2], group=GROUP, k=2, next_batch=(bt[3][0], bt[3][1]))
             with pytest.raises(RuntimeError):
                 e.check_errors()
-        # two counted steps before any flush (the twin gives up its counted batch here: flushed)
+        elif mode == "short":
+            # the same ids, not counted ahead (the engine gives up its counted batch: flushed)
+            e.train_step(short_users.clone(), bt[1][1].clone(), bt[1][2], group=GROUP, k=2,
+                         next_batch=(bt[3][0], bt[3][1]))
+        # two counted steps before any flush
         e.train_step(*bt[3], group=GROUP, k=2, next_batch=(bt[4][0], bt[4][1]))
         e.train_step(*bt[4], group=GROUP, k=2)
         e.check_errors()
