@@ -145,8 +145,10 @@ typedef struct ncf_hyper {
                                            beforehand by ncf_build_index (same ids, same ws): skip it;
                                            2: its contributions were counted and scanned by the
                                            previous ncf_train_step_ahead (same ids, same ws);
-                                           3: its index was finished (and its deferred rows
-                                           caught up) by the previous ncf_user_dp_step */
+                                           3: its contributions were counted and scanned (and
+                                           its own deferred rows caught up) by the previous
+                                           ncf_user_dp_step[_split]; the step fills its index
+                                           inside its forward/backward where it can */
     int32_t mlp_bf16;                   /* 1: the MLP tower's matrix products (forward, data and
                                            weight gradients) take bf16 operands with fp32
                                            accumulation; embeddings, GMF, loss, master weights

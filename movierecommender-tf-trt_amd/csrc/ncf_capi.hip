@@ -368,30 +368,6 @@ LaunchEvents& launch_events() {
 
 }  // namespace ncf
 
-namespace ncf {
-// ncf_user_dp_step's tail: the next batch's index finished ahead (its counts were taken and
-// scanned by the ncf_update_rows_lazy just enqueued): fill, list sort (+ the stale-count gate), so
-// the next step starts at its forward/backward (index_ready = 3)
-int build_next_index(const ncf_shape_t& s, const ncf_hyper_t& h, ncf_model_t* model, ncf_optim_t* optim,
-                     const int32_t* next_users, const int32_t* next_items, int64_t n, void* ws, size_t ws_bytes,
-                     hipStream_t st, int gate_ahead) {
-    WsLayout L;
-    if (int r = check_ws(s, n, ws, ws_bytes, &L)) return r;
-    prof_begin(NCF_K_INDEX, st);
-    hipError_t e = launch_index_build(s, L, ws, next_users, next_items, n, st, true, true, true, index_fold(s, &h));
-    prof_end(NCF_K_INDEX, st);
-    if (e != hipSuccess) return hip_check(e, "next index");
-    prof_begin(NCF_K_CATCHUP, st);
-    // gate_ahead 1: enqueued before ncf_apply_update bumps the step, a stale-count gate replays to
-    // *step + 1; 0: after it
-    e = launch_emb_catchup(s, L, ws, model->emb, optim->emb_m, optim->emb_v, optim->row_step, optim->step, h, false, st,
-                           true, n, true, next_users, next_items, gate_ahead);
-    prof_end(NCF_K_CATCHUP, st);
-    return hip_check(e, "next index sort");
-}
-
-}  // namespace ncf
-
 extern "C" {
 
 int ncf_abi_version(void) { return NCF_ABI_VERSION; }
@@ -996,6 +972,90 @@ int ncf_update_rows_lazy(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* 
     }
     return 0;
 }
+
+}  // extern "C"
+
+namespace ncf {
+
+// The one-call user-partitioned step's halves (ncf_comm.hip).  hyper->index_ready 3: the previous
+// one-call step counted this batch, scanned the counts and caught its own stale rows up, so —
+// where the in-kernel fill runs (fill_in_kernel; batches of 2,048 samples and up, every L2 factor
+// zero, one stream) — the forward/backward launch fills the index (its unsorted lists), the
+// gradient tail orders each item row's list itself (launch_part_tail_unsorted) and the own-user
+// update orders the user rows' (k_emb_adam_touched<true>): no index-build, list-sort or catch-up
+// launch in the step (round 6; the round-5 step built the next index with two more launches).
+// Otherwise (or index_ready 2, the call-by-call path's state) the index is built here from the
+// counts as ncf_forward_backward_part_lazy does.  A fill overflow (ids changed after they were
+// counted) is flagged, never dropped: a rank that skipped its step would leave the replicas apart.
+int dp_forward_backward(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* h,
+                        const int32_t* users, const int32_t* items, const float* labels, int64_t n, float* shared_grad,
+                        float* mlp_grad, float* summary, int32_t include_dense_reg, void* ws, size_t ws_bytes,
+                        void* stream, bool* filled) {
+    *filled = false;
+    if (int r = check_lazy_dp(s, model, optim, h)) return r;
+    if (int r = check_train_args(s, model, h, users, items, labels, n)) return r;
+    if (!shared_grad || !mlp_grad || !summary) return fail(NCF_EINVAL, "NULL gradient output");
+    ncf_hyper_t h2 = *h;
+    if (h->index_ready == 3) h2.index_ready = 2;  // counted and scanned ahead
+    WsLayout L;
+    if (int r = check_ws(*s, n, ws, ws_bytes, &L)) return r;
+    const int fmode = h->index_ready == 3 && n >= 2048 && side_stream_mode() == 0 &&
+                              part_tail_foldable(*s, *h, 1 << 30)
+                          ? fill_in_kernel(*s, L, &h2, n)
+                          : 0;
+    if (!fmode)
+        return forward_backward_rows(s, model, &h2, users, items, labels, n, h->lazy_rows, shared_grad, mlp_grad,
+                                     summary, nullptr, 0, 0, include_dense_reg, ws, ws_bytes, stream, optim);
+    hipStream_t st = (hipStream_t)stream;
+    FillArgs fa = fill_args(*s, L, ws);
+    fa.stale_step = nullptr;  // flagged, not dropped
+    if (fmode == 2) {
+        prof_begin(NCF_K_INDEX, st);
+        hipError_t e = launch_fill_ahead(fa, users, items, n, index_fold(*s, &h2), st);
+        prof_end(NCF_K_INDEX, st);
+        if (e != hipSuccess) return hip_check(e, "index fill");
+    }
+    FbOut fb;
+    if (int r = run_fb(*s, L, model, &h2, users, items, labels, n, ws, nullptr, &fb, st, false, nullptr, nullptr,
+                       fmode == 1 ? &fa : nullptr, fmode == 2))
+        return r;
+    if (!part_tail_foldable(*s, *h, fb.nslab))
+        return fail(NCF_EHIP, "in-kernel fill: %d slabs do not take the two-level reduction", fb.nslab);
+    *filled = true;
+    return hip_check(launch_part_tail_unsorted(*s, L, ws, shared_grad, h->lazy_rows, mlp_grad, fb.nslab, fb.nbce,
+                                               fb.nmet, fb.n_groups, summary, st),
+                     "gradient tail");
+}
+
+// The own users' touched-row update (+ the next batch counted, its own stale rows caught up ahead,
+// and its counts scanned for the next fill): `filled` — this step's lists came from the in-kernel
+// fill (dp_forward_backward)
+int dp_update_rows(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* h, int64_t n,
+                   const int32_t* next_users, const int32_t* next_items, int64_t n_next, void* ws, size_t ws_bytes,
+                   void* stream, bool filled) {
+    if (!filled) return ncf_update_rows_lazy(s, model, optim, h, n, next_users, next_items, n_next, ws, ws_bytes, stream);
+    if (int r = check_lazy_dp(s, model, optim, h)) return r;
+    if ((next_users || next_items) && (!next_users || !next_items || n_next != n || h->optimizer != NCF_OPT_ADAM))
+        return fail(NCF_EINVAL, "next batch: NULL ids, n_next != n, or not Adam");
+    WsLayout L;
+    if (int r = check_ws(*s, n, ws, ws_bytes, &L)) return r;
+    hipStream_t st = (hipStream_t)stream;
+    prof_begin(NCF_K_EMB_UPDATE, st);
+    hipError_t e = launch_emb_update_touched(*s, L, ws, model->emb, optim->emb_m, optim->emb_v, optim->row_step,
+                                             optim->step, *h, st, next_users, next_items, next_users ? n_next : 0,
+                                             nullptr, index_fold(*s, h), nullptr, nullptr, true, false);
+    prof_end(NCF_K_EMB_UPDATE, st);
+    if (e != hipSuccess) return hip_check(e, "touched-row update");
+    if (next_users) {
+        e = launch_scan_ahead(L, ws, s->num_rows, st);
+        if (e != hipSuccess) return hip_check(e, "scan ahead");
+    }
+    return 0;
+}
+
+}  // namespace ncf
+
+extern "C" {
 
 int ncf_build_index(const ncf_shape_t* s, const ncf_hyper_t* h, const int32_t* users, const int32_t* items,
                     int64_t n, void* ws, size_t ws_bytes, void* stream) {

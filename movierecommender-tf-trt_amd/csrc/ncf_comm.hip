@@ -191,8 +191,9 @@ int ncf_user_dp_step(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* opti
     float* mlp_grad = shared + (R - U) * W;
     float* summary = mlp_grad + P;
     hipStream_t st = (hipStream_t)stream;
-    if (int r = ncf_forward_backward_part_lazy(s, model, optim, h, users, items, labels, n, item_grad, mlp_grad, summary,
-                                               nullptr, include_dense_reg, ws, ws_bytes, stream))
+    bool filled = false;
+    if (int r = ncf::dp_forward_backward(s, model, optim, h, users, items, labels, n, item_grad, mlp_grad, summary,
+                                         include_dense_reg, ws, ws_bytes, stream, &filled))
         return r;   // the message is set
     const int64_t count = (R - U) * W + P + NCF_NUM_SUMMARY;
     hipStream_t side = c->side;
@@ -205,14 +206,11 @@ int ncf_user_dp_step(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* opti
         return r;
     if (int r = mark(c, kC1, side)) return r;
     if (int r = hip_ok(hipEventRecord(c->join, side), "join")) return r;
-    // meanwhile on the compute stream: the own users' update (+ the next batch counted and its own
-    // rows caught up ahead), then the next batch's index finished — none of it reads an item row,
-    // so all of it runs under the collective; the next step starts at its forward/backward
-    if (int r = ncf_update_rows_lazy(s, model, optim, h, n, next_users, next_items, n_next, ws, ws_bytes, stream))
+    // meanwhile on the compute stream: the own users' update (+ the next batch counted, its own rows
+    // caught up ahead and its counts scanned) — none of it reads an item row, so all of it runs
+    // under the collective; the next step fills its index inside its forward/backward
+    if (int r = ncf::dp_update_rows(s, model, optim, h, n, next_users, next_items, n_next, ws, ws_bytes, stream, filled))
         return r;
-    if (next_users)
-        if (int r = ncf::build_next_index(*s, *h, model, optim, next_users, next_items, n_next, ws, ws_bytes, st))
-            return r;
     if (int r = mark(c, kJ0, st)) return r;
     if (int r = hip_ok(hipStreamWaitEvent(st, c->join, 0), "join wait")) return r;
     if (int r = mark(c, kJ1, st)) return r;
@@ -233,10 +231,11 @@ int ncf_user_dp_step(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* opti
 //   dense-layer gradient | summary]
 //   comm stream: reduce-scatter of the item-row gradient (rank r receives rows [r Ic, r Ic + Ic) in
 //   slice_grad) + all-reduce of [dense-layer gradient | summary], one RCCL group ...
-//   ... beside the own-user update and the next batch's index on the compute stream
-//   join; Adam on this rank's item slice (table rows U + r Ic ..), the dense layers, stats
+//   ... beside the own-user update (with the next batch counted and scanned) on the compute stream
+//   join; Adam on this rank's item slice (table rows U + r Ic ..)
 //   comm stream: all-gather of the updated item rows (in place: the table holds item_world x Ic
-//   item rows, the rows past num_rows are zero padding); the compute stream waits for it
+//   item rows, the rows past num_rows are zero padding) beside the dense layers' Adam and the
+//   stats on the compute stream, which then waits for it
 // The same bytes cross the links as the all-reduce of ncf_user_dp_step; each rank's item Adam and
 // item-moment traffic shrink to 1/item_world.  item_world == 1 (or a one-rank communicator with
 // item_world > 1: the per-rank compute of that layout, no exchange) is bitwise ncf_user_dp_step.
@@ -261,8 +260,9 @@ int ncf_user_dp_step_split(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t
     float* mlp_grad = shared + item_world * Ic * W;
     float* summary = mlp_grad + P;
     hipStream_t st = (hipStream_t)stream;
-    if (int r = ncf_forward_backward_part_lazy(s, model, optim, h, users, items, labels, n, item_grad, mlp_grad, summary,
-                                               nullptr, include_dense_reg, ws, ws_bytes, stream))
+    bool filled = false;
+    if (int r = ncf::dp_forward_backward(s, model, optim, h, users, items, labels, n, item_grad, mlp_grad, summary,
+                                         include_dense_reg, ws, ws_bytes, stream, &filled))
         return r;
     hipStream_t side = c->side;
     timing_begin(c);
@@ -287,10 +287,9 @@ int ncf_user_dp_step_split(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t
     }
     if (int r = mark(c, kC1, side)) return r;
     if (int r = hip_ok(hipEventRecord(c->join, side), "join")) return r;
-    if (int r = ncf_update_rows_lazy(s, model, optim, h, n, next_users, next_items, n_next, ws, ws_bytes, stream))
+    // the own users' update, the next batch counted (own rows caught up ahead) and scanned
+    if (int r = ncf::dp_update_rows(s, model, optim, h, n, next_users, next_items, n_next, ws, ws_bytes, stream, filled))
         return r;
-    // (the next batch's index is built after the item rows' Adam, beside the all-gather below: this
-    // window already holds the own-user update; the all-gather's holds nothing else)
     if (int r = mark(c, kJ0, st)) return r;
     if (int r = hip_ok(hipStreamWaitEvent(st, c->join, 0), "join wait")) return r;
     if (int r = mark(c, kJ1, st)) return r;
@@ -301,18 +300,35 @@ int ncf_user_dp_step_split(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t
     if (items_opt.emb_m) items_opt.emb_m += (U + r0) * W;
     if (items_opt.emb_v) items_opt.emb_v += (U + r0) * W;
     items_opt.row_step = nullptr;
-    if (int r = ncf_apply_update(s, model, &items_opt, h, U + (cnt ? r0 : I), cnt, slice_grad, mlp_grad, summary, stats,
-                                 ws, ws_bytes, stream))
+    // Every L2 factor zero (the fused apply): only the item slice's Adam precedes the all-gather; the
+    // dense layers' Adam and the stats (step bump) run on the compute stream BESIDE it, with the next
+    // batch's index — off the exchange's critical path (round 6; same kernels' arithmetic, so the
+    // states stay bitwise those of ncf_apply_update)
+    const bool split_apply = cnt > 0 && ncf::part_tail_foldable(*s, *h, 1 << 30);
+    if (split_apply) {
+        if (int r = hip_ok(ncf::launch_apply_fused(*s, model->emb + (U + r0) * W, items_opt.emb_m, items_opt.emb_v,
+                                                   slice_grad, cnt, nullptr, nullptr, nullptr, nullptr, optim->step, *h,
+                                                   st, 1),
+                           "item-slice update"))
+            return r;
+    } else if (int r = ncf_apply_update(s, model, &items_opt, h, U + (cnt ? r0 : I), cnt, slice_grad, mlp_grad, summary,
+                                        stats, ws, ws_bytes, stream)) {
         return r;
-    if (!exchange) {
-        if (next_users)  // (after the step's bump)
-            if (int r = ncf::build_next_index(*s, *h, model, optim, next_users, next_items, n_next, ws, ws_bytes, st, 0))
-                return r;
-        return 0;
     }
-    // the updated slices to every rank (in place) on the side stream, while the compute stream
-    // builds the next batch's index (it reads ids and the own rows' steps, never an item row); the
-    // compute stream waits for the gather before the next forward pass can read an item row
+    auto dense_and_stats = [&]() -> int {
+        if (!split_apply) return 0;
+        if (int r = hip_ok(ncf::launch_apply_fused(*s, nullptr, nullptr, nullptr, nullptr, 0, model->mlp, optim->mlp_m,
+                                                   optim->mlp_v, mlp_grad, optim->step, *h, st, 2),
+                           "dense-layer update"))
+            return r;
+        // (as ncf_apply_update: the stats read only the caller's summary, so the one-sample layout serves)
+        const ncf::WsLayout L = ncf::make_layout(*s, 1);
+        return hip_ok(ncf::launch_stats(L, ws, summary, 0, 0, h->inv_batch, stats, optim->step, true, st), "stats");
+    };
+    if (!exchange) return dense_and_stats();
+    // the updated slices to every rank (in place) on the side stream, while the compute stream runs
+    // the dense layers' Adam and the stats (no item row read); the compute stream waits for the
+    // gather before the next forward pass can read an item row
     if (int r = hip_ok(hipEventRecord(c->fork, st), "fork")) return r;
     if (int r = hip_ok(hipStreamWaitEvent(side, c->fork, 0), "fork wait")) return r;
     if (c->cur) c->cur->gather = true;
@@ -323,9 +339,7 @@ int ncf_user_dp_step_split(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t
         return r;
     if (int r = mark(c, kA1, side)) return r;
     if (int r = hip_ok(hipEventRecord(c->join, side), "join")) return r;
-    if (next_users)  // (after the step's bump)
-        if (int r = ncf::build_next_index(*s, *h, model, optim, next_users, next_items, n_next, ws, ws_bytes, st, 0))
-            return r;
+    if (int r = dense_and_stats()) return r;
     if (int r = mark(c, kG0, st)) return r;
     if (int r = hip_ok(hipStreamWaitEvent(st, c->join, 0), "join wait")) return r;
     return mark(c, kG1, st);

@@ -423,7 +423,8 @@ struct FillArgs {
     int32_t* ifold;
     int32_t U, I;             // user u -> key u, item v -> key U + v
     int64_t list_cap, touched_cap, heavy_cap;  // region sizes (debug bound checks)
-    int32_t* stale_step;      // set when a contribution finds no slot: the step is dropped (below)
+    int32_t* stale_step;      // set when a contribution finds no slot: the step is dropped (below);
+                              // nullptr: never dropped (data parallelism: flagged only)
 };
 #if NCF_DEBUG_BOUNDS == 1
 #define NCF_BOUND(cond, ...)          \
@@ -597,16 +598,21 @@ __device__ inline void fill_wave(const FillArgs& f, const int32_t* __restrict__ 
             }
             if (ok && slot < 0) {
                 atomicOr(f.err, kErrStaleCount);
-                atomicOr(f.stale_step, 1);
+                if (f.stale_step) atomicOr(f.stale_step, 1);
             }
         }
     }
 }
 
-// ncf_user_dp_step's helpers (ncf_capi.hip)
-int build_next_index(const ncf_shape_t& s, const ncf_hyper_t& h, ncf_model_t* model, ncf_optim_t* optim,
-                     const int32_t* next_users, const int32_t* next_items, int64_t n, void* ws, size_t ws_bytes,
-                     hipStream_t st, int gate_ahead = 1);
+// ncf_user_dp_step's halves (ncf_capi.hip): forward/backward + gradient tail (*filled: the in-kernel
+// fill built this step's index), then the own-user update + the next batch counted and scanned
+int dp_forward_backward(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* h,
+                        const int32_t* users, const int32_t* items, const float* labels, int64_t n, float* shared_grad,
+                        float* mlp_grad, float* summary, int32_t include_dense_reg, void* ws, size_t ws_bytes,
+                        void* stream, bool* filled);
+int dp_update_rows(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* h, int64_t n,
+                   const int32_t* next_users, const int32_t* next_items, int64_t n_next, void* ws, size_t ws_bytes,
+                   void* stream, bool filled);
 
 // the thread's ncf_last_error() text (printf format); returns code
 int set_error(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
@@ -830,7 +836,9 @@ hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, vo
                                      const int32_t* next_items = nullptr, int64_t n_next = 0,
                                      const MlpDeferred* mlp = nullptr, int next_fold = 0,
                                      const MetricsDeferred* met = nullptr, const float* grad_rows = nullptr,
-                                     bool unsorted_lists = false);
+                                     bool unsorted_lists = false, bool may_drop = true);
+// (may_drop false: a fill overflow does not drop the step — data parallelism, where a rank that
+// skipped its step would leave the replicas apart; the error is still reported)
 // (grad_rows: the contribution rows the list indexes; default the workspace's per-sample rows gs)
 // (unsorted_lists: the index came from the in-kernel fill (FillArgs): the launch orders each row's
 // list itself and checks the touched rows' counters for a stale count)
@@ -845,12 +853,20 @@ hipError_t launch_emb_grad_dense(const ncf_shape_t& s, const WsLayout& L, void* 
 // one launch; launch_apply_fused = table-row update with a dense gradient + dense-layer update in
 // one launch.  Bitwise the unfolded sequences.
 bool part_tail_foldable(const ncf_shape_t& s, const ncf_hyper_t& h, int nslab);
+// launch_part_tail over the in-kernel fill's unsorted lists (FillArgs): the dense gradient of rows
+// [row_begin, num_rows) with each row's contributions in ascending order (bitwise launch_part_tail
+// over the sorted index), heavy rows in the first blocks
+hipError_t launch_part_tail_unsorted(const ncf_shape_t& s, const WsLayout& L, void* ws, float* emb_grad,
+                                     int64_t row_begin, float* mlp_grad, int nslab, int nbce, int nmet, float n_groups,
+                                     float* summary, hipStream_t st);
 hipError_t launch_part_tail(const ncf_shape_t& s, const WsLayout& L, void* ws, float* emb_grad, int64_t row_begin,
                             float* mlp_grad, int nslab, int nbce, int nmet, float n_groups, float* summary,
                             hipStream_t st);
+// parts: 1 the table rows only, 2 the dense layers only, 3 both (the split user-partitioned step runs
+// the item rows before its all-gather and the dense layers beside it)
 hipError_t launch_apply_fused(const ncf_shape_t& s, float* emb, float* m, float* v, const float* emb_grad,
                               int64_t rows, float* mlp, float* mlp_m, float* mlp_v, const float* mlp_grad,
-                              const int32_t* step, const ncf_hyper_t& h, hipStream_t st);
+                              const int32_t* step, const ncf_hyper_t& h, hipStream_t st, int parts = 3);
 // mlp: reduce slabs (if nslab > 0) or read grad_in; optionally write grad_out; optionally update
 // summary_nbce >= 0: the first-level slab reduction also writes the batch summary (what
 // launch_summary(L, ws, summary_nbce, summary_nmet, n_groups, 0, 0, summary) does)

@@ -724,6 +724,41 @@ __device__ __forceinline__ void row_adam(float4* __restrict__ emb, float4* __res
     }
 }
 
+// A heavy row's list [o, o + c) (in-kernel fill: unsorted; its lowest `res` slots unfilled) sorted
+// ascending into slist[o, o + c - res), block-wide: each entry's rank among the row's from the
+// list staged through LDS a chunk at a time.  Whole block; ends with a barrier (the sorted list is
+// the workgroup's own stores).
+__device__ inline void sort_heavy_list(const int32_t* __restrict__ clist, int o, int c, int res, int mcap,
+                                       int32_t* __restrict__ slist, int* chunk) {
+    int e[4], rk[4];
+    for (int j0 = 0; j0 < c; j0 += 4 * kBlock) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+            const int j = j0 + a * kBlock + (int)threadIdx.x;
+            e[a] = j >= res && j < c ? (int)min((unsigned)clist[o + j], (unsigned)(mcap - 1)) : INT_MAX;
+            rk[a] = 0;
+        }
+        for (int i0 = 0; i0 < c; i0 += kHeavyChunk) {
+            const int ni = min(kHeavyChunk, c - i0);
+            __syncthreads();
+            for (int i = threadIdx.x; i < ni; i += kBlock)
+                chunk[i] = i0 + i >= res ? (int)min((unsigned)clist[o + i0 + i], (unsigned)(mcap - 1)) : INT_MAX;
+            __syncthreads();
+            for (int i = 0; i < ni; ++i) {
+                const int x = chunk[i];
+#pragma unroll
+                for (int a = 0; a < 4; ++a) rk[a] += x < e[a];
+            }
+        }
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+            const int j = j0 + a * kBlock + (int)threadIdx.x;
+            if (j >= res && j < c) slist[o + rk[a]] = e[a];
+        }
+    }
+    __syncthreads();
+}
+
 template <bool UNSORTED>
 __global__ __launch_bounds__(kBlock, UNSORTED ? NCF_TOUCHED_MIN_BLOCKS_UNSORTED : NCF_TOUCHED_MIN_BLOCKS) void k_emb_adam_touched(float4* __restrict__ emb, float4* __restrict__ m4,
                                                              float4* __restrict__ v4, uint32_t w4,
@@ -766,34 +801,7 @@ __global__ __launch_bounds__(kBlock, UNSORTED ? NCF_TOUCHED_MIN_BLOCKS_UNSORTED 
 #endif
             // the key's residue: slots [0, res) were never filled (fill_wave; the light rows' rule)
             const int res = min(max(so.cursor[r], 0), c);
-            // rank of each entry among the row's: the list staged through LDS a chunk at a time
-            int e[4], rk[4];
-            for (int j0 = 0; j0 < c; j0 += 4 * kBlock) {
-#pragma unroll
-                for (int a = 0; a < 4; ++a) {
-                    const int j = j0 + a * kBlock + (int)threadIdx.x;
-                    e[a] = j >= res && j < c ? (int)min((unsigned)clist[o + j], (unsigned)(so.mcap - 1)) : INT_MAX;
-                    rk[a] = 0;
-                }
-                for (int i0 = 0; i0 < c; i0 += kHeavyChunk) {
-                    const int ni = min(kHeavyChunk, c - i0);
-                    __syncthreads();
-                    for (int i = threadIdx.x; i < ni; i += kBlock)
-                        chunk[i] = i0 + i >= res ? (int)min((unsigned)clist[o + i0 + i], (unsigned)(so.mcap - 1)) : INT_MAX;
-                    __syncthreads();
-                    for (int i = 0; i < ni; ++i) {
-                        const int x = chunk[i];
-#pragma unroll
-                        for (int a = 0; a < 4; ++a) rk[a] += x < e[a];
-                    }
-                }
-#pragma unroll
-                for (int a = 0; a < 4; ++a) {
-                    const int j = j0 + a * kBlock + (int)threadIdx.x;
-                    if (j >= res && j < c) so.slist[o + rk[a]] = e[a];
-                }
-            }
-            __syncthreads();  // the sorted list is the workgroup's own stores
+            sort_heavy_list(clist, o, c, res, so.mcap, so.slist, chunk);
             const bool mine = r < ca.lazy_rows;
             int rs = mine ? row_step[r] : 0;
             const bool fresh = rs == NCF_ROW_PRISTINE;
@@ -1370,6 +1378,154 @@ __global__ __launch_bounds__(kBlock) void k_part_tail(float4* __restrict__ out, 
 }
 
 
+// The dense gradient of the replicated rows [U, R) (the user-partitioned step's item rows) from the
+// in-kernel fill's UNSORTED lists (FillArgs): each row's contributions ordered by the touched-row
+// update's rules — a light row's entries ranked across the lanes of its row group, a heavy row's
+// (more than hc entries) sorted block-wide into slist by the first blocks — so every row sums in
+// ascending contribution order, bitwise the sorted index's emb_grad_dense_body; a counted key's
+// unfilled slots (its residue, left for the update launch to clear) are skipped; a row without
+// contributions gets zeros.  Offsets come from the scan ahead's per-block offsets (offs_local) and
+// the block totals' prefixes (no offs array exists).
+struct ItemGradArgs {
+    const int32_t* local;      // ws offs_local
+    const int32_t* tot;        // ws tot
+    int nscan;                 // scan blocks (<= kMaxFillScan)
+    const int32_t* clist;      // ws list
+    const int32_t* cursor;     // ws cnt (residues; read only)
+    const int32_t* touched;    // the fill's touched rows and their (offset, count)
+    const int2* toc;
+    const int32_t* heavy;      // touched-list positions of the heavy rows
+    const int32_t* heavy_n;
+    int nheavy;                // heavy blocks (the first blocks of the launch)
+    int32_t* slist;            // sorted heavy lists (this launch writes the item rows' ranges)
+    int hc, mcap;
+};
+
+__global__ __launch_bounds__(kBlock) void k_part_tail_unsorted(float4* __restrict__ out, int64_t U, int64_t R,
+                                                               uint32_t w4, const float4* __restrict__ gs,
+                                                               uint32_t ngrad, int P, const float* __restrict__ slabs,
+                                                               int nslab, int nmlp, float* __restrict__ mlp_grad,
+                                                               SummaryArgs sa, ItemGradArgs ig) {
+    int b = (int)blockIdx.x;
+    if (b < ig.nheavy) {
+        __shared__ int chunk[kHeavyChunk];
+        const int nh = *ig.heavy_n;
+        for (int hi = b; hi < nh; hi += ig.nheavy) {
+            const int u = ig.heavy[hi];
+            const int64_t r = ig.touched[u];
+            if (r < U || r >= R) continue;  // a user row: the touched-row update's (block-uniform)
+            const int2 oc = ig.toc[u];
+            const int res = min(max(ig.cursor[r], 0), oc.y);
+            sort_heavy_list(ig.clist, oc.x, oc.y, res, ig.mcap, ig.slist, chunk);
+            const int cv = oc.y - res;
+            for (uint32_t q = threadIdx.x; q < w4; q += kBlock) {
+                float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+                int j = 0;
+                for (; j + 4 <= cv; j += 4) {
+                    const int c0 = ig.slist[oc.x + j], c1 = ig.slist[oc.x + j + 1];
+                    const int c2 = ig.slist[oc.x + j + 2], c3 = ig.slist[oc.x + j + 3];
+                    const float4 g0 = gs[(size_t)c0 * w4 + q], g1 = gs[(size_t)c1 * w4 + q];
+                    const float4 g2 = gs[(size_t)c2 * w4 + q], g3 = gs[(size_t)c3 * w4 + q];
+                    g = f4add(g, g0);
+                    g = f4add(g, g1);
+                    g = f4add(g, g2);
+                    g = f4add(g, g3);
+                }
+                for (; j < cv; ++j) g = f4add(g, gs[(size_t)ig.slist[oc.x + j] * w4 + q]);
+                out[(size_t)(r - U) * w4 + q] = g;
+            }
+            __syncthreads();  // slist / chunk reused by the block's next heavy row
+        }
+        return;
+    }
+    b -= ig.nheavy;
+    if (b < nmlp) {
+        const float g = slab_grad16(slabs, P, nslab, b);
+        const int i = b * 16 + (threadIdx.x & 15);
+        if ((threadIdx.x >> 4) == 0 && i < P) mlp_grad[i] = g;
+        return;
+    }
+    b -= nmlp;
+    if (sa.summary) {
+        if (b == 0) {
+            __shared__ float red[4];
+            summary_body(sa.part_bce, sa.nbce, sa.part_hit, sa.part_dcg, sa.nmet, sa.n_groups, nullptr, 0, nullptr, 0,
+                         sa.summary, red);
+            return;
+        }
+        --b;
+    }
+    // the dense pass: block prefixes of the scan-block totals in LDS, then row groups over [U, R)
+    __shared__ int pre[kMaxFillScan];
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        const int t0 = lane < ig.nscan ? ig.tot[lane] : 0, t1 = lane + 64 < ig.nscan ? ig.tot[lane + 64] : 0;
+        int a0 = t0, a1 = t1;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int x0 = __shfl_up(a0, d, 64), x1 = __shfl_up(a1, d, 64);
+            if (lane >= d) a0 += x0, a1 += x1;
+        }
+        pre[lane] = a0 - t0;
+        pre[lane + 64] = __shfl(a0, 63, 64) + a1 - t1;
+    }
+    __syncthreads();
+    const RowLanes rl(w4);
+    const int lane = threadIdx.x & 63;
+    const int gsz = w4 <= 64 ? (int)w4 : 64;
+    const int base = w4 <= 64 ? rl.sub * (int)w4 : 0;
+    const int ql = lane - base;
+    const int64_t wave = ((int64_t)b * kBlock + threadIdx.x) >> 6;
+    const int64_t istep = (((int64_t)ngrad * kBlock) >> 6) * rl.rpw;
+    for (int64_t i0 = U + wave * rl.rpw; i0 < R; i0 += istep) {  // wave-uniform
+        const int64_t r = i0 + rl.sub;
+        const bool has = rl.on && r < R;
+        int c = 0, o = 0;
+        if (has) {
+            const int lo = ig.local[r];
+            const int hi = (r + 1) % kScanBlock != 0 ? ig.local[r + 1] : ig.tot[r / kScanBlock];
+            c = hi - lo;
+            o = lo + pre[r / kScanBlock];
+        }
+        const bool heavy = c > ig.hc;
+        const int cl = heavy ? 0 : c;
+        const int res = has && cl > 0 ? min(max(ig.cursor[r], 0), cl) : 0;
+        const bool valid = ql >= res && ql < cl;
+        const int e = valid ? (int)min((unsigned)ig.clist[o + ql], (unsigned)(ig.mcap - 1)) : INT_MAX;
+        int cmax = 0;
+        for (int g = 0; g < rl.rpw; ++g) cmax = max(cmax, __builtin_amdgcn_readlane(cl, g * (int)w4));
+        int rank = 0;
+        for (int j = 0; j < cmax; ++j) {
+            const int x = __shfl(e, base + j, 64);
+            rank += j < cl && x < e;
+        }
+        const int cv = cl - res;
+        const int to = valid ? base + rank : ql < res ? base + cv + ql : lane;
+        const int srt = __builtin_amdgcn_ds_permute(to * 4, e);
+        for (uint32_t q = w4 <= 64 ? (uint32_t)ql : (uint32_t)lane; ; q += 64) {
+            const bool act = has && !heavy && q < w4 && ql < gsz;
+            float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int j = 0; j < cmax; j += 4) {
+                const int c0 = __shfl(srt, base + j, 64), c1 = __shfl(srt, base + min(j + 1, gsz - 1), 64);
+                const int c2 = __shfl(srt, base + min(j + 2, gsz - 1), 64);
+                const int c3 = __shfl(srt, base + min(j + 3, gsz - 1), 64);
+                const bool v0 = act && j < cv, v1 = act && j + 1 < cv, v2 = act && j + 2 < cv, v3 = act && j + 3 < cv;
+                float4 g0, g1, g2, g3;
+                if (v0) g0 = gs[(size_t)c0 * w4 + q];
+                if (v1) g1 = gs[(size_t)c1 * w4 + q];
+                if (v2) g2 = gs[(size_t)c2 * w4 + q];
+                if (v3) g3 = gs[(size_t)c3 * w4 + q];
+                if (v0) g = f4add(g, g0);
+                if (v1) g = f4add(g, g1);
+                if (v2) g = f4add(g, g2);
+                if (v3) g = f4add(g, g3);
+            }
+            if (act) out[(size_t)(r - U) * w4 + q] = g;
+            if (w4 <= 64 || q + 64 >= w4) break;
+        }
+    }
+}
+
 template <int OPT>
 __global__ __launch_bounds__(kBlock) void k_mlp_update(float* __restrict__ p, float* __restrict__ m,
                                                        float* __restrict__ v, int P, const float* __restrict__ slabs,
@@ -1747,7 +1903,7 @@ hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, vo
                                      float* v, int32_t* row_step, int32_t* step, const ncf_hyper_t& h,
                                      hipStream_t st, const int32_t* next_users, const int32_t* next_items,
                                      int64_t n_next, const MlpDeferred* mlp, int next_fold, const MetricsDeferred* met,
-                                     const float* grad_rows, bool unsorted_lists) {
+                                     const float* grad_rows, bool unsorted_lists, bool may_drop) {
 #if NCF_DIAG_UPD == 1  // diagnostic timing builds only (wrong numerics): no catch-up ahead
     const bool replay_ahead = false;
 #else
@@ -1784,7 +1940,7 @@ hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, vo
             // heavy rows are rare (lists longer than a row group's lanes): a few blocks stride over them
             so = SortRows{1, unsorted_heavy_c(s), 32, at<const int32_t>(ws, L.heavy), at<const int32_t>(ws, L.heavy_n),
                           at<int32_t>(ws, L.cnt), at<int32_t>(ws, L.err), at<int32_t>(ws, L.slist),
-                          (int)(2 * L.max_batch), at<const int32_t>(ws, L.stale_step),
+                          (int)(2 * L.max_batch), may_drop ? at<const int32_t>(ws, L.stale_step) : nullptr,
                           at<const int32_t>(ws, L.offs_local), at<const int32_t>(ws, L.tot)};
         }
         launch(unsorted_lists ? k_emb_adam_touched<true> : k_emb_adam_touched<false>, (unsigned)so.nheavy + nupd + ncount + (unsigned)mt.nblocks + (unsigned)mm.nblocks,
@@ -1826,14 +1982,38 @@ hipError_t launch_part_tail(const ncf_shape_t& s, const WsLayout& L, void* ws, f
     return hipGetLastError();
 }
 
+hipError_t launch_part_tail_unsorted(const ncf_shape_t& s, const WsLayout& L, void* ws, float* emb_grad,
+                                     int64_t row_begin, float* mlp_grad, int nslab, int nbce, int nmet, float n_groups,
+                                     float* summary, hipStream_t st) {
+    if (L.world != 0 || L.nscan > kMaxFillScan || unsorted_heavy_c(s) < kHeavyMin || row_begin > s.num_rows)
+        return hipErrorInvalidValue;
+    const int P = s.mlp_params;
+    const int nmlp = (P + 15) / 16;
+    SummaryArgs sa{summary, at<float>(ws, L.part_bce), at<float>(ws, L.part_hit), at<float>(ws, L.part_dcg), nbce,
+                   nmet, n_groups};
+    const uint32_t w4 = (uint32_t)(s.row_width / 4);
+    const int64_t rows = s.num_rows - row_begin;
+    const unsigned ngrad = rows > 0 ? row_grid(rows, w4, kUpdateGrid) : 0u;
+    const ItemGradArgs ig{at<const int32_t>(ws, L.offs_local), at<const int32_t>(ws, L.tot), L.nscan,
+                          at<const int32_t>(ws, L.list), at<const int32_t>(ws, L.cnt), at<const int32_t>(ws, L.touched),
+                          at<const int2>(ws, L.touched_oc), at<const int32_t>(ws, L.heavy),
+                          at<const int32_t>(ws, L.heavy_n), 32, at<int32_t>(ws, L.slist), unsorted_heavy_c(s),
+                          (int)(2 * L.max_batch)};
+    launch(k_part_tail_unsorted, (unsigned)ig.nheavy + (unsigned)nmlp + (summary ? 1u : 0u) + ngrad, kBlock, 0, st,
+           (float4*)emb_grad, (int64_t)row_begin, (int64_t)s.num_rows, w4, at<const float4>(ws, L.gs), ngrad, P,
+           at<const float>(ws, L.slabs), nslab, nmlp, mlp_grad, sa, ig);
+    return hipGetLastError();
+}
+
 hipError_t launch_apply_fused(const ncf_shape_t& s, float* emb, float* m, float* v, const float* emb_grad,
                               int64_t rows, float* mlp, float* mlp_m, float* mlp_v, const float* mlp_grad,
-                              const int32_t* step, const ncf_hyper_t& h, hipStream_t st) {
+                              const int32_t* step, const ncf_hyper_t& h, hipStream_t st, int parts) {
     const uint32_t w4 = (uint32_t)(s.row_width / 4);
-    const uint32_t n4 = (uint32_t)(rows * w4);
+    const uint32_t n4 = (parts & 1) ? (uint32_t)(rows * w4) : 0u;
     const int P = s.mlp_params;
-    const unsigned gridp = (unsigned)((P + kBlock - 1) / kBlock);
+    const unsigned gridp = (parts & 2) ? (unsigned)((P + kBlock - 1) / kBlock) : 0u;
     const uint32_t nupd = n4 ? (uint32_t)kUpdateGrid : 0u;
+    if (nupd + gridp == 0) return hipSuccess;
     if (h.optimizer == NCF_OPT_ADAM)
         launch(k_emb_update_mlp<NCF_OPT_ADAM>, nupd + gridp, kBlock, 0, st, (float4*)emb, (float4*)m, (float4*)v, n4,
                w4, (const float4*)emb_grad, nupd, mlp, mlp_m, mlp_v, P, mlp_grad, step, h.lr, h.beta_1, h.beta_2,

@@ -681,11 +681,11 @@ def test_user_partitioned_full_config_c_tables_gpu(per, split):
     assert gpu_available()
 
 
-def _gpu_native_comm_worker(rank, world, port, q):
-    _reporting(_gpu_native_comm_worker_body, rank, world, port, q)
+def _gpu_native_comm_worker(rank, world, port, q, per=256):
+    _reporting(lambda *a: _gpu_native_comm_worker_body(*a, per=per), rank, world, port, q)
 
 
-def _gpu_native_comm_worker_body(rank, world, port, q):
+def _gpu_native_comm_worker_body(rank, world, port, q, per=256):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path[:0] = [here, os.path.dirname(here), os.path.join(os.path.dirname(here), "movierecommender-tf-trt_amd")]
@@ -695,7 +695,6 @@ def _gpu_native_comm_worker_body(rank, world, port, q):
     dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world,
                             device_id=torch.device("cuda", 0))
     shape, w = _weights(SHAPE_C)
-    per = 256
     out = []
     for native, split in ((True, False), (False, False), (True, True), (False, True)):
         eng = NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=per, lazy_adam=True,
@@ -735,15 +734,19 @@ def _gpu_native_comm_worker_body(rank, world, port, q):
 
 
 @pytest.mark.gpu
-def test_user_partitioned_native_comm_step_bitwise_gpu():
+@pytest.mark.parametrize("per", [256, 4096])
+def test_user_partitioned_native_comm_step_bitwise_gpu(per):
     """ncf_user_dp_step (one library call per step, the all-reduce on the library's own RCCL
     communicator and side stream) against the same step issued call by call from Python with
     torch.distributed's all-reduce: one rank over RCCL (the box has one GPU), 10 steps with the next
-    batch counted ahead (one step not), bitwise equal weights, moments, iteration count, metrics."""
+    batch counted ahead (one step not), bitwise equal weights, moments, iteration count, metrics.
+    At 4,096 samples the one-call step fills its index inside the forward/backward launch and
+    orders the unsorted lists in the gradient tail and the own-user update (round 6); the call-by-
+    call step builds and sorts it with launches of its own: same sums in the same order."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    p = ctx.Process(target=_gpu_native_comm_worker, args=(0, 1, port, q))
+    p = ctx.Process(target=_gpu_native_comm_worker, args=(0, 1, port, q, per))
     p.start()
     out, emu, U, w0 = _get(q, 1)[0]
     p.join(timeout=120)
