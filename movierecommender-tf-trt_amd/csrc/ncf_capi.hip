@@ -1032,8 +1032,7 @@ int dp_forward_backward(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* o
 // fill (dp_forward_backward)
 int dp_update_rows(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* h, int64_t n,
                    const int32_t* next_users, const int32_t* next_items, int64_t n_next, void* ws, size_t ws_bytes,
-                   void* stream, bool filled) {
-    if (!filled) return ncf_update_rows_lazy(s, model, optim, h, n, next_users, next_items, n_next, ws, ws_bytes, stream);
+                   void* stream, bool filled, bool scan_ahead) {
     if (int r = check_lazy_dp(s, model, optim, h)) return r;
     if ((next_users || next_items) && (!next_users || !next_items || n_next != n || h->optimizer != NCF_OPT_ADAM))
         return fail(NCF_EINVAL, "next batch: NULL ids, n_next != n, or not Adam");
@@ -1043,10 +1042,10 @@ int dp_update_rows(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* optim,
     prof_begin(NCF_K_EMB_UPDATE, st);
     hipError_t e = launch_emb_update_touched(*s, L, ws, model->emb, optim->emb_m, optim->emb_v, optim->row_step,
                                              optim->step, *h, st, next_users, next_items, next_users ? n_next : 0,
-                                             nullptr, index_fold(*s, h), nullptr, nullptr, true, false);
+                                             nullptr, index_fold(*s, h), nullptr, nullptr, filled, false);
     prof_end(NCF_K_EMB_UPDATE, st);
     if (e != hipSuccess) return hip_check(e, "touched-row update");
-    if (next_users) {
+    if (next_users && scan_ahead) {  // (else the caller's stats launch scans: launch_stats(..., scan_ahead))
         e = launch_scan_ahead(L, ws, s->num_rows, st);
         if (e != hipSuccess) return hip_check(e, "scan ahead");
     }

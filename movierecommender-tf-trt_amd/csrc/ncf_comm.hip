@@ -287,28 +287,30 @@ int ncf_user_dp_step_split(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t
     }
     if (int r = mark(c, kC1, side)) return r;
     if (int r = hip_ok(hipEventRecord(c->join, side), "join")) return r;
-    // the own users' update, the next batch counted (own rows caught up ahead) and scanned
-    if (int r = ncf::dp_update_rows(s, model, optim, h, n, next_users, next_items, n_next, ws, ws_bytes, stream, filled))
+    // the own users' update, the next batch counted (own rows caught up ahead); its counts are
+    // scanned by this step's stats launch when the apply is split below (k_stats_scan), else here
+    const int64_t r0 = item_rank * Ic;
+    const int64_t cnt = r0 >= I ? 0 : (I - r0 < Ic ? I - r0 : Ic);
+    const bool split_apply = cnt > 0 && ncf::part_tail_foldable(*s, *h, 1 << 30);
+    if (int r = ncf::dp_update_rows(s, model, optim, h, n, next_users, next_items, n_next, ws, ws_bytes, stream, filled,
+                                    !split_apply))
         return r;
     if (int r = mark(c, kJ0, st)) return r;
     if (int r = hip_ok(hipStreamWaitEvent(st, c->join, 0), "join wait")) return r;
     if (int r = mark(c, kJ1, st)) return r;
     // this rank's item slice (its moments indexed by table row) and the dense layers
-    const int64_t r0 = item_rank * Ic;
-    const int64_t cnt = r0 >= I ? 0 : (I - r0 < Ic ? I - r0 : Ic);
     ncf_optim_t items_opt = *optim;
     if (items_opt.emb_m) items_opt.emb_m += (U + r0) * W;
     if (items_opt.emb_v) items_opt.emb_v += (U + r0) * W;
     items_opt.row_step = nullptr;
     // Every L2 factor zero (the fused apply): only the item slice's Adam precedes the all-gather; the
-    // dense layers' Adam and the stats (step bump) run on the compute stream BESIDE it, with the next
-    // batch's index — off the exchange's critical path (round 6; same kernels' arithmetic, so the
-    // states stay bitwise those of ncf_apply_update)
-    const bool split_apply = cnt > 0 && ncf::part_tail_foldable(*s, *h, 1 << 30);
+    // dense layers' Adam and the stats (step bump, the next batch's scan) run on the compute stream
+    // BESIDE it — off the exchange's critical path (round 6; same kernels' arithmetic, so the states
+    // stay bitwise those of ncf_apply_update).  One rank (no all-gather): both in one launch.
     if (split_apply) {
         if (int r = hip_ok(ncf::launch_apply_fused(*s, model->emb + (U + r0) * W, items_opt.emb_m, items_opt.emb_v,
-                                                   slice_grad, cnt, nullptr, nullptr, nullptr, nullptr, optim->step, *h,
-                                                   st, 1),
+                                                   slice_grad, cnt, model->mlp, optim->mlp_m, optim->mlp_v, mlp_grad,
+                                                   optim->step, *h, st, exchange ? 1 : 3),
                            "item-slice update"))
             return r;
     } else if (int r = ncf_apply_update(s, model, &items_opt, h, U + (cnt ? r0 : I), cnt, slice_grad, mlp_grad, summary,
@@ -317,13 +319,17 @@ int ncf_user_dp_step_split(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t
     }
     auto dense_and_stats = [&]() -> int {
         if (!split_apply) return 0;
-        if (int r = hip_ok(ncf::launch_apply_fused(*s, nullptr, nullptr, nullptr, nullptr, 0, model->mlp, optim->mlp_m,
-                                                   optim->mlp_v, mlp_grad, optim->step, *h, st, 2),
-                           "dense-layer update"))
-            return r;
-        // (as ncf_apply_update: the stats read only the caller's summary, so the one-sample layout serves)
-        const ncf::WsLayout L = ncf::make_layout(*s, 1);
-        return hip_ok(ncf::launch_stats(L, ws, summary, 0, 0, h->inv_batch, stats, optim->step, true, st), "stats");
+        if (exchange)
+            if (int r = hip_ok(ncf::launch_apply_fused(*s, nullptr, nullptr, nullptr, nullptr, 0, model->mlp,
+                                                       optim->mlp_m, optim->mlp_v, mlp_grad, optim->step, *h, st, 2),
+                               "dense-layer update"))
+                return r;
+        // the stats (they read only the caller's summary) and the next batch's count scan in one
+        // launch (k_stats_scan); the scan's regions sit where the batch's layout puts them
+        const ncf::WsLayout L = ncf::make_layout(*s, n);
+        return hip_ok(ncf::launch_stats(L, ws, summary, 0, 0, h->inv_batch, stats, optim->step, true, st,
+                                        next_users != nullptr, s->num_rows),
+                      "stats");
     };
     if (!exchange) return dense_and_stats();
     // the updated slices to every rank (in place) on the side stream, while the compute stream runs

@@ -612,7 +612,7 @@ int dp_forward_backward(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* o
                         void* stream, bool* filled);
 int dp_update_rows(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t* optim, const ncf_hyper_t* h, int64_t n,
                    const int32_t* next_users, const int32_t* next_items, int64_t n_next, void* ws, size_t ws_bytes,
-                   void* stream, bool filled);
+                   void* stream, bool filled, bool scan_ahead = true);
 
 // the thread's ncf_last_error() text (printf format); returns code
 int set_error(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
