@@ -219,13 +219,17 @@ int fb_variant(const ncf_shape_t& s, const ncf_hyper_t* h, int64_t n) {
 }
 
 // user-row folding of a step's index and fused kernel (ncf_internal.h fold_of); h NULL: none.
-// NCF_FOLD_USERS=0 turns it off (A/B measurements)
+// NCF_FOLD_USERS=0 turns it off (A/B measurements).  The layered path (config D) folds in
+// k_lay_l1b since round 6; -DNCF_LAYERED_FOLD=0 builds the unfolded layered step (A/B)
+#ifndef NCF_LAYERED_FOLD
+#define NCF_LAYERED_FOLD 1
+#endif
 int index_fold(const ncf_shape_t& s, const ncf_hyper_t* h) {
     static const bool on = [] {
         const char* e = ncf::experiment_env("NCF_FOLD_USERS");
         return !e || atoi(e) != 0;
     }();
-    return h && on ? ncf::fold_of(h->group, use_fused(s, h)) : 0;
+    return h && on ? ncf::fold_of(h->group, use_fused(s, h) || (NCF_LAYERED_FOLD && use_layered(s, h))) : 0;
 }
 
 
@@ -651,7 +655,7 @@ static int run_fb(const ncf_shape_t& s, const ncf::WsLayout& L, const ncf_model_
                                  h->group, h->k, &out->nslab, &out->nbce, &out->nmet, st, fold);
     else if (use_layered(s, h))
         e = ncf::launch_fb_layered(s, L, ws, model->emb, model->mlp, users, items, labels, n, h->inv_batch, ids,
-                                   &out->nslab, &out->nbce, st);
+                                   &out->nslab, &out->nbce, st, fold);
     else
         e = ncf::launch_fb_generic(s, L, ws, model->emb, model->mlp, users, items, labels, n, h->inv_batch, ids,
                                    &out->nslab, &out->nbce, st);

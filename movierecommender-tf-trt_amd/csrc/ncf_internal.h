@@ -246,6 +246,7 @@ __device__ inline void scan_local_body(const int32_t* cnt, int64_t r1, int32_t* 
 // contribution c = 2 * head; the others' user contributions do not exist.  Samples whose user
 // differs from the head's keep their own contribution, so any batch stays exact.  Fold widths
 // 2, 4 (the reference's default: 3 negatives) and 8 have fused-kernel variants.
+// fused: the step runs a kernel that folds (the fused MFMA kernels and the layered path's k_lay_l1b)
 inline int fold_of(int group, bool fused) { return fused && (group == 2 || group == 4 || group == 8) ? group : 0; }
 __device__ __forceinline__ bool folded_user(const int32_t* __restrict__ users, int64_t i, int fold) {
     if (fold <= 1) return false;
@@ -751,7 +752,7 @@ bool layered_supported(const ncf_shape_t& s);
 bool layered_all_mfma(const ncf_shape_t& s);  // == layered_supported (no vendor-GEMM variant remains)
 hipError_t launch_fb_layered(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, const float* mlp,
                              const int32_t* users, const int32_t* items, const float* labels, int64_t n,
-                             float inv_batch, IdSpace ids, int* nslab, int* nbce, hipStream_t st);
+                             float inv_batch, IdSpace ids, int* nslab, int* nbce, hipStream_t st, int fold = 0);
 // layer 1 of the layered path on hand-written MFMA (ncf_layer1.hip, config D's widths):
 // forward = gather + X0 + (gmf != nullptr) GMF product + relu(W1^T x + b1); backward = dX = W1 G1 into the
 // gradient rows gs with their GMF part (the replaced gather / GEMM / bias / scatter kernels' outputs)
@@ -764,7 +765,7 @@ hipError_t launch_layer1_dw(const ncf_shape_t& s, const float* x0, const float* 
                             int nchunks, float* slabs, hipStream_t st);
 hipError_t launch_layer1_bwd(const ncf_shape_t& s, const float* emb, const float* mlp, const int32_t* users,
                              const int32_t* items, int64_t n, IdSpace ids, const float* dzo, const float* g1,
-                             float* gs, hipStream_t st);
+                             float* gs, hipStream_t st, int fold = 0);  // fold: user-row folding (fold_of)
 // layers 2.. of the layered path in one hand-written MFMA kernel (ncf_laymid.hip, config D's widths):
 // from H1 and the rows' GMF vectors to probs, dz, G1 (row-major), the BCE partials and, per workgroup
 // (grid of them), one slab of every dense parameter after layer 1

@@ -83,6 +83,19 @@ __device__ __forceinline__ void load_w1(float* wl, const float* __restrict__ mlp
     __syncthreads();
 }
 
+// sum over this lane's group of FOLD consecutive sample lanes (DPP quad butterfly, ds_swizzle for the
+// third step): every lane of the group gets it, the group head's association is ((s0 + s1) + (s2 +
+// s3)) as the fused kernels fold (ncf_wave.hip fold_sum)
+template <int FOLD>
+__device__ __forceinline__ float fold_sum(float x) {
+    static_assert(FOLD == 2 || FOLD == 4 || FOLD == 8, "fold width");
+    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xB1, 0xF, 0xF, false));  // [1,0,3,2]
+    if constexpr (FOLD >= 4)
+        x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x4E, 0xF, 0xF, false));  // [2,3,0,1]
+    if constexpr (FOLD >= 8) x += __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(x), 0x1F | (4 << 10)));
+    return x;
+}
+
 template <int NB>
 __device__ __forceinline__ void ldsv(const float* p, float (&o)[NB]) {
     if constexpr (NB == 8) {
@@ -207,7 +220,11 @@ __global__ __launch_bounds__(64 * NW, 1) void k_lay_l1f(const float* __restrict_
     }
 }
 
-template <class S, int NW>
+// FOLD (2, 4, 8; 0 none): user-row folding (ncf_internal.h fold_of) — the user-side gradient rows of
+// a group of FOLD samples that share the head's user are summed in fixed order into the head's row
+// (its contribution c = 2 hd) and the other samples' user rows are not written (the index skips
+// them: folded_user); a sample whose user is not its head's keeps its own row
+template <class S, int NW, int FOLD>
 __global__ __launch_bounds__(64 * NW, 1) void k_lay_l1b(const float* __restrict__ emb, const float* __restrict__ mlp,
                                                     int wo_off, const int32_t* __restrict__ users,
                                                     const int32_t* __restrict__ items, int64_t n, IdSpace ids,
@@ -238,6 +255,21 @@ __global__ __launch_bounds__(64 * NW, 1) void k_lay_l1b(const float* __restrict_
         int cu = 0, cv = 0;
         if (in) cu = users[s], cv = items[s];
         const bool ok = in && (unsigned)cu < (unsigned)ids.ubound && (unsigned)cv < (unsigned)ids.ibound;
+        // folding: this sample's user is its group head's (lane li & ~(FOLD - 1) of the same lane group)
+        const bool fmatch = FOLD > 1 && in && cu == __shfl(cu, lane & ~(FOLD > 1 ? FOLD - 1 : 0), 64);
+        const bool fhead = FOLD <= 1 || (li & (FOLD > 1 ? FOLD - 1 : 0)) == 0;
+        const bool uwrite = in && (!fmatch || fhead);   // this sample's user row is a contribution
+        auto fold4 = [&](float4 v) {
+            if constexpr (FOLD > 1) {
+                const float4 sm = make_float4(fold_sum<(FOLD > 1 ? FOLD : 2)>(fmatch ? v.x : 0.f),
+                                              fold_sum<(FOLD > 1 ? FOLD : 2)>(fmatch ? v.y : 0.f),
+                                              fold_sum<(FOLD > 1 ? FOLD : 2)>(fmatch ? v.z : 0.f),
+                                              fold_sum<(FOLD > 1 ? FOLD : 2)>(fmatch ? v.w : 0.f));
+                return fmatch ? sm : v;
+            } else {
+                return v;
+            }
+        };
         // the GMF part's operands go out now, under the dX MFMAs
         float4 pu[GQ / 4], pi[GQ / 4], pw[GQ / 4];
         float d = 0.f;
@@ -265,25 +297,25 @@ __global__ __launch_bounds__(64 * NW, 1) void k_lay_l1b(const float* __restrict_
 #pragma unroll
                 for (int t = 0; t < B1; ++t) acc = mfma16(a[r & 1][t], U.gv[t][r], acc);
             }
-            if (in) {
-                const int f0 = 16 * ti + 4 * g;
-                const bool user = 16 * ti < D0;
+            const int f0 = 16 * ti + 4 * g;
+            const bool user = 16 * ti < D0;   // uniform: ti is
+            float4 dv = make_float4(acc[0], acc[1], acc[2], acc[3]);
+            if (user) dv = fold4(dv);
+            if (user ? uwrite : in) {
                 float* dst = (user ? ur : ir) + G + (user ? f0 : f0 - D0);
-                *reinterpret_cast<float4*>(dst) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+                *reinterpret_cast<float4*>(dst) = dv;
             }
         }
-        if (in) {
-            // GMF part: dz w_gmf * the other side's GMF vector (zero rows for a masked sample)
+        // GMF part: dz w_gmf * the other side's GMF vector (zero rows for a masked sample)
 #pragma unroll
-            for (int k = 0; k < GQ / 4; ++k) {
-                const float4 p = pu[k], q = pi[k], w = pw[k];
-                const float4 zu = ok ? make_float4(d * w.x * q.x, d * w.y * q.y, d * w.z * q.z, d * w.w * q.w)
-                                     : make_float4(0.f, 0.f, 0.f, 0.f);
-                const float4 zi = ok ? make_float4(d * w.x * p.x, d * w.y * p.y, d * w.z * p.z, d * w.w * p.w)
-                                     : make_float4(0.f, 0.f, 0.f, 0.f);
-                reinterpret_cast<float4*>(ur + GQ * g)[k] = zu;
-                reinterpret_cast<float4*>(ir + GQ * g)[k] = zi;
-            }
+        for (int k = 0; k < GQ / 4; ++k) {
+            const float4 p = pu[k], q = pi[k], w = pw[k];
+            const float4 zu = fold4(ok ? make_float4(d * w.x * q.x, d * w.y * q.y, d * w.z * q.z, d * w.w * q.w)
+                                       : make_float4(0.f, 0.f, 0.f, 0.f));
+            const float4 zi = ok ? make_float4(d * w.x * p.x, d * w.y * p.y, d * w.z * p.z, d * w.w * p.w)
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+            if (uwrite) reinterpret_cast<float4*>(ur + GQ * g)[k] = zu;
+            if (in) reinterpret_cast<float4*>(ir + GQ * g)[k] = zi;
         }
     };
     const int64_t u0 = (int64_t)blockIdx.x * NW + wv;
@@ -483,16 +515,25 @@ hipError_t launch_layer1_dw(const ncf_shape_t& s, const float* x0, const float* 
 
 hipError_t launch_layer1_bwd(const ncf_shape_t& s, const float* emb, const float* mlp, const int32_t* users,
                              const int32_t* items, int64_t n, IdSpace ids, const float* dzo, const float* g1,
-                             float* gs, hipStream_t st) {
+                             float* gs, hipStream_t st, int fold) {
     using S = L1ShapeD;
-    if (!l1matches<S>(s)) return hipErrorInvalidValue;
+    if (!l1matches<S>(s) || (fold > 1 && fold != 2 && fold != 4 && fold != 8)) return hipErrorInvalidValue;
     static bool cfg = false;
     if (!cfg) {
-        if (hipError_t e = configure<S>((const void*)k_lay_l1b<S, NCF_L1B_WAVES>)) return e;
+        if (hipError_t e = configure<S>((const void*)k_lay_l1b<S, NCF_L1B_WAVES, 0>)) return e;
+        if (hipError_t e = configure<S>((const void*)k_lay_l1b<S, NCF_L1B_WAVES, 2>)) return e;
+        if (hipError_t e = configure<S>((const void*)k_lay_l1b<S, NCF_L1B_WAVES, 4>)) return e;
+        if (hipError_t e = configure<S>((const void*)k_lay_l1b<S, NCF_L1B_WAVES, 8>)) return e;
         cfg = true;
     }
-    launch(k_lay_l1b<S, NCF_L1B_WAVES>, grid_of<S, NCF_L1B_WAVES>(n), 64 * NCF_L1B_WAVES, S::LDS, st, emb, mlp,
-           s.layer_off[0], users, items, n, ids, dzo, g1, gs);
+#define NCF_L1B_LAUNCH(F)                                                                                   \
+    launch(k_lay_l1b<S, NCF_L1B_WAVES, F>, grid_of<S, NCF_L1B_WAVES>(n), 64 * NCF_L1B_WAVES, S::LDS, st, emb, mlp, \
+           s.layer_off[0], users, items, n, ids, dzo, g1, gs)
+    if (fold == 2) NCF_L1B_LAUNCH(2);
+    else if (fold == 4) NCF_L1B_LAUNCH(4);
+    else if (fold == 8) NCF_L1B_LAUNCH(8);
+    else NCF_L1B_LAUNCH(0);
+#undef NCF_L1B_LAUNCH
     return hipGetLastError();
 }
 

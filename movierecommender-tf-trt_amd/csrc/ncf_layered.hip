@@ -12,7 +12,8 @@
 //                                 biases and the output-layer gradients (model.py:175-188, 213-214)
 //   k_lay_dw1  (ncf_layer1.hip)  dW1 = X0^T G1, one batch chunk per workgroup pair
 //   k_lay_l1b  (ncf_layer1.hip)  dX0 = G1 W1^T straight into the per-sample gradient rows, with the
-//                                 GMF part dz w_gmf * (the other side's GMF vector)
+//                                 GMF part dz w_gmf * (the other side's GMF vector); a group's user
+//                                 rows folded into its head's (user-row folding, as the fused kernels)
 //
 // The outputs are exactly those of the other forward/backward kernels (probs, gs, part_bce, one
 // dense-gradient slab per batch chunk), so the index build, the optimizer sweeps and the data-
@@ -53,7 +54,7 @@ hipError_t launch_predict_layered(const ncf_shape_t& s, const WsLayout& L, void*
 
 hipError_t launch_fb_layered(const ncf_shape_t& s, const WsLayout& L, void* ws, const float* emb, const float* mlp,
                              const int32_t* users, const int32_t* items, const float* labels, int64_t n,
-                             float inv_batch, IdSpace ids, int* nslab, int* nbce, hipStream_t st) {
+                             float inv_batch, IdSpace ids, int* nslab, int* nbce, hipStream_t st, int fold) {
     if (!layered_supported(s) || n > L.max_batch) return hipErrorInvalidValue;
     const int nl = s.num_layers;
     // activation matrices X_l [n x L_l] back to back in `act`; gradients G_l [n x L_l] (l >= 1) in
@@ -85,7 +86,7 @@ hipError_t launch_fb_layered(const ncf_shape_t& s, const WsLayout& L, void* ws, 
     if (e != hipSuccess) return e;
     e = launch_layer1_dw(s, X[0], Gd[1], n, chunk, nsl, slab, st);
     if (e != hipSuccess) return e;
-    e = launch_layer1_bwd(s, emb, mlp, users, items, n, ids, (const float*)dzo, (const float*)Gd[1], gs, st);
+    e = launch_layer1_bwd(s, emb, mlp, users, items, n, ids, (const float*)dzo, (const float*)Gd[1], gs, st, fold);
     if (e != hipSuccess) return e;
     *nbce = nsl;
     *nslab = nsl;

@@ -1,5 +1,6 @@
-"""User-row folding (include/movierec_ncf.h, "User-row folding"): the fused kernel sums the
-user-row gradients of a group's samples that share the group head's user and writes one row;
+"""User-row folding (include/movierec_ncf.h, "User-row folding"): the fused kernels (and, since
+round 6, the layered path's backward k_lay_l1b at config D's widths) sum the user-row gradients of
+a group's samples that share the group head's user and write one row;
 the index lists that one contribution.  The reference's batches always share the user within a
 group (data_pipeline.py:141), but the device path must stay exact for any batch: a sample whose
 user differs from its head's keeps its own contribution.
@@ -24,12 +25,30 @@ if gpu_available():
     from movierec.engine import NCFEngine
 
 CONFIG_C = (200, 150, [128, 64, 32, 16], 64)
+CONFIG_D_SMALL = (160, 120, [256, 128, 64, 32], 128)   # config D's widths: the layered path (k_lay_l1b folds)
+KERNELS = [None, "wave", "layered"]
+KERNEL_IDS = ["default", "wave", "layered"]
 HYPER = dict(optimizer="adam", lr=0.001, beta_1=0.9, beta_2=0.999, layers_l2reg=[0.0] * 4)
 
 
 def _weights(shape, seed):
     from test_native_gpu import _weights as w
     return w(shape, seed)
+
+
+def _dims(kernel):
+    return CONFIG_D_SMALL if kernel == "layered" else CONFIG_C
+
+
+def _engine(shape, kernel, max_batch, **kw):
+    if kernel == "layered":
+        eng = NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=max_batch,
+                        force_layered=True, **kw)
+        assert eng.kernel_for(max_batch) == "layered-mfma"
+    else:
+        eng = NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=max_batch,
+                        fb_kernel=kernel, **kw)
+    return eng
 
 
 def _mixed_batch(shape, B, group, seed, w=None):
@@ -58,19 +77,19 @@ def _mixed_batch(shape, B, group, seed, w=None):
     return users.astype(np.int32), items.astype(np.int32), y
 
 
-@pytest.mark.parametrize("kernel", [None, "wave"], ids=["default", "wave"])
+@pytest.mark.parametrize("kernel", KERNELS, ids=KERNEL_IDS)
 @pytest.mark.parametrize("group", [2, 4, 8, 16, 32])
 def test_mixed_groups_grads_match_oracle(group, kernel):
-    shape = O.NCFShape(*CONFIG_C)
+    shape = O.NCFShape(*_dims(kernel))
     w = _weights(shape, 60 + group)
     B = 1024
     users, items, y = _mixed_batch(shape, B, group, 61 + group, w)
-    eng = NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=B, fb_kernel=kernel)
+    eng = _engine(shape, kernel, B)
     eng.set_keras_weights(w)
     grads = eng.alloc_grads()
     probs = torch.empty(B, dtype=torch.float32, device="cuda")
     eng.forward_backward(users, items, y, group=group, k=2, inv_batch=1.0 / B, grads=grads, probs_out=probs)
-    _, g, _ = O.loss_and_grads(shape, w, users, items, y, [0.0] * 4)
+    _, g, _ = O.loss_and_grads(shape, w, users, items, y, [0.0] * len(shape.layers))
     got = eng.keras_weights(grads[0], grads[1])
     for name in O.weight_names(shape):
         scale = np.max(np.abs(g[name])) + 1e-12
@@ -80,13 +99,12 @@ def test_mixed_groups_grads_match_oracle(group, kernel):
     assert np.max(np.abs(probs.cpu().numpy() - pref)) <= 2e-6
 
 
-@pytest.mark.parametrize("kernel", [None, "wave"], ids=["default", "wave"])
+@pytest.mark.parametrize("kernel", KERNELS, ids=KERNEL_IDS)
 @pytest.mark.parametrize("lazy", [False, True], ids=["dense", "deferred"])
 def test_mixed_groups_train_steps_match_oracle(lazy, kernel):
-    shape = O.NCFShape(*CONFIG_C)
+    shape = O.NCFShape(*_dims(kernel))
     w = _weights(shape, 70)
-    eng = NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=512, lazy_adam=lazy,
-                    fb_kernel=kernel)
+    eng = _engine(shape, kernel, 512, lazy_adam=lazy)
     eng.set_keras_weights(w)
     ref = {k: v.copy() for k, v in w.items()}
     st = O.new_opt_state(ref)
@@ -95,7 +113,7 @@ def test_mixed_groups_train_steps_match_oracle(lazy, kernel):
     for s, (u, it, yy) in enumerate(dev):
         nxt = (dev[s + 1][0], dev[s + 1][1]) if lazy and s + 1 < len(dev) else None
         eng.train_step(u, it, yy, group=4, k=2, next_batch=nxt)
-        O.train_step(shape, ref, st, *batches[s], HYPER)
+        O.train_step(shape, ref, st, *batches[s], dict(HYPER, layers_l2reg=[0.0] * len(shape.layers)))
     eng.check_errors()
     got = eng.keras_weights()
     for name in O.weight_names(shape):
@@ -104,15 +122,14 @@ def test_mixed_groups_train_steps_match_oracle(lazy, kernel):
         assert err <= tol, (name, err, tol)
 
 
-@pytest.mark.parametrize("kernel", [None, "wave"], ids=["default", "wave"])
+@pytest.mark.parametrize("kernel", KERNELS, ids=KERNEL_IDS)
 def test_folded_step_is_deterministic(kernel):
-    shape = O.NCFShape(*CONFIG_C)
+    shape = O.NCFShape(*_dims(kernel))
     w = _weights(shape, 80)
     users, items, y = _mixed_batch(shape, 2048, 4, 81)
     outs = []
     for _ in range(2):
-        eng = NCFEngine(shape.num_users, shape.num_items, shape.layers, shape.gmf_dim, max_batch=2048,
-                        fb_kernel=kernel)
+        eng = _engine(shape, kernel, 2048)
         eng.set_keras_weights(w)
         for _ in range(2):
             eng.train_step(users, items, y, group=4, k=2)
