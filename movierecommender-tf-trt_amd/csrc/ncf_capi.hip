@@ -263,6 +263,10 @@ WsLayout make_layout(const ncf_shape_t& s, int64_t B, int world) {
     L.err = take(4);
     L.ifold = take(4);
     L.stale_step = take(4);
+    if (world == 0) {
+        L.seen = take((size_t)(K + 1) * 4);
+        L.itag = take(4);
+    }
     const int64_t S = L.shard_rows;
     if (world > 0) {
         L.ocnt = take((size_t)(S + 1) * 4);
@@ -592,7 +596,7 @@ static int run_fb(const ncf_shape_t& s, const ncf::WsLayout& L, const ncf_model_
                   const int32_t* users, const int32_t* items, const float* labels, int64_t n, void* ws,
                   float* probs_out, FbOut* out, hipStream_t st, bool sharded = false,
                   int (*after_index)(void*) = nullptr, void* ctx = nullptr, const ncf::FillArgs* fill = nullptr,
-                  bool index_filled = false) {
+                  bool index_filled = false, bool sparse_index = false) {
     hipError_t e = hipSuccess;
     ncf::IdSpace ids = ncf::table_ids(s);
     const int fold = index_fold(s, h);
@@ -630,7 +634,7 @@ static int run_fb(const ncf_shape_t& s, const ncf::WsLayout& L, const ncf_model_
         prof_begin(NCF_K_INDEX, sti);
         // deferred decay: the catch-up launch (after_index) sorts the lists in extra workgroups
         e = ncf::launch_index_build(s, L, ws, users, items, n, sti, after_index != nullptr, h->index_ready == 2,
-                                    after_index != nullptr, fold);
+                                    after_index != nullptr, fold, sparse_index);
         prof_end(NCF_K_INDEX, sti);
         if (e != hipSuccess) return hip_check(e, "index build");
         out->index_side = ss;
@@ -766,6 +770,11 @@ static int train_step_impl(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t
     fb.defer_metrics = lazy && side_stream_mode() == 0;
     const int fmode = lazy ? fill_in_kernel(*s, L, h, n) : 0;
     const bool kfill = fmode != 0;
+    // large key spaces (config D): the counted-ahead index without a pass over every key — the
+    // previous step's stats launch scanned sparsely (sparse_scan below), k_fill_touched builds from
+    // its per-block lists, and this step's update tests "in the batch" with the seen tags
+    const bool sparse_ok = lazy && !kfill && h->optimizer == NCF_OPT_ADAM && ncf::sparse_index_ok(L);
+    const bool sparse_build = sparse_ok && h->index_ready == 2;
     const ncf::FillArgs fa = kfill ? fill_args(*s, L, ws) : ncf::FillArgs{};
     if (fmode == 2) {
         prof_begin(NCF_K_INDEX, st);
@@ -775,7 +784,7 @@ static int train_step_impl(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t
     }
     if (int r = run_fb(*s, L, model, h, users, items, labels, n, ws, probs_out, &fb, st, false,
                        lazy && !kfill ? catchup_touched : nullptr, &cc, fmode == 1 ? &fa : nullptr,
-                       fmode == 2))
+                       fmode == 2, sparse_build))
         return r;
     // the index (side stream) must be complete before the side stream takes the dense tail
     if (int r = index_join(st, fb)) return r;
@@ -821,7 +830,7 @@ static int train_step_impl(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t
         e = ncf::launch_emb_update_touched(*s, L, ws, model->emb, optim->emb_m, optim->emb_v, optim->row_step,
                                            optim->step, *h, st, next_users, next_items, n_next,
                                            mlp_def.p ? &mlp_def : nullptr, index_fold(*s, h),
-                                           fb.met.nblocks > 0 ? &fb.met : nullptr, nullptr, kfill);
+                                           fb.met.nblocks > 0 ? &fb.met : nullptr, nullptr, kfill, true, sparse_build);
     else
         e = ncf::launch_emb_update(*s, L, ws, model->emb, optim->emb_m, optim->emb_v, optim->step, *h, nullptr,
                                    s->num_rows, st);
@@ -836,7 +845,7 @@ static int train_step_impl(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t
     e = ncf::launch_stats(L, ws, summary, nreg_emb, nreg_mlp, h->inv_batch, stats, optim->step, true, st,
                           lazy && next_users != nullptr, s->num_rows,
                           two_level ? ncf::SummaryFirst{fb.nbce, fb.nmet, fb.n_groups} : ncf::SummaryFirst{-1, 0, 0.f},
-                          kfill ? ncf::at<int32_t>(ws, L.stale_step) : nullptr);
+                          kfill ? ncf::at<int32_t>(ws, L.stale_step) : nullptr, sparse_ok && next_users != nullptr);
     return hip_check(e, "stats");
 }
 

@@ -287,7 +287,6 @@ __global__ __launch_bounds__(kBlock) void k_fill(KeySrc ks, int64_t m, int32_t* 
 // One workgroup, one memory round trip: thread t loads the totals of its contiguous chunk of
 // ceil(nscan / 256) scan blocks all at once (at most kPrefixPer each), sums them, one block scan
 // of the chunk sums, then the chunk's prefixes are written.
-constexpr int kPrefixPer = 32;  // chunk length cap: nscan <= 8,192 scan blocks (16.7 M keys)
 __global__ __launch_bounds__(kBlock) void k_prefix(const int32_t* __restrict__ tot, const int32_t* __restrict__ utot,
                                                    int nscan, int32_t* __restrict__ pre, int32_t* __restrict__ upre) {
     __shared__ int sw[4];
@@ -435,6 +434,72 @@ __global__ __launch_bounds__(kBlock) void k_fill_big(KeySrc ks, int64_t m, int32
     }
 }
 
+// The sparse counted index (sparse_index_ok: large key spaces, a batch counted and scanned ahead by
+// the previous step with scan_local_body<true, true>): the touched rows come from the scan's
+// per-block lists (TouchedOut: block b's occupied keys in key order at tl[b 2048 ..], their
+// (offset inside the block, count) in tocl) — block b writes its rows at upre[b] .. of the touched
+// list with offsets pre[b] + the block's, and tags each with this index's seen tag (*itag + 1: the
+// touched-row update's count blocks test "in this step's batch" with it); then the contributions,
+// k_fill_big's scheme.  Same list, touched rows (key order) and cursors as k_fill_big<.., LIST>;
+// no pass over the keys of the table (k_fill_big writes every key's offset: 44 MB at config D).
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_fill_touched(KeySrc ks, int64_t m, int32_t* __restrict__ cnt,
+                                                         const int32_t* __restrict__ local,
+                                                         const int32_t* __restrict__ pre, const int32_t* __restrict__ upre,
+                                                         const int32_t* __restrict__ utot, int nscan,
+                                                         const int32_t* __restrict__ tl, const int2* __restrict__ tocl,
+                                                         int32_t* __restrict__ touched, int2* __restrict__ toc,
+                                                         int32_t* __restrict__ nuniq, int32_t* __restrict__ seen,
+                                                         const int32_t* __restrict__ itag, int32_t* __restrict__ list,
+                                                         int32_t* __restrict__ err, int32_t* __restrict__ ifold) {
+    const int lane = threadIdx.x & 63;
+    const int b = (int)blockIdx.x;
+    if (b == 0 && threadIdx.x == 0) *ifold = ks.fold;
+    if (b < nscan) {
+        const int nb = utot[b];
+        const int pb = pre[b], ub = upre[b];
+        const int tag = *itag + 1;
+        for (int i = threadIdx.x; i < nb; i += kBlock) {
+            const int64_t e = (int64_t)b * kScanBlock + i;
+            const int key = tl[e];
+            const int2 oc = tocl[e];
+            touched[ub + i] = key;
+            toc[ub + i] = make_int2(pb + oc.x, oc.y);
+            seen[key] = tag;
+        }
+        if (b == nscan - 1 && threadIdx.x == 0) *nuniq = ub + nb;
+    }
+    const uint64_t par = (lane & 1) ? 0xAAAAAAAAAAAAAAAAull : 0x5555555555555555ull;
+    const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+    const int64_t gstride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t cb = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); cb < m; cb += gstride) {
+        const int64_t c = cb + lane;
+        bool ok = false, own = true;
+        int key = 0;
+        if (c < m) {
+            key = contrib_key<MODE>(c, ks, &ok, &own);
+            if (!ok) atomicOr(err, kErrIdRange);
+            ok = ok && own;
+        }
+        const int kk = ok ? key : -2 - lane;
+        const int prev = __shfl_up(kk, 2, 64);
+        const uint64_t heads = ~__ballot(lane >= 2 && prev == kk) & par;
+        const int head = 63 - __clzll(heads & upto);
+        const uint64_t later = heads & ~upto;
+        const int next = later ? __ffsll((unsigned long long)later) - 1 : 64 + (lane & 1);
+        int top = 0;
+        if (ok && lane == head) {
+            top = atomicSub(&cnt[key], (next - head) >> 1);
+            const int over = ((next - head) >> 1) - max(top, 0);   // k_fill_big's give-back
+            if (over > 0) atomicAdd(&cnt[key], over);
+        }
+        top = __shfl(top, head, 64);
+        const int slot = top - 1 - ((lane - head) >> 1);
+        if (ok && slot >= 0) list[local[key] + pre[key / kScanBlock] + slot] = (int)c;
+        else if (ok) atomicOr(err, kErrStaleCount);
+    }
+}
+
 // Sort each key's contribution list ascending.  Keys of <= kSmallSeg entries: one thread,
 // odd-even network in registers.  Longer keys: queued in LDS and sorted by the whole
 // workgroup with a bitmap over the contribution ids (set bits, popcount scan, write back).
@@ -468,7 +533,8 @@ static hipError_t set_sort_lds(int nwords) {
 // count -> scan -> fill -> sort over K keys for m contributions.
 template <int MODE, bool UNIQ, bool LIST = false>
 static hipError_t build(const WsLayout& L, void* ws, const KeySrc& ks, int64_t m, int64_t K, PlanOut po,
-                        int nwords, hipStream_t st, bool counted = false, bool skip_sort = false) {
+                        int nwords, hipStream_t st, bool counted = false, bool skip_sort = false,
+                        bool sparse = false) {
     // skip_sort: the caller's next launch (the touched-row catch-up) sorts the lists in extra blocks
     // counted: the previous step counted AND scanned these ids (touched update + stats launch)
     const int64_t r1 = K + 1;
@@ -485,7 +551,18 @@ static hipError_t build(const WsLayout& L, void* ws, const KeySrc& ks, int64_t m
     if (!counted)
         launch(k_scan_local<U2>, nscan, kBlock, 0, st, cnt, r1, local, tot, U2 ? at<int32_t>(ws, L.uloc) : nullptr,
                                                    U2 ? at<int32_t>(ws, L.utot) : nullptr);
-    if (nscan > kFillBigScan && nscan <= kBlock * kPrefixPer) {
+    if (sparse) {
+        if (UNIQ || !LIST || !counted || !sparse_index_ok(L) || r1 != L.keys + 1) return hipErrorInvalidValue;
+        int32_t* pre = at<int32_t>(ws, L.pre);
+        launch(k_prefix, 1, kBlock, 0, st, (const int32_t*)tot, (const int32_t*)at<int32_t>(ws, L.utot), nscan, pre,
+               pre + nscan);
+        const int64_t gc = (m + kBlock - 1) / kBlock;
+        launch(k_fill_touched<MODE>, (unsigned)(gc > nscan ? gc : nscan), kBlock, 0, st, ks, m, cnt,
+               (const int32_t*)local, (const int32_t*)pre, (const int32_t*)(pre + nscan),
+               (const int32_t*)at<int32_t>(ws, L.utot), nscan, (const int32_t*)at<int32_t>(ws, L.tl),
+               (const int2*)at<int2>(ws, L.tocl), po.uniq_rows, po.uniq_oc, po.nuniq, at<int32_t>(ws, L.seen),
+               (const int32_t*)at<int32_t>(ws, L.itag), list, at<int32_t>(ws, L.err), at<int32_t>(ws, L.ifold));
+    } else if (nscan > kFillBigScan && nscan <= kBlock * kPrefixPer) {
         int32_t* pre = at<int32_t>(ws, L.pre);
         launch(k_prefix, 1, kBlock, 0, st, (const int32_t*)tot, U2 ? (const int32_t*)at<int32_t>(ws, L.utot) : nullptr,
                nscan, pre, pre + nscan);
@@ -511,7 +588,7 @@ static hipError_t build(const WsLayout& L, void* ws, const KeySrc& ks, int64_t m
 
 hipError_t launch_index_build(const ncf_shape_t& s, const WsLayout& L, void* ws, const int32_t* users,
                               const int32_t* items, int64_t n, hipStream_t st, bool touched_list, bool counted,
-                              bool skip_sort, int fold) {
+                              bool skip_sort, int fold, bool sparse) {
     KeySrc ks{users, items, nullptr, s.num_users, s.num_items, 1, 0, fold};
     if (touched_list) {
         PlanOut po{};
@@ -521,8 +598,9 @@ hipError_t launch_index_build(const ncf_shape_t& s, const WsLayout& L, void* ws,
         po.nuniq = at<int32_t>(ws, L.nuniq);
         po.uniq_oc = at<int2>(ws, L.touched_oc);
         return build<kKeyPair, false, true>(L, ws, ks, 2 * n, s.num_rows, po, (int)((2 * n + 31) / 32), st,
-                                            counted, skip_sort);
+                                            counted, skip_sort, sparse);
     }
+    if (sparse) return hipErrorInvalidValue;
     return build<kKeyPair, false>(L, ws, ks, 2 * n, s.num_rows, PlanOut{}, (int)((2 * n + 31) / 32), st, counted);
 }
 

@@ -23,6 +23,7 @@ constexpr int kUpdateGrid = 2048;      // grid of the embedding-table sweep (fix
 constexpr int64_t kMaxBatch = 262144;  // heavy-segment bitmap must fit the LDS (2*B bits = 64 KB)
 constexpr int kFillBigScan = 256;      // scan blocks above which the index fill uses k_prefix + k_fill_big
 constexpr int kMaxFillScan = 128;      // scan blocks (262,144 keys) the in-kernel index fill holds (FillArgs)
+constexpr int kPrefixPer = 32;         // k_prefix's chunk length cap: at most 8,192 scan blocks (16.7 M keys)
 constexpr int kHeavyMin = 8;           // smallest list length the touched-row update leaves to its heavy blocks
 
 #ifndef NCF_DEBUG_BOUNDS
@@ -72,6 +73,9 @@ struct WsLayout {
     size_t utot;      // int32[nscan]
     size_t ifold;     // int32       user-row folding of the last index build (persistent)
     size_t stale_step;// int32      persistent: nonzero while the current step is dropped (fill_wave)
+    size_t seen;      // int32[K+1] persistent (single table): the sparse index's tag of the batch that last
+                      // touched each key (sparse_index_ok: k_fill_touched writes it, the count blocks read it)
+    size_t itag;      // int32      persistent: the last sparse index's tag (bumped by the stats launch)
     size_t cid_u;     // int32[B]    compact (unique-row) id of each sample's user row
     size_t cid_i;     // int32[B]    compact id of each sample's item row
     size_t uoffs;     // int32[2B+1] compact row -> first list slot
@@ -147,7 +151,12 @@ struct TouchedOut {
 
 // move_to (optional): the counts were taken ahead (ws cnt_ahead); they also move to the fill's
 // cursors move_to (ws cnt) and cnt is zeroed for the next batch's count
-template <bool UNIQ>
+// SPARSE (large key spaces, sparse_index_ok): the move, the zeroing and the local offsets are written
+// for the occupied keys only (every other key's cursor and count are zero already — the fill and
+// the update leave them so — and its offset is never read: the fill reads the offsets of listed
+// keys, the count blocks test membership with the seen tags), the occupied-key numbering (uloc) not
+// at all: the scan's dense writes were 4 x 4 bytes per key of the table (11 M keys at config D)
+template <bool UNIQ, bool SPARSE = false>
 // (cnt is written through when moving: not a const __restrict__ pointer, whose memory the compiler
 // may assume nothing writes)
 __device__ inline void scan_local_body(const int32_t* cnt, int64_t r1, int32_t* __restrict__ offs,
@@ -168,7 +177,12 @@ __device__ inline void scan_local_body(const int32_t* cnt, int64_t r1, int32_t* 
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = (base + j < r1) ? cnt[base + j] : 0;
     }
-    if (move_to) {
+    if (SPARSE && move_to) {
+        int32_t* zc = const_cast<int32_t*>(cnt);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (v[j] != 0) move_to[base + j] = v[j], zc[base + j] = 0;
+    } else if (move_to) {
         int32_t* zc = const_cast<int32_t*>(cnt);
         if (full) {
             *reinterpret_cast<int4*>(move_to + base) = make_int4(v[0], v[1], v[2], v[3]);
@@ -194,7 +208,11 @@ __device__ inline void scan_local_body(const int32_t* cnt, int64_t r1, int32_t* 
         o[j] = run;
         run += v[j];
     }
-    if (full) {
+    if (SPARSE) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (v[j] != 0) offs[base + j] = o[j];
+    } else if (full) {
         *reinterpret_cast<int4*>(offs + base) = make_int4(o[0], o[1], o[2], o[3]);
         *reinterpret_cast<int4*>(offs + base + 4) = make_int4(o[4], o[5], o[6], o[7]);
     } else {
@@ -211,7 +229,8 @@ __device__ inline void scan_local_body(const int32_t* cnt, int64_t r1, int32_t* 
             o[j] = urun;
             urun += v[j] > 0;
         }
-        if (full) {
+        if (SPARSE) {
+        } else if (full) {
             *reinterpret_cast<int4*>(uloc + base) = make_int4(o[0], o[1], o[2], o[3]);
             *reinterpret_cast<int4*>(uloc + base + 4) = make_int4(o[4], o[5], o[6], o[7]);
         } else {
@@ -673,9 +692,22 @@ __host__ __device__ inline T* at(void* base, size_t off) {
 // index build: contribution c = 2*i + side (0 user row, 1 item row) grouped by table row
 // touched_list: also the ascending list of the touched rows (ws touched, count in nuniq)
 // fold: user-row folding group (fold_of), 0 = every sample's user row is a contribution
+// sparse (touched_list && counted && sparse_index_ok): the previous step's stats launch scanned the
+// counts sparsely (launch_stats sparse_scan); the rows come from its per-block touched lists and
+// the keys' seen tags are set (k_fill_touched) — no pass over every key of the table
 hipError_t launch_index_build(const ncf_shape_t& s, const WsLayout& L, void* ws, const int32_t* users,
                               const int32_t* items, int64_t n, hipStream_t st, bool touched_list = false,
-                              bool counted = false, bool skip_sort = false, int fold = 0);
+                              bool counted = false, bool skip_sort = false, int fold = 0, bool sparse = false);
+// the counted-ahead index of a single-table step without any pass over every key: large key spaces
+// (more scan blocks than k_fill holds, at most what k_prefix scans); the touched-row update's count
+// blocks then test "in this step's batch" with the seen tags instead of the offsets
+// (-DNCF_SPARSE_INDEX=0: the dense k_fill_big path, for A/B)
+#ifndef NCF_SPARSE_INDEX
+#define NCF_SPARSE_INDEX 1
+#endif
+inline bool sparse_index_ok(const WsLayout& L) {
+    return NCF_SPARSE_INDEX && L.world == 0 && L.nscan > kFillBigScan && L.nscan <= kBlock * kPrefixPer;
+}
 // row-sharded plan: index over owner-major keys + unique-row compaction (uniq_rows = local row
 // ids grouped by owner, send_counts[world], cid_u/cid_i/uoffs/nuniq in the workspace)
 // flags kErrFold unless the last index build folded with `fold` (an index built in another call)
@@ -837,7 +869,7 @@ hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, vo
                                      const int32_t* next_items = nullptr, int64_t n_next = 0,
                                      const MlpDeferred* mlp = nullptr, int next_fold = 0,
                                      const MetricsDeferred* met = nullptr, const float* grad_rows = nullptr,
-                                     bool unsorted_lists = false, bool may_drop = true);
+                                     bool unsorted_lists = false, bool may_drop = true, bool sparse_index = false);
 // (may_drop false: a fill overflow does not drop the step — data parallelism, where a rank that
 // skipped its step would leave the replicas apart; the error is still reported)
 // (grad_rows: the contribution rows the list indexes; default the workspace's per-sample rows gs)
@@ -893,7 +925,7 @@ struct SummaryFirst {
 hipError_t launch_stats(const WsLayout& L, void* ws, const float* summary, int nreg_emb, int nreg_mlp,
                         float inv_batch, double* stats, int32_t* step, bool bump_step, hipStream_t st,
                         bool scan_ahead = false, int64_t scan_keys = 0, SummaryFirst sf = SummaryFirst{-1, 0, 0.f},
-                        int32_t* drop = nullptr);
+                        int32_t* drop = nullptr, bool sparse_scan = false);
 
 // on-device negative sampling (ncf_sample.hip)
 hipError_t launch_sample_batch(const int32_t* pos_users, const int32_t* pos_items, const int32_t* excl_ptr,

@@ -580,6 +580,8 @@ struct CountAhead {
     int per;                   // contributions per count block and pass (16, 32 or 64)
     int64_t lazy_rows;         // rows [0, lazy_rows) are under deferred decay: only they are
                                // updated here and caught up ahead (the rest are swept densely)
+    const int32_t* seen;       // sparse index (sparse_index_ok): key in this step's batch <=> seen[key] ==
+    const int32_t* itag;       // *itag + 1 (k_fill_touched's tag); nullptr: the offsets tell
 };
 
 // the dense layers' Adam (k_mlp_update<ADAM>'s work) in blocks >= nupd + ncount of the same launch;
@@ -855,6 +857,7 @@ __global__ __launch_bounds__(kBlock, UNSORTED ? NCF_TOUCHED_MIN_BLOCKS_UNSORTED 
         // (A dropped step applies nothing: the next batch's rows are caught up to *step instead.)
         __shared__ float lut[kLrLut];
         const int t = *step + (dropped ? 0 : 1);
+        const int tagc = ca.seen ? *ca.itag + 1 : 0;
         if (ca.replay && threadIdx.x < kLrLut)
             lut[threadIdx.x] = t - (int)threadIdx.x >= 1 ? adam_lr_t(lr, b1, b2, t - threadIdx.x) : 0.f;
         const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -890,6 +893,8 @@ __global__ __launch_bounds__(kBlock, UNSORTED ? NCF_TOUCHED_MIN_BLOCKS_UNSORTED 
                     if (UNSORTED) {   // (the in-kernel fill writes no offs array: the key's count instead)
                         o0 = so.local[key];
                         o1 = (key + 1) % kScanBlock != 0 ? so.local[key + 1] : so.tot[key / kScanBlock];
+                    } else if (ca.seen) {   // sparse index: no offsets at keys outside the batch
+                        o1 = ca.seen[key] == tagc;
                     } else {
                         o0 = offs[key];
                         o1 = offs[key + 1];
@@ -1724,6 +1729,8 @@ struct ScanAhead {
     int32_t* cursor;           // ws cnt
     int32_t* heavy_n;          // the in-kernel fill's heavy-row count (FillArgs), zeroed here
     TouchedOut to;             // the next index's per-block touched rows (single-table workspaces)
+    int sparse;                // scan_local_body<true, true> (sparse_index_ok): occupied keys only
+    int32_t* itag;             // sparse: the seen tag, bumped by block 0 (after this step's update read it)
 };
 __global__ __launch_bounds__(kBlock) void k_stats_scan(float* __restrict__ summary,
                                                        const float* __restrict__ reg_emb, int nreg_emb,
@@ -1732,6 +1739,10 @@ __global__ __launch_bounds__(kBlock) void k_stats_scan(float* __restrict__ summa
                                                        int bump, ScanAhead sc, SummaryArgs sa) {
     if (blockIdx.x == 0) {
         summary_stats_block(sa, summary, reg_emb, nreg_emb, reg_mlp, nreg_mlp, inv_batch, stats, step, bump);
+        if (sc.itag && threadIdx.x == 0) *sc.itag += 1;
+    } else if (sc.sparse) {
+        scan_local_body<true, true>(sc.cnt, sc.r1, sc.offs, sc.tot, sc.uloc, sc.utot, (int)blockIdx.x - 1, sc.cursor,
+                                    sc.heavy_n, sc.to);
     } else {
         scan_local_body<true>(sc.cnt, sc.r1, sc.offs, sc.tot, sc.uloc, sc.utot, (int)blockIdx.x - 1, sc.cursor,
                               sc.heavy_n, sc.to);
@@ -1754,7 +1765,7 @@ hipError_t launch_scan_ahead(const WsLayout& L, void* ws, int64_t keys, hipStrea
     const int nscan = (int)((r1 + kScanBlock - 1) / kScanBlock);
     ScanAhead sc{at<const int32_t>(ws, L.cnt_ahead), r1, at<int32_t>(ws, L.offs_local), at<int32_t>(ws, L.tot),
                  at<int32_t>(ws, L.uloc), at<int32_t>(ws, L.utot), at<int32_t>(ws, L.cnt), at<int32_t>(ws, L.heavy_n),
-                 touched_out(L, ws)};
+                 touched_out(L, ws), 0, nullptr};
     launch(k_scan_ahead, nscan, kBlock, 0, st, sc);
     return hipGetLastError();
 }
@@ -1832,8 +1843,10 @@ hipError_t launch_emb_catchup(const ncf_shape_t& s, const WsLayout& L, void* ws,
     if (sort_lists && !all_rows) {
         so = SortAhead{0, at<const int32_t>(ws, L.offs), R, at<int32_t>(ws, L.list), (int)((2 * n + 31) / 32),
                        at<int32_t>(ws, L.cnt), at<int32_t>(ws, L.err), nullptr, nullptr, nullptr};
-        if (sort_rpt(R) == 8) {
-            // large key spaces (k_fill_big): only the touched list's rows (at most 2n)
+        if (sort_rpt(R) == 8 || (L.nscan > kFillBigScan && L.nscan <= kBlock * kPrefixPer)) {
+            // large key spaces (k_fill_big / k_fill_touched, which give back what a run takes below
+            // zero, so residues sit at counted keys only): the touched list's rows (at most 2n) — the
+            // sparse index (k_fill_touched) writes no per-key offsets
             so.touched = at<const int32_t>(ws, L.touched);
             so.toc = at<const int2>(ws, L.touched_oc);
             so.nuniq = at<const int32_t>(ws, L.nuniq);
@@ -1903,7 +1916,7 @@ hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, vo
                                      float* v, int32_t* row_step, int32_t* step, const ncf_hyper_t& h,
                                      hipStream_t st, const int32_t* next_users, const int32_t* next_items,
                                      int64_t n_next, const MlpDeferred* mlp, int next_fold, const MetricsDeferred* met,
-                                     const float* grad_rows, bool unsorted_lists, bool may_drop) {
+                                     const float* grad_rows, bool unsorted_lists, bool may_drop, bool sparse_index) {
 #if NCF_DIAG_UPD == 1  // diagnostic timing builds only (wrong numerics): no catch-up ahead
     const bool replay_ahead = false;
 #else
@@ -1923,8 +1936,11 @@ hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, vo
         const int per = mc >= 65536 ? NCF_COUNT_PER_MAX : mc >= 32768 ? 32 : NCF_COUNT_PER_SMALL;
         const int64_t npass = (mc + per - 1) / per;
         const unsigned ncount = mc > 0 ? (unsigned)(npass < NCF_COUNT_BLOCKS_MAX ? npass : NCF_COUNT_BLOCKS_MAX) : 0u;
+        if (sparse_index && (unsorted_lists || !sparse_index_ok(L))) return hipErrorInvalidValue;
         CountAhead ca{(int)nupd, (int)ncount, next_users, next_items, mc, s.num_users, s.num_items,
-                      at<int32_t>(ws, L.cnt_ahead), replay_ahead ? 1 : 0, next_fold, per, lazy_bound(s, h)};
+                      at<int32_t>(ws, L.cnt_ahead), replay_ahead ? 1 : 0, next_fold, per, lazy_bound(s, h),
+                      sparse_index ? at<const int32_t>(ws, L.seen) : nullptr,
+                      sparse_index ? at<const int32_t>(ws, L.itag) : nullptr};
         MlpTail mt{};
         if (mlp) {
             mt = MlpTail{mlp->two_level ? (s.mlp_params + 15) / 16 : (s.mlp_params + kBlock - 1) / kBlock, mlp->p,
@@ -2201,7 +2217,7 @@ hipError_t launch_summary(const WsLayout& L, void* ws, int nbce, int nmet, float
 
 hipError_t launch_stats(const WsLayout& L, void* ws, const float* summary_in, int nreg_emb, int nreg_mlp,
                         float inv_batch, double* stats, int32_t* step, bool bump_step, hipStream_t st,
-                        bool scan_ahead, int64_t scan_keys, SummaryFirst sf, int32_t* drop) {
+                        bool scan_ahead, int64_t scan_keys, SummaryFirst sf, int32_t* drop, bool sparse_scan) {
     const float* reg = at<float>(ws, L.part_reg);
     // written only by the summary_first block (the workspace's summary); read-only otherwise
     float* summary = const_cast<float*>(summary_in);
@@ -2214,7 +2230,8 @@ hipError_t launch_stats(const WsLayout& L, void* ws, const float* summary_in, in
         const int nscan = (int)((r1 + kScanBlock - 1) / kScanBlock);
         ScanAhead sc{at<const int32_t>(ws, L.cnt_ahead), r1, at<int32_t>(ws, L.offs_local), at<int32_t>(ws, L.tot),
                      at<int32_t>(ws, L.uloc), at<int32_t>(ws, L.utot), at<int32_t>(ws, L.cnt), at<int32_t>(ws, L.heavy_n),
-                     touched_out(L, ws)};
+                     touched_out(L, ws), sparse_scan ? 1 : 0, sparse_scan ? at<int32_t>(ws, L.itag) : nullptr};
+        if (sparse_scan && (!sparse_index_ok(L) || r1 != L.keys + 1)) return hipErrorInvalidValue;
         launch(k_stats_scan, 1 + nscan, kBlock, 0, st, summary, reg, nreg_emb, reg + kUpdateGrid, nreg_mlp, inv_batch,
                stats, step, bump_step ? 1 : 0, sc, sa);
         return hipGetLastError();
