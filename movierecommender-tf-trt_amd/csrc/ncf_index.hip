@@ -284,35 +284,48 @@ __global__ __launch_bounds__(kBlock) void k_fill(KeySrc ks, int64_t m, int32_t* 
 // workgroups and leaves each thread a grid-stride chain of ~40 dependent row passes.  Here one
 // workgroup writes the prefixes to the workspace once (k_prefix) and the fill runs one workgroup
 // per scan block (8 rows per thread) — same outputs as k_fill.
-// One workgroup, one memory round trip: thread t loads the totals of its contiguous chunk of
-// ceil(nscan / 256) scan blocks all at once (at most kPrefixPer each), sums them, one block scan
-// of the chunk sums, then the chunk's prefixes are written.
+// One workgroup per array (tot, and utot when given): the totals go through LDS — loaded (all in flight at once) and stored back
+// coalesced (a thread's contiguous chunk read straight from memory put 64 different cache lines
+// behind every wave instruction) — thread t scans its chunk of ceil(nscan / 256)
+// scan blocks (at most kPrefixPer), one block scan of the chunk sums, then the chunk's prefixes.
 __global__ __launch_bounds__(kBlock) void k_prefix(const int32_t* __restrict__ tot, const int32_t* __restrict__ utot,
                                                    int nscan, int32_t* __restrict__ pre, int32_t* __restrict__ upre) {
     __shared__ int sw[4];
+    __shared__ int buf[kBlock * kPrefixPer];   // 32 KB: one of the two arrays at a time
     const int per = (nscan + kBlock - 1) / kBlock;
     const int i0 = (int)threadIdx.x * per;
-    int t[kPrefixPer], u[kPrefixPer];
-    int ts = 0, us = 0;
+    {   // workgroup 0: tot -> pre; workgroup 1 (launched when utot is given): utot -> upre
+        const int pass = (int)blockIdx.x;
+        const int32_t* src = pass ? utot : tot;
+        int32_t* dst = pass ? upre : pre;
+        {   // every load in flight before the first LDS store (a load-store loop waits a round trip each)
+            int x[kPrefixPer];
 #pragma unroll
-    for (int j = 0; j < kPrefixPer; ++j) {
-        const bool in = j < per && i0 + j < nscan;
-        t[j] = in ? tot[i0 + j] : 0;
-        u[j] = in && utot ? utot[i0 + j] : 0;
-    }
+            for (int j = 0; j < kPrefixPer; ++j) {
+                const int i = (int)threadIdx.x + kBlock * j;
+                x[j] = i < nscan ? src[i] : 0;
+            }
 #pragma unroll
-    for (int j = 0; j < kPrefixPer; ++j) ts += t[j], us += u[j];
-    int total;
-    int run = block_exscan_256(ts, sw, &total);
-    int urun = utot ? block_exscan_256(us, sw, &total) : 0;
-#pragma unroll
-    for (int j = 0; j < kPrefixPer; ++j) {
-        if (j < per && i0 + j < nscan) {
-            pre[i0 + j] = run;
-            if (utot) upre[i0 + j] = urun;
+            for (int j = 0; j < kPrefixPer; ++j) {
+                const int i = (int)threadIdx.x + kBlock * j;
+                if (i < nscan) buf[i] = x[j];
+            }
         }
-        run += t[j];
-        urun += u[j];
+        __syncthreads();
+        int ts = 0;
+        for (int j = 0; j < per; ++j) ts += i0 + j < nscan ? buf[i0 + j] : 0;
+        int total;
+        int run = block_exscan_256(ts, sw, &total);
+        __syncthreads();   // every chunk read before the prefixes overwrite the buffer
+        for (int j = 0; j < per; ++j) {
+            if (i0 + j < nscan) {
+                const int t = buf[i0 + j];
+                buf[i0 + j] = run;
+                run += t;
+            }
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < nscan; i += kBlock) dst[i] = buf[i];
     }
 }
 
@@ -554,7 +567,7 @@ static hipError_t build(const WsLayout& L, void* ws, const KeySrc& ks, int64_t m
     if (sparse) {
         if (UNIQ || !LIST || !counted || !sparse_index_ok(L) || r1 != L.keys + 1) return hipErrorInvalidValue;
         int32_t* pre = at<int32_t>(ws, L.pre);
-        launch(k_prefix, 1, kBlock, 0, st, (const int32_t*)tot, (const int32_t*)at<int32_t>(ws, L.utot), nscan, pre,
+        launch(k_prefix, 2, kBlock, 0, st, (const int32_t*)tot, (const int32_t*)at<int32_t>(ws, L.utot), nscan, pre,
                pre + nscan);
         const int64_t gc = (m + kBlock - 1) / kBlock;
         launch(k_fill_touched<MODE>, (unsigned)(gc > nscan ? gc : nscan), kBlock, 0, st, ks, m, cnt,
@@ -564,7 +577,7 @@ static hipError_t build(const WsLayout& L, void* ws, const KeySrc& ks, int64_t m
                (const int32_t*)at<int32_t>(ws, L.itag), list, at<int32_t>(ws, L.err), at<int32_t>(ws, L.ifold));
     } else if (nscan > kFillBigScan && nscan <= kBlock * kPrefixPer) {
         int32_t* pre = at<int32_t>(ws, L.pre);
-        launch(k_prefix, 1, kBlock, 0, st, (const int32_t*)tot, U2 ? (const int32_t*)at<int32_t>(ws, L.utot) : nullptr,
+        launch(k_prefix, U2 ? 2 : 1, kBlock, 0, st, (const int32_t*)tot, U2 ? (const int32_t*)at<int32_t>(ws, L.utot) : nullptr,
                nscan, pre, pre + nscan);
         const int64_t gc = (m + kBlock - 1) / kBlock;
         launch(k_fill_big<MODE, UNIQ, LIST>, (unsigned)(gc > nscan ? gc : nscan), kBlock, 0, st, ks, m, cnt,

@@ -156,27 +156,31 @@ struct TouchedOut {
 // the update leave them so — and its offset is never read: the fill reads the offsets of listed
 // keys, the count blocks test membership with the seen tags), the occupied-key numbering (uloc) not
 // at all: the scan's dense writes were 4 x 4 bytes per key of the table (11 M keys at config D)
-template <bool UNIQ, bool SPARSE = false>
-// (cnt is written through when moving: not a const __restrict__ pointer, whose memory the compiler
-// may assume nothing writes)
-__device__ inline void scan_local_body(const int32_t* cnt, int64_t r1, int32_t* __restrict__ offs,
-                                       int32_t* __restrict__ tot, int32_t* __restrict__ uloc,
-                                       int32_t* __restrict__ utot, int blk, int32_t* __restrict__ move_to = nullptr,
-                                       int32_t* __restrict__ zero_at_end = nullptr, TouchedOut to = TouchedOut{}) {
-    __shared__ int sw[4];
+// scan block blk's counts, 8 keys per thread: two int4 loads when all 8 are inside (the workspace
+// regions are 256-byte aligned and the thread's first key a multiple of 8), else key by key
+__device__ __forceinline__ void scan_local_load(const int32_t* cnt, int64_t r1, int blk, int (&v)[8]) {
     const int64_t base = (int64_t)blk * kScanBlock + threadIdx.x * 8;
-    // 8 keys per thread: two int4 loads / stores when all 8 are inside (the workspace regions
-    // are 256-byte aligned and base a multiple of 8), else key by key
-    const bool full = base + 8 <= r1;
-    int v[8];
-    int sum = 0, nz = 0;
-    if (full) {
+    if (base + 8 <= r1) {
         const int4 a = *reinterpret_cast<const int4*>(cnt + base), b = *reinterpret_cast<const int4*>(cnt + base + 4);
         v[0] = a.x, v[1] = a.y, v[2] = a.z, v[3] = a.w, v[4] = b.x, v[5] = b.y, v[6] = b.z, v[7] = b.w;
     } else {
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = (base + j < r1) ? cnt[base + j] : 0;
     }
+}
+
+// the scan of block blk from its loaded counts v (scan_local_load)
+template <bool UNIQ, bool SPARSE = false>
+// (cnt is written through when moving: not a const __restrict__ pointer, whose memory the compiler
+// may assume nothing writes)
+__device__ inline void scan_local_apply(const int (&v)[8], const int32_t* cnt, int64_t r1, int32_t* __restrict__ offs,
+                                        int32_t* __restrict__ tot, int32_t* __restrict__ uloc,
+                                        int32_t* __restrict__ utot, int blk, int32_t* __restrict__ move_to = nullptr,
+                                        int32_t* __restrict__ zero_at_end = nullptr, TouchedOut to = TouchedOut{}) {
+    __shared__ int sw[4];
+    const int64_t base = (int64_t)blk * kScanBlock + threadIdx.x * 8;
+    const bool full = base + 8 <= r1;
+    int sum = 0, nz = 0;
     if (SPARSE && move_to) {
         int32_t* zc = const_cast<int32_t*>(cnt);
 #pragma unroll
@@ -255,6 +259,16 @@ __device__ inline void scan_local_body(const int32_t* cnt, int64_t r1, int32_t* 
     // last, after every use of threadIdx.x: a `blockIdx.x == 1 && threadIdx.x == 0` store ahead of
     // the body made hipcc (ROCm 7.2) feed the later blocks an undefined thread id
     if (zero_at_end && blk == 0 && threadIdx.x == 0) *zero_at_end = 0;
+}
+
+template <bool UNIQ, bool SPARSE = false>
+__device__ inline void scan_local_body(const int32_t* cnt, int64_t r1, int32_t* __restrict__ offs,
+                                       int32_t* __restrict__ tot, int32_t* __restrict__ uloc,
+                                       int32_t* __restrict__ utot, int blk, int32_t* __restrict__ move_to = nullptr,
+                                       int32_t* __restrict__ zero_at_end = nullptr, TouchedOut to = TouchedOut{}) {
+    int v[8];
+    scan_local_load(cnt, r1, blk, v);
+    scan_local_apply<UNIQ, SPARSE>(v, cnt, r1, offs, tot, uloc, utot, blk, move_to, zero_at_end, to);
 }
 
 // User-row folding (the north star's duplicate-index reduction, done where the gradients are

@@ -4,7 +4,7 @@ Both were found on the GPU from their symptoms (tools/dbg_scan.py, tools/dbg_row
 reordering source; no reduced reproducer was isolated, so these CPU checks keep the orderings from
 being undone unnoticed:
 
-1. scan_local_body (ncf_internal.h): the `zero_at_end` store — `blk == 0 && threadIdx.x == 0` — must
+1. scan_local_apply (ncf_internal.h, the scan body): the `zero_at_end` store — `blk == 0 && threadIdx.x == 0` — must
    come after every use of threadIdx.x.  With a `blockIdx.x == 1 && threadIdx.x == 0` store ahead of
    the scan body, the later workgroups read back garbage block totals (the scan was wrong for
    workgroups >= 2 on ROCm 7.2).
@@ -16,6 +16,8 @@ being undone unnoticed:
 
 import os
 import re
+
+import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "movierecommender-tf-trt_amd", "csrc", "ncf_internal.h")
@@ -35,8 +37,9 @@ def _function(text, name):
         k += 1
 
 
-def test_scan_zero_store_comes_last():
-    body = _function(open(SRC).read(), "__device__ inline void scan_local_body")
+@pytest.mark.parametrize("fn", ["__device__ inline void scan_local_apply"])
+def test_scan_zero_store_comes_last(fn):
+    body = _function(open(SRC).read(), fn)
     store = body.index("*zero_at_end = 0")
     # no use of threadIdx after the store, and the store is the body's last statement
     assert "threadIdx" not in body[store + len("*zero_at_end = 0"):]
