@@ -803,9 +803,11 @@ hipError_t launch_fb_layered(const ncf_shape_t& s, const WsLayout& L, void* ws, 
 // forward = gather + X0 + (gmf != nullptr) GMF product + relu(W1^T x + b1); backward = dX = W1 G1 into the
 // gradient rows gs with their GMF part (the replaced gather / GEMM / bias / scatter kernels' outputs)
 bool layer1_supported(const ncf_shape_t& s);
+// fold (2, 4, 8) with gpart ([n / fold][L1] floats of scratch): the user half once per group
+// (k_lay_l1f_gu); else per sample
 hipError_t launch_layer1_fwd(const ncf_shape_t& s, const float* emb, const float* mlp, const int32_t* users,
                              const int32_t* items, int64_t n, IdSpace ids, float* x0, float* gmf, float* h1,
-                             hipStream_t st);
+                             hipStream_t st, int fold = 0, float* gpart = nullptr);
 // dW1 = X0^T G1 per batch chunk of `chunk` samples into slab c (hidden_1 kernel at offset 0), c < nchunks
 hipError_t launch_layer1_dw(const ncf_shape_t& s, const float* x0, const float* g1, int64_t n, int64_t chunk,
                             int nchunks, float* slabs, hipStream_t st);

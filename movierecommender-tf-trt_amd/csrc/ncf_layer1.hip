@@ -27,6 +27,11 @@
 
 #include <cstdlib>
 
+// 1 (the default): with user-row folding the layer-1 forward computes the user half once per group
+// (k_lay_l1f_gu); 0: per sample (A/B)
+#ifndef NCF_LAYERED_GU
+#define NCF_LAYERED_GU 1
+#endif
 // timing diagnostic (wrong results): 1 = layer 1's user half skipped in all three kernels (the
 // work a per-group user half would leave)
 #ifndef NCF_DIAG_DHALF
@@ -217,6 +222,179 @@ __global__ __launch_bounds__(64 * NW, 1) void k_lay_l1f(const float* __restrict_
             if (u + 2 * ustride < nunits) load(u + 2 * ustride, A);
             if (hb) process(u + ustride, B);
         }
+    }
+}
+
+// Group-user form of the layer-1 forward (user-row folding, FOLD 2, 4, 8): the reference's batches
+// are groups of FOLD samples sharing one user (data_pipeline.py:141), and layer 1 is linear in the
+// user half of its input: W1^T [x_u; x_i] = W1_u^T x_u + W1_i^T x_i.  Phase 0: each wave computes
+// P_u = W1_u^T x_u of the group heads of its units, 16 groups per MFMA tile (column li: group
+// li % NGU of the wave's unit tau FOLD + li / NGU), into gpart [n / FOLD][L1], and writes X0's user
+// half for the groups' samples (their rows are the head's).  Per unit: the accumulators start from
+// the sample's group's P_u and only the item half is contracted (128 instead of 256 k-features at
+// config D).  A unit holding a sample whose user is not its head's, or a masked sample, runs the
+// per-sample form (k_lay_l1f's), so any batch stays exact.  Same sums, reassociated.
+template <class S, int NW, int FOLD>
+__global__ __launch_bounds__(64 * NW, 1) void k_lay_l1f_gu(const float* __restrict__ emb, const float* __restrict__ mlp,
+                                                       const int32_t* __restrict__ users,
+                                                       const int32_t* __restrict__ items, int64_t n, IdSpace ids,
+                                                       float* __restrict__ x0, float* __restrict__ h1,
+                                                       float* __restrict__ gpart) {
+    constexpr int L0 = S::L0, L1 = S::L1, G = S::G, W = S::W, B1 = S::B1, XQ = S::XQ, D0 = S::D0;
+    constexpr int XH = D0 / 4;       // features of one half per lane group
+    constexpr int NGU = 16 / FOLD;   // groups per unit
+    static_assert(FOLD == 2 || FOLD == 4 || FOLD == 8, "fold width");
+    extern __shared__ __attribute__((aligned(16))) float wl[];
+    load_w1<S, 64 * NW>(wl, mlp);
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
+    const int64_t nunits = (n + 15) / 16, ustride = (int64_t)gridDim.x * NW;
+    float bias[B1][4];
+#pragma unroll
+    for (int t = 0; t < B1; ++t) ldsv<4>(wl + S::SB + 16 * t + 4 * g, bias[t]);
+    const int64_t u0 = (int64_t)blockIdx.x * NW + wv;
+    const int64_t nown = u0 < nunits ? (nunits - u0 + ustride - 1) / ustride : 0;
+
+    // ---- phase 0
+    const int64_t ntile = (nown + FOLD - 1) / FOLD;
+    for (int64_t tau = 0; tau < ntile; ++tau) {
+        const int64_t k = tau * FOLD + li / NGU;
+        const int64_t hs = (u0 + k * ustride) * 16 + (li % NGU) * FOLD;
+        const bool hv = k < nown && hs < n;
+        const int hu = hv ? users[hs] : 0;
+        const int row = hv && (unsigned)hu < (unsigned)ids.ubound ? hu : 0;
+        float xu[XH];
+        {
+            const float4* xs = reinterpret_cast<const float4*>(emb + (size_t)row * W + G + XH * g);
+#pragma unroll
+            for (int k4 = 0; k4 < XH / 4; ++k4) {
+                const float4 v = xs[k4];
+                xu[4 * k4] = v.x, xu[4 * k4 + 1] = v.y, xu[4 * k4 + 2] = v.z, xu[4 * k4 + 3] = v.w;
+            }
+        }
+        f32x4 acc[B1];
+#pragma unroll
+        for (int t = 0; t < B1; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        float a[2][B1];
+        ldsv<B1>(wl + (XH * g) * S::S1 + li * B1, a[0]);
+#pragma unroll
+        for (int q = 0; q < XH; ++q) {
+            if (q + 1 < XH) ldsv<B1>(wl + (XH * g + q + 1) * S::S1 + li * B1, a[(q + 1) & 1]);
+#pragma unroll
+            for (int t = 0; t < B1; ++t) acc[t] = mfma16(a[q & 1][t], xu[q], acc[t]);
+        }
+        if (hv) {
+            float* pg = gpart + (hs / FOLD) * L1 + 4 * g;
+#pragma unroll
+            for (int t = 0; t < B1; ++t) *reinterpret_cast<f32x4*>(pg + 16 * t) = acc[t];
+            // X0's user half for the group's samples (a unit that takes the per-sample form rewrites it)
+#pragma unroll
+            for (int j = 0; j < FOLD; ++j) {
+                if (hs + j < n) {
+                    float4* xo = reinterpret_cast<float4*>(x0 + (hs + j) * L0 + XH * g);
+#pragma unroll
+                    for (int k4 = 0; k4 < XH / 4; ++k4)
+                        xo[k4] = make_float4(xu[4 * k4], xu[4 * k4 + 1], xu[4 * k4 + 2], xu[4 * k4 + 3]);
+                }
+            }
+        }
+    }
+    // the P_u rows are read back by other lanes of this wave (a fence emits no vmcnt wait on gfx950)
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+
+    struct Unit {
+        float x[XH];      // the item half (lane group lq: item features XH lq + q)
+        f32x4 pu[B1];     // the sample's group's P_u
+        bool ok, grp;     // grp: every sample of the unit valid and its user its head's
+        int irow;
+    };
+    auto load = [&](int64_t u, Unit& U) {
+        const int64_t s = u * 16 + li;
+        const bool in = s < n;
+        const int cu = in ? users[s] : 0, cv = in ? items[s] : 0;
+        const int hu = in ? users[s & ~(int64_t)(FOLD - 1)] : 0;
+        U.ok = in && (unsigned)cu < (unsigned)ids.ubound && (unsigned)cv < (unsigned)ids.ibound;
+        U.grp = __ballot(in && (!U.ok || cu != hu)) == 0;
+        U.irow = U.ok ? ids.ibase + cv : 0;
+        const float* xr = emb + (size_t)U.irow * W + G + XH * g;   // the item row's MLP half: features XH lq ..
+#pragma unroll
+        for (int k4 = 0; k4 < XH / 4; ++k4) {
+            const float4 v = reinterpret_cast<const float4*>(xr)[k4];
+            U.x[4 * k4] = v.x, U.x[4 * k4 + 1] = v.y, U.x[4 * k4 + 2] = v.z, U.x[4 * k4 + 3] = v.w;
+        }
+        const float* pg = gpart + ((in ? s : 0) / FOLD) * L1 + 4 * g;
+#pragma unroll
+        for (int t = 0; t < B1; ++t) U.pu[t] = *reinterpret_cast<const f32x4*>(pg + 16 * t);
+    };
+    auto store_h1 = [&](int64_t s, const f32x4 (&h)[B1]) {
+        float* ho = h1 + s * L1 + 4 * g;
+#pragma unroll
+        for (int t = 0; t < B1; ++t)
+            *reinterpret_cast<float4*>(ho + 16 * t) =
+                make_float4(fmaxf(h[t][0] + bias[t][0], 0.f), fmaxf(h[t][1] + bias[t][1], 0.f),
+                            fmaxf(h[t][2] + bias[t][2], 0.f), fmaxf(h[t][3] + bias[t][3], 0.f));
+    };
+    auto process = [&](int64_t u, Unit& U) {
+        const int64_t s = u * 16 + li;
+        const bool in = s < n;
+        f32x4 h[B1];
+        if (U.grp) {
+#pragma unroll
+            for (int t = 0; t < B1; ++t) h[t] = U.pu[t];
+            float a[2][B1];
+            ldsv<B1>(wl + (D0 + XH * g) * S::S1 + li * B1, a[0]);
+#pragma unroll
+            for (int q = 0; q < XH; ++q) {
+                if (q + 1 < XH) ldsv<B1>(wl + (D0 + XH * g + q + 1) * S::S1 + li * B1, a[(q + 1) & 1]);
+#pragma unroll
+                for (int t = 0; t < B1; ++t) h[t] = mfma16(a[q & 1][t], U.x[q], h[t]);
+            }
+            if (in) {
+                float4* xo = reinterpret_cast<float4*>(x0 + s * L0 + D0 + XH * g);
+#pragma unroll
+                for (int k4 = 0; k4 < XH / 4; ++k4)
+                    xo[k4] = make_float4(U.x[4 * k4], U.x[4 * k4 + 1], U.x[4 * k4 + 2], U.x[4 * k4 + 3]);
+                store_h1(s, h);
+            }
+        } else {
+            // the per-sample form (k_lay_l1f): lane group lq holds MLP-input features XQ lq + q
+            const int cu = in ? users[s] : 0, cv = in ? items[s] : 0;
+            const bool ok = in && (unsigned)cu < (unsigned)ids.ubound && (unsigned)cv < (unsigned)ids.ibound;
+            const int urow = ok ? cu : 0, irow = ok ? ids.ibase + cv : 0;
+            float x[XQ];
+            const float4* xs = reinterpret_cast<const float4*>(emb + (size_t)(g < 2 ? urow : irow) * W + G + (g & 1) * XQ);
+#pragma unroll
+            for (int k4 = 0; k4 < XQ / 4; ++k4) {
+                const float4 v = xs[k4];
+                x[4 * k4] = ok ? v.x : 0.f, x[4 * k4 + 1] = ok ? v.y : 0.f;
+                x[4 * k4 + 2] = ok ? v.z : 0.f, x[4 * k4 + 3] = ok ? v.w : 0.f;
+            }
+#pragma unroll
+            for (int t = 0; t < B1; ++t) h[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+            float a[2][B1];
+            ldsv<B1>(wl + (XQ * g) * S::S1 + li * B1, a[0]);
+#pragma unroll
+            for (int q = 0; q < XQ; ++q) {
+                if (q + 1 < XQ) ldsv<B1>(wl + (XQ * g + q + 1) * S::S1 + li * B1, a[(q + 1) & 1]);
+#pragma unroll
+                for (int t = 0; t < B1; ++t) h[t] = mfma16(a[q & 1][t], x[q], h[t]);
+            }
+            if (in) {
+                float4* xo = reinterpret_cast<float4*>(x0 + s * L0 + XQ * g);
+#pragma unroll
+                for (int k4 = 0; k4 < XQ / 4; ++k4)
+                    xo[k4] = make_float4(x[4 * k4], x[4 * k4 + 1], x[4 * k4 + 2], x[4 * k4 + 3]);
+                store_h1(s, h);
+            }
+        }
+    };
+    Unit A, B;
+    if (u0 < nunits) load(u0, A);
+    for (int64_t u = u0; u < nunits; u += 2 * ustride) {
+        const bool hb = u + ustride < nunits;
+        if (hb) load(u + ustride, B);
+        process(u, A);
+        if (u + 2 * ustride < nunits) load(u + 2 * ustride, A);
+        if (hb) process(u + ustride, B);
     }
 }
 
@@ -479,14 +657,27 @@ bool layer1_supported(const ncf_shape_t& s) { return l1matches<L1ShapeD>(s); }
 
 hipError_t launch_layer1_fwd(const ncf_shape_t& s, const float* emb, const float* mlp, const int32_t* users,
                              const int32_t* items, int64_t n, IdSpace ids, float* x0, float* gmf, float* h1,
-                             hipStream_t st) {
+                             hipStream_t st, int fold, float* gpart) {
     using S = L1ShapeD;
     if (!l1matches<S>(s)) return hipErrorInvalidValue;
     static bool cfg = false;
     if (!cfg) {
         if (hipError_t e = configure<S>((const void*)k_lay_l1f<S, NCF_L1F_WAVES, true>)) return e;
         if (hipError_t e = configure<S>((const void*)k_lay_l1f<S, NCF_L1F_WAVES, false>)) return e;
+        if (hipError_t e = configure<S>((const void*)k_lay_l1f_gu<S, NCF_L1F_WAVES, 2>)) return e;
+        if (hipError_t e = configure<S>((const void*)k_lay_l1f_gu<S, NCF_L1F_WAVES, 4>)) return e;
+        if (hipError_t e = configure<S>((const void*)k_lay_l1f_gu<S, NCF_L1F_WAVES, 8>)) return e;
         cfg = true;
+    }
+    if (NCF_LAYERED_GU && !gmf && gpart && (fold == 2 || fold == 4 || fold == 8)) {
+#define NCF_L1F_GU(F)                                                                                          \
+    launch(k_lay_l1f_gu<S, NCF_L1F_WAVES, F>, grid_of<S, NCF_L1F_WAVES>(n), 64 * NCF_L1F_WAVES, S::LDS, st, emb, mlp, \
+           users, items, n, ids, x0, h1, gpart)
+        if (fold == 2) NCF_L1F_GU(2);
+        else if (fold == 4) NCF_L1F_GU(4);
+        else NCF_L1F_GU(8);
+#undef NCF_L1F_GU
+        return hipGetLastError();
     }
     if (gmf)
         launch(k_lay_l1f<S, NCF_L1F_WAVES, true>, grid_of<S, NCF_L1F_WAVES>(n), 64 * NCF_L1F_WAVES, S::LDS, st, emb, mlp,

@@ -65,6 +65,7 @@ hipError_t launch_fb_layered(const ncf_shape_t& s, const WsLayout& L, void* ws, 
     float* Gd[NCF_MAX_LAYERS];
     int64_t o = 0;
     for (int l = 0; l < nl; ++l) { X[l] = act + o; o += (int64_t)L.max_batch * s.layers[l]; }
+    const int64_t xend = o;
     o = 0;
     Gd[0] = nullptr;
     for (int l = 1; l < nl; ++l) { Gd[l] = dzb + o; o += (int64_t)L.max_batch * s.layers[l]; }
@@ -72,8 +73,12 @@ hipError_t launch_fb_layered(const ncf_shape_t& s, const WsLayout& L, void* ws, 
     float* slab = at<float>(ws, L.slabs);
     float* probs = at<float>(ws, L.probs);
     float* gs = at<float>(ws, L.gs);
+    // the group-user form's P_u rows ([n / fold][L1]) behind the activations (the region's last
+    // gmf_dim columns per sample are unused on this path)
+    const int64_t gfree = (int64_t)L.max_batch * L.act_w - xend;
+    float* gpart = fold > 1 && gfree * fold >= (int64_t)L.max_batch * s.layers[1] ? act + xend : nullptr;
     // layer 1 forward with the gather (the middle kernel forms the GMF product itself)
-    hipError_t e = launch_layer1_fwd(s, emb, mlp, users, items, n, ids, X[0], nullptr, X[1], st);
+    hipError_t e = launch_layer1_fwd(s, emb, mlp, users, items, n, ids, X[0], nullptr, X[1], st, fold, gpart);
     if (e != hipSuccess) return e;
     // layers 2.., output, BCE and the backward to G1 (+ db1) in one kernel, one workgroup per batch
     // chunk of dW1: slab c = that workgroup's parameters other than dW1 + chunk c's dW1
