@@ -809,8 +809,10 @@ hipError_t launch_layer1_fwd(const ncf_shape_t& s, const float* emb, const float
                              const int32_t* items, int64_t n, IdSpace ids, float* x0, float* gmf, float* h1,
                              hipStream_t st, int fold = 0, float* gpart = nullptr);
 // dW1 = X0^T G1 per batch chunk of `chunk` samples into slab c (hidden_1 kernel at offset 0), c < nchunks
+// fold (2, 4, 8) with the ids: the user half per group (k_lay_dw1<FOLD>, with k_lay_l1f_gu's X0)
 hipError_t launch_layer1_dw(const ncf_shape_t& s, const float* x0, const float* g1, int64_t n, int64_t chunk,
-                            int nchunks, float* slabs, hipStream_t st);
+                            int nchunks, float* slabs, hipStream_t st, int fold = 0, const int32_t* users = nullptr,
+                            const int32_t* items = nullptr, IdSpace ids = IdSpace{});
 hipError_t launch_layer1_bwd(const ncf_shape_t& s, const float* emb, const float* mlp, const int32_t* users,
                              const int32_t* items, int64_t n, IdSpace ids, const float* dzo, const float* g1,
                              float* gs, hipStream_t st, int fold = 0);  // fold: user-row folding (fold_of)

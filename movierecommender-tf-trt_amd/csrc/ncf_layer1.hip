@@ -230,7 +230,7 @@ __global__ __launch_bounds__(64 * NW, 1) void k_lay_l1f(const float* __restrict_
 // user half of its input: W1^T [x_u; x_i] = W1_u^T x_u + W1_i^T x_i.  Phase 0: each wave computes
 // P_u = W1_u^T x_u of the group heads of its units, 16 groups per MFMA tile (column li: group
 // li % NGU of the wave's unit tau FOLD + li / NGU), into gpart [n / FOLD][L1], and writes X0's user
-// half for the groups' samples (their rows are the head's).  Per unit: the accumulators start from
+// half for the group heads (k_lay_dw1<FOLD> contracts the user half per group from the heads' rows).  Per unit: the accumulators start from
 // the sample's group's P_u and only the item half is contracted (128 instead of 256 k-features at
 // config D).  A unit holding a sample whose user is not its head's, or a masked sample, runs the
 // per-sample form (k_lay_l1f's), so any batch stays exact.  Same sums, reassociated.
@@ -286,15 +286,13 @@ __global__ __launch_bounds__(64 * NW, 1) void k_lay_l1f_gu(const float* __restri
             float* pg = gpart + (hs / FOLD) * L1 + 4 * g;
 #pragma unroll
             for (int t = 0; t < B1; ++t) *reinterpret_cast<f32x4*>(pg + 16 * t) = acc[t];
-            // X0's user half for the group's samples (a unit that takes the per-sample form rewrites it)
+            // X0's user half of the group head (k_lay_dw1<FOLD> reads the heads' only in units of the
+            // group form; a unit that takes the per-sample form rewrites all of its X0 rows)
+            {
+                float4* xo = reinterpret_cast<float4*>(x0 + hs * L0 + XH * g);
 #pragma unroll
-            for (int j = 0; j < FOLD; ++j) {
-                if (hs + j < n) {
-                    float4* xo = reinterpret_cast<float4*>(x0 + (hs + j) * L0 + XH * g);
-#pragma unroll
-                    for (int k4 = 0; k4 < XH / 4; ++k4)
-                        xo[k4] = make_float4(xu[4 * k4], xu[4 * k4 + 1], xu[4 * k4 + 2], xu[4 * k4 + 3]);
-                }
+                for (int k4 = 0; k4 < XH / 4; ++k4)
+                    xo[k4] = make_float4(xu[4 * k4], xu[4 * k4 + 1], xu[4 * k4 + 2], xu[4 * k4 + 3]);
             }
         }
     }
@@ -528,6 +526,23 @@ __global__ __launch_bounds__(64 * NW, 1) void k_lay_l1b(const float* __restrict_
 // 4 j + lq and lane li feature li of a tile (A = X0[s][16 x + li], B = G1[s][16 y + li]).  Tile
 // element (lane 16 lq + c, register r) is dW1 row 16 x + 4 lq + r (input feature), column 16 y + c
 // (output feature): Keras' [in][out] kernel.
+// the sum of FOLD consecutive rows (stride sg) at p, pairwise in fold_sum's order
+template <int FOLD>
+__device__ __forceinline__ float group_sum_rows(const float* p, int sg) {
+    if constexpr (FOLD == 2) {
+        return p[0] + p[sg];
+    } else if constexpr (FOLD == 4) {
+        return (p[0] + p[sg]) + (p[2 * sg] + p[3 * sg]);
+    } else {
+        return ((p[0] + p[sg]) + (p[2 * sg] + p[3 * sg])) + ((p[4 * sg] + p[5 * sg]) + (p[6 * sg] + p[7 * sg]));
+    }
+}
+
+// waves per SIMD the dW1 kernel is compiled for (4: two workgroups per CU, the group form then
+// spills a few registers; 3: one workgroup per CU, no spill) — measured in profiles/r06_ab
+#ifndef NCF_DW1_WPE
+#define NCF_DW1_WPE 4
+#endif
 constexpr int kDw1Waves = 8;
 constexpr int kDw1Split = 2;    // workgroups per chunk (each takes 1 / kDw1Split of the G1 features)
 constexpr int kDw1Depth = 3;    // LDS unit buffers: units u + 1, u + 2 in flight while u computes
@@ -535,10 +550,17 @@ template <int L0, int L1>
 constexpr size_t dw1_lds() {
     return (size_t)kDw1Depth * (16 * (L0 + 16) + 16 * (L1 / kDw1Split + 16)) * 4;
 }
-template <int L0, int L1>
-__global__ __launch_bounds__(64 * kDw1Waves, 2) void k_lay_dw1(const float* __restrict__ x0,
+// FOLD (2, 4, 8; 0 none, the group-user form with k_lay_l1f_gu): the user-feature waves (the first
+// half) contract a unit over its groups instead of its samples — x_u of the group head (its X0 row:
+// the group's rows are the head's) against the group's G1 sum — one k-step per four groups instead
+// of one per four samples; a unit with a sample whose user is not its head's, or a masked sample,
+// runs the per-sample k-steps (k_lay_l1f_gu wrote its whole X0 rows; in the others only the heads')
+template <int L0, int L1, int FOLD>
+__global__ __launch_bounds__(64 * kDw1Waves) __attribute__((amdgpu_waves_per_eu(NCF_DW1_WPE))) void k_lay_dw1(const float* __restrict__ x0,
                                                              const float* __restrict__ g1, int64_t n, int chunk,
-                                                             float* __restrict__ slabs, int64_t P) {
+                                                             float* __restrict__ slabs, int64_t P,
+                                                             const int32_t* __restrict__ users,
+                                                             const int32_t* __restrict__ items, IdSpace ids) {
     constexpr int LY = L1 / kDw1Split;                      // G1 features of this workgroup
     constexpr int XT = L0 / 16 / kDw1Waves, YT = LY / 16;
     constexpr int NT = 64 * kDw1Waves;
@@ -556,6 +578,24 @@ __global__ __launch_bounds__(64 * kDw1Waves, 2) void k_lay_dw1(const float* __re
     const int64_t s1 = s0 + chunk < n ? s0 + chunk : n;
     const int nu = (int)((s1 - s0 + 15) / 16);
     const float* g1y = g1 + LY * ysplit;
+    // FOLD: bit u of bad: unit u holds a masked sample or one whose user is not its head's
+    constexpr int NGU = FOLD > 1 ? 16 / FOLD : 16;
+    __shared__ unsigned bad[8];
+    // the group sums of G1 of the next unit (two buffers by unit parity), computed by the whole
+    // workgroup one unit ahead (at the end of the unit before, whose barrier made the rows visible)
+    __shared__ float gsum[2][NGU * SG];
+    if constexpr (FOLD > 1) {
+        if (threadIdx.x < 8) bad[threadIdx.x] = nu > 256 ? ~0u : 0u;
+        __syncthreads();
+        for (int64_t s = s0 + threadIdx.x; s < s1; s += NT) {
+            const int cu = users[s], cv = items[s];
+            const int hu = users[s - (s - s0) % FOLD];
+            const bool ok = (unsigned)cu < (unsigned)ids.ubound && (unsigned)cv < (unsigned)ids.ibound;
+            const int u = (int)((s - s0) >> 4);
+            if ((!ok || cu != hu) && u < 256) atomicOr(&bad[u >> 5], 1u << (u & 31));
+        }
+        __syncthreads();
+    }
     f32x4 acc[XT][YT];
 #pragma unroll
     for (int x = 0; x < XT; ++x)
@@ -587,12 +627,24 @@ __global__ __launch_bounds__(64 * kDw1Waves, 2) void k_lay_dw1(const float* __re
         float* dst = isx ? (B) + r * SX + 4 * c : (B) + 16 * SX + r * SG + 4 * c;                      \
         if (q < QX + QG) *reinterpret_cast<f32x4*>(dst) = VV[j];                                       \
     }
+    // FOLD, unit U of the group form: its group sums (row gi of gsum[U & 1]: G1 of the group's FOLD
+    // rows summed pairwise) — unit U's rows are in LDS once the barrier before U - 1 has passed
+#define NCF_DW1_GSUM(U)                                                                                \
+    if (FOLD > 1 && (U) < nu && !((bad[(U) >> 5] >> ((U) & 31)) & 1u)) {                               \
+        const float* gb = lds + ((U) % kDw1Depth) * BUF + 16 * SX;                                     \
+        for (int e = threadIdx.x; e < NGU * LY; e += NT) {                                             \
+            const int gi = e / LY, c = e % LY;                                                         \
+            gsum[(U) & 1][gi * SG + c] = group_sum_rows<(FOLD > 1 ? FOLD : 2)>(gb + gi * (FOLD > 1 ? FOLD : 2) * SG + c, SG); \
+        }                                                                                              \
+    }
     // prologue: units 0 and 1 staged, unit 2 in registers
     NCF_DW1_FETCH(0, v0);
     NCF_DW1_FETCH(1, v1);
     NCF_DW1_STASH(v0, lds);
     NCF_DW1_STASH(v1, lds + BUF);
     NCF_DW1_FETCH(2, v0);
+    __syncthreads();   // unit 0's rows, for its group sums
+    NCF_DW1_GSUM(0);
     // one unit (a macro, not a lambda: the accumulators must stay in registers): unit u + 3's loads
     // go out into NXT (in flight under units u and u + 1), unit u's MFMAs, then unit u + 2 (held in
     // CUR since the previous unit) into the buffer unit u - 1 used
@@ -604,6 +656,17 @@ __global__ __launch_bounds__(64 * kDw1Waves, 2) void k_lay_dw1(const float* __re
         const float* base = lds + (u_ % kDw1Depth) * BUF;                                              \
         const float* bx = base + 16 * XT * wv + li;                                                    \
         const float* bg = base + 16 * SX + li;                                                         \
+        if (FOLD > 1 && wv < kDw1Waves / 2 && !((bad[u_ >> 5] >> (u_ & 31)) & 1u)) {                   \
+            _Pragma("unroll") for (int k2 = 0; k2 < (NGU + 3) / 4; ++k2) {                             \
+                const int gi = 4 * k2 + lq, hr = gi * (FOLD > 1 ? FOLD : 1);                           \
+                const bool gv = gi < NGU;                                                              \
+                float a[XT], b[YT];                                                                    \
+                _Pragma("unroll") for (int x = 0; x < XT; ++x) a[x] = gv ? bx[hr * SX + 16 * x] : 0.f; \
+                _Pragma("unroll") for (int y = 0; y < YT; ++y) b[y] = gv ? gsum[u_ & 1][gi * SG + 16 * y + li] : 0.f; \
+                _Pragma("unroll") for (int x = 0; x < XT; ++x)                                         \
+                _Pragma("unroll") for (int y = 0; y < YT; ++y) acc[x][y] = mfma16(a[x], b[y], acc[x][y]); \
+            }                                                                                          \
+        } else {                                                                                       \
         _Pragma("unroll") for (int k = 0; k < 4; ++k) {                                                \
             if (NCF_DIAG_DHALF && wv < kDw1Waves / 2) break;                                           \
             const int row = 4 * k + lq;                                                                \
@@ -613,7 +676,9 @@ __global__ __launch_bounds__(64 * kDw1Waves, 2) void k_lay_dw1(const float* __re
             _Pragma("unroll") for (int x = 0; x < XT; ++x)                                             \
             _Pragma("unroll") for (int y = 0; y < YT; ++y) acc[x][y] = mfma16(a[x], b[y], acc[x][y]);  \
         }                                                                                              \
+        }                                                                                              \
         if (u_ + 2 < nu) { NCF_DW1_STASH(CUR, lds + ((u_ + 2) % kDw1Depth) * BUF); }                  \
+        NCF_DW1_GSUM(u_ + 1);                                                                          \
     }
     for (int u = 0; u < nu; u += 2) {   // two units per trip: the register sets alternate statically
         NCF_DW1_UNIT(u, v0, v1);
@@ -622,6 +687,7 @@ __global__ __launch_bounds__(64 * kDw1Waves, 2) void k_lay_dw1(const float* __re
 #undef NCF_DW1_UNIT
 #undef NCF_DW1_FETCH
 #undef NCF_DW1_STASH
+#undef NCF_DW1_GSUM
     float* slab = slabs + (int64_t)chunk_id * P + LY * ysplit;
 #pragma unroll
     for (int x = 0; x < XT; ++x)
@@ -689,18 +755,28 @@ hipError_t launch_layer1_fwd(const ncf_shape_t& s, const float* emb, const float
 }
 
 hipError_t launch_layer1_dw(const ncf_shape_t& s, const float* x0, const float* g1, int64_t n, int64_t chunk,
-                            int nchunks, float* slabs, hipStream_t st) {
+                            int nchunks, float* slabs, hipStream_t st, int fold, const int32_t* users,
+                            const int32_t* items, IdSpace ids) {
     using S = L1ShapeD;
-    if (!l1matches<S>(s) || chunk <= 0 || nchunks <= 0) return hipErrorInvalidValue;
+    if (!l1matches<S>(s) || chunk <= 0 || nchunks <= 0 || chunk % 16 != 0) return hipErrorInvalidValue;
     static bool cfg = false;
     if (!cfg) {
-        if (hipError_t e = hipFuncSetAttribute((const void*)k_lay_dw1<S::L0, S::L1>,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)dw1_lds<S::L0, S::L1>()))
-            return e;
+        for (const void* f : {(const void*)k_lay_dw1<S::L0, S::L1, 0>, (const void*)k_lay_dw1<S::L0, S::L1, 2>,
+                              (const void*)k_lay_dw1<S::L0, S::L1, 4>, (const void*)k_lay_dw1<S::L0, S::L1, 8>})
+            if (hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                   (int)dw1_lds<S::L0, S::L1>()))
+                return e;
         cfg = true;
     }
-    launch(k_lay_dw1<S::L0, S::L1>, nchunks * kDw1Split, 64 * kDw1Waves, dw1_lds<S::L0, S::L1>(), st, x0, g1, n,
-           (int)chunk, slabs, (int64_t)s.mlp_params);
+    const bool gu = NCF_LAYERED_GU && users && items && (fold == 2 || fold == 4 || fold == 8);
+#define NCF_DW1_LAUNCH(F)                                                                                     \
+    launch(k_lay_dw1<S::L0, S::L1, F>, nchunks * kDw1Split, 64 * kDw1Waves, dw1_lds<S::L0, S::L1>(), st, x0, g1, n, \
+           (int)chunk, slabs, (int64_t)s.mlp_params, users, items, ids)
+    if (gu && fold == 2) NCF_DW1_LAUNCH(2);
+    else if (gu && fold == 4) NCF_DW1_LAUNCH(4);
+    else if (gu && fold == 8) NCF_DW1_LAUNCH(8);
+    else NCF_DW1_LAUNCH(0);
+#undef NCF_DW1_LAUNCH
     return hipGetLastError();
 }
 

@@ -89,7 +89,8 @@ hipError_t launch_fb_layered(const ncf_shape_t& s, const WsLayout& L, void* ws, 
     e = launch_laymid(s, mlp, X[1], emb, labels, users, items, n, ids, inv_batch, probs, dzo, Gd[1], slab,
                       at<float>(ws, L.part_bce), nsl, st);
     if (e != hipSuccess) return e;
-    e = launch_layer1_dw(s, X[0], Gd[1], n, chunk, nsl, slab, st);
+    // (the group form of dW1 needs the group form's X0: both follow gpart)
+    e = launch_layer1_dw(s, X[0], Gd[1], n, chunk, nsl, slab, st, gpart ? fold : 0, users, items, ids);
     if (e != hipSuccess) return e;
     e = launch_layer1_bwd(s, emb, mlp, users, items, n, ids, (const float*)dzo, (const float*)Gd[1], gs, st, fold);
     if (e != hipSuccess) return e;
