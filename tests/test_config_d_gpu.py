@@ -260,3 +260,56 @@ def test_large_key_space_index_matches_compacted_table(lazy):
     assert torch.equal(big.emb[rows], small.emb)
     assert torch.equal(big.emb_m[rows], small.emb_m) and torch.equal(big.emb_v[rows], small.emb_v)
     assert torch.equal(big.mlp, small.mlp) and torch.equal(big.stats, small.stats)
+
+
+def test_layered_sparse_index_mixed_groups_matches_compacted_table():
+    """Config D's widths on a table past 256 scan blocks (600,000 x 500 rows): the layered path with
+    the sparse counted index (k_fill_touched, seen tags), user-row folding and layer 1's user half
+    once per group (k_lay_l1f_gu, k_lay_dw1<4>), on batches that mix folded groups, groups with
+    another user and masked-free samples, equals bit for bit the same steps on the compacted table
+    (the rows the batches read, ids remapped: the dense index of a small key space).  Both engines
+    run the same kernels on the same samples, so only the index paths differ."""
+    Ub, Ib = 600_000, 500
+    B, steps = 4096, 3
+    rng = np.random.RandomState(17)
+    bt = []
+    for s in range(steps):
+        users = rng.randint(0, Ub, B // GROUP).repeat(GROUP)
+        pos = np.arange(B) % GROUP
+        swap = (pos != 0) & (rng.rand(B) < 0.05)          # a few samples with another user
+        users[swap] = rng.randint(0, Ub, int(swap.sum()))
+        if s == 0:
+            users[:GROUP] = 0
+            users[GROUP:2 * GROUP] = Ub - 1
+        bt.append((users.astype(np.int32), rng.randint(0, Ib, B).astype(np.int32),
+                   np.tile([0.0] * (GROUP - 1) + [1.0], B // GROUP).astype(np.float32)))
+    uu = np.unique(np.concatenate([b[0] for b in bt]))
+    ii = np.unique(np.concatenate([b[1] for b in bt]))
+    big = NCFEngine(Ub, Ib, LAYERS, GMF, max_batch=B, lazy_adam=True)
+    assert big.kernel_for(B) == "layered-mfma" and big.num_rows + 1 > 256 * 2048
+    _device_tables(big, seed=18)
+    small = NCFEngine(len(uu), len(ii), LAYERS, GMF, max_batch=B, lazy_adam=True)
+    small.emb[:len(uu)].copy_(big.emb[torch.from_numpy(uu.astype(np.int64)).cuda()])
+    small.emb[len(uu):].copy_(big.emb[torch.from_numpy(ii.astype(np.int64) + Ub).cuda()])
+    dense = _dense_weights(19)
+    from movierec.layout import Layout
+    flat = Layout(1, 1, LAYERS, GMF).to_device({**dense, "user_embedding": np.zeros((1, 128)),
+                                                 "item_embedding": np.zeros((1, 128)),
+                                                 "user_gmf_embedding": np.zeros((1, GMF)),
+                                                 "item_gmf_embedding": np.zeros((1, GMF))})[1]
+    big.mlp.copy_(torch.from_numpy(flat))
+    small.mlp.copy_(big.mlp)
+    dev_b = [tuple(torch.from_numpy(a).cuda() for a in b) for b in bt]
+    dev_s = [(torch.from_numpy(np.searchsorted(uu, b[0]).astype(np.int32)).cuda(),
+              torch.from_numpy(np.searchsorted(ii, b[1]).astype(np.int32)).cuda(), d[2]) for b, d in zip(bt, dev_b)]
+    for eng, dev in ((big, dev_b), (small, dev_s)):
+        for s, (u, it, y) in enumerate(dev):
+            nxt = (dev[s + 1][0], dev[s + 1][1]) if s + 1 < steps else None
+            eng.train_step(u, it, y, group=GROUP, k=2, next_batch=nxt)
+        eng.check_errors()
+        eng.flush()
+    torch.cuda.synchronize()
+    rows = torch.from_numpy(np.concatenate([uu, ii + Ub]).astype(np.int64)).cuda()
+    assert torch.equal(big.emb[rows], small.emb)
+    assert torch.equal(big.emb_m[rows], small.emb_m) and torch.equal(big.emb_v[rows], small.emb_v)
+    assert torch.equal(big.mlp, small.mlp) and torch.equal(big.stats, small.stats)
