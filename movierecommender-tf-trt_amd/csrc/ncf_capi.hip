@@ -224,6 +224,9 @@ int fb_variant(const ncf_shape_t& s, const ncf_hyper_t* h, int64_t n) {
 #ifndef NCF_LAYERED_FOLD
 #define NCF_LAYERED_FOLD 1
 #endif
+#ifndef NCF_REPLAY_IN_SCAN
+#define NCF_REPLAY_IN_SCAN 1   // short catch-up-ahead replays in the stats launch (0: all in the update's count blocks)
+#endif
 int index_fold(const ncf_shape_t& s, const ncf_hyper_t* h) {
     static const bool on = [] {
         const char* e = ncf::experiment_env("NCF_FOLD_USERS");
@@ -274,6 +277,11 @@ WsLayout make_layout(const ncf_shape_t& s, int64_t B, int world) {
         L.oifold = take(4);
     }
     L.persistent_end = off;
+    if (world == 0) {
+        L.claims = take((size_t)2 * B * 8);
+        L.nclaim = take((size_t)(2 * B / 16 + 1) * 4);
+        L.claim_t = take(4);
+    }
     if (world > 0) {
         // the owner index: sized by the shard only, ahead of every per-batch region
         L.onscan = (int)((S + 1 + kScanBlock - 1) / kScanBlock);
@@ -825,12 +833,18 @@ static int train_step_impl(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t
                                fb.n_groups, fold && !two_level ? summary : nullptr, defer_mlp ? &mlp_def : nullptr);
     prof_end(NCF_K_MLP_UPDATE, st2);
     if (e != hipSuccess) return hip_check(e, "dense update");
+    // counting ahead: the next batch's stale rows are claimed in the touched-row update launch; those
+    // owing a few steps are replayed in the stats launch behind it (off the update's HBM stream),
+    // the long chains stay under the update (profiles/r06_ab/replay_in_scan)
+    bool defer_replay = NCF_REPLAY_IN_SCAN && lazy && next_users != nullptr && L.world == 0 &&
+                        h->optimizer == NCF_OPT_ADAM;
     prof_begin(NCF_K_EMB_UPDATE, st);
     if (lazy)
         e = ncf::launch_emb_update_touched(*s, L, ws, model->emb, optim->emb_m, optim->emb_v, optim->row_step,
                                            optim->step, *h, st, next_users, next_items, n_next,
                                            mlp_def.p ? &mlp_def : nullptr, index_fold(*s, h),
-                                           fb.met.nblocks > 0 ? &fb.met : nullptr, nullptr, kfill, true, sparse_build);
+                                           fb.met.nblocks > 0 ? &fb.met : nullptr, nullptr, kfill, true, sparse_build,
+                                           &defer_replay);
     else
         e = ncf::launch_emb_update(*s, L, ws, model->emb, optim->emb_m, optim->emb_v, optim->step, *h, nullptr,
                                    s->num_rows, st);
@@ -839,13 +853,16 @@ static int train_step_impl(const ncf_shape_t* s, ncf_model_t* model, ncf_optim_t
     e = join_side(st, ss);
     if (e != hipSuccess) return hip_check(e, "side-stream join");
     const int nreg_emb = h->l2[0] != 0.0f ? ncf::kUpdateGrid : 0;
+    const ncf::ReplayDeferred rdef{model->emb, optim->emb_m, optim->emb_v, s->row_width, h->lr, h->beta_1, h->beta_2,
+                                   h->epsilon, lazy && defer_replay ? 2 * n_next : 0};
     // counting ahead: the stats launch also scans the next batch's counts
     // (an in-kernel fill's step may have been dropped: the stats launch then adds nothing, bumps
     // nothing and clears the word)
     e = ncf::launch_stats(L, ws, summary, nreg_emb, nreg_mlp, h->inv_batch, stats, optim->step, true, st,
                           lazy && next_users != nullptr, s->num_rows,
                           two_level ? ncf::SummaryFirst{fb.nbce, fb.nmet, fb.n_groups} : ncf::SummaryFirst{-1, 0, 0.f},
-                          kfill ? ncf::at<int32_t>(ws, L.stale_step) : nullptr, sparse_ok && next_users != nullptr);
+                          kfill ? ncf::at<int32_t>(ws, L.stale_step) : nullptr, sparse_ok && next_users != nullptr,
+                          &rdef);
     return hip_check(e, "stats");
 }
 

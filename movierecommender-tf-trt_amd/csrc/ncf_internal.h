@@ -76,6 +76,9 @@ struct WsLayout {
     size_t seen;      // int32[K+1] persistent (single table): the sparse index's tag of the batch that last
                       // touched each key (sparse_index_ok: k_fill_touched writes it, the count blocks read it)
     size_t itag;      // int32      persistent: the last sparse index's tag (bumped by the stats launch)
+    size_t claims;    // int2[2B]    single table: the catch-up-ahead claims (key, s0) per count pass
+    size_t nclaim;    // int32[2B / 16 + 1] their number per pass
+    size_t claim_t;   // int32       their replay target step
     size_t cid_u;     // int32[B]    compact (unique-row) id of each sample's user row
     size_t cid_i;     // int32[B]    compact id of each sample's item row
     size_t uoffs;     // int32[2B+1] compact row -> first list slot
@@ -887,7 +890,12 @@ hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, vo
                                      const int32_t* next_items = nullptr, int64_t n_next = 0,
                                      const MlpDeferred* mlp = nullptr, int next_fold = 0,
                                      const MetricsDeferred* met = nullptr, const float* grad_rows = nullptr,
-                                     bool unsorted_lists = false, bool may_drop = true, bool sparse_index = false);
+                                     bool unsorted_lists = false, bool may_drop = true, bool sparse_index = false,
+                                     bool* defer_replay = nullptr);
+// *defer_replay (in: asked, out: done): the count blocks only claim the next batch's stale rows (ws
+// claims / nclaim / claim_t); the stats launch behind this one must replay them (launch_stats'
+// ReplayDeferred with 2 n_next contributions)
+int64_t count_ahead_passes(int64_t contributions);
 // (may_drop false: a fill overflow does not drop the step — data parallelism, where a rank that
 // skipped its step would leave the replicas apart; the error is still reported)
 // (grad_rows: the contribution rows the list indexes; default the workspace's per-sample rows gs)
@@ -934,6 +942,14 @@ hipError_t launch_scan_ahead(const WsLayout& L, void* ws, int64_t keys, hipStrea
 // over the counts the touched update took ahead)
 // summary_first (nbce >= 0): block 0 first writes the batch summary (launch_summary's work with
 // no L2 partials) and then folds it into stats
+// the catch-up-ahead replay a defer_replay update left to the stats launch: the tables, the
+// hyperparameters and the counted contributions (2 n_next)
+struct ReplayDeferred {
+    float *emb, *m, *v;
+    int row_width;
+    float lr, beta_1, beta_2, epsilon;
+    int64_t contributions;
+};
 struct SummaryFirst {
     int nbce, nmet;
     float n_groups;
@@ -943,7 +959,7 @@ struct SummaryFirst {
 hipError_t launch_stats(const WsLayout& L, void* ws, const float* summary, int nreg_emb, int nreg_mlp,
                         float inv_batch, double* stats, int32_t* step, bool bump_step, hipStream_t st,
                         bool scan_ahead = false, int64_t scan_keys = 0, SummaryFirst sf = SummaryFirst{-1, 0, 0.f},
-                        int32_t* drop = nullptr, bool sparse_scan = false);
+                        int32_t* drop = nullptr, bool sparse_scan = false, const ReplayDeferred* replay = nullptr);
 
 // on-device negative sampling (ncf_sample.hip)
 hipError_t launch_sample_batch(const int32_t* pos_users, const int32_t* pos_items, const int32_t* excl_ptr,

@@ -582,7 +582,124 @@ struct CountAhead {
                                // updated here and caught up ahead (the rest are swept densely)
     const int32_t* seen;       // sparse index (sparse_index_ok): key in this step's batch <=> seen[key] ==
     const int32_t* itag;       // *itag + 1 (k_fill_touched's tag); nullptr: the offsets tell
+    // replay deferred to the scan launch behind this one (claims != nullptr): pass p's claimed rows
+    // (key, s0) at claims[p per ..), their number at nclaim[p], the replay target step at *claim_t
+    int2* claims;
+    int32_t* nclaim;
+    int32_t* claim_t;
 };
+
+// The claimed rows crow[0, ncl) (their steps cstep) replayed to step t, p only under P-ahead: the
+// block's 4 waves share the (row, 128-element slice) items, kRepC per wave at a time (2 in the
+// update launch's count blocks keep its 72-VGPR cap unspilled).  Whole block; lut holds the bias-
+// corrected lr of steps t, t - 1, ...
+template <int kRepC = 2>
+__device__ __forceinline__ void replay_claimed(float* __restrict__ embf, float* __restrict__ mf, float* __restrict__ vf,
+                                               int W, int ncl, const int* crow, const int* cstep, int t,
+                                               const float* lut, float lr, float b1, float b2, float eps,
+                                               int wv, int nwv) {
+    const int lane = threadIdx.x & 63;
+    const int per_row = (W + 127) >> 7;
+    const int items = ncl * per_row;
+    // item it = row it / per_row, elements (it % per_row) * 128 + 2 lane + {0, 1} (W is a
+    // multiple of 4); wave wv of the nwv sharing the rows takes it = wv + nwv j (wave-uniform: the
+    // step loops do not diverge)
+    const f32x2 z2 = {0.f, 0.f};
+    for (int i0 = wv; i0 < items; i0 += nwv * kRepC) {
+        f32x2 p[kRepC], mm[kRepC], vv[kRepC];
+        size_t e[kRepC];
+        int sr[kRepC];
+        bool act[kRepC];
+#pragma unroll
+        for (int j = 0; j < kRepC; ++j) {
+            const int it = i0 + nwv * j;
+            const int k = it < items ? it / per_row : 0;
+            const int q = (it - k * per_row) * 128 + 2 * lane;
+            act[j] = it < items && q < W;
+            sr[j] = it < items ? cstep[k] : t;
+            e[j] = (size_t)crow[k] * W + (act[j] ? q : 0);
+            p[j] = act[j] ? *reinterpret_cast<const f32x2*>(embf + e[j]) : z2;
+            mm[j] = act[j] ? *reinterpret_cast<const f32x2*>(mf + e[j]) : z2;
+            vv[j] = act[j] ? *reinterpret_cast<const f32x2*>(vf + e[j]) : z2;
+        }
+#if NCF_REPLAY_UNROLL > 1
+#pragma unroll
+        for (int j = 0; j < kRepC; ++j) replay2<NCF_REPLAY_UNROLL>(p[j], mm[j], vv[j], sr[j], t, lut, lr, b1, b2, eps);
+#else
+        // the items' chains advance together (same per-element arithmetic, step by step)
+        int smin = t;
+#pragma unroll
+        for (int j = 0; j < kRepC; ++j) smin = sr[j] < smin ? sr[j] : smin;
+        for (int st = smin + 1; st <= t; ++st) {
+            const float lrt = t - st < kLrLut ? lut[t - st] : adam_lr_t(lr, b1, b2, st);
+#pragma unroll
+            for (int j = 0; j < kRepC; ++j)
+                if (st > sr[j]) adam2_zero(p[j], mm[j], vv[j], lrt, b1, b2, eps);
+        }
+#endif
+#pragma unroll
+        for (int j = 0; j < kRepC; ++j) {
+            if (act[j]) {
+                *reinterpret_cast<f32x2*>(embf + e[j]) = p[j];
+                if (!NCF_AHEAD_P_ONLY) {  // P-ahead: the next update re-derives m and v
+                    *reinterpret_cast<f32x2*>(mf + e[j]) = mm[j];
+                    *reinterpret_cast<f32x2*>(vf + e[j]) = vv[j];
+                }
+            }
+        }
+    }
+}
+
+// The replay half of the catch-up ahead in the scan launch (CountAhead::claims): one block per
+// count pass, the pass's claims staged in LDS, then replay_claimed — the same items, arithmetic
+// and stores as when the count blocks replay (bitwise), off the touched-row update's HBM stream.
+struct ReplayAhead {
+    int npass;                 // 0: none
+    int per;
+    const int2* claims;
+    const int32_t* nclaim;
+    const int32_t* claim_t;
+    float *emb, *m, *v;
+    int W;
+    float lr, b1, b2, eps;
+};
+#ifndef NCF_DEFER_OWED
+#define NCF_DEFER_OWED 8   // deferred replay: rows owing at most this many steps go to the scan launch
+#endif
+constexpr int kDeferOwed = NCF_DEFER_OWED;
+#ifndef NCF_REPLAY_PASSES
+#define NCF_REPLAY_PASSES 2   // count passes per replay block of the scan launch (4 items per wave in flight)
+#endif
+constexpr int kReplayPasses = NCF_REPLAY_PASSES;
+__device__ inline void replay_ahead_block(const ReplayAhead& ra, int blk) {
+    static_assert(kReplayPasses * 64 <= kBlock, "one claim slot per thread");
+    __shared__ float lut[kLrLut];
+    __shared__ int crow[64 * kReplayPasses], cstep[64 * kReplayPasses];
+    // this block's passes' claims, compacted into LDS (every thread reads the passes' counts)
+    const int p0 = blk * kReplayPasses;
+    int cnt[kReplayPasses];
+#pragma unroll
+    for (int j = 0; j < kReplayPasses; ++j) cnt[j] = p0 + j < ra.npass ? ra.nclaim[p0 + j] : 0;
+    const int t = *ra.claim_t;
+    const int jp = (int)threadIdx.x >> 6, q = (int)threadIdx.x & 63;
+    int before = 0, ncl = 0;
+#pragma unroll
+    for (int j = 0; j < kReplayPasses; ++j) {
+        before += j < jp ? cnt[j] : 0;
+        ncl += cnt[j];
+    }
+    if (jp < kReplayPasses && q < cnt[jp]) {
+        const int2 c = ra.claims[(int64_t)(p0 + jp) * ra.per + q];
+        crow[before + q] = c.x;
+        cstep[before + q] = c.y;
+    }
+    if (ncl > 0 && threadIdx.x < kLrLut)
+        lut[threadIdx.x] = t - (int)threadIdx.x >= 1 ? adam_lr_t(ra.lr, ra.b1, ra.b2, t - threadIdx.x) : 0.f;
+    if (ncl == 0) return;  // (block-uniform)
+    __syncthreads();
+    replay_claimed<2 * kReplayPasses>(ra.emb, ra.m, ra.v, ra.W, ncl, crow, cstep, t, lut, ra.lr, ra.b1, ra.b2,
+                                      ra.eps, (int)threadIdx.x >> 6, kBlock / 64);
+}
 
 // the dense layers' Adam (k_mlp_update<ADAM>'s work) in blocks >= nupd + ncount of the same launch;
 // two_level: in the FIRST blocks of the launch, 16 parameters per block, from the raw slabs
@@ -858,57 +975,95 @@ __global__ __launch_bounds__(kBlock, UNSORTED ? NCF_TOUCHED_MIN_BLOCKS_UNSORTED 
         __shared__ float lut[kLrLut];
         const int t = *step + (dropped ? 0 : 1);
         const int tagc = ca.seen ? *ca.itag + 1 : 0;
+        const bool defer = ca.claims != nullptr;
         if (ca.replay && threadIdx.x < kLrLut)
             lut[threadIdx.x] = t - (int)threadIdx.x >= 1 ? adam_lr_t(lr, b1, b2, t - threadIdx.x) : 0.f;
         const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
         const int W = 4 * (int)w4;
+        // one pass of one wave: count contributions [cb, cb + per) and claim their stale rows;
+        // returns the claims' ballot (the claiming lanes in ascending order)
+        const int per = ca.per;
+        auto count_pass = [&](int64_t cb, int& key, int& s0) -> uint64_t {
+            const int64_t c = cb + lane;
+            bool ok = false;
+            key = 0;
+            if (lane < per && c < ca.m) {
+                const int64_t i = c >> 1;
+                const int id = (c & 1) ? ca.items[i] : ca.users[i];
+                const int bound = (c & 1) ? ca.I : ca.U;
+                ok = (unsigned)id < (unsigned)bound && ((c & 1) || !folded_user(ca.users, i, ca.fold));
+                key = (c & 1) ? ca.U + id : id;
+            }
+            // the row's step and offsets go out before the count's atomic returns (one memory
+            // round trip); the lane whose run is the key's first occurrence in the next batch
+            // (its count was 0) owns the row's replay — no claim atomic of its own
+            int o0 = 0, o1 = 0, sv = t;
+            if (ca.replay && ok && key < ca.lazy_rows) {
+                if (UNSORTED) {   // (the in-kernel fill writes no offs array: the key's count instead)
+                    o0 = so.local[key];
+                    o1 = (key + 1) % kScanBlock != 0 ? so.local[key + 1] : so.tot[key / kScanBlock];
+                } else if (ca.seen) {   // sparse index: no offsets at keys outside the batch
+                    o1 = ca.seen[key] == tagc;
+                } else {
+                    o0 = offs[key];
+                    o1 = offs[key + 1];
+                }
+                sv = row_step[key];
+            }
+            const bool first = wave_run_count<true>(ca.cnt, key, ok);
+            // not in this step's batch (this launch's update blocks do not touch it) and behind
+            // (a P-ahead mark, negative, never occurs here: the previous step's update consumed it)
+            const bool claim = ca.replay && first && key < ca.lazy_rows && o1 == o0 && (unsigned)sv < (unsigned)t;
+            s0 = sv;
+            if (claim) row_step[key] = NCF_AHEAD_P_ONLY ? pahead_mark(s0) : t;
+            return __ballot(claim);
+        };
         float* embf = reinterpret_cast<float*>(emb);
         float* mf = reinterpret_cast<float*>(m4);
         float* vf = reinterpret_cast<float*>(v4);
+        if (defer) {
+            // replay in the scan launch behind this one (ReplayAhead): every wave counts passes of
+            // its own and writes the claims (key, s0) of rows owing at most kDeferOwed steps at the
+            // pass's slots, their number per pass; it replays the rest itself (the long chains stay
+            // under this launch's HBM stream — in the short scan launch they would be its critical path)
+            __shared__ int wrow[kBlock / 64][64], wstep[kBlock / 64][64];
+            __syncthreads();  // lut
+            const int64_t nw = (int64_t)ca.ncount * (kBlock / 64);
+            const uint64_t below = (1ull << lane) - 1;
+            for (int64_t ps = (int64_t)cblk * (kBlock / 64) + wv; ps * per < ca.m; ps += nw) {
+                int key, s0;
+                const uint64_t cm = count_pass(ps * per, key, s0);
+                const bool mine = (cm >> lane) & 1ull;
+                const bool near = mine && t - s0 <= kDeferOwed;
+                const uint64_t sm = __ballot(near), lm = cm & ~sm;
+                if (near) ca.claims[ps * per + __popcll(sm & below)] = make_int2(key, s0);
+                if (lane == 0) ca.nclaim[ps] = __popcll(sm);
+                if (lm) {  // (wave-uniform)
+                    if (mine && !near) {
+                        const int slot = __popcll(lm & below);
+                        wrow[wv][slot] = key;
+                        wstep[wv][slot] = s0;
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    replay_claimed(embf, mf, vf, W, __popcll(lm), wrow[wv], wstep[wv], t, lut, lr, b1, b2, eps, 0, 1);
+                    __builtin_amdgcn_wave_barrier();
+                }
+            }
+            if (cblk == 0 && threadIdx.x == 0) *ca.claim_t = t;
+            return;
+        }
         // a block takes ca.per contributions per pass: wave 0 counts them and claims the stale
         // rows, then the block's 4 waves share the claimed rows' replay, kRep (row, 64-element
         // slice) items per wave at a time with all their loads in flight and their step chains
         // interleaved — many short replay chains in flight (small batches get 16 contributions
         // per block: their rows owe many steps each), one memory round trip per batch of items
         __shared__ int crow[64], cstep[64], ncl;
-        const int per = ca.per;
         for (int64_t cb = (int64_t)cblk * per; cb < ca.m; cb += (int64_t)ca.ncount * per) {
             __syncthreads();  // lut ready, the previous pass's replay done
             if (wv == 0) {
-                const int64_t c = cb + lane;
-                bool ok = false;
-                int key = 0;
-                if (lane < per && c < ca.m) {
-                    const int64_t i = c >> 1;
-                    const int id = (c & 1) ? ca.items[i] : ca.users[i];
-                    const int bound = (c & 1) ? ca.I : ca.U;
-                    ok = (unsigned)id < (unsigned)bound && ((c & 1) || !folded_user(ca.users, i, ca.fold));
-                    key = (c & 1) ? ca.U + id : id;
-                }
-                // the row's step and offsets go out before the count's atomic returns (one memory
-                // round trip); the lane whose run is the key's first occurrence in the next batch
-                // (its count was 0) owns the row's replay — no claim atomic of its own
-                int o0 = 0, o1 = 0, sv = t;
-                if (ca.replay && ok && key < ca.lazy_rows) {
-                    if (UNSORTED) {   // (the in-kernel fill writes no offs array: the key's count instead)
-                        o0 = so.local[key];
-                        o1 = (key + 1) % kScanBlock != 0 ? so.local[key + 1] : so.tot[key / kScanBlock];
-                    } else if (ca.seen) {   // sparse index: no offsets at keys outside the batch
-                        o1 = ca.seen[key] == tagc;
-                    } else {
-                        o0 = offs[key];
-                        o1 = offs[key + 1];
-                    }
-                    sv = row_step[key];
-                }
-                const bool first = wave_run_count<true>(ca.cnt, key, ok);
-                // not in this step's batch (this launch's update blocks do not touch it) and behind
-                // (a P-ahead mark, negative, never occurs here: the previous step's update consumed it)
-                const bool claim = ca.replay && first && key < ca.lazy_rows && o1 == o0 && (unsigned)sv < (unsigned)t;
-                const int s0 = sv;
-                if (claim) row_step[key] = NCF_AHEAD_P_ONLY ? pahead_mark(s0) : t;
-                const uint64_t cm = __ballot(claim);
-                if (claim) {
+                int key, s0;
+                const uint64_t cm = count_pass(cb, key, s0);
+                if ((cm >> lane) & 1ull) {
                     const int slot = __popcll(cm & ((1ull << lane) - 1));
                     crow[slot] = key;
                     cstep[slot] = s0;
@@ -916,56 +1071,7 @@ __global__ __launch_bounds__(kBlock, UNSORTED ? NCF_TOUCHED_MIN_BLOCKS_UNSORTED 
                 if (lane == 0) ncl = __popcll(cm);
             }
             __syncthreads();
-            const int per_row = (W + 127) >> 7;
-            const int items = ncl * per_row;
-            // item it = row it / per_row, elements (it % per_row) * 128 + 2 lane + {0, 1} (W is a
-            // multiple of 4); wave wv takes it = wv + 4 j (wave-uniform: the step loops do not diverge)
-            const f32x2 z2 = {0.f, 0.f};
-            constexpr int kRepC = 2;  // float2 items: two per wave keep the launch's 72-VGPR cap unspilled
-            for (int i0 = wv; i0 < items; i0 += 4 * kRepC) {
-                f32x2 p[kRepC], mm[kRepC], vv[kRepC];
-                size_t e[kRepC];
-                int sr[kRepC];
-                bool act[kRepC];
-#pragma unroll
-                for (int j = 0; j < kRepC; ++j) {
-                    const int it = i0 + 4 * j;
-                    const int k = it < items ? it / per_row : 0;
-                    const int q = (it - k * per_row) * 128 + 2 * lane;
-                    act[j] = it < items && q < W;
-                    sr[j] = it < items ? cstep[k] : t;
-                    e[j] = (size_t)crow[k] * W + (act[j] ? q : 0);
-                    p[j] = act[j] ? *reinterpret_cast<const f32x2*>(embf + e[j]) : z2;
-                    mm[j] = act[j] ? *reinterpret_cast<const f32x2*>(mf + e[j]) : z2;
-                    vv[j] = act[j] ? *reinterpret_cast<const f32x2*>(vf + e[j]) : z2;
-                }
-#if NCF_REPLAY_UNROLL > 1
-#pragma unroll
-                for (int j = 0; j < kRepC; ++j)
-                    replay2<NCF_REPLAY_UNROLL>(p[j], mm[j], vv[j], sr[j], t, lut, lr, b1, b2, eps);
-#else
-                // the items' chains advance together (same per-element arithmetic, step by step)
-                int smin = t;
-#pragma unroll
-                for (int j = 0; j < kRepC; ++j) smin = sr[j] < smin ? sr[j] : smin;
-                for (int st = smin + 1; st <= t; ++st) {
-                    const float lrt = t - st < kLrLut ? lut[t - st] : adam_lr_t(lr, b1, b2, st);
-#pragma unroll
-                    for (int j = 0; j < kRepC; ++j)
-                        if (st > sr[j]) adam2_zero(p[j], mm[j], vv[j], lrt, b1, b2, eps);
-                }
-#endif
-#pragma unroll
-                for (int j = 0; j < kRepC; ++j) {
-                    if (act[j]) {
-                        *reinterpret_cast<f32x2*>(embf + e[j]) = p[j];
-                        if (!NCF_AHEAD_P_ONLY) {  // P-ahead: the next update re-derives m and v
-                            *reinterpret_cast<f32x2*>(mf + e[j]) = mm[j];
-                            *reinterpret_cast<f32x2*>(vf + e[j]) = vv[j];
-                        }
-                    }
-                }
-            }
+            replay_claimed(embf, mf, vf, W, ncl, crow, cstep, t, lut, lr, b1, b2, eps, wv, kBlock / 64);
         }
         return;
     }
@@ -1736,16 +1842,18 @@ __global__ __launch_bounds__(kBlock) void k_stats_scan(float* __restrict__ summa
                                                        const float* __restrict__ reg_emb, int nreg_emb,
                                                        const float* __restrict__ reg_mlp, int nreg_mlp,
                                                        float inv_batch, double* __restrict__ stats, int32_t* step,
-                                                       int bump, ScanAhead sc, SummaryArgs sa) {
+                                                       int bump, ScanAhead sc, SummaryArgs sa, ReplayAhead ra) {
+    // block order: [stats] [replay ahead: the latency-bound chains first] [scan]
+    const int b = (int)blockIdx.x - 1 - (ra.npass + kReplayPasses - 1) / kReplayPasses;
     if (blockIdx.x == 0) {
         summary_stats_block(sa, summary, reg_emb, nreg_emb, reg_mlp, nreg_mlp, inv_batch, stats, step, bump);
         if (sc.itag && threadIdx.x == 0) *sc.itag += 1;
+    } else if (b < 0) {
+        replay_ahead_block(ra, (int)blockIdx.x - 1);
     } else if (sc.sparse) {
-        scan_local_body<true, true>(sc.cnt, sc.r1, sc.offs, sc.tot, sc.uloc, sc.utot, (int)blockIdx.x - 1, sc.cursor,
-                                    sc.heavy_n, sc.to);
+        scan_local_body<true, true>(sc.cnt, sc.r1, sc.offs, sc.tot, sc.uloc, sc.utot, b, sc.cursor, sc.heavy_n, sc.to);
     } else {
-        scan_local_body<true>(sc.cnt, sc.r1, sc.offs, sc.tot, sc.uloc, sc.utot, (int)blockIdx.x - 1, sc.cursor,
-                              sc.heavy_n, sc.to);
+        scan_local_body<true>(sc.cnt, sc.r1, sc.offs, sc.tot, sc.uloc, sc.utot, b, sc.cursor, sc.heavy_n, sc.to);
     }
 }
 
@@ -1822,6 +1930,14 @@ hipError_t launch_emb_update(const ncf_shape_t& s, const WsLayout& L, void* ws, 
 #ifndef NCF_TOUCHED_GRID_MAX
 #define NCF_TOUCHED_GRID_MAX 8192
 #endif
+// count (+ catch-up ahead) blocks: 64 contributions per pass, 32 below 65,536 contributions
+// (NCF_COUNT_PER_SMALL below 32,768)
+static int count_per(int64_t mc) { return mc >= 65536 ? NCF_COUNT_PER_MAX : mc >= 32768 ? 32 : NCF_COUNT_PER_SMALL; }
+int64_t count_ahead_passes(int64_t mc) {
+    const int per = count_per(mc);
+    return (mc + per - 1) / per;
+}
+
 static unsigned row_grid(int64_t rows, uint32_t w4, int64_t cap) {
     const int64_t rpw = w4 <= 64 ? 64 / w4 : 1;
     int64_t g = (rows + rpw * 4 - 1) / (rpw * 4);  // 4 waves per block
@@ -1916,7 +2032,8 @@ hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, vo
                                      float* v, int32_t* row_step, int32_t* step, const ncf_hyper_t& h,
                                      hipStream_t st, const int32_t* next_users, const int32_t* next_items,
                                      int64_t n_next, const MlpDeferred* mlp, int next_fold, const MetricsDeferred* met,
-                                     const float* grad_rows, bool unsorted_lists, bool may_drop, bool sparse_index) {
+                                     const float* grad_rows, bool unsorted_lists, bool may_drop, bool sparse_index,
+                                     bool* defer_replay) {
 #if NCF_DIAG_UPD == 1  // diagnostic timing builds only (wrong numerics): no catch-up ahead
     const bool replay_ahead = false;
 #else
@@ -1931,16 +2048,21 @@ hipError_t launch_emb_update_touched(const ncf_shape_t& s, const WsLayout& L, vo
     if (h.optimizer == NCF_OPT_ADAM) {
         const unsigned nupd = row_grid(R < 2 * L.max_batch ? R : 2 * L.max_batch, w4, NCF_TOUCHED_GRID_MAX);
         const int64_t mc = next_users ? 2 * n_next : 0;
-        // count (+ catch-up ahead) blocks: 64 contributions per block and pass, 32 below 65,536
-        // contributions (NCF_COUNT_PER_SMALL below 32,768)
-        const int per = mc >= 65536 ? NCF_COUNT_PER_MAX : mc >= 32768 ? 32 : NCF_COUNT_PER_SMALL;
-        const int64_t npass = (mc + per - 1) / per;
-        const unsigned ncount = mc > 0 ? (unsigned)(npass < NCF_COUNT_BLOCKS_MAX ? npass : NCF_COUNT_BLOCKS_MAX) : 0u;
+        const int per = count_per(mc);
+        const int64_t npass = count_ahead_passes(mc);
+        // deferred replay: the count blocks' 4 waves take a pass each (no replay to share)
+        const bool defer = defer_replay && *defer_replay && replay_ahead && mc > 0;
+        if (defer_replay) *defer_replay = defer;
+        if (defer && (L.world != 0 || mc > 2 * L.max_batch)) return hipErrorInvalidValue;
+        const int64_t nblk = defer ? (npass + kBlock / 64 - 1) / (kBlock / 64) : npass;
+        const unsigned ncount = mc > 0 ? (unsigned)(nblk < NCF_COUNT_BLOCKS_MAX ? nblk : NCF_COUNT_BLOCKS_MAX) : 0u;
         if (sparse_index && (unsorted_lists || !sparse_index_ok(L))) return hipErrorInvalidValue;
         CountAhead ca{(int)nupd, (int)ncount, next_users, next_items, mc, s.num_users, s.num_items,
                       at<int32_t>(ws, L.cnt_ahead), replay_ahead ? 1 : 0, next_fold, per, lazy_bound(s, h),
                       sparse_index ? at<const int32_t>(ws, L.seen) : nullptr,
-                      sparse_index ? at<const int32_t>(ws, L.itag) : nullptr};
+                      sparse_index ? at<const int32_t>(ws, L.itag) : nullptr,
+                      defer ? at<int2>(ws, L.claims) : nullptr, defer ? at<int32_t>(ws, L.nclaim) : nullptr,
+                      defer ? at<int32_t>(ws, L.claim_t) : nullptr};
         MlpTail mt{};
         if (mlp) {
             mt = MlpTail{mlp->two_level ? (s.mlp_params + 15) / 16 : (s.mlp_params + kBlock - 1) / kBlock, mlp->p,
@@ -2217,7 +2339,8 @@ hipError_t launch_summary(const WsLayout& L, void* ws, int nbce, int nmet, float
 
 hipError_t launch_stats(const WsLayout& L, void* ws, const float* summary_in, int nreg_emb, int nreg_mlp,
                         float inv_batch, double* stats, int32_t* step, bool bump_step, hipStream_t st,
-                        bool scan_ahead, int64_t scan_keys, SummaryFirst sf, int32_t* drop, bool sparse_scan) {
+                        bool scan_ahead, int64_t scan_keys, SummaryFirst sf, int32_t* drop, bool sparse_scan,
+                        const ReplayDeferred* replay) {
     const float* reg = at<float>(ws, L.part_reg);
     // written only by the summary_first block (the workspace's summary); read-only otherwise
     float* summary = const_cast<float*>(summary_in);
@@ -2232,10 +2355,19 @@ hipError_t launch_stats(const WsLayout& L, void* ws, const float* summary_in, in
                      at<int32_t>(ws, L.uloc), at<int32_t>(ws, L.utot), at<int32_t>(ws, L.cnt), at<int32_t>(ws, L.heavy_n),
                      touched_out(L, ws), sparse_scan ? 1 : 0, sparse_scan ? at<int32_t>(ws, L.itag) : nullptr};
         if (sparse_scan && (!sparse_index_ok(L) || r1 != L.keys + 1)) return hipErrorInvalidValue;
-        launch(k_stats_scan, 1 + nscan, kBlock, 0, st, summary, reg, nreg_emb, reg + kUpdateGrid, nreg_mlp, inv_batch,
-               stats, step, bump_step ? 1 : 0, sc, sa);
+        ReplayAhead ra{};
+        if (replay && replay->contributions > 0) {
+            if (L.world != 0 || replay->contributions > 2 * L.max_batch) return hipErrorInvalidValue;
+            const int64_t mc = replay->contributions;
+            ra = ReplayAhead{(int)count_ahead_passes(mc), count_per(mc), at<const int2>(ws, L.claims),
+                             at<const int32_t>(ws, L.nclaim), at<const int32_t>(ws, L.claim_t), replay->emb, replay->m,
+                             replay->v, replay->row_width, replay->lr, replay->beta_1, replay->beta_2, replay->epsilon};
+        }
+        launch(k_stats_scan, 1 + (ra.npass + kReplayPasses - 1) / kReplayPasses + nscan, kBlock, 0, st, summary, reg, nreg_emb, reg + kUpdateGrid, nreg_mlp,
+               inv_batch, stats, step, bump_step ? 1 : 0, sc, sa, ra);
         return hipGetLastError();
     }
+    if (replay && replay->contributions > 0) return hipErrorInvalidValue;  // (the replay rides on the scan)
     launch(k_stats, 1, kBlock, 0, st, summary, reg, nreg_emb, reg + kUpdateGrid, nreg_mlp, inv_batch, stats, step,
                                   bump_step ? 1 : 0, sa);
     return hipGetLastError();
