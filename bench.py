@@ -39,6 +39,7 @@ process may use), the run length bounded by ``--cpu-seconds`` unless
 import argparse
 import json
 import os
+import re
 import sys
 import time
 
@@ -167,27 +168,43 @@ def emb_update_bytes(cfg_shape, batch, dense_rows=None, sparse_rows=None, touche
     return 24 * R * W + c * W * 4 + c * 4 + (R + 1) * 4
 
 
-def replayed_rows(pool, warmup, steps, U, rows, items=True):
+def replayed_rows(pool, warmup, steps, U, rows, items=True, far=0):
     """Rows the catch-up-ahead blocks of a timed step's update launch replay, averaged over the
     timed steps: those of the next batch that this step does not touch and that some earlier step
     did (a row no step has touched yet is pristine: its zero moments make the zero-gradient steps
     a fixed point, nothing to replay).  ``items``: item rows are under deferred decay too (one
-    table; the user layout sweeps its replicated item rows)."""
+    table; the user layout sweeps its replicated item rows).  ``far`` > 0: only rows owing more than
+    that many steps (the one-table step replays the nearer ones in its stats launch, NCF_DEFER_OWED)."""
     seq = [pool[i % len(pool)] for i in range(warmup + steps + 1)]
 
     def rows_of(b):
         r = torch.unique(b[0].long())
         return torch.cat([r, U + torch.unique(b[1].long())]) if items else r
     seen = torch.zeros(rows, dtype=torch.bool, device=seq[0][0].device)
+    last = torch.zeros(rows, dtype=torch.long, device=seq[0][0].device)  # batch index of the last touch
     out = []
     cur = rows_of(seq[0])
     for t in range(len(seq) - 1):
         nxt = rows_of(seq[t + 1])
         if t >= warmup:
-            out.append(int((~torch.isin(nxt, cur) & seen[nxt]).sum()))
+            rep = ~torch.isin(nxt, cur) & seen[nxt]
+            if far > 0:
+                rep &= (t - last[nxt]) > far   # the update of batch t takes the row from step last + 1 to t + 1
+            out.append(int(rep.sum()))
         seen[cur] = True
+        last[cur] = t
         cur = nxt
     return float(np.mean(out)) if out else 0.0
+
+
+def deferred_replay_owed(info):
+    """The library's NCF_DEFER_OWED (rows owing at most this many steps are replayed in the stats
+    launch of a one-table step), from its build defines; 0 when the replays all run in the update."""
+    d = (info or {}).get("defines", "") or ""
+    if "NCF_REPLAY_IN_SCAN=0" in d:
+        return 0
+    m = re.search(r"NCF_DEFER_OWED=(\d+)", d)
+    return int(m.group(1)) if m else 8
 
 
 def fwd_bwd_flops(cfg):
@@ -852,7 +869,7 @@ def main():
     fb_ms = ms_fb / nfb if nfb else float("nan")
     fb_flops = fwd_bwd_flops(cfg) * B
     contribs = grad_rows(eng, B, g) if mode != "sharded" else 2 * B
-    replay_rows = 0.0
+    replay_rows = replay_rows_here = 0.0
     fb_bytes = fwd_bwd_bytes(eng.shape, B, contribs)
     fill_bytes = 0
     train_exchange = dp.last_exchange if mode == "sharded" else None
@@ -876,8 +893,12 @@ def main():
             # ... and catches the next batch's stale rows up (the rows it touches that this step
             # did not): their p, m, v read and written once more before the next forward pass
             replay_rows = replayed_rows(pool, args.warmup, args.steps, eng.num_users, eng.num_rows, items=True)
-            # a replayed row: p, m, v read, p written (the next update re-derives m and v: P-ahead rows)
-            nbytes += 16 * replay_rows * eng.shape.row_width
+            # a replayed row: p, m, v read, p written (the next update re-derives m and v: P-ahead rows);
+            # the rows owing few steps are replayed in the stats launch, not in this one
+            owed = deferred_replay_owed(N.build_info())
+            replay_rows_here = (replayed_rows(pool, args.warmup, args.steps, eng.num_users, eng.num_rows, items=True,
+                                              far=owed) if owed else replay_rows)
+            nbytes += 16 * replay_rows_here * eng.shape.row_width
         if eng.kernel_for(B) == "fused-mfma-wave" and B >= 16384:
             # the launch's dense-layer blocks reduce the wave kernel's 256 dense-gradient slabs (both
             # levels) and step the dense layers: slab reads + p, m, v of every dense parameter
@@ -893,7 +914,8 @@ def main():
             # batch's id reads + counter atomics and the replay of its own rows this step missed
             tu = float(np.mean([torch.unique(u).numel() for u, _, _ in pool[:16]]))
             own = 24 * tu * W + cu * W * 4 + cu * 4 + 2 * B * (4 + 8)
-            replay_rows = replayed_rows(pool, args.warmup, args.steps, eng.num_users, Uloc, items=False)
+            replay_rows = replay_rows_here = replayed_rows(pool, args.warmup, args.steps, eng.num_users, Uloc,
+                                                           items=False)
             own += 16 * replay_rows * W   # P-ahead replays: p, m, v read, p written
         else:
             own = 24 * Uloc * W + cu * W * 4 + cu * 4 + (Uloc + 1) * 4
@@ -1028,6 +1050,7 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "algorithmic_bytes_per_launch": nbytes, "avg_launch_ms": round(kern_ms, 5),
                 "gradient_rows_per_step": contribs, "replayed_rows_per_step": replay_rows,
+                "replayed_rows_in_launch": replay_rows_here,
                 "launches_per_step": round(nl / steps_of(N.K_EMB_UPDATE), 2),
                 "timed_steps": "every %d-th step of the timed region, one launch group per sampled step "
                                "(HIP events in the dispatch packets): %d launches timed" % (every, nl),
