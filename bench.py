@@ -204,7 +204,7 @@ def deferred_replay_owed(info):
     if "NCF_REPLAY_IN_SCAN=0" in d:
         return 0
     m = re.search(r"NCF_DEFER_OWED=(\d+)", d)
-    return int(m.group(1)) if m else 8
+    return int(m.group(1)) if m else 4   # ncf_update.hip's default
 
 
 def fwd_bwd_flops(cfg):

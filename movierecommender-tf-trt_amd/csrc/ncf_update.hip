@@ -664,9 +664,12 @@ struct ReplayAhead {
     float lr, b1, b2, eps;
 };
 #ifndef NCF_DEFER_OWED
-#define NCF_DEFER_OWED 8   // deferred replay: rows owing at most this many steps go to the scan launch
+#define NCF_DEFER_OWED 4   // deferred replay: rows owing at most this many steps go to the scan launch
 #endif
 constexpr int kDeferOwed = NCF_DEFER_OWED;
+#ifndef NCF_DEFER_LONG_REPC
+#define NCF_DEFER_LONG_REPC 1   // items in flight per wave of the count blocks' own (long) replays
+#endif
 #ifndef NCF_REPLAY_PASSES
 #define NCF_REPLAY_PASSES 2   // count passes per replay block of the scan launch (4 items per wave in flight)
 #endif
@@ -1045,7 +1048,8 @@ __global__ __launch_bounds__(kBlock, UNSORTED ? NCF_TOUCHED_MIN_BLOCKS_UNSORTED 
                         wstep[wv][slot] = s0;
                     }
                     __builtin_amdgcn_wave_barrier();
-                    replay_claimed(embf, mf, vf, W, __popcll(lm), wrow[wv], wstep[wv], t, lut, lr, b1, b2, eps, 0, 1);
+                    replay_claimed<NCF_DEFER_LONG_REPC>(embf, mf, vf, W, __popcll(lm), wrow[wv], wstep[wv], t, lut, lr,
+                                                        b1, b2, eps, 0, 1);
                     __builtin_amdgcn_wave_barrier();
                 }
             }
