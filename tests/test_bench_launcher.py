@@ -61,3 +61,29 @@ def test_gloo_two_ranks_report_in_step_exchange():
     for k in ("rs_ar_exposed_ms", "ag_exposed_ms"):
         assert s[k]["max"] >= s[k]["min"] >= 0.0, (k, s[k])
     assert s["rs_ar_ms"] is None and s["ag_ms"] is None   # torch's collectives: not observable
+
+
+def _bench_module():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_for_test", os.path.join(ROOT, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    return b
+
+
+def test_replay_accounting_counts_only_the_far_rows_in_the_update():
+    """The update launch's algorithmic bytes count the catch-up replays it still runs: with the
+    replay split (NCF_DEFER_OWED) only rows owing more than that many steps; the build defines
+    select the threshold (0: every replay in the update)."""
+    import torch
+    b = _bench_module()
+    assert b.deferred_replay_owed({"defines": ""}) == 4
+    assert b.deferred_replay_owed({"defines": "-DNCF_DEFER_OWED=8"}) == 8
+    assert b.deferred_replay_owed({"defines": "-DNCF_REPLAY_IN_SCAN=0"}) == 0
+    g = torch.Generator().manual_seed(3)
+    pool = [(torch.randint(0, 50, (40,), generator=g, dtype=torch.int32),
+             torch.randint(0, 20, (40,), generator=g, dtype=torch.int32), None) for _ in range(7)]
+    total = b.replayed_rows(pool, 3, 12, 50, 70, items=True)
+    far = b.replayed_rows(pool, 3, 12, 50, 70, items=True, far=2)
+    assert 0 < far < total
+    assert b.replayed_rows(pool, 3, 12, 50, 70, items=True, far=1000) == 0.0
